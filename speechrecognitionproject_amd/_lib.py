@@ -1,0 +1,75 @@
+"""ctypes binding of libsrk.so (include/srk.h).  The product path has NO fallback: if the library
+or a GPU is missing, every op raises.
+
+torch is imported first on purpose: its bundled libamdhip64.so.7 is then the HIP runtime that
+libsrk.so binds to (same SONAME), so torch tensors, streams and our kernels share one runtime.
+"""
+import ctypes
+import os
+import re
+
+import torch  # noqa: F401  (load torch's HIP runtime before libsrk.so)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsrk.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "srk.h")
+ABI_VERSION = 1
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I = ctypes.c_int
+_F = ctypes.c_float
+_D = ctypes.c_double
+
+# name -> argtypes (restype is int unless listed in _RESTYPE)
+_SIGS = {
+    "srk_version": [],
+    "srk_last_error": [],
+    "srk_init": [_I],
+    "srk_fbank_fwd": [_P, _I64, _P, _P],
+    "srk_mfcc_fwd": [_P, _I64, _P, _I, _P],
+    "srk_spec_fwd": [_P, _I64, _P, _I, _P],
+    "srk_noise_mix": [_P, _P, _I64, _I64, _P, _P, _P, _I64, _P, _P],
+}
+_RESTYPE = {"srk_last_error": ctypes.c_char_p}
+
+
+class SrkError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libsrk.so once and declare every signature; raises if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SrkError("libsrk.so is not built (%s); run `python -m speechrecognitionproject_amd.build`" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPE.get(name, ctypes.c_int)
+        v = L.srk_version()
+        if v != ABI_VERSION:
+            raise SrkError("libsrk.so ABI version %d != expected %d (rebuild)" % (v, ABI_VERSION))
+        _lib = L
+    return _lib
+
+
+def call(name, *args):
+    """Invoke an srk_* entry point and raise SrkError with srk_last_error() on failure."""
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().srk_last_error().decode(errors="replace")
+        raise SrkError("%s failed (status %d): %s" % (name, rc, msg))
+    return rc
+
+
+def header_symbols():
+    """Every srk_* function declared in include/srk.h."""
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(srk_[a-z0-9_]+)\s*\(", text)))

@@ -1,0 +1,457 @@
+// K1 MFCC, K2 log-mel fbank, K3 log spectrogram, K4 noise-mix — gfx950 HIP kernels.
+//
+// Design: one workgroup per clip, frames processed in chunks of F.
+// Per chunk:
+//   load   : wave-per-frame coalesced float2 loads of PCM, window applied in fp64, packed as
+//            z[n] = x[2n] + i x[2n+1] (real N-point FFT via an N/2-point complex FFT); the DC and
+//            Nyquist sums are accumulated in fp64 in the same pass (fp32 cancellation in the DC
+//            bin costs up to 0.17 dB in fbank column 1 otherwise — SURVEY.md Appendix A).
+//   fft    : mixed-radix Stockham passes (radix 4 / 5) in LDS, twiddles from a table.
+//   untangle + |X|^2, then the feature-specific reduction (sparse mel, log, DCT ...).
+#include "srk_internal.h"
+
+namespace srk {
+namespace {
+
+constexpr int kPcmLen = 16000;
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }   // -i * a
+
+template <int R>
+__device__ __forceinline__ void dft(float2 (&v)[R]);
+
+template <>
+__device__ __forceinline__ void dft<4>(float2 (&v)[4]) {
+  const float2 s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
+  const float2 s13 = cadd(v[1], v[3]), d13 = mul_mi(csub(v[1], v[3]));
+  v[0] = cadd(s02, s13);
+  v[2] = csub(s02, s13);
+  v[1] = cadd(d02, d13);
+  v[3] = csub(d02, d13);
+}
+
+template <>
+__device__ __forceinline__ void dft<5>(float2 (&v)[5]) {
+  constexpr float c1 = 0.30901699437494745f, c2 = -0.8090169943749473f;
+  constexpr float s1 = 0.9510565162951535f, s2 = 0.5877852522924732f;
+  const float2 t1 = cadd(v[1], v[4]), t2 = cadd(v[2], v[3]);
+  const float2 t3 = csub(v[1], v[4]), t4 = csub(v[2], v[3]);
+  const float2 b1 = make_float2(v[0].x + c1 * t1.x + c2 * t2.x, v[0].y + c1 * t1.y + c2 * t2.y);
+  const float2 b2 = make_float2(v[0].x + c2 * t1.x + c1 * t2.x, v[0].y + c2 * t1.y + c1 * t2.y);
+  const float2 q1 = make_float2(s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y);   // -i*q1 for y1
+  const float2 q2 = make_float2(s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y);
+  v[0] = make_float2(v[0].x + t1.x + t2.x, v[0].y + t1.y + t2.y);
+  v[1] = cadd(b1, mul_mi(q1));
+  v[4] = csub(b1, mul_mi(q1));
+  v[2] = cadd(b2, mul_mi(q2));
+  v[3] = csub(b2, mul_mi(q2));
+}
+
+// One Stockham autosort pass of radix R over F frames of M complex points held in `buf`
+// (frame-major).  Ns = product of the radices of the previous passes.  Butterfly j reads
+// x[j + r*M/R], scales input r by W_{Ns*R}^{(j mod Ns)*r}, and writes y[(j/Ns)*Ns*R + j%Ns + r*Ns].
+// In place: every thread keeps its butterflies in registers across the barrier.
+template <int R, int NS, int M, int F, int NT>
+__device__ __forceinline__ void stockham_pass(float2* buf, const float2* __restrict__ tw) {
+  constexpr int MR = M / R;
+  constexpr int NB = F * MR;
+  constexpr int CNT = (NB + NT - 1) / NT;
+  float2 v[CNT][R];
+  int dst[CNT];
+#pragma unroll
+  for (int i = 0; i < CNT; ++i) {
+    const int b = threadIdx.x + i * NT;
+    dst[i] = -1;
+    if (b < NB) {
+      const int fr = b / MR, j = b % MR, k = j % NS;
+      const int base = fr * M;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        float2 a = buf[base + j + r * MR];
+        if (NS > 1 && r > 0) a = cmul(a, tw[k * r * (M / (NS * R))]);
+        v[i][r] = a;
+      }
+      dft<R>(v[i]);
+      dst[i] = base + (j / NS) * NS * R + k;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < CNT; ++i) {
+    if (dst[i] >= 0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) buf[dst[i] + r * NS] = v[i][r];
+    }
+  }
+  __syncthreads();
+}
+
+template <int M, int F, int NT>
+__device__ __forceinline__ void fft_frames(float2* buf, const float2* __restrict__ tw);
+
+template <>
+__device__ __forceinline__ void fft_frames<256, 14, 256>(float2* buf, const float2* __restrict__ tw) {
+  stockham_pass<4, 1, 256, 14, 256>(buf, tw);
+  stockham_pass<4, 4, 256, 14, 256>(buf, tw);
+  stockham_pass<4, 16, 256, 14, 256>(buf, tw);
+  stockham_pass<4, 64, 256, 14, 256>(buf, tw);
+}
+
+template <int F, int NT>
+__device__ __forceinline__ void fft320(float2* buf, const float2* __restrict__ tw) {
+  stockham_pass<4, 1, 320, F, NT>(buf, tw);
+  stockham_pass<4, 4, 320, F, NT>(buf, tw);
+  stockham_pass<4, 16, 320, F, NT>(buf, tw);
+  stockham_pass<5, 64, 320, F, NT>(buf, tw);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Untangle the packed real FFT and store |X[k]|^2 (k = 0..M) as floats over `buf`, frame
+// stride M+1.  X[0] / X[M] come from the fp64 sums `dcny` instead of the fp32 FFT.
+template <int M, int F, int NT>
+__device__ __forceinline__ void power_spectrum(float2* buf, const float2* __restrict__ post,
+                                               const double2* dcny, bool fix_dc, bool fix_nyq) {
+  constexpr int NI = F * (M + 1);
+  constexpr int CNT = (NI + NT - 1) / NT;
+  float p[CNT];
+#pragma unroll
+  for (int i = 0; i < CNT; ++i) {
+    const int it = threadIdx.x + i * NT;
+    p[i] = 0.f;
+    if (it < NI) {
+      const int fr = it / (M + 1), k = it % (M + 1);
+      const float2 a = buf[fr * M + (k % M)];
+      const float2 bz = buf[fr * M + ((M - k) % M)];
+      const float2 bc = make_float2(bz.x, -bz.y);
+      const float2 e = make_float2(0.5f * (a.x + bc.x), 0.5f * (a.y + bc.y));
+      const float2 o = mul_mi(make_float2(0.5f * (a.x - bc.x), 0.5f * (a.y - bc.y)));
+      const float2 x = cadd(e, cmul(post[k], o));
+      p[i] = x.x * x.x + x.y * x.y;
+      if (k == 0 && fix_dc) p[i] = (float)(dcny[fr].x * dcny[fr].x);
+      if (k == M && fix_nyq) p[i] = (float)(dcny[fr].y * dcny[fr].y);
+    }
+  }
+  __syncthreads();
+  float* pb = reinterpret_cast<float*>(buf);
+#pragma unroll
+  for (int i = 0; i < CNT; ++i) {
+    const int it = threadIdx.x + i * NT;
+    if (it < NI) pb[it] = p[i];
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------- per-feature loads
+// Each returns the two windowed fp64 samples feeding z[n] = x[2n] + i x[2n+1] of frame gf.
+struct FbankLoad {   // model_fbanks_cnn.py:21 (fp32 pre-emphasis), :36-41 (frames, Hamming)
+  static constexpr int N = 512, M = 256, NFRAMES = 98;
+  __device__ static __forceinline__ double emph(const float* x, int i) {
+    // numpy rounds the product and the difference separately: no FMA contraction here
+#pragma clang fp contract(off)
+    return i == 0 ? (double)x[0] : (double)(x[i] - 0.97f * x[i - 1]);
+  }
+  __device__ static __forceinline__ void load(const float* x, const DeviceTables& t, int gf, int n,
+                                              double& a, double& b) {
+    const int m = 2 * n;
+    if (m >= 400) { a = b = 0.0; return; }
+    const int s = 160 * gf + m;
+    a = emph(x, s) * t.hamming400[m];
+    b = emph(x, s + 1) * t.hamming400[m + 1];
+  }
+};
+
+struct SpecLoad {    // scipy.signal.spectrogram segments, model_spec_bgru.py:13
+  static constexpr int N = 640, M = 320, NFRAMES = 49;
+  __device__ static __forceinline__ void load(const float* x, const DeviceTables& t, int gf, int n,
+                                              double& a, double& b) {
+    const int s = 320 * gf + 2 * n;
+    const float2 v = *reinterpret_cast<const float2*>(x + s);
+    a = (double)v.x * t.tukey640[2 * n];
+    b = (double)v.y * t.tukey640[2 * n + 1];
+  }
+};
+
+struct MfccLoad {    // librosa stft(center=True, pad_mode='reflect'), periodic Hann(640)
+  static constexpr int N = 640, M = 320, NFRAMES = 51;
+  __device__ static __forceinline__ int reflect(int s) {
+    s = s < 0 ? -s : s;
+    return s > kPcmLen - 1 ? 2 * (kPcmLen - 1) - s : s;
+  }
+  __device__ static __forceinline__ void load(const float* x, const DeviceTables& t, int gf, int n,
+                                              double& a, double& b) {
+    const int s = 320 * gf + 2 * n - 320;
+    a = (double)x[reflect(s)] * t.hann640[2 * n];
+    b = (double)x[reflect(s + 1)] * t.hann640[2 * n + 1];
+  }
+};
+
+// Load frames [f0, f0+F) of clip x into buf, windowed; frames past NFRAMES are zero.
+template <class L, int F, int NT>
+__device__ __forceinline__ void load_frames(float2* buf, double2* dcny, const float* x,
+                                            const DeviceTables& t, int f0) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int fr = wave; fr < F; fr += NW) {
+    const int gf = f0 + fr;
+    double se = 0.0, so = 0.0;
+#pragma unroll
+    for (int i = 0; i < L::M / 64; ++i) {
+      const int n = lane + 64 * i;
+      double a = 0.0, b = 0.0;
+      if (gf < L::NFRAMES) L::load(x, t, gf, n, a, b);
+      buf[fr * L::M + n] = make_float2((float)a, (float)b);
+      se += a;
+      so += b;
+    }
+    se = wave_sum(se);
+    so = wave_sum(so);
+    if (lane == 0) dcny[fr] = make_double2(se + so, se - so);
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------- K2 fbank
+constexpr int kFbF = 14, kFbNT = 256;
+constexpr float kFbEpsDb = -313.07119549076395f;   // 20*log10(np.finfo(float).eps), :61-62
+
+__global__ __launch_bounds__(kFbNT) void fbank_kernel(const float* __restrict__ pcm, float* __restrict__ out,
+                                                      DeviceTables t) {
+  __shared__ float2 buf[kFbF * 256];
+  __shared__ double2 dcny[kFbF];
+  const int clip = blockIdx.x;
+  const float* x = pcm + (size_t)clip * kPcmLen;
+  float* o = out + (size_t)clip * 98 * 120;
+  for (int f0 = 0; f0 < 98; f0 += kFbF) {
+    load_frames<FbankLoad, kFbF, kFbNT>(buf, dcny, x, t, f0);
+    fft_frames<256, kFbF, kFbNT>(buf, t.tw256);
+    power_spectrum<256, kFbF, kFbNT>(buf, t.post512, dcny, true, true);
+    const float* pb = reinterpret_cast<const float*>(buf);
+    for (int it = threadIdx.x; it < kFbF * 120; it += kFbNT) {
+      const int fr = it / 120, m = it % 120;
+      const int cnt = t.fb_cnt[m];
+      float acc = 0.f;
+      if (cnt > 0) {
+        const int lo = t.fb_lo[m], off = t.fb_off[m];
+        const float* p = pb + fr * 257 + lo;
+        for (int c = 0; c < cnt; ++c) acc = fmaf(t.fb_w[off + c], p[c], acc);
+      }
+      // |rfft|^2 / NFFT (:44): the 1/512 is an exact power of two, applied after the sum
+      acc *= (1.0f / 512.0f);
+      o[(f0 + fr) * 120 + m] = acc == 0.f ? kFbEpsDb : 20.0f * log10f(acc);
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------- K3 spectrogram
+constexpr int kSpF = 7, kSpNT = 256;
+
+__global__ __launch_bounds__(kSpNT) void spec_kernel(const float* __restrict__ pcm, float* __restrict__ out,
+                                                     int transposed, float scale, DeviceTables t) {
+  __shared__ float2 buf[kSpF * 320];
+  __shared__ double2 dcny[kSpF];
+  const int clip = blockIdx.x;
+  const float* x = pcm + (size_t)clip * kPcmLen;
+  float* o = out + (size_t)clip * 49 * 321;
+  for (int f0 = 0; f0 < 49; f0 += kSpF) {
+    load_frames<SpecLoad, kSpF, kSpNT>(buf, dcny, x, t, f0);
+    fft320<kSpF, kSpNT>(buf, t.tw320);
+    power_spectrum<320, kSpF, kSpNT>(buf, t.post640, dcny, true, true);
+    const float* pb = reinterpret_cast<const float*>(buf);
+    for (int it = threadIdx.x; it < kSpF * 321; it += kSpNT) {
+      const int fr = it / 321, k = it % 321;
+      float v = pb[it] * scale;
+      if (k > 0 && k < 320) v *= 2.0f;                 // one-sided, DC/Nyquist not doubled
+      v = logf(__fadd_rn(v, 1e-10f));                  // model_spec_bgru.py:14
+      const int f = f0 + fr;
+      if (transposed) o[f * 321 + k] = v; else o[k * 49 + f] = v;
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------- K1 MFCC
+constexpr int kMfF = 17, kMfNT = 256;
+
+__global__ __launch_bounds__(kMfNT) void mfcc_kernel(const float* __restrict__ pcm, float* __restrict__ out,
+                                                     int layout, DeviceTables t) {
+  __shared__ float2 buf[kMfF * 320];
+  __shared__ float db[51 * 128];
+  __shared__ double2 dcny[kMfF];
+  __shared__ float red[kMfNT / 64];
+  const int clip = blockIdx.x;
+  const float* x = pcm + (size_t)clip * kPcmLen;
+  float vmax = -INFINITY;
+  for (int f0 = 0; f0 < 51; f0 += kMfF) {
+    load_frames<MfccLoad, kMfF, kMfNT>(buf, dcny, x, t, f0);
+    fft320<kMfF, kMfNT>(buf, t.tw320);
+    power_spectrum<320, kMfF, kMfNT>(buf, t.post640, dcny, false, false);
+    const float* pb = reinterpret_cast<const float*>(buf);
+    for (int it = threadIdx.x; it < kMfF * 128; it += kMfNT) {
+      const int fr = it / 128, m = it % 128;
+      const int lo = t.mel_lo[m], cnt = t.mel_cnt[m], off = t.mel_off[m];
+      const float* p = pb + fr * 321 + lo;
+      float acc = 0.f;
+      for (int c = 0; c < cnt; ++c) acc = fmaf(t.mel_w[off + c], p[c], acc);
+      // power_to_db(ref=1.0, amin=1e-10): 10*log10(max(amin, S))
+      const float v = acc > 1e-10f ? 10.0f * log10f(acc) : -100.0f;
+      db[(f0 + fr) * 128 + m] = v;
+      vmax = fmaxf(vmax, v);
+    }
+    __syncthreads();
+  }
+  // per-clip top_db = 80 clamp (the reduction between mel and DCT)
+  vmax = wave_max(vmax);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = vmax;
+  __syncthreads();
+  float m = red[0];
+#pragma unroll
+  for (int w = 1; w < kMfNT / 64; ++w) m = fmaxf(m, red[w]);
+  const float floor_db = m - 80.0f;
+  // DCT-II ortho [:13] per frame -> C[13][51] in LDS (reuse buf)
+  float* C = reinterpret_cast<float*>(buf);
+  float* D = C + 13 * 51;
+  for (int it = threadIdx.x; it < 13 * 51; it += kMfNT) {
+    const int c = it / 51, f = it % 51;
+    const float* d = db + f * 128;
+    const float* w = t.dct + c * 128;
+    float acc = 0.f;
+    for (int k = 0; k < 128; ++k) acc = fmaf(w[k], fmaxf(d[k], floor_db), acc);
+    C[it] = acc;
+  }
+  __syncthreads();
+  // np.gradient(axis=1), edge_order=1: one-sided at the ends, central inside
+  auto grad = [](const float* r, int f) {
+    return f == 0 ? r[1] - r[0] : (f == 50 ? r[50] - r[49] : (r[f + 1] - r[f - 1]) * 0.5f);
+  };
+  for (int it = threadIdx.x; it < 13 * 51; it += kMfNT) D[it] = grad(C + (it / 51) * 51, it % 51);
+  __syncthreads();
+  float* o = out + (size_t)clip * 39 * 51;
+  for (int it = threadIdx.x; it < 39 * 51; it += kMfNT) {
+    const int row = it / 51, f = it % 51;
+    float v;
+    if (row < 13) v = C[row * 51 + f];
+    else if (row < 26) v = D[(row - 13) * 51 + f];
+    else v = grad(D + (row - 26) * 51, f);
+    if (layout == 0) o[row * 51 + f] = v; else o[f * 39 + row] = v;
+  }
+}
+
+// ------------------------------------------------------------------------- K4 noise mix
+// numpy: sample + (gain * noise) in float64 (two roundings, never fused), then np.int16()
+// truncates toward zero.
+__device__ __forceinline__ float mix_one(short s, double g, short n) {
+#pragma clang fp contract(off)
+  const double v = (double)s + g * (double)n;
+  return (float)(int16_t)(int)v;
+}
+
+__global__ void noise_mix_kernel(const int16_t* __restrict__ pcm, const int16_t* __restrict__ bank,
+                                 int64_t bank_len, const int64_t* __restrict__ file_idx,
+                                 const int64_t* __restrict__ offs, const double* __restrict__ gains,
+                                 int64_t n_clips, float* __restrict__ out) {
+  // 8 samples per thread: 16-B int16 loads of pcm, 16-B + 16-B fp32 stores.
+  const int64_t i8 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total8 = n_clips * (kPcmLen / 8);
+  if (i8 >= total8) return;
+  const int64_t clip = i8 / (kPcmLen / 8);
+  const int s0 = (int)(i8 % (kPcmLen / 8)) * 8;
+  const int16_t* nz = bank + file_idx[clip] * bank_len + offs[clip] + s0;
+  const double g = gains[clip];
+  const short4 a = *reinterpret_cast<const short4*>(pcm + clip * kPcmLen + s0);
+  const short4 b = *reinterpret_cast<const short4*>(pcm + clip * kPcmLen + s0 + 4);
+  const short sv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = mix_one(sv[j], g, nz[j]);
+  float4* o = reinterpret_cast<float4*>(out + clip * kPcmLen + s0);
+  o[0] = make_float4(r[0], r[1], r[2], r[3]);
+  o[1] = make_float4(r[4], r[5], r[6], r[7]);
+}
+
+}  // namespace
+}  // namespace srk
+
+using srk::DeviceTables;
+
+extern "C" {
+
+int srk_fbank_fwd(const float* pcm, int64_t n_clips, float* out, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(n_clips >= 0 && n_clips <= INT32_MAX, SRK_ERR_INVALID, "srk_fbank_fwd: bad n_clips %lld", (long long)n_clips);
+  if (n_clips == 0) return SRK_OK;
+  SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_fbank_fwd: null pointer");
+  const DeviceTables* t = nullptr;
+  if (int rc = srk::get_tables(&t)) return rc;
+  hipLaunchKernelGGL(srk::fbank_kernel, dim3((unsigned)n_clips), dim3(srk::kFbNT), 0, srk::as_stream(stream),
+                     pcm, out, *t);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_spec_fwd(const float* pcm, int64_t n_clips, float* out, int transposed, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(n_clips >= 0 && n_clips <= INT32_MAX, SRK_ERR_INVALID, "srk_spec_fwd: bad n_clips");
+  if (n_clips == 0) return SRK_OK;
+  SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_spec_fwd: null pointer");
+  const DeviceTables* t = nullptr;
+  if (int rc = srk::get_tables(&t)) return rc;
+  hipLaunchKernelGGL(srk::spec_kernel, dim3((unsigned)n_clips), dim3(srk::kSpNT), 0, srk::as_stream(stream),
+                     pcm, out, transposed ? 1 : 0, (float)t->spec_scale, *t);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_mfcc_fwd(const float* pcm, int64_t n_clips, float* out, int layout, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(n_clips >= 0 && n_clips <= INT32_MAX, SRK_ERR_INVALID, "srk_mfcc_fwd: bad n_clips");
+  SRK_REQUIRE(layout == 0 || layout == 1, SRK_ERR_INVALID, "srk_mfcc_fwd: layout must be 0 or 1");
+  if (n_clips == 0) return SRK_OK;
+  SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_mfcc_fwd: null pointer");
+  const DeviceTables* t = nullptr;
+  if (int rc = srk::get_tables(&t)) return rc;
+  hipLaunchKernelGGL(srk::mfcc_kernel, dim3((unsigned)n_clips), dim3(srk::kMfNT), 0, srk::as_stream(stream),
+                     pcm, out, layout, *t);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_noise_mix(const int16_t* pcm, const int16_t* bank, int64_t n_files, int64_t bank_len,
+                  const int64_t* file_idx, const int64_t* offset, const double* gain, int64_t n_clips,
+                  float* out, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(n_clips >= 0, SRK_ERR_INVALID, "srk_noise_mix: bad n_clips");
+  if (n_clips == 0) return SRK_OK;
+  SRK_REQUIRE(pcm && bank && file_idx && offset && gain && out, SRK_ERR_INVALID, "srk_noise_mix: null pointer");
+  SRK_REQUIRE(n_files > 0 && bank_len >= 16000, SRK_ERR_INVALID, "srk_noise_mix: bank must hold >= 1 file of >= 16000 samples");
+  SRK_REQUIRE(((uintptr_t)pcm % 16) == 0 && ((uintptr_t)out % 16) == 0, SRK_ERR_INVALID,
+              "srk_noise_mix: pcm/out must be 16-byte aligned");
+  const int64_t total8 = n_clips * (16000 / 8);
+  const int nt = 256;
+  const int64_t blocks = (total8 + nt - 1) / nt;
+  hipLaunchKernelGGL(srk::noise_mix_kernel, dim3((unsigned)blocks), dim3(nt), 0, srk::as_stream(stream), pcm, bank,
+                     bank_len, file_idx, offset, gain, n_clips, out);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,207 @@
+// libsrk runtime: error reporting, per-device constant tables, srk_init.
+//
+// The tables are built on the host in double precision from the same closed forms the
+// reference evaluates with numpy/scipy/librosa, then uploaded once per device:
+//  * fbank triangles       models/model_fbanks_cnn.py:46-59 (rebuilt per call there)
+//  * Slaney mel (norm=1)   librosa.filters.mel as called by model_mfcc_bgru.py:13
+//  * DCT-II ortho [:13]    librosa.filters.dct / scipy.fftpack.dct(norm='ortho')
+//  * windows               np.hamming(400) (model_fbanks_cnn.py:41), periodic Hann(640)
+//                          (librosa stft), periodic Tukey(640, 0.25) (scipy spectrogram)
+#include <cmath>
+#include <cstdarg>
+#include <mutex>
+#include <vector>
+
+#include "srk_internal.h"
+
+namespace srk {
+
+static thread_local std::string g_last_error;
+
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+}
+
+namespace {
+
+constexpr int kMaxDevices = 64;
+DeviceTables g_tables[kMaxDevices];
+std::mutex g_mutex;
+
+template <class T>
+int upload(T** dst, const std::vector<T>& src) {
+  SRK_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(dst), src.size() * sizeof(T)));
+  SRK_CHECK_HIP(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+  return SRK_OK;
+}
+
+std::vector<double> linspace(double a, double b, int n) {   // numpy.linspace semantics
+  std::vector<double> y(n);
+  const double step = (b - a) / (n - 1);
+  for (int i = 0; i < n; ++i) y[i] = i * step + a;
+  y[n - 1] = b;
+  return y;
+}
+
+std::vector<float2> twiddles(int m, int count) {
+  std::vector<float2> t(count);
+  for (int k = 0; k < count; ++k) {
+    const double a = -2.0 * M_PI * (double)k / (double)m;
+    t[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+  }
+  return t;
+}
+
+// Dense [nf][nbins] matrix -> CSR by filter (each filter is one contiguous run of bins).
+void to_csr(const std::vector<double>& w, int nf, int nbins, std::vector<int>& lo,
+            std::vector<int>& cnt, std::vector<int>& off, std::vector<float>& vals) {
+  lo.assign(nf, 0); cnt.assign(nf, 0); off.assign(nf, 0); vals.clear();
+  for (int m = 0; m < nf; ++m) {
+    int first = -1, last = -1;
+    for (int k = 0; k < nbins; ++k)
+      if (w[(size_t)m * nbins + k] != 0.0) { if (first < 0) first = k; last = k; }
+    off[m] = (int)vals.size();
+    if (first < 0) continue;
+    lo[m] = first; cnt[m] = last - first + 1;
+    for (int k = first; k <= last; ++k) vals.push_back((float)w[(size_t)m * nbins + k]);
+  }
+}
+
+// models/model_fbanks_cnn.py:46-59
+std::vector<double> fbank_matrix() {
+  const int nfilt = 120, nfft = 512, sr = 16000, nb = nfft / 2 + 1;
+  const double high = 2595.0 * std::log10(1.0 + (sr / 2.0) / 700.0);
+  std::vector<double> mel = linspace(0.0, high, nfilt + 2), bin(nfilt + 2);
+  for (int i = 0; i < nfilt + 2; ++i)
+    bin[i] = std::floor((nfft + 1) * (700.0 * (std::pow(10.0, mel[i] / 2595.0) - 1.0)) / sr);
+  std::vector<double> fb((size_t)nfilt * nb, 0.0);
+  for (int m = 1; m <= nfilt; ++m) {
+    const int fl = (int)bin[m - 1], fc = (int)bin[m], fr = (int)bin[m + 1];
+    for (int k = fl; k < fc; ++k) fb[(size_t)(m - 1) * nb + k] = (k - bin[m - 1]) / (bin[m] - bin[m - 1]);
+    for (int k = fc; k < fr; ++k) fb[(size_t)(m - 1) * nb + k] = (bin[m + 1] - k) / (bin[m + 1] - bin[m]);
+  }
+  return fb;
+}
+
+double hz_to_mel(double f) {   // Slaney (htk=False)
+  const double f_sp = 200.0 / 3.0, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp;
+  const double logstep = std::log(6.4) / 27.0;
+  return f >= min_log_hz ? min_log_mel + std::log(f / min_log_hz) / logstep : f / f_sp;
+}
+double mel_to_hz(double m) {
+  const double f_sp = 200.0 / 3.0, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp;
+  const double logstep = std::log(6.4) / 27.0;
+  return m >= min_log_mel ? min_log_hz * std::exp(logstep * (m - min_log_mel)) : f_sp * m;
+}
+
+// librosa.filters.mel(16000, 640, n_mels=128, norm=1)
+std::vector<double> slaney_mel() {
+  const int nmel = 128, nb = 321;
+  std::vector<double> fft = linspace(0.0, 8000.0, nb);
+  std::vector<double> mels = linspace(hz_to_mel(0.0), hz_to_mel(8000.0), nmel + 2), mf(nmel + 2);
+  for (int i = 0; i < nmel + 2; ++i) mf[i] = mel_to_hz(mels[i]);
+  std::vector<double> w((size_t)nmel * nb, 0.0);
+  for (int i = 0; i < nmel; ++i) {
+    const double fd0 = mf[i + 1] - mf[i], fd1 = mf[i + 2] - mf[i + 1];
+    const double enorm = 2.0 / (mf[i + 2] - mf[i]);
+    for (int k = 0; k < nb; ++k) {
+      const double lower = -(mf[i] - fft[k]) / fd0, upper = (mf[i + 2] - fft[k]) / fd1;
+      w[(size_t)i * nb + k] = std::max(0.0, std::min(lower, upper)) * enorm;
+    }
+  }
+  return w;
+}
+
+int build_tables(DeviceTables& t) {
+  int rc;
+  if ((rc = upload(&t.tw256, twiddles(256, 256)))) return rc;
+  if ((rc = upload(&t.tw320, twiddles(320, 320)))) return rc;
+  if ((rc = upload(&t.post512, twiddles(512, 257)))) return rc;
+  if ((rc = upload(&t.post640, twiddles(640, 321)))) return rc;
+
+  std::vector<double> ham(400), hann(640), tuk(641);
+  for (int n = 0; n < 400; ++n) ham[n] = 0.54 - 0.46 * std::cos(2.0 * M_PI * n / 399.0);
+  for (int n = 0; n < 640; ++n) hann[n] = 0.5 - 0.5 * std::cos(2.0 * M_PI * n / 640.0);
+  {  // scipy tukey(641, 0.25, sym=True)[:640]
+    const int m = 641;
+    const double alpha = 0.25;
+    const int width = (int)std::floor(alpha * (m - 1) / 2.0);
+    for (int n = 0; n < m; ++n) tuk[n] = 1.0;
+    for (int n = 0; n <= width; ++n)
+      tuk[n] = 0.5 * (1.0 + std::cos(M_PI * (-1.0 + 2.0 * n / alpha / (m - 1))));
+    for (int n = m - width - 1; n < m; ++n)
+      tuk[n] = 0.5 * (1.0 + std::cos(M_PI * (-2.0 / alpha + 1.0 + 2.0 * n / alpha / (m - 1))));
+    tuk.resize(640);
+  }
+  double s2 = 0.0;
+  for (double v : tuk) s2 += v * v;
+  t.spec_scale = 1.0 / (16000.0 * s2);
+  if ((rc = upload(&t.hamming400, ham))) return rc;
+  if ((rc = upload(&t.hann640, hann))) return rc;
+  if ((rc = upload(&t.tukey640, tuk))) return rc;
+
+  std::vector<int> lo, cnt, off;
+  std::vector<float> vals;
+  to_csr(fbank_matrix(), 120, 257, lo, cnt, off, vals);
+  if ((rc = upload(&t.fb_lo, lo)) || (rc = upload(&t.fb_cnt, cnt)) || (rc = upload(&t.fb_off, off)) ||
+      (rc = upload(&t.fb_w, vals)))
+    return rc;
+  to_csr(slaney_mel(), 128, 321, lo, cnt, off, vals);
+  if ((rc = upload(&t.mel_lo, lo)) || (rc = upload(&t.mel_cnt, cnt)) || (rc = upload(&t.mel_off, off)) ||
+      (rc = upload(&t.mel_w, vals)))
+    return rc;
+
+  std::vector<float> dct(13 * 128);
+  for (int k = 0; k < 128; ++k) dct[k] = (float)(1.0 / std::sqrt(128.0));
+  for (int i = 1; i < 13; ++i)
+    for (int k = 0; k < 128; ++k)
+      dct[i * 128 + k] = (float)(std::cos(i * (2 * k + 1) * M_PI / 256.0) * std::sqrt(2.0 / 128.0));
+  if ((rc = upload(&t.dct, dct))) return rc;
+  t.ready = true;
+  return SRK_OK;
+}
+
+}  // namespace
+
+int get_tables(const DeviceTables** out) {
+  int dev = 0;
+  SRK_CHECK_HIP(hipGetDevice(&dev));
+  SRK_REQUIRE(dev >= 0 && dev < kMaxDevices, SRK_ERR_INVALID, "device %d out of range", dev);
+  DeviceTables& t = g_tables[dev];
+  if (!t.ready) {
+    std::lock_guard<std::mutex> lk(g_mutex);
+    if (!t.ready) {
+      int rc = build_tables(t);
+      if (rc) return rc;
+    }
+  }
+  *out = &t;
+  return SRK_OK;
+}
+
+}  // namespace srk
+
+extern "C" {
+
+int srk_version(void) { return SRK_ABI_VERSION; }
+
+const char* srk_last_error(void) { return srk::g_last_error.c_str(); }
+
+int srk_init(int device) {
+  SRK_API_BEGIN
+  int prev = 0;
+  SRK_CHECK_HIP(hipGetDevice(&prev));
+  SRK_CHECK_HIP(hipSetDevice(device));
+  const srk::DeviceTables* t = nullptr;
+  int rc = srk::get_tables(&t);
+  SRK_CHECK_HIP(hipSetDevice(prev));
+  return rc;
+  SRK_API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,68 @@
+// Internal helpers shared by every translation unit of libsrk.so (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/srk.h"
+
+namespace srk {
+
+// Thread-local last-error text, read back through srk_last_error() (include/srk.h).
+void set_error(const char* fmt, ...);
+
+#define SRK_CHECK_HIP(expr)                                                              \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess) {                                                              \
+      ::srk::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr, hipGetErrorString(_e)); \
+      return SRK_ERR_HIP;                                                                \
+    }                                                                                    \
+  } while (0)
+
+#define SRK_REQUIRE(cond, code, ...)     \
+  do {                                   \
+    if (!(cond)) {                       \
+      ::srk::set_error(__VA_ARGS__);     \
+      return (code);                     \
+    }                                    \
+  } while (0)
+
+// Wraps the body of every extern "C" entry point: C++ exceptions never cross the C ABI.
+#define SRK_API_BEGIN try {
+#define SRK_API_END                                              \
+  }                                                              \
+  catch (const std::exception& e) {                              \
+    ::srk::set_error("exception: %s", e.what());                 \
+    return SRK_ERR_INTERNAL;                                     \
+  }                                                              \
+  catch (...) {                                                  \
+    ::srk::set_error("unknown exception");                       \
+    return SRK_ERR_INTERNAL;                                     \
+  }
+
+// Per-device constant tables (twiddles, windows, filterbanks, DCT), uploaded once by srk_init.
+struct DeviceTables {
+  bool ready = false;
+  // FFT twiddles exp(-2*pi*i*t/M), float2 interleaved
+  float2* tw256 = nullptr;     // M = 256 (fbank, N = 512)
+  float2* tw320 = nullptr;     // M = 320 (mfcc / spec, N = 640)
+  float2* post512 = nullptr;   // exp(-2*pi*i*k/512), k = 0..256
+  float2* post640 = nullptr;   // exp(-2*pi*i*k/640), k = 0..320
+  double* hamming400 = nullptr;
+  double* tukey640 = nullptr;
+  double* hann640 = nullptr;
+  // sparse filterbanks (CSR by filter): lo bin, count, offset into weights
+  int* fb_lo = nullptr; int* fb_cnt = nullptr; int* fb_off = nullptr; float* fb_w = nullptr;   // 120 filters
+  int* mel_lo = nullptr; int* mel_cnt = nullptr; int* mel_off = nullptr; float* mel_w = nullptr; // 128 filters
+  float* dct = nullptr;        // [13][128] orthonormal DCT-II
+  double spec_scale = 0.0;     // 1 / (fs * sum(w^2)) for the Tukey window
+};
+
+// Returns the tables for the current HIP device, building them on first use.
+int get_tables(const DeviceTables** out);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace srk

@@ -1,0 +1,89 @@
+"""Host wrappers of the feature kernels K1-K4 (include/srk.h).  Batched, device-resident.
+
+All functions take PCM as float32 [B, 16000] (int16-valued, as dataset.py:117 produces); a CPU
+tensor is copied to the current GPU first (the reference forward receives CPU batches,
+training.py:86).  There is no CPU path: without a GPU and libsrk.so these raise.
+"""
+import ctypes
+
+import torch
+
+from ._lib import SrkError, call
+
+SEQ_LENGTH = 16000
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise SrkError("speechrecognitionproject_amd needs a ROCm GPU (MI355X); none is visible")
+
+
+def stream_ptr():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def as_device_pcm(pcm):
+    require_gpu()
+    if not torch.is_tensor(pcm):
+        pcm = torch.as_tensor(pcm)
+    if pcm.dim() == 1:
+        pcm = pcm.unsqueeze(0)
+    if pcm.dim() != 2 or pcm.shape[1] != SEQ_LENGTH:
+        raise SrkError("expected PCM of shape [B, %d], got %s" % (SEQ_LENGTH, tuple(pcm.shape)))
+    if pcm.device.type != "cuda":
+        pcm = pcm.to("cuda", non_blocking=True)
+    return pcm.to(torch.float32).contiguous()
+
+
+def fbank(pcm, out=None):
+    """K2 log-mel filter banks [B, 98, 120] (models/model_fbanks_cnn.py:15-66)."""
+    x = as_device_pcm(pcm)
+    out = torch.empty((x.shape[0], 98, 120), device=x.device, dtype=torch.float32) if out is None else out
+    call("srk_fbank_fwd", ptr(x), x.shape[0], ptr(out), stream_ptr())
+    return out
+
+
+def mfcc(pcm, time_major=False, out=None):
+    """K1 MFCC+deltas: [B, 39, 51], or [B, 51, 39] if ``time_major`` (model_mfcc_bgru.py:11-19,34)."""
+    x = as_device_pcm(pcm)
+    shape = (x.shape[0], 51, 39) if time_major else (x.shape[0], 39, 51)
+    out = torch.empty(shape, device=x.device, dtype=torch.float32) if out is None else out
+    call("srk_mfcc_fwd", ptr(x), x.shape[0], ptr(out), 1 if time_major else 0, stream_ptr())
+    return out
+
+
+def spec(pcm, transposed=False, out=None):
+    """K3 log spectrogram: [B, 321, 49], or [B, 49, 321] if ``transposed`` (model_spec_*.py)."""
+    x = as_device_pcm(pcm)
+    shape = (x.shape[0], 49, 321) if transposed else (x.shape[0], 321, 49)
+    out = torch.empty(shape, device=x.device, dtype=torch.float32) if out is None else out
+    call("srk_spec_fwd", ptr(x), x.shape[0], ptr(out), 1 if transposed else 0, stream_ptr())
+    return out
+
+
+def noise_mix(pcm_i16, bank_i16, file_idx, offsets, gains, out=None):
+    """K4: float32 [B,16000] = int16(pcm + gain*bank[file, off:off+16000]) (dataset.py:183-193)."""
+    require_gpu()
+    dev = torch.device("cuda")
+    x = torch.as_tensor(pcm_i16).to(dev, torch.int16).contiguous()
+    bank = torch.as_tensor(bank_i16).to(dev, torch.int16).contiguous()
+    if bank.dim() == 1:
+        bank = bank.unsqueeze(0)
+    fi = torch.as_tensor(file_idx).to(dev, torch.int64).contiguous()
+    of = torch.as_tensor(offsets).to(dev, torch.int64).contiguous()
+    g = torch.as_tensor(gains).to(dev, torch.float64).contiguous()
+    n = x.shape[0]
+    if x.shape != (n, SEQ_LENGTH) or fi.numel() != n or of.numel() != n or g.numel() != n:
+        raise SrkError("noise_mix: inconsistent shapes")
+    # host-side bounds check of the draws (the kernel trusts them)
+    if n and (int(of.min()) < 0 or int(of.max()) > bank.shape[1] - SEQ_LENGTH or int(fi.min()) < 0
+              or int(fi.max()) >= bank.shape[0]):
+        raise SrkError("noise_mix: file index / offset out of range")
+    out = torch.empty((n, SEQ_LENGTH), device=dev, dtype=torch.float32) if out is None else out
+    call("srk_noise_mix", ptr(x), ptr(bank), bank.shape[0], bank.shape[1], ptr(fi), ptr(of), ptr(g), n, ptr(out),
+         stream_ptr())
+    return out

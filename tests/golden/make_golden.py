@@ -1,0 +1,188 @@
+"""Generate the golden parity fixtures in tests/golden/ FROM THE REFERENCE ITSELF.
+
+Run in the build container only (``/root/reference`` does not exist on the GPU box):
+
+    python tests/golden/make_golden.py
+
+The reference is imported read-only from /root/reference.  Three third-party modules it imports
+are absent from this image: ``librosa`` (model_mfcc_bgru.py:5, dataset.py:9) and
+``cv2`` (dataset.py:8).  They are replaced by stubs that raise if called — except
+``librosa.feature.mfcc``, which is bound to the oracle's librosa-0.6 restatement so that the
+reference's MFCC *glue* (np.gradient x2, concat, cast; model_mfcc_bgru.py:12-18) and its
+GRU/FC run unmodified.  The librosa arithmetic itself stays "parity unpinned".
+
+Outputs are data only (inputs + expected outputs), no reference source.
+"""
+import os
+import random
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+from oracle import features as OF            # noqa: E402
+from oracle import models as OM              # noqa: E402
+from speechrecognitionproject_amd.synthetic import synthetic_clips   # noqa: E402
+
+
+def _install_stubs():
+    def _absent(*a, **k):
+        raise RuntimeError("stubbed third-party call (absent in this image)")
+
+    librosa = types.ModuleType("librosa")
+    feat = types.ModuleType("librosa.feature")
+    eff = types.ModuleType("librosa.effects")
+
+    def mfcc(y, sr=22050, n_mfcc=20, n_fft=2048, hop_length=512):
+        assert (sr, n_mfcc, n_fft, hop_length) == (16000, 13, 640, 320)
+        return OF.mfcc13(y)
+
+    feat.mfcc = mfcc
+    eff.pitch_shift = _absent
+    librosa.feature, librosa.effects = feat, eff
+    cv2 = types.ModuleType("cv2")
+    cv2.resize = _absent
+    sys.modules.update({"librosa": librosa, "librosa.feature": feat, "librosa.effects": eff, "cv2": cv2})
+
+
+def golden_clips():
+    """8 clips covering the amplitude range named in SURVEY.md §8c."""
+    rng = np.random.default_rng(123)
+    t = np.arange(16000) / 16000.0
+    clips = [
+        rng.normal(0, 1, 16000),
+        rng.normal(0, 30, 16000),
+        rng.normal(0, 3000, 16000),
+        rng.normal(0, 30000, 16000),
+        np.zeros(16000),
+        np.concatenate([rng.normal(0, 3000, 8000), np.zeros(8000)]),
+        8000 * np.sin(2 * np.pi * 440 * t) + 4000 * np.sin(2 * np.pi * 1000 * t + 0.3),
+        1000 + rng.normal(0, 200, 16000),   # strong DC: stresses the pre-emphasis/DC bin
+    ]
+    return np.stack([np.clip(np.rint(c), -32768, 32767) for c in clips]).astype(np.float32)
+
+
+def sample_entries(t, n=256, seed=99):
+    flat = t.detach().reshape(-1).numpy()
+    if flat.size <= 4096:
+        return np.arange(flat.size), flat.copy()
+    idx = np.sort(np.random.default_rng(seed).choice(flat.size, n, replace=False))
+    return idx, flat[idx].copy()
+
+
+def model_golden(name, net, x, labels, train_mode=False):
+    sd = OM.seeded_state_dict(net, seed=0)
+    net.load_state_dict(sd)
+    net.train(train_mode)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    before = {k: v.detach().clone() for k, v in net.named_parameters()}
+    opt.zero_grad()
+    out = net(torch.from_numpy(x))
+    loss = torch.nn.CrossEntropyLoss()(out, torch.from_numpy(labels))
+    loss.backward()
+    grads = {k: v.grad.detach().clone() for k, v in net.named_parameters() if v.grad is not None}
+    opt.step()
+    rec = {"pcm": x, "labels": labels, "logits": out.detach().numpy(), "loss": np.float32(loss.item()),
+           "train_mode": np.int64(train_mode), "names": np.array(list(grads.keys()))}
+    for k in grads:
+        gi, gv = sample_entries(grads[k])
+        di, dv = sample_entries(dict(net.named_parameters())[k].detach() - before[k])
+        rec["gidx__" + k], rec["gval__" + k] = gi, gv
+        rec["dval__" + k] = dv
+        rec["gsum__" + k] = np.float64(grads[k].double().sum())
+        rec["gabs__" + k] = np.float64(grads[k].double().abs().sum())
+    np.savez_compressed(os.path.join(HERE, name), **rec)
+    print("wrote", name, "logits", out.shape)
+
+
+def main():
+    _install_stubs()
+    sys.path.insert(0, REF)
+    sys.path.insert(0, REF + "/models")
+    import model_fbanks_cnn as R_fb
+    import model_spec_bgru as R_sb
+    import model_spec_cnn as R_sc
+    import model_mfcc_bgru as R_mb
+    import model_resnet_bgru as R_rb
+    import dataset as R_ds
+    torch.set_default_dtype(torch.float32)
+
+    pcm = golden_clips()
+    # ---- K2 fbank (model_fbanks_cnn.py:15-66)
+    fb = np.stack([R_fb.filter_banks(torch.from_numpy(c)).numpy() for c in pcm])
+    np.savez_compressed(os.path.join(HERE, "fbank_golden.npz"), pcm=pcm, out=fb)
+    # ---- K3 spectrogram (model_spec_bgru.py:11-17; model_spec_cnn.py:12-18 is its transpose)
+    sp = np.stack([R_sb.compute_spec(torch.from_numpy(c)).numpy() for c in pcm])
+    spt = np.stack([R_sc.compute_spec(torch.from_numpy(c)).numpy() for c in pcm])
+    assert np.array_equal(sp.transpose(0, 2, 1), spt)
+    np.savez_compressed(os.path.join(HERE, "spec_golden.npz"), pcm=pcm, out=sp)
+    # ---- K1 MFCC glue with the oracle's librosa restatement (arithmetic unpinned, glue pinned)
+    mf = np.stack([R_mb.compute_mfcc(torch.from_numpy(c)).numpy() for c in pcm])
+    np.savez_compressed(os.path.join(HERE, "mfcc_glue_golden.npz"), pcm=pcm, out=mf)
+
+    # ---- K4 noise-mix + Dataset PCM path on a synthetic Kaggle-layout tree (dataset.py)
+    from scipy.io import wavfile
+    with tempfile.TemporaryDirectory() as root:
+        rng = np.random.default_rng(7)
+        os.makedirs(root + "/_background_noise_")
+        open(root + "/_background_noise_/README.md", "w").close()
+        bank = np.clip(np.rint(rng.normal(0, 2000, (2, 60000))), -6000, 6000).astype(np.int16)
+        for i in range(2):
+            wavfile.write(root + "/_background_noise_/noise%d.wav" % i, 16000, bank[i])
+        for d in ("yes", "go", "bed"):
+            os.makedirs(root + "/" + d)
+        lens = {"yes/a.wav": 12000, "go/b.wav": 16000, "bed/c.wav": 9000}
+        wavs = {}
+        for f, n in lens.items():
+            w = np.clip(np.rint(rng.normal(0, 3000, n)), -32768, 32767).astype(np.int16)
+            wavfile.write(root + "/" + f, 16000, w)
+            wavs[f] = w
+        with open(root + "/validation_list.txt", "w") as fh:
+            fh.write("\n".join(lens) + "\n")
+        ds = R_ds.Dataset(root + "/validation_list.txt", root)
+        items = [ds[i] for i in range(len(ds))]
+        np.savez_compressed(os.path.join(HERE, "dataset_golden.npz"),
+                            names=np.array(list(lens)), audio=np.stack([it["audio"] for it in items]),
+                            labels=np.array([it["label"] for it in items]),
+                            wav_a=wavs["yes/a.wav"], wav_b=wavs["go/b.wav"], wav_c=wavs["bed/c.wav"])
+        # add_noise_uniform with seeded draws; the draws are re-derived in the same order
+        names = sorted(ds.noise_list)
+        samples, outs, files, starts, gains = [], [], [], [], []
+        for i in range(6):
+            s = np.concatenate((wavs["yes/a.wav"], np.zeros(4000, dtype=int))) if i % 2 == 0 else wavs["go/b.wav"]
+            random.seed(i)
+            np.random.seed(i)
+            out = ds.add_noise_uniform(s, 0.1)
+            random.seed(i)
+            np.random.seed(i)
+            fname = ds.noise_list[random.randint(0, len(ds.noise_list) - 1)]
+            start = random.randint(0, 60000 - 16000)
+            gain = np.random.uniform(0, 0.1)
+            assert np.array_equal(out, OF.add_noise_uniform(s, bank[names.index(fname)], start, gain))
+            samples.append(s.astype(np.int64))
+            outs.append(out)
+            files.append(names.index(fname))
+            starts.append(start)
+            gains.append(gain)
+        np.savez_compressed(os.path.join(HERE, "noise_mix_golden.npz"), bank=bank, pcm=np.stack(samples),
+                            file_idx=np.array(files), start=np.array(starts), gain=np.array(gains), out=np.stack(outs))
+
+    # ---- module-level goldens (logits, CE loss, sampled grads, 1-step Adam delta)
+    x, y = synthetic_clips(4, seed=5)
+    torch.manual_seed(0)
+    model_golden("fbanks_cnn_golden.npz", R_fb.Network(), x, y, train_mode=False)
+    model_golden("mfcc_bgru_golden.npz", R_mb.Network(), x, y)
+    model_golden("spec_bgru_golden.npz", R_sb.Network(), x, y)
+    x2, y2 = synthetic_clips(2, seed=6)
+    model_golden("resnet_bgru_golden.npz", R_rb.Network(), x2, y2, train_mode=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,100 @@
+"""K1-K4 feature kernels on the GPU vs the oracle and the reference's golden vectors."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import features as OF
+from tolerances import MFCC_REL, fbank_ok, mfcc_err, spec_ok
+from speechrecognitionproject_amd import features as K
+from speechrecognitionproject_amd.synthetic import synthetic_clips, synthetic_noise_bank, synthetic_noise_draws
+
+pytestmark = pytest.mark.gpu
+
+
+def test_fbank_vs_reference_golden(gpu):
+    g = golden("fbank_golden.npz")
+    out = K.fbank(torch.from_numpy(g["pcm"])).cpu().numpy()
+    for o, r in zip(out, g["out"]):
+        ok, errs = fbank_ok(o, r)
+        assert ok, errs
+
+
+def test_fbank_vs_oracle_synthetic(gpu):
+    x, _ = synthetic_clips(40, seed=11)
+    out = K.fbank(torch.from_numpy(x)).cpu().numpy()
+    for o, c in zip(out, x):
+        ok, errs = fbank_ok(o, OF.filter_banks(c))
+        assert ok, errs
+
+
+def test_spec_vs_reference_golden(gpu):
+    g = golden("spec_golden.npz")
+    out = K.spec(torch.from_numpy(g["pcm"])).cpu().numpy()
+    for o, r in zip(out, g["out"]):
+        ok, errs = spec_ok(o, r)
+        assert ok, errs
+    t = K.spec(torch.from_numpy(g["pcm"]), transposed=True).cpu().numpy()
+    assert np.array_equal(t, out.transpose(0, 2, 1))
+
+
+def test_spec_vs_oracle_synthetic(gpu):
+    x, _ = synthetic_clips(30, seed=12)
+    out = K.spec(torch.from_numpy(x)).cpu().numpy()
+    for o, c in zip(out, x):
+        ok, errs = spec_ok(o, OF.compute_spec(c))
+        assert ok, errs
+
+
+def test_mfcc_vs_oracle(gpu):
+    g = golden("mfcc_glue_golden.npz")
+    x = np.concatenate([g["pcm"], synthetic_clips(30, seed=13)[0]])
+    out = K.mfcc(torch.from_numpy(x)).cpu().numpy()
+    for o, c in zip(out, x):
+        assert mfcc_err(o, OF.compute_mfcc(c)) <= MFCC_REL
+    tm = K.mfcc(torch.from_numpy(x), time_major=True).cpu().numpy()
+    assert np.array_equal(tm, out.transpose(0, 2, 1))
+
+
+def test_mfcc_silence_known_answer(gpu):
+    out = K.mfcc(torch.zeros(3, 16000)).cpu().numpy()
+    assert np.allclose(out[:, 0], -100 * np.sqrt(128), rtol=1e-5)
+    assert np.abs(out[:, 1:]).max() < 1e-3
+
+
+def test_noise_mix_bit_exact_vs_reference_golden(gpu):
+    g = golden("noise_mix_golden.npz")
+    pcm = g["pcm"].astype(np.int16)
+    out = K.noise_mix(pcm, g["bank"], g["file_idx"], g["start"], g["gain"]).cpu().numpy()
+    assert np.array_equal(out, g["out"].astype(np.float32))
+
+
+def test_noise_mix_bit_exact_vs_oracle_large(gpu):
+    n = 2048
+    x, _ = synthetic_clips(n, seed=3, clip=30000)
+    bank = synthetic_noise_bank()
+    f, o, gns = synthetic_noise_draws(n)
+    out = K.noise_mix(x.astype(np.int16), bank, f, o, gns).cpu().numpy()
+    ref = np.stack([OF.add_noise_uniform(x[i].astype(np.int16), bank[f[i]], int(o[i]), float(gns[i])) for i in range(n)])
+    assert np.array_equal(out, ref.astype(np.float32))
+
+
+@pytest.mark.parametrize("fn", ["fbank", "mfcc", "spec"])
+def test_batch_independence_and_determinism(gpu, fn):
+    # size-independent properties at a large batch: each clip's features do not depend on the
+    # batch it is in, and two launches are bitwise identical
+    x, _ = synthetic_clips(4096, seed=21)
+    xd = torch.from_numpy(x).cuda()
+    f = getattr(K, fn)
+    a = f(xd)
+    b = f(xd)
+    assert torch.equal(a, b)
+    idx = [0, 1, 777, 4095]
+    single = torch.cat([f(xd[i:i + 1]) for i in idx])
+    assert torch.equal(a[idx], single)
+    assert torch.isfinite(a).all()
+
+
+def test_empty_batch(gpu):
+    assert K.fbank(torch.zeros(0, 16000)).shape == (0, 98, 120)
+    assert K.mfcc(torch.zeros(0, 16000)).shape == (0, 39, 51)

@@ -67,6 +67,48 @@ int srk_noise_mix(const int16_t* pcm, const int16_t* bank, int64_t n_files, int6
                   const int64_t* file_idx, const int64_t* offset, const double* gain,
                   int64_t n_clips, float* out, void* stream);
 
+/* ---------------------------------------------------------------- dense algebra (fp32 MFMA)
+ * C[M,N] = alpha * op(A) op(B) + beta * C (+ bias), row-major.  op(A) = A [M,K] (lda) or, with
+ * trans_a, A stored [K,M]; op(B) = B [K,N] (ldb) or, with trans_b, B stored [N,K].
+ * bias_mode: 0 none, 1 bias[N] per column, 2 bias[M] per row.  Replaces the cuBLAS/CPU GEMMs of
+ * nn.Linear (model_mfcc_bgru.py:26,36; model_fbanks_cnn.py:80-81,99-100).                  */
+int srk_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
+                 int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc,
+                 const float* bias, int bias_mode, void* stream);
+/* out[n] = beta * out[n] + sum_m X[m, n]  (bias gradients).                                 */
+int srk_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, float beta, void* stream);
+
+/* ---------------------------------------------------------------- K5: bidirectional GRU layer
+ * nn.GRU(in, H, bidirectional=True, batch_first=True), one layer, PyTorch gate order [r; z; n],
+ * h0 = 0 (model_mfcc_bgru.py:25,35; model_spec_bgru.py:23,33; model_resnet_bgru.py:130,135).
+ * x [B, T, in]; y [B, T, 2H] (forward direction in [..., :H], reverse in [..., H:]).
+ * Weights are direction-stacked: w_ih [2][3H][in] (= weight_ih_lK ; weight_ih_lK_reverse),
+ * w_hh [2][3H][H], b_ih [2][3H], b_hh [2][3H].  H must be a multiple of 32.
+ * ws (fwd, kept until the backward): srk_gru_workspace_floats(.., backward=0) floats;
+ * ws (bwd scratch): srk_gru_workspace_floats(.., backward=1) floats.
+ * Backward OVERWRITES dw_ih, dw_hh, db_ih, db_hh (same stacked layouts) and dx [B, T, in]
+ * (dx may be NULL when the input needs no gradient).                                        */
+int64_t srk_gru_workspace_floats(int64_t B, int64_t T, int64_t in, int64_t H, int backward);
+int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t H, const float* w_ih,
+                      const float* w_hh, const float* b_ih, const float* b_hh, float* y, float* ws,
+                      void* stream);
+int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t H, const float* w_ih,
+                      const float* w_hh, const float* y, const float* ws_fwd, const float* dy, float* dx,
+                      float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, float* ws, void* stream);
+
+/* ---------------------------------------------------------------- K7/K8: step ops
+ * Cross-entropy, mean over the batch (nn.CrossEntropyLoss, training.py:73,87):
+ * loss[0] = mean_b(logsumexp(logits_b) - logits_b[label_b]); dlogits (nullable) =
+ * (softmax - onehot) / B.  ws: B + 1 floats.  An out-of-range label makes the loss NaN.     */
+int srk_cross_entropy(const float* logits, const int64_t* labels, int64_t B, int64_t C, float* loss,
+                      float* dlogits, float* ws, void* stream);
+/* torch.optim.Adam step (no weight decay / amsgrad) over n contiguous floats (training.py:74,91);
+ * step is the 1-based step count after increment; grad is multiplied by grad_scale first.   */
+int srk_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
+                  float beta1, float beta2, float eps, int64_t step, float grad_scale, void* stream);
+/* y = keep ? x * scale : 0 (nn.Dropout with an explicit Bernoulli keep-mask, scale = 1/(1-p)). */
+int srk_dropout_apply(const float* x, const uint8_t* keep, int64_t n, float scale, float* y, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

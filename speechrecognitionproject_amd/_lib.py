@@ -30,8 +30,16 @@ _SIGS = {
     "srk_mfcc_fwd": [_P, _I64, _P, _I, _P],
     "srk_spec_fwd": [_P, _I64, _P, _I, _P],
     "srk_noise_mix": [_P, _P, _I64, _I64, _P, _P, _P, _I64, _P, _P],
+    "srk_gemm_f32": [_I, _I, _I64, _I64, _I64, _F, _P, _I64, _P, _I64, _F, _P, _I64, _P, _I, _P],
+    "srk_colsum_f32": [_P, _I64, _I64, _I64, _P, _F, _P],
+    "srk_gru_workspace_floats": [_I64, _I64, _I64, _I64, _I],
+    "srk_gru_layer_fwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P],
+    "srk_gru_layer_bwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "srk_cross_entropy": [_P, _P, _I64, _I64, _P, _P, _P, _P],
+    "srk_adam_step": [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _I64, _F, _P],
+    "srk_dropout_apply": [_P, _P, _I64, _F, _P, _P],
 }
-_RESTYPE = {"srk_last_error": ctypes.c_char_p}
+_RESTYPE = {"srk_last_error": ctypes.c_char_p, "srk_gru_workspace_floats": ctypes.c_int64}
 
 
 class SrkError(RuntimeError):

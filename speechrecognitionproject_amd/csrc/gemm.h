@@ -1,0 +1,27 @@
+// Internal GEMM interface (row-major):  C[M,N] = alpha * op(A) * op(B) + beta * C (+ bias)
+//   op(A) = A [M,K] (lda)       or A^T with A stored [K,M] when ta
+//   op(B) = B [K,N] (ldb)       or B^T with B stored [N,K] when tb
+// bias_mode: 0 none, 1 bias[N] added to every row, 2 bias[M] added to every column.
+// Batched over `batch` with element strides sA/sB/sC (0 = shared operand).
+#pragma once
+#include "srk_internal.h"
+
+namespace srk {
+
+struct GemmDesc {
+  int64_t M = 0, N = 0, K = 0;
+  const float* A = nullptr; int64_t lda = 0; bool ta = false;
+  const float* B = nullptr; int64_t ldb = 0; bool tb = false;
+  float* C = nullptr; int64_t ldc = 0;
+  float alpha = 1.f, beta = 0.f;
+  const float* bias = nullptr; int bias_mode = 0;
+  int batch = 1; int64_t sA = 0, sB = 0, sC = 0;
+};
+
+// Enqueue on `stream`; returns SRK_OK or an srk_status.
+int gemm_f32(const GemmDesc& d, hipStream_t stream);
+
+// Column sums: out[n] = beta*out[n] + sum_m X[m, n] (X row-major [M,N], ldx).
+int colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, float beta, hipStream_t stream);
+
+}  // namespace srk

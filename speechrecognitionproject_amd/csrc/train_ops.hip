@@ -1,0 +1,150 @@
+// K7/K8: the small training-step kernels around the acoustic models.
+//  * cross-entropy (mean over the batch) forward + backward  — nn.CrossEntropyLoss, training.py:73,87
+//  * Adam (beta1, beta2, eps; no weight decay, no amsgrad)     — torch.optim.Adam, training.py:74,91
+//    over one flat fp32 parameter buffer (one launch for the whole model)
+//  * inverted dropout with an explicit mask                     — nn.Dropout(), model_fbanks_cnn.py:79,98
+#include "srk_internal.h"
+
+namespace srk {
+namespace {
+
+// One wave per row; C <= 64 * 4.  loss_rows[b] = logsumexp(x_b) - x_b[label_b];
+// dx = (softmax(x_b) - onehot(label_b)) * scale.
+__global__ __launch_bounds__(256) void ce_rows_kernel(const float* __restrict__ x, const int64_t* __restrict__ labels,
+                                                      int B, int C, float scale, float* __restrict__ loss_rows,
+                                                      float* __restrict__ dx, int* __restrict__ bad) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float* row = x + (size_t)b * C;
+  const int64_t lab = labels[b];
+  if (lab < 0 || lab >= C) {   // out-of-range label: the loss becomes NaN (loud), flag set
+    if (lane == 0) {
+      atomicExch(bad, 1);
+      loss_rows[b] = NAN;
+    }
+    return;
+  }
+  float m = -INFINITY;
+  for (int c = lane; c < C; c += 64) m = fmaxf(m, row[c]);
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += expf(row[c] - m);
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float lse = m + logf(s);
+  if (lane == 0) loss_rows[b] = lse - row[lab];
+  if (dx)
+    for (int c = lane; c < C; c += 64) dx[(size_t)b * C + c] = (expf(row[c] - lse) - (c == lab ? 1.f : 0.f)) * scale;
+}
+
+// Deterministic mean of the per-row losses (one workgroup).
+__global__ __launch_bounds__(256) void mean_kernel(const float* __restrict__ v, int n, float* __restrict__ out) {
+  __shared__ float part[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += v[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = part[0] / (float)n;
+}
+
+// torch.optim.Adam single-tensor update, in torch's operation order:
+//   m = b1*m + (1-b1)*g ; v = b2*v + (1-b2)*g*g
+//   denom = sqrt(v) / sqrt(1 - b2^t) + eps ; p -= (lr / (1 - b1^t)) * m / denom
+// grad_scale multiplies g first (1/world for a summed all-reduce, or 1).
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
+                            float bc1, float bc2_sqrt, float grad_scale) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 3 < n) {
+      float4 gv = *reinterpret_cast<const float4*>(g + i);
+      float4 mv = *reinterpret_cast<float4*>(m + i);
+      float4 vv = *reinterpret_cast<float4*>(v + i);
+      float4 pv = *reinterpret_cast<float4*>(p + i);
+      float* gp = &gv.x; float* mp = &mv.x; float* vp = &vv.x; float* pp = &pv.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float gg = gp[k] * grad_scale;
+        mp[k] = mp[k] * b1 + (1.f - b1) * gg;
+        vp[k] = vp[k] * b2 + (1.f - b2) * gg * gg;
+        const float denom = sqrtf(vp[k]) / bc2_sqrt + eps;
+        pp[k] = pp[k] - (lr / bc1) * (mp[k] / denom);
+      }
+      *reinterpret_cast<float4*>(m + i) = mv;
+      *reinterpret_cast<float4*>(v + i) = vv;
+      *reinterpret_cast<float4*>(p + i) = pv;
+    } else {
+      for (int64_t k = i; k < n; ++k) {
+        const float gg = g[k] * grad_scale;
+        m[k] = m[k] * b1 + (1.f - b1) * gg;
+        v[k] = v[k] * b2 + (1.f - b2) * gg * gg;
+        const float denom = sqrtf(v[k]) / bc2_sqrt + eps;
+        p[k] = p[k] - (lr / bc1) * (m[k] / denom);
+      }
+    }
+  }
+}
+
+__global__ void dropout_kernel(const float* __restrict__ x, const uint8_t* __restrict__ keep, int64_t n, float scale,
+                               float* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = keep[i] ? x[i] * scale : 0.f;
+}
+
+}  // namespace
+}  // namespace srk
+
+extern "C" {
+
+int srk_cross_entropy(const float* logits, const int64_t* labels, int64_t B, int64_t C, float* loss,
+                      float* dlogits, float* ws, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(B > 0 && C > 0 && C <= 4096, SRK_ERR_INVALID, "cross_entropy: bad shape");
+  SRK_REQUIRE(logits && labels && loss && ws, SRK_ERR_INVALID, "cross_entropy: null pointer");
+  hipStream_t s = srk::as_stream(stream);
+  // ws: B floats of per-row loss, then one int error flag
+  int* bad = reinterpret_cast<int*>(ws + B);
+  SRK_CHECK_HIP(hipMemsetAsync(bad, 0, sizeof(int), s));
+  hipLaunchKernelGGL(srk::ce_rows_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, logits, labels, (int)B,
+                     (int)C, 1.0f / (float)B, ws, dlogits, bad);
+  hipLaunchKernelGGL(srk::mean_kernel, dim3(1), dim3(256), 0, s, ws, (int)B, loss);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
+                  float beta1, float beta2, float eps, int64_t step, float grad_scale, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(n >= 0 && step >= 1, SRK_ERR_INVALID, "adam: bad n/step");
+  if (n == 0) return SRK_OK;
+  SRK_REQUIRE(param && grad && exp_avg && exp_avg_sq, SRK_ERR_INVALID, "adam: null pointer");
+  SRK_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
+              SRK_ERR_INVALID, "adam: buffers must be 16-byte aligned");
+  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  const int nt = 256;
+  const int64_t blocks = std::min<int64_t>((n + nt * 4 - 1) / (nt * 4), 256 * 8);
+  hipLaunchKernelGGL(srk::adam_kernel, dim3((unsigned)blocks), dim3(nt), 0, srk::as_stream(stream), param, grad,
+                     exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, (float)bc1, (float)std::sqrt(bc2), grad_scale);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_dropout_apply(const float* x, const uint8_t* keep, int64_t n, float scale, float* y, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(n >= 0 && (n == 0 || (x && keep && y)), SRK_ERR_INVALID, "dropout: bad args");
+  if (n == 0) return SRK_OK;
+  hipLaunchKernelGGL(srk::dropout_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, srk::as_stream(stream), x,
+                     keep, n, scale, y);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+}  // extern "C"

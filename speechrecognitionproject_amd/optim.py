@@ -1,0 +1,71 @@
+"""Flat parameter/gradient buffers and the fused Adam of training.py:74,91 (srk_adam_step).
+
+``FlatParams`` re-homes every parameter of a module into ONE contiguous fp32 buffer (each
+tensor 256-byte aligned) and points ``p.grad`` at views of ONE gradient buffer, so that
+  * the optimizer step is a single kernel launch over the whole model, and
+  * the data-parallel gradient exchange is a single all-reduce of one buffer (parallel.py).
+"""
+import torch
+
+from ._lib import call
+from .features import ptr, require_gpu, stream_ptr
+
+_ALIGN = 64   # floats
+
+
+class FlatParams:
+    def __init__(self, params, device=None):
+        require_gpu()
+        self.params = [p for p in params if p.requires_grad]
+        device = device or self.params[0].device
+        offs, n = [], 0
+        for p in self.params:
+            offs.append(n)
+            n += (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.numel = n
+        self.offsets = offs
+        self.data = torch.zeros(n, device=device, dtype=torch.float32)
+        self.grad = torch.zeros(n, device=device, dtype=torch.float32)
+        with torch.no_grad():
+            for p, o in zip(self.params, offs):
+                k = p.numel()
+                self.data[o:o + k].copy_(p.data.reshape(-1))
+                p.data = self.data[o:o + k].view_as(p)
+                p.grad = self.grad[o:o + k].view_as(p)
+
+    def zero_grad(self):
+        self.grad.zero_()
+        # autograd may have replaced a view with a fresh tensor; re-attach the views
+        for p, o in zip(self.params, self.offsets):
+            if p.grad is None or p.grad.data_ptr() != self.grad[o:o + 1].data_ptr():
+                p.grad = self.grad[o:o + p.numel()].view_as(p)
+
+
+class Adam(torch.optim.Optimizer):
+    """torch.optim.Adam semantics (betas=(0.9, 0.999), eps=1e-8, no weight decay), one fused
+    HIP launch per step over a FlatParams buffer.  ``grad_scale`` (e.g. 1/world_size after a
+    summed all-reduce) multiplies the gradient inside the kernel."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, flat=None):
+        params = list(params)
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+        self.flat = flat if flat is not None else FlatParams(params)
+        self.exp_avg = torch.zeros_like(self.flat.data)
+        self.exp_avg_sq = torch.zeros_like(self.flat.data)
+        self.step_count = 0
+        self.grad_scale = 1.0
+
+    def zero_grad(self, set_to_none=False):
+        self.flat.zero_grad()
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        g = self.param_groups[0]
+        self.step_count += 1
+        b1, b2 = g["betas"]
+        f = self.flat
+        call("srk_adam_step", ptr(f.data), ptr(f.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq), f.numel,
+             float(g["lr"]), float(b1), float(b2), float(g["eps"]), self.step_count, float(self.grad_scale),
+             stream_ptr())
+        return loss

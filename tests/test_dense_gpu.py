@@ -1,0 +1,100 @@
+"""GEMM / GRU / Linear / cross-entropy / Adam kernels vs plain PyTorch fp32 (CPU) references."""
+import numpy as np
+import pytest
+import torch
+
+from speechrecognitionproject_amd import nn as snn
+from speechrecognitionproject_amd._lib import call
+from speechrecognitionproject_amd.features import ptr, stream_ptr
+from speechrecognitionproject_amd.optim import Adam, FlatParams
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (37, 29, 39), (130, 260, 70), (300, 129, 1024), (12, 1024, 4)])
+def test_gemm_f32(gpu, ta, tb, M, N, K):
+    g = torch.Generator().manual_seed(M * 1000 + N + K)
+    A = torch.randn((K, M) if ta else (M, K), generator=g)
+    B = torch.randn((N, K) if tb else (K, N), generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    ref = 0.5 * ((A.T if ta else A).double() @ (B.T if tb else B).double()) + 2.0 * C0.double() + bias.double()
+    Ad, Bd, Cd, bd = A.cuda(), B.cuda(), C0.clone().cuda(), bias.cuda()
+    call("srk_gemm_f32", ta, tb, M, N, K, 0.5, ptr(Ad), Ad.shape[1], ptr(Bd), Bd.shape[1], 2.0, ptr(Cd), N,
+         ptr(bd), 1, stream_ptr())
+    out = Cd.cpu().double()
+    assert (out - ref).abs().max() <= 1e-5 * (1 + (A.abs().max() * B.abs().max() * K).item())
+
+
+def _ref_gru(IN, H, L):
+    return torch.nn.GRU(IN, H, num_layers=L, bidirectional=True, batch_first=True)
+
+
+@pytest.mark.parametrize("B,T,IN,H,L", [(5, 7, 39, 64, 2), (33, 3, 20, 32, 1), (4, 51, 39, 512, 2)])
+def test_bigru_fwd_bwd_vs_torch(gpu, B, T, IN, H, L):
+    torch.manual_seed(0)
+    ref = _ref_gru(IN, H, L)
+    mine = snn.BiGRU(IN, H, num_layers=L).cuda()
+    mine.load_state_dict(ref.state_dict())
+    x = torch.randn(B, T, IN)
+    w = torch.randn(B, T, 2 * H)
+    xr = x.clone().requires_grad_(True)
+    yr, hr = ref(xr)
+    (yr * w).sum().backward()
+    xm = x.cuda().requires_grad_(True)
+    ym, hm = mine(xm)
+    (ym * w.cuda()).sum().backward()
+    tol = 2e-5 * max(1.0, T / 10)
+    assert (ym.detach().cpu() - yr.detach()).abs().max() <= tol
+    assert (hm.detach().cpu() - hr.detach()).abs().max() <= tol
+    assert (xm.grad.cpu() - xr.grad).abs().max() <= 50 * tol * (1 + xr.grad.abs().max())
+    refp = dict(ref.named_parameters())
+    for n, p in mine.named_parameters():
+        gr = refp[n].grad
+        err = (p.grad.cpu() - gr).abs().max() / (gr.abs().max() + 1e-12)
+        assert err <= 1e-4, (n, float(err))
+
+
+def test_linear_strided_and_ce(gpu):
+    torch.manual_seed(1)
+    ref = torch.nn.Linear(1024, 12)
+    mine = snn.Linear(1024, 12).cuda()
+    mine.load_state_dict(ref.state_dict())
+    h = torch.randn(6, 5, 1024)
+    labels = torch.tensor([0, 3, 11, 5, 5, 2])
+    hr = h.clone().requires_grad_(True)
+    lr_ = torch.nn.CrossEntropyLoss()(ref(hr[:, -1, :]), labels)
+    lr_.backward()
+    hm = h.cuda().requires_grad_(True)
+    lm = snn.CrossEntropyLoss()(mine(hm[:, -1, :]), labels.cuda())
+    lm.backward()
+    assert abs(lm.item() - lr_.item()) <= 1e-5 * max(1, abs(lr_.item()))
+    assert (hm.grad.cpu() - hr.grad).abs().max() <= 1e-6
+    assert (mine.weight.grad.cpu() - ref.weight.grad).abs().max() <= 1e-6
+    assert (mine.bias.grad.cpu() - ref.bias.grad).abs().max() <= 1e-6
+
+
+def test_ce_bad_label_is_nan(gpu):
+    loss = snn.CrossEntropyLoss()(torch.zeros(2, 12, device="cuda"), torch.tensor([0, 12], device="cuda"))
+    assert torch.isnan(loss).item()
+
+
+def test_adam_matches_torch(gpu):
+    torch.manual_seed(2)
+    ref = torch.nn.Linear(37, 5)
+    mine = torch.nn.Linear(37, 5).cuda()
+    mine.load_state_dict(ref.state_dict())
+    fp = FlatParams(mine.parameters())
+    opt_m = Adam(mine.parameters(), lr=1e-2, flat=fp)
+    opt_r = torch.optim.Adam(ref.parameters(), lr=1e-2)
+    for it in range(5):
+        x = torch.randn(8, 37)
+        opt_r.zero_grad()
+        ref(x).pow(2).sum().backward()
+        opt_r.step()
+        opt_m.zero_grad()
+        mine(x.cuda()).pow(2).sum().backward()
+        opt_m.step()
+    for (n, a), (_, b) in zip(ref.named_parameters(), mine.named_parameters()):
+        assert (a.detach() - b.detach().cpu()).abs().max() <= 1e-5, n

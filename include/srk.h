@@ -37,6 +37,13 @@ enum srk_status {
 int srk_version(void);                 /* ABI version, bumped on any signature change */
 const char* srk_last_error(void);      /* thread-local, never NULL */
 int srk_init(int device);              /* build + upload constant tables on `device` */
+/* Opt-in kernel timing: while enabled, instrumented launches record a HIP event pair on their
+ * stream; srk_prof_read sums, over every launch named `name` ("mfcc", "fbank", "spec",
+ * "noise_mix", "gemm_f32", "gru_fwd_step", "gru_bwd_step", "adam", ...), the elapsed time and
+ * the launches' ALGORITHMIC work (flops for matrix kernels, bytes for streaming kernels).
+ * srk_prof_enable synchronizes the device and clears previous records.                     */
+int srk_prof_enable(int on);
+int srk_prof_read(const char* name, int64_t* count, double* total_ms, double* total_work);
 
 /* ---------------------------------------------------------------- feature extraction
  * pcm: float32 [n_clips, 16000], int16-valued (NOT scaled to +-1), exactly what

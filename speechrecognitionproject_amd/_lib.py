@@ -26,6 +26,9 @@ _SIGS = {
     "srk_version": [],
     "srk_last_error": [],
     "srk_init": [_I],
+    "srk_prof_enable": [_I],
+    "srk_prof_read": [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
+                      ctypes.POINTER(ctypes.c_double)],
     "srk_fbank_fwd": [_P, _I64, _P, _P],
     "srk_mfcc_fwd": [_P, _I64, _P, _I, _P],
     "srk_spec_fwd": [_P, _I64, _P, _I, _P],
@@ -74,6 +77,19 @@ def call(name, *args):
         msg = lib().srk_last_error().decode(errors="replace")
         raise SrkError("%s failed (status %d): %s" % (name, rc, msg))
     return rc
+
+
+def prof_enable(on):
+    call("srk_prof_enable", 1 if on else 0)
+
+
+def prof_read(name):
+    """(launch count, total ms, total algorithmic work) of the recorded launches of `name`."""
+    n = ctypes.c_int64(0)
+    ms = ctypes.c_double(0.0)
+    w = ctypes.c_double(0.0)
+    call("srk_prof_read", name.encode(), ctypes.byref(n), ctypes.byref(ms), ctypes.byref(w))
+    return int(n.value), float(ms.value), float(w.value)
 
 
 def header_symbols():

@@ -398,6 +398,7 @@ int srk_fbank_fwd(const float* pcm, int64_t n_clips, float* out, void* stream) {
   SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_fbank_fwd: null pointer");
   const DeviceTables* t = nullptr;
   if (int rc = srk::get_tables(&t)) return rc;
+  srk::ProfScope prof("fbank", srk::as_stream(stream), 111040.0 * (double)n_clips);   // 64000 in + 47040 out B/clip
   hipLaunchKernelGGL(srk::fbank_kernel, dim3((unsigned)n_clips), dim3(srk::kFbNT), 0, srk::as_stream(stream),
                      pcm, out, *t);
   SRK_CHECK_HIP(hipGetLastError());
@@ -412,6 +413,7 @@ int srk_spec_fwd(const float* pcm, int64_t n_clips, float* out, int transposed, 
   SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_spec_fwd: null pointer");
   const DeviceTables* t = nullptr;
   if (int rc = srk::get_tables(&t)) return rc;
+  srk::ProfScope prof("spec", srk::as_stream(stream), 126916.0 * (double)n_clips);    // 64000 + 62916 B/clip
   hipLaunchKernelGGL(srk::spec_kernel, dim3((unsigned)n_clips), dim3(srk::kSpNT), 0, srk::as_stream(stream),
                      pcm, out, transposed ? 1 : 0, (float)t->spec_scale, *t);
   SRK_CHECK_HIP(hipGetLastError());
@@ -427,6 +429,7 @@ int srk_mfcc_fwd(const float* pcm, int64_t n_clips, float* out, int layout, void
   SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_mfcc_fwd: null pointer");
   const DeviceTables* t = nullptr;
   if (int rc = srk::get_tables(&t)) return rc;
+  srk::ProfScope prof("mfcc", srk::as_stream(stream), 71956.0 * (double)n_clips);     // 64000 + 7956 B/clip
   hipLaunchKernelGGL(srk::mfcc_kernel, dim3((unsigned)n_clips), dim3(srk::kMfNT), 0, srk::as_stream(stream),
                      pcm, out, layout, *t);
   SRK_CHECK_HIP(hipGetLastError());
@@ -447,6 +450,7 @@ int srk_noise_mix(const int16_t* pcm, const int16_t* bank, int64_t n_files, int6
   const int64_t total8 = n_clips * (16000 / 8);
   const int nt = 256;
   const int64_t blocks = (total8 + nt - 1) / nt;
+  srk::ProfScope prof("noise_mix", srk::as_stream(stream), 128000.0 * (double)n_clips); // 32000+32000+64000 B/clip
   hipLaunchKernelGGL(srk::noise_mix_kernel, dim3((unsigned)blocks), dim3(nt), 0, srk::as_stream(stream), pcm, bank,
                      bank_len, file_idx, offset, gain, n_clips, out);
   SRK_CHECK_HIP(hipGetLastError());

@@ -166,6 +166,7 @@ template <bool TA, bool TB, int BM, int BN, int BK>
 int launch(const GemmDesc& d, hipStream_t s, bool vec_a, bool vec_b) {
   const int64_t tm = (d.M + BM - 1) / BM, tn = (d.N + BN - 1) / BN;
   SRK_REQUIRE(tm * tn <= INT32_MAX && d.batch <= 65535, SRK_ERR_INVALID, "gemm: grid too large");
+  ProfScope prof("gemm_f32", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
   hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK>), dim3((unsigned)(tm * tn), 1, (unsigned)d.batch),
                      dim3(256), 0, s, d, (int)tn, (int)vec_a, (int)vec_b);
   SRK_CHECK_HIP(hipGetLastError());

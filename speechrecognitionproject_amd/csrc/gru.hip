@@ -257,8 +257,10 @@ int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
   a.B = (int)B; a.T = (int)T; a.H = (int)H; a.in = (int)in;
   a.y_in = y; a.y = y; a.gi = gi; a.w_hh = w_hh; a.b_hh = b_hh; a.gates = gates;
   const dim3 grid((unsigned)((B + srk::kBMB - 1) / srk::kBMB), (unsigned)(H / srk::kBJ), 2);
-  for (int step = 0; step < T; ++step)
+  for (int step = 0; step < T; ++step) {
+    srk::ProfScope prof("gru_fwd_step", s, step > 0 ? 2.0 * 2.0 * (double)B * 3 * H * H : 0.0);   // 2 dirs x [B,H]x[H,3H]
     hipLaunchKernelGGL(srk::gru_fwd_step_kernel, grid, dim3(256), 0, s, a, step);
+  }
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END
@@ -282,8 +284,10 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
   a.y_in = y; a.w_hh = w_hh; a.gates = const_cast<float*>(ws_fwd + BT * 6 * H);
   a.dy = dy; a.dgi = dgi; a.dgh = dgh; a.dgh_edge = dgh_edge; a.dhz = dhz;
   const dim3 grid((unsigned)((B + srk::kBMB - 1) / srk::kBMB), (unsigned)(H / srk::kBJ), 2);
-  for (int step = 0; step < T; ++step)
+  for (int step = 0; step < T; ++step) {
+    srk::ProfScope prof("gru_bwd_step", s, step > 0 ? 2.0 * 2.0 * (double)B * 3 * H * H : 0.0);   // 2 dirs x [B,3H]x[3H,H]
     hipLaunchKernelGGL(srk::gru_bwd_step_kernel, grid, dim3(256), 0, s, a, step);
+  }
   SRK_CHECK_HIP(hipGetLastError());
 
   int rc;

@@ -65,4 +65,20 @@ int get_tables(const DeviceTables** out);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// RAII event pair around one kernel launch (prof.hip); inert unless srk_prof_enable(1).
+// `work` = the launch's ALGORITHMIC flops (matrix kernels) or bytes (streaming kernels).
+class ProfScope {
+ public:
+  ProfScope(const char* name, hipStream_t s, double work = 0.0);
+  ~ProfScope();
+  ProfScope(const ProfScope&) = delete;
+  ProfScope& operator=(const ProfScope&) = delete;
+
+ private:
+  const char* name_;
+  hipStream_t s_;
+  void* a_;
+  double work_;
+};
+
 }  // namespace srk

@@ -129,6 +129,7 @@ int srk_adam_step(float* param, const float* grad, float* exp_avg, float* exp_av
   const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
   const int nt = 256;
   const int64_t blocks = std::min<int64_t>((n + nt * 4 - 1) / (nt * 4), 256 * 8);
+  srk::ProfScope prof("adam", srk::as_stream(stream), 28.0 * (double)n);   // p,g,m,v read + p,m,v written
   hipLaunchKernelGGL(srk::adam_kernel, dim3((unsigned)blocks), dim3(nt), 0, srk::as_stream(stream), param, grad,
                      exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, (float)bc1, (float)std::sqrt(bc2), grad_scale);
   SRK_CHECK_HIP(hipGetLastError());

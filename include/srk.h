@@ -82,6 +82,11 @@ int srk_noise_mix(const int16_t* pcm, const int16_t* bank, int64_t n_files, int6
 int srk_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
                  int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc,
                  const float* bias, int bias_mode, void* stream);
+/* The same GEMM (alpha, beta, no bias) that also writes rowsum[m] = sum_k op(A)[m, k]: the weight
+ * and bias gradients of a Linear in one pass (dW = dY^T X, db = sum over the batch of dY).   */
+int srk_gemm_rowsum_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
+                        int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc,
+                        float* rowsum, void* stream);
 /* out[n] = beta * out[n] + sum_m X[m, n]  (bias gradients).                                 */
 int srk_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, float beta, void* stream);
 
@@ -90,7 +95,7 @@ int srk_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out
  * h0 = 0 (model_mfcc_bgru.py:25,35; model_spec_bgru.py:23,33; model_resnet_bgru.py:130,135).
  * x [B, T, in]; y [B, T, 2H] (forward direction in [..., :H], reverse in [..., H:]).
  * Weights are direction-stacked: w_ih [2][3H][in] (= weight_ih_lK ; weight_ih_lK_reverse),
- * w_hh [2][3H][H], b_ih [2][3H], b_hh [2][3H].  H must be a multiple of 32.
+ * w_hh [2][3H][H], b_ih [2][3H], b_hh [2][3H].  H must be a multiple of 128.
  * ws (fwd, kept until the backward): srk_gru_workspace_floats(.., backward=0) floats;
  * ws (bwd scratch): srk_gru_workspace_floats(.., backward=1) floats.
  * Backward OVERWRITES dw_ih, dw_hh, db_ih, db_hh (same stacked layouts) and dx [B, T, in]

@@ -17,6 +17,7 @@ LIB = os.path.join(PKG, "libsrk.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+         "-mllvm", "-disable-promote-alloca-to-lds",   # private arrays stay in VGPRs, never silently in LDS
          "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-I", os.path.join(REPO, "include")]
 
 

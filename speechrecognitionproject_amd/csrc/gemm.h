@@ -3,6 +3,7 @@
 //   op(B) = B [K,N] (ldb)       or B^T with B stored [N,K] when tb
 // bias_mode: 0 none, 1 bias[N] added to every row, 2 bias[M] added to every column.
 // Batched over `batch` with element strides sA/sB/sC (0 = shared operand).
+// Long-K shapes are split over K internally (deterministic slab reduction, grow-only scratch).
 #pragma once
 #include "srk_internal.h"
 
@@ -16,6 +17,8 @@ struct GemmDesc {
   float alpha = 1.f, beta = 0.f;
   const float* bias = nullptr; int bias_mode = 0;
   int batch = 1; int64_t sA = 0, sB = 0, sC = 0;
+  // optional fused row sums of op(A): rowsum[m] = rowsum_beta * rowsum[m] + sum_k op(A)[m, k]
+  float* rowsum = nullptr; float rowsum_beta = 0.f;
 };
 
 // Enqueue on `stream`; returns SRK_OK or an srk_status.

@@ -20,14 +20,23 @@
 namespace srk {
 namespace {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int kBMB = 32;   // batch rows per workgroup
-constexpr int kBJ = 32;    // hidden units per workgroup
-constexpr int kBK = 32;    // k per LDS stage
+// Recurrence step tiling.  One workgroup = 64 batch rows x 16 hidden units of one direction
+// (all three gates: 48 columns of W_hh for the forward step), 4 waves = 4 x 16 rows.
+// Both operands are staged ROW-major in LDS (row pitch BK+4 floats) and read as float4: for
+// MFMA k-substep s a lane with k-quad q uses k = kbase + 4q + s, for A and B alike (any fixed
+// permutation of k is a valid GEMM order), so one ds_read_b128 feeds four v_mfma_f32_16x16x4_f32.
+// Workgroup -> (direction, batch group, unit slice) is XCD-aware: the 32 workgroups that share
+// an XCD (blockIdx % 8, observed round-robin dispatch) take the slices of ONE (direction, group)
+// pair, so that direction's W_hh (3 MB fp32) stays resident in that XCD's 4 MB L2 from one step
+// launch to the next.  (Placement only changes speed, never results.)
+constexpr int kRows = 64;    // batch rows per workgroup
+constexpr int kUnits = 16;   // hidden units per workgroup
+constexpr int kBK = 128;     // k per LDS stage
+constexpr int kPitch = kBK + 4;
 
 struct GruArgs {
   int B, T, H, in;
+  int G, S;             // batch groups (ceil(B/64)), unit slices (H/16)
   const float* y_in;    // fwd: y (h_prev source); bwd: y
   float* y;             // fwd output [B][T][2H]
   const float* gi;      // [B*T][6H]
@@ -43,54 +52,73 @@ struct GruArgs {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Native 4-float vector: HIP's float4 is a struct whose copies lower to memcpy, which SROA cannot
+// keep in registers (a float4 staging array ends up in scratch); ext_vector loads/stores do not.
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4f ld4(const float* p) { return *reinterpret_cast<const v4f*>(p); }
+__device__ __forceinline__ void st4(float* p, v4f v) { *reinterpret_cast<v4f*>(p) = v; }
+
+__device__ __forceinline__ void map_block(const GruArgs& a, int& dir, int& group, int& slice) {
+  const int nwg = 2 * a.G * a.S;
+  const int b = blockIdx.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  const int pair = wgid / a.S;
+  slice = wgid % a.S;
+  dir = pair / a.G;
+  group = pair % a.G;
+}
+
 // ------------------------------------------------------------------ forward step
+// gh[b, g*H + j] = sum_k h_prev[b, k] W_hh[g*H + j, k];  epilogue = the GRU cell.
 __global__ __launch_bounds__(256) void gru_fwd_step_kernel(GruArgs a, int step) {
-  __shared__ float As[2][kBK][kBMB + 16];
-  __shared__ float Bs[2][kBK][3 * kBJ + 16];
+  constexpr int WR = 3 * kUnits;                        // W rows (gate columns) per workgroup
+  constexpr int VA = kRows * kBK / 4 / 256;             // float4 per thread per stage: 8
+  constexpr int VW = WR * kBK / 4 / 256;                // 6
+  __shared__ __attribute__((aligned(16))) float smem[2 * (kRows + WR) * kPitch];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int lr = lane >> 4, lc = lane & 15;
-  const int rh = wave & 1, ch = wave >> 1;
-  const int dir = blockIdx.z;
+  const int lr = lane & 15, lq = lane >> 4;
+  int dir, group, slice;
+  map_block(a, dir, group, slice);
   const int B = a.B, T = a.T, H = a.H;
   const int t = dir == 0 ? step : T - 1 - step;
   const int tprev = dir == 0 ? t - 1 : t + 1;
-  const int b0 = blockIdx.x * kBMB, j0 = blockIdx.y * kBJ;
+  const int b0 = group * kRows, j0 = slice * kUnits;
   const float* __restrict__ W = a.w_hh + (size_t)dir * 3 * H * H;
 
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
   f32x4 acc[3];
 #pragma unroll
   for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (step > 0) {
-    // A = h_prev rows (y[b][tprev][dir*H + k]), B = W_hh rows {g*H + j0 + jj}
-    float4 ra, rb[3];
+    v4f ra[VA], rw[VW];
     auto load = [&](int k0) {
-      {
-        const int row = tid >> 3, kq = (tid & 7) * 4;
+#pragma unroll
+      for (int i = 0; i < VA; ++i) {
+        const int v = tid + i * 256, row = v / (kBK / 4), kq = (v % (kBK / 4)) * 4;
         const int b = b0 + row;
-        ra = b < B ? *reinterpret_cast<const float4*>(a.y_in + ((size_t)b * T + tprev) * 2 * H + dir * H + k0 + kq)
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        const v4f x = ld4(a.y_in + ((size_t)(b < B ? b : B - 1) * T + tprev) * 2 * H + dir * H + k0 + kq);
+        ra[i] = b < B ? x : v4f{0.f, 0.f, 0.f, 0.f};   // clamped row + select: no exec-masked loads
       }
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int vi = tid + i * 256;
-        const int c = vi >> 3, kq = (vi & 7) * 4;
-        const int g = c / kBJ, jj = c % kBJ;
-        rb[i] = *reinterpret_cast<const float4*>(W + (size_t)(g * H + j0 + jj) * H + k0 + kq);
+      for (int i = 0; i < VW; ++i) {
+        const int v = tid + i * 256, c = v / (kBK / 4), kq = (v % (kBK / 4)) * 4;
+        const int g = c / kUnits, jj = c % kUnits;
+        rw[i] = ld4(W + (size_t)(g * H + j0 + jj) * H + k0 + kq);
       }
     };
     auto store = [&](int buf) {
-      {
-        const int row = tid >> 3, kq = (tid & 7) * 4;
-        As[buf][kq + 0][row] = ra.x; As[buf][kq + 1][row] = ra.y;
-        As[buf][kq + 2][row] = ra.z; As[buf][kq + 3][row] = ra.w;
+      float* As = smem + buf * (kRows + WR) * kPitch;
+      float* Ws = As + kRows * kPitch;
+#pragma unroll
+      for (int i = 0; i < VA; ++i) {
+        const int v = tid + i * 256, row = v / (kBK / 4), kq = (v % (kBK / 4)) * 4;
+        st4(As + row * kPitch + kq, ra[i]);
       }
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int vi = tid + i * 256;
-        const int c = vi >> 3, kq = (vi & 7) * 4;
-        Bs[buf][kq + 0][c] = rb[i].x; Bs[buf][kq + 1][c] = rb[i].y;
-        Bs[buf][kq + 2][c] = rb[i].z; Bs[buf][kq + 3][c] = rb[i].w;
+      for (int i = 0; i < VW; ++i) {
+        const int v = tid + i * 256, c = v / (kBK / 4), kq = (v % (kBK / 4)) * 4;
+        st4(Ws + c * kPitch + kq, rw[i]);
       }
     };
     const int nk = H / kBK;
@@ -100,24 +128,35 @@ __global__ __launch_bounds__(256) void gru_fwd_step_kernel(GruArgs a, int step) 
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
       if (kt + 1 < nk) load((kt + 1) * kBK);
+      const float* As = smem + cur * (kRows + WR) * kPitch;
+      const float* Ws = As + kRows * kPitch;
 #pragma unroll
-      for (int kk = 0; kk < kBK; kk += 4) {
-        const float av = As[cur][kk + lr][rh * 16 + lc];
+      for (int kb = 0; kb < kBK; kb += 16) {
+        const v4f av = ld4(As + (wave * 16 + lr) * kPitch + kb + 4 * lq);
+        v4f wv[3];
 #pragma unroll
-        for (int g = 0; g < 3; ++g)
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, Bs[cur][kk + lr][g * kBJ + ch * 16 + lc], acc[g], 0, 0, 0);
+        for (int g = 0; g < 3; ++g) wv[g] = ld4(Ws + (g * kUnits + lr) * kPitch + kb + 4 * lq);
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, wv[g].x, acc[g], 0, 0, 0);
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, wv[g].y, acc[g], 0, 0, 0);
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, wv[g].z, acc[g], 0, 0, 0);
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, wv[g].w, acc[g], 0, 0, 0);
+        }
       }
+      asm volatile("" ::: "memory");      // keep the stage-k+1 LDS store (and its vmcnt wait)
+      __builtin_amdgcn_sched_barrier(0);   // after this stage's MFMAs
       if (kt + 1 < nk) store(cur ^ 1);
       __syncthreads();
     }
   }
 
-  // epilogue: lane owns rows rh*16 + 4*lr + r, unit j = j0 + ch*16 + lc, all three gates
-  const int j = j0 + ch * 16 + lc;
+  // epilogue: lane owns rows 16*wave + 4*lq + r, unit j = j0 + lr, all three gates
+  const int j = j0 + lr;
   const float bhr = a.b_hh[dir * 3 * H + j], bhz = a.b_hh[dir * 3 * H + H + j], bhn = a.b_hh[dir * 3 * H + 2 * H + j];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int b = b0 + rh * 16 + lr * 4 + r;
+    const int b = b0 + wave * 16 + lq * 4 + r;
     if (b >= B) continue;
     const float* gi = a.gi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
     const float ghn = acc[2][r] + bhn;
@@ -136,38 +175,58 @@ __global__ __launch_bounds__(256) void gru_fwd_step_kernel(GruArgs a, int step) 
 }
 
 // ------------------------------------------------------------------ backward step
+// dh_rec[b, j] = sum_c dgh_next[b, c] W_hh[c, j] (c over 3H);  epilogue = the cell derivatives.
 __global__ __launch_bounds__(256) void gru_bwd_step_kernel(GruArgs a, int step) {
-  __shared__ float As[2][kBK][kBMB + 16];
-  __shared__ float Bs[2][kBK][kBJ + 16];
+  constexpr int VA = kRows * kBK / 4 / 256;             // 8
+  constexpr int VW = kBK * kUnits / 4 / 256;            // 2
+  __shared__ __attribute__((aligned(16))) float smem[2 * (kRows + kUnits) * kPitch];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int lr = lane >> 4, lc = lane & 15;
-  const int rh = wave & 1, ch = wave >> 1;
-  const int dir = blockIdx.z;
+  const int lr = lane & 15, lq = lane >> 4;
+  int dir, group, slice;
+  map_block(a, dir, group, slice);
   const int B = a.B, T = a.T, H = a.H;
   const int t = dir == 0 ? T - 1 - step : step;          // time processed now
   const int tnext = dir == 0 ? t + 1 : t - 1;           // processed by the previous step
   const int tprev = dir == 0 ? t - 1 : t + 1;           // h_prev source
   const bool edge = (step == T - 1);                    // h_prev = 0 here
-  const int b0 = blockIdx.x * kBMB, j0 = blockIdx.y * kBJ;
+  const int b0 = group * kRows, j0 = slice * kUnits;
   const float* __restrict__ W = a.w_hh + (size_t)dir * 3 * H * H;
   const float* __restrict__ dghn = a.dgh + (size_t)dir * B * T * 3 * H;   // [B][T][3H] of this dir
 
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   if (step > 0) {
-    // dh_rec[b][j] = sum_c dgh[b][tnext][c] * W_hh[c][j],  c in [0, 3H)
-    float4 ra, rb;
+    v4f ra[VA], rw[VW];
     auto load = [&](int k0) {
-      const int row = tid >> 3, q = (tid & 7) * 4;
-      const int b = b0 + row;
-      ra = b < B ? *reinterpret_cast<const float4*>(dghn + ((size_t)b * T + tnext) * 3 * H + k0 + q)
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
-      rb = *reinterpret_cast<const float4*>(W + (size_t)(k0 + row) * H + j0 + q);
+#pragma unroll
+      for (int i = 0; i < VA; ++i) {
+        const int v = tid + i * 256, row = v / (kBK / 4), kq = (v % (kBK / 4)) * 4;
+        const int b = b0 + row;
+        const v4f x = ld4(dghn + ((size_t)(b < B ? b : B - 1) * T + tnext) * 3 * H + k0 + kq);
+        ra[i] = b < B ? x : v4f{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < VW; ++i) {   // W_hh[k0 + kr][j0 .. j0+15], 4 units per float4
+        const int v = tid + i * 256, kr = v / (kUnits / 4), jq = (v % (kUnits / 4)) * 4;
+        rw[i] = ld4(W + (size_t)(k0 + kr) * H + j0 + jq);
+      }
     };
     auto store = [&](int buf) {
-      const int row = tid >> 3, q = (tid & 7) * 4;
-      As[buf][q + 0][row] = ra.x; As[buf][q + 1][row] = ra.y;
-      As[buf][q + 2][row] = ra.z; As[buf][q + 3][row] = ra.w;
-      *reinterpret_cast<float4*>(&Bs[buf][row][q]) = rb;
+      float* As = smem + buf * (kRows + kUnits) * kPitch;
+      float* Ws = As + kRows * kPitch;    // [unit][k]
+#pragma unroll
+      for (int i = 0; i < VA; ++i) {
+        const int v = tid + i * 256, row = v / (kBK / 4), kq = (v % (kBK / 4)) * 4;
+        st4(As + row * kPitch + kq, ra[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < VW; ++i) {
+        const int v = tid + i * 256, kr = v / (kUnits / 4), jq = (v % (kUnits / 4)) * 4;
+        Ws[(jq + 0) * kPitch + kr] = rw[i].x;
+        Ws[(jq + 1) * kPitch + kr] = rw[i].y;
+        Ws[(jq + 2) * kPitch + kr] = rw[i].z;
+        Ws[(jq + 3) * kPitch + kr] = rw[i].w;
+      }
     };
     const int nk = 3 * H / kBK;
     load(0);
@@ -176,20 +235,28 @@ __global__ __launch_bounds__(256) void gru_bwd_step_kernel(GruArgs a, int step) 
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
       if (kt + 1 < nk) load((kt + 1) * kBK);
+      const float* As = smem + cur * (kRows + kUnits) * kPitch;
+      const float* Ws = As + kRows * kPitch;
 #pragma unroll
-      for (int kk = 0; kk < kBK; kk += 4)
-        acc[(kk >> 2) & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(As[cur][kk + lr][rh * 16 + lc],
-                                                                   Bs[cur][kk + lr][ch * 16 + lc],
-                                                                   acc[(kk >> 2) & 1], 0, 0, 0);
+      for (int kb = 0; kb < kBK; kb += 16) {
+        const v4f av = ld4(As + (wave * 16 + lr) * kPitch + kb + 4 * lq);
+        const v4f wv = ld4(Ws + lr * kPitch + kb + 4 * lq);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, wv.x, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, wv.y, acc[1], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, wv.z, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, wv.w, acc[1], 0, 0, 0);
+      }
+      asm volatile("" ::: "memory");      // keep the stage-k+1 LDS store (and its vmcnt wait)
+      __builtin_amdgcn_sched_barrier(0);   // after this stage's MFMAs
       if (kt + 1 < nk) store(cur ^ 1);
       __syncthreads();
     }
   }
 
-  const int j = j0 + ch * 16 + lc;
+  const int j = j0 + lr;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int b = b0 + rh * 16 + lr * 4 + r;
+    const int b = b0 + wave * 16 + lq * 4 + r;
     if (b >= B) continue;
     float* dhz = a.dhz + ((size_t)dir * B + b) * H + j;
     float dh = a.dy[((size_t)b * T + t) * 2 * H + dir * H + j];
@@ -220,7 +287,7 @@ __global__ __launch_bounds__(256) void gru_bwd_step_kernel(GruArgs a, int step) 
 
 int check_dims(int64_t B, int64_t T, int64_t in, int64_t H) {
   SRK_REQUIRE(B > 0 && T > 0 && in > 0 && H > 0, SRK_ERR_INVALID, "gru: dims must be positive");
-  SRK_REQUIRE(H % kBJ == 0 && H % kBK == 0, SRK_ERR_INVALID, "gru: hidden size must be a multiple of 32");
+  SRK_REQUIRE(H % kBK == 0, SRK_ERR_INVALID, "gru: hidden size must be a multiple of 128");
   SRK_REQUIRE(B * T * 6 * H < ((int64_t)1 << 40), SRK_ERR_INVALID, "gru: problem too large");
   return SRK_OK;
 }
@@ -256,7 +323,9 @@ int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
   srk::GruArgs a{};
   a.B = (int)B; a.T = (int)T; a.H = (int)H; a.in = (int)in;
   a.y_in = y; a.y = y; a.gi = gi; a.w_hh = w_hh; a.b_hh = b_hh; a.gates = gates;
-  const dim3 grid((unsigned)((B + srk::kBMB - 1) / srk::kBMB), (unsigned)(H / srk::kBJ), 2);
+  a.G = (int)((B + srk::kRows - 1) / srk::kRows);
+  a.S = (int)(H / srk::kUnits);
+  const dim3 grid((unsigned)(2 * a.G * a.S));
   for (int step = 0; step < T; ++step) {
     srk::ProfScope prof("gru_fwd_step", s, step > 0 ? 2.0 * 2.0 * (double)B * 3 * H * H : 0.0);   // 2 dirs x [B,H]x[H,3H]
     hipLaunchKernelGGL(srk::gru_fwd_step_kernel, grid, dim3(256), 0, s, a, step);
@@ -283,7 +352,9 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
   a.B = (int)B; a.T = (int)T; a.H = (int)H; a.in = (int)in;
   a.y_in = y; a.w_hh = w_hh; a.gates = const_cast<float*>(ws_fwd + BT * 6 * H);
   a.dy = dy; a.dgi = dgi; a.dgh = dgh; a.dgh_edge = dgh_edge; a.dhz = dhz;
-  const dim3 grid((unsigned)((B + srk::kBMB - 1) / srk::kBMB), (unsigned)(H / srk::kBJ), 2);
+  a.G = (int)((B + srk::kRows - 1) / srk::kRows);
+  a.S = (int)(H / srk::kUnits);
+  const dim3 grid((unsigned)(2 * a.G * a.S));
   for (int step = 0; step < T; ++step) {
     srk::ProfScope prof("gru_bwd_step", s, step > 0 ? 2.0 * 2.0 * (double)B * 3 * H * H : 0.0);   // 2 dirs x [B,3H]x[3H,H]
     hipLaunchKernelGGL(srk::gru_bwd_step_kernel, grid, dim3(256), 0, s, a, step);
@@ -291,29 +362,34 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
   SRK_CHECK_HIP(hipGetLastError());
 
   int rc;
-  {  // dW_ih_cat[6H, in] = dgi^T [6H, BT] * x [BT, in]
+  {  // dW_ih_cat[6H, in] = dgi^T [6H, BT] * x [BT, in]; db_ih fused as the row sums of dgi^T
     GemmDesc g;
     g.M = 6 * H; g.N = in; g.K = BT;
     g.A = dgi; g.lda = 6 * H; g.ta = true;
     g.B = x; g.ldb = in;
     g.C = dw_ih; g.ldc = in;
+    g.rowsum = db_ih;
     if ((rc = srk::gemm_f32(g, s))) return rc;
   }
-  if ((rc = srk::colsum_f32(dgi, BT, 6 * H, 6 * H, db_ih, 0.f, s))) return rc;
   for (int dir = 0; dir < 2; ++dir) {
     // dW_hh[dir][3H, H] = sum_(b,t) dgh[b][t]^T h_prev[b][t]; h_prev of row (b,t) is y row (b,t-1)
     // (dir 0) or (b,t+1) (dir 1); the edge rows of dgh are zero so the batch seams contribute 0.
+    // db_hh = row sums of dgh^T (fused) + the edge rows kept aside in dgh_edge.
     const float* dg = dgh + (size_t)dir * BT * 3 * H;
+    float* dbh = db_hh + dir * 3 * H;
     GemmDesc g;
     g.M = 3 * H; g.N = H; g.K = BT - 1;
     g.ta = true; g.lda = 3 * H; g.ldb = 2 * H;
     g.A = dir == 0 ? dg + 3 * H : dg;
     g.B = dir == 0 ? y + dir * H : y + 2 * H + dir * H;
     g.C = dw_hh + (size_t)dir * 3 * H * H; g.ldc = H;
-    if (g.K > 0 && (rc = srk::gemm_f32(g, s))) return rc;
-    if (g.K == 0) SRK_CHECK_HIP(hipMemsetAsync(g.C, 0, sizeof(float) * 3 * H * H, s));
-    float* dbh = db_hh + dir * 3 * H;
-    if ((rc = srk::colsum_f32(dg, BT, 3 * H, 3 * H, dbh, 0.f, s))) return rc;
+    g.rowsum = dbh;
+    if (g.K > 0) {
+      if ((rc = srk::gemm_f32(g, s))) return rc;
+    } else {
+      SRK_CHECK_HIP(hipMemsetAsync(g.C, 0, sizeof(float) * 3 * H * H, s));
+      SRK_CHECK_HIP(hipMemsetAsync(dbh, 0, sizeof(float) * 3 * H, s));
+    }
     if ((rc = srk::colsum_f32(dgh_edge + (size_t)dir * B * 3 * H, B, 3 * H, 3 * H, dbh, 1.f, s))) return rc;
   }
   if (dx) {  // dx[BT, in] = dgi[BT, 6H] * W_ih_cat[6H, in]

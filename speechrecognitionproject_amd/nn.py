@@ -117,10 +117,16 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty((M, K), device=x.device)
             call("srk_gemm_f32", 0, 0, M, K, N, 1.0, ptr(dy), N, ptr(w), K, 0.0, ptr(dx), K, None, 0, s)
+        want_db = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             dw = torch.empty((N, K), device=x.device)
-            call("srk_gemm_f32", 1, 0, N, K, M, 1.0, ptr(dy), N, ptr(x), x.stride(0), 0.0, ptr(dw), K, None, 0, s)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+            if want_db:   # dW = dy^T x with db = row sums of dy^T fused into the same kernel
+                db = torch.empty((N,), device=x.device)
+                call("srk_gemm_rowsum_f32", 1, 0, N, K, M, 1.0, ptr(dy), N, ptr(x), x.stride(0), 0.0, ptr(dw), K,
+                     ptr(db), s)
+            else:
+                call("srk_gemm_f32", 1, 0, N, K, M, 1.0, ptr(dy), N, ptr(x), x.stride(0), 0.0, ptr(dw), K, None, 0, s)
+        if want_db and db is None:
             db = torch.empty((N,), device=x.device)
             call("srk_colsum_f32", ptr(dy), M, N, N, ptr(db), 0.0, s)
         return dx, dw, db

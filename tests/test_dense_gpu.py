@@ -31,7 +31,7 @@ def _ref_gru(IN, H, L):
     return torch.nn.GRU(IN, H, num_layers=L, bidirectional=True, batch_first=True)
 
 
-@pytest.mark.parametrize("B,T,IN,H,L", [(5, 7, 39, 64, 2), (33, 3, 20, 32, 1), (4, 51, 39, 512, 2)])
+@pytest.mark.parametrize("B,T,IN,H,L", [(5, 7, 39, 128, 2), (33, 3, 20, 128, 1), (70, 5, 16, 256, 1), (4, 51, 39, 512, 2)])
 def test_bigru_fwd_bwd_vs_torch(gpu, B, T, IN, H, L):
     torch.manual_seed(0)
     ref = _ref_gru(IN, H, L)
@@ -98,3 +98,32 @@ def test_adam_matches_torch(gpu):
         opt_m.step()
     for (n, a), (_, b) in zip(ref.named_parameters(), mine.named_parameters()):
         assert (a.detach() - b.detach().cpu()).abs().max() <= 1e-5, n
+
+
+@pytest.mark.parametrize("ta", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(96, 64, 13056), (3072, 39, 4999), (12, 1024, 256)])
+def test_gemm_rowsum_splitk(gpu, ta, M, N, K):
+    # the weight-gradient shape class: tall K (split over K), fused row sums of op(A) (= db)
+    g = torch.Generator().manual_seed(K)
+    A = torch.randn((K, M) if ta else (M, K), generator=g)
+    B = torch.randn(K, N, generator=g)
+    opA = (A.T if ta else A).double()
+    ref = opA @ B.double()
+    ref_rs = opA.sum(1)
+    Ad, Bd = A.cuda(), B.cuda()
+    C = torch.empty(M, N, device="cuda")
+    rs = torch.empty(M, device="cuda")
+    for _ in range(2):   # deterministic: two launches are bitwise equal
+        call("srk_gemm_rowsum_f32", ta, 0, M, N, K, 1.0, ptr(Ad), Ad.shape[1], ptr(Bd), N, 0.0, ptr(C), N, ptr(rs),
+             stream_ptr())
+        c1, r1 = C.clone(), rs.clone()
+    assert torch.equal(c1, C) and torch.equal(r1, rs)
+    assert (C.cpu().double() - ref).abs().max() <= 1e-5 * (1 + 4 * K ** 0.5 * 16)
+    assert (rs.cpu().double() - ref_rs).abs().max() <= 1e-3
+
+
+def test_colsum_large(gpu):
+    X = torch.randn(13056, 3072)
+    out = torch.empty(3072, device="cuda")
+    call("srk_colsum_f32", ptr(X.cuda()), 13056, 3072, 3072, ptr(out), 0.0, stream_ptr())
+    assert (out.cpu().double() - X.double().sum(0)).abs().max() <= 1e-3

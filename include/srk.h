@@ -108,6 +108,28 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
                       const float* w_hh, const float* y, const float* ws_fwd, const float* dy, float* dx,
                       float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, float* ws, void* stream);
 
+/* ---------------------------------------------------------------- K6: convolution / pooling
+ * nn.Conv2d / nn.Conv1d (zero padding ph/pw, stride sh/sw, no dilation/groups) as implicit GEMM
+ * on CHANNELS-LAST activations: x [N][H][W][Ci], y [N][Ho][Wo][Co], Ho = (H + 2ph - KH)/sh + 1.
+ * Weights stay in torch layout w [Co][Ci][KH][KW] (the state_dict tensor), bias [Co] (nullable).
+ * ws: srk_conv2d_workspace_floats() floats (re-laid-out weights).  The 1-D convolutions of
+ * model_resnet_bgru.py are H = 1, KH = 1.  Replaces model_fbanks_cnn.py:72-75,89-94.
+ * Backward writes dw [Co][Ci][KH][KW] (overwrite), db (nullable) and dx (nullable).          */
+int64_t srk_conv2d_workspace_floats(int64_t Ci, int64_t Co, int64_t KH, int64_t KW);
+int srk_conv2d_nhwc_fwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w,
+                        const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh,
+                        int64_t sw, float* y, float* ws, void* stream);
+int srk_conv2d_nhwc_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co,
+                        int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw, const float* dy,
+                        float* dx, float* dw, float* db, float* ws, void* stream);
+/* Max pooling, window = stride = (kh, kw), floor mode, channels-last (nn.MaxPool2d((1,3)),
+ * ((1,4)) and nn.MaxPool1d(98), model_fbanks_cnn.py:73,75,78).  Backward routes each gradient to
+ * the first maximum of its window, as PyTorch does.                                          */
+int srk_maxpool_nhwc_fwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t C, int64_t kh, int64_t kw,
+                         float* y, void* stream);
+int srk_maxpool_nhwc_bwd(const float* x, const float* dy, int64_t N, int64_t H, int64_t W, int64_t C, int64_t kh,
+                         int64_t kw, float* dx, void* stream);
+
 /* ---------------------------------------------------------------- K7/K8: step ops
  * Cross-entropy, mean over the batch (nn.CrossEntropyLoss, training.py:73,87):
  * loss[0] = mean_b(logsumexp(logits_b) - logits_b[label_b]); dlogits (nullable) =
@@ -118,7 +140,10 @@ int srk_cross_entropy(const float* logits, const int64_t* labels, int64_t B, int
  * step is the 1-based step count after increment; grad is multiplied by grad_scale first.   */
 int srk_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
                   float beta1, float beta2, float eps, int64_t step, float grad_scale, void* stream);
-/* y = keep ? x * scale : 0 (nn.Dropout with an explicit Bernoulli keep-mask, scale = 1/(1-p)). */
+/* nn.Dropout(p) training forward: keep[i] = Bernoulli(1-p) from a counter-based hash of
+ * (seed, i) (not torch's RNG stream), y = keep ? x / (1-p) : 0.                              */
+int srk_dropout_fwd(const float* x, int64_t n, float p, uint64_t seed, float* y, uint8_t* keep, void* stream);
+/* y = keep ? x * scale : 0 (dropout with an explicit keep-mask; also its backward).          */
 int srk_dropout_apply(const float* x, const uint8_t* keep, int64_t n, float scale, float* y, void* stream);
 
 #ifdef __cplusplus

@@ -39,11 +39,20 @@ _SIGS = {
     "srk_gru_workspace_floats": [_I64, _I64, _I64, _I64, _I],
     "srk_gru_layer_fwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P],
     "srk_gru_layer_bwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "srk_conv2d_workspace_floats": [_I64, _I64, _I64, _I64],
+    "srk_conv2d_nhwc_fwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P,
+                            _P],
+    "srk_conv2d_nhwc_bwd": [_P, _I64, _I64, _I64, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P,
+                            _P, _P, _P],
+    "srk_maxpool_nhwc_fwd": [_P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P],
+    "srk_maxpool_nhwc_bwd": [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P],
     "srk_cross_entropy": [_P, _P, _I64, _I64, _P, _P, _P, _P],
     "srk_adam_step": [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _I64, _F, _P],
+    "srk_dropout_fwd": [_P, _I64, _F, ctypes.c_uint64, _P, _P, _P],
     "srk_dropout_apply": [_P, _P, _I64, _F, _P, _P],
 }
-_RESTYPE = {"srk_last_error": ctypes.c_char_p, "srk_gru_workspace_floats": ctypes.c_int64}
+_RESTYPE = {"srk_last_error": ctypes.c_char_p, "srk_gru_workspace_floats": ctypes.c_int64,
+            "srk_conv2d_workspace_floats": ctypes.c_int64}
 
 
 class SrkError(RuntimeError):

@@ -89,6 +89,24 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   }
 }
 
+// Counter-based Bernoulli mask (splitmix64 of seed ^ index): keep with probability 1 - p.
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);   // 24 random bits -> [0, 1)
+}
+
+__global__ void dropout_fwd_kernel(const float* __restrict__ x, int64_t n, float p, float scale, uint64_t seed,
+                                   float* __restrict__ y, uint8_t* __restrict__ keep) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool k = uniform01(seed, (uint64_t)i) >= p;
+  keep[i] = k;
+  y[i] = k ? x[i] * scale : 0.f;
+}
+
 __global__ void dropout_kernel(const float* __restrict__ x, const uint8_t* __restrict__ keep, int64_t n, float scale,
                                float* __restrict__ y) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -132,6 +150,17 @@ int srk_adam_step(float* param, const float* grad, float* exp_avg, float* exp_av
   srk::ProfScope prof("adam", srk::as_stream(stream), 28.0 * (double)n);   // p,g,m,v read + p,m,v written
   hipLaunchKernelGGL(srk::adam_kernel, dim3((unsigned)blocks), dim3(nt), 0, srk::as_stream(stream), param, grad,
                      exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, (float)bc1, (float)std::sqrt(bc2), grad_scale);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_dropout_fwd(const float* x, int64_t n, float p, uint64_t seed, float* y, uint8_t* keep, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(n >= 0 && p >= 0.f && p < 1.f && (n == 0 || (x && y && keep)), SRK_ERR_INVALID, "dropout_fwd: bad args");
+  if (n == 0) return SRK_OK;
+  hipLaunchKernelGGL(srk::dropout_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, srk::as_stream(stream), x,
+                     n, p, 1.0f / (1.0f - p), seed, y, keep);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END

@@ -181,3 +181,165 @@ class CrossEntropyLoss(tnn.Module):
     def forward(self, logits, labels):
         require_gpu()
         return _CrossEntropyFn.apply(logits, labels)
+
+
+# ----------------------------------------------------------------------------- conv / pool (NHWC)
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+class _Conv2dNHWCFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, padding, stride):
+        x = x.contiguous()
+        w = w.contiguous()
+        _check_cuda(x, w, b)
+        N, H, W, Ci = x.shape
+        Co, Ci2, KH, KW = w.shape
+        if Ci2 != Ci:
+            raise _lib.SrkError("conv: input has %d channels, weight expects %d" % (Ci, Ci2))
+        ph, pw = padding
+        sh, sw = stride
+        Ho, Wo = (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
+        y = torch.empty((N, Ho, Wo, Co), device=x.device)
+        ws = torch.empty(int(_lib.lib().srk_conv2d_workspace_floats(Ci, Co, KH, KW)), device=x.device)
+        call("srk_conv2d_nhwc_fwd", ptr(x), N, H, W, Ci, ptr(w), ptr(b) if b is not None else None, Co, KH, KW,
+             ph, pw, sh, sw, ptr(y), ptr(ws), stream_ptr())
+        ctx.save_for_backward(x, w)
+        ctx.geom = (padding, stride, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        (ph, pw), (sh, sw), has_b = ctx.geom
+        N, H, W, Ci = x.shape
+        Co, _, KH, KW = w.shape
+        dy = dy.contiguous()
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty_like(w)
+        db = torch.empty((Co,), device=x.device) if has_b else None
+        ws = torch.empty(int(_lib.lib().srk_conv2d_workspace_floats(Ci, Co, KH, KW)), device=x.device)
+        call("srk_conv2d_nhwc_bwd", ptr(x), N, H, W, Ci, ptr(w), Co, KH, KW, ph, pw, sh, sw, ptr(dy),
+             ptr(dx) if dx is not None else None, ptr(dw), ptr(db) if db is not None else None, ptr(ws), stream_ptr())
+        return dx, dw, db, None, None
+
+
+class Conv2d(tnn.Module):
+    """nn.Conv2d-compatible parameters (weight [Co, Ci, KH, KW], bias [Co], torch init) applied to
+    CHANNELS-LAST input [N, H, W, Ci] -> [N, Ho, Wo, Co] (the models keep activations NHWC)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, bias=True):
+        super().__init__()
+        ref = tnn.Conv2d(in_channels, out_channels, kernel_size, stride=stride, padding=padding, bias=bias)
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.kernel_size, self.stride, self.padding = ref.kernel_size, ref.stride, ref.padding
+        self.weight = tnn.Parameter(ref.weight.detach().clone())
+        self.bias = tnn.Parameter(ref.bias.detach().clone()) if bias else None
+
+    def forward(self, x):
+        require_gpu()
+        return _Conv2dNHWCFn.apply(x, self.weight, self.bias, self.padding, self.stride)
+
+
+class Conv1d(tnn.Module):
+    """nn.Conv1d-compatible parameters (weight [Co, Ci, K]) on channels-last input [N, L, Ci]."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, bias=True):
+        super().__init__()
+        ref = tnn.Conv1d(in_channels, out_channels, kernel_size, stride=stride, padding=padding, bias=bias)
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.kernel_size, self.stride, self.padding = ref.kernel_size, ref.stride, ref.padding
+        self.weight = tnn.Parameter(ref.weight.detach().clone())
+        self.bias = tnn.Parameter(ref.bias.detach().clone()) if bias else None
+
+    def forward(self, x):
+        require_gpu()
+        N, L, C = x.shape
+        y = _Conv2dNHWCFn.apply(x.reshape(N, 1, L, C), self.weight.unsqueeze(2), self.bias, (0, self.padding[0]),
+                                (1, self.stride[0]))
+        return y.reshape(N, y.shape[2], self.out_channels)
+
+
+class _MaxPoolNHWCFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kh, kw):
+        x = x.contiguous()
+        _check_cuda(x)
+        N, H, W, C = x.shape
+        y = torch.empty((N, H // kh, W // kw, C), device=x.device)
+        call("srk_maxpool_nhwc_fwd", ptr(x), N, H, W, C, kh, kw, ptr(y), stream_ptr())
+        ctx.save_for_backward(x)
+        ctx.k = (kh, kw)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        kh, kw = ctx.k
+        N, H, W, C = x.shape
+        dx = torch.empty_like(x)
+        call("srk_maxpool_nhwc_bwd", ptr(x), ptr(dy.contiguous()), N, H, W, C, kh, kw, ptr(dx), stream_ptr())
+        return dx, None, None
+
+
+class MaxPool2d(tnn.Module):
+    """nn.MaxPool2d(kernel_size) (stride = kernel, floor mode) on channels-last input."""
+
+    def __init__(self, kernel_size):
+        super().__init__()
+        self.kernel_size = _pair(kernel_size)
+
+    def forward(self, x):
+        return _MaxPoolNHWCFn.apply(x, self.kernel_size[0], self.kernel_size[1])
+
+
+class MaxPool1d(tnn.Module):
+    """nn.MaxPool1d(kernel_size) (stride = kernel) over the length axis of [N, L, C] input."""
+
+    def __init__(self, kernel_size):
+        super().__init__()
+        self.kernel_size = kernel_size
+
+    def forward(self, x):
+        N, L, C = x.shape
+        y = _MaxPoolNHWCFn.apply(x.reshape(N, L, 1, C), self.kernel_size, 1)
+        return y.reshape(N, L // self.kernel_size, C)
+
+
+class _DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, seed):
+        x = x.contiguous()
+        _check_cuda(x)
+        y = torch.empty_like(x)
+        keep = torch.empty(x.shape, device=x.device, dtype=torch.uint8)
+        call("srk_dropout_fwd", ptr(x), x.numel(), float(p), int(seed), ptr(y), ptr(keep), stream_ptr())
+        ctx.save_for_backward(keep)
+        ctx.scale = 1.0 / (1.0 - p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (keep,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        call("srk_dropout_apply", ptr(dy), ptr(keep), dy.numel(), float(ctx.scale), ptr(dx), stream_ptr())
+        return dx, None, None
+
+
+class Dropout(tnn.Module):
+    """nn.Dropout(p=0.5): identity in eval mode; in training a Bernoulli(1-p) mask from a
+    counter-based hash seeded per call (seed advances every forward)."""
+
+    def __init__(self, p=0.5, seed=0):
+        super().__init__()
+        self.p = p
+        self._seed = int(seed) * 1000003 + 12345
+        self._calls = 0
+
+    def forward(self, x):
+        if not self.training or self.p == 0.0:
+            return x
+        self._calls += 1
+        return _DropoutFn.apply(x, self.p, (self._seed + self._calls * 0x9E3779B1) & ((1 << 63) - 1))

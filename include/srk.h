@@ -130,6 +130,20 @@ int srk_maxpool_nhwc_fwd(const float* x, int64_t N, int64_t H, int64_t W, int64_
 int srk_maxpool_nhwc_bwd(const float* x, const float* dy, int64_t N, int64_t H, int64_t W, int64_t C, int64_t kh,
                          int64_t kw, float* dx, void* stream);
 
+/* ---------------------------------------------------------------- K9: batch norm (+ residual, ReLU)
+ * nn.BatchNorm1d on channels-last x [M][C] (M = N * L), fused with an optional residual add and
+ * ReLU: y = act((x - mean) * invstd * gamma + beta [+ residual]) (model_resnet_bgru.py:20-39,49).
+ * training = 1: batch statistics (biased variance), running stats updated in place with
+ * `momentum` (unbiased variance), as nn.BatchNorm1d; training = 0: running statistics.
+ * save_mean / save_invstd [C] are written for the backward.  Backward takes the forward's y (for
+ * the ReLU mask) and writes dx (nullable), dgamma, dbeta and dresidual (nullable).            */
+int srk_batchnorm_fwd(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta, float eps,
+                      float momentum, int training, float* running_mean, float* running_var, const float* residual,
+                      int relu, float* y, float* save_mean, float* save_invstd, void* stream);
+int srk_batchnorm_bwd(const float* x, const float* y, const float* dy, int64_t M, int64_t C, const float* gamma,
+                      const float* save_mean, const float* save_invstd, int training, int relu, float* dx,
+                      float* dgamma, float* dbeta, float* dresidual, void* stream);
+
 /* ---------------------------------------------------------------- K7/K8: step ops
  * Cross-entropy, mean over the batch (nn.CrossEntropyLoss, training.py:73,87):
  * loss[0] = mean_b(logsumexp(logits_b) - logits_b[label_b]); dlogits (nullable) =

@@ -1,0 +1,117 @@
+"""Drop-in for the reference plugin ``models/model_resnet_bgru.py``: raw-waveform ResNet-18-style
+1-D front end (Conv1d k=80/s=16 stem, 4 stages x 2 BasicBlocks with k=15 convs, BatchNorm, ReLU)
+-> Linear(512, 512) per step -> 2-layer BiGRU(512) -> Linear(1024, 12) on the last step
+(model_resnet_bgru.py:14-150).
+
+Same constructor ``Network(num_features=512, num_layers=2, mode=0)``, ``state_dict`` keys/shapes
+(including the ``mode == 1`` backend head, :57-71, so reference checkpoints load) and helpers.
+Activations stay channels-last [B, L, C] through the ResNet, so the reference's transpose before
+``fc1`` (:107-111) is free.  Convolutions = K6, BatchNorm(+residual+ReLU) = K9, GRU = K5.
+``mode == 1`` (the auxiliary backend of the staged training, :113-118) is not implemented on the
+device path and raises.
+
+BatchNorm under data parallelism uses per-rank batch statistics.
+"""
+import torch
+import torch.nn as nn
+
+from ..nn import BatchNorm1d, BiGRU, Conv1d, Linear
+from ._common import DEVICE, accuracy, class_accuracy   # noqa: F401
+
+
+def _kaiming(conv):
+    nn.init.kaiming_normal_(conv.weight, mode="fan_out", nonlinearity="relu")
+
+
+class BasicBlock(nn.Module):
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.kernel_size, self.padding = 15, 7
+        self.conv1 = Conv1d(inplanes, planes, 15, stride=stride, padding=7, bias=False)
+        self.bn1 = BatchNorm1d(planes)
+        self.conv2 = Conv1d(planes, planes, 15, stride=1, padding=7, bias=False)
+        self.bn2 = BatchNorm1d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        residual = x
+        if self.downsample is not None:
+            residual = self.downsample[1](self.downsample[0](x))
+        out = self.bn1(self.conv1(x), relu=True)
+        return self.bn2(self.conv2(out), residual=residual, relu=True)
+
+
+class ResNet(nn.Module):
+    def __init__(self, block, mode):
+        super().__init__()
+        self.mode = mode
+        self.inplanes = 64
+        self.dim = 125
+        self.conv1 = Conv1d(1, 64, kernel_size=80, stride=16, padding=38, bias=False)
+        self.bn1 = BatchNorm1d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.layer1 = self._make_layer(block, 64, 2)
+        self.layer2 = self._make_layer(block, 128, 2, stride=2)
+        self.layer3 = self._make_layer(block, 256, 2, stride=2)
+        self.layer4 = self._make_layer(block, 512, 2, stride=2)
+        self.fc1 = Linear(512, 512)
+        # mode == 1 auxiliary head: kept for state_dict compatibility (model_resnet_bgru.py:57-71)
+        self.backend_conv1 = nn.Sequential(
+            nn.Conv1d(self.dim, 2 * self.dim, 5, 2, 0, bias=False), nn.BatchNorm1d(2 * self.dim), nn.ReLU(True),
+            nn.MaxPool1d(2, 2),
+            nn.Conv1d(2 * self.dim, 4 * self.dim, 5, 2, 0, bias=False), nn.BatchNorm1d(4 * self.dim), nn.ReLU(True))
+        self.backend_conv2 = nn.Sequential(
+            nn.Linear(4 * self.dim, self.dim), nn.BatchNorm1d(self.dim), nn.ReLU(True), nn.Linear(self.dim, 12))
+        for m in self.modules():
+            if isinstance(m, (Conv1d, nn.Conv1d)):
+                _kaiming(m)
+
+    def _make_layer(self, block, planes, blocks, stride=1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes:
+            downsample = nn.Sequential(Conv1d(self.inplanes, planes, kernel_size=1, stride=stride, bias=False),
+                                       BatchNorm1d(planes))
+        layers = [block(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes
+        for _ in range(1, blocks):
+            layers.append(block(self.inplanes, planes))
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        # x: [B, L, 1] channels-last waveform
+        x = self.bn1(self.conv1(x), relu=True)            # [B, 1000, 64]
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))   # [B, 125, 512]
+        bs, sl, _ = x.shape
+        x = self.fc1(x.reshape(bs * sl, -1))
+        if self.mode == 1:
+            raise NotImplementedError("model_resnet_bgru mode=1 backend head is not on the device path")
+        return x.view(bs, sl, 512)
+
+
+class GRU(nn.Module):
+    def __init__(self, num_features=512, num_layers=2):
+        super().__init__()
+        self.gru = BiGRU(512, num_features, num_layers=num_layers, bidirectional=True, batch_first=True)
+        self.fc2 = Linear(num_features * 2, 12)
+
+    def forward(self, x):
+        x, _ = self.gru(x)
+        return self.fc2(x[:, -1, :])
+
+
+class Network(nn.Module):
+    def __init__(self, num_features=512, num_layers=2, mode=0):
+        super().__init__()
+        self.mode = mode
+        self.resnet = ResNet(BasicBlock, mode=mode)
+        self.gru = GRU(num_features=num_features, num_layers=num_layers)
+
+    def forward(self, x):
+        if not torch.is_tensor(x):
+            x = torch.as_tensor(x)
+        x = x.to(DEVICE, torch.float32).reshape(x.shape[0], -1, 1)   # [B, 16000, 1]
+        x = self.resnet(x)
+        if self.mode != 1:
+            x = self.gru(x)
+        return x

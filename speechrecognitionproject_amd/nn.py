@@ -343,3 +343,60 @@ class Dropout(tnn.Module):
             return x
         self._calls += 1
         return _DropoutFn.apply(x, self.p, (self._seed + self._calls * 0x9E3779B1) & ((1 << 63) - 1))
+
+
+# ----------------------------------------------------------------------------- batch norm
+class _BatchNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu):
+        x = x.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        _check_cuda(x, gamma, beta, residual)
+        y = torch.empty_like(x)
+        mean = torch.empty(C, device=x.device)
+        invstd = torch.empty(C, device=x.device)
+        res = residual.contiguous() if residual is not None else None
+        call("srk_batchnorm_fwd", ptr(x), M, C, ptr(gamma), ptr(beta), float(eps), float(momentum), int(training),
+             ptr(running_mean), ptr(running_var), ptr(res) if res is not None else None, int(relu), ptr(y), ptr(mean),
+             ptr(invstd), stream_ptr())
+        ctx.save_for_backward(x, y, gamma, mean, invstd)
+        ctx.flags = (int(training), int(relu), residual is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, gamma, mean, invstd = ctx.saved_tensors
+        training, relu, has_res = ctx.flags
+        C = x.shape[-1]
+        M = x.numel() // C
+        dy = dy.contiguous()
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dres = torch.empty_like(x) if has_res and ctx.needs_input_grad[3] else None
+        dgamma = torch.empty(C, device=x.device)
+        dbeta = torch.empty(C, device=x.device)
+        call("srk_batchnorm_bwd", ptr(x), ptr(y), ptr(dy), M, C, ptr(gamma), ptr(mean), ptr(invstd), training, relu,
+             ptr(dx) if dx is not None else None, ptr(dgamma), ptr(dbeta), ptr(dres) if dres is not None else None,
+             stream_ptr())
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None
+
+
+class BatchNorm1d(tnn.Module):
+    """nn.BatchNorm1d(C) parameters/buffers (weight, bias, running_mean, running_var,
+    num_batches_tracked) on channels-last input [..., C]; optional fused residual add + ReLU."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1):
+        super().__init__()
+        self.num_features, self.eps, self.momentum = num_features, eps, momentum
+        self.weight = tnn.Parameter(torch.ones(num_features))
+        self.bias = tnn.Parameter(torch.zeros(num_features))
+        self.register_buffer("running_mean", torch.zeros(num_features))
+        self.register_buffer("running_var", torch.ones(num_features))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+    def forward(self, x, residual=None, relu=False):
+        require_gpu()
+        if self.training:
+            self.num_batches_tracked.add_(1)
+        return _BatchNormFn.apply(x, self.weight, self.bias, residual, self.running_mean, self.running_var,
+                                  self.training, self.momentum, self.eps, relu)

@@ -1,0 +1,122 @@
+"""The reference's ``training.py`` entry point (training.py:29-117), on the MI355X path.
+
+    python training.py -key K -lr LR                               # reference CLI
+    python training.py --model mfcc_bgru --synthetic 4096 --epochs 1 --batch-size 256
+    python -m torch.distributed.run --nproc-per-node 8 training.py --synthetic 65536 ...
+
+Same loop: Adam(lr) + CrossEntropyLoss, ExponentialLR(0.87) stepped once per epoch after epoch 5,
+one ``str(loss)`` line per step appended to ``loss_<KEY>.txt``, per-epoch validation / training
+accuracy lines via the plugin's ``accuracy`` (``val_<KEY>.txt``, ``train_<KEY>.txt``) and
+``resample_unknown_class`` after each epoch.  Additions (all optional): ``--model`` selects the
+plugin instead of editing an import line (training.py:39-46), ``--synthetic N`` trains on
+synthetic clips when no Kaggle tree is available, ``--data-path/--output-path`` replace the
+hard-coded paths (:21-24), ``--log-every`` batches loss lines to avoid a host sync per step, and
+torchrun environments train data-parallel (one process per GPU, RCCL all-reduce).
+"""
+import argparse
+import importlib
+import os
+import time
+
+import torch
+from torch.utils.data import DataLoader
+
+from . import parallel
+from .nn import CrossEntropyLoss
+from .optim import Adam, FlatParams
+
+PLUGINS = ("mfcc_bgru", "fbanks_cnn", "spec_bgru", "resnet_bgru")
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument('-key', '--filekey', type=str, help='key for multiple trainings')
+    p.add_argument('-lr', '--learning_rate', type=float, help='LEARNING_RATE')
+    p.add_argument('--model', default='mfcc_bgru', choices=PLUGINS)
+    p.add_argument('--data-path', default=None, help="parent of 'audio' and the *_list.txt files")
+    p.add_argument('--output-path', default='.')
+    p.add_argument('--epochs', type=int, default=1)
+    p.add_argument('--batch-size', type=int, default=2)
+    p.add_argument('--synthetic', type=int, default=0, help='train on N synthetic clips instead of WAV files')
+    p.add_argument('--reduce', type=int, default=0, help='reduce_dataset(n) like training.py:66-67')
+    p.add_argument('--log-every', type=int, default=1, help='write buffered loss lines every n steps')
+    p.add_argument('--no-eval', action='store_true')
+    return p.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse(argv)
+    rank, world, local = parallel.init_from_env()
+    key = args.filekey or ''
+    lr = args.learning_rate if args.learning_rate is not None else 0.0001
+    mod = importlib.import_module('speechrecognitionproject_amd.models.model_' + args.model)
+    start = time.time()
+    device = torch.device('cuda', local)
+
+    if args.synthetic:
+        from .dataset import SyntheticDataset
+        data = SyntheticDataset(args.synthetic, seed=0)
+        valset = SyntheticDataset(max(args.synthetic // 10, args.batch_size), seed=1)
+    else:
+        from .dataset import Dataset
+        if not args.data_path:
+            raise SystemExit("--data-path (Kaggle layout) or --synthetic N is required")
+        data = Dataset(args.data_path + '/training_list.txt', args.data_path + '/audio')
+        valset = Dataset(args.data_path + '/validation_list.txt', args.data_path + '/audio')
+        if args.reduce:
+            data.reduce_dataset(args.reduce)
+            valset.reduce_dataset(args.reduce)
+
+    torch.manual_seed(0)
+    model = mod.Network().to(device)
+    flat = FlatParams(model.parameters())
+    optimizer = Adam(model.parameters(), lr=lr, flat=flat)
+    optimizer.grad_scale = 1.0 / world
+    parallel.broadcast_flat(flat)
+    scheduler = torch.optim.lr_scheduler.ExponentialLR(optimizer, 0.87)
+    criterion = CrossEntropyLoss()
+    os.makedirs(args.output_path, exist_ok=True)
+    loss_file = os.path.join(args.output_path, 'loss_' + key + '.txt')
+
+    epoch = 0
+    while epoch < args.epochs:
+        if epoch > 4:
+            scheduler.step()
+        if world > 1:
+            idx = parallel.shard_indices(len(data), rank, world, seed=0, epoch=epoch)
+            sampler = torch.utils.data.SubsetRandomSampler(idx.tolist())
+            loader = DataLoader(data, batch_size=args.batch_size, sampler=sampler, drop_last=False)
+        else:
+            loader = DataLoader(data, batch_size=args.batch_size, shuffle=True, drop_last=False)
+        pending = []
+        for batch in loader:
+            optimizer.zero_grad()
+            outputs = model(batch['audio'])
+            loss = criterion(outputs, batch['label'].to(device))
+            loss.backward()
+            parallel.allreduce_grads(flat)
+            optimizer.step()
+            pending.append(loss.detach())
+            if len(pending) >= args.log_every and rank == 0:
+                with open(loss_file, 'a') as f:
+                    for v in torch.stack(pending).tolist():
+                        f.write(str(v) + '\n')
+                pending = []
+        if pending and rank == 0:
+            with open(loss_file, 'a') as f:
+                for v in torch.stack(pending).tolist():
+                    f.write(str(v) + '\n')
+        if not args.no_eval and rank == 0:
+            mod.accuracy(model, valset, os.path.join(args.output_path, 'val_' + key + '.txt'), 4)
+            mod.accuracy(model, data, os.path.join(args.output_path, 'train_' + key + '.txt'), 4)
+        epoch += 1
+        if hasattr(data, 'resample_unknown_class'):
+            data.resample_unknown_class()
+    if rank == 0:
+        print('key  ', key)
+        print('time  ', time.time() - start)
+        print('epochs  ', epoch)
+
+
+if __name__ == '__main__':
+    main()

@@ -186,20 +186,6 @@ struct SpecLoad {    // scipy.signal.spectrogram segments, model_spec_bgru.py:13
   }
 };
 
-struct MfccLoad {    // librosa stft(center=True, pad_mode='reflect'), periodic Hann(640)
-  static constexpr int N = 640, M = 320, NFRAMES = 51;
-  __device__ static __forceinline__ int reflect(int s) {
-    s = s < 0 ? -s : s;
-    return s > kPcmLen - 1 ? 2 * (kPcmLen - 1) - s : s;
-  }
-  __device__ static __forceinline__ void load(const float* x, const DeviceTables& t, int gf, int n,
-                                              double& a, double& b) {
-    const int s = 320 * gf + 2 * n - 320;
-    a = (double)x[reflect(s)] * t.hann640[2 * n];
-    b = (double)x[reflect(s + 1)] * t.hann640[2 * n + 1];
-  }
-};
-
 // Load frames [f0, f0+F) of clip x into buf, windowed; frames past NFRAMES are zero.
 template <class L, int F, int NT>
 __device__ __forceinline__ void load_frames(float2* buf, double2* dcny, const float* x,
@@ -285,70 +271,289 @@ __global__ __launch_bounds__(kSpNT) void spec_kernel(const float* __restrict__ p
   }
 }
 
-// ------------------------------------------------------------------------- K1 MFCC
-constexpr int kMfF = 17, kMfNT = 256;
+// ------------------------------------------------------------------------- register FFT (v2)
+// N = 640 real = 320 complex, factored 320 = 16 (j) x 20 (i): n = j + 16 i, k = k1 + 20 k2.
+//   pass A (lane per (frame, j), 16 lanes / frame): 20-point DFT over i in registers,
+//                                                   then twiddle W320^(j k1)
+//   LDS transpose (row pitch 17 complex: conflict-free ds_read_b64 / ds_write_b64)
+//   pass B (lane per (frame, k1), 20 lanes / frame): 16-point DFT over j in registers
+// A wave processes 3 frames at a time (48 lanes in pass A, 60 in pass B); no workgroup barrier
+// is needed inside the frame loop (each wave owns its LDS slices).
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef float v4f __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(kMfNT) void mfcc_kernel(const float* __restrict__ pcm, float* __restrict__ out,
-                                                     int layout, DeviceTables t) {
-  __shared__ float2 buf[kMfF * 320];
-  __shared__ float db[51 * 128];
-  __shared__ double2 dcny[kMfF];
-  __shared__ float red[kMfNT / 64];
-  const int clip = blockIdx.x;
-  const float* x = pcm + (size_t)clip * kPcmLen;
-  float vmax = -INFINITY;
-  for (int f0 = 0; f0 < 51; f0 += kMfF) {
-    load_frames<MfccLoad, kMfF, kMfNT>(buf, dcny, x, t, f0);
-    fft320<kMfF, kMfNT>(buf, t.tw320);
-    power_spectrum<320, kMfF, kMfNT>(buf, t.post640, dcny, false, false);
-    const float* pb = reinterpret_cast<const float*>(buf);
-    for (int it = threadIdx.x; it < kMfF * 128; it += kMfNT) {
-      const int fr = it / 128, m = it % 128;
-      const int lo = t.mel_lo[m], cnt = t.mel_cnt[m], off = t.mel_off[m];
-      const float* p = pb + fr * 321 + lo;
-      float acc = 0.f;
-      for (int c = 0; c < cnt; ++c) acc = fmaf(t.mel_w[off + c], p[c], acc);
-      // power_to_db(ref=1.0, amin=1e-10): 10*log10(max(amin, S))
-      const float v = acc > 1e-10f ? 10.0f * log10f(acc) : -100.0f;
-      db[(f0 + fr) * 128 + m] = v;
-      vmax = fmaxf(vmax, v);
+__device__ __forceinline__ v2f cm2(v2f a, v2f b) { return v2f{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+__device__ __forceinline__ v2f mi2(v2f a) { return v2f{a.y, -a.x}; }   // -i * a
+
+__device__ constexpr float kW20[4][5][2] = {
+  {{1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}},
+  {{1.f, 0.f}, {9.510565163e-01f, -3.090169944e-01f}, {8.090169944e-01f, -5.877852523e-01f},
+   {5.877852523e-01f, -8.090169944e-01f}, {3.090169944e-01f, -9.510565163e-01f}},
+  {{1.f, 0.f}, {8.090169944e-01f, -5.877852523e-01f}, {3.090169944e-01f, -9.510565163e-01f},
+   {-3.090169944e-01f, -9.510565163e-01f}, {-8.090169944e-01f, -5.877852523e-01f}},
+  {{1.f, 0.f}, {5.877852523e-01f, -8.090169944e-01f}, {-3.090169944e-01f, -9.510565163e-01f},
+   {-9.510565163e-01f, -3.090169944e-01f}, {-8.090169944e-01f, 5.877852523e-01f}}};
+__device__ constexpr float kW16[4][4][2] = {
+  {{1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}},
+  {{1.f, 0.f}, {9.238795325e-01f, -3.826834324e-01f}, {7.071067812e-01f, -7.071067812e-01f},
+   {3.826834324e-01f, -9.238795325e-01f}},
+  {{1.f, 0.f}, {7.071067812e-01f, -7.071067812e-01f}, {0.f, -1.f}, {-7.071067812e-01f, -7.071067812e-01f}},
+  {{1.f, 0.f}, {3.826834324e-01f, -9.238795325e-01f}, {-7.071067812e-01f, -7.071067812e-01f},
+   {-9.238795325e-01f, 3.826834324e-01f}}};
+
+__device__ __forceinline__ void dft4v(v2f& a0, v2f& a1, v2f& a2, v2f& a3) {
+  const v2f s02 = a0 + a2, d02 = a0 - a2, s13 = a1 + a3, d13 = mi2(a1 - a3);
+  a0 = s02 + s13;
+  a2 = s02 - s13;
+  a1 = d02 + d13;
+  a3 = d02 - d13;
+}
+
+__device__ __forceinline__ void dft5v(v2f& a0, v2f& a1, v2f& a2, v2f& a3, v2f& a4) {
+  constexpr float c1 = 0.30901699437494745f, c2 = -0.8090169943749473f;
+  constexpr float s1 = 0.9510565162951535f, s2 = 0.5877852522924732f;
+  const v2f t1 = a1 + a4, t2 = a2 + a3, t3 = a1 - a4, t4 = a2 - a3;
+  const v2f b1 = a0 + c1 * t1 + c2 * t2, b2 = a0 + c2 * t1 + c1 * t2;
+  const v2f q1 = s1 * t3 + s2 * t4, q2 = s2 * t3 - s1 * t4;
+  a0 = a0 + t1 + t2;
+  a1 = b1 + mi2(q1);
+  a4 = b1 - mi2(q1);
+  a2 = b2 + mi2(q2);
+  a3 = b2 - mi2(q2);
+}
+
+// in-place 20-point forward DFT, natural order in and out (i = 4p + q, k = k1 + 5 k2)
+__device__ __forceinline__ void dft20v(v2f (&a)[20]) {
+  v2f b[4][5];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v2f t0 = a[q], t1 = a[4 + q], t2 = a[8 + q], t3 = a[12 + q], t4 = a[16 + q];
+    dft5v(t0, t1, t2, t3, t4);
+    b[q][0] = t0; b[q][1] = t1; b[q][2] = t2; b[q][3] = t3; b[q][4] = t4;
+#pragma unroll
+    for (int k1 = 1; k1 < 5; ++k1)
+      if (q > 0) b[q][k1] = cm2(b[q][k1], v2f{kW20[q][k1][0], kW20[q][k1][1]});
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < 5; ++k1) {
+    v2f u0 = b[0][k1], u1 = b[1][k1], u2 = b[2][k1], u3 = b[3][k1];
+    dft4v(u0, u1, u2, u3);
+    a[k1] = u0; a[k1 + 5] = u1; a[k1 + 10] = u2; a[k1 + 15] = u3;
+  }
+}
+
+// in-place 16-point forward DFT (j = 4p + q, k = k1 + 4 k2)
+__device__ __forceinline__ void dft16v(v2f (&a)[16]) {
+  v2f b[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v2f t0 = a[q], t1 = a[4 + q], t2 = a[8 + q], t3 = a[12 + q];
+    dft4v(t0, t1, t2, t3);
+    b[q][0] = t0; b[q][1] = t1; b[q][2] = t2; b[q][3] = t3;
+#pragma unroll
+    for (int k1 = 1; k1 < 4; ++k1)
+      if (q > 0) b[q][k1] = cm2(b[q][k1], v2f{kW16[q][k1][0], kW16[q][k1][1]});
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    v2f u0 = b[0][k1], u1 = b[1][k1], u2 = b[2][k1], u3 = b[3][k1];
+    dft4v(u0, u1, u2, u3);
+    a[k1] = u0; a[k1 + 4] = u1; a[k1 + 8] = u2; a[k1 + 12] = u3;
+  }
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+  // orders this wave's LDS writes before its later LDS reads (no workgroup barrier needed)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave computes the 320-point complex FFT of 3 frames whose packed inputs z[n] it supplies
+// through `a` (pass-A lanes, frame = lane >> 4, j = lane & 15, a[i] = z[j + 16 i]); on return the
+// natural-order spectra are in xs[f * 320 + k] (f < 3).  tb = this wave's transpose slice.
+__device__ __forceinline__ void fft320x3(v2f (&a)[20], const v2f (&tw)[20], v2f* tb, v2f* xs, int lane) {
+  const int fa = lane >> 4, j = lane & 15;
+  dft20v(a);
+  if (fa < 3) {
+#pragma unroll
+    for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? cm2(a[k1], tw[k1]) : a[0];
+  }
+  wave_lds_fence();
+  const int fb = lane / 20, k1 = lane % 20;
+  v2f b[16];
+  if (fb < 3) {
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) b[jj] = tb[fb * 340 + k1 * 17 + jj];
+  }
+  dft16v(b);
+  if (fb < 3) {
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) xs[fb * 320 + k1 + 20 * k2] = b[k2];
+  }
+  wave_lds_fence();
+}
+
+// ------------------------------------------------------------------------- K1 MFCC (v2)
+// Workgroup = 4 waves, persistent over clips (grid-stride), 2 workgroups per CU: the pass-A
+// twiddles and the Hann window are staged in LDS once per workgroup; the 16-tap mel windows
+// (filters lane and lane+64, [q][128] so a wave's loads coalesce), the untangle twiddles and the
+// DCT rows are read through L1.  Per clip the waves split the 17 chunks of 3 frames; the
+// per-clip top_db max is combined across the waves through LDS.
+constexpr int kMfWaves = 4;   // 2 workgroups (8 waves) per CU: LDS = 80,096 B each
+
+__device__ __forceinline__ void mfcc_load_chunk(const float* __restrict__ x, int c, int lane, v2f (&raw)[20]) {
+  const int fa = lane >> 4, j = lane & 15;
+  const int gf = 3 * c + (fa < 3 ? fa : 0);
+  if (c > 0 && c < 16) {   // wave-uniform: frames 3..47 never touch the reflected padding
+#pragma unroll
+    for (int i = 0; i < 20; ++i) raw[i] = *reinterpret_cast<const v2f*>(x + 320 * gf + 2 * (j + 16 * i) - 320);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 20; ++i) {
+      int s0 = 320 * gf + 2 * (j + 16 * i) - 320, s1 = s0 + 1;
+      s0 = s0 < 0 ? -s0 : (s0 > kPcmLen - 1 ? 2 * (kPcmLen - 1) - s0 : s0);
+      s1 = s1 < 0 ? -s1 : (s1 > kPcmLen - 1 ? 2 * (kPcmLen - 1) - s1 : s1);
+      raw[i] = v2f{x[s0], x[s1]};
+    }
+  }
+}
+
+// 2 workgroups per CU need <= 256 VGPRs (no AGPR spill-over): waves_per_eu(2) and no prefetch
+// of the next chunk (measured: prefetch + 1 wave/SIMD 7.2 ms, prefetch + spills 4.95 ms, no
+// prefetch 4.65 ms per 65,536 clips).
+__global__ __launch_bounds__(64 * kMfWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void mfcc2_kernel(const float* __restrict__ pcm, float* __restrict__ out,
+                                                              int layout, int64_t n_clips, DeviceTables t) {
+  __shared__ v2f tbuf[kMfWaves][3 * 340];
+  __shared__ float pbuf[kMfWaves][3 * 321];
+  __shared__ __attribute__((aligned(16))) float db[51 * 132];   // row pitch 132: conflict-free b128 reads
+  __shared__ v2f s_tw[20 * 16];   // W320^(j k1) at [k1][j]
+  __shared__ float s_hann[640];
+  __shared__ float red[kMfWaves];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 320; i += 64 * kMfWaves)
+    s_tw[i] = *reinterpret_cast<const v2f*>(t.tw320 + ((i >> 4) * (i & 15)));   // [k1][j]
+  for (int i = threadIdx.x; i < 640; i += 64 * kMfWaves) s_hann[i] = t.hann640f[i];
+  __syncthreads();
+  // mel windows / DCT / untangle twiddles stay in global memory (L1/L2-resident, coalesced)
+  const int lo0 = t.mel16_lo[lane], lo1 = t.mel16_lo[lane + 64];
+  const float* w0 = t.mel16_wt + lane;        // [q][128] layout: w0[q * 128]
+  const float* w1 = t.mel16_wt + lane + 64;
+  const v2f* __restrict__ s_post = reinterpret_cast<const v2f*>(t.post640);
+  const int fa = lane >> 4, j = lane & 15;
+  v2f* tb = tbuf[wave];
+  float* pb = pbuf[wave];
+
+  for (int64_t clip = blockIdx.x; clip < n_clips; clip += gridDim.x) {
+    const float* __restrict__ x = pcm + clip * kPcmLen;
+    float vmax = -INFINITY;
+    for (int c = wave; c < 17; c += kMfWaves) {
+      v2f raw[20];
+      mfcc_load_chunk(x, c, lane, raw);
+      const int f0 = 3 * c;
+      v2f a[20];
+#pragma unroll
+      for (int i = 0; i < 20; ++i) {
+        const v2f w = *reinterpret_cast<const v2f*>(s_hann + 2 * (j + 16 * i));
+        a[i] = raw[i] * w;
+      }
+      // pass A: 20-point DFTs + twiddle, transpose through LDS
+      dft20v(a);
+      if (fa < 3) {
+#pragma unroll
+        for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? cm2(a[k1], s_tw[k1 * 16 + j]) : a[0];
+      }
+      wave_lds_fence();
+      // pass B: 16-point DFTs -> natural-order spectra (overwrite the transpose slice)
+      const int fb = lane / 20, k1 = lane % 20;
+      v2f b[16];
+      if (fb < 3) {
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) b[jj] = tb[fb * 340 + k1 * 17 + jj];
+      }
+      dft16v(b);
+      wave_lds_fence();
+      if (fb < 3) {
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) tb[fb * 320 + k1 + 20 * k2] = b[k2];
+      }
+      wave_lds_fence();
+      // untangle the packed real FFT -> |X[k]|^2, k = 0..320
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+          const int k = lane + 64 * m;
+          if (k <= 320) {
+            const v2f A = tb[f * 320 + (k == 320 ? 0 : k)];
+            const v2f Bz = tb[f * 320 + (k == 0 ? 0 : 320 - k)];
+            const v2f Bc = v2f{Bz.x, -Bz.y};
+            const v2f e = 0.5f * (A + Bc), o = mi2(0.5f * (A - Bc));
+            const v2f X = e + cm2(s_post[k], o);
+            pb[f * 321 + k] = X.x * X.x + X.y * X.y;
+          }
+        }
+      }
+      wave_lds_fence();
+      // Slaney mel (two 16-tap filters per lane) -> power_to_db(ref=1, amin=1e-10)
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        const float* p = pb + f * 321;
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          s0 = fmaf(w0[q * 128], p[lo0 + q], s0);
+          s1 = fmaf(w1[q * 128], p[lo1 + q], s1);
+        }
+        const float v0 = s0 > 1e-10f ? 10.0f * log10f(s0) : -100.0f;
+        const float v1 = s1 > 1e-10f ? 10.0f * log10f(s1) : -100.0f;
+        db[(f0 + f) * 132 + lane] = v0;
+        db[(f0 + f) * 132 + lane + 64] = v1;
+        vmax = fmaxf(vmax, fmaxf(v0, v1));
+      }
+      wave_lds_fence();
+    }
+    vmax = wave_max(vmax);
+    if (lane == 0) red[wave] = vmax;
+    __syncthreads();
+    float mx = red[0];
+#pragma unroll
+    for (int w = 1; w < kMfWaves; ++w) mx = fmaxf(mx, red[w]);
+    const float floor_db = mx - 80.0f;
+    float* C = reinterpret_cast<float*>(&tbuf[0][0]);   // 13 x 51 coefficients
+    float* D = C + 13 * 51;                             // deltas
+    for (int it = threadIdx.x; it < 13 * 51; it += 64 * kMfWaves) {
+      const int cc = it / 51, f = it % 51;
+      const float* d = db + f * 132;
+      const float* w = t.dct + cc * 128;
+      v4f acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+      for (int k = 0; k < 128; k += 4) {
+        const v4f dv = *reinterpret_cast<const v4f*>(d + k);
+        const v4f wv = *reinterpret_cast<const v4f*>(w + k);
+        acc.x = fmaf(wv.x, fmaxf(dv.x, floor_db), acc.x);
+        acc.y = fmaf(wv.y, fmaxf(dv.y, floor_db), acc.y);
+        acc.z = fmaf(wv.z, fmaxf(dv.z, floor_db), acc.z);
+        acc.w = fmaf(wv.w, fmaxf(dv.w, floor_db), acc.w);
+      }
+      C[it] = (acc.x + acc.y) + (acc.z + acc.w);
     }
     __syncthreads();
-  }
-  // per-clip top_db = 80 clamp (the reduction between mel and DCT)
-  vmax = wave_max(vmax);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = vmax;
-  __syncthreads();
-  float m = red[0];
-#pragma unroll
-  for (int w = 1; w < kMfNT / 64; ++w) m = fmaxf(m, red[w]);
-  const float floor_db = m - 80.0f;
-  // DCT-II ortho [:13] per frame -> C[13][51] in LDS (reuse buf)
-  float* C = reinterpret_cast<float*>(buf);
-  float* D = C + 13 * 51;
-  for (int it = threadIdx.x; it < 13 * 51; it += kMfNT) {
-    const int c = it / 51, f = it % 51;
-    const float* d = db + f * 128;
-    const float* w = t.dct + c * 128;
-    float acc = 0.f;
-    for (int k = 0; k < 128; ++k) acc = fmaf(w[k], fmaxf(d[k], floor_db), acc);
-    C[it] = acc;
-  }
-  __syncthreads();
-  // np.gradient(axis=1), edge_order=1: one-sided at the ends, central inside
-  auto grad = [](const float* r, int f) {
-    return f == 0 ? r[1] - r[0] : (f == 50 ? r[50] - r[49] : (r[f + 1] - r[f - 1]) * 0.5f);
-  };
-  for (int it = threadIdx.x; it < 13 * 51; it += kMfNT) D[it] = grad(C + (it / 51) * 51, it % 51);
-  __syncthreads();
-  float* o = out + (size_t)clip * 39 * 51;
-  for (int it = threadIdx.x; it < 39 * 51; it += kMfNT) {
-    const int row = it / 51, f = it % 51;
-    float v;
-    if (row < 13) v = C[row * 51 + f];
-    else if (row < 26) v = D[(row - 13) * 51 + f];
-    else v = grad(D + (row - 26) * 51, f);
-    if (layout == 0) o[row * 51 + f] = v; else o[f * 39 + row] = v;
+    auto grad = [](const float* r, int f) {
+      return f == 0 ? r[1] - r[0] : (f == 50 ? r[50] - r[49] : (r[f + 1] - r[f - 1]) * 0.5f);
+    };
+    for (int it = threadIdx.x; it < 13 * 51; it += 64 * kMfWaves) D[it] = grad(C + (it / 51) * 51, it % 51);
+    __syncthreads();
+    float* o = out + clip * 39 * 51;
+    for (int it = threadIdx.x; it < 39 * 51; it += 64 * kMfWaves) {
+      const int row = it / 51, f = it % 51;
+      float v;
+      if (row < 13) v = C[row * 51 + f];
+      else if (row < 26) v = D[(row - 13) * 51 + f];
+      else v = grad(D + (row - 26) * 51, f);
+      if (layout == 0) o[row * 51 + f] = v; else o[f * 39 + row] = v;
+    }
+    __syncthreads();   // tbuf / db are reused by the next clip
   }
 }
 
@@ -430,8 +635,9 @@ int srk_mfcc_fwd(const float* pcm, int64_t n_clips, float* out, int layout, void
   const DeviceTables* t = nullptr;
   if (int rc = srk::get_tables(&t)) return rc;
   srk::ProfScope prof("mfcc", srk::as_stream(stream), 71956.0 * (double)n_clips);     // 64000 + 7956 B/clip
-  hipLaunchKernelGGL(srk::mfcc_kernel, dim3((unsigned)n_clips), dim3(srk::kMfNT), 0, srk::as_stream(stream),
-                     pcm, out, layout, *t);
+  const int64_t grid = std::min<int64_t>(n_clips, 256 * 4);   // persistent over clips
+  hipLaunchKernelGGL(srk::mfcc2_kernel, dim3((unsigned)grid), dim3(64 * srk::kMfWaves), 0,
+                     srk::as_stream(stream), pcm, out, layout, n_clips, *t);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END

@@ -57,6 +57,25 @@ std::vector<float2> twiddles(int m, int count) {
   return t;
 }
 
+// Dense [nf][nbins] -> fixed-width windows: lo[m] (clamped so lo + width <= nbins) and
+// w[m][q] = dense[m][lo + q] (zero outside the filter).  Every filter here spans <= 15 bins.
+int to_windows(const std::vector<double>& w, int nf, int nbins, int width, std::vector<int>& lo,
+               std::vector<float>& vals) {
+  lo.assign(nf, 0);
+  vals.assign((size_t)nf * width, 0.f);
+  for (int m = 0; m < nf; ++m) {
+    int first = -1, last = -1;
+    for (int k = 0; k < nbins; ++k)
+      if (w[(size_t)m * nbins + k] != 0.0) { if (first < 0) first = k; last = k; }
+    if (first < 0) continue;
+    SRK_REQUIRE(last - first + 1 <= width, SRK_ERR_INTERNAL, "filter %d wider than %d bins", m, width);
+    const int l = std::min(first, nbins - width);
+    lo[m] = l;
+    for (int k = first; k <= last; ++k) vals[(size_t)m * width + (k - l)] = (float)w[(size_t)m * nbins + k];
+  }
+  return SRK_OK;
+}
+
 // Dense [nf][nbins] matrix -> CSR by filter (each filter is one contiguous run of bins).
 void to_csr(const std::vector<double>& w, int nf, int nbins, std::vector<int>& lo,
             std::vector<int>& cnt, std::vector<int>& off, std::vector<float>& vals) {
@@ -142,11 +161,30 @@ int build_tables(DeviceTables& t) {
   for (double v : tuk) s2 += v * v;
   t.spec_scale = 1.0 / (16000.0 * s2);
   if ((rc = upload(&t.hamming400, ham))) return rc;
+  {
+    std::vector<float> hf(hann.begin(), hann.end()), tf(tuk.begin(), tuk.end()), mf(ham.begin(), ham.end());
+    if ((rc = upload(&t.hann640f, hf)) || (rc = upload(&t.tukey640f, tf)) || (rc = upload(&t.hamming400f, mf)))
+      return rc;
+  }
   if ((rc = upload(&t.hann640, hann))) return rc;
   if ((rc = upload(&t.tukey640, tuk))) return rc;
 
   std::vector<int> lo, cnt, off;
   std::vector<float> vals;
+  {
+    std::vector<int> wl;
+    std::vector<float> wv;
+    if ((rc = to_windows(fbank_matrix(), 120, 257, 16, wl, wv)) || (rc = upload(&t.fb16_lo, wl)) ||
+        (rc = upload(&t.fb16_w, wv)))
+      return rc;
+    if ((rc = to_windows(slaney_mel(), 128, 321, 16, wl, wv)) || (rc = upload(&t.mel16_lo, wl)) ||
+        (rc = upload(&t.mel16_w, wv)))
+      return rc;
+    std::vector<float> wt(16 * 128);
+    for (int m = 0; m < 128; ++m)
+      for (int q = 0; q < 16; ++q) wt[q * 128 + m] = wv[m * 16 + q];
+    if ((rc = upload(&t.mel16_wt, wt))) return rc;
+  }
   to_csr(fbank_matrix(), 120, 257, lo, cnt, off, vals);
   if ((rc = upload(&t.fb_lo, lo)) || (rc = upload(&t.fb_cnt, cnt)) || (rc = upload(&t.fb_off, off)) ||
       (rc = upload(&t.fb_w, vals)))

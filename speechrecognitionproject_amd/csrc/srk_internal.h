@@ -53,10 +53,17 @@ struct DeviceTables {
   double* hamming400 = nullptr;
   double* tukey640 = nullptr;
   double* hann640 = nullptr;
+  float* hann640f = nullptr;   // fp32 copies for the register-FFT kernels
+  float* tukey640f = nullptr;
+  float* hamming400f = nullptr;
   // sparse filterbanks (CSR by filter): lo bin, count, offset into weights
   int* fb_lo = nullptr; int* fb_cnt = nullptr; int* fb_off = nullptr; float* fb_w = nullptr;   // 120 filters
   int* mel_lo = nullptr; int* mel_cnt = nullptr; int* mel_off = nullptr; float* mel_w = nullptr; // 128 filters
   float* dct = nullptr;        // [13][128] orthonormal DCT-II
+  // the same filterbanks as fixed 16-tap windows (zero-padded, start clamped so lo+16 <= bins)
+  int* mel16_lo = nullptr; float* mel16_w = nullptr;   // [128], [128][16]
+  float* mel16_wt = nullptr;                           // [16][128] (lane-coalesced)
+  int* fb16_lo = nullptr; float* fb16_w = nullptr;     // [120], [120][16]
   double spec_scale = 0.0;     // 1 / (fs * sum(w^2)) for the Tukey window
 };
 

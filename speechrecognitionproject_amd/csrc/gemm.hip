@@ -12,6 +12,8 @@
 // order (deterministic) and applies alpha / beta / bias.  Optionally the kernel also produces
 // rowsum[m] = sum_k op(A)[m, k] from the A tiles it already stages (the bias gradient of a
 // dW = dY^T X GEMM, fused: no separate pass over dY).
+#include <algorithm>
+#include <cstdlib>
 #include <mutex>
 
 #include "gemm.h"
@@ -21,109 +23,144 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// p[r][c0..c0+3] (contiguous along c), zero outside rows [0, r_end) and columns [0, c_end)
-__device__ __forceinline__ float4 load4(const float* __restrict__ p, int64_t ld, int64_t r, int64_t r_end, int64_t c0,
-                                        int64_t c_end, bool vec) {
-  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (r < r_end) {
-    const float* q = p + r * ld + c0;
-    if (vec && c0 + 3 < c_end) {
-      v = *reinterpret_cast<const float4*>(q);
-    } else {
-      if (c0 + 0 < c_end) v.x = q[0];
-      if (c0 + 1 < c_end) v.y = q[1];
-      if (c0 + 2 < c_end) v.z = q[2];
-      if (c0 + 3 < c_end) v.w = q[3];
-    }
-  }
-  return v;
-}
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4f ld4(const float* p) { return *reinterpret_cast<const v4f*>(p); }
+__device__ __forceinline__ void st4(float* p, v4f v) { *reinterpret_cast<v4f*>(p) = v; }
 
 struct KernelArgs {
   GemmDesc d;
-  int tiles_n;
-  int vec_a, vec_b;
-  int64_t kchunk;        // K range per split
+  int tiles_m, tiles_n;
+  int tiles;             // tiles_m * tiles_n (one split's output grid)
+  int nblk;              // tiles * splits = gridDim.x
+  int group_m;           // tile rows per swizzle group (L2 reuse of B panels)
+  int remap;             // XCD-aware block remap on/off (A/B measurement only)
+  int64_t kchunk;        // K range per split (a multiple of BK)
   float* partial;        // [splits][M][N] when split
   float* rs_partial;     // [splits][M] when split and rowsum requested
 };
 
-template <bool TA, bool TB, int BM, int BN, int BK>
+// LDS images (pitches in floats, all multiples of 4 so every 16-B store is aligned):
+//   operand stored k-contiguous in HBM (A when !TA, B when TB): [row][BK + 4]   (float4 along k)
+//   operand stored row-contiguous (A when TA, B when !TB):      [BK][rows + 8]   (float4 along rows)
+// MFMA 32x32x2 operand = element (row = lane & 31, k = lane >> 5).  The k order is permuted per
+// 8-deep block: sub-step s (0..3) of block kb gives lanes of half h the real k = 8 kb + 4 h + s, the
+// same for A and B (any fixed permutation of k is a valid summation order), so a k-contiguous image
+// feeds 4 MFMAs from ONE ds_read_b128 per operand, and a row-contiguous image from 4 ds_read_b32 at
+// a pitch (rows + 8) that puts the two lane halves on disjoint banks.
+template <bool KC, int ROWS, int BK>
+struct Img {
+  static constexpr int P = KC ? BK + 4 : ROWS + 8;
+  static constexpr int FLOATS = KC ? ROWS * P : BK * P;
+  __device__ static __forceinline__ v4f frag(const float* s, int row, int kb, int h) {
+    if (KC) return ld4(s + row * P + kb * 8 + 4 * h);
+    const float* q = s + (kb * 8 + 4 * h) * P + row;
+    return v4f{q[0], q[P], q[2 * P], q[3 * P]};
+  }
+};
+
+template <bool TA, bool TB, int BM, int BN, int BK, bool VEC>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(KernelArgs ka) {
   constexpr int NT = 256;
-  constexpr int LA = TA ? BM : BM + 1;   // float4 stores (TA) stay aligned; scalar stores get +1
-  constexpr int LB = TB ? BN + 1 : BN;
+  constexpr bool AKC = !TA, BKC = TB;         // k-contiguous in HBM?
+  using IA = Img<AKC, BM, BK>;
+  using IB = Img<BKC, BN, BK>;
   constexpr int VA = BM * BK / 4 / NT, VB = BN * BK / 4 / NT;
   constexpr int TM = BM / 64, TN = BN / 64;   // 32x32 tiles per wave per dim
-  static_assert(VA >= 1 && VB >= 1 && TM >= 1 && TN >= 1, "bad tile");
-  __shared__ float As[2][BK][LA];
-  __shared__ float Bs[2][BK][LB];
+  static_assert(VA >= 1 && VB >= 1 && TM >= 1 && TN >= 1 && BK % 8 == 0, "bad tile");
+  __shared__ __attribute__((aligned(16))) float smem[2 * (IA::FLOATS + IB::FLOATS)];
   const GemmDesc& d = ka.d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tm = blockIdx.x / ka.tiles_n, tn = blockIdx.x % ka.tiles_n;
-  const int split = blockIdx.y;
+
+  // Block -> (split, tile) map.  Workgroups are dealt round-robin over the 8 XCDs (block b and
+  // b + 8 share an XCD; speed only, never correctness), so consecutive LOGICAL tiles are given to
+  // blocks of ONE XCD: the tiles an XCD runs concurrently then share A and B panels in its L2
+  // instead of every XCD fetching every panel.  Within a split, tiles are walked in groups of
+  // group_m tile rows (column-major inside a group) so resident tiles form a compact 2-D patch.
+  int lin = blockIdx.x;
+  if (ka.remap) {
+    const int b = blockIdx.x, xcd = b & 7, q = ka.nblk >> 3, r = ka.nblk & 7;
+    lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  }
+  const int split = lin / ka.tiles;
+  const int t = lin - split * ka.tiles;
+  const int gsz_full = ka.group_m * ka.tiles_n;
+  const int grp = t / gsz_full, first_m = grp * ka.group_m;
+  const int gm = ka.tiles_m - first_m < ka.group_m ? ka.tiles_m - first_m : ka.group_m;
+  const int tin = t - grp * gsz_full;
+  const int tm = first_m + tin % gm, tn = tin / gm;
+
   const int64_t z = blockIdx.z;
   const float* __restrict__ A = d.A + z * d.sA;
   const float* __restrict__ B = d.B + z * d.sB;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int64_t kb = split * ka.kchunk;
-  const int64_t ke = (kb + ka.kchunk < d.K) ? kb + ka.kchunk : d.K;
+  const int64_t kb0 = split * ka.kchunk;
+  const int64_t ke = (kb0 + ka.kchunk < d.K) ? kb0 + ka.kchunk : d.K;
   const int wm0 = (wave >> 1) * (BM / 2), wn0 = (wave & 1) * (BN / 2);
   const bool do_rs = d.rowsum != nullptr && tn == 0;
 
-  float4 ra[VA], rb[VB];
+  // Global -> register staging.  Every index is CLAMPED into range instead of predicated, so no
+  // load is exec-masked and nothing waits on a load before this tile's MFMAs: rows >= M (A) or
+  // >= N (B) only feed output rows / columns that are never stored, and k >= ke (the k tail of the
+  // last tile of a split) is zeroed in the A image at LDS-store time (after the MFMAs), which
+  // makes those products exactly 0 (clamped B values are copies of finite inputs).
+  v4f ra[VA], rb[VB];
+  // KC: 4 consecutive k of row r (stored [row][ld]);  !KC: rows r..r+3 at k (stored [k][ld])
+  auto ld_op = [&](const float* __restrict__ P, int64_t ld, bool kc, int64_t rows, int64_t r, int64_t k) -> v4f {
+    if (kc) {
+      const float* q = P + (r < rows ? r : rows - 1) * ld;
+      if (VEC) return ld4(q + (k < ke - 3 ? k : ke - 4));   // VEC: ke % 4 == 0 (see gemm_f32)
+      v4f v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = q[k + e < ke ? k + e : ke - 1];
+      return v;
+    }
+    const float* q = P + (k < ke ? k : ke - 1) * ld;
+    if (VEC) return ld4(q + (r < rows ? r : rows - 4));     // VEC: rows % 4 == 0
+    v4f v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = q[r + e < rows ? r + e : rows - 1];
+    return v;
+  };
   auto load_tile = [&](int64_t k0) {
 #pragma unroll
     for (int i = 0; i < VA; ++i) {
       const int vi = tid + i * NT;
-      if (!TA) {   // A [M][K]: vectors along k
-        const int row = vi / (BK / 4), kq = (vi % (BK / 4)) * 4;
-        ra[i] = load4(A, d.lda, m0 + row, d.M, k0 + kq, ke, ka.vec_a);
-      } else {     // A stored [K][M]: vectors along m
-        const int kr = vi / (BM / 4), mq = (vi % (BM / 4)) * 4;
-        ra[i] = load4(A, d.lda, k0 + kr, ke, m0 + mq, d.M, ka.vec_a);
-      }
+      if (AKC) ra[i] = ld_op(A, d.lda, true, d.M, m0 + vi / (BK / 4), k0 + (vi % (BK / 4)) * 4);
+      else     ra[i] = ld_op(A, d.lda, false, d.M, m0 + (vi % (BM / 4)) * 4, k0 + vi / (BM / 4));
     }
 #pragma unroll
     for (int i = 0; i < VB; ++i) {
       const int vi = tid + i * NT;
-      if (!TB) {   // B [K][N]: vectors along n
-        const int kr = vi / (BN / 4), nq = (vi % (BN / 4)) * 4;
-        rb[i] = load4(B, d.ldb, k0 + kr, ke, n0 + nq, d.N, ka.vec_b);
-      } else {     // B stored [N][K]: vectors along k
-        const int row = vi / (BK / 4), kq = (vi % (BK / 4)) * 4;
-        rb[i] = load4(B, d.ldb, n0 + row, d.N, k0 + kq, ke, ka.vec_b);
-      }
+      if (BKC) rb[i] = ld_op(B, d.ldb, true, d.N, n0 + vi / (BK / 4), k0 + (vi % (BK / 4)) * 4);
+      else     rb[i] = ld_op(B, d.ldb, false, d.N, n0 + (vi % (BN / 4)) * 4, k0 + vi / (BN / 4));
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, int64_t k0) {
+    float* As = smem + buf * (IA::FLOATS + IB::FLOATS);
+    float* Bs = As + IA::FLOATS;
+    const bool tail = k0 + BK > ke;
 #pragma unroll
     for (int i = 0; i < VA; ++i) {
       const int vi = tid + i * NT;
-      if (!TA) {
-        const int row = vi / (BK / 4), kq = (vi % (BK / 4)) * 4;
-        As[buf][kq + 0][row] = ra[i].x;
-        As[buf][kq + 1][row] = ra[i].y;
-        As[buf][kq + 2][row] = ra[i].z;
-        As[buf][kq + 3][row] = ra[i].w;
+      v4f v = ra[i];
+      if (AKC) {
+        const int kq = (vi % (BK / 4)) * 4;
+        if (tail) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = k0 + kq + e < ke ? v[e] : 0.f;
+        }
+        st4(As + (vi / (BK / 4)) * IA::P + kq, v);
       } else {
-        const int kr = vi / (BM / 4), mq = (vi % (BM / 4)) * 4;
-        *reinterpret_cast<float4*>(&As[buf][kr][mq]) = ra[i];
+        const int kr = vi / (BM / 4);
+        if (tail && k0 + kr >= ke) v = v4f{0.f, 0.f, 0.f, 0.f};
+        st4(As + kr * IA::P + (vi % (BM / 4)) * 4, v);
       }
     }
 #pragma unroll
     for (int i = 0; i < VB; ++i) {
       const int vi = tid + i * NT;
-      if (!TB) {
-        const int kr = vi / (BN / 4), nq = (vi % (BN / 4)) * 4;
-        *reinterpret_cast<float4*>(&Bs[buf][kr][nq]) = rb[i];
-      } else {
-        const int row = vi / (BK / 4), kq = (vi % (BK / 4)) * 4;
-        Bs[buf][kq + 0][row] = rb[i].x;
-        Bs[buf][kq + 1][row] = rb[i].y;
-        Bs[buf][kq + 2][row] = rb[i].z;
-        Bs[buf][kq + 3][row] = rb[i].w;
-      }
+      if (BKC) st4(Bs + (vi / (BK / 4)) * IB::P + (vi % (BK / 4)) * 4, rb[i]);
+      else     st4(Bs + (vi / (BN / 4)) * IB::P + (vi % (BN / 4)) * 4, rb[i]);
     }
   };
 
@@ -139,35 +176,48 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(KernelArgs ka) {
   constexpr int RSP = NT / BM;
   float rs = 0.f;
 
-  const int64_t nk = ke > kb ? (ke - kb + BK - 1) / BK : 0;
-  const int lk = lane >> 5, lc = lane & 31;
+  const int64_t nk = ke > kb0 ? (ke - kb0 + BK - 1) / BK : 0;
+  const int lh = lane >> 5, lc = lane & 31;
   if (nk > 0) {
-    load_tile(kb);
-    store_tile(0);
+    load_tile(kb0);
+    store_tile(0, kb0);
   }
   __syncthreads();
   for (int64_t kt = 0; kt < nk; ++kt) {
     const int cur = (int)(kt & 1);
-    if (kt + 1 < nk) load_tile(kb + (kt + 1) * BK);
+    if (kt + 1 < nk) load_tile(kb0 + (kt + 1) * BK);
+    const float* As = smem + cur * (IA::FLOATS + IB::FLOATS);
+    const float* Bs = As + IA::FLOATS;
+    v4f fa[2][TM], fb[2][TN];
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      float a[TM], b[TN];
+    for (int i = 0; i < TM; ++i) fa[0][i] = IA::frag(As, wm0 + i * 32 + lc, 0, lh);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = As[cur][kk + lk][wm0 + i * 32 + lc];
+    for (int j = 0; j < TN; ++j) fb[0][j] = IB::frag(Bs, wn0 + j * 32 + lc, 0, lh);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = Bs[cur][kk + lk][wn0 + j * 32 + lc];
+    for (int kb = 0; kb < BK / 8; ++kb) {
+      const int c = kb & 1;
+      if (kb + 1 < BK / 8) {   // fragments of the next 8-deep block ahead of this block's MFMAs
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i) fa[c ^ 1][i] = IA::frag(As, wm0 + i * 32 + lc, kb + 1, lh);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) fb[c ^ 1][j] = IB::frag(Bs, wn0 + j * 32 + lc, kb + 1, lh);
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[c][i][s], fb[c][j][s], acc[i][j], 0, 0, 0);
     }
     if (do_rs) {
 #pragma unroll
-      for (int k = tid / BM; k < BK; k += RSP) rs += As[cur][k][tid % BM];
+      for (int k = tid / BM; k < BK; k += RSP)
+        rs += AKC ? As[(tid % BM) * IA::P + k] : As[k * IA::P + tid % BM];
     }
     asm volatile("" ::: "memory");      // keep the stage-k+1 LDS store (and its vmcnt wait)
-      __builtin_amdgcn_sched_barrier(0);   // after this stage's MFMAs
-    if (kt + 1 < nk) store_tile(cur ^ 1);
+    __builtin_amdgcn_sched_barrier(0);   // after this stage's MFMAs
+    if (kt + 1 < nk) store_tile(cur ^ 1, kb0 + (kt + 1) * BK);
     __syncthreads();
   }
 
@@ -181,7 +231,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(KernelArgs ka) {
       if (col >= d.N) continue;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        const int64_t row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         if (row >= d.M) continue;
         if (split_mode) {
           ka.partial[((int64_t)split * d.M + row) * d.N + col] = acc[i][j][r];
@@ -198,7 +248,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(KernelArgs ka) {
     }
   }
   if (do_rs) {
-    float* red = &As[0][0][0];
+    float* red = smem;
     __syncthreads();
     red[tid] = rs;
     __syncthreads();
@@ -288,24 +338,50 @@ int get_scratch(size_t floats, float** out) {
   return SRK_OK;
 }
 
+// Resident workgroups per CU for the 256-thread, 2 x (BK x BM + BK x BN) fp32 LDS tile kernels.
+constexpr int kCUs = 256;
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
 template <bool TA, bool TB, int BM, int BN, int BK>
-int launch(const GemmDesc& d, hipStream_t s, bool vec_a, bool vec_b) {
+int launch(const GemmDesc& d, hipStream_t s, bool vec) {
   const int64_t tm = (d.M + BM - 1) / BM, tn = (d.N + BN - 1) / BN;
-  SRK_REQUIRE(tm * tn <= INT32_MAX && d.batch <= 65535, SRK_ERR_INVALID, "gemm: grid too large");
+  SRK_REQUIRE(tm * tn <= (INT32_MAX >> 5) && d.batch <= 65535, SRK_ERR_INVALID, "gemm: grid too large");
+  static const int remap = env_int("SRK_GEMM_REMAP", 1);
+  constexpr int lds = 2 * 4 * (Img<!TA, BM, BK>::FLOATS + Img<TB, BN, BK>::FLOATS);
+  constexpr int per_cu = (160 * 1024) / lds < 8 ? (160 * 1024) / lds : 8;
+  const int64_t slots = (int64_t)kCUs * per_cu;
   KernelArgs ka{};
   ka.d = d;
+  ka.tiles_m = (int)tm;
   ka.tiles_n = (int)tn;
-  ka.vec_a = vec_a;
-  ka.vec_b = vec_b;
-  // split K when the output grid cannot fill the chip (256 CUs) and K is long
+  ka.tiles = (int)(tm * tn);
+  ka.group_m = 8;
+  ka.remap = remap;
+  // Split K when the output grid leaves resident slots idle and K is long: pick the split count
+  // (<= 16, >= 4 k-tiles per split) whose last round of workgroups is fullest, preferring fewer splits
+  // (each split adds an M x N fp32 partial slab write + read).
   int splits = 1;
   const int64_t tiles = tm * tn * d.batch;
-  if (d.batch == 1 && tiles < 256 && d.K >= 16 * BK) {
-    splits = (int)std::min<int64_t>((512 + tiles - 1) / tiles, d.K / (4 * BK));
-    splits = std::max(1, std::min(splits, 16));
+  if (d.batch == 1 && d.K >= 16 * BK) {
+    auto eff = [&](int64_t sp) {
+      const int64_t w = tiles * sp, rounds = (w + slots - 1) / slots;
+      return (double)w / (double)(rounds * slots);
+    };
+    double best = eff(1);
+    const int64_t smax = std::min<int64_t>(16, d.K / (4 * BK));
+    for (int64_t sp = 2; sp <= smax; ++sp) {
+      const double e = eff(sp);
+      // a split must buy >= 10 % more filled slots to pay for its slab traffic
+      if (e > best * 1.10 + 1e-9 && tiles * sp <= 4 * slots) { best = e; splits = (int)sp; }
+    }
   }
   ka.kchunk = splits > 1 ? ((d.K + splits - 1) / splits + BK - 1) / BK * BK : std::max<int64_t>(d.K, 1);
   if (splits > 1) splits = (int)((d.K + ka.kchunk - 1) / ka.kchunk);
+  ka.nblk = ka.tiles * splits;
   if (splits > 1) {
     float* scratch = nullptr;
     const size_t need = (size_t)splits * d.M * d.N + (d.rowsum ? (size_t)splits * d.M : 0);
@@ -314,8 +390,12 @@ int launch(const GemmDesc& d, hipStream_t s, bool vec_a, bool vec_b) {
     ka.rs_partial = d.rowsum ? scratch + (size_t)splits * d.M * d.N : nullptr;
   }
   ProfScope prof("gemm_f32", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
-  hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK>), dim3((unsigned)(tm * tn), (unsigned)splits,
-                     (unsigned)d.batch), dim3(256), 0, s, ka);
+  if (vec)
+    hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK, true>), dim3((unsigned)ka.nblk, 1, (unsigned)d.batch),
+                       dim3(256), 0, s, ka);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK, false>), dim3((unsigned)ka.nblk, 1, (unsigned)d.batch),
+                       dim3(256), 0, s, ka);
   SRK_CHECK_HIP(hipGetLastError());
   if (splits > 1) {
     const int64_t n = d.M * d.N;
@@ -330,10 +410,10 @@ int launch(const GemmDesc& d, hipStream_t s, bool vec_a, bool vec_b) {
 }
 
 template <bool TA, bool TB>
-int dispatch_tile(const GemmDesc& d, hipStream_t s, bool va, bool vb) {
+int dispatch_tile(const GemmDesc& d, hipStream_t s, bool vec) {
   const int64_t big_tiles = ((d.M + 127) / 128) * ((d.N + 127) / 128) * d.batch;
-  if (big_tiles >= 64 || d.K >= 2048) return launch<TA, TB, 128, 128, 32>(d, s, va, vb);
-  return launch<TA, TB, 64, 64, 32>(d, s, va, vb);
+  if (d.M > 64 && d.N > 64 && (big_tiles >= 64 || d.K >= 2048)) return launch<TA, TB, 128, 128, 32>(d, s, vec);
+  return launch<TA, TB, 64, 64, 32>(d, s, vec);
 }
 
 }  // namespace
@@ -344,12 +424,16 @@ int gemm_f32(const GemmDesc& d, hipStream_t s) {
   SRK_REQUIRE(d.C && (d.K == 0 || (d.A && d.B)), SRK_ERR_INVALID, "gemm: null operand");
   SRK_REQUIRE(d.bias_mode == 0 || d.bias, SRK_ERR_INVALID, "gemm: bias_mode without bias");
   SRK_REQUIRE(!d.rowsum || d.batch == 1, SRK_ERR_INVALID, "gemm: rowsum needs batch == 1");
-  const bool va = (d.lda % 4 == 0) && ((uintptr_t)d.A % 16 == 0) && (d.sA % 4 == 0);
-  const bool vb = (d.ldb % 4 == 0) && ((uintptr_t)d.B % 16 == 0) && (d.sB % 4 == 0);
-  if (!d.ta && !d.tb) return dispatch_tile<false, false>(d, s, va, vb);
-  if (!d.ta && d.tb) return dispatch_tile<false, true>(d, s, va, vb);
-  if (d.ta && !d.tb) return dispatch_tile<true, false>(d, s, va, vb);
-  return dispatch_tile<true, true>(d, s, va, vb);
+  // 16-B loads need 16-B aligned rows, K % 4 == 0 (a clamped k vector stays inside the row) and,
+  // along M / N (A when ta, B when !tb), a row count that is a multiple of 4 (a clamped vector is
+  // wholly in or wholly out of range).  Otherwise the kernel stages with 4-B loads.
+  const bool vec = (d.lda % 4 == 0) && ((uintptr_t)d.A % 16 == 0) && (d.sA % 4 == 0) && (d.ldb % 4 == 0) &&
+                   ((uintptr_t)d.B % 16 == 0) && (d.sB % 4 == 0) && (d.K % 4 == 0) && (!d.ta || d.M % 4 == 0) &&
+                   (d.tb || d.N % 4 == 0);
+  if (!d.ta && !d.tb) return dispatch_tile<false, false>(d, s, vec);
+  if (!d.ta && d.tb) return dispatch_tile<false, true>(d, s, vec);
+  if (d.ta && !d.tb) return dispatch_tile<true, false>(d, s, vec);
+  return dispatch_tile<true, true>(d, s, vec);
 }
 
 int colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, float beta, hipStream_t s) {

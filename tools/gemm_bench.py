@@ -1,0 +1,66 @@
+"""GEMM micro-benchmark: the fp32 GEMM shapes of one model_mfcc_bgru train step (B = 256, T = 51,
+H = 512), timed with srk_prof events and checked against torch fp32 matmul on the same device.
+
+    python tools/gemm_bench.py [--reps 10]      (env SRK_GEMM_REMAP=0 disables the XCD remap)
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from speechrecognitionproject_amd import _lib  # noqa: E402
+
+B, T, H = 256, 51, 512
+BT = B * T
+# name, ta, tb, M, N, K, lda, ldb  (A stored [M][K] or [K][M] when ta; B stored [K][N] or [N][K] when tb)
+SHAPES = [
+    ("gi_l1", 0, 1, BT, 6 * H, 1024, 1024, 1024),
+    ("gi_l0", 0, 1, BT, 6 * H, 39, 39, 39),
+    ("dx_l1", 0, 0, BT, 1024, 6 * H, 6 * H, 1024),
+    ("dWih_l1", 1, 0, 6 * H, 1024, BT, 6 * H, 1024),
+    ("dWih_l0", 1, 0, 6 * H, 39, BT, 6 * H, 39),
+    ("dWhh", 1, 0, 3 * H, H, BT - 1, 3 * H, 2 * H),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    torch.backends.cuda.matmul.allow_tf32 = False
+    dev = torch.device("cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    res = {}
+    g = torch.Generator(device=dev).manual_seed(0)
+    for name, ta, tb, M, N, K, lda, ldb in SHAPES:
+        A = torch.randn((K if ta else M) * lda, device=dev, generator=g)
+        Bm = torch.randn((N if tb else K) * ldb, device=dev, generator=g)
+        C = torch.empty(M * N, device=dev)
+        rs = torch.empty(M, device=dev)
+        args = (ta, tb, M, N, K, 1.0, A.data_ptr(), lda, Bm.data_ptr(), ldb, 0.0, C.data_ptr(), N)
+        fn = lambda: _lib.call("srk_gemm_rowsum_f32", *args, rs.data_ptr(), stream) if ta else \
+            _lib.call("srk_gemm_f32", *args, None, 0, stream)
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        _lib.prof_enable(True)
+        for _ in range(a.reps):
+            fn()
+        c, ms, w = _lib.prof_read("gemm_f32")
+        _lib.prof_enable(False)
+        Am = (A.view(K, lda)[:, :M].t() if ta else A.view(M, lda)[:, :K])
+        Bmm = (Bm.view(N, ldb)[:, :K].t() if tb else Bm.view(K, ldb)[:, :N])
+        ref = Am @ Bmm
+        err = float((C.view(M, N) - ref).abs().max() / ref.abs().max())
+        tf = w / (ms * 1e-3) / 1e12
+        res[name] = {"us": round(ms / c * 1e3, 1), "TF": round(tf, 1), "frac": round(tf / 157.3, 3), "rel_err": err}
+        print(name, json.dumps(res[name]), flush=True)
+    print(json.dumps({"remap": os.environ.get("SRK_GEMM_REMAP", "1"), "shapes": res}))
+
+
+if __name__ == "__main__":
+    main()

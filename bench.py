@@ -169,7 +169,7 @@ def main():
 
     kernels = {}
     if not args.no_prof:
-        for name in ("gru_fwd_step", "gru_bwd_step", "gemm_f32", "mfcc", "adam"):
+        for name in ("gru_fwd_seq", "gru_bwd_seq", "gru_fwd_step", "gru_bwd_step", "gemm_f32", "mfcc", "adam"):
             c, ms, w = _lib.prof_read(name)
             if c:
                 kernels[name] = {"launches": c, "ms_total": round(ms, 3), "work": w}
@@ -179,7 +179,7 @@ def main():
         return
     value = world * B * args.steps / el
     roof = None
-    mm = {k: v for k, v in kernels.items() if k in ("gru_fwd_step", "gru_bwd_step", "gemm_f32")}
+    mm = {k: v for k, v in kernels.items() if k in ("gru_fwd_seq", "gru_bwd_seq", "gru_fwd_step", "gru_bwd_step", "gemm_f32")}
     if mm:
         dom = max(mm, key=lambda k: mm[k]["ms_total"])
         k = mm[dom]

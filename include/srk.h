@@ -44,6 +44,12 @@ int srk_init(int device);              /* build + upload constant tables on `dev
  * srk_prof_enable synchronizes the device and clears previous records.                     */
 int srk_prof_enable(int on);
 int srk_prof_read(const char* name, int64_t* count, double* total_ms, double* total_work);
+/* Runtime options: "gru_persistent" (default 1) = run each GRU layer's recurrence as ONE
+ * persistent launch with W_hh resident in LDS (0 = one launch per time step).              */
+int srk_set_option(const char* name, int64_t value);
+/* Number of bounded spin-waits of the persistent kernels that gave up (synchronizes the
+ * device; must stay 0 — a non-zero value means a co-residency assumption failed).  -1 on error. */
+int64_t srk_spin_timeouts(void);
 
 /* ---------------------------------------------------------------- feature extraction
  * pcm: float32 [n_clips, 16000], int16-valued (NOT scaled to +-1), exactly what

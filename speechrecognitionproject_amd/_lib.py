@@ -29,6 +29,8 @@ _SIGS = {
     "srk_prof_enable": [_I],
     "srk_prof_read": [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
                       ctypes.POINTER(ctypes.c_double)],
+    "srk_set_option": [ctypes.c_char_p, _I64],
+    "srk_spin_timeouts": [],
     "srk_fbank_fwd": [_P, _I64, _P, _P],
     "srk_mfcc_fwd": [_P, _I64, _P, _I, _P],
     "srk_spec_fwd": [_P, _I64, _P, _I, _P],
@@ -53,7 +55,7 @@ _SIGS = {
     "srk_dropout_fwd": [_P, _I64, _F, ctypes.c_uint64, _P, _P, _P],
     "srk_dropout_apply": [_P, _P, _I64, _F, _P, _P],
 }
-_RESTYPE = {"srk_last_error": ctypes.c_char_p, "srk_gru_workspace_floats": ctypes.c_int64,
+_RESTYPE = {"srk_last_error": ctypes.c_char_p, "srk_spin_timeouts": ctypes.c_int64, "srk_gru_workspace_floats": ctypes.c_int64,
             "srk_conv2d_workspace_floats": ctypes.c_int64}
 
 
@@ -102,6 +104,16 @@ def prof_read(name):
     w = ctypes.c_double(0.0)
     call("srk_prof_read", name.encode(), ctypes.byref(n), ctypes.byref(ms), ctypes.byref(w))
     return int(n.value), float(ms.value), float(w.value)
+
+
+def set_option(name, value):
+    """srk_set_option (include/srk.h): e.g. set_option("gru_persistent", 0)."""
+    call("srk_set_option", name.encode(), int(value))
+
+
+def spin_timeouts():
+    """Persistent-kernel spin waits that gave up since load (synchronizes; must stay 0)."""
+    return int(lib().srk_spin_timeouts())
 
 
 def header_symbols():

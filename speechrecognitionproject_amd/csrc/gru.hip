@@ -16,6 +16,7 @@
 //   fwd:  gi [B*T, 6H] | gates [2][T][B][4H] (r, z, n, W_hn h + b_hn)       — kept for backward
 //   bwd:  dgi [B*T, 6H] | dgh [2][B][T][3H] | dgh_edge [2][B][3H] | dhz [2][B][H]
 #include "gemm.h"
+#include "gru_internal.h"
 
 namespace srk {
 namespace {
@@ -299,10 +300,18 @@ using srk::GemmDesc;
 
 extern "C" {
 
+// Both workspaces end with a 64-float-aligned block of kCounterFloats arrival counters (the
+// persistent recurrence kernels' step ordering; see gru_persistent.hip).
+static int64_t fwd_counter_off(int64_t B, int64_t T, int64_t H) {
+  return (B * T * 6 * H + 2 * T * B * 4 * H + 63) / 64 * 64;
+}
+static int64_t bwd_counter_off(int64_t B, int64_t T, int64_t H) {
+  return (B * T * 6 * H + 2 * B * T * 3 * H + 2 * B * 3 * H + 2 * B * H + 63) / 64 * 64;
+}
+
 int64_t srk_gru_workspace_floats(int64_t B, int64_t T, int64_t in, int64_t H, int backward) {
   (void)in;
-  if (!backward) return B * T * 6 * H + 2 * T * B * 4 * H;
-  return B * T * 6 * H + 2 * B * T * 3 * H + 2 * B * 3 * H + 2 * B * H;
+  return (backward ? bwd_counter_off(B, T, H) : fwd_counter_off(B, T, H)) + srk::kCounterFloats + 64;
 }
 
 int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t H, const float* w_ih,
@@ -320,6 +329,13 @@ int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
   g.C = gi; g.ldc = 6 * H;
   g.bias = b_ih; g.bias_mode = 1;
   if (int rc = srk::gemm_f32(g, s)) return rc;
+  if (srk::g_opt_gru_persistent && srk::gru_persistent_supported(B, T, H, false)) {
+    srk::GruPArgs p{};
+    p.B = (int)B; p.T = (int)T; p.H = (int)H;
+    p.gi = gi; p.w_hh = w_hh; p.b_hh = b_hh; p.y = y; p.gates = gates;
+    p.counters = reinterpret_cast<unsigned*>(ws + fwd_counter_off(B, T, H));
+    return srk::gru_persistent_launch(p, false, s);
+  }
   srk::GruArgs a{};
   a.B = (int)B; a.T = (int)T; a.H = (int)H; a.in = (int)in;
   a.y_in = y; a.y = y; a.gi = gi; a.w_hh = w_hh; a.b_hh = b_hh; a.gates = gates;
@@ -354,12 +370,20 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
   a.dy = dy; a.dgi = dgi; a.dgh = dgh; a.dgh_edge = dgh_edge; a.dhz = dhz;
   a.G = (int)((B + srk::kRows - 1) / srk::kRows);
   a.S = (int)(H / srk::kUnits);
+  if (srk::g_opt_gru_persistent && srk::gru_persistent_supported(B, T, H, true)) {
+    srk::GruPArgs p{};
+    p.B = (int)B; p.T = (int)T; p.H = (int)H;
+    p.w_hh = w_hh; p.y_in = y; p.gates = a.gates; p.dy = dy; p.dgi = dgi; p.dgh = dgh; p.dgh_edge = dgh_edge;
+    p.counters = reinterpret_cast<unsigned*>(ws + bwd_counter_off(B, T, H));
+    if (int rc = srk::gru_persistent_launch(p, true, s)) return rc;
+  } else {
   const dim3 grid((unsigned)(2 * a.G * a.S));
   for (int step = 0; step < T; ++step) {
     srk::ProfScope prof("gru_bwd_step", s, step > 0 ? 2.0 * 2.0 * (double)B * 3 * H * H : 0.0);   // 2 dirs x [B,3H]x[3H,H]
     hipLaunchKernelGGL(srk::gru_bwd_step_kernel, grid, dim3(256), 0, s, a, step);
   }
   SRK_CHECK_HIP(hipGetLastError());
+  }
 
   int rc;
   {  // dW_ih_cat[6H, in] = dgi^T [6H, BT] * x [BT, in]; db_ih fused as the row sums of dgi^T

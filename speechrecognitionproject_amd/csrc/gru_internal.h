@@ -1,0 +1,41 @@
+// Internal interface between gru.hip (entry points, per-step kernels) and gru_persistent.hip
+// (one-launch-per-layer recurrence kernels).
+#pragma once
+#include <algorithm>
+
+#include "srk_internal.h"
+
+namespace srk {
+
+// Arrival counters of the persistent kernels: [2 directions][groups <= 4] at a 64-B stride,
+// zeroed by a hipMemsetAsync of exactly this block before every launch.
+constexpr int kCounterFloats = 256;
+
+struct GruPArgs {
+  int B, T, H;
+  int G;                 // 64-row groups in this launch
+  int b_begin, b_end;    // batch rows [b_begin, b_end) of this launch
+  const float* gi;       // fwd: [B*T][6H]
+  const float* w_hh;     // [2][3H][H]
+  const float* b_hh;     // [2][3H]
+  float* y;              // fwd output [B][T][2H] (also the h hand-off buffer)
+  const float* y_in;     // bwd: the forward output
+  float* gates;          // [2][T][B][4H]
+  const float* dy;       // bwd: [B][T][2H]
+  float* dgi;            // bwd: [B*T][6H]
+  float* dgh;            // bwd: [2][B][T][3H] (also the dg hand-off buffer)
+  float* dgh_edge;       // bwd: [2][B][3H]
+  unsigned* counters;    // kCounterFloats words
+};
+
+size_t fwd_lds_bytes(int H);
+size_t bwd_lds_bytes(int H);
+// 1 if the persistent kernels can run this layer (H, co-residency, 32-bit buffer offsets).
+int gru_persistent_supported(int64_t B, int64_t T, int64_t H, bool backward);
+// Enqueue the whole recurrence (all T steps; batch split into co-resident chunks).
+int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s);
+
+// Runtime options (srk_set_option): persistent GRU recurrence on/off (default on).
+extern int g_opt_gru_persistent;
+
+}  // namespace srk

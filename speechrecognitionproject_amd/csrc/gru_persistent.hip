@@ -1,0 +1,381 @@
+// K5, persistent form: ONE launch runs all T steps of a bidirectional GRU layer's recurrence
+// (forward or backward), replacing the T per-step launches of gru.hip for the shapes the
+// reference uses (H = 512; models/model_mfcc_bgru.py:25, model_spec_bgru.py:23,
+// model_resnet_bgru.py:130).  Same arithmetic, same operand order, same outputs as the per-step
+// kernels — only the schedule changes:
+//
+//  * each workgroup owns (direction, 64 batch rows, 16 hidden units) for the whole sequence and
+//    keeps ITS slice of W_hh resident in LDS (fwd: the 3 x 16 gate rows x H, bwd: the 16 unit
+//    columns x 3H) — ~97 KB per workgroup, 3 MB per direction, read from HBM once per layer
+//    instead of once per step;
+//  * the recurrent state crosses workgroups through the layer's own output (fwd: y[b][t][dir]
+//    half, bwd: dgh[dir][b][t]) written write-through (`sc1`, 16-B per lane after an LDS
+//    transpose) and read back with `sc1` loads; one agent-scope arrival counter per (direction,
+//    64-row group) orders the steps (MI355X_MICROARCH.md "Valid forms", table row 1: one lane of
+//    each storing workgroup adds after every storing wave drained; consumers poll with an `sc1`
+//    load; every load of the handed-off bytes is an `sc1` load; one workgroup per CU);
+//  * the register-resident carries (fwd: h_{t-1} of the lane's own cells, bwd: dh*z) never touch
+//    memory.
+//
+// Co-residency: the grid (2 directions x 64-row groups x H/16 slices, <= one workgroup per CU)
+// must be resident at once; the host checks the occupancy query against the CU count and falls
+// back to the per-step kernels otherwise, and splits larger batches into 64*G-row chunk launches.
+// Every spin is bounded: a workgroup that waits ~2 s gives up, bumps g_spin_timeouts (read by
+// srk_spin_timeouts(); the tests assert it stays 0) and carries on, so a fault can never hang the
+// GPU.
+#include "gru_internal.h"
+
+namespace srk {
+
+__device__ unsigned long long g_spin_timeouts = 0;
+
+namespace {
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kRows = 64;     // batch rows per workgroup (4 waves x 16)
+constexpr int kUnits = 16;    // hidden units per workgroup
+constexpr int kSc1 = 16;      // buffer-instruction aux bit: sc1 (write-through / L1-bypass)
+constexpr unsigned kSpinLimit = 1u << 24;   // x s_sleep(2) (~128 clk) ~= 2 s at 2.4 GHz
+
+__device__ __forceinline__ v4f ld4(const float* p) { return *reinterpret_cast<const v4f*>(p); }
+__device__ __forceinline__ void st4(float* p, v4f v) { *reinterpret_cast<v4f*>(p) = v; }
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ v4f ld4_sc1(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  return __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, kSc1));
+}
+__device__ __forceinline__ void st4_sc1(__amdgpu_buffer_rsrc_t r, unsigned byte_off, v4f v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)byte_off, 0, kSc1);
+}
+
+// One lane of the workgroup waits until *cnt >= target (relaxed agent-scope = sc1 load), then
+// the whole workgroup passes a barrier.  Bounded.
+__device__ __forceinline__ void wait_count(unsigned* cnt, unsigned target) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins >= kSpinLimit) {
+        atomicAdd(&g_spin_timeouts, 1ull);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Every storing wave drains its sc1 stores, the workgroup meets, one lane arrives.
+__device__ __forceinline__ void arrive(unsigned* cnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// (direction, group, slice) of this workgroup: the S slices of one (direction, group) pair are
+// dealt to blocks of ONE XCD (blocks b, b+8, ... share an XCD under round-robin dispatch), so the
+// handed-off rows stay in that XCD's L2.  Speed only; the protocol does not depend on it.
+__device__ __forceinline__ void map_block(int G, int S, int& dir, int& group, int& slice) {
+  const int nwg = 2 * G * S;
+  const int b = blockIdx.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  const int pair = wgid / S;
+  slice = wgid % S;
+  dir = pair / G;
+  group = pair % G;
+}
+
+// ------------------------------------------------------------------ forward
+// LDS: W slice [48][H + 4] (gate g, unit jj -> row g*16 + jj), then the h transpose tile [64][20].
+template <int H>
+__global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) {
+  constexpr int WP = H + 4, HTP = kUnits + 4, NKB = H / 16;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Ws = smem;
+  float* hT = smem + 3 * kUnits * WP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
+  int dir, group, slice;
+  map_block(a.G, H / kUnits, dir, group, slice);
+  const int T = a.T, j0 = slice * kUnits, j = j0 + lr;
+  const int b0 = a.b_begin + group * kRows;
+  const int b_last = a.b_end - 1;
+  unsigned* cnt = a.counters + (dir * a.G + group) * 16;
+
+  {  // this slice of W_hh[dir] -> LDS (read once per layer)
+    const float* W = a.w_hh + (size_t)dir * 3 * H * H;
+    for (int v = tid; v < 3 * kUnits * H / 4; v += 256) {
+      const int c = v / (H / 4), kq = (v % (H / 4)) * 4, g = c / kUnits, jj = c % kUnits;
+      st4(Ws + c * WP + kq, ld4(W + (size_t)(g * H + j0 + jj) * H + kq));
+    }
+  }
+  const float bhr = a.b_hh[dir * 3 * H + j], bhz = a.b_hh[dir * 3 * H + H + j], bhn = a.b_hh[dir * 3 * H + 2 * H + j];
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t ry = rsrc(a.y);
+  const int arow = min(b0 + wave * 16 + lr, b_last);   // A-operand row of this lane (clamped)
+  float hreg[4] = {0.f, 0.f, 0.f, 0.f};                 // h_{t-1} of the lane's own 4 cells
+
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? step : T - 1 - step;
+    const int tprev = dir == 0 ? t - 1 : t + 1;
+    float gr[4], gz[4], gn[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {   // input projections of the lane's cells (written by an earlier launch)
+      const int b = min(b0 + wave * 16 + lq * 4 + r, b_last);
+      const float* gi = a.gi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
+      gr[r] = gi[j];
+      gz[r] = gi[H + j];
+      gn[r] = gi[2 * H + j];
+    }
+    f32x4 acc[3];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (step > 0) {
+      wait_count(cnt, (unsigned)(H / kUnits) * step);
+      // h_{t-1}[arow][k], k = 16 kb + 4 lq + s  (k-permuted: one b128 feeds 4 MFMAs)
+      const unsigned base = (unsigned)((((size_t)arow * T + tprev) * 2 * H + dir * H + 4 * lq) * 4);
+      v4f hv[NKB];
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) hv[kb] = ld4_sc1(ry, base + kb * 64);
+      __builtin_amdgcn_sched_barrier(0);   // all loads in flight before the first MFMA (no sinking)
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) {
+        v4f wv[3];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) wv[g] = ld4(Ws + (g * kUnits + lr) * WP + kb * 16 + 4 * lq);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[kb][s], wv[g][s], acc[g], 0, 0, 0);
+      }
+    }
+    // cell epilogue: lane owns rows 16*wave + 4*lq + r, unit j
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = wave * 16 + lq * 4 + r, b = b0 + rl;
+      const float ghn = acc[2][r] + bhn;
+      const float rg = sigmoidf_(gr[r] + (acc[0][r] + bhr));
+      const float zg = sigmoidf_(gz[r] + (acc[1][r] + bhz));
+      const float ng = tanhf(gn[r] + rg * ghn);
+      const float h = (1.0f - zg) * ng + zg * hreg[r];
+      hreg[r] = h;
+      hT[rl * HTP + lr] = h;
+      if (b <= b_last) {
+        float* gs = a.gates + (((size_t)dir * T + t) * a.B + b) * 4 * H;
+        gs[j] = rg;
+        gs[H + j] = zg;
+        gs[2 * H + j] = ng;
+        gs[3 * H + j] = ghn;
+      }
+    }
+    __syncthreads();
+    {  // h_t -> y (write-through): thread = (row tid/4, units 4*(tid%4) .. +3)
+      const int rl = tid >> 2, uq = (tid & 3) * 4, b = b0 + rl;
+      if (b <= b_last)
+        st4_sc1(ry, (unsigned)((((size_t)b * T + t) * 2 * H + dir * H + j0 + uq) * 4), ld4(hT + rl * HTP + uq));
+    }
+    arrive(cnt);
+  }
+}
+
+// ------------------------------------------------------------------ backward
+// dh[b][j] = dy[b][t][dir, j] + sum_c dgh_next[b][c] W_hh[c][j] + (dh z)_next[b][j]
+// LDS: W^T slice [16][3H + 4] (unit jj, gate row c), then the dg transpose tile [64][3][16 + 4].
+template <int H>
+__global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) {
+  constexpr int WP = 3 * H + 4, DTP = kUnits + 4, NKB = 3 * H / 16, CH = 16;   // CH k-blocks per chunk
+  static_assert(NKB % CH == 0, "chunking");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Wt = smem;
+  float* dT = smem + kUnits * WP;   // [64][3][DTP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
+  int dir, group, slice;
+  map_block(a.G, H / kUnits, dir, group, slice);
+  const int T = a.T, B = a.B, j0 = slice * kUnits, j = j0 + lr;
+  const int b0 = a.b_begin + group * kRows;
+  const int b_last = a.b_end - 1;
+  unsigned* cnt = a.counters + (dir * a.G + group) * 16;
+
+  {  // W_hh[dir][c][j0 .. j0+15] for all 3H rows c, stored transposed [jj][c]
+    const float* W = a.w_hh + (size_t)dir * 3 * H * H;
+    for (int v = tid; v < 3 * H * kUnits / 4; v += 256) {
+      const int c = v / (kUnits / 4), jq = (v % (kUnits / 4)) * 4;
+      const v4f w = ld4(W + (size_t)c * H + j0 + jq);
+      Wt[(jq + 0) * WP + c] = w.x;
+      Wt[(jq + 1) * WP + c] = w.y;
+      Wt[(jq + 2) * WP + c] = w.z;
+      Wt[(jq + 3) * WP + c] = w.w;
+    }
+  }
+  __syncthreads();
+
+  float* dgh_dir = a.dgh + (size_t)dir * B * T * 3 * H;   // [B][T][3H] of this direction
+  const __amdgpu_buffer_rsrc_t rg_ = rsrc(dgh_dir);
+  const int arow = min(b0 + wave * 16 + lr, b_last);
+  float dhz[4] = {0.f, 0.f, 0.f, 0.f};
+
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? T - 1 - step : step;
+    const int tnext = dir == 0 ? t + 1 : t - 1;
+    const int tprev = dir == 0 ? t - 1 : t + 1;
+    const bool edge = (step == T - 1);   // h_prev = 0 here
+    // epilogue operands (written by earlier launches): gates, dy, h_prev
+    float g_r[4], g_z[4], g_n[4], g_h[4], dyv[4], hpv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = min(b0 + wave * 16 + lq * 4 + r, b_last);
+      const float* gs = a.gates + (((size_t)dir * T + t) * B + b) * 4 * H;
+      g_r[r] = gs[j];
+      g_z[r] = gs[H + j];
+      g_n[r] = gs[2 * H + j];
+      g_h[r] = gs[3 * H + j];
+      dyv[r] = a.dy[((size_t)b * T + t) * 2 * H + dir * H + j];
+      hpv[r] = edge ? 0.f : a.y_in[((size_t)b * T + tprev) * 2 * H + dir * H + j];
+    }
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    if (step > 0) {
+      wait_count(cnt, (unsigned)(H / kUnits) * step);
+      const unsigned base = (unsigned)((((size_t)arow * T + tnext) * 3 * H + 4 * lq) * 4);
+      v4f dv[2][CH];
+#pragma unroll
+      for (int kb = 0; kb < CH; ++kb) dv[0][kb] = ld4_sc1(rg_, base + kb * 64);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ch = 0; ch < NKB / CH; ++ch) {
+        const int cur = ch & 1;
+        if (ch + 1 < NKB / CH) {
+#pragma unroll
+          for (int kb = 0; kb < CH; ++kb) dv[cur ^ 1][kb] = ld4_sc1(rg_, base + ((ch + 1) * CH + kb) * 64);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // next chunk's loads in flight before this chunk's MFMAs
+#pragma unroll
+        for (int kb = 0; kb < CH; ++kb) {
+          const v4f wv = ld4(Wt + lr * WP + (ch * CH + kb) * 16 + 4 * lq);
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][kb].x, wv.x, acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][kb].y, wv.y, acc[1], 0, 0, 0);
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][kb].z, wv.z, acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][kb].w, wv.w, acc[1], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = wave * 16 + lq * 4 + r, b = b0 + rl;
+      float dh = dyv[r];
+      if (step > 0) dh += (acc[0][r] + acc[1][r]) + dhz[r];
+      const float rg = g_r[r], zg = g_z[r], ng = g_n[r], ghn = g_h[r], hp = hpv[r];
+      const float dn = dh * (1.0f - zg);
+      const float daz = dh * (hp - ng) * zg * (1.0f - zg);
+      const float dan = dn * (1.0f - ng * ng);
+      const float dar = dan * ghn * rg * (1.0f - rg);
+      dhz[r] = dh * zg;
+      dT[(rl * 3 + 0) * DTP + lr] = dar;
+      dT[(rl * 3 + 1) * DTP + lr] = daz;
+      dT[(rl * 3 + 2) * DTP + lr] = dan * rg;
+      if (b <= b_last) {
+        float* dgi = a.dgi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
+        dgi[j] = dar;
+        dgi[H + j] = daz;
+        dgi[2 * H + j] = dan;
+      }
+    }
+    __syncthreads();
+    // dgh row slice (gates x 16 units) of 64 rows: 768 float4, 3 per thread.  Interior steps go
+    // write-through into dgh (the next step's operand); the edge step has no consumer: it goes to
+    // dgh_edge and zeroes its dgh row (kept out of the dW_hh GEMM, see srk_gru_layer_bwd).
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int v = tid + i * 256, rl = v / 12, g = (v % 12) / 4, uq = (v % 4) * 4, b = b0 + rl;
+      if (b > b_last) continue;
+      const v4f val = ld4(dT + (rl * 3 + g) * DTP + uq);
+      if (!edge) {
+        st4_sc1(rg_, (unsigned)((((size_t)b * T + t) * 3 * H + g * H + j0 + uq) * 4), val);
+      } else {
+        st4(a.dgh_edge + ((size_t)dir * B + b) * 3 * H + g * H + j0 + uq, val);
+        st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + j0 + uq, v4f{0.f, 0.f, 0.f, 0.f});
+      }
+    }
+    arrive(cnt);
+  }
+}
+
+template <int H>
+int occupancy_ok(bool backward, int grid, size_t lds) {
+  static int cus = -1, occ_f = -1, occ_b = -1;
+  if (cus < 0) {
+    int dev = 0;
+    SRK_CHECK_HIP(hipGetDevice(&dev));
+    hipDeviceProp_t p;
+    SRK_CHECK_HIP(hipGetDeviceProperties(&p, dev));
+    cus = p.multiProcessorCount;
+    SRK_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_fwd_persistent_kernel<H>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)fwd_lds_bytes(H)));
+    SRK_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_bwd_persistent_kernel<H>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd_lds_bytes(H)));
+    SRK_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, gru_fwd_persistent_kernel<H>, 256,
+                                                               fwd_lds_bytes(H)));
+    SRK_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_b, gru_bwd_persistent_kernel<H>, 256,
+                                                               bwd_lds_bytes(H)));
+  }
+  (void)lds;
+  const int occ = backward ? occ_b : occ_f;
+  return (occ >= 1 && grid <= cus) ? 1 : 0;   // one workgroup per CU: the sc1 hand-off form measured
+}
+
+}  // namespace
+
+size_t fwd_lds_bytes(int H) { return (size_t)(3 * 16 * (H + 4) + 64 * 20) * 4; }
+size_t bwd_lds_bytes(int H) { return (size_t)(16 * (3 * H + 4) + 64 * 3 * 20) * 4; }
+
+int gru_persistent_groups(int64_t H) {
+  if (H != 512) return 0;
+  return 4;   // 2 dirs x 4 groups x 32 slices = 256 workgroups (one per CU)
+}
+
+int gru_persistent_supported(int64_t B, int64_t T, int64_t H, bool backward) {
+  const int gmax = gru_persistent_groups(H);
+  if (gmax == 0) return 0;
+  // byte offsets of the buffer instructions are 32-bit
+  if ((double)B * T * 3 * H * 4 >= 2147483647.0 || (double)B * T * 2 * H * 4 >= 2147483647.0) return 0;
+  const int64_t G = std::min<int64_t>((B + kRows - 1) / kRows, gmax);
+  const int grid = (int)(2 * G * (H / kUnits));
+  const int ok = occupancy_ok<512>(backward, grid, backward ? bwd_lds_bytes(512) : fwd_lds_bytes(512));
+  return ok < 0 ? 0 : ok;
+}
+
+int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
+  const int gmax = gru_persistent_groups(a.H);
+  SRK_REQUIRE(gmax > 0 && a.H == 512, SRK_ERR_INVALID, "gru persistent: unsupported H");
+  const int rows_per_launch = gmax * kRows;
+  for (int c0 = 0; c0 < a.B; c0 += rows_per_launch) {
+    GruPArgs ac = a;
+    ac.b_begin = c0;
+    ac.b_end = std::min(a.B, c0 + rows_per_launch);
+    ac.G = (ac.b_end - c0 + kRows - 1) / kRows;
+    SRK_CHECK_HIP(hipMemsetAsync(ac.counters, 0, (size_t)kCounterFloats * 4, s));
+    const dim3 grid((unsigned)(2 * ac.G * (a.H / kUnits)));
+    if (!backward) {
+      ProfScope prof("gru_fwd_seq", s, 2.0 * 2.0 * (double)(ac.b_end - c0) * 3 * a.H * a.H * (a.T - 1));
+      hipLaunchKernelGGL(gru_fwd_persistent_kernel<512>, grid, dim3(256), fwd_lds_bytes(512), s, ac);
+    } else {
+      ProfScope prof("gru_bwd_seq", s, 2.0 * 2.0 * (double)(ac.b_end - c0) * 3 * a.H * a.H * (a.T - 1));
+      hipLaunchKernelGGL(gru_bwd_persistent_kernel<512>, grid, dim3(256), bwd_lds_bytes(512), s, ac);
+    }
+    SRK_CHECK_HIP(hipGetLastError());
+  }
+  return SRK_OK;
+}
+
+}  // namespace srk
+
+extern "C" int64_t srk_spin_timeouts(void) {
+  unsigned long long v = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(srk::g_spin_timeouts), sizeof(v)) != hipSuccess) return -1;
+  return (int64_t)v;
+}

@@ -12,9 +12,12 @@
 #include <mutex>
 #include <vector>
 
+#include "gru_internal.h"
 #include "srk_internal.h"
 
 namespace srk {
+
+int g_opt_gru_persistent = 1;
 
 static thread_local std::string g_last_error;
 
@@ -239,6 +242,18 @@ int srk_init(int device) {
   int rc = srk::get_tables(&t);
   SRK_CHECK_HIP(hipSetDevice(prev));
   return rc;
+  SRK_API_END
+}
+
+int srk_set_option(const char* name, int64_t value) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(name, SRK_ERR_INVALID, "set_option: null name");
+  const std::string n(name);
+  if (n == "gru_persistent") {
+    srk::g_opt_gru_persistent = value != 0;
+    return SRK_OK;
+  }
+  SRK_REQUIRE(false, SRK_ERR_INVALID, "set_option: unknown option '%s'", name);
   SRK_API_END
 }
 

@@ -127,3 +127,42 @@ def test_colsum_large(gpu):
     out = torch.empty(3072, device="cuda")
     call("srk_colsum_f32", ptr(X.cuda()), 13056, 3072, 3072, ptr(out), 0.0, stream_ptr())
     assert (out.cpu().double() - X.double().sum(0)).abs().max() <= 1e-3
+
+
+@pytest.mark.parametrize("B,T", [(1, 6), (67, 13), (256, 51), (300, 7)])
+def test_bigru_persistent_matches_per_step_and_torch(gpu, B, T):
+    """The one-launch persistent recurrence (H = 512) agrees with the per-step kernels (same MFMA
+    k order and cell math; only the compiler's fma contraction of the epilogue may differ, so
+    1e-6 relative, not bitwise) and matches torch's CPU GRU; B = 300 exercises the 256-row
+    chunking, B = 1 / 67 the clamped partial 64-row groups."""
+    from speechrecognitionproject_amd import _lib
+    IN, H = 24, 512
+    torch.manual_seed(3)
+    ref = _ref_gru(IN, H, 1)
+    mine = snn.BiGRU(IN, H, num_layers=1).cuda()
+    mine.load_state_dict(ref.state_dict())
+    x = torch.randn(B, T, IN)
+    w = torch.randn(B, T, 2 * H)
+    outs = {}
+    try:
+        for mode in (1, 0):
+            _lib.set_option("gru_persistent", mode)
+            mine.zero_grad()
+            xm = x.cuda().requires_grad_(True)
+            ym, _ = mine(xm)
+            (ym * w.cuda()).sum().backward()
+            outs[mode] = [ym.detach().cpu(), xm.grad.cpu()] + [p.grad.cpu() for p in mine.parameters()]
+    finally:
+        _lib.set_option("gru_persistent", 1)
+    assert _lib.spin_timeouts() == 0
+    for i, (a, b) in enumerate(zip(outs[1], outs[0])):
+        err = float((a - b).abs().max() / (b.abs().max() + 1e-30))
+        assert err <= 1e-6, (i, err)
+    if B * T <= 4000:
+        xr = x.clone().requires_grad_(True)
+        yr, _ = ref(xr)
+        (yr * w).sum().backward()
+        assert (outs[1][0] - yr.detach()).abs().max() <= 2e-5 * max(1.0, T / 10)
+        gr = ref.weight_hh_l0.grad
+        gm = dict(mine.named_parameters())["weight_hh_l0"].grad.cpu()
+        assert (gm - gr).abs().max() / gr.abs().max() <= 1e-4

@@ -26,6 +26,7 @@ struct GruPArgs {
   float* dgh;            // bwd: [2][B][T][3H] (also the dg hand-off buffer)
   float* dgh_edge;       // bwd: [2][B][3H]
   unsigned* counters;    // kCounterFloats words
+  unsigned long long* trace;   // optional per-(workgroup, step) timestamps (tools/gru_trace.py)
 };
 
 size_t fwd_lds_bytes(int H);
@@ -37,5 +38,6 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s);
 
 // Runtime options (srk_set_option): persistent GRU recurrence on/off (default on).
 extern int g_opt_gru_persistent;
+extern unsigned long long* g_opt_gru_trace;   // device buffer or nullptr
 
 }  // namespace srk

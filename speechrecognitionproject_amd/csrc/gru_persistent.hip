@@ -77,6 +77,13 @@ __device__ __forceinline__ void arrive(unsigned* cnt) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Diagnostics (tools/gru_trace.py): thread 0 stamps s_memrealtime (100 MHz) at step start, after
+// the arrival wait, after the cell epilogue and after publishing.  Off (null) in production.
+__device__ __forceinline__ void stamp(const GruPArgs& a, int step, int i) {
+  if (a.trace && threadIdx.x == 0)
+    a.trace[((size_t)blockIdx.x * a.T + step) * 4 + i] = __builtin_amdgcn_s_memrealtime();
+}
+
 // (direction, group, slice) of this workgroup: the S slices of one (direction, group) pair are
 // dealt to blocks of ONE XCD (blocks b, b+8, ... share an XCD under round-robin dispatch), so the
 // handed-off rows stay in that XCD's L2.  Speed only; the protocol does not depend on it.
@@ -123,6 +130,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
   for (int step = 0; step < T; ++step) {
     const int t = dir == 0 ? step : T - 1 - step;
     const int tprev = dir == 0 ? t - 1 : t + 1;
+    stamp(a, step, 0);
     float gr[4], gz[4], gn[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {   // input projections of the lane's cells (written by an earlier launch)
@@ -137,6 +145,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
     for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (step > 0) {
       wait_count(cnt, (unsigned)(H / kUnits) * step);
+      stamp(a, step, 1);
       // h_{t-1}[arow][k], k = 16 kb + 4 lq + s  (k-permuted: one b128 feeds 4 MFMAs)
       const unsigned base = (unsigned)((((size_t)arow * T + tprev) * 2 * H + dir * H + 4 * lq) * 4);
       v4f hv[NKB];
@@ -174,12 +183,14 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
       }
     }
     __syncthreads();
+    stamp(a, step, 2);
     {  // h_t -> y (write-through): thread = (row tid/4, units 4*(tid%4) .. +3)
       const int rl = tid >> 2, uq = (tid & 3) * 4, b = b0 + rl;
       if (b <= b_last)
         st4_sc1(ry, (unsigned)((((size_t)b * T + t) * 2 * H + dir * H + j0 + uq) * 4), ld4(hT + rl * HTP + uq));
     }
     arrive(cnt);
+    stamp(a, step, 3);
   }
 }
 
@@ -224,6 +235,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
     const int tnext = dir == 0 ? t + 1 : t - 1;
     const int tprev = dir == 0 ? t - 1 : t + 1;
     const bool edge = (step == T - 1);   // h_prev = 0 here
+    stamp(a, step, 0);
     // epilogue operands (written by earlier launches): gates, dy, h_prev
     float g_r[4], g_z[4], g_n[4], g_h[4], dyv[4], hpv[4];
 #pragma unroll
@@ -240,6 +252,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     if (step > 0) {
       wait_count(cnt, (unsigned)(H / kUnits) * step);
+      stamp(a, step, 1);
       const unsigned base = (unsigned)((((size_t)arow * T + tnext) * 3 * H + 4 * lq) * 4);
       v4f dv[2][CH];
 #pragma unroll
@@ -285,6 +298,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
       }
     }
     __syncthreads();
+    stamp(a, step, 2);
     // dgh row slice (gates x 16 units) of 64 rows: 768 float4, 3 per thread.  Interior steps go
     // write-through into dgh (the next step's operand); the edge step has no consumer: it goes to
     // dgh_edge and zeroes its dgh row (kept out of the dW_hh GEMM, see srk_gru_layer_bwd).
@@ -301,6 +315,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
       }
     }
     arrive(cnt);
+    stamp(a, step, 3);
   }
 }
 
@@ -354,6 +369,7 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
   const int rows_per_launch = gmax * kRows;
   for (int c0 = 0; c0 < a.B; c0 += rows_per_launch) {
     GruPArgs ac = a;
+    ac.trace = g_opt_gru_trace;
     ac.b_begin = c0;
     ac.b_end = std::min(a.B, c0 + rows_per_launch);
     ac.G = (ac.b_end - c0 + kRows - 1) / kRows;

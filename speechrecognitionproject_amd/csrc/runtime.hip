@@ -18,6 +18,7 @@
 namespace srk {
 
 int g_opt_gru_persistent = 1;
+unsigned long long* g_opt_gru_trace = nullptr;
 
 static thread_local std::string g_last_error;
 
@@ -251,6 +252,10 @@ int srk_set_option(const char* name, int64_t value) {
   const std::string n(name);
   if (n == "gru_persistent") {
     srk::g_opt_gru_persistent = value != 0;
+    return SRK_OK;
+  }
+  if (n == "gru_trace_ptr") {   // diagnostics: device buffer of 4 x u64 per (workgroup, step), 0 = off
+    srk::g_opt_gru_trace = reinterpret_cast<unsigned long long*>(value);
     return SRK_OK;
   }
   SRK_REQUIRE(false, SRK_ERR_INVALID, "set_option: unknown option '%s'", name);

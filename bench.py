@@ -1,6 +1,14 @@
 """Benchmark: utterances/s of the MFCC + BiGRU train step on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256] [--model mfcc_bgru]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model mfcc_bgru|fbanks_cnn|resnet_bgru|spec_bgru]
+                    [--batch B]
+
+--model selects the BASELINE.json config (default = configs[1], the metric's headline model):
+  mfcc_bgru   cfg2: on-device MFCC[39x51] + model_mfcc_bgru, 256 clips per GPU
+  fbanks_cnn  cfg3: on-device log-mel fbank[98x120] + model_fbanks_cnn (dropout on), 512 per GPU
+  resnet_bgru cfg4: raw-wave model_resnet_bgru (BatchNorm, per-rank statistics), 512 per GPU
+  spec_bgru   cfg5: K4 noise-mix of int16 PCM with a resident noise bank + log spectrogram +
+              model_spec_bgru, 512 per GPU
 
 For N > 1 the driver launches one process per GPU with torch.distributed.run; each rank takes its
 own shard of synthetic clips (weak scaling: per-GPU batch fixed) and the flat gradient buffer is
@@ -38,7 +46,20 @@ from speechrecognitionproject_amd.synthetic import synthetic_clips    # noqa: E4
 PEAK_FP32_MFMA_TFLOPS = 157.3     # MI355X_MICROARCH.md, dense fp32 matrix (= vector) peak
 PEAK_HBM_GBS = 8000.0             # MI355X HBM3E spec
 MFCC_BYTES_PER_CLIP = 71956       # 64,000 in + 7,956 out
-TRAIN_GFLOP_PER_UTT = {"mfcc_bgru": 1.9434, "spec_bgru": 2.0367}
+TRAIN_GFLOP_PER_UTT = {"mfcc_bgru": 1.9434, "fbanks_cnn": 2.1449, "resnet_bgru": 25.8191,
+                       "spec_bgru": 2.0367}   # SURVEY.md §8d (FlopCounterMode on the reference modules)
+DEFAULT_BATCH = {"mfcc_bgru": 256, "fbanks_cnn": 512, "resnet_bgru": 512, "spec_bgru": 512}
+CFG = {"mfcc_bgru": "cfg2 mfcc_bgru: on-device MFCC[39x51] + 2-layer BiGRU(512) + FC",
+       "fbanks_cnn": "cfg3 fbanks_cnn: on-device log-mel fbank[98x120] + 4 Conv2d + pools + dropout + 2 FC",
+       "resnet_bgru": "cfg4 resnet_bgru: raw-wave ResNet-1D (BN, ReLU) + Linear + 2-layer BiGRU(512) + FC",
+       "spec_bgru": "cfg5 spec_bgru: on-device noise-mix (K4) + log spectrogram[49x321] + 2-layer BiGRU(512) + FC"}
+# feature kernel of each model and its algorithmic bytes per clip
+FEATURE = {"mfcc_bgru": ("mfcc", 71956), "fbanks_cnn": ("fbank", 111040), "spec_bgru": ("spec", 126916)}
+MATRIX_KERNELS = ("gru_fwd_seq", "gru_bwd_seq", "gru_fwd_step", "gru_bwd_step", "gemm_f32",
+                  "conv_fwd", "conv_dgrad", "conv_wgrad")
+OTHER_KERNELS = ("mfcc", "fbank", "spec", "noise_mix", "adam", "batchnorm_fwd", "batchnorm_bwd", "conv1_pool_fwd",
+                 "conv1_pool_wgrad",
+                 "maxpool_fwd", "maxpool_bwd")
 
 
 def log(*a):
@@ -46,13 +67,10 @@ def log(*a):
 
 
 def build_model(name):
-    if name == "mfcc_bgru":
-        from speechrecognitionproject_amd.models.model_mfcc_bgru import Network
-    elif name == "spec_bgru":
-        from speechrecognitionproject_amd.models.model_spec_bgru import Network
-    else:
+    import importlib
+    if name not in DEFAULT_BATCH:
         raise SystemExit("unknown --model %s" % name)
-    return Network()
+    return importlib.import_module("speechrecognitionproject_amd.models.model_%s" % name).Network()
 
 
 def cpu_baseline(model_name, batch, seconds):
@@ -60,7 +78,8 @@ def cpu_baseline(model_name, batch, seconds):
     from oracle import models as OM
     threads = max(1, min(16, os.cpu_count() or 1))
     torch.set_num_threads(threads)
-    cls = {"mfcc_bgru": OM.MfccBGRU, "spec_bgru": OM.SpecBGRU}[model_name]
+    cls = {"mfcc_bgru": OM.MfccBGRU, "spec_bgru": OM.SpecBGRU, "fbanks_cnn": OM.FbanksCNN,
+           "resnet_bgru": OM.ResnetBGRU}[model_name]
     torch.manual_seed(0)
     net = cls()
     opt = torch.optim.Adam(net.parameters(), lr=1e-4)
@@ -82,26 +101,28 @@ def cpu_baseline(model_name, batch, seconds):
         pass
     return {"value": round(n * batch / el, 2), "unit": "utt/s", "cores": threads, "kind": "port",
             "sample": "%d train steps x %d clips (%s CPU restatement: per-clip numpy features + torch-CPU "
-                      "fp32 BiGRU fwd/bwd + Adam), %.1f s, %s" % (n, batch, model_name, el, cpu)}
+                      "fp32 model fwd/bwd + Adam), %.1f s, %s" % (n, batch, model_name, el, cpu)}
 
 
-def mfcc_roofline(n_clips=65536):
+def feature_roofline(model_name, n_clips=65536):
+    """The model's feature kernel alone on a large batch (HBM-bound): algorithmic bytes / time."""
+    name, per_clip = FEATURE[model_name]
+    fn = {"mfcc": features.mfcc, "fbank": features.fbank, "spec": features.spec}[name]
     x, _ = synthetic_clips(1024, seed=123)
     xd = torch.from_numpy(x).cuda().repeat(n_clips // 1024, 1)
-    out = torch.empty((n_clips, 39, 51), device="cuda")
+    out = None
     for _ in range(2):
-        features.mfcc(xd, out=out)
+        out = fn(xd, out=out)
     torch.cuda.synchronize()
     _lib.prof_enable(True)
     for _ in range(5):
-        features.mfcc(xd, out=out)
-    cnt, ms, work = _lib.prof_read("mfcc")
+        fn(xd, out=out)
+    cnt, ms, work = _lib.prof_read(name)
     _lib.prof_enable(False)
     gbs = work / (ms * 1e-3) / 1e9
-    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+    return {"kernel": name, "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
-            "clips_per_launch": n_clips, "ms_per_launch": round(ms / cnt, 4),
-            "bytes_per_clip": MFCC_BYTES_PER_CLIP}
+            "clips_per_launch": n_clips, "ms_per_launch": round(ms / cnt, 4), "bytes_per_clip": per_clip}
 
 
 def main():
@@ -109,13 +130,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="clips per GPU per step")
+    ap.add_argument("--batch", type=int, default=None, help="clips per GPU per step (default per model)")
     ap.add_argument("--model", default="mfcc_bgru")
     ap.add_argument("--pool", type=int, default=4, help="distinct pre-staged batches per rank")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true")
-    ap.add_argument("--no-mfcc-roofline", action="store_true")
+    ap.add_argument("--no-feature-roofline", "--no-mfcc-roofline", dest="no_feature_roofline", action="store_true")
     args = ap.parse_args()
 
     rank, world, local = parallel.init_from_env()
@@ -130,14 +151,31 @@ def main():
     parallel.broadcast_flat(flat)
     crit = CrossEntropyLoss()
 
-    B = args.batch
-    x, y = synthetic_clips(args.pool * B, seed=1000 + rank)
-    pcm = torch.from_numpy(x).to(dev).view(args.pool, B, -1)
+    B = args.batch or DEFAULT_BATCH[args.model]
+    x, y = synthetic_clips(args.pool * B, seed=1000 + rank, clip=30000 if args.model == "spec_bgru" else 32767)
     lab = torch.from_numpy(y).to(dev).view(args.pool, B)
+    if args.model == "spec_bgru":
+        # cfg5: int16 PCM + resident noise bank; the per-clip (file, offset, gain) draws of
+        # dataset.py:190-193 are made up front (numpy), the mix runs on the device every step.
+        from speechrecognitionproject_amd.synthetic import synthetic_noise_bank, synthetic_noise_draws
+        pcm16 = torch.from_numpy(x.astype(np.int16)).to(dev).view(args.pool, B, -1)
+        bank = torch.from_numpy(synthetic_noise_bank()).to(dev)
+        draws = [torch.from_numpy(a).to(dev).view(args.pool, B)
+                 for a in synthetic_noise_draws(args.pool * B, seed=2 + rank)]
+        mixed = torch.empty((B, 16000), device=dev)
+
+        def inputs(i):
+            j = i % args.pool
+            return features.noise_mix(pcm16[j], bank, draws[0][j], draws[1][j], draws[2][j], out=mixed)
+    else:
+        pcm = torch.from_numpy(x).to(dev).view(args.pool, B, -1)
+
+        def inputs(i):
+            return pcm[i % args.pool]
 
     def step(i):
         opt.zero_grad()
-        out = model(pcm[i % args.pool])
+        out = model(inputs(i))
         loss = crit(out, lab[i % args.pool])
         loss.backward()
         parallel.allreduce_grads(flat)
@@ -169,7 +207,7 @@ def main():
 
     kernels = {}
     if not args.no_prof:
-        for name in ("gru_fwd_seq", "gru_bwd_seq", "gru_fwd_step", "gru_bwd_step", "gemm_f32", "mfcc", "adam"):
+        for name in MATRIX_KERNELS + OTHER_KERNELS:
             c, ms, w = _lib.prof_read(name)
             if c:
                 kernels[name] = {"launches": c, "ms_total": round(ms, 3), "work": w}
@@ -179,7 +217,7 @@ def main():
         return
     value = world * B * args.steps / el
     roof = None
-    mm = {k: v for k, v in kernels.items() if k in ("gru_fwd_seq", "gru_bwd_seq", "gru_fwd_step", "gru_bwd_step", "gemm_f32")}
+    mm = {k: v for k, v in kernels.items() if k in MATRIX_KERNELS}
     if mm:
         dom = max(mm, key=lambda k: mm[k]["ms_total"])
         k = mm[dom]
@@ -193,16 +231,16 @@ def main():
         "value": round(value, 2), "unit": "utt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SURVEY.md §8d clip mix, pre-staged in HBM)",
-        "config": {"workload": "cfg2 %s: on-device MFCC[39x51] + 2-layer BiGRU(512) + FC, CE, backward, Adam "
-                               "(full training.py step), per-GPU batch %d" % (args.model, B),
+        "config": {"workload": "%s, CE, backward, Adam (full training.py step), per-GPU batch %d"
+                               % (CFG[args.model], B), "model": args.model,
                    "global_batch": world * B, "clip_samples": 16000, "parallelism": "dp%d" % world},
         "model_tflops": round(value * TRAIN_GFLOP_PER_UTT.get(args.model, 0) / 1e3, 2),
         "final_loss": round(final_loss, 5),
         "roofline": roof,
         "kernels": {k: {"launches": v["launches"], "ms_total": v["ms_total"]} for k, v in kernels.items()},
     }
-    if not args.no_mfcc_roofline:
-        res["mfcc_roofline"] = mfcc_roofline()
+    if not args.no_feature_roofline and args.model in FEATURE:
+        res["feature_roofline"] = feature_roofline(args.model)
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.model, 32, args.cpu_seconds)
     print(json.dumps(res), flush=True)

@@ -131,6 +131,19 @@ int srk_conv2d_nhwc_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t
 /* Max pooling, window = stride = (kh, kw), floor mode, channels-last (nn.MaxPool2d((1,3)),
  * ((1,4)) and nn.MaxPool1d(98), model_fbanks_cnn.py:73,75,78).  Backward routes each gradient to
  * the first maximum of its window, as PyTorch does.                                          */
+/* Fused first layer of model_fbanks_cnn (models/model_fbanks_cnn.py:72-73,89-90): Conv2d(1, 64,
+ * (7,3), padding (3,1)) + bias + MaxPool2d((1,3)) in one pass.  x: [N, H, W] (one input channel);
+ * y: pooled [N, H, W/3, 64] (NHWC); argmax: uint8 [N, H, W/3, 64] = position (0..2) of each window's
+ * first maximum (PyTorch's rule, NaN wins).  Only that geometry is accepted (SRK_ERR_INVALID else).
+ * The backward gives dW [64,1,7,3] and db [64] (db may be NULL) from the POOLED gradient dy and
+ * argmax (the unpooled gradient is never formed); ws: srk_conv1_pool_workspace_floats() floats. */
+int64_t srk_conv1_pool_workspace_floats(int64_t Co, int64_t KH, int64_t KW);
+int srk_conv1_pool_fwd(const float* x, int64_t N, int64_t H, int64_t W, const float* w, const float* bias,
+                       int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t pool, float* y,
+                       uint8_t* argmax, void* stream);
+int srk_conv1_pool_wgrad(const float* x, int64_t N, int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW,
+                         int64_t ph, int64_t pw, int64_t pool, const float* dy, const uint8_t* argmax, float* dw,
+                         float* db, float* ws, void* stream);
 int srk_maxpool_nhwc_fwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t C, int64_t kh, int64_t kw,
                          float* y, void* stream);
 int srk_maxpool_nhwc_bwd(const float* x, const float* dy, int64_t N, int64_t H, int64_t W, int64_t C, int64_t kh,

@@ -46,6 +46,9 @@ _SIGS = {
                             _P],
     "srk_conv2d_nhwc_bwd": [_P, _I64, _I64, _I64, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P,
                             _P, _P, _P],
+    "srk_conv1_pool_workspace_floats": [_I64, _I64, _I64],
+    "srk_conv1_pool_fwd": [_P, _I64, _I64, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P],
+    "srk_conv1_pool_wgrad": [_P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P],
     "srk_maxpool_nhwc_fwd": [_P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P],
     "srk_maxpool_nhwc_bwd": [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P],
     "srk_batchnorm_fwd": [_P, _I64, _I64, _P, _P, _F, _F, _I, _P, _P, _P, _I, _P, _P, _P, _P],
@@ -56,7 +59,7 @@ _SIGS = {
     "srk_dropout_apply": [_P, _P, _I64, _F, _P, _P],
 }
 _RESTYPE = {"srk_last_error": ctypes.c_char_p, "srk_spin_timeouts": ctypes.c_int64, "srk_gru_workspace_floats": ctypes.c_int64,
-            "srk_conv2d_workspace_floats": ctypes.c_int64}
+            "srk_conv2d_workspace_floats": ctypes.c_int64, "srk_conv1_pool_workspace_floats": ctypes.c_int64}
 
 
 class SrkError(RuntimeError):

@@ -13,12 +13,12 @@
 #include <mutex>
 
 #include "gemm.h"
+#include "mfma_tile.h"
 
 namespace srk {
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float v4f __attribute__((ext_vector_type(4)));
+using namespace tile;
 
 enum { kFwd = 0, kDgrad = 1, kWgrad = 2 };
 
@@ -30,176 +30,173 @@ struct ConvArgs {
   float* out;          // fwd: Y [N*Ho*Wo][Co]; dgrad: dX [N*H*W][Ci]; wgrad: dWt [KH*KW*Ci][Co]
   const float* bias;   // fwd only, [Co]
   int64_t M, Nn, K;    // GEMM dims
-  int tiles_n;
+  int tiles_m, tiles_n, tiles, nblk, group_m;
   int64_t kchunk;
-  float* partial;      // split-K slabs (wgrad)
+  float* partial;      // split-K slabs
 };
 
-// ---- operand element gathers (return 0 outside the image / problem)
-__device__ __forceinline__ float gather_fwd_a(const ConvArgs& c, int64_t m, int64_t k) {
-  if (m >= c.M || k >= c.K) return 0.f;
-  const int ci = (int)(k % c.Ci);
-  const int64_t t = k / c.Ci;
-  const int kw = (int)(t % c.KW), kh = (int)(t / c.KW);
-  const int wo = (int)(m % c.Wo);
-  const int64_t u = m / c.Wo;
-  const int ho = (int)(u % c.Ho), n = (int)(u / c.Ho);
-  const int hi = ho * c.sh + kh - c.ph, wi = wo * c.sw + kw - c.pw;
-  if (hi < 0 || hi >= c.H || wi < 0 || wi >= c.W) return 0.f;
-  return c.x[(((int64_t)n * c.H + hi) * c.W + wi) * c.Ci + ci];
-}
+// Implicit-GEMM operand gathers.  Each returns the ELEMENT OFFSET of the value (clamped to 0 when
+// the position is outside the image / problem) and whether it is valid; the caller loads
+// unconditionally and zeroes invalid values at LDS-store time (after the stage's MFMAs), so no load
+// is exec-masked and no select waits on a load in front of the MFMAs.
+//   fwd   A[m = pixel (n,ho,wo)][k = (kh,kw,ci)] = X[n, ho*sh+kh-ph, wo*sw+kw-pw, ci]
+//   dgrad A[m = pixel (n,h,w)][k = (kh,kw,co)]   = dY[n, (h+ph-kh)/sh, (w+pw-kw)/sw, co] (exact division only)
+//   wgrad A[m = (kh,kw,ci)][k = pixel (n,ho,wo)] = X[n, ho*sh+kh-ph, wo*sw+kw-pw, ci]
+struct Pix { int n, a, b; bool ok; };   // pixel (n, row, col) + "row index < rows"
 
-__device__ __forceinline__ float gather_dgrad_a(const ConvArgs& c, int64_t m, int64_t k) {
-  if (m >= c.M || k >= c.K) return 0.f;
-  const int co = (int)(k % c.Co);
-  const int64_t t = k / c.Co;
-  const int kw = (int)(t % c.KW), kh = (int)(t / c.KW);
-  const int w = (int)(m % c.W);
-  const int64_t u = m / c.W;
-  const int h = (int)(u % c.H), n = (int)(u / c.H);
-  const int ht = h + c.ph - kh, wt = w + c.pw - kw;
-  if (ht < 0 || wt < 0 || ht % c.sh || wt % c.sw) return 0.f;
-  const int ho = ht / c.sh, wo = wt / c.sw;
-  if (ho >= c.Ho || wo >= c.Wo) return 0.f;
-  return c.dy[(((int64_t)n * c.Ho + ho) * c.Wo + wo) * c.Co + co];
+__device__ __forceinline__ Pix split_pix(int64_t p, int64_t rows, int Hh, int Ww) {
+  Pix q;
+  q.ok = p < rows;
+  const int64_t pc = q.ok ? p : 0;
+  q.b = (int)(pc % Ww);
+  const int64_t u = pc / Ww;
+  q.a = (int)(u % Hh);
+  q.n = (int)(u / Hh);
+  return q;
 }
-
-// wgrad: op(A)[m = (kh,kw,ci)][k = pixel] = X gathered at that pixel's receptive field
-__device__ __forceinline__ float gather_wgrad_a(const ConvArgs& c, int64_t m, int64_t k) {
-  if (m >= c.M || k >= c.K) return 0.f;
-  const int ci = (int)(m % c.Ci);
-  const int64_t t = m / c.Ci;
-  const int kw = (int)(t % c.KW), kh = (int)(t / c.KW);
-  const int wo = (int)(k % c.Wo);
-  const int64_t u = k / c.Wo;
-  const int ho = (int)(u % c.Ho), n = (int)(u / c.Ho);
-  const int hi = ho * c.sh + kh - c.ph, wi = wo * c.sw + kw - c.pw;
-  if (hi < 0 || hi >= c.H || wi < 0 || wi >= c.W) return 0.f;
-  return c.x[(((int64_t)n * c.H + hi) * c.W + wi) * c.Ci + ci];
+struct Tap { int kh, kw, ch; };   // k (or wgrad m) = (kh, kw, channel)
+__device__ __forceinline__ Tap split_tap(int64_t k, int C, int KW) {
+  Tap t;
+  t.ch = (int)(k % C);
+  const int64_t u = k / C;
+  t.kw = (int)(u % KW);
+  t.kh = (int)(u / KW);
+  return t;
 }
 
 template <int MODE>
-__device__ __forceinline__ v4f load_a4(const ConvArgs& c, int64_t m, int64_t k, bool along_k) {
-  // four consecutive elements along k (fwd/dgrad) or along m (wgrad) of op(A)
-  v4f v;
-  if (MODE == kFwd) {
-    if (c.Ci % 4 == 0 && m < c.M && k + 3 < c.K) {   // one contiguous channel run
-      const int ci = (int)(k % c.Ci);
-      const int64_t t = k / c.Ci;
-      const int kw = (int)(t % c.KW), kh = (int)(t / c.KW);
-      const int wo = (int)(m % c.Wo);
-      const int64_t u = m / c.Wo;
-      const int ho = (int)(u % c.Ho), n = (int)(u / c.Ho);
-      const int hi = ho * c.sh + kh - c.ph, wi = wo * c.sw + kw - c.pw;
-      if (hi < 0 || hi >= c.H || wi < 0 || wi >= c.W) return v4f{0.f, 0.f, 0.f, 0.f};
-      return *reinterpret_cast<const v4f*>(c.x + (((int64_t)n * c.H + hi) * c.W + wi) * c.Ci + ci);
-    }
-    for (int i = 0; i < 4; ++i) v[i] = gather_fwd_a(c, m, k + i);
-  } else if (MODE == kDgrad) {
-    if (c.Co % 4 == 0 && m < c.M && k + 3 < c.K) {
-      const int co = (int)(k % c.Co);
-      const int64_t t = k / c.Co;
-      const int kw = (int)(t % c.KW), kh = (int)(t / c.KW);
-      const int w = (int)(m % c.W);
-      const int64_t u = m / c.W;
-      const int h = (int)(u % c.H), n = (int)(u / c.H);
-      const int ht = h + c.ph - kh, wt = w + c.pw - kw;
-      if (ht < 0 || wt < 0 || ht % c.sh || wt % c.sw) return v4f{0.f, 0.f, 0.f, 0.f};
-      const int ho = ht / c.sh, wo = wt / c.sw;
-      if (ho >= c.Ho || wo >= c.Wo) return v4f{0.f, 0.f, 0.f, 0.f};
-      return *reinterpret_cast<const v4f*>(c.dy + (((int64_t)n * c.Ho + ho) * c.Wo + wo) * c.Co + co);
-    }
-    for (int i = 0; i < 4; ++i) v[i] = gather_dgrad_a(c, m, k + i);
-  } else {   // wgrad, vectors along m (channel run of one pixel)
-    if (c.Ci % 4 == 0 && k < c.K && m + 3 < c.M) {
-      const int ci = (int)(m % c.Ci);
-      const int64_t t = m / c.Ci;
-      const int kw = (int)(t % c.KW), kh = (int)(t / c.KW);
-      const int wo = (int)(k % c.Wo);
-      const int64_t u = k / c.Wo;
-      const int ho = (int)(u % c.Ho), n = (int)(u / c.Ho);
-      const int hi = ho * c.sh + kh - c.ph, wi = wo * c.sw + kw - c.pw;
-      if (hi < 0 || hi >= c.H || wi < 0 || wi >= c.W) return v4f{0.f, 0.f, 0.f, 0.f};
-      return *reinterpret_cast<const v4f*>(c.x + (((int64_t)n * c.H + hi) * c.W + wi) * c.Ci + ci);
-    }
-    for (int i = 0; i < 4; ++i) v[i] = gather_wgrad_a(c, m + i, k);
+__device__ __forceinline__ int64_t a_offset(const ConvArgs& c, const Pix& p, const Tap& t, bool& ok) {
+  if (MODE == kDgrad) {
+    const int ht = p.a + c.ph - t.kh, wt = p.b + c.pw - t.kw;
+    const int ho = ht / c.sh, wo = wt / c.sw;
+    ok = ok && p.ok && ht >= 0 && wt >= 0 && ho * c.sh == ht && wo * c.sw == wt && ho < c.Ho && wo < c.Wo;
+    return ok ? (((int64_t)p.n * c.Ho + ho) * c.Wo + wo) * c.Co + t.ch : 0;
   }
-  (void)along_k;
-  return v;
+  const int hi = p.a * c.sh + t.kh - c.ph, wi = p.b * c.sw + t.kw - c.pw;
+  ok = ok && p.ok && hi >= 0 && hi < c.H && wi >= 0 && wi < c.W;
+  return ok ? (((int64_t)p.n * c.H + hi) * c.W + wi) * c.Ci + t.ch : 0;
 }
 
-// B operand: a plain row-major [K][Nn] matrix (fwd: Wt, dgrad: Wd, wgrad: dY as [pixels][Co]).
-__device__ __forceinline__ v4f load_b4(const float* B, int64_t ldb, int64_t k, int64_t n0, int64_t K, int64_t N,
-                                       bool vec) {
-  v4f v = {0.f, 0.f, 0.f, 0.f};
-  if (k >= K) return v;
-  const float* q = B + k * ldb + n0;
-  if (vec && n0 + 3 < N) return *reinterpret_cast<const v4f*>(q);
-  for (int i = 0; i < 4; ++i)
-    if (n0 + i < N) v[i] = q[i];
-  return v;
-}
-
-template <int MODE, int BM, int BN, int BK>
+// VEC: the 4 elements of a staged A float4 share one pixel and one (kh, kw) — channel count % 4 == 0
+// (fwd / wgrad: Ci, dgrad: Co).  VECB: the B operand's N % 4 == 0 (16-B loads along n).
+template <int MODE, int BM, int BN, int BK, bool VEC, bool VECB>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   constexpr int NT = 256;
-  constexpr bool A_ALONG_M = (MODE == kWgrad);
-  constexpr int LA = A_ALONG_M ? BM : BM + 1;
-  constexpr int LB = BN;
+  constexpr bool AKC = MODE != kWgrad;   // A k-contiguous (channels along k) for fwd / dgrad
+  using IA = Img<AKC, BM, BK>;
+  using IB = Img<false, BN, BK>;         // B = row-major [K][N] (Wt / Wd / dY)
   constexpr int VA = BM * BK / 4 / NT, VB = BN * BK / 4 / NT;
   constexpr int TM = BM / 64, TN = BN / 64;
-  __shared__ float As[2][BK][LA];
-  __shared__ float Bs[2][BK][LB];
+  static_assert(VA >= 1 && VB >= 1 && TM >= 1 && TN >= 1 && VA * 4 <= 32, "bad tile");
+  __shared__ __attribute__((aligned(16))) float smem[2 * (IA::FLOATS + IB::FLOATS)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tm = blockIdx.x / c.tiles_n, tn = blockIdx.x % c.tiles_n;
-  const int split = blockIdx.y;
+  int split, tm, tn;
+  map_tile(c.nblk, c.tiles, c.tiles_m, c.tiles_n, c.group_m, true, split, tm, tn);
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int64_t kb = split * c.kchunk;
-  const int64_t ke = (kb + c.kchunk < c.K) ? kb + c.kchunk : c.K;
+  const int64_t kb0 = split * c.kchunk;
+  const int64_t ke = (kb0 + c.kchunk < c.K) ? kb0 + c.kchunk : c.K;
   const int wm0 = (wave >> 1) * (BM / 2), wn0 = (wave & 1) * (BN / 2);
-  const float* Bmat = MODE == kWgrad ? c.dy : c.wmat;
-  const bool vec_b = (c.Nn % 4 == 0);
-  ConvArgs cc = c;
-  cc.K = ke;   // gathers zero-fill past this split's k range
+  const float* __restrict__ Asrc = MODE == kDgrad ? c.dy : c.x;
+  const float* __restrict__ Bsrc = MODE == kWgrad ? c.dy : c.wmat;
+  const int Cch = MODE == kDgrad ? c.Co : c.Ci;   // channel count along A's k (fwd/dgrad) or m (wgrad)
+  const int Hh = MODE == kDgrad ? c.H : c.Ho, Ww = MODE == kDgrad ? c.W : c.Wo;   // pixel grid of A's rows / k
+
+  // fwd / dgrad: this thread's A rows are fixed for the whole k loop (decomposed once);
+  // wgrad: its A "rows" (= taps m) are fixed instead.
+  Pix prow[VA];
+  Tap mtap[4];   // wgrad: the taps m0 + aq + e of this thread (fixed for the whole k loop)
+  int aq;        // fwd/dgrad: k offset of this thread's float4 in a stage; wgrad: m offset
+  if (AKC) {
+    aq = (tid % (BK / 4)) * 4;
+#pragma unroll
+    for (int i = 0; i < VA; ++i) prow[i] = split_pix(m0 + (tid + i * NT) / (BK / 4), c.M, Hh, Ww);
+  } else {
+    aq = (tid % (BM / 4)) * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) mtap[e] = split_tap(m0 + aq + e < c.M ? m0 + aq + e : 0, Cch, c.KW);
+  }
 
   v4f ra[VA], rb[VB];
+  unsigned amask = 0, bmask = 0;   // bit = element valid (4 per staged float4)
   auto load_tile = [&](int64_t k0) {
+    amask = 0;
+    bmask = 0;
+    if (AKC) {   // 4 consecutive k = (kh, kw, ch .. ch+3) of one pixel row
+      const int64_t k = k0 + aq;
+      if (VEC) {
+        const Tap t = split_tap(k < ke ? k : 0, Cch, c.KW);
 #pragma unroll
-    for (int i = 0; i < VA; ++i) {
-      const int vi = tid + i * NT;
-      if (!A_ALONG_M) {
-        const int row = vi / (BK / 4), kq = (vi % (BK / 4)) * 4;
-        ra[i] = load_a4<MODE>(cc, m0 + row, k0 + kq, true);
+        for (int i = 0; i < VA; ++i) {
+          bool ok = k < ke;
+          const int64_t off = a_offset<MODE>(c, prow[i], t, ok);
+          ra[i] = ld4(Asrc + off);
+          amask |= (ok ? 0xFu : 0u) << (4 * i);
+        }
       } else {
-        const int kr = vi / (BM / 4), mq = (vi % (BM / 4)) * 4;
-        ra[i] = load_a4<MODE>(cc, m0 + mq, k0 + kr, false);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t ke_ = k + e;
+          const Tap t = split_tap(ke_ < ke ? ke_ : 0, Cch, c.KW);
+#pragma unroll
+          for (int i = 0; i < VA; ++i) {
+            bool ok = ke_ < ke;
+            const int64_t off = a_offset<MODE>(c, prow[i], t, ok);
+            ra[i][e] = Asrc[off];
+            amask |= (ok ? 1u : 0u) << (4 * i + e);
+          }
+        }
+      }
+    } else {     // wgrad: 4 consecutive taps m (channels ch .. ch+3) at pixel k
+#pragma unroll
+      for (int i = 0; i < VA; ++i) {
+        const int64_t k = k0 + (tid + i * NT) / (BM / 4);
+        const Pix p = split_pix(k < ke ? k : 0, c.K, Hh, Ww);
+        if (VEC) {
+          bool ok = k < ke && m0 + aq < c.M;
+          const int64_t off = a_offset<MODE>(c, p, mtap[0], ok);
+          ra[i] = ld4(Asrc + off);
+          amask |= (ok ? 0xFu : 0u) << (4 * i);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            bool ok = k < ke && m0 + aq + e < c.M;
+            const int64_t off = a_offset<MODE>(c, p, mtap[e], ok);
+            ra[i][e] = Asrc[off];
+            amask |= (ok ? 1u : 0u) << (4 * i + e);
+          }
+        }
       }
     }
+    // B [K][N] row-major, float4 along n: rows clamped (k >= ke zeroed at store), columns clamped
+    // (columns >= N only feed output columns that are never stored)
 #pragma unroll
     for (int i = 0; i < VB; ++i) {
       const int vi = tid + i * NT;
-      const int kr = vi / (BN / 4), nq = (vi % (BN / 4)) * 4;
-      rb[i] = load_b4(Bmat, c.Nn, k0 + kr, n0 + nq, ke, c.Nn, vec_b);
+      const int64_t k = k0 + vi / (BN / 4), n = n0 + (vi % (BN / 4)) * 4;
+      const float* q = Bsrc + (k < ke ? k : ke - 1) * c.Nn;
+      if (VECB) {
+        rb[i] = ld4(q + (n < c.Nn ? n : c.Nn - 4));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) rb[i][e] = q[n + e < c.Nn ? n + e : c.Nn - 1];
+      }
+      bmask |= (k < ke ? 1u : 0u) << i;
     }
   };
   auto store_tile = [&](int buf) {
+    float* As = smem + buf * (IA::FLOATS + IB::FLOATS);
+    float* Bs = As + IA::FLOATS;
 #pragma unroll
     for (int i = 0; i < VA; ++i) {
-      const int vi = tid + i * NT;
-      if (!A_ALONG_M) {
-        const int row = vi / (BK / 4), kq = (vi % (BK / 4)) * 4;
+      v4f v = ra[i];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) As[buf][kq + q][row] = ra[i][q];
-      } else {
-        const int kr = vi / (BM / 4), mq = (vi % (BM / 4)) * 4;
-        *reinterpret_cast<v4f*>(&As[buf][kr][mq]) = ra[i];
-      }
+      for (int e = 0; e < 4; ++e) v[e] = (amask >> (4 * i + e)) & 1u ? v[e] : 0.f;
+      st4(As + IA::store_off(tid + i * NT), v);
     }
 #pragma unroll
     for (int i = 0; i < VB; ++i) {
-      const int vi = tid + i * NT;
-      const int kr = vi / (BN / 4), nq = (vi % (BN / 4)) * 4;
-      *reinterpret_cast<v4f*>(&Bs[buf][kr][nq]) = rb[i];
+      const v4f v = (bmask >> i) & 1u ? rb[i] : v4f{0.f, 0.f, 0.f, 0.f};
+      st4(Bs + IB::store_off(tid + i * NT), v);
     }
   };
 
@@ -211,51 +208,38 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int64_t nk = ke > kb ? (ke - kb + BK - 1) / BK : 0;
-  const int lk = lane >> 5, lc = lane & 31;
+  const int64_t nk = ke > kb0 ? (ke - kb0 + BK - 1) / BK : 0;
   if (nk > 0) {
-    load_tile(kb);
+    load_tile(kb0);
     store_tile(0);
   }
   __syncthreads();
   for (int64_t kt = 0; kt < nk; ++kt) {
     const int cur = (int)(kt & 1);
-    if (kt + 1 < nk) load_tile(kb + (kt + 1) * BK);
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      float a[TM], b[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = As[cur][kk + lk][wm0 + i * 32 + lc];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = Bs[cur][kk + lk][wn0 + j * 32 + lc];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 1 < nk) load_tile(kb0 + (kt + 1) * BK);
+    const float* As = smem + cur * (IA::FLOATS + IB::FLOATS);
+    mma_stage<IA, IB, TM, TN, BK>(As, As + IA::FLOATS, acc, wm0, wn0, lane);
+    asm volatile("" ::: "memory");      // keep the stage-k+1 LDS store (and its vmcnt wait)
+    __builtin_amdgcn_sched_barrier(0);   // after this stage's MFMAs
     if (kt + 1 < nk) store_tile(cur ^ 1);
     __syncthreads();
   }
 
+  const int lh = lane >> 5, lc = lane & 31;
+  // epilogue.  32x32 accumulator: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int64_t col = n0 + wn0 + j * 32 + lc;
       if (col >= c.Nn) continue;
+      const float bv = (MODE == kFwd && c.bias && !c.partial) ? c.bias[col] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        const int64_t row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         if (row >= c.M) continue;
-        float v = acc[i][j][r];
-        if (c.partial) {
-          c.partial[((int64_t)split * c.M + row) * c.Nn + col] = v;
-        } else {
-          if (MODE == kFwd && c.bias) v += c.bias[col];
-          c.out[row * c.Nn + col] = v;
-        }
+        if (c.partial) c.partial[((int64_t)split * c.M + row) * c.Nn + col] = acc[i][j][r];
+        else c.out[row * c.Nn + col] = acc[i][j][r] + bv;
       }
     }
   }
@@ -301,48 +285,65 @@ __global__ void weight_grad_layout_kernel(const float* __restrict__ dwt, int Co,
 
 // ------------------------------------------------------------------ max pooling (NHWC)
 // window = stride = (kh, kw), floor mode (nn.MaxPool2d((1,3)), MaxPool1d(98) as (98,1)).
-// Backward routes each output gradient to the FIRST maximum of its window (PyTorch's rule).
+// Backward routes each output gradient to the FIRST maximum of its window (PyTorch's rule); a
+// NaN wins its window.  One thread = 4 consecutive channels of one output pixel (16-B accesses;
+// C % 4 == 0 — every pooled layer of the reference models).
+__device__ __forceinline__ bool takes(float v, float m, bool first) { return first || v > m || (v != v && m == m); }
+
 __global__ void maxpool_fwd_kernel(const float* __restrict__ x, int N, int H, int W, int C, int kh, int kw,
                                    float* __restrict__ y) {
-  const int Ho = H / kh, Wo = W / kw;
+  const int Ho = H / kh, Wo = W / kw, C4 = C / 4;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n_out = (int64_t)N * Ho * Wo * C;
+  const int64_t n_out = (int64_t)N * Ho * Wo * C4;
   if (i >= n_out) return;
-  const int c = (int)(i % C);
-  int64_t t = i / C;
+  const int c = (int)(i % C4) * 4;
+  int64_t t = i / C4;
   const int wo = (int)(t % Wo);
   t /= Wo;
   const int ho = (int)(t % Ho), n = (int)(t / Ho);
-  float m = -INFINITY;
+  v4f m = {0.f, 0.f, 0.f, 0.f};
+  bool first = true;
   for (int a = 0; a < kh; ++a)
     for (int b = 0; b < kw; ++b) {
-      const float v = x[(((int64_t)n * H + ho * kh + a) * W + wo * kw + b) * C + c];
-      if (v > m || v != v) m = v;
+      const v4f v = ld4(x + (((int64_t)n * H + ho * kh + a) * W + wo * kw + b) * C + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m[e] = takes(v[e], m[e], first) ? v[e] : m[e];
+      first = false;
     }
-  y[i] = m;
+  st4(y + i * 4, m);
 }
 
 __global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy, int N, int H, int W,
                                    int C, int kh, int kw, float* __restrict__ dx) {
-  const int Ho = H / kh, Wo = W / kw;
+  const int Ho = H / kh, Wo = W / kw, C4 = C / 4;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n_out = (int64_t)N * Ho * Wo * C;
+  const int64_t n_out = (int64_t)N * Ho * Wo * C4;
   if (i >= n_out) return;
-  const int c = (int)(i % C);
-  int64_t t = i / C;
+  const int c = (int)(i % C4) * 4;
+  int64_t t = i / C4;
   const int wo = (int)(t % Wo);
   t /= Wo;
   const int ho = (int)(t % Ho), n = (int)(t / Ho);
-  float m = -INFINITY;
-  int64_t arg = -1;
+  v4f m = {0.f, 0.f, 0.f, 0.f};
+  int arg[4] = {0, 0, 0, 0};
+  bool first = true;
   for (int a = 0; a < kh; ++a)
     for (int b = 0; b < kw; ++b) {
-      const int64_t idx = (((int64_t)n * H + ho * kh + a) * W + wo * kw + b) * C + c;
-      const float v = x[idx];
-      if (arg < 0 || v > m || (v != v && m == m)) { m = v; arg = idx; }
-      dx[idx] = 0.f;
+      const v4f v = ld4(x + (((int64_t)n * H + ho * kh + a) * W + wo * kw + b) * C + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (takes(v[e], m[e], first)) { m[e] = v[e]; arg[e] = a * kw + b; }
+      first = false;
     }
-  dx[arg] = dy[i];
+  const v4f g = ld4(dy + i * 4);
+  for (int a = 0; a < kh; ++a)
+    for (int b = 0; b < kw; ++b) {
+      const int q = a * kw + b;
+      v4f o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = arg[e] == q ? g[e] : 0.f;
+      st4(dx + (((int64_t)n * H + ho * kh + a) * W + wo * kw + b) * C + c, o);
+    }
 }
 
 __global__ void zero_kernel(float* __restrict__ p, int64_t n) {
@@ -374,29 +375,46 @@ int conv_scratch(size_t floats, float** out) {
   return SRK_OK;
 }
 
+template <int MODE, int BM, int BN>
+void launch_conv(const ConvArgs& c, dim3 grid, hipStream_t s, bool vec, bool vecb) {
+  if (vec && vecb) hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, 32, true, true>), grid, dim3(256), 0, s, c);
+  else if (vecb) hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, 32, false, true>), grid, dim3(256), 0, s, c);
+  else hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, 32, false, false>), grid, dim3(256), 0, s, c);
+}
+
 template <int MODE>
 int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
   constexpr int BK = 32;
-  const bool big = ((c.M + 127) / 128) * ((c.Nn + 127) / 128) >= 128;
-  const int BM = big ? 128 : 64, BN = big ? 128 : 64;
+  // tile: 128 x 128 unless the GEMM is narrow (N <= 64: 128 x 64) or small (64 x 64)
+  int BM = 128, BN = c.Nn <= 64 ? 64 : 128;
+  if (((c.M + 127) / 128) * ((c.Nn + BN - 1) / BN) < 64 && c.K < 2048) { BM = 64; BN = 64; }
   const int64_t tm = (c.M + BM - 1) / BM, tn = (c.Nn + BN - 1) / BN;
+  SRK_REQUIRE(tm * tn <= (INT32_MAX >> 9), SRK_ERR_INVALID, "conv: grid too large");
+  const int lds = 2 * 4 * ((MODE != kWgrad ? BM * (BK + 4) : BK * (BM + 8)) + BK * (BN + 8));
+  const int64_t slots = (int64_t)kCUs * std::min(8, (160 * 1024) / lds);
+  // weight-gradient GEMMs reduce over every pixel (K up to millions) onto a few hundred tiles:
+  // allow deep splits there (deterministic slab reduction)
+  const int splits0 = choose_splits(tm * tn, c.K, BK, slots, MODE == kWgrad ? 256 : 16);
+  c.kchunk = splits0 > 1 ? ((c.K + splits0 - 1) / splits0 + BK - 1) / BK * BK : std::max<int64_t>(c.K, 1);
+  const int splits = splits0 > 1 ? (int)((c.K + c.kchunk - 1) / c.kchunk) : 1;
+  c.tiles_m = (int)tm;
   c.tiles_n = (int)tn;
-  int splits = 1;
-  if (tm * tn < 256 && c.K >= 16 * BK) {
-    splits = (int)std::min<int64_t>((1024 + tm * tn - 1) / (tm * tn), c.K / (8 * BK));
-    splits = std::max(1, std::min(splits, 256));
-  }
-  c.kchunk = splits > 1 ? ((c.K + splits - 1) / splits + BK - 1) / BK * BK : std::max<int64_t>(c.K, 1);
-  if (splits > 1) splits = (int)((c.K + c.kchunk - 1) / c.kchunk);
+  c.tiles = (int)(tm * tn);
+  c.nblk = c.tiles * splits;
+  c.group_m = 8;
   c.partial = nullptr;
   float* final_out = c.out;
   if (splits > 1) {
     if (int rc = conv_scratch((size_t)splits * c.M * c.Nn, &c.partial)) return rc;
   }
+  const int chans = MODE == kDgrad ? c.Co : c.Ci;
+  const bool vecb = c.Nn % 4 == 0;
+  const bool vec = (chans % 4 == 0) && vecb;
   ProfScope prof(name, s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
-  const dim3 grid((unsigned)(tm * tn), (unsigned)splits);
-  if (big) hipLaunchKernelGGL((conv_gemm_kernel<MODE, 128, 128, BK>), grid, dim3(256), 0, s, c);
-  else hipLaunchKernelGGL((conv_gemm_kernel<MODE, 64, 64, BK>), grid, dim3(256), 0, s, c);
+  const dim3 grid((unsigned)c.nblk);
+  if (BM == 64) launch_conv<MODE, 64, 64>(c, grid, s, vec, vecb);
+  else if (BN == 64) launch_conv<MODE, 128, 64>(c, grid, s, vec, vecb);
+  else launch_conv<MODE, 128, 128>(c, grid, s, vec, vecb);
   SRK_CHECK_HIP(hipGetLastError());
   if (splits > 1) {
     const int64_t n = c.M * c.Nn;
@@ -460,7 +478,21 @@ int srk_conv2d_nhwc_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t
   c.KH = (int)KH; c.KW = (int)KW; c.ph = (int)ph; c.pw = (int)pw; c.sh = (int)sh; c.sw = (int)sw;
   c.x = x; c.dy = dy;
   int rc;
-  if (dx) {
+  if (dx && KH == 1 && ph == 0 && sh == 1 && pw == 0 && KW == W && Wo == 1) {
+    // A full-width "valid" conv (model_fbanks_cnn.py:74, conv3 1x10 on width 10): every input
+    // column meets exactly one tap, so the data gradient is the plain GEMM
+    //   dX[(n,h)][(kw,ci)] = dY[(n,h)][co] * Wt[(kw,ci)][co]^T
+    // instead of an implicit GEMM whose k range is 90 % structurally-zero taps.
+    hipLaunchKernelGGL(srk::weight_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, (int)Co,
+                       (int)Ci, (int)KH, (int)KW, 0, ws);
+    srk::GemmDesc g;
+    g.M = N * H; g.N = KW * Ci; g.K = Co;
+    g.A = dy; g.lda = Co;
+    g.B = ws; g.ldb = Co; g.tb = true;
+    g.C = dx; g.ldc = KW * Ci;
+    srk::ProfScope prof("conv_dgrad", s, 2.0 * (double)g.M * (double)g.N * (double)g.K);
+    if ((rc = srk::gemm_f32(g, s))) return rc;
+  } else if (dx) {
     hipLaunchKernelGGL(srk::weight_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, (int)Co,
                        (int)Ci, (int)KH, (int)KW, 1, ws);
     srk::ConvArgs d = c;
@@ -486,9 +518,11 @@ int srk_maxpool_nhwc_fwd(const float* x, int64_t N, int64_t H, int64_t W, int64_
                          float* y, void* stream) {
   SRK_API_BEGIN
   SRK_REQUIRE(x && y && N > 0 && C > 0 && kh > 0 && kw > 0 && H >= kh && W >= kw, SRK_ERR_INVALID, "maxpool: bad args");
+  SRK_REQUIRE(C % 4 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0, SRK_ERR_INVALID,
+              "maxpool: channels must be a multiple of 4 and tensors 16-B aligned");
   const int64_t n = N * (H / kh) * (W / kw) * C;
   srk::ProfScope prof("maxpool_fwd", srk::as_stream(stream), 4.0 * (N * H * W * C + n));
-  hipLaunchKernelGGL(srk::maxpool_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, srk::as_stream(stream), x,
+  hipLaunchKernelGGL(srk::maxpool_fwd_kernel, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, srk::as_stream(stream), x,
                      (int)N, (int)H, (int)W, (int)C, (int)kh, (int)kw, y);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
@@ -500,6 +534,8 @@ int srk_maxpool_nhwc_bwd(const float* x, const float* dy, int64_t N, int64_t H, 
   SRK_API_BEGIN
   SRK_REQUIRE(x && dy && dx && N > 0 && C > 0 && kh > 0 && kw > 0 && H >= kh && W >= kw, SRK_ERR_INVALID,
               "maxpool bwd: bad args");
+  SRK_REQUIRE(C % 4 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)dy % 16 == 0 && (uintptr_t)dx % 16 == 0,
+              SRK_ERR_INVALID, "maxpool bwd: channels must be a multiple of 4 and tensors 16-B aligned");
   hipStream_t s = srk::as_stream(stream);
   const int64_t Ho = H / kh, Wo = W / kw;
   const int64_t n = N * Ho * Wo * C;
@@ -508,7 +544,7 @@ int srk_maxpool_nhwc_bwd(const float* x, const float* dy, int64_t N, int64_t H, 
     hipLaunchKernelGGL(srk::zero_kernel, dim3((unsigned)((all + 255) / 256)), dim3(256), 0, s, dx, all);
   }
   srk::ProfScope prof("maxpool_bwd", s, 4.0 * (2 * N * H * W * C + n));
-  hipLaunchKernelGGL(srk::maxpool_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, dy, (int)N, (int)H,
+  hipLaunchKernelGGL(srk::maxpool_bwd_kernel, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, s, x, dy, (int)N, (int)H,
                      (int)W, (int)C, (int)kh, (int)kw, dx);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;

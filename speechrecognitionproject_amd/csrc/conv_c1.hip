@@ -1,0 +1,243 @@
+// K6 fused first layer of model_fbanks_cnn (models/model_fbanks_cnn.py:72-73,89-90):
+//   conv1 = Conv2d(1, 64, (7, 3), padding=(3, 1)) + bias, then MaxPool2d((1, 3)),
+// as ONE pass over the [N, 98, 120] fbank image instead of an implicit GEMM that writes the
+// 1.5 GB (B = 512) pre-pool activation and a pooling kernel that reads it back.
+//
+// Forward  : each output pixel's 21-tap dot product on the VALU (a single input channel gives a
+//            K = 21 GEMM that the matrix cores cannot use well), max over the pool window in
+//            registers; writes the pooled activation [N][H][W/3][64] and the window argmax (uint8,
+//            PyTorch's first-maximum rule, NaN wins) that the backward needs.
+// Backward : the pooled gradient routes to exactly one pixel per (window, channel) (the argmax),
+//            so dW[co][kh][kw] = sum_q dP[q][co] * x[pixel*(q, co) + tap] and db[co] = sum_q dP[q][co]
+//            are accumulated straight from dP — the dense 1.5 GB unpooled gradient is never formed.
+//            Per-block partial sums are reduced in a fixed order (deterministic).
+// The input needs no gradient (it is the feature tensor, computed under no_grad).
+#include "srk_internal.h"
+
+namespace srk {
+namespace {
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+constexpr int kCo = 64;              // output channels (model_fbanks_cnn.py:72)
+constexpr int kC4 = kCo / 4;         // threads per pixel group (4 channels each)
+constexpr int kPG = 256 / kC4;       // pixel groups per block
+constexpr int kRows = 2;             // image rows per block (per grid-stride step)
+constexpr int kWgradBlocks = 1024;   // persistent blocks of the backward (partials: 5.8 MB)
+
+struct C1Args {
+  int N, H, W, ph, pw;
+  const float* x;      // [N][H][W]
+  const float* w;      // [64][1][KH][KW] (torch layout)
+  const float* bias;   // [64]
+  float* y;            // fwd: pooled [N][H][W/PW][64]
+  uint8_t* arg;        // [N][H][W/PW][64] window argmax
+  const float* dy;     // bwd: pooled gradient [N][H][W/PW][64]
+  float* partial;      // bwd: [blocks][64 * (KH*KW + 1)]
+};
+
+__device__ __forceinline__ bool takes(float v, float m, bool first) { return first || v > m || (v != v && m == m); }
+
+// x rows [h0 - ph, h0 + kRows - 1 + KH - 1 - ph], cols [-pw, W - 1 + KW - 1 - pw] -> LDS, zero padded
+template <int KH, int KW>
+__device__ __forceinline__ void load_patch(const C1Args& a, int n, int h0, float* patch, int pitch) {
+  constexpr int PR = kRows + KH - 1;
+  const int PC = a.W + KW - 1;
+  for (int i = threadIdx.x; i < PR * PC; i += 256) {
+    const int r = i / PC, cidx = i % PC;
+    const int h = h0 - a.ph + r, w = cidx - a.pw;
+    patch[r * pitch + cidx] = (h >= 0 && h < a.H && w >= 0 && w < a.W) ? a.x[((size_t)n * a.H + h) * a.W + w] : 0.f;
+  }
+}
+
+template <int KH, int KW, int PW>
+__global__ __launch_bounds__(256) void conv1_pool_fwd_kernel(C1Args a) {
+  constexpr int T = KH * KW;
+  extern __shared__ float patch[];
+  const int pitch = a.W + KW - 1 + 1;
+  const int c4 = threadIdx.x % kC4, pg = threadIdx.x / kC4;
+  const int hp = (a.H + kRows - 1) / kRows;
+  const int n = blockIdx.x / hp, h0 = (blockIdx.x % hp) * kRows;
+  load_patch<KH, KW>(a, n, h0, patch, pitch);
+  v4f wr[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wr[t][e] = a.w[(c4 * 4 + e) * T + t];
+  v4f bv;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) bv[e] = a.bias[c4 * 4 + e];
+  __syncthreads();
+  const int Wq = a.W / PW;
+  const int rows = min(kRows, a.H - h0);
+  for (int wi = pg; wi < rows * Wq; wi += kPG) {
+    const int r = wi / Wq, wq = wi % Wq;
+    v4f best = {0.f, 0.f, 0.f, 0.f};
+    unsigned idx = 0;
+#pragma unroll
+    for (int p = 0; p < PW; ++p) {
+      const int col = wq * PW + p;
+      v4f acc = bv;
+#pragma unroll
+      for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < KW; ++kw) {
+          const float xv = patch[(r + kh) * pitch + col + kw];
+          acc += xv * wr[kh * KW + kw];
+        }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (takes(acc[e], best[e], p == 0)) {
+          best[e] = acc[e];
+          idx = (idx & ~(0xFFu << (8 * e))) | ((unsigned)p << (8 * e));
+        }
+    }
+    const size_t o = (((size_t)n * a.H + h0 + r) * Wq + wq) * kCo + c4 * 4;
+    *reinterpret_cast<v4f*>(a.y + o) = best;
+    *reinterpret_cast<unsigned*>(a.arg + o) = idx;
+  }
+}
+
+template <int KH, int KW, int PW>
+__global__ __launch_bounds__(256) void conv1_pool_wgrad_kernel(C1Args a) {
+  constexpr int T = KH * KW;
+  extern __shared__ float smem[];
+  float* patch = smem;
+  const int pitch = a.W + KW - 1 + 1;
+  const int c4 = threadIdx.x % kC4, pg = threadIdx.x / kC4;
+  const int hp = (a.H + kRows - 1) / kRows;
+  const int Wq = a.W / PW;
+  v4f acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
+  v4f dbacc = {0.f, 0.f, 0.f, 0.f};
+  for (int blk = blockIdx.x; blk < a.N * hp; blk += gridDim.x) {
+    const int n = blk / hp, h0 = (blk % hp) * kRows;
+    __syncthreads();   // previous patch fully consumed
+    load_patch<KH, KW>(a, n, h0, patch, pitch);
+    __syncthreads();
+    const int rows = min(kRows, a.H - h0);
+    for (int wi = pg; wi < rows * Wq; wi += kPG) {
+      const int r = wi / Wq, wq = wi % Wq;
+      const size_t o = (((size_t)n * a.H + h0 + r) * Wq + wq) * kCo + c4 * 4;
+      const v4f g = *reinterpret_cast<const v4f*>(a.dy + o);
+      const unsigned idx = *reinterpret_cast<const unsigned*>(a.arg + o);
+      dbacc += g;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int col = wq * PW + (int)((idx >> (8 * e)) & 0xFFu);
+        const float* pp = patch + r * pitch + col;
+#pragma unroll
+        for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < KW; ++kw) acc[kh * KW + kw][e] = fmaf(g[e], pp[kh * pitch + kw], acc[kh * KW + kw][e]);
+      }
+    }
+  }
+  // Reduce the kPG pixel groups of each channel quad (fixed order): the 4 groups of a wave with
+  // xor-shuffles (lanes c4, c4+16, c4+32, c4+48), then the 4 waves through LDS.  One partial row
+  // [64 x (T + 1)] per block.
+  constexpr int S = (T + 1) * 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int t = 0; t <= T; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = t < T ? acc[t][e] : dbacc[e];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (t < T) acc[t][e] = v; else dbacc[e] = v;
+    }
+  __syncthreads();   // patch reads done
+  float* red = smem;   // [4 waves][kC4][T + 1][4]
+  if (lane < kC4) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) *reinterpret_cast<v4f*>(red + ((wave * kC4 + c4) * (T + 1) + t) * 4) = acc[t];
+    *reinterpret_cast<v4f*>(red + ((wave * kC4 + c4) * (T + 1) + T) * 4) = dbacc;
+  }
+  __syncthreads();
+  float* out = a.partial + (size_t)blockIdx.x * kCo * (T + 1);
+  for (int i = threadIdx.x; i < kC4 * S; i += 256) {   // i = (c4, t, e)
+    const float s = (red[i] + red[kC4 * S + i]) + (red[2 * kC4 * S + i] + red[3 * kC4 * S + i]);
+    const int cq = i / S, rem = i % S, t = rem / 4, e = rem % 4;
+    out[(cq * 4 + e) * (T + 1) + t] = s;   // [co][t], t == T -> bias
+  }
+}
+
+// dw[co][t] = sum over blocks (in block order); db[co] likewise
+__global__ void conv1_pool_reduce_kernel(const float* __restrict__ partial, int blocks, int T, float* __restrict__ dw,
+                                         float* __restrict__ db) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int per = kCo * (T + 1);
+  if (i >= per) return;
+  float s = 0.f;
+  for (int b = 0; b < blocks; ++b) s += partial[(size_t)b * per + i];
+  const int co = i / (T + 1), t = i % (T + 1);
+  if (t < T) dw[co * T + t] = s;
+  else if (db) db[co] = s;
+}
+
+int check_c1(int64_t N, int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t pool) {
+  SRK_REQUIRE(Co == kCo && KH == 7 && KW == 3 && pool == 3 && ph == 3 && pw == 1, SRK_ERR_INVALID,
+              "conv1_pool: only the model_fbanks_cnn conv1 geometry (Co 64, 7x3, pad (3,1), pool (1,3)) is fused");
+  SRK_REQUIRE(N > 0 && H > 0 && W >= pool && N * H * W < ((int64_t)1 << 31), SRK_ERR_INVALID, "conv1_pool: bad dims");
+  return SRK_OK;
+}
+
+}  // namespace
+}  // namespace srk
+
+extern "C" {
+
+int64_t srk_conv1_pool_workspace_floats(int64_t Co, int64_t KH, int64_t KW) {
+  return (int64_t)srk::kWgradBlocks * Co * (KH * KW + 1);
+}
+
+int srk_conv1_pool_fwd(const float* x, int64_t N, int64_t H, int64_t W, const float* w, const float* bias, int64_t Co,
+                       int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t pool, float* y, uint8_t* argmax,
+                       void* stream) {
+  SRK_API_BEGIN
+  if (int rc = srk::check_c1(N, H, W, Co, KH, KW, ph, pw, pool)) return rc;
+  SRK_REQUIRE(x && w && bias && y && argmax, SRK_ERR_INVALID, "conv1_pool_fwd: null pointer");
+  SRK_REQUIRE((uintptr_t)y % 16 == 0 && (uintptr_t)argmax % 4 == 0, SRK_ERR_INVALID, "conv1_pool_fwd: misaligned output");
+  srk::C1Args a{};
+  a.N = (int)N; a.H = (int)H; a.W = (int)W; a.ph = (int)ph; a.pw = (int)pw;
+  a.x = x; a.w = w; a.bias = bias; a.y = y; a.arg = argmax;
+  hipStream_t s = srk::as_stream(stream);
+  const int hp = (int)((H + srk::kRows - 1) / srk::kRows);
+  const size_t lds = (size_t)(srk::kRows + KH - 1) * (W + KW) * 4;
+  // algorithmic: the input image once + pooled output + argmax
+  srk::ProfScope prof("conv1_pool_fwd", s, 4.0 * N * H * W + 5.0 * N * H * (W / pool) * Co);
+  hipLaunchKernelGGL((srk::conv1_pool_fwd_kernel<7, 3, 3>), dim3((unsigned)(N * hp)), dim3(256), lds, s, a);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_conv1_pool_wgrad(const float* x, int64_t N, int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW,
+                         int64_t ph, int64_t pw, int64_t pool, const float* dy, const uint8_t* argmax, float* dw,
+                         float* db, float* ws, void* stream) {
+  SRK_API_BEGIN
+  if (int rc = srk::check_c1(N, H, W, Co, KH, KW, ph, pw, pool)) return rc;
+  SRK_REQUIRE(x && dy && argmax && dw && ws, SRK_ERR_INVALID, "conv1_pool_wgrad: null pointer");
+  srk::C1Args a{};
+  a.N = (int)N; a.H = (int)H; a.W = (int)W; a.ph = (int)ph; a.pw = (int)pw;
+  a.x = x; a.dy = dy; a.arg = const_cast<uint8_t*>(argmax); a.partial = ws;
+  hipStream_t s = srk::as_stream(stream);
+  const int T = (int)(KH * KW);
+  const int hp = (int)((H + srk::kRows - 1) / srk::kRows);
+  const int blocks = (int)std::min<int64_t>(srk::kWgradBlocks, N * hp);
+  const size_t patch = (size_t)(srk::kRows + KH - 1) * (W + KW) * 4;
+  const size_t red = (size_t)4 * srk::kC4 * (T + 1) * 4 * 4;
+  srk::ProfScope prof("conv1_pool_wgrad", s, 4.0 * N * H * W + 5.0 * N * H * (W / pool) * Co);
+  hipLaunchKernelGGL((srk::conv1_pool_wgrad_kernel<7, 3, 3>), dim3((unsigned)blocks), dim3(256), std::max(patch, red), s,
+                     a);
+  const int per = (int)(Co * (T + 1));
+  hipLaunchKernelGGL(srk::conv1_pool_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, ws, blocks, T,
+                     dw, db);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+}  // extern "C"

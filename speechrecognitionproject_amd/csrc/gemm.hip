@@ -17,15 +17,12 @@
 #include <mutex>
 
 #include "gemm.h"
+#include "mfma_tile.h"
 
 namespace srk {
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-typedef float v4f __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ v4f ld4(const float* p) { return *reinterpret_cast<const v4f*>(p); }
-__device__ __forceinline__ void st4(float* p, v4f v) { *reinterpret_cast<v4f*>(p) = v; }
+using namespace tile;
 
 struct KernelArgs {
   GemmDesc d;
@@ -37,25 +34,6 @@ struct KernelArgs {
   int64_t kchunk;        // K range per split (a multiple of BK)
   float* partial;        // [splits][M][N] when split
   float* rs_partial;     // [splits][M] when split and rowsum requested
-};
-
-// LDS images (pitches in floats, all multiples of 4 so every 16-B store is aligned):
-//   operand stored k-contiguous in HBM (A when !TA, B when TB): [row][BK + 4]   (float4 along k)
-//   operand stored row-contiguous (A when TA, B when !TB):      [BK][rows + 8]   (float4 along rows)
-// MFMA 32x32x2 operand = element (row = lane & 31, k = lane >> 5).  The k order is permuted per
-// 8-deep block: sub-step s (0..3) of block kb gives lanes of half h the real k = 8 kb + 4 h + s, the
-// same for A and B (any fixed permutation of k is a valid summation order), so a k-contiguous image
-// feeds 4 MFMAs from ONE ds_read_b128 per operand, and a row-contiguous image from 4 ds_read_b32 at
-// a pitch (rows + 8) that puts the two lane halves on disjoint banks.
-template <bool KC, int ROWS, int BK>
-struct Img {
-  static constexpr int P = KC ? BK + 4 : ROWS + 8;
-  static constexpr int FLOATS = KC ? ROWS * P : BK * P;
-  __device__ static __forceinline__ v4f frag(const float* s, int row, int kb, int h) {
-    if (KC) return ld4(s + row * P + kb * 8 + 4 * h);
-    const float* q = s + (kb * 8 + 4 * h) * P + row;
-    return v4f{q[0], q[P], q[2 * P], q[3 * P]};
-  }
 };
 
 template <bool TA, bool TB, int BM, int BN, int BK, bool VEC>
@@ -71,23 +49,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(KernelArgs ka) {
   const GemmDesc& d = ka.d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-  // Block -> (split, tile) map.  Workgroups are dealt round-robin over the 8 XCDs (block b and
-  // b + 8 share an XCD; speed only, never correctness), so consecutive LOGICAL tiles are given to
-  // blocks of ONE XCD: the tiles an XCD runs concurrently then share A and B panels in its L2
-  // instead of every XCD fetching every panel.  Within a split, tiles are walked in groups of
-  // group_m tile rows (column-major inside a group) so resident tiles form a compact 2-D patch.
-  int lin = blockIdx.x;
-  if (ka.remap) {
-    const int b = blockIdx.x, xcd = b & 7, q = ka.nblk >> 3, r = ka.nblk & 7;
-    lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-  }
-  const int split = lin / ka.tiles;
-  const int t = lin - split * ka.tiles;
-  const int gsz_full = ka.group_m * ka.tiles_n;
-  const int grp = t / gsz_full, first_m = grp * ka.group_m;
-  const int gm = ka.tiles_m - first_m < ka.group_m ? ka.tiles_m - first_m : ka.group_m;
-  const int tin = t - grp * gsz_full;
-  const int tm = first_m + tin % gm, tn = tin / gm;
+  int split, tm, tn;
+  map_tile(ka.nblk, ka.tiles, ka.tiles_m, ka.tiles_n, ka.group_m, ka.remap != 0, split, tm, tn);
 
   const int64_t z = blockIdx.z;
   const float* __restrict__ A = d.A + z * d.sA;
@@ -188,28 +151,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(KernelArgs ka) {
     if (kt + 1 < nk) load_tile(kb0 + (kt + 1) * BK);
     const float* As = smem + cur * (IA::FLOATS + IB::FLOATS);
     const float* Bs = As + IA::FLOATS;
-    v4f fa[2][TM], fb[2][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) fa[0][i] = IA::frag(As, wm0 + i * 32 + lc, 0, lh);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) fb[0][j] = IB::frag(Bs, wn0 + j * 32 + lc, 0, lh);
-#pragma unroll
-    for (int kb = 0; kb < BK / 8; ++kb) {
-      const int c = kb & 1;
-      if (kb + 1 < BK / 8) {   // fragments of the next 8-deep block ahead of this block's MFMAs
-#pragma unroll
-        for (int i = 0; i < TM; ++i) fa[c ^ 1][i] = IA::frag(As, wm0 + i * 32 + lc, kb + 1, lh);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) fb[c ^ 1][j] = IB::frag(Bs, wn0 + j * 32 + lc, kb + 1, lh);
-      }
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[c][i][s], fb[c][j][s], acc[i][j], 0, 0, 0);
-    }
+    mma_stage<IA, IB, TM, TN, BK>(As, Bs, acc, wm0, wn0, lane);
     if (do_rs) {
 #pragma unroll
       for (int k = tid / BM; k < BK; k += RSP)
@@ -339,8 +281,6 @@ int get_scratch(size_t floats, float** out) {
 }
 
 // Resident workgroups per CU for the 256-thread, 2 x (BK x BM + BK x BN) fp32 LDS tile kernels.
-constexpr int kCUs = 256;
-
 int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : dflt;
@@ -361,24 +301,9 @@ int launch(const GemmDesc& d, hipStream_t s, bool vec) {
   ka.tiles = (int)(tm * tn);
   ka.group_m = 8;
   ka.remap = remap;
-  // Split K when the output grid leaves resident slots idle and K is long: pick the split count
-  // (<= 16, >= 4 k-tiles per split) whose last round of workgroups is fullest, preferring fewer splits
-  // (each split adds an M x N fp32 partial slab write + read).
-  int splits = 1;
-  const int64_t tiles = tm * tn * d.batch;
-  if (d.batch == 1 && d.K >= 16 * BK) {
-    auto eff = [&](int64_t sp) {
-      const int64_t w = tiles * sp, rounds = (w + slots - 1) / slots;
-      return (double)w / (double)(rounds * slots);
-    };
-    double best = eff(1);
-    const int64_t smax = std::min<int64_t>(16, d.K / (4 * BK));
-    for (int64_t sp = 2; sp <= smax; ++sp) {
-      const double e = eff(sp);
-      // a split must buy >= 10 % more filled slots to pay for its slab traffic
-      if (e > best * 1.10 + 1e-9 && tiles * sp <= 4 * slots) { best = e; splits = (int)sp; }
-    }
-  }
+  // Split K when the output grid leaves resident slots idle and K is long (tile::choose_splits).
+  const int splits0 = d.batch == 1 ? choose_splits(tm * tn, d.K, BK, slots, 16) : 1;
+  int splits = splits0;
   ka.kchunk = splits > 1 ? ((d.K + splits - 1) / splits + BK - 1) / BK * BK : std::max<int64_t>(d.K, 1);
   if (splits > 1) splits = (int)((d.K + ka.kchunk - 1) / ka.kchunk);
   ka.nblk = ka.tiles * splits;

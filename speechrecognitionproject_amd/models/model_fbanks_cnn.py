@@ -3,14 +3,15 @@
 -> max over time -> dropout -> fc1 -> fc2, no nonlinearities (model_fbanks_cnn.py:68-147).
 
 Same constructor, ``state_dict`` keys/shapes and helpers.  The per-clip CPU ``filter_banks`` loop
-(:84-87) becomes one batched HIP launch (K2); the convolutions run as channels-last implicit GEMMs
-on the matrix cores (K6), so the [B, 98, 120] fbank tensor is already the NHWC input (C = 1).
+(:84-87) becomes one batched HIP launch (K2); conv1 + maxpool1 run as one fused one-channel kernel
+(srk_conv1_pool_*: the pre-pool activation is never written), conv2-4 as channels-last implicit GEMMs
+on the matrix cores (K6).
 """
 import torch
 import torch.nn as nn
 
 from .. import features
-from ..nn import Conv2d, Dropout, Linear, MaxPool1d, MaxPool2d
+from ..nn import Conv2d, Dropout, Linear, MaxPool1d, MaxPool2d, conv1_pool
 from ._common import DEVICE, accuracy, class_accuracy   # noqa: F401
 
 
@@ -36,8 +37,7 @@ class Network(nn.Module):
     def forward(self, x):
         with torch.no_grad():
             inx = features.fbank(x)                       # [B, 98, 120]
-        h = inx.unsqueeze(-1)                             # NHWC [B, 98, 120, 1]
-        h = self.maxpool1(self.conv1(h))                  # [B, 98, 40, 64]
+        h = conv1_pool(inx, self.conv1, self.maxpool1)   # fused conv1 + maxpool1: NHWC [B, 98, 40, 64]
         h = self.maxpool2(self.conv2(h))                  # [B, 98, 10, 128]
         h = self.conv4(self.conv3(h))                     # [B, 98, 1, 512]
         h = self.maxpool3(h.squeeze(2)).squeeze(1)        # [B, 512]

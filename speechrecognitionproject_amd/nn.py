@@ -261,6 +261,49 @@ class Conv1d(tnn.Module):
         return y.reshape(N, y.shape[2], self.out_channels)
 
 
+class _Conv1PoolFn(torch.autograd.Function):
+    """conv1 + bias + MaxPool2d((1, 3)) of model_fbanks_cnn (srk_conv1_pool_fwd / _wgrad): one
+    input channel, the pooled NHWC output; the input (features) gets no gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, padding, pool):
+        x = x.contiguous()
+        _check_cuda(x, w, b)
+        N, H, W = x.shape
+        Co, _, KH, KW = w.shape
+        y = torch.empty((N, H, W // pool, Co), device=x.device)
+        arg = torch.empty((N, H, W // pool, Co), device=x.device, dtype=torch.uint8)
+        call("srk_conv1_pool_fwd", ptr(x), N, H, W, ptr(w.contiguous()), ptr(b), Co, KH, KW, padding[0], padding[1],
+             pool, ptr(y), ptr(arg), stream_ptr())
+        ctx.save_for_backward(x, arg)
+        ctx.geom = (Co, KH, KW, padding, pool)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, arg = ctx.saved_tensors
+        Co, KH, KW, padding, pool = ctx.geom
+        N, H, W = x.shape
+        dw = torch.empty((Co, 1, KH, KW), device=x.device)
+        db = torch.empty((Co,), device=x.device)
+        ws = torch.empty(int(_lib.lib().srk_conv1_pool_workspace_floats(Co, KH, KW)), device=x.device)
+        call("srk_conv1_pool_wgrad", ptr(x), N, H, W, Co, KH, KW, padding[0], padding[1], pool, ptr(dy.contiguous()),
+             ptr(arg), ptr(dw), ptr(db), ptr(ws), stream_ptr())
+        return None, dw, db, None, None
+
+
+def conv1_pool(x, conv, pool):
+    """Fused ``pool(conv(x))`` for a one-channel NHW input when the geometry is the one
+    srk_conv1_pool supports (model_fbanks_cnn conv1 + maxpool1) and ``x`` needs no gradient;
+    otherwise the separate conv and pool kernels.  Returns NHWC."""
+    if (conv.in_channels == 1 and conv.out_channels == 64 and tuple(conv.kernel_size) == (7, 3)
+            and tuple(conv.padding) == (3, 1) and tuple(conv.stride) == (1, 1) and conv.bias is not None
+            and tuple(pool.kernel_size) == (1, 3) and not x.requires_grad):
+        require_gpu()
+        return _Conv1PoolFn.apply(x, conv.weight, conv.bias, conv.padding, 3)
+    return pool(conv(x.unsqueeze(-1)))
+
+
 class _MaxPoolNHWCFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kh, kw):

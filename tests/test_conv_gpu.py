@@ -20,6 +20,8 @@ CONV2D = [  # N, H, W, Ci, Co, KH, KW, ph, pw   (model_fbanks_cnn.py:72-75 + odd
     (2, 98, 10, 128, 256, 1, 10, 0, 0),
     (3, 98, 1, 256, 512, 7, 1, 3, 0),
     (2, 9, 11, 5, 7, 3, 2, 1, 0),
+    (24, 98, 40, 64, 128, 1, 7, 0, 3),   # many tiles + deep split-K weight gradient
+    (4, 17, 13, 12, 36, 3, 3, 1, 1),     # N % 4 == 0 but odd tile edges
 ]
 
 
@@ -57,7 +59,7 @@ def test_conv1d_strided_vs_torch(gpu, shape):
 
 
 @pytest.mark.parametrize("N,H,W,C,kh,kw", [(2, 98, 120, 64, 1, 3), (2, 98, 40, 128, 1, 4), (3, 98, 1, 512, 98, 1),
-                                           (2, 5, 7, 3, 2, 3)])
+                                           (2, 5, 7, 4, 2, 3)])
 def test_maxpool_vs_torch(gpu, N, H, W, C, kh, kw):
     g = torch.Generator().manual_seed(H * W)
     x = torch.randn(N, C, H, W, generator=g)
@@ -71,6 +73,32 @@ def test_maxpool_vs_torch(gpu, N, H, W, C, kh, kw):
     (ym * gy.permute(0, 2, 3, 1).cuda()).sum().backward()
     assert torch.equal(ym.detach().permute(0, 3, 1, 2).cpu(), yr.detach())
     assert torch.equal(xm.grad.permute(0, 3, 1, 2).cpu(), xr.grad)
+
+
+@pytest.mark.parametrize("N,H,W", [(3, 98, 120), (2, 7, 9), (1, 5, 31)])
+def test_conv1_pool_fused_vs_torch(gpu, N, H, W):
+    """Fused conv1 + bias + maxpool (1,3) (model_fbanks_cnn.py:72-73,89-90) vs torch conv2d +
+    max_pool2d: pooled values, and dW / db through the pool (gradient routed by the argmax)."""
+    g = torch.Generator().manual_seed(N * 7 + W)
+    x = torch.randn(N, 1, H, W, generator=g) * 30.0
+    w = torch.randn(64, 1, 7, 3, generator=g) * 0.2
+    b = torch.randn(64, generator=g)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = F.max_pool2d(F.conv2d(x, wr, br, padding=(3, 1)), (1, 3))
+    gy = torch.randn(yr.shape, generator=g)
+    (yr * gy).sum().backward()
+    wm, bm = w.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+    ym = snn._Conv1PoolFn.apply(x[:, 0].cuda(), wm, bm, (3, 1), 3)
+    (ym * gy.permute(0, 2, 3, 1).cuda()).sum().backward()
+    assert rel_err(ym.detach().permute(0, 3, 1, 2).cpu().numpy(), yr.detach().numpy()) <= 1e-5
+    assert rel_err(wm.grad.cpu().numpy(), wr.grad.numpy()) <= 1e-4
+    assert rel_err(bm.grad.cpu().numpy(), br.grad.numpy()) <= 1e-5
+
+
+def test_maxpool_rejects_unaligned_channels(gpu):
+    from speechrecognitionproject_amd._lib import SrkError
+    with pytest.raises(SrkError):
+        snn._MaxPoolNHWCFn.apply(torch.zeros(1, 4, 6, 3, device="cuda"), 1, 3)
 
 
 def test_dropout_mask(gpu):

@@ -107,7 +107,8 @@ def cpu_baseline(model_name, batch, seconds):
 def feature_roofline(model_name, n_clips=65536):
     """The model's feature kernel alone on a large batch (HBM-bound): algorithmic bytes / time."""
     name, per_clip = FEATURE[model_name]
-    fn = {"mfcc": features.mfcc, "fbank": features.fbank, "spec": features.spec}[name]
+    fn = {"mfcc": lambda x, out=None: features.mfcc(x, time_major=True, out=out), "fbank": features.fbank,
+          "spec": lambda x, out=None: features.spec(x, transposed=True, out=out)}[name]   # the models' layouts
     x, _ = synthetic_clips(1024, seed=123)
     xd = torch.from_numpy(x).cuda().repeat(n_clips // 1024, 1)
     out = None

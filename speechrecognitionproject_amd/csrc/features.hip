@@ -1,397 +1,274 @@
 // K1 MFCC, K2 log-mel fbank, K3 log spectrogram, K4 noise-mix — gfx950 HIP kernels.
 //
-// Design: one workgroup per clip, frames processed in chunks of F.
-// Per chunk:
-//   load   : wave-per-frame coalesced float2 loads of PCM, window applied in fp64, packed as
-//            z[n] = x[2n] + i x[2n+1] (real N-point FFT via an N/2-point complex FFT); the DC and
-//            Nyquist sums are accumulated in fp64 in the same pass (fp32 cancellation in the DC
-//            bin costs up to 0.17 dB in fbank column 1 otherwise — SURVEY.md Appendix A).
-//   fft    : mixed-radix Stockham passes (radix 4 / 5) in LDS, twiddles from a table.
-//   untangle + |X|^2, then the feature-specific reduction (sparse mel, log, DCT ...).
-#include "srk_internal.h"
+// STFT design: a wave computes several frames at once entirely in registers —
+// the N-point real FFT is an N/2-point complex FFT of z[n] = x[2n] + i x[2n+1] factored 16 x M2:
+// pass A (lane per (frame, j)) runs an M2-point DFT over its samples in registers and applies the
+// twiddles W^(j k1); one LDS transpose (row pitch 17 complex: conflict-free); pass B (lane per
+// (frame, k1)) runs a 16-point DFT.  The real spectrum is untangled from Z[k] and Z[N/2 - k], then
+// the feature-specific reduction (sparse mel pairs, log, DCT ...) runs on the wave's own LDS
+// slice — no workgroup barrier inside the frame loop for fbank / spectrogram (waves take
+// (clip, frame-chunk) items independently).  Lane-constant operands (window samples, pass-A
+// twiddles, untangle twiddles, mel weights) live in registers for the whole kernel.
+// The DC and Nyquist bins come from fp64 sums of the windowed samples (pre-emphasis makes the DC
+// bin a cancellation: an fp32 FFT costs up to 0.17 dB in fbank column 1 — SURVEY.md App. A).
+#include <algorithm>
+
+#include "fft_regs.h"
 
 namespace srk {
 namespace {
 
+using namespace fftr;
+
 constexpr int kPcmLen = 16000;
 
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }   // -i * a
-
-template <int R>
-__device__ __forceinline__ void dft(float2 (&v)[R]);
-
-template <>
-__device__ __forceinline__ void dft<4>(float2 (&v)[4]) {
-  const float2 s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
-  const float2 s13 = cadd(v[1], v[3]), d13 = mul_mi(csub(v[1], v[3]));
-  v[0] = cadd(s02, s13);
-  v[2] = csub(s02, s13);
-  v[1] = cadd(d02, d13);
-  v[3] = csub(d02, d13);
-}
-
-template <>
-__device__ __forceinline__ void dft<5>(float2 (&v)[5]) {
-  constexpr float c1 = 0.30901699437494745f, c2 = -0.8090169943749473f;
-  constexpr float s1 = 0.9510565162951535f, s2 = 0.5877852522924732f;
-  const float2 t1 = cadd(v[1], v[4]), t2 = cadd(v[2], v[3]);
-  const float2 t3 = csub(v[1], v[4]), t4 = csub(v[2], v[3]);
-  const float2 b1 = make_float2(v[0].x + c1 * t1.x + c2 * t2.x, v[0].y + c1 * t1.y + c2 * t2.y);
-  const float2 b2 = make_float2(v[0].x + c2 * t1.x + c1 * t2.x, v[0].y + c2 * t1.y + c1 * t2.y);
-  const float2 q1 = make_float2(s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y);   // -i*q1 for y1
-  const float2 q2 = make_float2(s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y);
-  v[0] = make_float2(v[0].x + t1.x + t2.x, v[0].y + t1.y + t2.y);
-  v[1] = cadd(b1, mul_mi(q1));
-  v[4] = csub(b1, mul_mi(q1));
-  v[2] = cadd(b2, mul_mi(q2));
-  v[3] = csub(b2, mul_mi(q2));
-}
-
-// One Stockham autosort pass of radix R over F frames of M complex points held in `buf`
-// (frame-major).  Ns = product of the radices of the previous passes.  Butterfly j reads
-// x[j + r*M/R], scales input r by W_{Ns*R}^{(j mod Ns)*r}, and writes y[(j/Ns)*Ns*R + j%Ns + r*Ns].
-// In place: every thread keeps its butterflies in registers across the barrier.
-template <int R, int NS, int M, int F, int NT>
-__device__ __forceinline__ void stockham_pass(float2* buf, const float2* __restrict__ tw) {
-  constexpr int MR = M / R;
-  constexpr int NB = F * MR;
-  constexpr int CNT = (NB + NT - 1) / NT;
-  float2 v[CNT][R];
-  int dst[CNT];
-#pragma unroll
-  for (int i = 0; i < CNT; ++i) {
-    const int b = threadIdx.x + i * NT;
-    dst[i] = -1;
-    if (b < NB) {
-      const int fr = b / MR, j = b % MR, k = j % NS;
-      const int base = fr * M;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        float2 a = buf[base + j + r * MR];
-        if (NS > 1 && r > 0) a = cmul(a, tw[k * r * (M / (NS * R))]);
-        v[i][r] = a;
-      }
-      dft<R>(v[i]);
-      dst[i] = base + (j / NS) * NS * R + k;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < CNT; ++i) {
-    if (dst[i] >= 0) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) buf[dst[i] + r * NS] = v[i][r];
-    }
-  }
-  __syncthreads();
-}
-
-template <int M, int F, int NT>
-__device__ __forceinline__ void fft_frames(float2* buf, const float2* __restrict__ tw);
-
-template <>
-__device__ __forceinline__ void fft_frames<256, 14, 256>(float2* buf, const float2* __restrict__ tw) {
-  stockham_pass<4, 1, 256, 14, 256>(buf, tw);
-  stockham_pass<4, 4, 256, 14, 256>(buf, tw);
-  stockham_pass<4, 16, 256, 14, 256>(buf, tw);
-  stockham_pass<4, 64, 256, 14, 256>(buf, tw);
-}
-
-template <int F, int NT>
-__device__ __forceinline__ void fft320(float2* buf, const float2* __restrict__ tw) {
-  stockham_pass<4, 1, 320, F, NT>(buf, tw);
-  stockham_pass<4, 4, 320, F, NT>(buf, tw);
-  stockham_pass<4, 16, 320, F, NT>(buf, tw);
-  stockham_pass<5, 64, 320, F, NT>(buf, tw);
-}
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+// Hardware log2 (v_log_f32, ~1 ulp on normal inputs; every caller feeds values >= 1e-10) scaled to
+// log10 / ln: the features are compared in dB / log units where this is far inside the tolerances.
+__device__ __forceinline__ float fast_log10(float x) { return __builtin_amdgcn_logf(x) * 0.30102999566398120f; }
+__device__ __forceinline__ float fast_ln(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
 
-// Untangle the packed real FFT and store |X[k]|^2 (k = 0..M) as floats over `buf`, frame
-// stride M+1.  X[0] / X[M] come from the fp64 sums `dcny` instead of the fp32 FFT.
-template <int M, int F, int NT>
-__device__ __forceinline__ void power_spectrum(float2* buf, const float2* __restrict__ post,
-                                               const double2* dcny, bool fix_dc, bool fix_nyq) {
-  constexpr int NI = F * (M + 1);
-  constexpr int CNT = (NI + NT - 1) / NT;
-  float p[CNT];
+// sum over the 16 lanes of a frame group (lanes 16f .. 16f+15)
+__device__ __forceinline__ double group16_sum(double v) {
 #pragma unroll
-  for (int i = 0; i < CNT; ++i) {
-    const int it = threadIdx.x + i * NT;
-    p[i] = 0.f;
-    if (it < NI) {
-      const int fr = it / (M + 1), k = it % (M + 1);
-      const float2 a = buf[fr * M + (k % M)];
-      const float2 bz = buf[fr * M + ((M - k) % M)];
-      const float2 bc = make_float2(bz.x, -bz.y);
-      const float2 e = make_float2(0.5f * (a.x + bc.x), 0.5f * (a.y + bc.y));
-      const float2 o = mul_mi(make_float2(0.5f * (a.x - bc.x), 0.5f * (a.y - bc.y)));
-      const float2 x = cadd(e, cmul(post[k], o));
-      p[i] = x.x * x.x + x.y * x.y;
-      if (k == 0 && fix_dc) p[i] = (float)(dcny[fr].x * dcny[fr].x);
-      if (k == M && fix_nyq) p[i] = (float)(dcny[fr].y * dcny[fr].y);
-    }
-  }
-  __syncthreads();
-  float* pb = reinterpret_cast<float*>(buf);
-#pragma unroll
-  for (int i = 0; i < CNT; ++i) {
-    const int it = threadIdx.x + i * NT;
-    if (it < NI) pb[it] = p[i];
-  }
-  __syncthreads();
-}
-
-// ------------------------------------------------------------------------- per-feature loads
-// Each returns the two windowed fp64 samples feeding z[n] = x[2n] + i x[2n+1] of frame gf.
-struct FbankLoad {   // model_fbanks_cnn.py:21 (fp32 pre-emphasis), :36-41 (frames, Hamming)
-  static constexpr int N = 512, M = 256, NFRAMES = 98;
-  __device__ static __forceinline__ double emph(const float* x, int i) {
-    // numpy rounds the product and the difference separately: no FMA contraction here
-#pragma clang fp contract(off)
-    return i == 0 ? (double)x[0] : (double)(x[i] - 0.97f * x[i - 1]);
-  }
-  __device__ static __forceinline__ void load(const float* x, const DeviceTables& t, int gf, int n,
-                                              double& a, double& b) {
-    const int m = 2 * n;
-    if (m >= 400) { a = b = 0.0; return; }
-    const int s = 160 * gf + m;
-    a = emph(x, s) * t.hamming400[m];
-    b = emph(x, s + 1) * t.hamming400[m + 1];
-  }
-};
-
-struct SpecLoad {    // scipy.signal.spectrogram segments, model_spec_bgru.py:13
-  static constexpr int N = 640, M = 320, NFRAMES = 49;
-  __device__ static __forceinline__ void load(const float* x, const DeviceTables& t, int gf, int n,
-                                              double& a, double& b) {
-    const int s = 320 * gf + 2 * n;
-    const float2 v = *reinterpret_cast<const float2*>(x + s);
-    a = (double)v.x * t.tukey640[2 * n];
-    b = (double)v.y * t.tukey640[2 * n + 1];
-  }
-};
-
-// Load frames [f0, f0+F) of clip x into buf, windowed; frames past NFRAMES are zero.
-template <class L, int F, int NT>
-__device__ __forceinline__ void load_frames(float2* buf, double2* dcny, const float* x,
-                                            const DeviceTables& t, int f0) {
-  constexpr int NW = NT / 64;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int fr = wave; fr < F; fr += NW) {
-    const int gf = f0 + fr;
-    double se = 0.0, so = 0.0;
-#pragma unroll
-    for (int i = 0; i < L::M / 64; ++i) {
-      const int n = lane + 64 * i;
-      double a = 0.0, b = 0.0;
-      if (gf < L::NFRAMES) L::load(x, t, gf, n, a, b);
-      buf[fr * L::M + n] = make_float2((float)a, (float)b);
-      se += a;
-      so += b;
-    }
-    se = wave_sum(se);
-    so = wave_sum(so);
-    if (lane == 0) dcny[fr] = make_double2(se + so, se - so);
-  }
-  __syncthreads();
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
 }
 
 // ------------------------------------------------------------------------- K2 fbank
-constexpr int kFbF = 14, kFbNT = 256;
+// models/model_fbanks_cnn.py:15-66.  N = 512 (400-sample frames, Hamming, zero-padded), hop 160,
+// 98 frames; 256-point complex FFT = 16 (j) x 16 (i), n = j + 16 i, k = k1 + 16 k2.
+// A wave = 4 frames (lanes 16 f + j in pass A, 16 f + k1 in pass B): 25 chunks per clip.
 constexpr float kFbEpsDb = -313.07119549076395f;   // 20*log10(np.finfo(float).eps), :61-62
+constexpr int kFbChunks = 25;
+constexpr int kFbPairs = 60, kFbPairTaps = 12;     // filters (l, 119 - l); max pair width 11
 
-__global__ __launch_bounds__(kFbNT) void fbank_kernel(const float* __restrict__ pcm, float* __restrict__ out,
-                                                      DeviceTables t) {
-  __shared__ float2 buf[kFbF * 256];
-  __shared__ double2 dcny[kFbF];
-  const int clip = blockIdx.x;
-  const float* x = pcm + (size_t)clip * kPcmLen;
-  float* o = out + (size_t)clip * 98 * 120;
-  for (int f0 = 0; f0 < 98; f0 += kFbF) {
-    load_frames<FbankLoad, kFbF, kFbNT>(buf, dcny, x, t, f0);
-    fft_frames<256, kFbF, kFbNT>(buf, t.tw256);
-    power_spectrum<256, kFbF, kFbNT>(buf, t.post512, dcny, true, true);
-    const float* pb = reinterpret_cast<const float*>(buf);
-    for (int it = threadIdx.x; it < kFbF * 120; it += kFbNT) {
-      const int fr = it / 120, m = it % 120;
-      const int cnt = t.fb_cnt[m];
-      float acc = 0.f;
-      if (cnt > 0) {
-        const int lo = t.fb_lo[m], off = t.fb_off[m];
-        const float* p = pb + fr * 257 + lo;
-        for (int c = 0; c < cnt; ++c) acc = fmaf(t.fb_w[off + c], p[c], acc);
+struct FbankTables {
+  const double* hamming400;
+  const float2* tw256;      // W256^t
+  const float2* post512;    // W512^k, k = 0..256
+  const int4* pair_meta;    // [60] {lo_a, cnt_a, lo_b, cnt_b}
+  const float* pair_w;      // [60][12] weights of filter a then filter b, zero padded
+};
+
+// 4 waves per SIMD (<= 128 VGPRs): the window and the pass-A twiddles are read from LDS tables
+// staged once per workgroup; only the small lane constants stay in registers.
+__global__ __launch_bounds__(256, 4) void fbank_kernel(const float* __restrict__ pcm, float* __restrict__ out,
+                                                       int64_t n_clips, FbankTables t) {
+  __shared__ v2f sbuf[4][4 * 272];   // per wave: 4 frames x (16 x 17) transpose, reused for spectra / power
+  __shared__ double s_win[400];
+  __shared__ v2f s_tw[16 * 16];      // W256^(j k1) at [k1][j]
+  __shared__ v2f s_post[257];        // W512^k
+  __shared__ float s_pw[kFbPairs * kFbPairTaps];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int f = lane >> 4, j = lane & 15;
+  for (int i = threadIdx.x; i < 400; i += 256) s_win[i] = t.hamming400[i];
+  for (int i = threadIdx.x; i < 257; i += 256) s_post[i] = v2f{t.post512[i].x, t.post512[i].y};
+  for (int i = threadIdx.x; i < kFbPairs * kFbPairTaps; i += 256) s_pw[i] = t.pair_w[i];
+  {
+    const int k1 = threadIdx.x >> 4, jj = threadIdx.x & 15;
+    const float2 w = t.tw256[(jj * k1) & 255];
+    s_tw[threadIdx.x] = v2f{w.x, w.y};
+  }
+  __syncthreads();
+  v2f* tb = sbuf[wave];
+  float* pb = reinterpret_cast<float*>(tb);   // power [4][260] after the untangle
+  const int pl = lane < kFbPairs ? lane : 0;
+  const int4 meta = t.pair_meta[pl];
+  const float* pw = s_pw + pl * kFbPairTaps;
+
+  const int64_t items = n_clips * kFbChunks;
+  for (int64_t it = (int64_t)blockIdx.x * 4 + wave; it < items; it += (int64_t)gridDim.x * 4) {
+    const int64_t clip = it / kFbChunks;
+    const int c = (int)(it % kFbChunks);
+    const int gf = 4 * c + f;                     // this lane's frame (pass A)
+    const bool live = gf < 98;
+    const float* __restrict__ x = pcm + clip * kPcmLen + 160 * (live ? gf : 0);
+    // pre-emphasis (fp32, numpy's two roundings) x Hamming (fp64, :33-41), DC / Nyquist sums in fp64
+    v2f a[16];
+    double dc = 0.0, ny = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      a[i] = v2f{0.f, 0.f};
+      const int n = j + 16 * i;
+      if (i < 13 && n < 200 && live) {
+#pragma clang fp contract(off)
+        const v2f xv = *reinterpret_cast<const v2f*>(x + 2 * n);
+        const bool first = (gf == 0 && n == 0);
+        const float xm = first ? 0.f : x[2 * n - 1];
+        const float e0 = first ? xv.x : xv.x - 0.97f * xm;
+        const float e1 = xv.y - 0.97f * xv.x;
+        const double d0 = (double)e0 * s_win[2 * n], d1 = (double)e1 * s_win[2 * n + 1];
+        a[i] = v2f{(float)d0, (float)d1};
+        dc += d0 + d1;
+        ny += d0 - d1;
       }
-      // |rfft|^2 / NFFT (:44): the 1/512 is an exact power of two, applied after the sum
-      acc *= (1.0f / 512.0f);
-      o[(f0 + fr) * 120 + m] = acc == 0.f ? kFbEpsDb : 20.0f * log10f(acc);
     }
-    __syncthreads();
+    dc = group16_sum(dc);
+    ny = group16_sum(ny);
+    // pass A: 16-point DFT over i, twiddle W256^(j k1), transpose
+    dft16v(a);
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) tb[f * 272 + k1 * 17 + j] = k1 ? cm2(a[k1], s_tw[k1 * 16 + j]) : a[0];
+    wave_lds_fence();
+    // pass B: lane = (f, k1): 16-point DFT over j -> Z[k1 + 16 k2]
+    v2f b[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) b[jj] = tb[f * 272 + j * 17 + jj];
+    dft16v(b);
+    wave_lds_fence();
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) tb[f * 272 + j + 16 * k2] = b[k2];
+    wave_lds_fence();
+    // untangle -> |X[k]|^2 (k = 0..256) of the 4 frames, held in registers, then written over tb
+    float p[4][5];
+#pragma unroll
+    for (int ff = 0; ff < 4; ++ff) {
+      const double dcf = __shfl(dc, 16 * ff, 64), nyf = __shfl(ny, 16 * ff, 64);
+#pragma unroll
+      for (int m = 0; m < 5; ++m) {
+        const int k = lane + 64 * m;
+        const v2f A = tb[ff * 272 + (k & 255)];
+        const v2f Bz = tb[ff * 272 + ((256 - k) & 255)];
+        const v2f Bc = v2f{Bz.x, -Bz.y};
+        const v2f e = 0.5f * (A + Bc), o = mi2(0.5f * (A - Bc));
+        const v2f X = e + cm2(s_post[min(k, 256)], o);
+        float v = X.x * X.x + X.y * X.y;
+        if (k == 0) v = (float)(dcf * dcf);
+        if (k == 256) v = (float)(nyf * nyf);
+        p[ff][m] = v;
+      }
+    }
+    wave_lds_fence();
+#pragma unroll
+    for (int ff = 0; ff < 4; ++ff)
+#pragma unroll
+      for (int m = 0; m < 5; ++m)
+        if (lane + 64 * m <= 256) pb[ff * 260 + lane + 64 * m] = p[ff][m];
+    wave_lds_fence();
+    // mel pairs (filter l and 119 - l), |X|^2 / 512 (:44, an exact power of two), eps floor, 20 log10
+    if (lane < kFbPairs) {
+      float* o = out + (clip * 98 + 4 * c) * 120;
+#pragma unroll
+      for (int ff = 0; ff < 4; ++ff) {
+        if (4 * c + ff >= 98) break;
+        const float* pp = pb + ff * 260;
+        float sa = 0.f, sb = 0.f;
+#pragma unroll
+        for (int q = 0; q < kFbPairTaps; ++q) {
+          const bool in_a = q < meta.y;
+          const int k = in_a ? meta.x + q : meta.z + (q - meta.y);
+          const float v = pw[q] * pp[min(k, 256)];
+          sa += in_a ? v : 0.f;
+          sb += in_a ? 0.f : v;
+        }
+        sa *= (1.0f / 512.0f);
+        sb *= (1.0f / 512.0f);
+        o[ff * 120 + lane] = sa == 0.f ? kFbEpsDb : 20.0f * fast_log10(sa);
+        o[ff * 120 + 119 - lane] = sb == 0.f ? kFbEpsDb : 20.0f * fast_log10(sb);
+      }
+    }
+    wave_lds_fence();
   }
 }
 
 // ------------------------------------------------------------------------- K3 spectrogram
-constexpr int kSpF = 7, kSpNT = 256;
+// models/model_spec_bgru.py:11-17: scipy.signal.spectrogram(fs=16000, nperseg=640, noverlap=320)
+// = 49 frames of 640 samples (no padding), periodic Tukey(0.25), PSD density scaling, one-sided
+// (interior bins doubled), then log(S + 1e-10).  320-point complex FFT = 16 (j) x 20 (i); a wave
+// = 3 frames (17 chunks per clip, the last one holds frame 48 only).
+constexpr int kSpChunks = 17;
 
-__global__ __launch_bounds__(kSpNT) void spec_kernel(const float* __restrict__ pcm, float* __restrict__ out,
-                                                     int transposed, float scale, DeviceTables t) {
-  __shared__ float2 buf[kSpF * 320];
-  __shared__ double2 dcny[kSpF];
-  const int clip = blockIdx.x;
-  const float* x = pcm + (size_t)clip * kPcmLen;
-  float* o = out + (size_t)clip * 49 * 321;
-  for (int f0 = 0; f0 < 49; f0 += kSpF) {
-    load_frames<SpecLoad, kSpF, kSpNT>(buf, dcny, x, t, f0);
-    fft320<kSpF, kSpNT>(buf, t.tw320);
-    power_spectrum<320, kSpF, kSpNT>(buf, t.post640, dcny, true, true);
-    const float* pb = reinterpret_cast<const float*>(buf);
-    for (int it = threadIdx.x; it < kSpF * 321; it += kSpNT) {
-      const int fr = it / 321, k = it % 321;
-      float v = pb[it] * scale;
-      if (k > 0 && k < 320) v *= 2.0f;                 // one-sided, DC/Nyquist not doubled
-      v = logf(__fadd_rn(v, 1e-10f));                  // model_spec_bgru.py:14
-      const int f = f0 + fr;
-      if (transposed) o[f * 321 + k] = v; else o[k * 49 + f] = v;
+struct SpecTables {
+  const double* tukey640;
+  const float2* tw320;
+  const float2* post640;
+  float scale;              // 1 / (fs * sum(w^2))
+};
+
+__global__ __launch_bounds__(256, 4) void spec_kernel(const float* __restrict__ pcm, float* __restrict__ out,
+                                                      int64_t n_clips, int transposed, SpecTables t) {
+  __shared__ v2f sbuf[4][3 * 340];
+  __shared__ double s_win[640];
+  __shared__ v2f s_tw[20 * 16];      // W320^(j k1) at [k1][j]
+  __shared__ v2f s_post[321];        // W640^k
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fa = lane >> 4, j = lane & 15;       // pass A: frame, j
+  const int fb = lane / 20, k1b = lane % 20;     // pass B: frame, k1
+  for (int i = threadIdx.x; i < 640; i += 256) s_win[i] = t.tukey640[i];
+  for (int i = threadIdx.x; i < 321; i += 256) s_post[i] = v2f{t.post640[i].x, t.post640[i].y};
+  for (int i = threadIdx.x; i < 320; i += 256) {
+    const float2 w = t.tw320[((i & 15) * (i >> 4)) % 320];
+    s_tw[i] = v2f{w.x, w.y};
+  }
+  __syncthreads();
+  v2f* tb = sbuf[wave];
+  const int64_t items = n_clips * kSpChunks;
+  for (int64_t it = (int64_t)blockIdx.x * 4 + wave; it < items; it += (int64_t)gridDim.x * 4) {
+    const int64_t clip = it / kSpChunks;
+    const int c = (int)(it % kSpChunks);
+    const int gf = 3 * c + fa;
+    const bool live = fa < 3 && gf < 49;
+    const float* __restrict__ x = pcm + clip * kPcmLen + 320 * (live ? gf : 0);
+    v2f a[20];
+    double dc = 0.0, ny = 0.0;
+#pragma unroll
+    for (int i = 0; i < 20; ++i) {
+      const v2f xv = *reinterpret_cast<const v2f*>(x + 2 * (j + 16 * i));
+      const int n = j + 16 * i;
+      const double d0 = live ? (double)xv.x * s_win[2 * n] : 0.0, d1 = live ? (double)xv.y * s_win[2 * n + 1] : 0.0;
+      a[i] = v2f{(float)d0, (float)d1};
+      dc += d0 + d1;
+      ny += d0 - d1;
     }
-    __syncthreads();
+    dc = group16_sum(dc);
+    ny = group16_sum(ny);
+    dft20v(a);
+    if (fa < 3) {
+#pragma unroll
+      for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? cm2(a[k1], s_tw[k1 * 16 + j]) : a[0];
+    }
+    wave_lds_fence();
+    v2f b[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) b[jj] = fb < 3 ? tb[fb * 340 + k1b * 17 + jj] : v2f{0.f, 0.f};
+    dft16v(b);
+    wave_lds_fence();
+    if (fb < 3) {
+#pragma unroll
+      for (int k2 = 0; k2 < 16; ++k2) tb[fb * 320 + k1b + 20 * k2] = b[k2];
+    }
+    wave_lds_fence();
+#pragma unroll
+    for (int ff = 0; ff < 3; ++ff) {
+      const int f = 3 * c + ff;
+      if (f >= 49) break;
+      const double dcf = __shfl(dc, 16 * ff, 64), nyf = __shfl(ny, 16 * ff, 64);
+      float* o = out + clip * 49 * 321;
+#pragma unroll
+      for (int m = 0; m < 6; ++m) {
+        const int k = lane + 64 * m;
+        if (k > 320) continue;
+        const v2f A = tb[ff * 320 + (k == 320 ? 0 : k)];
+        const v2f Bz = tb[ff * 320 + (k == 0 ? 0 : 320 - k)];
+        const v2f Bc = v2f{Bz.x, -Bz.y};
+        const v2f e = 0.5f * (A + Bc), oo = mi2(0.5f * (A - Bc));
+        const v2f X = e + cm2(s_post[k], oo);
+        float v = X.x * X.x + X.y * X.y;
+        if (k == 0) v = (float)(dcf * dcf);
+        if (k == 320) v = (float)(nyf * nyf);
+        v *= t.scale;
+        if (k > 0 && k < 320) v *= 2.0f;           // one-sided, DC / Nyquist not doubled
+        v = fast_ln(__fadd_rn(v, 1e-10f));         // model_spec_bgru.py:14
+        if (transposed) o[f * 321 + k] = v; else o[k * 49 + f] = v;
+      }
+    }
+    wave_lds_fence();
   }
-}
-
-// ------------------------------------------------------------------------- register FFT (v2)
-// N = 640 real = 320 complex, factored 320 = 16 (j) x 20 (i): n = j + 16 i, k = k1 + 20 k2.
-//   pass A (lane per (frame, j), 16 lanes / frame): 20-point DFT over i in registers,
-//                                                   then twiddle W320^(j k1)
-//   LDS transpose (row pitch 17 complex: conflict-free ds_read_b64 / ds_write_b64)
-//   pass B (lane per (frame, k1), 20 lanes / frame): 16-point DFT over j in registers
-// A wave processes 3 frames at a time (48 lanes in pass A, 60 in pass B); no workgroup barrier
-// is needed inside the frame loop (each wave owns its LDS slices).
-typedef float v2f __attribute__((ext_vector_type(2)));
-typedef float v4f __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ v2f cm2(v2f a, v2f b) { return v2f{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
-__device__ __forceinline__ v2f mi2(v2f a) { return v2f{a.y, -a.x}; }   // -i * a
-
-__device__ constexpr float kW20[4][5][2] = {
-  {{1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}},
-  {{1.f, 0.f}, {9.510565163e-01f, -3.090169944e-01f}, {8.090169944e-01f, -5.877852523e-01f},
-   {5.877852523e-01f, -8.090169944e-01f}, {3.090169944e-01f, -9.510565163e-01f}},
-  {{1.f, 0.f}, {8.090169944e-01f, -5.877852523e-01f}, {3.090169944e-01f, -9.510565163e-01f},
-   {-3.090169944e-01f, -9.510565163e-01f}, {-8.090169944e-01f, -5.877852523e-01f}},
-  {{1.f, 0.f}, {5.877852523e-01f, -8.090169944e-01f}, {-3.090169944e-01f, -9.510565163e-01f},
-   {-9.510565163e-01f, -3.090169944e-01f}, {-8.090169944e-01f, 5.877852523e-01f}}};
-__device__ constexpr float kW16[4][4][2] = {
-  {{1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}},
-  {{1.f, 0.f}, {9.238795325e-01f, -3.826834324e-01f}, {7.071067812e-01f, -7.071067812e-01f},
-   {3.826834324e-01f, -9.238795325e-01f}},
-  {{1.f, 0.f}, {7.071067812e-01f, -7.071067812e-01f}, {0.f, -1.f}, {-7.071067812e-01f, -7.071067812e-01f}},
-  {{1.f, 0.f}, {3.826834324e-01f, -9.238795325e-01f}, {-7.071067812e-01f, -7.071067812e-01f},
-   {-9.238795325e-01f, 3.826834324e-01f}}};
-
-__device__ __forceinline__ void dft4v(v2f& a0, v2f& a1, v2f& a2, v2f& a3) {
-  const v2f s02 = a0 + a2, d02 = a0 - a2, s13 = a1 + a3, d13 = mi2(a1 - a3);
-  a0 = s02 + s13;
-  a2 = s02 - s13;
-  a1 = d02 + d13;
-  a3 = d02 - d13;
-}
-
-__device__ __forceinline__ void dft5v(v2f& a0, v2f& a1, v2f& a2, v2f& a3, v2f& a4) {
-  constexpr float c1 = 0.30901699437494745f, c2 = -0.8090169943749473f;
-  constexpr float s1 = 0.9510565162951535f, s2 = 0.5877852522924732f;
-  const v2f t1 = a1 + a4, t2 = a2 + a3, t3 = a1 - a4, t4 = a2 - a3;
-  const v2f b1 = a0 + c1 * t1 + c2 * t2, b2 = a0 + c2 * t1 + c1 * t2;
-  const v2f q1 = s1 * t3 + s2 * t4, q2 = s2 * t3 - s1 * t4;
-  a0 = a0 + t1 + t2;
-  a1 = b1 + mi2(q1);
-  a4 = b1 - mi2(q1);
-  a2 = b2 + mi2(q2);
-  a3 = b2 - mi2(q2);
-}
-
-// in-place 20-point forward DFT, natural order in and out (i = 4p + q, k = k1 + 5 k2)
-__device__ __forceinline__ void dft20v(v2f (&a)[20]) {
-  v2f b[4][5];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    v2f t0 = a[q], t1 = a[4 + q], t2 = a[8 + q], t3 = a[12 + q], t4 = a[16 + q];
-    dft5v(t0, t1, t2, t3, t4);
-    b[q][0] = t0; b[q][1] = t1; b[q][2] = t2; b[q][3] = t3; b[q][4] = t4;
-#pragma unroll
-    for (int k1 = 1; k1 < 5; ++k1)
-      if (q > 0) b[q][k1] = cm2(b[q][k1], v2f{kW20[q][k1][0], kW20[q][k1][1]});
-  }
-#pragma unroll
-  for (int k1 = 0; k1 < 5; ++k1) {
-    v2f u0 = b[0][k1], u1 = b[1][k1], u2 = b[2][k1], u3 = b[3][k1];
-    dft4v(u0, u1, u2, u3);
-    a[k1] = u0; a[k1 + 5] = u1; a[k1 + 10] = u2; a[k1 + 15] = u3;
-  }
-}
-
-// in-place 16-point forward DFT (j = 4p + q, k = k1 + 4 k2)
-__device__ __forceinline__ void dft16v(v2f (&a)[16]) {
-  v2f b[4][4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    v2f t0 = a[q], t1 = a[4 + q], t2 = a[8 + q], t3 = a[12 + q];
-    dft4v(t0, t1, t2, t3);
-    b[q][0] = t0; b[q][1] = t1; b[q][2] = t2; b[q][3] = t3;
-#pragma unroll
-    for (int k1 = 1; k1 < 4; ++k1)
-      if (q > 0) b[q][k1] = cm2(b[q][k1], v2f{kW16[q][k1][0], kW16[q][k1][1]});
-  }
-#pragma unroll
-  for (int k1 = 0; k1 < 4; ++k1) {
-    v2f u0 = b[0][k1], u1 = b[1][k1], u2 = b[2][k1], u3 = b[3][k1];
-    dft4v(u0, u1, u2, u3);
-    a[k1] = u0; a[k1 + 4] = u1; a[k1 + 8] = u2; a[k1 + 12] = u3;
-  }
-}
-
-__device__ __forceinline__ void wave_lds_fence() {
-  // orders this wave's LDS writes before its later LDS reads (no workgroup barrier needed)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// One wave computes the 320-point complex FFT of 3 frames whose packed inputs z[n] it supplies
-// through `a` (pass-A lanes, frame = lane >> 4, j = lane & 15, a[i] = z[j + 16 i]); on return the
-// natural-order spectra are in xs[f * 320 + k] (f < 3).  tb = this wave's transpose slice.
-__device__ __forceinline__ void fft320x3(v2f (&a)[20], const v2f (&tw)[20], v2f* tb, v2f* xs, int lane) {
-  const int fa = lane >> 4, j = lane & 15;
-  dft20v(a);
-  if (fa < 3) {
-#pragma unroll
-    for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? cm2(a[k1], tw[k1]) : a[0];
-  }
-  wave_lds_fence();
-  const int fb = lane / 20, k1 = lane % 20;
-  v2f b[16];
-  if (fb < 3) {
-#pragma unroll
-    for (int jj = 0; jj < 16; ++jj) b[jj] = tb[fb * 340 + k1 * 17 + jj];
-  }
-  dft16v(b);
-  if (fb < 3) {
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) xs[fb * 320 + k1 + 20 * k2] = b[k2];
-  }
-  wave_lds_fence();
 }
 
 // ------------------------------------------------------------------------- K1 MFCC (v2)
@@ -505,8 +382,8 @@ __global__ __launch_bounds__(64 * kMfWaves) __attribute__((amdgpu_waves_per_eu(2
           s0 = fmaf(w0[q * 128], p[lo0 + q], s0);
           s1 = fmaf(w1[q * 128], p[lo1 + q], s1);
         }
-        const float v0 = s0 > 1e-10f ? 10.0f * log10f(s0) : -100.0f;
-        const float v1 = s1 > 1e-10f ? 10.0f * log10f(s1) : -100.0f;
+        const float v0 = s0 > 1e-10f ? 10.0f * fast_log10(s0) : -100.0f;
+        const float v1 = s1 > 1e-10f ? 10.0f * fast_log10(s1) : -100.0f;
         db[(f0 + f) * 132 + lane] = v0;
         db[(f0 + f) * 132 + lane + 64] = v1;
         vmax = fmaxf(vmax, fmaxf(v0, v1));
@@ -601,11 +478,15 @@ int srk_fbank_fwd(const float* pcm, int64_t n_clips, float* out, void* stream) {
   SRK_REQUIRE(n_clips >= 0 && n_clips <= INT32_MAX, SRK_ERR_INVALID, "srk_fbank_fwd: bad n_clips %lld", (long long)n_clips);
   if (n_clips == 0) return SRK_OK;
   SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_fbank_fwd: null pointer");
+  SRK_REQUIRE((uintptr_t)pcm % 8 == 0, SRK_ERR_INVALID, "srk_fbank_fwd: pcm must be 8-byte aligned");
   const DeviceTables* t = nullptr;
   if (int rc = srk::get_tables(&t)) return rc;
+  srk::FbankTables ft{t->hamming400, t->tw256, t->post512, t->fbp_meta, t->fbp_w};
+  const int64_t items = n_clips * srk::kFbChunks;
+  const int64_t blocks = std::min<int64_t>((items + 3) / 4, 2048);   // waves take (clip, 4-frame chunk) items
   srk::ProfScope prof("fbank", srk::as_stream(stream), 111040.0 * (double)n_clips);   // 64000 in + 47040 out B/clip
-  hipLaunchKernelGGL(srk::fbank_kernel, dim3((unsigned)n_clips), dim3(srk::kFbNT), 0, srk::as_stream(stream),
-                     pcm, out, *t);
+  hipLaunchKernelGGL(srk::fbank_kernel, dim3((unsigned)blocks), dim3(256), 0, srk::as_stream(stream), pcm, out, n_clips,
+                     ft);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END
@@ -616,11 +497,15 @@ int srk_spec_fwd(const float* pcm, int64_t n_clips, float* out, int transposed, 
   SRK_REQUIRE(n_clips >= 0 && n_clips <= INT32_MAX, SRK_ERR_INVALID, "srk_spec_fwd: bad n_clips");
   if (n_clips == 0) return SRK_OK;
   SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_spec_fwd: null pointer");
+  SRK_REQUIRE((uintptr_t)pcm % 8 == 0, SRK_ERR_INVALID, "srk_spec_fwd: pcm must be 8-byte aligned");
   const DeviceTables* t = nullptr;
   if (int rc = srk::get_tables(&t)) return rc;
+  srk::SpecTables st{t->tukey640, t->tw320, t->post640, (float)t->spec_scale};
+  const int64_t items = n_clips * srk::kSpChunks;
+  const int64_t blocks = std::min<int64_t>((items + 3) / 4, 2048);
   srk::ProfScope prof("spec", srk::as_stream(stream), 126916.0 * (double)n_clips);    // 64000 + 62916 B/clip
-  hipLaunchKernelGGL(srk::spec_kernel, dim3((unsigned)n_clips), dim3(srk::kSpNT), 0, srk::as_stream(stream),
-                     pcm, out, transposed ? 1 : 0, (float)t->spec_scale, *t);
+  hipLaunchKernelGGL(srk::spec_kernel, dim3((unsigned)blocks), dim3(256), 0, srk::as_stream(stream), pcm, out, n_clips,
+                     transposed ? 1 : 0, st);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END

@@ -1,0 +1,107 @@
+// Register-resident FFT building blocks for the feature kernels (features.hip), gfx950.
+// Complex values are 2-float ext vectors so the compiler emits packed v_pk_{add,mul,fma}_f32.
+#pragma once
+#include "srk_internal.h"
+
+namespace srk {
+namespace fftr {
+
+// N = 640 real = 320 complex, factored 320 = 16 (j) x 20 (i): n = j + 16 i, k = k1 + 20 k2.
+//   pass A (lane per (frame, j), 16 lanes / frame): 20-point DFT over i in registers,
+//                                                   then twiddle W320^(j k1)
+//   LDS transpose (row pitch 17 complex: conflict-free ds_read_b64 / ds_write_b64)
+//   pass B (lane per (frame, k1), 20 lanes / frame): 16-point DFT over j in registers
+// A wave processes 3 frames at a time (48 lanes in pass A, 60 in pass B); no workgroup barrier
+// is needed inside the frame loop (each wave owns its LDS slices).
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v2f cm2(v2f a, v2f b) { return v2f{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+__device__ __forceinline__ v2f mi2(v2f a) { return v2f{a.y, -a.x}; }   // -i * a
+
+__device__ constexpr float kW20[4][5][2] = {
+  {{1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}},
+  {{1.f, 0.f}, {9.510565163e-01f, -3.090169944e-01f}, {8.090169944e-01f, -5.877852523e-01f},
+   {5.877852523e-01f, -8.090169944e-01f}, {3.090169944e-01f, -9.510565163e-01f}},
+  {{1.f, 0.f}, {8.090169944e-01f, -5.877852523e-01f}, {3.090169944e-01f, -9.510565163e-01f},
+   {-3.090169944e-01f, -9.510565163e-01f}, {-8.090169944e-01f, -5.877852523e-01f}},
+  {{1.f, 0.f}, {5.877852523e-01f, -8.090169944e-01f}, {-3.090169944e-01f, -9.510565163e-01f},
+   {-9.510565163e-01f, -3.090169944e-01f}, {-8.090169944e-01f, 5.877852523e-01f}}};
+__device__ constexpr float kW16[4][4][2] = {
+  {{1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}},
+  {{1.f, 0.f}, {9.238795325e-01f, -3.826834324e-01f}, {7.071067812e-01f, -7.071067812e-01f},
+   {3.826834324e-01f, -9.238795325e-01f}},
+  {{1.f, 0.f}, {7.071067812e-01f, -7.071067812e-01f}, {0.f, -1.f}, {-7.071067812e-01f, -7.071067812e-01f}},
+  {{1.f, 0.f}, {3.826834324e-01f, -9.238795325e-01f}, {-7.071067812e-01f, -7.071067812e-01f},
+   {-9.238795325e-01f, 3.826834324e-01f}}};
+
+__device__ __forceinline__ void dft4v(v2f& a0, v2f& a1, v2f& a2, v2f& a3) {
+  const v2f s02 = a0 + a2, d02 = a0 - a2, s13 = a1 + a3, d13 = mi2(a1 - a3);
+  a0 = s02 + s13;
+  a2 = s02 - s13;
+  a1 = d02 + d13;
+  a3 = d02 - d13;
+}
+
+__device__ __forceinline__ void dft5v(v2f& a0, v2f& a1, v2f& a2, v2f& a3, v2f& a4) {
+  constexpr float c1 = 0.30901699437494745f, c2 = -0.8090169943749473f;
+  constexpr float s1 = 0.9510565162951535f, s2 = 0.5877852522924732f;
+  const v2f t1 = a1 + a4, t2 = a2 + a3, t3 = a1 - a4, t4 = a2 - a3;
+  const v2f b1 = a0 + c1 * t1 + c2 * t2, b2 = a0 + c2 * t1 + c1 * t2;
+  const v2f q1 = s1 * t3 + s2 * t4, q2 = s2 * t3 - s1 * t4;
+  a0 = a0 + t1 + t2;
+  a1 = b1 + mi2(q1);
+  a4 = b1 - mi2(q1);
+  a2 = b2 + mi2(q2);
+  a3 = b2 - mi2(q2);
+}
+
+// in-place 20-point forward DFT, natural order in and out (i = 4p + q, k = k1 + 5 k2)
+__device__ __forceinline__ void dft20v(v2f (&a)[20]) {
+  v2f b[4][5];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v2f t0 = a[q], t1 = a[4 + q], t2 = a[8 + q], t3 = a[12 + q], t4 = a[16 + q];
+    dft5v(t0, t1, t2, t3, t4);
+    b[q][0] = t0; b[q][1] = t1; b[q][2] = t2; b[q][3] = t3; b[q][4] = t4;
+#pragma unroll
+    for (int k1 = 1; k1 < 5; ++k1)
+      if (q > 0) b[q][k1] = cm2(b[q][k1], v2f{kW20[q][k1][0], kW20[q][k1][1]});
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < 5; ++k1) {
+    v2f u0 = b[0][k1], u1 = b[1][k1], u2 = b[2][k1], u3 = b[3][k1];
+    dft4v(u0, u1, u2, u3);
+    a[k1] = u0; a[k1 + 5] = u1; a[k1 + 10] = u2; a[k1 + 15] = u3;
+  }
+}
+
+// in-place 16-point forward DFT (j = 4p + q, k = k1 + 4 k2)
+__device__ __forceinline__ void dft16v(v2f (&a)[16]) {
+  v2f b[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v2f t0 = a[q], t1 = a[4 + q], t2 = a[8 + q], t3 = a[12 + q];
+    dft4v(t0, t1, t2, t3);
+    b[q][0] = t0; b[q][1] = t1; b[q][2] = t2; b[q][3] = t3;
+#pragma unroll
+    for (int k1 = 1; k1 < 4; ++k1)
+      if (q > 0) b[q][k1] = cm2(b[q][k1], v2f{kW16[q][k1][0], kW16[q][k1][1]});
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    v2f u0 = b[0][k1], u1 = b[1][k1], u2 = b[2][k1], u3 = b[3][k1];
+    dft4v(u0, u1, u2, u3);
+    a[k1] = u0; a[k1 + 4] = u1; a[k1 + 8] = u2; a[k1 + 12] = u3;
+  }
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+  // orders this wave's LDS writes before its later LDS reads (no workgroup barrier needed)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+}  // namespace fftr
+}  // namespace srk

@@ -95,6 +95,32 @@ void to_csr(const std::vector<double>& w, int nf, int nbins, std::vector<int>& l
   }
 }
 
+// Dense [nf][nbins] -> lane pairs (filter l, filter nf-1-l), l < ceil(nf/2): meta {lo_a, cnt_a,
+// lo_b, cnt_b} and the two weight runs back to back, zero padded to `taps`.
+int to_pairs(const std::vector<double>& w, int nf, int nbins, int taps, std::vector<int4>& meta,
+             std::vector<float>& vals) {
+  const int np = (nf + 1) / 2;
+  meta.assign(np, int4{0, 0, 0, 0});
+  vals.assign((size_t)np * taps, 0.f);
+  auto run = [&](int m, int& lo, int& cnt) {
+    int first = -1, last = -1;
+    for (int k = 0; k < nbins; ++k)
+      if (w[(size_t)m * nbins + k] != 0.0) { if (first < 0) first = k; last = k; }
+    lo = first < 0 ? 0 : first;
+    cnt = first < 0 ? 0 : last - first + 1;
+  };
+  for (int l = 0; l < np; ++l) {
+    int la, ca, lb = 0, cb = 0;
+    run(l, la, ca);
+    if (nf - 1 - l != l) run(nf - 1 - l, lb, cb);
+    SRK_REQUIRE(ca + cb <= taps, SRK_ERR_INTERNAL, "filter pair %d spans %d > %d taps", l, ca + cb, taps);
+    meta[l] = int4{la, ca, lb, cb};
+    for (int q = 0; q < ca; ++q) vals[(size_t)l * taps + q] = (float)w[(size_t)l * nbins + la + q];
+    for (int q = 0; q < cb; ++q) vals[(size_t)l * taps + ca + q] = (float)w[(size_t)(nf - 1 - l) * nbins + lb + q];
+  }
+  return SRK_OK;
+}
+
 // models/model_fbanks_cnn.py:46-59
 std::vector<double> fbank_matrix() {
   const int nfilt = 120, nfft = 512, sr = 16000, nb = nfft / 2 + 1;
@@ -173,14 +199,14 @@ int build_tables(DeviceTables& t) {
   if ((rc = upload(&t.hann640, hann))) return rc;
   if ((rc = upload(&t.tukey640, tuk))) return rc;
 
-  std::vector<int> lo, cnt, off;
-  std::vector<float> vals;
   {
+    std::vector<int4> meta;
+    std::vector<float> pv;
+    if ((rc = to_pairs(fbank_matrix(), 120, 257, 12, meta, pv)) || (rc = upload(&t.fbp_meta, meta)) ||
+        (rc = upload(&t.fbp_w, pv)))
+      return rc;
     std::vector<int> wl;
     std::vector<float> wv;
-    if ((rc = to_windows(fbank_matrix(), 120, 257, 16, wl, wv)) || (rc = upload(&t.fb16_lo, wl)) ||
-        (rc = upload(&t.fb16_w, wv)))
-      return rc;
     if ((rc = to_windows(slaney_mel(), 128, 321, 16, wl, wv)) || (rc = upload(&t.mel16_lo, wl)) ||
         (rc = upload(&t.mel16_w, wv)))
       return rc;
@@ -189,14 +215,6 @@ int build_tables(DeviceTables& t) {
       for (int q = 0; q < 16; ++q) wt[q * 128 + m] = wv[m * 16 + q];
     if ((rc = upload(&t.mel16_wt, wt))) return rc;
   }
-  to_csr(fbank_matrix(), 120, 257, lo, cnt, off, vals);
-  if ((rc = upload(&t.fb_lo, lo)) || (rc = upload(&t.fb_cnt, cnt)) || (rc = upload(&t.fb_off, off)) ||
-      (rc = upload(&t.fb_w, vals)))
-    return rc;
-  to_csr(slaney_mel(), 128, 321, lo, cnt, off, vals);
-  if ((rc = upload(&t.mel_lo, lo)) || (rc = upload(&t.mel_cnt, cnt)) || (rc = upload(&t.mel_off, off)) ||
-      (rc = upload(&t.mel_w, vals)))
-    return rc;
 
   std::vector<float> dct(13 * 128);
   for (int k = 0; k < 128; ++k) dct[k] = (float)(1.0 / std::sqrt(128.0));

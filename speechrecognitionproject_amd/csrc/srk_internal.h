@@ -56,14 +56,13 @@ struct DeviceTables {
   float* hann640f = nullptr;   // fp32 copies for the register-FFT kernels
   float* tukey640f = nullptr;
   float* hamming400f = nullptr;
-  // sparse filterbanks (CSR by filter): lo bin, count, offset into weights
-  int* fb_lo = nullptr; int* fb_cnt = nullptr; int* fb_off = nullptr; float* fb_w = nullptr;   // 120 filters
-  int* mel_lo = nullptr; int* mel_cnt = nullptr; int* mel_off = nullptr; float* mel_w = nullptr; // 128 filters
+  // filter banks as lane pairs (filter l and nf - 1 - l, balancing narrow and wide triangles):
+  // meta {lo_a, cnt_a, lo_b, cnt_b}, weights of a then b, zero padded to a fixed tap count
+  int4* fbp_meta = nullptr; float* fbp_w = nullptr;     // fbank: 60 pairs x 12 taps
   float* dct = nullptr;        // [13][128] orthonormal DCT-II
-  // the same filterbanks as fixed 16-tap windows (zero-padded, start clamped so lo+16 <= bins)
+  // Slaney mel as fixed 16-tap windows (zero-padded, start clamped so lo+16 <= bins)
   int* mel16_lo = nullptr; float* mel16_w = nullptr;   // [128], [128][16]
   float* mel16_wt = nullptr;                           // [16][128] (lane-coalesced)
-  int* fb16_lo = nullptr; float* fb16_w = nullptr;     // [120], [120][16]
   double spec_scale = 0.0;     // 1 / (fs * sum(w^2)) for the Tukey window
 };
 

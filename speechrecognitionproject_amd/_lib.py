@@ -11,7 +11,7 @@ import re
 import torch  # noqa: F401  (load torch's HIP runtime before libsrk.so)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsrk.so")
+LIB_PATH = os.environ.get("SRK_LIB") or os.path.join(_HERE, "libsrk.so")   # SRK_LIB: experiment builds
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "srk.h")
 ABI_VERSION = 1
 

@@ -15,6 +15,8 @@
 // Workspace (fp32, caller-owned; sizes in srk_gru_workspace_floats):
 //   fwd:  gi [B*T, 6H] | gates [2][T][B][4H] (r, z, n, W_hn h + b_hn)       — kept for backward
 //   bwd:  dgi [B*T, 6H] | dgh [2][B][T][3H] | dgh_edge [2][B][3H] | dhz [2][B][H]
+#include <algorithm>
+
 #include "gemm.h"
 #include "gru_internal.h"
 
@@ -302,12 +304,16 @@ extern "C" {
 
 // Both workspaces end with a 64-float-aligned block of kCounterFloats arrival counters (the
 // persistent recurrence kernels' step ordering; see gru_persistent.hip).
-static int64_t fwd_counter_off(int64_t B, int64_t T, int64_t H) {
-  return (B * T * 6 * H + 2 * T * B * 4 * H + 63) / 64 * 64;
-}
-static int64_t bwd_counter_off(int64_t B, int64_t T, int64_t H) {
+// Before them, 64-float aligned, the persistent kernels' hand-off ping-pong buffer in MFMA-fragment
+// order (fwd: h [2 dir][2][rows][H], bwd: dg [2 dir][2][rows][3H]).
+static int64_t fwd_xbuf_off(int64_t B, int64_t T, int64_t H) { return (B * T * 6 * H + 2 * T * B * 4 * H + 63) / 64 * 64; }
+static int64_t bwd_xbuf_off(int64_t B, int64_t T, int64_t H) {
   return (B * T * 6 * H + 2 * B * T * 3 * H + 2 * B * 3 * H + 2 * B * H + 63) / 64 * 64;
 }
+// (rows padded to the 64-row groups of one launch chunk: <= 256 rows, or B rounded up to 64)
+static int64_t xbuf_rows(int64_t B) { return std::min<int64_t>((B + 63) / 64 * 64, 256); }
+static int64_t fwd_counter_off(int64_t B, int64_t T, int64_t H) { return fwd_xbuf_off(B, T, H) + 4 * xbuf_rows(B) * H; }
+static int64_t bwd_counter_off(int64_t B, int64_t T, int64_t H) { return bwd_xbuf_off(B, T, H) + 12 * xbuf_rows(B) * H; }
 
 int64_t srk_gru_workspace_floats(int64_t B, int64_t T, int64_t in, int64_t H, int backward) {
   (void)in;
@@ -333,6 +339,7 @@ int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
     srk::GruPArgs p{};
     p.B = (int)B; p.T = (int)T; p.H = (int)H;
     p.gi = gi; p.w_hh = w_hh; p.b_hh = b_hh; p.y = y; p.gates = gates;
+    p.xbuf = ws + fwd_xbuf_off(B, T, H);
     p.counters = reinterpret_cast<unsigned*>(ws + fwd_counter_off(B, T, H));
     return srk::gru_persistent_launch(p, false, s);
   }
@@ -374,6 +381,7 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
     srk::GruPArgs p{};
     p.B = (int)B; p.T = (int)T; p.H = (int)H;
     p.w_hh = w_hh; p.y_in = y; p.gates = a.gates; p.dy = dy; p.dgi = dgi; p.dgh = dgh; p.dgh_edge = dgh_edge;
+    p.xbuf = ws + bwd_xbuf_off(B, T, H);
     p.counters = reinterpret_cast<unsigned*>(ws + bwd_counter_off(B, T, H));
     if (int rc = srk::gru_persistent_launch(p, true, s)) return rc;
   } else {

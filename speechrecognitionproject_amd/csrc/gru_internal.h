@@ -25,6 +25,7 @@ struct GruPArgs {
   float* dgi;            // bwd: [B*T][6H]
   float* dgh;            // bwd: [2][B][T][3H] (also the dg hand-off buffer)
   float* dgh_edge;       // bwd: [2][B][3H]
+  float* xbuf;           // hand-off ping-pong: fwd h [2 dir][2][B][H], bwd dg [2 dir][2][B][3H]
   unsigned* counters;    // kCounterFloats words
   unsigned long long* trace;   // optional per-(workgroup, step) timestamps (tools/gru_trace.py)
 };

@@ -8,9 +8,13 @@
 //    keeps ITS slice of W_hh resident in LDS (fwd: the 3 x 16 gate rows x H, bwd: the 16 unit
 //    columns x 3H) — ~97 KB per workgroup, 3 MB per direction, read from HBM once per layer
 //    instead of once per step;
-//  * the recurrent state crosses workgroups through the layer's own output (fwd: y[b][t][dir]
-//    half, bwd: dgh[dir][b][t]) written write-through (`sc1`, 16-B per lane after an LDS
-//    transpose) and read back with `sc1` loads; one agent-scope arrival counter per (direction,
+//  * the recurrent state crosses workgroups through a ping-pong buffer laid out in MFMA-FRAGMENT
+//    order: for each 16-row block and 16-wide k block, the 64 lanes' float4 A-operands are one
+//    contiguous 1 KB chunk ([group][row block][k block][lane][4]), so every consumer load is a fully
+//    coalesced 1 KB wave access (the natural [row][k] layout puts 16 rows in each quarter-wave:
+//    measured 3-4 us of load time per step, independent of caching); written write-through (`sc1`,
+//    16 B per lane, after an LDS transpose) and read back with `sc1` loads (the outputs y / dgh get
+//    plain stores for the later GEMMs); one agent-scope arrival counter per (direction,
 //    64-row group) orders the steps (MI355X_MICROARCH.md "Valid forms", table row 1: one lane of
 //    each storing workgroup adds after every storing wave drained; consumers poll with an `sc1`
 //    load; every load of the handed-off bytes is an `sc1` load; one workgroup per CU);
@@ -77,11 +81,12 @@ __device__ __forceinline__ void arrive(unsigned* cnt) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Diagnostics (tools/gru_trace.py): thread 0 stamps s_memrealtime (100 MHz) at step start, after
-// the arrival wait, after the cell epilogue and after publishing.  Off (null) in production.
+// Diagnostics (tools/gru_trace.py): thread 0 stamps s_memrealtime (100 MHz) at step start (0), after
+// the arrival wait (1), after its MFMAs retired (2), after the cell epilogue (3) and after
+// publishing (4).  Off (null) in production.
 __device__ __forceinline__ void stamp(const GruPArgs& a, int step, int i) {
   if (a.trace && threadIdx.x == 0)
-    a.trace[((size_t)blockIdx.x * a.T + step) * 4 + i] = __builtin_amdgcn_s_memrealtime();
+    a.trace[((size_t)blockIdx.x * a.T + step) * 8 + i] = __builtin_amdgcn_s_memrealtime();
 }
 
 // (direction, group, slice) of this workgroup: the S slices of one (direction, group) pair are
@@ -123,8 +128,9 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
   const float bhr = a.b_hh[dir * 3 * H + j], bhz = a.b_hh[dir * 3 * H + H + j], bhn = a.b_hh[dir * 3 * H + 2 * H + j];
   __syncthreads();
 
-  const __amdgpu_buffer_rsrc_t ry = rsrc(a.y);
-  const int arow = min(b0 + wave * 16 + lr, b_last);   // A-operand row of this lane (clamped)
+  const int B = a.B;
+  const int Gp = a.G;   // 64-row groups in this launch (the hand-off buffer is padded to Gp * 64 rows)
+  const __amdgpu_buffer_rsrc_t rx = rsrc(a.xbuf + (size_t)dir * 2 * Gp * 64 * H);   // [2][Gp][4][H/16][64][4]
   float hreg[4] = {0.f, 0.f, 0.f, 0.f};                 // h_{t-1} of the lane's own 4 cells
 
   for (int step = 0; step < T; ++step) {
@@ -146,21 +152,45 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
     if (step > 0) {
       wait_count(cnt, (unsigned)(H / kUnits) * step);
       stamp(a, step, 1);
-      // h_{t-1}[arow][k], k = 16 kb + 4 lq + s  (k-permuted: one b128 feeds 4 MFMAs)
-      const unsigned base = (unsigned)((((size_t)arow * T + tprev) * 2 * H + dir * H + 4 * lq) * 4);
+      // h_{t-1}[row 16 wave + lr][k], k = 16 kb + 4 lq + s  (k-permuted: one b128 feeds 4 MFMAs)
+      // fragment chunk (group, row block = wave, k block) of the previous step's buffer; lane = lane
+      const unsigned base = (unsigned)(((((size_t)((step - 1) & 1) * Gp + group) * 4 + wave) * NKB * 64 + lane) * 16);
+      // The 32 workgroups of a (direction, group) read the SAME 64 rows: each walks k starting at a
+      // different block (rot = its slice) so they do not all hit the same L2 lines / channel at once
+      // (measured: the hand-off loads, not the MFMAs, set the step time).  The k order is fixed per
+      // slice, so results stay deterministic.
+      const int rot = slice % NKB;
       v4f hv[NKB];
 #pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) hv[kb] = ld4_sc1(ry, base + kb * 64);
+      for (int kb = 0; kb < NKB; ++kb) hv[kb] = ld4_sc1(rx, base + ((kb + rot) & (NKB - 1)) * 1024);
       __builtin_amdgcn_sched_barrier(0);   // all loads in flight before the first MFMA (no sinking)
+      // W fragments one k-block ahead of their MFMAs (issued first, behind a hard scheduling fence,
+      // so a block's MFMAs never wait on LDS); within a block the 12 MFMAs rotate over the three
+      // gate accumulators (dependent issue distance 3 x 32 cycles > the 40-cycle latency), pinned
+      // with scheduling groups (the default scheduler batches one accumulator).
+      v4f wv[2][3];
+#pragma unroll
+      for (int g = 0; g < 3; ++g) wv[0][g] = ld4(Ws + (g * kUnits + lr) * WP + rot * 16 + 4 * lq);
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb) {
-        v4f wv[3];
+        const int c = kb & 1;
+        if (kb + 1 < NKB) {
+          const int kn = (kb + 1 + rot) & (NKB - 1);
 #pragma unroll
-        for (int g = 0; g < 3; ++g) wv[g] = ld4(Ws + (g * kUnits + lr) * WP + kb * 16 + 4 * lq);
+          for (int g = 0; g < 3; ++g) wv[c ^ 1][g] = ld4(Ws + (g * kUnits + lr) * WP + kn * 16 + 4 * lq);
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
-          for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[kb][s], wv[g][s], acc[g], 0, 0, 0);
+          for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[kb][s], wv[c][g][s], acc[g], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (a.trace) {
+        asm volatile("" ::"v"(acc[0][0]), "v"(acc[1][0]), "v"(acc[2][0]));
+        stamp(a, step, 2);
       }
     }
     // cell epilogue: lane owns rows 16*wave + 4*lq + r, unit j
@@ -183,14 +213,19 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
       }
     }
     __syncthreads();
-    stamp(a, step, 2);
-    {  // h_t -> y (write-through): thread = (row tid/4, units 4*(tid%4) .. +3)
+    stamp(a, step, 3);
+    {  // h_t -> the hand-off buffer (write-through) and y: thread = (row tid/4, units 4*(tid%4) .. +3)
       const int rl = tid >> 2, uq = (tid & 3) * 4, b = b0 + rl;
-      if (b <= b_last)
-        st4_sc1(ry, (unsigned)((((size_t)b * T + t) * 2 * H + dir * H + j0 + uq) * 4), ld4(hT + rl * HTP + uq));
+      if (b <= b_last) {
+        const v4f hv4 = ld4(hT + rl * HTP + uq);
+        if (step + 1 < T)   // fragment slot (row block rl/16, k block = slice, lane = (uq/4)*16 + rl%16)
+          st4_sc1(rx, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB * 64 + slice * 64 +
+                                  (uq >> 2) * 16 + (rl & 15)) * 16), hv4);
+        st4(a.y + ((size_t)b * T + t) * 2 * H + dir * H + j0 + uq, hv4);
+      }
     }
     arrive(cnt);
-    stamp(a, step, 3);
+    stamp(a, step, 4);
   }
 }
 
@@ -226,8 +261,8 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
   __syncthreads();
 
   float* dgh_dir = a.dgh + (size_t)dir * B * T * 3 * H;   // [B][T][3H] of this direction
-  const __amdgpu_buffer_rsrc_t rg_ = rsrc(dgh_dir);
-  const int arow = min(b0 + wave * 16 + lr, b_last);
+  const int Gp = a.G;
+  const __amdgpu_buffer_rsrc_t rg_ = rsrc(a.xbuf + (size_t)dir * 2 * Gp * 64 * 3 * H);   // [2][Gp][4][3H/16][64][4]
   float dhz[4] = {0.f, 0.f, 0.f, 0.f};
 
   for (int step = 0; step < T; ++step) {
@@ -253,27 +288,39 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
     if (step > 0) {
       wait_count(cnt, (unsigned)(H / kUnits) * step);
       stamp(a, step, 1);
-      const unsigned base = (unsigned)((((size_t)arow * T + tnext) * 3 * H + 4 * lq) * 4);
+      const unsigned base = (unsigned)(((((size_t)((step - 1) & 1) * Gp + group) * 4 + wave) * NKB * 64 + lane) * 16);
+      // k rotation per slice (see the forward kernel): block index kr(i) = (i + rot) mod NKB
+      const int rot = (slice * (NKB / (H / kUnits))) % NKB;
+      auto kr = [&](int i) { const int v = i + rot; return v >= NKB ? v - NKB : v; };
       v4f dv[2][CH];
 #pragma unroll
-      for (int kb = 0; kb < CH; ++kb) dv[0][kb] = ld4_sc1(rg_, base + kb * 64);
+      for (int kb = 0; kb < CH; ++kb) dv[0][kb] = ld4_sc1(rg_, base + kr(kb) * 1024);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ch = 0; ch < NKB / CH; ++ch) {
         const int cur = ch & 1;
         if (ch + 1 < NKB / CH) {
 #pragma unroll
-          for (int kb = 0; kb < CH; ++kb) dv[cur ^ 1][kb] = ld4_sc1(rg_, base + ((ch + 1) * CH + kb) * 64);
+          for (int kb = 0; kb < CH; ++kb) dv[cur ^ 1][kb] = ld4_sc1(rg_, base + kr((ch + 1) * CH + kb) * 1024);
         }
         __builtin_amdgcn_sched_barrier(0);   // next chunk's loads in flight before this chunk's MFMAs
+        v4f wv[2];
+        wv[0] = ld4(Wt + lr * WP + kr(ch * CH) * 16 + 4 * lq);
 #pragma unroll
         for (int kb = 0; kb < CH; ++kb) {
-          const v4f wv = ld4(Wt + lr * WP + (ch * CH + kb) * 16 + 4 * lq);
-          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][kb].x, wv.x, acc[0], 0, 0, 0);
-          acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][kb].y, wv.y, acc[1], 0, 0, 0);
-          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][kb].z, wv.z, acc[0], 0, 0, 0);
-          acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][kb].w, wv.w, acc[1], 0, 0, 0);
+          const int c = kb & 1;
+          if (kb + 1 < CH) wv[c ^ 1] = ld4(Wt + lr * WP + kr(ch * CH + kb + 1) * 16 + 4 * lq);
+          __builtin_amdgcn_sched_barrier(0);
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][kb].x, wv[c].x, acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][kb].y, wv[c].y, acc[1], 0, 0, 0);
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][kb].z, wv[c].z, acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][kb].w, wv[c].w, acc[1], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
         }
+      }
+      if (a.trace) {
+        asm volatile("" ::"v"(acc[0][0]), "v"(acc[1][0]));
+        stamp(a, step, 2);
       }
     }
 #pragma unroll
@@ -298,7 +345,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
       }
     }
     __syncthreads();
-    stamp(a, step, 2);
+    stamp(a, step, 3);
     // dgh row slice (gates x 16 units) of 64 rows: 768 float4, 3 per thread.  Interior steps go
     // write-through into dgh (the next step's operand); the edge step has no consumer: it goes to
     // dgh_edge and zeroes its dgh row (kept out of the dW_hh GEMM, see srk_gru_layer_bwd).
@@ -308,14 +355,16 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
       if (b > b_last) continue;
       const v4f val = ld4(dT + (rl * 3 + g) * DTP + uq);
       if (!edge) {
-        st4_sc1(rg_, (unsigned)((((size_t)b * T + t) * 3 * H + g * H + j0 + uq) * 4), val);
+        st4_sc1(rg_, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB * 64 +
+                                 (g * (H / 16) + slice) * 64 + (uq >> 2) * 16 + (rl & 15)) * 16), val);
+        st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + j0 + uq, val);
       } else {
         st4(a.dgh_edge + ((size_t)dir * B + b) * 3 * H + g * H + j0 + uq, val);
         st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + j0 + uq, v4f{0.f, 0.f, 0.f, 0.f});
       }
     }
     arrive(cnt);
-    stamp(a, step, 3);
+    stamp(a, step, 4);
   }
 }
 

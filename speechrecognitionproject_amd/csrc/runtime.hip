@@ -272,7 +272,7 @@ int srk_set_option(const char* name, int64_t value) {
     srk::g_opt_gru_persistent = value != 0;
     return SRK_OK;
   }
-  if (n == "gru_trace_ptr") {   // diagnostics: device buffer of 4 x u64 per (workgroup, step), 0 = off
+  if (n == "gru_trace_ptr") {   // diagnostics: device buffer of 8 x u64 per (workgroup, step), 0 = off
     srk::g_opt_gru_trace = reinterpret_cast<unsigned long long*>(value);
     return SRK_OK;
   }

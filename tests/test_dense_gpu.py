@@ -131,10 +131,10 @@ def test_colsum_large(gpu):
 
 @pytest.mark.parametrize("B,T", [(1, 6), (67, 13), (256, 51), (300, 7)])
 def test_bigru_persistent_matches_per_step_and_torch(gpu, B, T):
-    """The one-launch persistent recurrence (H = 512) agrees with the per-step kernels (same MFMA
-    k order and cell math; only the compiler's fma contraction of the epilogue may differ, so
-    1e-6 relative, not bitwise) and matches torch's CPU GRU; B = 300 exercises the 256-row
-    chunking, B = 1 / 67 the clamped partial 64-row groups."""
+    """The one-launch persistent recurrence (H = 512) agrees with the per-step kernels (same cell
+    math; each workgroup walks the recurrent k sum in its own rotated order, so fp32 rounding
+    differs: 2e-5 relative) and matches torch's CPU GRU; B = 300 exercises the 256-row chunking,
+    B = 1 / 67 the clamped partial 64-row groups."""
     from speechrecognitionproject_amd import _lib
     IN, H = 24, 512
     torch.manual_seed(3)
@@ -157,7 +157,7 @@ def test_bigru_persistent_matches_per_step_and_torch(gpu, B, T):
     assert _lib.spin_timeouts() == 0
     for i, (a, b) in enumerate(zip(outs[1], outs[0])):
         err = float((a - b).abs().max() / (b.abs().max() + 1e-30))
-        assert err <= 1e-6, (i, err)
+        assert err <= 2e-5, (i, err)
     if B * T <= 4000:
         xr = x.clone().requires_grad_(True)
         yr, _ = ref(xr)

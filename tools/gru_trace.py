@@ -1,8 +1,9 @@
 """Per-step timeline of the persistent GRU kernels (srk_set_option("gru_trace_ptr")).
 
 Runs one BiGRU(39 -> 512, 1 layer) fwd + bwd at B = 256, T = 51 with tracing on and prints, per
-kernel, the mean over workgroups and steps of: wait (step start -> arrival wait done), body
-(-> epilogue done: h / dg loads, MFMAs, cell math), publish (-> arrival), in microseconds.
+kernel, the mean over workgroups and steps of: wait (step start -> arrival wait done), loads_mfma
+(-> the MFMAs retired: h / dg loads + matrix work), epilogue (-> cell math + LDS transpose done),
+publish (-> arrival), in microseconds.
 """
 import json
 import os
@@ -20,7 +21,7 @@ res = {}
 m = snn.BiGRU(IN, H, 1).cuda()
 x = torch.randn(B, T, IN, device="cuda", requires_grad=True)
 for it in range(3):
-    buf = torch.zeros(nwg * T * 4, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(nwg * T * 8, dtype=torch.int64, device="cuda")
     _lib.set_option("gru_trace_ptr", buf.data_ptr() if it == 2 else 0)
     y, _ = m(x)
     torch.cuda.synchronize()
@@ -31,12 +32,13 @@ for it in range(3):
     bwd = buf.clone()
 _lib.set_option("gru_trace_ptr", 0)
 for name, b in (("fwd", fwd), ("bwd", bwd)):
-    ts = b.view(nwg, T, 4).double().cpu() * 0.01   # 100 MHz ticks -> us
+    ts = b.view(nwg, T, 8).double().cpu() * 0.01   # 100 MHz ticks -> us
     wait = (ts[:, 1:, 1] - ts[:, 1:, 0]).mean().item()
-    body = (ts[:, 1:, 2] - ts[:, 1:, 1]).mean().item()
-    pub = (ts[:, 1:, 3] - ts[:, 1:, 2]).mean().item()
-    step = ((ts[:, -1, 3] - ts[:, 0, 0]) / T).mean().item()
+    mfma = (ts[:, 1:, 2] - ts[:, 1:, 1]).mean().item()
+    epi = (ts[:, 1:, 3] - ts[:, 1:, 2]).mean().item()
+    pub = (ts[:, 1:, 4] - ts[:, 1:, 3]).mean().item()
+    step = ((ts[:, -1, 4] - ts[:, 0, 0]) / T).mean().item()
     start_skew = (ts[:, 0, 0].max() - ts[:, 0, 0].min()).item()
-    res[name] = {"us_per_step": round(step, 2), "wait": round(wait, 2), "body": round(body, 2),
-                 "publish": round(pub, 2), "launch_skew_us": round(start_skew, 2)}
+    res[name] = {"us_per_step": round(step, 2), "wait": round(wait, 2), "loads_mfma": round(mfma, 2),
+                 "epilogue": round(epi, 2), "publish": round(pub, 2), "launch_skew_us": round(start_skew, 2)}
 print(json.dumps(res))

@@ -104,6 +104,19 @@ def cpu_baseline(model_name, batch, seconds):
                       "fp32 model fwd/bwd + Adam), %.1f s, %s" % (n, batch, model_name, el, cpu)}
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of the same bench command
+    (tools/pmc_traffic.py over separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected),
+    or None if no summary is committed."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            v = json.load(f)["bytes_per_launch"].get(kernel)
+        return None if v is None else v["total"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def feature_roofline(model_name, n_clips=65536):
     """The model's feature kernel alone on a large batch (HBM-bound): algorithmic bytes / time."""
     name, per_clip = FEATURE[model_name]
@@ -224,7 +237,8 @@ def main():
         k = mm[dom]
         tf = k["work"] / (k["ms_total"] * 1e-3) / 1e12
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(tf / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(tf / PEAK_FP32_MFMA_TFLOPS, 4),
+                "traffic": pmc_traffic(dom) if args.model == "mfcc_bgru" else None, "traffic_unit": "bytes/launch",
                 "avg_launch_ms": round(k["ms_total"] / k["launches"], 5),
                 "flops_per_launch": k["work"] / k["launches"]}
     res = {

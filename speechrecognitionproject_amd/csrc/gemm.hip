@@ -363,12 +363,14 @@ int gemm_f32(const GemmDesc& d, hipStream_t s) {
   SRK_REQUIRE(d.C && (d.K == 0 || (d.A && d.B)), SRK_ERR_INVALID, "gemm: null operand");
   SRK_REQUIRE(d.bias_mode == 0 || d.bias, SRK_ERR_INVALID, "gemm: bias_mode without bias");
   SRK_REQUIRE(!d.rowsum || d.batch == 1, SRK_ERR_INVALID, "gemm: rowsum needs batch == 1");
-  // 16-B loads need 16-B aligned rows, K % 4 == 0 (a clamped k vector stays inside the row) and,
+  // 16-B loads need 16-B aligned rows, K % 4 == 0 when an operand is k-contiguous (a clamped k vector
+  // stays inside the row) and,
   // along M / N (A when ta, B when !tb), a row count that is a multiple of 4 (a clamped vector is
   // wholly in or wholly out of range).  Otherwise the kernel stages with 4-B loads.
+  const bool kc_operand = !d.ta || d.tb;   // some operand is k-contiguous: its vectors run along k
   const bool vec = (d.lda % 4 == 0) && ((uintptr_t)d.A % 16 == 0) && (d.sA % 4 == 0) && (d.ldb % 4 == 0) &&
-                   ((uintptr_t)d.B % 16 == 0) && (d.sB % 4 == 0) && (d.K % 4 == 0) && (!d.ta || d.M % 4 == 0) &&
-                   (d.tb || d.N % 4 == 0);
+                   ((uintptr_t)d.B % 16 == 0) && (d.sB % 4 == 0) && (!kc_operand || d.K % 4 == 0) &&
+                   (!d.ta || d.M % 4 == 0) && (d.tb || d.N % 4 == 0);
   if (!d.ta && !d.tb) return dispatch_tile<false, false>(d, s, vec);
   if (!d.ta && d.tb) return dispatch_tile<false, true>(d, s, vec);
   if (d.ta && !d.tb) return dispatch_tile<true, false>(d, s, vec);
@@ -378,8 +380,9 @@ int gemm_f32(const GemmDesc& d, hipStream_t s) {
 int colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, float beta, hipStream_t s) {
   if (N == 0) return SRK_OK;
   const int64_t cblocks = (N + 63) / 64;
+  // split the rows when there are too few column blocks to fill the chip (>= 32 rows per split)
   int64_t rsplit = 1;
-  if (cblocks < 256 && M >= 2048) rsplit = std::min<int64_t>((512 + cblocks - 1) / cblocks, (M + 511) / 512);
+  if (cblocks < 256 && M >= 64) rsplit = std::min<int64_t>((512 + cblocks - 1) / cblocks, (M + 31) / 32);
   if (rsplit <= 1) {
     hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)cblocks, 1), dim3(256), 0, s, X, M, N, ldx, out, beta, M,
                        (float*)nullptr);

@@ -1,0 +1,61 @@
+"""Per-launch HBM traffic of the bench kernels from rocprofv3 PMC passes -> profiles/pmc_traffic.json.
+
+    python tools/pmc_traffic.py FETCH_DIR WRITE_DIR [-o profiles/pmc_traffic.json]
+
+FETCH_SIZE / WRITE_SIZE come from two separate `rocprofv3 --kernel-trace --pmc ...` runs of the same
+bench command.  Corrections per MI355X_MICROARCH.md (HBM section, gfx950): FETCH_SIZE (KiB) x 2
+(wide 128-B streaming reads are tallied at 64 B), WRITE_SIZE as reported.  Kernels are grouped
+under the names bench.py / srk_prof use ("gemm_f32" = every gemm_f32_kernel instantiation, ...);
+the value is total bytes / launches, i.e. the same per-launch average as the bench's 'achieved'.
+"""
+import argparse
+import glob
+import json
+import os
+import sqlite3
+
+GROUPS = {  # srk_prof name -> substring of the rocprof kernel symbol
+    "gemm_f32": "gemm_f32_kernel", "gru_fwd_seq": "gru_fwd_persistent_kernel",
+    "gru_bwd_seq": "gru_bwd_persistent_kernel", "gru_fwd_step": "gru_fwd_step_kernel",
+    "gru_bwd_step": "gru_bwd_step_kernel", "mfcc": "mfcc2_kernel", "fbank": "fbank_kernel", "spec": "spec_kernel",
+    "conv_fwd": "conv_gemm_kernel<0", "conv_dgrad": "conv_gemm_kernel<1", "conv_wgrad": "conv_gemm_kernel<2",
+    "adam": "adam_kernel", "noise_mix": "noise_mix_kernel",
+}
+
+
+def collect(d, counter):
+    db = sorted(glob.glob(os.path.join(d, "**", "*.db"), recursive=True))[0]
+    c = sqlite3.connect(db)
+    out = {}
+    for name, n, tot in c.execute("select kernel_name, count(*), sum(value) from counters_collection where "
+                                  "counter_name = ? group by kernel_name", (counter,)):
+        for g, sub in GROUPS.items():
+            if sub in name:
+                a = out.setdefault(g, [0, 0.0])
+                a[0] += n
+                a[1] += tot
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("-o", default="profiles/pmc_traffic.json")
+    ap.add_argument("--source", default="")
+    a = ap.parse_args()
+    f, w = collect(a.fetch, "FETCH_SIZE"), collect(a.write, "WRITE_SIZE")
+    res = {"source": a.source, "correction": "FETCH_SIZE KiB x 2 x 1024 + WRITE_SIZE KiB x 1024 (gfx950)",
+           "bytes_per_launch": {}}
+    for g in sorted(set(f) & set(w)):
+        fb = 2.0 * 1024.0 * f[g][1] / f[g][0]
+        wb = 1024.0 * w[g][1] / w[g][0]
+        res["bytes_per_launch"][g] = {"fetch": round(fb), "write": round(wb), "total": round(fb + wb),
+                                      "launches": f[g][0]}
+    with open(a.o, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -127,10 +127,11 @@ class _Block(nn.Module):
 
 
 class _ResNet1d(nn.Module):
-    def __init__(self):
+    def __init__(self, stem=(80, 16, 38), backend=True):
         super().__init__()
         self.inplanes = 64
-        self.conv1 = nn.Conv1d(1, 64, kernel_size=80, stride=16, padding=38, bias=False)
+        k, st, pd = stem
+        self.conv1 = nn.Conv1d(1, 64, kernel_size=k, stride=st, padding=pd, bias=False)
         self.bn1 = nn.BatchNorm1d(64)
         self.relu = nn.ReLU(inplace=True)
         self.layer1 = self._layer(64, 2)
@@ -138,6 +139,8 @@ class _ResNet1d(nn.Module):
         self.layer3 = self._layer(256, 2, 2)
         self.layer4 = self._layer(512, 2, 2)
         self.fc1 = nn.Linear(512, 512)
+        if not backend:   # model_mfrn_bgru.py:49-66 has no auxiliary head
+            return
         dim = 125   # the mode==1 backend exists in the state_dict (model_resnet_bgru.py:57-71)
         self.backend_conv1 = nn.Sequential(
             nn.Conv1d(dim, 2 * dim, 5, 2, 0, bias=False), nn.BatchNorm1d(2 * dim), nn.ReLU(True),
@@ -164,9 +167,10 @@ class _ResNet1d(nn.Module):
 
 
 class _GRUHead(nn.Module):
-    def __init__(self, num_features=512, num_layers=2):
+    def __init__(self, num_features=512, num_layers=2, input_size=512):
         super().__init__()
-        self.gru = nn.GRU(512, hidden_size=num_features, num_layers=num_layers, bidirectional=True, batch_first=True)
+        self.gru = nn.GRU(input_size, hidden_size=num_features, num_layers=num_layers, bidirectional=True,
+                          batch_first=True)
         self.fc2 = nn.Linear(num_features * 2, NUM_CLASSES)
 
     def forward(self, x):
@@ -183,6 +187,27 @@ class ResnetBGRU(nn.Module):
 
     def forward(self, x):
         return self.gru(self.resnet(x.float().unsqueeze(1)))
+
+
+# ---------------------------------------------------------------- model_mfrn_bgru.py:11-140
+class MfrnBGRU(nn.Module):
+    """MFCC [51, 39] (per clip, as compute_mfcc) concatenated with a raw-wave ResNet-1D (stem
+    Conv1d(1, 64, 640, stride 40, padding 320) -> 401 -> 51 steps) + fc1, then BiGRU(551) + fc2."""
+
+    def __init__(self, num_features=512, num_layers=2):
+        super().__init__()
+        self.resnet = _ResNet1d(stem=(640, 40, 320), backend=False)
+        self.gru = _GRUHead(num_features, num_layers, input_size=551)
+
+    @staticmethod
+    def features(x):
+        return torch.from_numpy(np.stack([F.compute_mfcc(c) for c in x.numpy()]))
+
+    def forward(self, x):
+        with torch.no_grad():
+            mf = self.features(x).transpose(1, 2)               # [B, 51, 39] (:128-131)
+        r = self.resnet(x.float().unsqueeze(1))                 # [B, 51, 512] (:133)
+        return self.gru(torch.cat((r, mf), 2))                  # (:135-136)
 
 
 def train_step(model, x, labels, lr=1e-4, optimizer=None):

@@ -77,7 +77,20 @@ def sample_entries(t, n=256, seed=99):
     return idx, flat[idx].copy()
 
 
+ONLY = set(sys.argv[1:])   # optional subset of fixture file names to (re)write
+if ONLY:
+    _savez = np.savez_compressed
+
+    def _savez_only(path, **kw):
+        if os.path.basename(path) in ONLY:
+            _savez(path, **kw)
+
+    np.savez_compressed = _savez_only
+
+
 def model_golden(name, net, x, labels, train_mode=False):
+    if ONLY and name not in ONLY:
+        return
     sd = OM.seeded_state_dict(net, seed=0)
     net.load_state_dict(sd)
     net.train(train_mode)
@@ -110,6 +123,7 @@ def main():
     import model_spec_bgru as R_sb
     import model_spec_cnn as R_sc
     import model_mfcc_bgru as R_mb
+    import model_mfrn_bgru as R_mr
     import model_resnet_bgru as R_rb
     import dataset as R_ds
     torch.set_default_dtype(torch.float32)
@@ -182,6 +196,9 @@ def main():
     model_golden("spec_bgru_golden.npz", R_sb.Network(), x, y)
     x2, y2 = synthetic_clips(2, seed=6)
     model_golden("resnet_bgru_golden.npz", R_rb.Network(), x2, y2, train_mode=True)
+    x3, y3 = synthetic_clips(2, seed=7)
+    torch.manual_seed(0)
+    model_golden("mfrn_bgru_golden.npz", R_mr.Network(), x3, y3, train_mode=True)
 
 
 if __name__ == "__main__":

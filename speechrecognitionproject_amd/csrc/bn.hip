@@ -3,8 +3,9 @@
 // downsample branches (:67-70).
 //
 // Training mode uses the batch statistics (biased variance for the normalisation, unbiased for the
-// running estimate, momentum 0.1 as nn.BatchNorm1d), computed in two deterministic passes
-// (mean, then centred sum of squares) from per-row-chunk partial sums reduced in a fixed order.
+// running estimate, momentum 0.1 as nn.BatchNorm1d), computed in ONE pass: per-thread shifted sums
+// -> per-chunk (mean, M2) -> Chan's pairwise combination in a fixed order (deterministic, and
+// accurate without a second centred pass).  All element kernels move 16 B per lane.
 // Eval mode normalises with the running statistics.
 //   y = act( (x - mean) * invstd * gamma + beta  [+ residual] ),  act = ReLU or identity
 // Backward (training statistics):
@@ -17,71 +18,106 @@
 namespace srk {
 namespace {
 
-constexpr int kChunkRows = 256;   // rows per partial-sum block
+typedef float v4f __attribute__((ext_vector_type(4)));
 
-// partial[chunk][c] = sum over the chunk's rows of f(x[r][c]) with f = x (mode 0) or (x - mean)^2
-// (mode 1) or dy*act' (mode 2: two outputs, g and g*xhat).
-__global__ __launch_bounds__(256) void bn_partial_kernel(const float* __restrict__ x, const float* __restrict__ y,
-                                                         const float* __restrict__ dy, int64_t M, int C,
-                                                         const float* __restrict__ mean,
-                                                         const float* __restrict__ invstd, int relu, int mode,
-                                                         float* __restrict__ part0, float* __restrict__ part1) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rp = threadIdx.x >> 6;
-  const int64_t r0 = (int64_t)blockIdx.y * kChunkRows;
-  const int64_t r1 = r0 + kChunkRows < M ? r0 + kChunkRows : M;
-  __shared__ float s0[4][64], s1[4][64];
-  float a0 = 0.f, a1 = 0.f;
-  if (c < C) {
-    const float mu = mode >= 1 ? mean[c] : 0.f;
-    const float is = mode == 2 ? invstd[c] : 0.f;
-    for (int64_t r = r0 + rp; r < r1; r += 4) {
-      const float v = x[r * C + c];
-      if (mode == 0) {
-        a0 += v;
-      } else if (mode == 1) {
-        const float d = v - mu;
-        a0 += d * d;
-      } else {
-        float g = dy[r * C + c];
-        if (relu && y[r * C + c] <= 0.f) g = 0.f;
-        a0 += g;
-        a1 += g * (v - mu) * is;
-      }
+// Work split: a block = 256 threads = CQ channel quads (4 channels each, 16-B accesses) x RP row
+// phases; blockIdx.x walks channel groups of 4*CQ channels, blockIdx.y row chunks.  The chunk count
+// is capped (kMaxChunks) so the per-channel finalize reads a short, fixed-order list of partials.
+constexpr int kMaxChunks = 256;
+
+struct BnGeom {
+  int C, C4, CQ, RP;   // channels, channel quads, quads per block, row phases per block
+  int64_t M, rows_per_chunk;
+  int chunks;
+};
+
+inline BnGeom bn_geom(int64_t M, int C) {
+  BnGeom g;
+  g.M = M;
+  g.C = C;
+  g.C4 = C / 4;
+  g.CQ = g.C4 < 64 ? g.C4 : 64;
+  g.RP = 256 / g.CQ;
+  int64_t rows = (M + kMaxChunks - 1) / kMaxChunks;
+  rows = ((rows + g.RP - 1) / g.RP) * g.RP;
+  g.rows_per_chunk = rows < g.RP ? g.RP : rows;
+  g.chunks = (int)((M + g.rows_per_chunk - 1) / g.rows_per_chunk);
+  return g;
+}
+
+__device__ __forceinline__ v4f ld4(const float* p) { return *reinterpret_cast<const v4f*>(p); }
+__device__ __forceinline__ void st4(float* p, v4f v) { *reinterpret_cast<v4f*>(p) = v; }
+
+// Chan et al. pairwise combination of (count, mean, M2) — fixed call order => deterministic.
+__device__ __forceinline__ void chan(float& n, float& mu, float& m2, float nb, float mub, float m2b) {
+  if (nb == 0.f) return;
+  if (n == 0.f) { n = nb; mu = mub; m2 = m2b; return; }
+  const float nt = n + nb, d = mub - mu;
+  mu += d * (nb / nt);
+  m2 += m2b + d * d * (n * nb / nt);
+  n = nt;
+}
+
+// Training statistics, one pass: per thread shifted sums (pivot = the chunk's first row) for its
+// 4 channels over its row phase, turned into (n, mean, M2) and combined across row phases in LDS
+// (fixed order).  Output per chunk: mean and M2 per channel.
+__global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__ x, BnGeom g,
+                                                       float* __restrict__ pmean, float* __restrict__ pm2) {
+  const int q = threadIdx.x % g.CQ, rp = threadIdx.x / g.CQ;
+  const int c4 = blockIdx.x * g.CQ + q;
+  const int64_t r0 = (int64_t)blockIdx.y * g.rows_per_chunk;
+  const int64_t r1 = r0 + g.rows_per_chunk < g.M ? r0 + g.rows_per_chunk : g.M;
+  __shared__ float sn[256], smu[256][4], sm2[256][4];
+  v4f s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+  float n = 0.f;
+  v4f piv = {0.f, 0.f, 0.f, 0.f};
+  if (c4 < g.C4) {
+    piv = ld4(x + r0 * g.C + c4 * 4);
+    for (int64_t r = r0 + rp; r < r1; r += g.RP) {
+      const v4f d = ld4(x + r * g.C + c4 * 4) - piv;
+      s1 += d;
+      s2 += d * d;
+      n += 1.f;
     }
   }
-  s0[rp][threadIdx.x & 63] = a0;
-  s1[rp][threadIdx.x & 63] = a1;
+  sn[threadIdx.x] = n;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float m = n > 0.f ? s1[e] / n : 0.f;
+    smu[threadIdx.x][e] = piv[e] + m;
+    sm2[threadIdx.x][e] = n > 0.f ? s2[e] - s1[e] * m : 0.f;
+  }
   __syncthreads();
-  if (rp == 0 && c < C) {
-    const int l = threadIdx.x & 63;
-    part0[(int64_t)blockIdx.y * C + c] = (s0[0][l] + s0[1][l]) + (s0[2][l] + s0[3][l]);
-    if (mode == 2) part1[(int64_t)blockIdx.y * C + c] = (s1[0][l] + s1[1][l]) + (s1[2][l] + s1[3][l]);
+  if (rp == 0 && c4 < g.C4) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float nn = 0.f, mu = 0.f, m2 = 0.f;
+      for (int k = 0; k < g.RP; ++k) chan(nn, mu, m2, sn[k * g.CQ + q], smu[k * g.CQ + q][e], sm2[k * g.CQ + q][e]);
+      pmean[(int64_t)blockIdx.y * g.C + c4 * 4 + e] = mu;
+      pm2[(int64_t)blockIdx.y * g.C + c4 * 4 + e] = m2;
+    }
   }
 }
 
-// Sum the chunk partials in order; finalize per-channel statistics.
-__global__ void bn_finalize_mean_kernel(const float* __restrict__ part, int chunks, int C, int64_t M,
-                                        float* __restrict__ mean) {
+// Combine the chunk partials in order; biased variance for the normalisation, unbiased for the
+// running estimate (nn.BatchNorm1d, momentum update).
+__global__ void bn_finalize_kernel(const float* __restrict__ pmean, const float* __restrict__ pm2, BnGeom g,
+                                   float eps, float momentum, float* __restrict__ mean, float* __restrict__ invstd,
+                                   float* __restrict__ running_mean, float* __restrict__ running_var) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int k = 0; k < chunks; ++k) s += part[(int64_t)k * C + c];
-  mean[c] = s / (float)M;
-}
-
-__global__ void bn_finalize_var_kernel(const float* __restrict__ part, int chunks, int C, int64_t M, float eps,
-                                       float momentum, const float* __restrict__ mean, float* __restrict__ invstd,
-                                       float* __restrict__ running_mean, float* __restrict__ running_var) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int k = 0; k < chunks; ++k) s += part[(int64_t)k * C + c];
-  const float var = s / (float)M;
+  if (c >= g.C) return;
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  for (int k = 0; k < g.chunks; ++k) {
+    const int64_t r0 = (int64_t)k * g.rows_per_chunk;
+    const float nb = (float)((r0 + g.rows_per_chunk < g.M ? g.rows_per_chunk : g.M - r0));
+    chan(n, mu, m2, nb, pmean[(int64_t)k * g.C + c], pm2[(int64_t)k * g.C + c]);
+  }
+  const float var = m2 / (float)g.M;
+  mean[c] = mu;
   invstd[c] = 1.0f / sqrtf(var + eps);
   if (running_mean) {
-    const float unbiased = M > 1 ? s / (float)(M - 1) : var;
-    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean[c];
+    const float unbiased = g.M > 1 ? m2 / (float)(g.M - 1) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mu;
     running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
   }
 }
@@ -90,13 +126,17 @@ __global__ void bn_apply_kernel(const float* __restrict__ x, int64_t M, int C, c
                                 const float* __restrict__ invstd, const float* __restrict__ gamma,
                                 const float* __restrict__ beta, const float* __restrict__ residual, int relu,
                                 float* __restrict__ y) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= M * C) return;
-  const int c = (int)(i % C);
-  float v = (x[i] - mean[c]) * invstd[c] * gamma[c] + beta[c];
-  if (residual) v += residual[i];
-  if (relu) v = v > 0.f ? v : 0.f;
-  y[i] = v;
+  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i4 * 4 >= M * C) return;
+  const int c = (int)((i4 * 4) % C);
+  const v4f mu = ld4(mean + c), is = ld4(invstd + c), ga = ld4(gamma + c), be = ld4(beta + c);
+  v4f v = (ld4(x + i4 * 4) - mu) * is * ga + be;
+  if (residual) v += ld4(residual + i4 * 4);
+  if (relu) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+  }
+  st4(y + i4 * 4, v);
 }
 
 __global__ void bn_eval_stats_kernel(const float* __restrict__ rm, const float* __restrict__ rv, int C, float eps,
@@ -105,6 +145,46 @@ __global__ void bn_eval_stats_kernel(const float* __restrict__ rm, const float* 
   if (c >= C) return;
   mean[c] = rm[c];
   invstd[c] = 1.0f / sqrtf(rv[c] + eps);
+}
+
+// Backward partials: per chunk and channel, sum g and sum g * xhat, g = dy * act'(y).
+__global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                             const float* __restrict__ dy, BnGeom g,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd, int relu,
+                                                             float* __restrict__ p0, float* __restrict__ p1) {
+  const int q = threadIdx.x % g.CQ, rp = threadIdx.x / g.CQ;
+  const int c4 = blockIdx.x * g.CQ + q;
+  const int64_t r0 = (int64_t)blockIdx.y * g.rows_per_chunk;
+  const int64_t r1 = r0 + g.rows_per_chunk < g.M ? r0 + g.rows_per_chunk : g.M;
+  __shared__ v4f s0[256], s1[256];
+  v4f a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+  if (c4 < g.C4) {
+    const v4f mu = ld4(mean + c4 * 4), is = ld4(invstd + c4 * 4);
+    for (int64_t r = r0 + rp; r < r1; r += g.RP) {
+      const int64_t o = r * g.C + c4 * 4;
+      v4f gr = ld4(dy + o);
+      if (relu) {
+        const v4f yv = ld4(y + o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gr[e] = yv[e] <= 0.f ? 0.f : gr[e];
+      }
+      a0 += gr;
+      a1 += gr * ((ld4(x + o) - mu) * is);
+    }
+  }
+  s0[threadIdx.x] = a0;
+  s1[threadIdx.x] = a1;
+  __syncthreads();
+  if (rp == 0 && c4 < g.C4) {
+    v4f t0 = {0.f, 0.f, 0.f, 0.f}, t1 = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < g.RP; ++k) {
+      t0 += s0[k * g.CQ + q];
+      t1 += s1[k * g.CQ + q];
+    }
+    st4(p0 + (int64_t)blockIdx.y * g.C + c4 * 4, t0);
+    st4(p1 + (int64_t)blockIdx.y * g.C + c4 * 4, t1);
+  }
 }
 
 __global__ void bn_dgamma_kernel(const float* __restrict__ p0, const float* __restrict__ p1, int chunks, int C,
@@ -125,19 +205,26 @@ __global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restric
                              const float* __restrict__ gamma, const float* __restrict__ dbeta,
                              const float* __restrict__ dgamma, int relu, int train, float* __restrict__ dx,
                              float* __restrict__ dres) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= M * C) return;
-  const int c = (int)(i % C);
-  float g = dy[i];
-  if (relu && y[i] <= 0.f) g = 0.f;
-  if (dres) dres[i] = g;
+  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i4 * 4 >= M * C) return;
+  const int64_t o = i4 * 4;
+  const int c = (int)(o % C);
+  v4f gr = ld4(dy + o);
+  if (relu) {
+    const v4f yv = ld4(y + o);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gr[e] = yv[e] <= 0.f ? 0.f : gr[e];
+  }
+  if (dres) st4(dres + o, gr);
   if (!dx) return;
-  const float is = invstd[c];
+  const v4f is = ld4(invstd + c), ga = ld4(gamma + c);
   if (train) {
-    const float xhat = (x[i] - mean[c]) * is;
-    dx[i] = gamma[c] * is / (float)M * ((float)M * g - dbeta[c] - xhat * dgamma[c]);
+    const v4f xhat = (ld4(x + o) - ld4(mean + c)) * is;
+    const float inv_m = 1.0f / (float)M;
+    const v4f db = ld4(dbeta + c), dg = ld4(dgamma + c);
+    st4(dx + o, ga * is * inv_m * ((float)M * gr - db - xhat * dg));
   } else {
-    dx[i] = gamma[c] * is * g;
+    st4(dx + o, ga * is * gr);
   }
 }
 
@@ -175,28 +262,26 @@ int srk_batchnorm_fwd(const float* x, int64_t M, int64_t C, const float* gamma, 
                       int relu, float* y, float* save_mean, float* save_invstd, void* stream) {
   SRK_API_BEGIN
   SRK_REQUIRE(M > 0 && C > 0 && C <= (1 << 24), SRK_ERR_INVALID, "batchnorm: bad shape");
+  SRK_REQUIRE(C % 4 == 0, SRK_ERR_INVALID, "batchnorm: channels must be a multiple of 4");
   SRK_REQUIRE(x && gamma && beta && y && save_mean && save_invstd && running_mean && running_var, SRK_ERR_INVALID,
               "batchnorm: null pointer");
   hipStream_t s = srk::as_stream(stream);
   srk::ProfScope prof("batchnorm_fwd", s, (training ? 12.0 : 8.0) * (double)M * C);
-  const unsigned cb = (unsigned)((C + 63) / 64);
-  const int64_t chunks = (M + srk::kChunkRows - 1) / srk::kChunkRows;
+  const srk::BnGeom g = srk::bn_geom(M, (int)C);
   if (training) {
     float* part = nullptr;
-    if (int rc = srk::bn_scratch((size_t)chunks * C, &part)) return rc;
-    hipLaunchKernelGGL(srk::bn_partial_kernel, dim3(cb, (unsigned)chunks), dim3(256), 0, s, x, nullptr, nullptr, M,
-                       (int)C, nullptr, nullptr, 0, 0, part, nullptr);
-    hipLaunchKernelGGL(srk::bn_finalize_mean_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
-                       (int)chunks, (int)C, M, save_mean);
-    hipLaunchKernelGGL(srk::bn_partial_kernel, dim3(cb, (unsigned)chunks), dim3(256), 0, s, x, nullptr, nullptr, M,
-                       (int)C, save_mean, nullptr, 0, 1, part, nullptr);
-    hipLaunchKernelGGL(srk::bn_finalize_var_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
-                       (int)chunks, (int)C, M, eps, momentum, save_mean, save_invstd, running_mean, running_var);
+    if (int rc = srk::bn_scratch((size_t)2 * g.chunks * C, &part)) return rc;
+    hipLaunchKernelGGL(srk::bn_stats_kernel, dim3((unsigned)((g.C4 + g.CQ - 1) / g.CQ), (unsigned)g.chunks), dim3(256),
+                       0, s, x, g, part, part + (size_t)g.chunks * C);
+    hipLaunchKernelGGL(srk::bn_finalize_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
+                       part + (size_t)g.chunks * C, g, eps, momentum, save_mean, save_invstd, running_mean,
+                       running_var);
   } else {
     hipLaunchKernelGGL(srk::bn_eval_stats_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, running_mean,
                        running_var, (int)C, eps, save_mean, save_invstd);
   }
-  hipLaunchKernelGGL(srk::bn_apply_kernel, dim3((unsigned)((M * C + 255) / 256)), dim3(256), 0, s, x, M, (int)C,
+  const int64_t n4 = M * C / 4;
+  hipLaunchKernelGGL(srk::bn_apply_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, M, (int)C,
                      save_mean, save_invstd, gamma, beta, residual, relu, y);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
@@ -207,20 +292,20 @@ int srk_batchnorm_bwd(const float* x, const float* y, const float* dy, int64_t M
                       const float* save_mean, const float* save_invstd, int training, int relu, float* dx,
                       float* dgamma, float* dbeta, float* dresidual, void* stream) {
   SRK_API_BEGIN
-  SRK_REQUIRE(M > 0 && C > 0, SRK_ERR_INVALID, "batchnorm_bwd: bad shape");
+  SRK_REQUIRE(M > 0 && C > 0 && C % 4 == 0, SRK_ERR_INVALID, "batchnorm_bwd: bad shape (C % 4 == 0 required)");
   SRK_REQUIRE(x && y && dy && gamma && save_mean && save_invstd && dgamma && dbeta, SRK_ERR_INVALID,
               "batchnorm_bwd: null pointer");
   hipStream_t s = srk::as_stream(stream);
   srk::ProfScope prof("batchnorm_bwd", s, 16.0 * (double)M * C);
-  const unsigned cb = (unsigned)((C + 63) / 64);
-  const int64_t chunks = (M + srk::kChunkRows - 1) / srk::kChunkRows;
+  const srk::BnGeom g = srk::bn_geom(M, (int)C);
   float* part = nullptr;
-  if (int rc = srk::bn_scratch((size_t)2 * chunks * C, &part)) return rc;
-  hipLaunchKernelGGL(srk::bn_partial_kernel, dim3(cb, (unsigned)chunks), dim3(256), 0, s, x, y, dy, M, (int)C,
-                     save_mean, save_invstd, relu, 2, part, part + chunks * C);
+  if (int rc = srk::bn_scratch((size_t)2 * g.chunks * C, &part)) return rc;
+  hipLaunchKernelGGL(srk::bn_bwd_partial_kernel, dim3((unsigned)((g.C4 + g.CQ - 1) / g.CQ), (unsigned)g.chunks),
+                     dim3(256), 0, s, x, y, dy, g, save_mean, save_invstd, relu, part, part + (size_t)g.chunks * C);
   hipLaunchKernelGGL(srk::bn_dgamma_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
-                     part + chunks * C, (int)chunks, (int)C, dbeta, dgamma);
-  hipLaunchKernelGGL(srk::bn_dx_kernel, dim3((unsigned)((M * C + 255) / 256)), dim3(256), 0, s, x, y, dy, M, (int)C,
+                     part + (size_t)g.chunks * C, g.chunks, (int)C, dbeta, dgamma);
+  const int64_t n4 = M * C / 4;
+  hipLaunchKernelGGL(srk::bn_dx_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, y, dy, M, (int)C,
                      save_mean, save_invstd, gamma, dbeta, dgamma, relu, training, dx, dresidual);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;

@@ -1,7 +1,7 @@
 """Benchmark: utterances/s of the MFCC + BiGRU train step on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-                    [--model mfcc_bgru|fbanks_cnn|resnet_bgru|spec_bgru|mfrn_bgru]
+                    [--model mfcc_bgru|fbanks_cnn|resnet_bgru|spec_bgru|mfrn_bgru|cnn_bgru|spec_cnn]
                     [--batch B]
 
 --model selects the BASELINE.json config (default = configs[1], the metric's headline model):
@@ -11,6 +11,9 @@
   spec_bgru   cfg5: K4 noise-mix of int16 PCM with a resident noise bank + log spectrogram +
               model_spec_bgru, 512 per GPU
   mfrn_bgru   SURVEY.md §8f rank 1: MFCC (+) raw-wave ResNet-1D -> BiGRU(551), 256 per GPU
+  cnn_bgru    SURVEY.md §8f rank 3: raw-wave strided CNN (BN, ReLU) -> BiGRU(512) over 498 steps, 512 per GPU
+  spec_cnn    SURVEY.md §8f rank 3: on-device log spectrogram[49x321] + 4 Conv2d + pools + dropout + 2 FC,
+              512 per GPU
 
 For N > 1 the driver launches one process per GPU with torch.distributed.run; each rank takes its
 own shard of synthetic clips (weak scaling: per-GPU batch fixed) and the flat gradient buffer is
@@ -48,18 +51,23 @@ from speechrecognitionproject_amd.synthetic import synthetic_clips    # noqa: E4
 PEAK_FP32_MFMA_TFLOPS = 157.3     # MI355X_MICROARCH.md, dense fp32 matrix (= vector) peak
 PEAK_HBM_GBS = 8000.0             # MI355X HBM3E spec
 MFCC_BYTES_PER_CLIP = 71956       # 64,000 in + 7,956 out
+# FlopCounterMode on the reference modules (cnn_bgru / spec_cnn: on the oracle restatements)
 TRAIN_GFLOP_PER_UTT = {"mfcc_bgru": 1.9434, "fbanks_cnn": 2.1449, "resnet_bgru": 25.8191,
-                       "spec_bgru": 2.0367, "mfrn_bgru": 10.5777}   # FlopCounterMode on the reference modules
-DEFAULT_BATCH = {"mfcc_bgru": 256, "fbanks_cnn": 512, "resnet_bgru": 512, "spec_bgru": 512, "mfrn_bgru": 256}
+                       "spec_bgru": 2.0367, "mfrn_bgru": 10.5777, "cnn_bgru": 27.1020, "spec_cnn": 1.4726}
+DEFAULT_BATCH = {"mfcc_bgru": 256, "fbanks_cnn": 512, "resnet_bgru": 512, "spec_bgru": 512, "mfrn_bgru": 256,
+                 "cnn_bgru": 512, "spec_cnn": 512}
 CFG = {"mfcc_bgru": "cfg2 mfcc_bgru: on-device MFCC[39x51] + 2-layer BiGRU(512) + FC",
        "fbanks_cnn": "cfg3 fbanks_cnn: on-device log-mel fbank[98x120] + 4 Conv2d + pools + dropout + 2 FC",
        "resnet_bgru": "cfg4 resnet_bgru: raw-wave ResNet-1D (BN, ReLU) + Linear + 2-layer BiGRU(512) + FC",
        "spec_bgru": "cfg5 spec_bgru: on-device noise-mix (K4) + log spectrogram[49x321] + 2-layer BiGRU(512) + FC",
        "mfrn_bgru": "§8f-1 mfrn_bgru: on-device MFCC[51x39] (+) raw-wave ResNet-1D(k640/s40) + fc1 -> 2-layer "
-                    "BiGRU(551 -> 512) + FC"}
+                    "BiGRU(551 -> 512) + FC",
+       "cnn_bgru": "§8f-3 cnn_bgru: raw-wave Conv1d(k80/s4) + 3 Conv1d(k4/s2) (BN, ReLU) + fc -> 2-layer BiGRU(512) "
+                   "over 498 steps + FC",
+       "spec_cnn": "§8f-3 spec_cnn: on-device log spectrogram[49x321] + 4 Conv2d + pools + dropout + 2 FC"}
 # feature kernel of each model and its algorithmic bytes per clip
 FEATURE = {"mfcc_bgru": ("mfcc", 71956), "fbanks_cnn": ("fbank", 111040), "spec_bgru": ("spec", 126916),
-           "mfrn_bgru": ("mfcc", 71956)}
+           "mfrn_bgru": ("mfcc", 71956), "spec_cnn": ("spec", 126916)}
 MATRIX_KERNELS = ("gru_fwd_seq", "gru_bwd_seq", "gru_fwd_step", "gru_bwd_step", "gemm_f32",
                   "conv_fwd", "conv_dgrad", "conv_wgrad")
 OTHER_KERNELS = ("mfcc", "fbank", "spec", "noise_mix", "adam", "batchnorm_fwd", "batchnorm_bwd", "conv1_pool_fwd",
@@ -84,7 +92,8 @@ def cpu_baseline(model_name, batch, seconds):
     threads = max(1, min(16, os.cpu_count() or 1))
     torch.set_num_threads(threads)
     cls = {"mfcc_bgru": OM.MfccBGRU, "spec_bgru": OM.SpecBGRU, "fbanks_cnn": OM.FbanksCNN,
-           "resnet_bgru": OM.ResnetBGRU, "mfrn_bgru": OM.MfrnBGRU}[model_name]
+           "resnet_bgru": OM.ResnetBGRU, "mfrn_bgru": OM.MfrnBGRU, "cnn_bgru": OM.CnnBGRU,
+           "spec_cnn": OM.SpecCNN}[model_name]
     torch.manual_seed(0)
     net = cls()
     opt = torch.optim.Adam(net.parameters(), lr=1e-4)

@@ -210,6 +210,68 @@ class MfrnBGRU(nn.Module):
         return self.gru(torch.cat((r, mf), 2))                  # (:135-136)
 
 
+# ---------------------------------------------------------------- model_cnn_bgru.py:11-56
+class _CNN1d(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv1 = nn.Conv1d(1, 64, kernel_size=80, stride=4, padding=38, bias=False)
+        self.bn1 = nn.BatchNorm1d(64)
+        self.conv2 = nn.Conv1d(64, 128, kernel_size=4, stride=2, padding=0, bias=False)
+        self.bn2 = nn.BatchNorm1d(128)
+        self.conv3 = nn.Conv1d(128, 256, kernel_size=4, stride=2, padding=0, bias=False)
+        self.bn3 = nn.BatchNorm1d(256)
+        self.conv4 = nn.Conv1d(256, 512, kernel_size=4, stride=2, padding=0, bias=False)
+        self.bn4 = nn.BatchNorm1d(512)
+        self.fc = nn.Linear(512, 512)
+
+    def forward(self, x):
+        for i in range(1, 5):
+            x = torch.relu(getattr(self, "bn%d" % i)(getattr(self, "conv%d" % i)(x)))
+        return self.fc(x.transpose(1, 2))
+
+
+class CnnBGRU(nn.Module):
+    """Raw wave [B, 16000] -> 4 strided Conv1d + BN + ReLU (T = 498) -> fc -> BiGRU(512) -> fc2."""
+
+    def __init__(self):
+        super().__init__()
+        self.cnn = _CNN1d()
+        self.gru = _GRUHead(512, 2)
+
+    def forward(self, x):
+        return self.gru(self.cnn(x.float().unsqueeze(1)))
+
+
+# ---------------------------------------------------------------- model_spec_cnn.py:20-57
+class SpecCNN(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.bn1 = nn.BatchNorm2d(1)   # constructed, never called (:23)
+        self.conv1 = nn.Conv2d(1, 64, (3, 7), padding=(1, 3))
+        self.maxpool1 = nn.MaxPool2d((1, 5))
+        self.conv2 = nn.Conv2d(64, 128, (1, 7), padding=(0, 3))
+        self.maxpool2 = nn.MaxPool2d((1, 5))
+        self.conv3 = nn.Conv2d(128, 256, (1, 12))
+        self.conv4 = nn.Conv2d(256, 512, (5, 1), padding=(2, 0))
+        self.maxpool3 = nn.MaxPool1d(49)
+        self.dropout = nn.Dropout(0.5)
+        self.fc1 = nn.Linear(512, 256)
+        self.fc2 = nn.Linear(256, NUM_CLASSES)
+
+    @staticmethod
+    def features(x):
+        return torch.from_numpy(np.stack([F.compute_spec(c).T for c in x.numpy()]))   # [B, 49, 321]
+
+    def forward(self, x):
+        with torch.no_grad():
+            inx = self.features(x)
+        h = self.maxpool1(self.conv1(inx.unsqueeze(1)))
+        h = self.maxpool2(self.conv2(h))
+        h = self.conv4(self.conv3(h)).squeeze(3)
+        h = self.maxpool3(h).squeeze(2)
+        return self.fc2(self.fc1(self.dropout(h)))
+
+
 def train_step(model, x, labels, lr=1e-4, optimizer=None):
     """One training.py:85-91 step on the CPU: zero_grad, forward, CE(mean), backward, Adam."""
     crit = nn.CrossEntropyLoss()

@@ -1,7 +1,10 @@
-// K6 fused first layer of model_fbanks_cnn (models/model_fbanks_cnn.py:72-73,89-90):
-//   conv1 = Conv2d(1, 64, (7, 3), padding=(3, 1)) + bias, then MaxPool2d((1, 3)),
-// as ONE pass over the [N, 98, 120] fbank image instead of an implicit GEMM that writes the
-// 1.5 GB (B = 512) pre-pool activation and a pooling kernel that reads it back.
+// K6 fused first layer of the one-channel image CNNs:
+//   model_fbanks_cnn (models/model_fbanks_cnn.py:72-73,89-90): Conv2d(1, 64, (7, 3), padding=(3, 1))
+//     + bias, then MaxPool2d((1, 3)) over the [N, 98, 120] fbank image;
+//   model_spec_cnn (models/model_spec_cnn.py:24-25,44-45): Conv2d(1, 64, (3, 7), padding=(1, 3))
+//     + bias, then MaxPool2d((1, 5)) over the [N, 49, 321] spectrogram,
+// as ONE pass over the image instead of an implicit GEMM that writes the pre-pool activation
+// (1.5 GB for fbanks_cnn at B = 512) and a pooling kernel that reads it back.
 //
 // Forward  : each output pixel's 21-tap dot product on the VALU (a single input channel gives a
 //            K = 21 GEMM that the matrix cores cannot use well), max over the pool window in
@@ -178,8 +181,11 @@ __global__ void conv1_pool_reduce_kernel(const float* __restrict__ partial, int 
 }
 
 int check_c1(int64_t N, int64_t H, int64_t W, int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t pool) {
-  SRK_REQUIRE(Co == kCo && KH == 7 && KW == 3 && pool == 3 && ph == 3 && pw == 1, SRK_ERR_INVALID,
-              "conv1_pool: only the model_fbanks_cnn conv1 geometry (Co 64, 7x3, pad (3,1), pool (1,3)) is fused");
+  const bool fb = KH == 7 && KW == 3 && ph == 3 && pw == 1 && pool == 3;
+  const bool sc = KH == 3 && KW == 7 && ph == 1 && pw == 3 && pool == 5;
+  SRK_REQUIRE(Co == kCo && (fb || sc), SRK_ERR_INVALID,
+              "conv1_pool: only the fbanks_cnn (7x3, pad (3,1), pool (1,3)) and spec_cnn (3x7, pad (1,3), pool (1,5)) "
+              "conv1 geometries with Co 64 are fused");
   SRK_REQUIRE(N > 0 && H > 0 && W >= pool && N * H * W < ((int64_t)1 << 31), SRK_ERR_INVALID, "conv1_pool: bad dims");
   return SRK_OK;
 }
@@ -208,7 +214,10 @@ int srk_conv1_pool_fwd(const float* x, int64_t N, int64_t H, int64_t W, const fl
   const size_t lds = (size_t)(srk::kRows + KH - 1) * (W + KW) * 4;
   // algorithmic: the input image once + pooled output + argmax
   srk::ProfScope prof("conv1_pool_fwd", s, 4.0 * N * H * W + 5.0 * N * H * (W / pool) * Co);
-  hipLaunchKernelGGL((srk::conv1_pool_fwd_kernel<7, 3, 3>), dim3((unsigned)(N * hp)), dim3(256), lds, s, a);
+  if (KH == 7)
+    hipLaunchKernelGGL((srk::conv1_pool_fwd_kernel<7, 3, 3>), dim3((unsigned)(N * hp)), dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL((srk::conv1_pool_fwd_kernel<3, 7, 5>), dim3((unsigned)(N * hp)), dim3(256), lds, s, a);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END
@@ -230,8 +239,12 @@ int srk_conv1_pool_wgrad(const float* x, int64_t N, int64_t H, int64_t W, int64_
   const size_t patch = (size_t)(srk::kRows + KH - 1) * (W + KW) * 4;
   const size_t red = (size_t)4 * srk::kC4 * (T + 1) * 4 * 4;
   srk::ProfScope prof("conv1_pool_wgrad", s, 4.0 * N * H * W + 5.0 * N * H * (W / pool) * Co);
-  hipLaunchKernelGGL((srk::conv1_pool_wgrad_kernel<7, 3, 3>), dim3((unsigned)blocks), dim3(256), std::max(patch, red), s,
-                     a);
+  if (KH == 7)
+    hipLaunchKernelGGL((srk::conv1_pool_wgrad_kernel<7, 3, 3>), dim3((unsigned)blocks), dim3(256), std::max(patch, red),
+                       s, a);
+  else
+    hipLaunchKernelGGL((srk::conv1_pool_wgrad_kernel<3, 7, 5>), dim3((unsigned)blocks), dim3(256), std::max(patch, red),
+                       s, a);
   const int per = (int)(Co * (T + 1));
   hipLaunchKernelGGL(srk::conv1_pool_reduce_kernel, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, ws, blocks, T,
                      dw, db);

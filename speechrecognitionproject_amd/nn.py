@@ -262,8 +262,8 @@ class Conv1d(tnn.Module):
 
 
 class _Conv1PoolFn(torch.autograd.Function):
-    """conv1 + bias + MaxPool2d((1, 3)) of model_fbanks_cnn (srk_conv1_pool_fwd / _wgrad): one
-    input channel, the pooled NHWC output; the input (features) gets no gradient."""
+    """conv1 + bias + MaxPool2d((1, pool)) of model_fbanks_cnn / model_spec_cnn (srk_conv1_pool_fwd /
+    _wgrad): one input channel, the pooled NHWC output; the input (features) gets no gradient."""
 
     @staticmethod
     def forward(ctx, x, w, b, padding, pool):
@@ -294,13 +294,13 @@ class _Conv1PoolFn(torch.autograd.Function):
 
 def conv1_pool(x, conv, pool):
     """Fused ``pool(conv(x))`` for a one-channel NHW input when the geometry is the one
-    srk_conv1_pool supports (model_fbanks_cnn conv1 + maxpool1) and ``x`` needs no gradient;
-    otherwise the separate conv and pool kernels.  Returns NHWC."""
-    if (conv.in_channels == 1 and conv.out_channels == 64 and tuple(conv.kernel_size) == (7, 3)
-            and tuple(conv.padding) == (3, 1) and tuple(conv.stride) == (1, 1) and conv.bias is not None
-            and tuple(pool.kernel_size) == (1, 3) and not x.requires_grad):
+    srk_conv1_pool supports (conv1 + maxpool1 of model_fbanks_cnn / model_spec_cnn) and ``x`` needs
+    no gradient; otherwise the separate conv and pool kernels.  Returns NHWC."""
+    geom = (tuple(conv.kernel_size), tuple(conv.padding), tuple(pool.kernel_size))
+    if (conv.in_channels == 1 and conv.out_channels == 64 and tuple(conv.stride) == (1, 1) and conv.bias is not None
+            and geom in (((7, 3), (3, 1), (1, 3)), ((3, 7), (1, 3), (1, 5))) and not x.requires_grad):
         require_gpu()
-        return _Conv1PoolFn.apply(x, conv.weight, conv.bias, conv.padding, 3)
+        return _Conv1PoolFn.apply(x, conv.weight, conv.bias, conv.padding, pool.kernel_size[1])
     return pool(conv(x.unsqueeze(-1)))
 
 

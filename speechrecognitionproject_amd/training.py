@@ -25,7 +25,7 @@ from . import parallel
 from .nn import CrossEntropyLoss
 from .optim import Adam, FlatParams
 
-PLUGINS = ("mfcc_bgru", "fbanks_cnn", "spec_bgru", "resnet_bgru", "mfrn_bgru")
+PLUGINS = ("mfcc_bgru", "fbanks_cnn", "spec_bgru", "resnet_bgru", "mfrn_bgru", "cnn_bgru", "spec_cnn")
 
 
 def parse(argv=None):

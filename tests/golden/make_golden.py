@@ -124,6 +124,7 @@ def main():
     import model_spec_cnn as R_sc
     import model_mfcc_bgru as R_mb
     import model_mfrn_bgru as R_mr
+    import model_cnn_bgru as R_cb
     import model_resnet_bgru as R_rb
     import dataset as R_ds
     torch.set_default_dtype(torch.float32)
@@ -199,6 +200,12 @@ def main():
     x3, y3 = synthetic_clips(2, seed=7)
     torch.manual_seed(0)
     model_golden("mfrn_bgru_golden.npz", R_mr.Network(), x3, y3, train_mode=True)
+    x4, y4 = synthetic_clips(2, seed=8)
+    torch.manual_seed(0)
+    model_golden("cnn_bgru_golden.npz", R_cb.Network(), x4, y4, train_mode=True)
+    x5, y5 = synthetic_clips(4, seed=9)
+    torch.manual_seed(0)
+    model_golden("spec_cnn_golden.npz", R_sc.Network(), x5, y5, train_mode=False)
 
 
 if __name__ == "__main__":

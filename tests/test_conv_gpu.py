@@ -75,20 +75,23 @@ def test_maxpool_vs_torch(gpu, N, H, W, C, kh, kw):
     assert torch.equal(xm.grad.permute(0, 3, 1, 2).cpu(), xr.grad)
 
 
-@pytest.mark.parametrize("N,H,W", [(3, 98, 120), (2, 7, 9), (1, 5, 31)])
-def test_conv1_pool_fused_vs_torch(gpu, N, H, W):
-    """Fused conv1 + bias + maxpool (1,3) (model_fbanks_cnn.py:72-73,89-90) vs torch conv2d +
-    max_pool2d: pooled values, and dW / db through the pool (gradient routed by the argmax)."""
+@pytest.mark.parametrize("N,H,W,KH,KW,pool", [
+    (3, 98, 120, 7, 3, 3), (2, 7, 9, 7, 3, 3), (1, 5, 31, 7, 3, 3),     # model_fbanks_cnn.py:72-73
+    (3, 49, 321, 3, 7, 5), (2, 4, 13, 3, 7, 5)])                        # model_spec_cnn.py:24-25
+def test_conv1_pool_fused_vs_torch(gpu, N, H, W, KH, KW, pool):
+    """Fused conv1 + bias + maxpool (1,pool) vs torch conv2d + max_pool2d (floor mode: trailing
+    columns dropped): pooled values, and dW / db through the pool (gradient routed by the argmax)."""
     g = torch.Generator().manual_seed(N * 7 + W)
+    pad = (KH // 2, KW // 2)
     x = torch.randn(N, 1, H, W, generator=g) * 30.0
-    w = torch.randn(64, 1, 7, 3, generator=g) * 0.2
+    w = torch.randn(64, 1, KH, KW, generator=g) * 0.2
     b = torch.randn(64, generator=g)
     wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
-    yr = F.max_pool2d(F.conv2d(x, wr, br, padding=(3, 1)), (1, 3))
+    yr = F.max_pool2d(F.conv2d(x, wr, br, padding=pad), (1, pool))
     gy = torch.randn(yr.shape, generator=g)
     (yr * gy).sum().backward()
     wm, bm = w.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
-    ym = snn._Conv1PoolFn.apply(x[:, 0].cuda(), wm, bm, (3, 1), 3)
+    ym = snn._Conv1PoolFn.apply(x[:, 0].cuda(), wm, bm, pad, pool)
     (ym * gy.permute(0, 2, 3, 1).cuda()).sum().backward()
     assert rel_err(ym.detach().permute(0, 3, 1, 2).cpu().numpy(), yr.detach().numpy()) <= 1e-5
     assert rel_err(wm.grad.cpu().numpy(), wr.grad.numpy()) <= 1e-4

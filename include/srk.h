@@ -80,6 +80,29 @@ int srk_noise_mix(const int16_t* pcm, const int16_t* bank, int64_t n_files, int6
                   const int64_t* file_idx, const int64_t* offset, const double* gain,
                   int64_t n_clips, float* out, void* stream);
 
+/* K10: batched training-mode augmentation, dataset.py:103-118 and its helpers :148-223, with the
+ * random draws made explicit (one op per clip; the Python `Dataset.__getitem__` draws them per
+ * item, srk_augment applies a whole batch in one launch).  op[b]:
+ *   SRK_AUG_NONE      out = pcm
+ *   SRK_AUG_SPEED     speed_tuning (:206-223): cv2 INTER_LINEAR resample to iparam[b] =
+ *                     int(16000 * rate) samples, then centre cut, or random pad when shorter
+ *   SRK_AUG_SHIFT     time_stretching (:195-204): shift by iparam[b] in (-16000, 16000)
+ *   SRK_AUG_NOISE     add_noise_uniform (:183-193): int16(pcm + dparam[b] * noise)
+ *   SRK_AUG_NOISE_SNR add_noise_snr (:163-181): dparam[b] = 10 ** (snr_dB / 10)
+ *   SRK_AUG_SILENCE   generate_silence_sample (:148-161): float32(noise * dparam[b]); pcm unused;
+ *                     noise_pos[b] < 0 gives the all-zero sample
+ * noise = bank[noise_pos[b] .. + 16000) of the flat int16 noise bank (ragged files concatenated);
+ * ops without noise ignore noise_pos.  The pad samples the reference draws with
+ * np.random.randint(-32, 32, k) come from a counter hash of (seed, b, output position)
+ * (oracle/augment.py aug_fill).  pcm: int16 [n_clips, 16000] (zero padded as dataset.py:100-102),
+ * out: float32 [n_clips, 16000]; both 16-byte aligned.  op/iparam/noise_pos/dparam: device arrays
+ * of n_clips entries, validated by the caller (out-of-range noise windows read as silence). */
+enum { SRK_AUG_NONE = 0, SRK_AUG_SPEED = 1, SRK_AUG_SHIFT = 2, SRK_AUG_NOISE = 3, SRK_AUG_NOISE_SNR = 4,
+       SRK_AUG_SILENCE = 5 };
+int srk_augment(const int16_t* pcm, int64_t n_clips, const int16_t* bank, int64_t bank_len, const int32_t* op,
+                const int64_t* iparam, const int64_t* noise_pos, const double* dparam, uint64_t seed, float* out,
+                void* stream);
+
 /* ---------------------------------------------------------------- dense algebra (fp32 MFMA)
  * C[M,N] = alpha * op(A) op(B) + beta * C (+ bias), row-major.  op(A) = A [M,K] (lda) or, with
  * trans_a, A stored [K,M]; op(B) = B [K,N] (ldb) or, with trans_b, B stored [N,K].

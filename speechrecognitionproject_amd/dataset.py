@@ -9,9 +9,14 @@ the arithmetic that the train step repeats per clip moves to the device:
 
 Augmentations (training mode, dataset.py:107-116): time shift, uniform noise, SNR noise and
 silence synthesis are implemented here exactly.  ``speed_tuning`` re-implements cv2.resize's
-INTER_LINEAR 1-D resampling (half-pixel centres, edge clamp) in numpy — cv2 is absent from this
-image, so this path is parity-unpinned.  ``pitch_shifting`` needs librosa.effects.pitch_shift,
-which is absent: it returns the sample unchanged and warns once (DESIGN.md §Out of scope).
+INTER_LINEAR 1-D resampling (OpenCV's generic path: fp32 source coordinate and coefficients, rows
+clamped) in numpy — cv2 is absent from this image, so this path is parity-unpinned.
+``pitch_shifting`` needs librosa.effects.pitch_shift, which is absent: it returns the sample
+unchanged and warns once (DESIGN.md §Out of scope).
+
+``DeviceAugment`` is the batched device counterpart of the per-item augmentation of
+``__getitem__`` (K10, ``srk_augment``): the same draws in the same order per clip on the host
+(a handful of numbers), the arithmetic for the whole batch in one kernel launch.
 """
 import os
 import warnings
@@ -181,16 +186,20 @@ class Dataset(_TorchDataset):
 
 
 def _resize_linear(x, n_out):
-    """cv2.resize(x, (1, n_out), interpolation=INTER_LINEAR) for a column vector: half-pixel
-    centres, edge clamping (parity unpinned: cv2 is absent)."""
+    """cv2.resize(x, (1, n_out), interpolation=INTER_LINEAR) for a float64 column vector, as
+    OpenCV's generic resize computes it (parity unpinned: cv2 is absent): scale = 1 / (dst / src);
+    fy = float32((dy + 0.5) * scale - 0.5), sy = floor(fy), fy -= sy; fp32 coefficients
+    (1 - fy, fy); source rows sy, sy + 1 clamped to the clip; float64 products and sum."""
+    x = np.asarray(x, dtype=np.float64)
     n_in = len(x)
-    scale = n_in / float(n_out)
-    src = (np.arange(n_out) + 0.5) * scale - 0.5
-    src = np.clip(src, 0, n_in - 1)
-    i0 = np.floor(src).astype(np.int64)
-    i1 = np.minimum(i0 + 1, n_in - 1)
-    w = src - i0
-    return x[i0] * (1 - w) + x[i1] * w
+    scale = 1.0 / (float(n_out) / float(n_in))
+    fy = ((np.arange(n_out, dtype=np.float64) + 0.5) * scale - 0.5).astype(np.float32)
+    sy = np.floor(fy).astype(np.int64)
+    fy = (fy - sy.astype(np.float32)).astype(np.float32)
+    b0 = (np.float32(1.0) - fy).astype(np.float64)
+    r0 = np.clip(sy, 0, n_in - 1)
+    r1 = np.clip(sy + 1, 0, n_in - 1)
+    return x[r0] * b0 + x[r1] * fy.astype(np.float64)
 
 
 class SyntheticDataset(_TorchDataset):
@@ -228,3 +237,88 @@ class DeviceNoiseMix:
         offs = self.rng.integers(0, self.bank.shape[1] - SEQ_LENGTH + 1, n)
         gains = self.rng.uniform(0, self.upper_bound, n)
         return noise_mix(pcm_i16, self.bank, files, offs, gains)
+
+
+class DeviceAugment:
+    """Batched training-mode augmentation of ``Dataset.__getitem__`` (dataset.py:103-118) on the
+    device (K10).  Per clip, the host makes the reference's draws in the reference's order —
+    ``prob = np.random.uniform(0, 1)`` then the chosen op's own draws (python ``random`` for file /
+    offset / shift / levels, ``np.random`` for rates and gains) — and one kernel launch applies the
+    whole batch.  Silence items (label 11) follow ``generate_silence_sample``: the first 185 are all
+    zero, later ones a scaled noise window.  The pad samples of shifted / resampled clips come from
+    the kernel's counter hash rather than ``np.random.randint`` (include/srk.h).
+
+    noise_files: list of 1-D int16 arrays (the ``_background_noise_`` WAVs, any lengths).
+    """
+
+    def __init__(self, noise_files, seed=0, shift_range=4800, upper_bound=0.1):
+        from .features import require_gpu
+        require_gpu()
+        files = [np.asarray(f, dtype=np.int16).reshape(-1) for f in noise_files]
+        if not files or min(len(f) for f in files) < SEQ_LENGTH:
+            raise ValueError("DeviceAugment needs >= 1 noise file of >= %d samples" % SEQ_LENGTH)
+        self.starts = np.cumsum([0] + [len(f) for f in files[:-1]]).astype(np.int64)
+        self.lengths = np.array([len(f) for f in files], dtype=np.int64)
+        self.bank = torch.from_numpy(np.concatenate(files)).cuda()
+        self.shift_range = shift_range
+        self.upper_bound = upper_bound
+        self.silence_class_zeros_count = 0
+        self.seed = int(seed) * 0x100000001B3
+        self.calls = 0
+
+    def _noise_window(self):
+        f = randint(0, len(self.lengths) - 1)
+        return int(self.starts[f] + randint(0, int(self.lengths[f]) - SEQ_LENGTH))
+
+    def draw(self, labels, train=True):
+        """Per-clip (op, iparam, noise_pos, dparam) following dataset.py:103-116 / :148-161."""
+        from . import features as K
+        n = len(labels)
+        op = np.zeros(n, np.int64)
+        ip = np.zeros(n, np.int64)
+        pos = np.full(n, -1, np.int64)
+        dp = np.zeros(n, np.float64)
+        for b, lab in enumerate(labels):
+            if int(lab) == 11 and train:                  # generate_silence_sample
+                op[b] = K.AUG_SILENCE
+                if self.silence_class_zeros_count < 185:
+                    self.silence_class_zeros_count += 1
+                else:
+                    pos[b] = self._noise_window()
+                    dp[b] = np.random.uniform(0, 1)
+                continue
+            if not train:
+                continue
+            prob = np.random.uniform(0, 1)
+            if prob < 0.2:                                 # pitch_shifting (librosa absent: unchanged)
+                randint(0, 4)
+            if 0.2 < prob < 0.4:                           # speed_tuning
+                op[b], ip[b] = K.AUG_SPEED, int(SEQ_LENGTH * np.random.uniform(0.7, 1.3))
+            if 0.4 < prob < 0.6:                           # time_stretching
+                op[b], ip[b] = K.AUG_SHIFT, randint(-self.shift_range, self.shift_range)
+            if 0.6 < prob < 0.8:                           # add_noise_uniform
+                op[b], pos[b] = K.AUG_NOISE, self._noise_window()
+                dp[b] = np.random.uniform(0, self.upper_bound)
+        return op, ip, pos, dp
+
+    def __call__(self, pcm_i16, labels, train=True, out=None):
+        """int16 [B, 16000] PCM (zero padded) + labels -> augmented float32 [B, 16000] on the device."""
+        from .features import augment
+        op, ip, pos, dp = self.draw(np.asarray(labels).reshape(-1), train)
+        self.calls += 1
+        return augment(pcm_i16, self.bank, op, ip, pos, dp, self.seed + self.calls, out=out)
+
+    def add_noise_snr(self, pcm_i16, levels=(-5, 0, 5, 10, None)):
+        """Batched ``add_noise_snr`` (dataset.py:163-181): one noise window and SNR level per clip."""
+        from . import features as K
+        n = pcm_i16.shape[0]
+        op = np.zeros(n, np.int64)
+        pos = np.full(n, -1, np.int64)
+        dp = np.zeros(n, np.float64)
+        for b in range(n):
+            pos[b] = self._noise_window()
+            snr = levels[randint(0, len(levels) - 1)]
+            if snr is not None:
+                op[b], dp[b] = K.AUG_NOISE_SNR, 10 ** (snr / 10.0)
+        self.calls += 1
+        return K.augment(pcm_i16, self.bank, op, np.zeros(n, np.int64), pos, dp, self.seed + self.calls)

@@ -1,4 +1,5 @@
-"""Host wrappers of the feature kernels K1-K4 (include/srk.h).  Batched, device-resident.
+"""Host wrappers of the feature kernels K1-K4 and the augmentation kernel K10 (include/srk.h).
+Batched, device-resident.
 
 All functions take PCM as float32 [B, 16000] (int16-valued, as dataset.py:117 produces); a CPU
 tensor is copied to the current GPU first (the reference forward receives CPU batches,
@@ -86,4 +87,58 @@ def noise_mix(pcm_i16, bank_i16, file_idx, offsets, gains, out=None):
     out = torch.empty((n, SEQ_LENGTH), device=dev, dtype=torch.float32) if out is None else out
     call("srk_noise_mix", ptr(x), ptr(bank), bank.shape[0], bank.shape[1], ptr(fi), ptr(of), ptr(g), n, ptr(out),
          stream_ptr())
+    return out
+
+
+AUG_NONE, AUG_SPEED, AUG_SHIFT, AUG_NOISE, AUG_NOISE_SNR, AUG_SILENCE = 0, 1, 2, 3, 4, 5
+
+
+def augment(pcm_i16, bank_i16, op, iparam, noise_pos, dparam, seed, out=None):
+    """K10 (srk_augment): one training-mode augmentation per clip, whole batch in one launch.
+
+    pcm_i16: int16 [B, 16000] (device or host); bank_i16: flat int16 noise bank (device or host);
+    op / iparam / noise_pos / dparam: host arrays of B draws (see include/srk.h for their meaning),
+    validated here — the kernel trusts them — and uploaded in ONE host-to-device copy.
+    Returns float32 [B, 16000] on the device."""
+    import numpy as np
+    require_gpu()
+    dev = torch.device("cuda")
+    x = torch.as_tensor(pcm_i16).to(dev, torch.int16).contiguous()
+    bank = torch.as_tensor(bank_i16).to(dev, torch.int16).reshape(-1).contiguous()
+    n = x.shape[0]
+    op = np.asarray(op, dtype=np.int64).reshape(-1)
+    ip = np.asarray(iparam, dtype=np.int64).reshape(-1)
+    pos = np.asarray(noise_pos, dtype=np.int64).reshape(-1)
+    dp = np.asarray(dparam, dtype=np.float64).reshape(-1)
+    if x.shape != (n, SEQ_LENGTH) or not (op.size == ip.size == pos.size == dp.size == n):
+        raise SrkError("augment: inconsistent shapes")
+    if n == 0:
+        return torch.empty((0, SEQ_LENGTH), device=dev, dtype=torch.float32) if out is None else out
+    if op.min() < AUG_NONE or op.max() > AUG_SILENCE:
+        raise SrkError("augment: unknown op")
+    blen = bank.numel()
+    speed, shift = op == AUG_SPEED, op == AUG_SHIFT
+    noisy = (op == AUG_NOISE) | (op == AUG_NOISE_SNR) | ((op == AUG_SILENCE) & (pos >= 0))
+    if np.any(speed & ((ip < 1) | (ip > 4 * SEQ_LENGTH))):
+        raise SrkError("augment: speed_tuning length out of range")
+    if np.any(shift & (np.abs(ip) >= SEQ_LENGTH)):
+        raise SrkError("augment: shift out of range")
+    if np.any(noisy & ((pos < 0) | (pos > blen - SEQ_LENGTH))):
+        raise SrkError("augment: noise window outside the bank")
+    if np.any((op == AUG_NOISE_SNR) & ~(dp > 0)):
+        raise SrkError("augment: SNR ratio must be > 0")
+    # one packed upload: iparam | noise_pos | dparam (8-B each) | op (int32)
+    packed = np.empty(n * 28, dtype=np.uint8)
+    packed[:8 * n] = ip.view(np.uint8)
+    packed[8 * n:16 * n] = pos.view(np.uint8)
+    packed[16 * n:24 * n] = dp.view(np.uint8)
+    packed[24 * n:] = op.astype(np.int32).view(np.uint8)
+    d = torch.from_numpy(packed).to(dev, non_blocking=False)
+    base = d.data_ptr()
+    out = torch.empty((n, SEQ_LENGTH), device=dev, dtype=torch.float32) if out is None else out
+    if out.shape != (n, SEQ_LENGTH) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise SrkError("augment: bad output tensor")
+    call("srk_augment", ptr(x), n, ptr(bank) if blen else None, blen, ctypes.c_void_p(base + 24 * n),
+         ctypes.c_void_p(base), ctypes.c_void_p(base + 8 * n), ctypes.c_void_p(base + 16 * n),
+         ctypes.c_uint64(int(seed) & ((1 << 64) - 1)), ptr(out), stream_ptr())
     return out

@@ -189,6 +189,64 @@ def main():
         np.savez_compressed(os.path.join(HERE, "noise_mix_golden.npz"), bank=bank, pcm=np.stack(samples),
                             file_idx=np.array(files), start=np.array(starts), gain=np.array(gains), out=np.stack(outs))
 
+        # time_stretching / add_noise_snr / generate_silence_sample (dataset.py:148-204): call the
+        # reference under a seed, then replay the same draws to record them explicitly
+        from oracle import augment as OA
+        base = np.concatenate((wavs["yes/a.wav"], np.zeros(4000, dtype=int)))
+        shifts, shift_fill, shift_out = [], np.zeros((8, 4800), dtype=np.int64), []
+        for i in range(8):
+            random.seed(100 + i)
+            np.random.seed(100 + i)
+            out = ds.time_stretching(base, 4800)
+            random.seed(100 + i)
+            np.random.seed(100 + i)
+            sh = random.randint(-4800, 4800)
+            fill = np.random.randint(-32, 32, abs(sh))
+            assert np.array_equal(out, OA.time_stretching(base, sh, fill))
+            shifts.append(sh)
+            shift_fill[i, :abs(sh)] = fill
+            shift_out.append(out)
+        snr_pcm, snr_files, snr_starts, snr_db, snr_out = [], [], [], [], []
+        for i in range(10):
+            s = wavs["go/b.wav"].astype(np.int64) // (1 + 7 * (i % 2))
+            random.seed(200 + i)
+            np.random.seed(200 + i)
+            out = ds.add_noise_snr(s)
+            random.seed(200 + i)
+            np.random.seed(200 + i)
+            fname = ds.noise_list[random.randint(0, len(ds.noise_list) - 1)]
+            start = random.randint(0, 60000 - 16000)
+            snr = [-5, 0, 5, 10, None][random.randint(0, 4)]
+            seg = bank[names.index(fname)][start:start + 16000]
+            assert np.array_equal(out, OA.add_noise_snr(s, seg, snr))
+            snr_pcm.append(s)
+            snr_files.append(names.index(fname))
+            snr_starts.append(start)
+            snr_db.append(np.nan if snr is None else snr)
+            snr_out.append(np.asarray(out).astype(np.int64))
+        sil_files, sil_starts, sil_gains, sil_out = [], [], [], []
+        ds.silence_class_zeros_count = 185
+        for i in range(4):
+            random.seed(300 + i)
+            np.random.seed(300 + i)
+            out = ds.generate_silence_sample()
+            random.seed(300 + i)
+            np.random.seed(300 + i)
+            fname = ds.noise_list[random.randint(0, len(ds.noise_list) - 1)]
+            start = random.randint(0, 60000 - 16000)
+            gain = np.random.uniform(0, 1)
+            assert np.array_equal(out, OA.generate_silence_sample(bank[names.index(fname)][start:start + 16000], gain))
+            sil_files.append(names.index(fname))
+            sil_starts.append(start)
+            sil_gains.append(gain)
+            sil_out.append(out)
+        np.savez_compressed(os.path.join(HERE, "augment_golden.npz"), bank=bank, shift_pcm=base.astype(np.int64),
+                            shift=np.array(shifts), shift_fill=shift_fill, shift_out=np.stack(shift_out),
+                            snr_pcm=np.stack(snr_pcm), snr_file=np.array(snr_files), snr_start=np.array(snr_starts),
+                            snr_db=np.array(snr_db, dtype=np.float64), snr_out=np.stack(snr_out),
+                            sil_file=np.array(sil_files), sil_start=np.array(sil_starts),
+                            sil_gain=np.array(sil_gains), sil_out=np.stack(sil_out))
+
     # ---- module-level goldens (logits, CE loss, sampled grads, 1-step Adam delta)
     x, y = synthetic_clips(4, seed=5)
     torch.manual_seed(0)

@@ -1,0 +1,136 @@
+"""K10 srk_augment on the GPU: bit-exact vs the oracle restatement on every op and edge case,
+vs the reference's golden outputs where the reference's draws can be replayed, and the batched
+DeviceAugment draw path."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import augment as OA
+from speechrecognitionproject_amd import features as K
+from speechrecognitionproject_amd._lib import SrkError
+from speechrecognitionproject_amd.dataset import DeviceAugment
+
+pytestmark = pytest.mark.gpu
+
+
+def _pcm(n, seed, scale=3000):
+    rng = np.random.default_rng(seed)
+    return np.clip(np.rint(rng.normal(0, scale, (n, 16000))), -32768, 32767).astype(np.int16)
+
+
+def test_augment_all_ops_vs_oracle(gpu):
+    rng = np.random.default_rng(1)
+    bank = np.clip(np.rint(rng.normal(0, 2000, 100000)), -6000, 6000).astype(np.int16)
+    cases = [(OA.OP_NONE, 0, -1, 0.0)]
+    cases += [(OA.OP_SHIFT, s, -1, 0.0) for s in (0, 1, -1, 4800, -4800, 15999, -15999, 333)]
+    cases += [(OA.OP_SPEED, n, -1, 0.0) for n in (11200, 11201, 15998, 15999, 16000, 16001, 16002, 20799, 1, 64000,
+                                                  int(16000 * 0.7), int(16000 * 1.3))]
+    cases += [(OA.OP_NOISE, 0, p, g) for p, g in ((0, 0.1), (100000 - 16000, 0.05), (4321, 0.0), (17, 0.0999))]
+    cases += [(OA.OP_NOISE_SNR, 0, p, 10 ** (db / 10.0)) for p, db in ((5, -5), (50000, 0), (12345, 5), (999, 10))]
+    cases += [(OA.OP_SILENCE, 0, -1, 0.0), (OA.OP_SILENCE, 0, 60000, 0.7), (OA.OP_SILENCE, 0, 0, 0.999)]
+    n = len(cases)
+    pcm = _pcm(n, 2)
+    pcm[3] = 0                                       # silent clip through a shift
+    pcm[-5] = 0                                      # zero signal power -> factor 0 (SNR)
+    pcm[5, :10] = 32767
+    pcm[6, -10:] = -32768
+    op, ip, pos, dp = (np.array(c) for c in zip(*cases))
+    out = K.augment(torch.from_numpy(pcm).cuda(), torch.from_numpy(bank).cuda(), op, ip, pos, dp, seed=77)
+    ref = OA.augment_batch(pcm, bank, op, ip, pos, dp, seed=77)
+    got = out.cpu().numpy()
+    for b in range(n):
+        assert np.array_equal(got[b], ref[b]), (b, cases[b], np.flatnonzero(got[b] != ref[b])[:5])
+
+
+def test_augment_large_batch_random_ops_vs_oracle(gpu):
+    rng = np.random.default_rng(9)
+    n = 300
+    pcm = _pcm(n, 10, scale=3000)           # keeps int16(x + g * noise) in range (overflow is undefined in numpy)
+    bank = np.clip(np.rint(rng.normal(0, 2000, 2 * 960000)), -6000, 6000).astype(np.int16)
+    op = rng.integers(0, 6, n)
+    ip = np.where(op == OA.OP_SPEED, (16000 * rng.uniform(0.7, 1.3, n)).astype(np.int64),
+                  rng.integers(-4800, 4801, n))
+    pos = rng.integers(0, bank.size - 16000 + 1, n)
+    pos[(op == OA.OP_SILENCE) & (rng.uniform(size=n) < 0.3)] = -1
+    dp = np.where(op == OA.OP_NOISE_SNR, 10 ** (rng.choice([-5, 0, 5, 10], n) / 10.0), rng.uniform(0, 1, n))
+    got = K.augment(pcm, bank, op, ip, pos, dp, seed=2024).cpu().numpy()
+    assert np.array_equal(got, OA.augment_batch(pcm, bank, op, ip, pos, dp, seed=2024))
+
+
+def test_augment_vs_reference_golden(gpu):
+    """Outputs of the reference's own methods (dataset.py) where no pad samples are involved:
+    add_noise_snr, generate_silence_sample, and the unpadded part of time_stretching."""
+    g = golden("augment_golden.npz")
+    bank = g["bank"].reshape(-1)
+    L = g["bank"].shape[1]
+    # add_noise_snr
+    keep = ~np.isnan(g["snr_db"])
+    pcm = g["snr_pcm"][keep].astype(np.int16)
+    pos = g["snr_file"][keep] * L + g["snr_start"][keep]
+    ratio = 10 ** (g["snr_db"][keep] / 10.0)
+    n = int(keep.sum())
+    got = K.augment(pcm, bank, np.full(n, OA.OP_NOISE_SNR), np.zeros(n), pos, ratio, seed=0).cpu().numpy()
+    assert np.array_equal(got, g["snr_out"][keep].astype(np.float32))
+    # generate_silence_sample
+    n = len(g["sil_file"])
+    pos = g["sil_file"] * L + g["sil_start"]
+    got = K.augment(np.zeros((n, 16000), np.int16), bank, np.full(n, OA.OP_SILENCE), np.zeros(n), pos, g["sil_gain"],
+                    seed=0).cpu().numpy()
+    assert np.array_equal(got, g["sil_out"])
+    # time_stretching: identical outside the pad region
+    n = len(g["shift"])
+    pcm = np.repeat(g["shift_pcm"][None].astype(np.int16), n, 0)
+    got = K.augment(pcm, bank, np.full(n, OA.OP_SHIFT), g["shift"], np.full(n, -1), np.zeros(n), seed=0).cpu().numpy()
+    for b, sh in enumerate(g["shift"]):
+        keep = slice(0, 16000 - sh) if sh >= 0 else slice(-sh, 16000)
+        assert np.array_equal(got[b, keep], g["shift_out"][b, keep].astype(np.float32))
+        pad = got[b, 16000 - sh:] if sh >= 0 else got[b, :-sh]
+        assert pad.min() >= -32 and pad.max() <= 31
+
+
+def test_noise_op_matches_k4_noise_mix(gpu):
+    g = golden("noise_mix_golden.npz")
+    L = g["bank"].shape[1]
+    n = len(g["out"])
+    pos = g["file_idx"] * L + g["start"]
+    got = K.augment(g["pcm"].astype(np.int16), g["bank"].reshape(-1), np.full(n, OA.OP_NOISE), np.zeros(n), pos,
+                    g["gain"], seed=0).cpu().numpy()
+    assert np.array_equal(got, g["out"].astype(np.float32))
+
+
+def test_augment_rejects_bad_draws(gpu):
+    pcm = np.zeros((1, 16000), np.int16)
+    bank = np.zeros(20000, np.int16)
+    for op, ip, pos, dp in ((9, 0, -1, 0.0), (OA.OP_SHIFT, 16000, -1, 0.0), (OA.OP_SPEED, 0, -1, 0.0),
+                            (OA.OP_NOISE, 0, 4001, 0.1), (OA.OP_NOISE, 0, -1, 0.1), (OA.OP_NOISE_SNR, 0, 0, 0.0)):
+        with pytest.raises(SrkError):
+            K.augment(pcm, bank, [op], [ip], [pos], [dp], seed=0)
+
+
+def test_device_augment_draws_replay_through_oracle(gpu):
+    rng = np.random.default_rng(4)
+    files = [np.clip(np.rint(rng.normal(0, 2000, n)), -6000, 6000).astype(np.int16) for n in (40000, 25000, 61000)]
+    aug = DeviceAugment(files, seed=3)
+    aug.silence_class_zeros_count = 183                       # the 185-zero silence quota runs out mid-batch
+    labels = np.array([11, 0, 11, 3, 11, 5, 10, 11] * 8)
+    pcm = _pcm(len(labels), 5)
+    random.seed(11)
+    np.random.seed(11)
+    got = aug(torch.from_numpy(pcm).cuda(), labels).cpu().numpy()
+    # replay the same draws and apply them through the oracle
+    aug2 = DeviceAugment(files, seed=3)
+    aug2.silence_class_zeros_count = 183
+    random.seed(11)
+    np.random.seed(11)
+    op, ip, pos, dp = aug2.draw(labels)
+    assert (op[labels == 11] == OA.OP_SILENCE).all()
+    assert (pos[labels == 11] == -1).sum() == 2                # the last two zero samples of the quota
+    assert len(set(op[labels != 11].tolist())) >= 3           # several ops drawn
+    bank = np.concatenate(files)
+    assert np.array_equal(got, OA.augment_batch(pcm, bank, op, ip, pos, dp, seed=aug.seed + 1))
+    # eval mode: no augmentation, silence untouched pcm
+    ev = aug(torch.from_numpy(pcm).cuda(), labels, train=False).cpu().numpy()
+    assert np.array_equal(ev, pcm.astype(np.float32))

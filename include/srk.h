@@ -97,6 +97,18 @@ int srk_noise_mix(const int16_t* pcm, const int16_t* bank, int64_t n_files, int6
  * (oracle/augment.py aug_fill).  pcm: int16 [n_clips, 16000] (zero padded as dataset.py:100-102),
  * out: float32 [n_clips, 16000]; both 16-byte aligned.  op/iparam/noise_pos/dparam: device arrays
  * of n_clips entries, validated by the caller (out-of-range noise windows read as silence). */
+/* ---------------------------------------------------------------- input pipeline (host)
+ * Batched WAV decode, dataset.py:98-102 (scipy.io.wavfile.read + zero pad to 16000): n files
+ * (NUL-terminated paths) decoded by up to min(n_threads, 16) host threads (n_threads <= 0: all
+ * hardware threads, capped at 16) into out int16 [n, 16000] (HOST memory, e.g. pinned): the first
+ * min(len, 16000) samples, zero padded.  lengths[b] = the file's sample count (a count > 16000
+ * is reported as is — dataset.py:104-106 then fails on that item), or a negative SRK_WAV_ERR_*
+ * with out[b] all zero.  PCM16 mono RIFF/WAVE only (tag 1 or WAVE_FORMAT_EXTENSIBLE/PCM); other
+ * chunks skipped.  Returns SRK_OK unless the arguments are invalid: per-file errors are data,
+ * as __getitem__'s except branch (dataset.py:124-128) makes them.  Touches no GPU state.      */
+enum { SRK_WAV_ERR_OPEN = -1, SRK_WAV_ERR_FORMAT = -2, SRK_WAV_ERR_UNSUPPORTED = -3 };
+int srk_wav_read_batch(const char* const* paths, int64_t n, int16_t* out, int64_t* lengths, int n_threads);
+
 enum { SRK_AUG_NONE = 0, SRK_AUG_SPEED = 1, SRK_AUG_SHIFT = 2, SRK_AUG_NOISE = 3, SRK_AUG_NOISE_SNR = 4,
        SRK_AUG_SILENCE = 5 };
 int srk_augment(const int16_t* pcm, int64_t n_clips, const int16_t* bank, int64_t bank_len, const int32_t* op,

@@ -22,7 +22,8 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-at
 
 
 def _sources():
-    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    # *.hip: device + host code; *.cpp: host-only code (input pipeline), same compiler and flags
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
 def _headers():
@@ -42,7 +43,7 @@ def _compile(src, force):
 
 
 def build(force=False, jobs=None, verbose=True):
-    """Compile every csrc/*.hip for gfx950 and link libsrk.so; returns the library path."""
+    """Compile every csrc/*.hip (+ host-only *.cpp) for gfx950 and link libsrk.so; returns its path."""
     os.makedirs(BUILD, exist_ok=True)
     srcs = _sources()
     jobs = jobs or min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)

@@ -270,8 +270,9 @@ class DeviceAugment:
         f = randint(0, len(self.lengths) - 1)
         return int(self.starts[f] + randint(0, int(self.lengths[f]) - SEQ_LENGTH))
 
-    def draw(self, labels, train=True):
-        """Per-clip (op, iparam, noise_pos, dparam) following dataset.py:103-116 / :148-161."""
+    def draw(self, labels, train=True, skip=None):
+        """Per-clip (op, iparam, noise_pos, dparam) following dataset.py:103-116 / :148-161;
+        clips flagged in ``skip`` (failed decodes) pass through unchanged and draw nothing."""
         from . import features as K
         n = len(labels)
         op = np.zeros(n, np.int64)
@@ -279,6 +280,8 @@ class DeviceAugment:
         pos = np.full(n, -1, np.int64)
         dp = np.zeros(n, np.float64)
         for b, lab in enumerate(labels):
+            if skip is not None and skip[b]:
+                continue
             if int(lab) == 11 and train:                  # generate_silence_sample
                 op[b] = K.AUG_SILENCE
                 if self.silence_class_zeros_count < 185:
@@ -301,10 +304,10 @@ class DeviceAugment:
                 dp[b] = np.random.uniform(0, self.upper_bound)
         return op, ip, pos, dp
 
-    def __call__(self, pcm_i16, labels, train=True, out=None):
+    def __call__(self, pcm_i16, labels, train=True, out=None, skip=None):
         """int16 [B, 16000] PCM (zero padded) + labels -> augmented float32 [B, 16000] on the device."""
         from .features import augment
-        op, ip, pos, dp = self.draw(np.asarray(labels).reshape(-1), train)
+        op, ip, pos, dp = self.draw(np.asarray(labels).reshape(-1), train, skip)
         self.calls += 1
         return augment(pcm_i16, self.bank, op, ip, pos, dp, self.seed + self.calls, out=out)
 
@@ -322,3 +325,106 @@ class DeviceAugment:
                 op[b], dp[b] = K.AUG_NOISE_SNR, 10 ** (snr / 10.0)
         self.calls += 1
         return K.augment(pcm_i16, self.bank, op, np.zeros(n, np.int64), pos, dp, self.seed + self.calls)
+
+
+def read_wav_batch(paths, out=None, threads=0):
+    """Native batched WAV decode (srk_wav_read_batch): int16 [n, 16000] (zero padded) and the
+    per-file sample counts (negative = unreadable / unsupported file, its row all zero).
+    ``out``: optional int16 CPU tensor [n, 16000] to fill (e.g. pinned for an async upload)."""
+    import ctypes
+    from ._lib import call
+    n = len(paths)
+    if out is None:
+        out = torch.empty((n, SEQ_LENGTH), dtype=torch.int16)
+    if out.shape != (n, SEQ_LENGTH) or out.dtype != torch.int16 or out.device.type != "cpu" or not out.is_contiguous():
+        raise ValueError("read_wav_batch: out must be a contiguous int16 CPU tensor [n, 16000]")
+    lengths = np.empty(n, dtype=np.int64)
+    arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+    call("srk_wav_read_batch", arr, n, ctypes.c_void_p(out.data_ptr()), lengths.ctypes.data_as(ctypes.c_void_p),
+         int(threads))
+    return out, lengths
+
+
+class DeviceBatchLoader:
+    """Batched, device-resident replacement of ``DataLoader(Dataset(...), batch_size, shuffle)``
+    (training.py:77) for a WAV ``Dataset``: per batch, native multi-threaded WAV decode into pinned
+    memory (srk_wav_read_batch), one host-to-device copy, and in training mode the augmentation of
+    ``__getitem__`` as ONE K10 launch (``DeviceAugment``).  Yields ``{'audio': float32 [B, 16000]
+    (device), 'label': int64 [B] (device)}``.
+
+    Item semantics follow dataset.py:89-128: label from the directory name; training-mode silence
+    items are synthesised, not read; a file that cannot be decoded or is longer than 16000
+    samples becomes an all-zero clip with label 11 (the reference's except branch), un-augmented.
+    Submission mode (labels = file names) is not batched here: use the Dataset directly.
+    """
+
+    def __init__(self, dataset, batch_size, shuffle=False, drop_last=False, sampler=None, threads=0, seed=0):
+        if dataset.mode == "submission":
+            raise ValueError("DeviceBatchLoader: submission mode yields file names; iterate the Dataset")
+        self.ds = dataset
+        self.batch_size = batch_size
+        self.shuffle = shuffle
+        self.drop_last = drop_last
+        self.sampler = sampler
+        self.threads = threads
+        self.aug = None
+        if dataset.train:
+            noise = [read(dataset.root_dir + '/_background_noise_/' + f)[1] for f in dataset.noise_list]
+            self.aug = DeviceAugment(noise, seed=seed)
+            self.aug.silence_class_zeros_count = dataset.silence_class_zeros_count
+        self._pinned = [None, None]     # double-buffered pinned staging (the upload is async)
+        self._events = [None, None]
+        self._flip = 0
+
+    def __len__(self):
+        n = len(self.sampler) if self.sampler is not None else len(self.ds)
+        return n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
+
+    def _order(self):
+        if self.sampler is not None:
+            return list(iter(self.sampler))
+        return torch.randperm(len(self.ds)).tolist() if self.shuffle else list(range(len(self.ds)))
+
+    def __iter__(self):
+        order = self._order()
+        bs = self.batch_size
+        for s0 in range(0, len(order), bs):
+            idx = order[s0:s0 + bs]
+            if len(idx) < bs and self.drop_last:
+                return
+            yield self._batch(idx)
+
+    def _batch(self, idx):
+        names = [self.ds.data_list[i] for i in idx]
+        labels = np.array([Dataset.label_index(x) for x in names], dtype=np.int64)
+        synth = (labels == 11) & self.ds.train
+        n = len(idx)
+        k = self._flip
+        self._flip ^= 1
+        if self._events[k] is not None:
+            self._events[k].synchronize()    # the upload that last read this buffer is done
+        if self._pinned[k] is None or self._pinned[k].shape[0] < n:
+            self._pinned[k] = torch.empty((n, SEQ_LENGTH), dtype=torch.int16).pin_memory()
+        pcm = self._pinned[k][:n]
+        paths = [None if synth[b] else self.ds.root_dir + '/' + names[b] for b in range(n)]
+        read_idx = [b for b in range(n) if paths[b] is not None]
+        bad = np.zeros(n, dtype=bool)
+        if read_idx:
+            sub, lengths = read_wav_batch([paths[b] for b in read_idx], threads=self.threads)
+            bad[read_idx] = (lengths < 0) | (lengths > SEQ_LENGTH)
+            pcm[read_idx] = sub
+        pcm[synth.nonzero()[0].tolist()] = 0
+        for b in np.flatnonzero(bad):            # dataset.py:124-128
+            print("bugged item:", names[b])
+            print("label", labels[b], names[b].split('/')[0])
+            pcm[int(b)] = 0
+        labels[bad] = 11
+        dev_pcm = pcm.to("cuda", non_blocking=True)
+        self._events[k] = torch.cuda.Event()
+        self._events[k].record()
+        if self.aug is not None:
+            audio = self.aug(dev_pcm, labels, skip=bad)
+            self.ds.silence_class_zeros_count = self.aug.silence_class_zeros_count   # persists across epochs
+        else:
+            audio = dev_pcm.to(torch.float32)
+        return {'audio': audio, 'label': torch.from_numpy(labels).to("cuda", non_blocking=True)}

@@ -10,8 +10,10 @@ accuracy lines via the plugin's ``accuracy`` (``val_<KEY>.txt``, ``train_<KEY>.t
 ``resample_unknown_class`` after each epoch.  Additions (all optional): ``--model`` selects the
 plugin instead of editing an import line (training.py:39-46), ``--synthetic N`` trains on
 synthetic clips when no Kaggle tree is available, ``--data-path/--output-path`` replace the
-hard-coded paths (:21-24), ``--log-every`` batches loss lines to avoid a host sync per step, and
-torchrun environments train data-parallel (one process per GPU, RCCL all-reduce).
+hard-coded paths (:21-24), ``--log-every`` batches loss lines to avoid a host sync per step,
+``--loader device`` (default for WAV trees) replaces the per-item DataLoader with native batched
+decode + one on-device augmentation launch per batch, and torchrun environments train
+data-parallel (one process per GPU, RCCL all-reduce).
 """
 import argparse
 import importlib
@@ -41,6 +43,9 @@ def parse(argv=None):
     p.add_argument('--reduce', type=int, default=0, help='reduce_dataset(n) like training.py:66-67')
     p.add_argument('--log-every', type=int, default=1, help='write buffered loss lines every n steps')
     p.add_argument('--no-eval', action='store_true')
+    p.add_argument('--loader', choices=('device', 'torch'), default='device',
+                   help='WAV datasets: device = native batched decode + K10 on-device augmentation '
+                        '(DeviceBatchLoader); torch = per-item Dataset.__getitem__ through DataLoader')
     return p.parse_args(argv)
 
 
@@ -82,9 +87,15 @@ def main(argv=None):
     while epoch < args.epochs:
         if epoch > 4:
             scheduler.step()
+        sampler = None
         if world > 1:
             idx = parallel.shard_indices(len(data), rank, world, seed=0, epoch=epoch)
             sampler = torch.utils.data.SubsetRandomSampler(idx.tolist())
+        if not args.synthetic and args.loader == 'device':
+            from .dataset import DeviceBatchLoader
+            loader = DeviceBatchLoader(data, batch_size=args.batch_size, shuffle=sampler is None, sampler=sampler,
+                                       seed=rank)
+        elif sampler is not None:
             loader = DataLoader(data, batch_size=args.batch_size, sampler=sampler, drop_last=False)
         else:
             loader = DataLoader(data, batch_size=args.batch_size, shuffle=True, drop_last=False)

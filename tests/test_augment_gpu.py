@@ -1,6 +1,7 @@
 """K10 srk_augment on the GPU: bit-exact vs the oracle restatement on every op and edge case,
 vs the reference's golden outputs where the reference's draws can be replayed, and the batched
 DeviceAugment draw path."""
+import os
 import random
 
 import numpy as np
@@ -134,3 +135,65 @@ def test_device_augment_draws_replay_through_oracle(gpu):
     # eval mode: no augmentation, silence untouched pcm
     ev = aug(torch.from_numpy(pcm).cuda(), labels, train=False).cpu().numpy()
     assert np.array_equal(ev, pcm.astype(np.float32))
+
+
+def _tree(root, rng):
+    from scipy.io import wavfile
+    os.makedirs(root + "/_background_noise_")
+    open(root + "/_background_noise_/README.md", "w").close()
+    for i, n in enumerate((40000, 30000)):
+        wavfile.write(root + "/_background_noise_/n%d.wav" % i, 16000,
+                      np.clip(np.rint(rng.normal(0, 2000, n)), -6000, 6000).astype(np.int16))
+    names = []
+    for d in ("yes", "no", "bed", "cat"):
+        os.makedirs(root + "/" + d)
+        for j in range(5):
+            n = [16000, 12000, 9000, 16000, 17000][j]          # one too long -> error item
+            wavfile.write(root + "/%s/f%d.wav" % (d, j), 16000,
+                          np.clip(np.rint(rng.normal(0, 3000, n)), -32768, 32767).astype(np.int16))
+            names.append("%s/f%d.wav" % (d, j))
+    names.append("yes/missing.wav")
+    return names
+
+
+def test_device_batch_loader_eval_matches_dataset_items(gpu, tmp_path):
+    from speechrecognitionproject_amd.dataset import Dataset, DeviceBatchLoader
+    root = str(tmp_path)
+    names = _tree(root, np.random.default_rng(0))
+    with open(root + "/validation_list.txt", "w") as f:
+        f.write("\n".join(names) + "\n")
+    ds = Dataset(root + "/validation_list.txt", root)
+    loader = DeviceBatchLoader(ds, batch_size=8)
+    got_a, got_l = [], []
+    for batch in loader:
+        got_a.append(batch["audio"].cpu().numpy())
+        got_l.append(batch["label"].cpu().numpy())
+    got_a, got_l = np.concatenate(got_a), np.concatenate(got_l)
+    assert len(loader) == 3 and got_a.shape == (len(names), 16000)
+    for i in range(len(ds)):
+        it = ds[i]
+        assert got_l[i] == it["label"], names[i]
+        assert np.array_equal(got_a[i], np.asarray(it["audio"], dtype=np.float32)), names[i]
+
+
+def test_device_batch_loader_training_mode(gpu, tmp_path):
+    from speechrecognitionproject_amd.dataset import Dataset, DeviceBatchLoader
+    root = str(tmp_path)
+    names = _tree(root, np.random.default_rng(1))
+    with open(root + "/training_list.txt", "w") as f:
+        f.write("\n".join(names) + "\n")
+    random.seed(0)
+    np.random.seed(0)
+    ds = Dataset(root + "/training_list.txt", root)
+    ds.reduce_dataset(400)                 # keep every item: 10 commands + 3700 unknown/silence entries
+    loader = DeviceBatchLoader(ds, batch_size=512, shuffle=True)
+    seen = 0
+    for batch in loader:
+        a, lab = batch["audio"].cpu().numpy(), batch["label"].cpu().numpy()
+        assert a.dtype == np.float32 and np.all(np.abs(a) <= 32768)
+        spoken = lab != 11                 # int16-valued; synthesised silence is noise * U(0, 1), not cast
+        assert np.array_equal(a[spoken], np.trunc(a[spoken]))
+        assert lab.min() >= 0 and lab.max() <= 11
+        seen += len(lab)
+    assert seen == len(ds)
+    assert loader.aug.silence_class_zeros_count == 185      # the zero-silence quota is used first

@@ -34,3 +34,35 @@ def test_device_noise_mix_matches_numpy(gpu):
     ref = np.stack([OF.add_noise_uniform(x[i].astype(np.int16), bank[files[i]], int(offs[i]), float(gains[i]))
                     for i in range(64)])
     assert np.array_equal(out, ref.astype(np.float32))
+
+
+@pytest.mark.parametrize("loader", ["device", "torch"])
+def test_training_on_wav_tree(gpu, tmp_path, loader):
+    """training.py on a Kaggle-layout WAV tree: the device input pipeline (native decode + K10
+    augmentation) and the per-item DataLoader path both train; silence quota persists across epochs."""
+    import random
+    from scipy.io import wavfile
+    from speechrecognitionproject_amd.training import main
+    rng = np.random.default_rng(0)
+    audio = tmp_path / "data" / "audio"
+    os.makedirs(audio / "_background_noise_")
+    open(audio / "_background_noise_" / "README.md", "w").close()
+    wavfile.write(str(audio / "_background_noise_" / "n.wav"), 16000,
+                  np.clip(np.rint(rng.normal(0, 2000, 48000)), -6000, 6000).astype(np.int16))
+    names = []
+    for d in ("yes", "no", "up", "bed"):
+        os.makedirs(audio / d)
+        for j in range(6):
+            wavfile.write(str(audio / d / ("%d.wav" % j)), 16000,
+                          np.clip(np.rint(rng.normal(0, 3000, 16000 - 1000 * j)), -32768, 32767).astype(np.int16))
+            names.append("%s/%d.wav" % (d, j))
+    (tmp_path / "data" / "training_list.txt").write_text("\n".join(names) + "\n")
+    (tmp_path / "data" / "validation_list.txt").write_text("\n".join(names[::3]) + "\n")
+    random.seed(0)
+    np.random.seed(0)
+    out = tmp_path / "out"
+    main(["-key", "w", "--model", "mfcc_bgru", "--data-path", str(tmp_path / "data"), "--output-path", str(out),
+          "--epochs", "2", "--batch-size", "16", "--reduce", "12", "--log-every", "4", "--loader", loader])
+    losses = [float(l) for l in open(out / "loss_w.txt")]
+    assert len(losses) == 2 * 3 and all(np.isfinite(losses))      # 18 commands + 12 unknown + 12 silence = 42
+    assert len(open(out / "val_w.txt").readlines()) == 2

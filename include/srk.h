@@ -97,6 +97,14 @@ int srk_noise_mix(const int16_t* pcm, const int16_t* bank, int64_t n_files, int6
  * (oracle/augment.py aug_fill).  pcm: int16 [n_clips, 16000] (zero padded as dataset.py:100-102),
  * out: float32 [n_clips, 16000]; both 16-byte aligned.  op/iparam/noise_pos/dparam: device arrays
  * of n_clips entries, validated by the caller (out-of-range noise windows read as silence). */
+/* ---------------------------------------------------------------- evaluation callers
+ * K11: softmax ensemble, predictions.py:56-69 / models/model_analyst.py:22-53: logits float32
+ * [K, B, C] (model-major) -> per clip the softmax of each model's logits; probs_cat [B, K*C] their
+ * concatenation (the analyst's input, nullable), mean [B, C] = (p_1 + ... + p_K) / K (nullable),
+ * pred int64 [B] = first arg-max of the mean (nullable).  1 <= K <= 8, 1 <= C <= 64.          */
+int srk_softmax_ensemble(const float* logits, int64_t K, int64_t B, int64_t C, float* probs_cat, float* mean,
+                         int64_t* pred, void* stream);
+
 /* ---------------------------------------------------------------- input pipeline (host)
  * Batched WAV decode, dataset.py:98-102 (scipy.io.wavfile.read + zero pad to 16000): n files
  * (NUL-terminated paths) decoded by up to min(n_threads, 16) host threads (n_threads <= 0: all

@@ -272,6 +272,19 @@ class SpecCNN(nn.Module):
         return self.fc2(self.fc1(self.dropout(h)))
 
 
+# ---------------------------------------------------------------- models/model_analyst.py:10-20
+class Analyst(nn.Module):
+    """Stacking head over 4 x 12 softmax outputs: fc1 (48 -> 96) -> fc2 (96 -> 12), no activation."""
+
+    def __init__(self):
+        super().__init__()
+        self.fc1 = nn.Linear(48, 96)
+        self.fc2 = nn.Linear(96, NUM_CLASSES)
+
+    def forward(self, x):
+        return self.fc2(self.fc1(x.float()))
+
+
 def train_step(model, x, labels, lr=1e-4, optimizer=None):
     """One training.py:85-91 step on the CPU: zero_grad, forward, CE(mean), backward, Adam."""
     crit = nn.CrossEntropyLoss()

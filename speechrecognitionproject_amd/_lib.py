@@ -37,6 +37,7 @@ _SIGS = {
     "srk_noise_mix": [_P, _P, _I64, _I64, _P, _P, _P, _I64, _P, _P],
     "srk_augment": [_P, _I64, _P, _I64, _P, _P, _P, _P, ctypes.c_uint64, _P, _P],
     "srk_wav_read_batch": [ctypes.POINTER(ctypes.c_char_p), _I64, _P, _P, _I],
+    "srk_softmax_ensemble": [_P, _I64, _I64, _I64, _P, _P, _P, _P],
     "srk_gemm_f32": [_I, _I, _I64, _I64, _I64, _F, _P, _I64, _P, _I64, _F, _P, _I64, _P, _I, _P],
     "srk_gemm_rowsum_f32": [_I, _I, _I64, _I64, _I64, _F, _P, _I64, _P, _I64, _F, _P, _I64, _P, _P],
     "srk_colsum_f32": [_P, _I64, _I64, _I64, _P, _F, _P],

@@ -125,6 +125,7 @@ def main():
     import model_mfcc_bgru as R_mb
     import model_mfrn_bgru as R_mr
     import model_cnn_bgru as R_cb
+    import model_analyst as R_an
     import model_resnet_bgru as R_rb
     import dataset as R_ds
     torch.set_default_dtype(torch.float32)
@@ -264,6 +265,11 @@ def main():
     x5, y5 = synthetic_clips(4, seed=9)
     torch.manual_seed(0)
     model_golden("spec_cnn_golden.npz", R_sc.Network(), x5, y5, train_mode=False)
+    # the analyst's input: 4 concatenated 12-way softmax vectors per clip (analyst_training.py:94-99)
+    lg = np.random.default_rng(10).normal(0, 3, (6, 4, 12))
+    probs = (np.exp(lg) / np.exp(lg).sum(-1, keepdims=True)).reshape(6, 48).astype(np.float32)
+    torch.manual_seed(0)
+    model_golden("analyst_golden.npz", R_an.Network(), probs, np.array([0, 3, 11, 5, 5, 10]), train_mode=True)
 
 
 if __name__ == "__main__":

@@ -9,15 +9,15 @@ from conftest import golden
 from oracle import models as OM
 from tolerances import LOGITS_REL, rel_err
 from speechrecognitionproject_amd import nn as snn
-from speechrecognitionproject_amd.models import (model_cnn_bgru, model_mfcc_bgru, model_mfrn_bgru, model_spec_bgru,
-                                                 model_spec_cnn)
+from speechrecognitionproject_amd.models import (model_analyst, model_cnn_bgru, model_mfcc_bgru, model_mfrn_bgru,
+                                                 model_spec_bgru, model_spec_cnn)
 from speechrecognitionproject_amd.optim import Adam
 
 pytestmark = pytest.mark.gpu
 
 PLUGINS = {"mfcc_bgru": (model_mfcc_bgru, OM.MfccBGRU), "spec_bgru": (model_spec_bgru, OM.SpecBGRU),
            "mfrn_bgru": (model_mfrn_bgru, OM.MfrnBGRU), "cnn_bgru": (model_cnn_bgru, OM.CnnBGRU),
-           "spec_cnn": (model_spec_cnn, OM.SpecCNN)}
+           "spec_cnn": (model_spec_cnn, OM.SpecCNN), "analyst": (model_analyst, OM.Analyst)}
 
 
 @pytest.mark.parametrize("name", sorted(PLUGINS))

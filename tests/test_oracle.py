@@ -80,7 +80,7 @@ def test_noise_mix_oracle_vs_reference():
 @pytest.mark.parametrize("name,cls", [("fbanks_cnn", OM.FbanksCNN), ("mfcc_bgru", OM.MfccBGRU),
                                       ("spec_bgru", OM.SpecBGRU), ("resnet_bgru", OM.ResnetBGRU),
                                       ("mfrn_bgru", OM.MfrnBGRU), ("cnn_bgru", OM.CnnBGRU),
-                                      ("spec_cnn", OM.SpecCNN)])
+                                      ("spec_cnn", OM.SpecCNN), ("analyst", OM.Analyst)])
 def test_model_oracle_vs_reference(name, cls):
     g = golden(name + "_golden.npz")
     net = cls()

@@ -1,2 +1,2 @@
 mkdir -p gpurun_out
-timeout -k 10 600 python tools/input_bench.py > gpurun_out/input_bench.json 2> gpurun_out/input_bench.err; tail -3 gpurun_out/input_bench.err; cat gpurun_out/input_bench.json
+timeout -k 10 600 python -m pytest tests/test_evaluation_gpu.py tests/test_models_gpu.py -q -x -m gpu > gpurun_out/t.log 2>&1; tail -5 gpurun_out/t.log

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
 
 #include "gemm.h"
 #include "mfma_tile.h"
@@ -38,13 +39,26 @@ struct KernelArgs {
 
 // NW = waves per workgroup: 4 (2 x 2, each wave (BM/2) x (BN/2)) or 8 (2 x 4, each (BM/2) x (BN/4):
 // twice the waves per SIMD to cover the k-tile barrier / staging phases).
-template <bool TA, bool TB, int BM, int BN, int BK, bool VEC, int NW>
+#ifndef SRK_GEMM_PREFETCH
+#define SRK_GEMM_PREFETCH 1
+#endif
+constexpr int kGemmPrefetch = SRK_GEMM_PREFETCH;   // k-tiles staged ahead in registers (1 or 2)
+static_assert(kGemmPrefetch == 1 || kGemmPrefetch == 2, "SRK_GEMM_PREFETCH must be 1 or 2");
+
+// 16 zero bytes: the LDS-DMA source of k >= ke quads (the k tail must multiply as exact zeros)
+__device__ __attribute__((aligned(16))) float g_zero4[4];
+
+// GL: operands staged by global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip, lane-linear
+// ImgL images) instead of global_load -> registers -> ds_write (needs the VEC conditions).
+template <bool TA, bool TB, int BM, int BN, int BK, bool VEC, int NW, bool GL = false>
 __global__ __launch_bounds__(NW * 64) void gemm_f32_kernel(KernelArgs ka) {
   constexpr int NT = NW * 64;
-  constexpr int WM = 2, WN = NW / 2;
+  // wave grid: 2 x NW/2, except the 256-row tile (8 waves as 4 x 2: every wave 64 x 64)
+  constexpr int WM = (BM == 256) ? 4 : 2, WN = NW / WM;
   constexpr bool AKC = !TA, BKC = TB;         // k-contiguous in HBM?
-  using IA = Img<AKC, BM, BK>;
-  using IB = Img<BKC, BN, BK>;
+  static_assert(!GL || VEC, "LDS-DMA staging needs the 16-B vector conditions");
+  using IA = std::conditional_t<GL, ImgL<AKC, BM, BK>, Img<AKC, BM, BK>>;
+  using IB = std::conditional_t<GL, ImgL<BKC, BN, BK>, Img<BKC, BN, BK>>;
   constexpr int VA = BM * BK / 4 / NT, VB = BN * BK / 4 / NT;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;   // 32x32 tiles per wave per dim
   static_assert(VA >= 1 && VB >= 1 && TM >= 1 && TN >= 1 && BK % 8 == 0, "bad tile");
@@ -69,7 +83,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_f32_kernel(KernelArgs ka) {
   // >= N (B) only feed output rows / columns that are never stored, and k >= ke (the k tail of the
   // last tile of a split) is zeroed in the A image at LDS-store time (after the MFMAs), which
   // makes those products exactly 0 (clamped B values are copies of finite inputs).
-  v4f ra[VA], rb[VB];
+  // PF register sets: tile t is staged in set t % PF, so with PF = 2 the loads of tile k + 2 are in
+  // flight while tile k is multiplied and tile k + 1 waits in registers for its LDS store.
+  constexpr int PF = kGemmPrefetch;
+  v4f ra[PF][VA], rb[PF][VB];
   // KC: 4 consecutive k of row r (stored [row][ld]);  !KC: rows r..r+3 at k (stored [k][ld])
   auto ld_op = [&](const float* __restrict__ P, int64_t ld, bool kc, int64_t rows, int64_t r, int64_t k) -> v4f {
     if (kc) {
@@ -87,28 +104,28 @@ __global__ __launch_bounds__(NW * 64) void gemm_f32_kernel(KernelArgs ka) {
     for (int e = 0; e < 4; ++e) v[e] = q[r + e < rows ? r + e : rows - 1];
     return v;
   };
-  auto load_tile = [&](int64_t k0) {
+  auto load_tile = [&](int st, int64_t k0) {
 #pragma unroll
     for (int i = 0; i < VA; ++i) {
       const int vi = tid + i * NT;
-      if (AKC) ra[i] = ld_op(A, d.lda, true, d.M, m0 + vi / (BK / 4), k0 + (vi % (BK / 4)) * 4);
-      else     ra[i] = ld_op(A, d.lda, false, d.M, m0 + (vi % (BM / 4)) * 4, k0 + vi / (BM / 4));
+      if (AKC) ra[st][i] = ld_op(A, d.lda, true, d.M, m0 + vi / (BK / 4), k0 + (vi % (BK / 4)) * 4);
+      else     ra[st][i] = ld_op(A, d.lda, false, d.M, m0 + (vi % (BM / 4)) * 4, k0 + vi / (BM / 4));
     }
 #pragma unroll
     for (int i = 0; i < VB; ++i) {
       const int vi = tid + i * NT;
-      if (BKC) rb[i] = ld_op(B, d.ldb, true, d.N, n0 + vi / (BK / 4), k0 + (vi % (BK / 4)) * 4);
-      else     rb[i] = ld_op(B, d.ldb, false, d.N, n0 + (vi % (BN / 4)) * 4, k0 + vi / (BN / 4));
+      if (BKC) rb[st][i] = ld_op(B, d.ldb, true, d.N, n0 + vi / (BK / 4), k0 + (vi % (BK / 4)) * 4);
+      else     rb[st][i] = ld_op(B, d.ldb, false, d.N, n0 + (vi % (BN / 4)) * 4, k0 + vi / (BN / 4));
     }
   };
-  auto store_tile = [&](int buf, int64_t k0) {
+  auto store_tile = [&](int st, int buf, int64_t k0) {
     float* As = smem + buf * (IA::FLOATS + IB::FLOATS);
     float* Bs = As + IA::FLOATS;
     const bool tail = k0 + BK > ke;
 #pragma unroll
     for (int i = 0; i < VA; ++i) {
       const int vi = tid + i * NT;
-      v4f v = ra[i];
+      v4f v = ra[st][i];
       if (AKC) {
         const int kq = (vi % (BK / 4)) * 4;
         if (tail) {
@@ -125,8 +142,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_f32_kernel(KernelArgs ka) {
 #pragma unroll
     for (int i = 0; i < VB; ++i) {
       const int vi = tid + i * NT;
-      if (BKC) st4(Bs + (vi / (BK / 4)) * IB::P + (vi % (BK / 4)) * 4, rb[i]);
-      else     st4(Bs + (vi / (BN / 4)) * IB::P + (vi % (BN / 4)) * 4, rb[i]);
+      if (BKC) st4(Bs + (vi / (BK / 4)) * IB::P + (vi % (BK / 4)) * 4, rb[st][i]);
+      else     st4(Bs + (vi / (BN / 4)) * IB::P + (vi % (BN / 4)) * 4, rb[st][i]);
     }
   };
 
@@ -144,27 +161,93 @@ __global__ __launch_bounds__(NW * 64) void gemm_f32_kernel(KernelArgs ka) {
 
   const int64_t nk = ke > kb0 ? (ke - kb0 + BK - 1) / BK : 0;
   const int lh = lane >> 5, lc = lane & 31;
-  if (nk > 0) {
-    load_tile(kb0);
-    store_tile(0, kb0);
-  }
+  if constexpr (GL) {
+    // LDS-DMA staging: wave w fills 1 KB chunks w, w + NW, ... of each image.  Rows >= M / N are
+    // clamped (finite values feeding discarded outputs), k >= ke quads read zeros.
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    constexpr int CA = IA::FLOATS / 256, CB = IB::FLOATS / 256;
+    static_assert(CA % NW == 0 && CB % NW == 0, "image chunks must split evenly over the waves");
+    auto chunk = [&](auto KC_, auto ROWS_, const float* __restrict__ P, int64_t ld, int64_t rows, int64_t r0,
+                     int64_t k0, float* dst, int c) {
+      constexpr bool KC = decltype(KC_)::value;
+      constexpr int ROWS = decltype(ROWS_)::value;
+      const float* src;
+      if constexpr (KC) {
+        const int row = c * (256 / BK) + lane / (BK / 4);
+        const int lq = (lane % (BK / 4)) ^ ImgL<true, ROWS, BK>::swz(row);
+        const int64_t k = k0 + lq * 4, r = r0 + row < rows ? r0 + row : rows - 1;
+        src = k < ke ? P + r * ld + k : g_zero4;
+      } else {
+        const int64_t k = k0 + c * (256 / ROWS) + lane / (ROWS / 4);
+        const int64_t col = r0 + (lane % (ROWS / 4)) * 4;
+        src = k < ke ? P + k * ld + (col < rows ? col : rows - 4) : g_zero4;
+      }
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr)(dst + c * 256), 16, 0, 0);
+    };
+    auto dma_tile = [&](int buf, int64_t k0) {
+      float* As = smem + buf * (IA::FLOATS + IB::FLOATS);
+      float* Bs = As + IA::FLOATS;
+#pragma unroll
+      for (int i = 0; i < CA / NW; ++i)
+        chunk(std::integral_constant<bool, AKC>{}, std::integral_constant<int, BM>{}, A, d.lda, d.M, m0, k0, As,
+              wave + i * NW);
+#pragma unroll
+      for (int i = 0; i < CB / NW; ++i)
+        chunk(std::integral_constant<bool, BKC>{}, std::integral_constant<int, BN>{}, B, d.ldb, d.N, n0, k0, Bs,
+              wave + i * NW);
+    };
+    if (nk > 0) dma_tile(0, kb0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int64_t kt = 0; kt < nk; ++kt) {
+      const int cur = (int)(kt & 1);
+      if (kt + 1 < nk) dma_tile(cur ^ 1, kb0 + (kt + 1) * BK);   // buffer cur^1 was last read before the barrier
+      const float* As = smem + cur * (IA::FLOATS + IB::FLOATS);
+      const float* Bs = As + IA::FLOATS;
+      mma_stage<IA, IB, TM, TN, BK>(As, Bs, acc, wm0, wn0, lane);
+      if (do_rs) {
+#pragma unroll
+        for (int k = tid / BM; k < BK; k += RSP) rs += IA::elem(As, tid % BM, k);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of tile kt+1 has landed
+      __syncthreads();                                     // ... and every other wave's
+    }
+  } else {
+  if (nk > 0) load_tile(0, kb0);
+  if (PF == 2 && nk > 1) load_tile(1 % PF, kb0 + BK);
+  if (nk > 0) store_tile(0, 0, kb0);
   __syncthreads();
-  for (int64_t kt = 0; kt < nk; ++kt) {
-    const int cur = (int)(kt & 1);
-    if (kt + 1 < nk) load_tile(kb0 + (kt + 1) * BK);
-    const float* As = smem + cur * (IA::FLOATS + IB::FLOATS);
+  // one k-tile: buffer (and register set) parity P = kt & 1 (static, the loop is unrolled by 2)
+  auto step = [&](auto P_, int64_t kt) {
+    constexpr int P = decltype(P_)::value;
+#if !(defined(SRK_GEMM_EXP) && SRK_GEMM_EXP >= 1)   // experiment builds only: no global loads in the loop
+    if (PF == 2) {
+      if (kt + 2 < nk) load_tile(P % PF, kb0 + (kt + 2) * BK);
+    } else {
+      if (kt + 1 < nk) load_tile(0, kb0 + (kt + 1) * BK);
+    }
+#endif
+    const float* As = smem + P * (IA::FLOATS + IB::FLOATS);
     const float* Bs = As + IA::FLOATS;
     mma_stage<IA, IB, TM, TN, BK>(As, Bs, acc, wm0, wn0, lane);
     if (do_rs) {
 #pragma unroll
       for (int k = tid / BM; k < BK; k += RSP)
-        rs += AKC ? As[(tid % BM) * IA::P + k] : As[k * IA::P + tid % BM];
+        rs += IA::elem(As, tid % BM, k);
     }
     asm volatile("" ::: "memory");      // keep the stage-k+1 LDS store (and its vmcnt wait)
     __builtin_amdgcn_sched_barrier(0);   // after this stage's MFMAs
-    if (kt + 1 < nk) store_tile(cur ^ 1, kb0 + (kt + 1) * BK);
+#if defined(SRK_GEMM_EXP) && SRK_GEMM_EXP >= 2   // experiment builds only: no LDS stores either
+    if (false)
+#endif
+    if (kt + 1 < nk) store_tile((P ^ 1) % PF, P ^ 1, kb0 + (kt + 1) * BK);
     __syncthreads();
+  };
+  for (int64_t kt = 0; kt < nk; kt += 2) {
+    step(std::integral_constant<int, 0>{}, kt);
+    if (kt + 1 < nk) step(std::integral_constant<int, 1>{}, kt + 1);
   }
+  }   // register staging
 
   const bool split_mode = ka.partial != nullptr;
   // epilogue.  32x32 accumulator: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
@@ -295,7 +378,8 @@ int launch(const GemmDesc& d, hipStream_t s, bool vec) {
   SRK_REQUIRE(tm * tn <= (INT32_MAX >> 5) && d.batch <= 65535, SRK_ERR_INVALID, "gemm: grid too large");
   static const int remap = env_int("SRK_GEMM_REMAP", 1);
   constexpr int lds = 2 * 4 * (Img<!TA, BM, BK>::FLOATS + Img<TB, BN, BK>::FLOATS);
-  constexpr int per_cu = (160 * 1024) / lds < 8 ? (160 * 1024) / lds : 8;
+  constexpr int per_cu0 = (160 * 1024) / lds < 8 ? (160 * 1024) / lds : 8;
+  constexpr int per_cu = per_cu0 > 0 ? per_cu0 : 1;
   const int64_t slots = (int64_t)kCUs * per_cu;
   KernelArgs ka{};
   ka.d = d;
@@ -321,19 +405,26 @@ int launch(const GemmDesc& d, hipStream_t s, bool vec) {
   // 8 waves (4 per SIMD at 2 workgroups / CU) cover the k-tile staging + barrier phases better
   // (measured: weight-gradient GEMMs +4..17 %); the x W^T projection shape keeps 4.
   static const int waves_env = env_int("SRK_GEMM_WAVES", 0);
-  const int waves = waves_env ? waves_env : ((!TA && TB) ? 4 : 8);
+  const int waves = BM == 256 ? 8 : (waves_env ? waves_env : ((!TA && TB) ? 4 : 8));
   const dim3 grid((unsigned)ka.nblk, 1, (unsigned)d.batch);
+  // LDS-DMA staging (global_load_lds_dwordx4) whenever the 16-B vector conditions hold
+  static const int glds_env = env_int("SRK_GEMM_GLDS", 1);
+  const bool gl = vec && glds_env != 0;
   bool done = false;
   if constexpr (BN >= 128) {
     if (waves == 8) {
-      if (vec) hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK, true, 8>), grid, dim3(512), 0, s, ka);
+      if (gl) hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK, true, 8, true>), grid, dim3(512), 0, s, ka);
+      else if (vec) hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK, true, 8>), grid, dim3(512), 0, s, ka);
       else hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK, false, 8>), grid, dim3(512), 0, s, ka);
       done = true;
     }
   }
-  if (!done) {
-    if (vec) hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK, true, 4>), grid, dim3(256), 0, s, ka);
-    else hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK, false, 4>), grid, dim3(256), 0, s, ka);
+  if constexpr (BM != 256) {
+    if (!done) {
+      if (gl) hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK, true, 4, true>), grid, dim3(256), 0, s, ka);
+      else if (vec) hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK, true, 4>), grid, dim3(256), 0, s, ka);
+      else hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK, false, 4>), grid, dim3(256), 0, s, ka);
+    }
   }
   SRK_CHECK_HIP(hipGetLastError());
   if (splits > 1) {
@@ -350,6 +441,12 @@ int launch(const GemmDesc& d, hipStream_t s, bool vec) {
 
 template <bool TA, bool TB>
 int dispatch_tile(const GemmDesc& d, hipStream_t s, bool vec) {
+  // 256 x 128 tiles (one 8-wave workgroup per CU, 110 KB of LDS) halve the L2 -> CU operand
+  // traffic per flop of the 128 x 128 tile; used when the grid still fills the chip several times
+  static const int tile_env = env_int("SRK_GEMM_TILE", 0);
+  const int64_t t256 = ((d.M + 255) / 256) * ((d.N + 127) / 128) * d.batch;
+  const bool big = tile_env ? tile_env == 256 : (d.M >= 2048 && d.N >= 128 && d.K >= 256 && (t256 >= 512 || d.K >= 4096));
+  if (big) return launch<TA, TB, 256, 128, 32>(d, s, vec);
   const int64_t big_tiles = ((d.M + 127) / 128) * ((d.N + 127) / 128) * d.batch;
   if (d.M > 64 && d.N > 64 && (big_tiles >= 64 || d.K >= 2048)) return launch<TA, TB, 128, 128, 32>(d, s, vec);
   return launch<TA, TB, 64, 64, 32>(d, s, vec);

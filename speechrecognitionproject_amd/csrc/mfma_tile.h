@@ -33,11 +33,41 @@ struct Img {
     const float* q = s + (kb * 8 + 4 * h) * P + row;
     return v4f{q[0], q[P], q[2 * P], q[3 * P]};
   }
+  __device__ static __forceinline__ float elem(const float* s, int row, int k) {
+    return KC ? s[row * P + k] : s[k * P + row];
+  }
   // element offset of the float4 a staging thread writes (row-major walk of the image's source)
   __device__ static __forceinline__ int store_off(int vi) {
     return KC ? (vi / (BK / 4)) * P + (vi % (BK / 4)) * 4 : (vi / (ROWS / 4)) * P + (vi % (ROWS / 4)) * 4;
   }
 };
+
+// Lane-linear LDS images, filled by global_load_lds_dwordx4 (LDS-DMA: a wave-instruction writes
+// 1 KB contiguously, lane l at +16 l), so no padding is possible:
+//   KC:  [row][BK] with the 16-B quads of each row XOR-swizzled by (row >> 1) & (BK/4 - 1) — the
+//        swizzle goes on the GLOBAL source address at load time; a fragment ds_read_b128 of 16 rows
+//        then touches 16 distinct bank quads (rows of one parity get distinct quads);
+//   !KC: [BK][ROWS] unpadded (each half-wave's ds_read_b32 reads 32 consecutive floats).
+template <bool KC, int ROWS, int BK>
+struct ImgL {
+  static constexpr int P = KC ? BK : ROWS;
+  static constexpr int FLOATS = ROWS * BK;
+  static constexpr int QMASK = BK / 4 - 1;
+  __device__ static __forceinline__ int swz(int row) { return (row >> 1) & QMASK; }
+  __device__ static __forceinline__ v4f frag(const float* s, int row, int kb, int h) {
+    if (KC) return ld4(s + row * P + (((kb * 2 + h) ^ swz(row)) << 2));
+    const float* q = s + (kb * 8 + 4 * h) * P + row;
+    return v4f{q[0], q[P], q[2 * P], q[3 * P]};
+  }
+  __device__ static __forceinline__ float elem(const float* s, int row, int k) {
+    return KC ? s[row * P + ((((k >> 2) ^ swz(row))) << 2) + (k & 3)] : s[k * P + row];
+  }
+};
+
+#ifndef SRK_PIN_PREFETCH
+#define SRK_PIN_PREFETCH 1
+#endif
+constexpr bool kPinPrefetch = SRK_PIN_PREFETCH != 0;
 
 // One BK-deep stage: acc[TM][TN] += A_img[wm0 .. +BM/2][k] * B_img[k][wn0 .. +BN/2], fragments of
 // the next 8-deep block are read ahead of this block's MFMAs.
@@ -59,6 +89,9 @@ __device__ __forceinline__ void mma_stage(const float* As, const float* Bs, f32x
 #pragma unroll
       for (int j = 0; j < TN; ++j) fb[c ^ 1][j] = IB::frag(Bs, wn0 + j * 32 + lc, kb + 1, lh);
     }
+    // pin the prefetch ABOVE this block's MFMAs: left alone, the scheduler sinks the ds_reads
+    // below them and the wave then waits on LDS latency with the matrix pipe idle
+    if (kPinPrefetch) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll

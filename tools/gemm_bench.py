@@ -57,7 +57,19 @@ def main():
         ref = Am @ Bmm
         err = float((C.view(M, N) - ref).abs().max() / ref.abs().max())
         tf = w / (ms * 1e-3) / 1e12
-        res[name] = {"us": round(ms / c * 1e3, 1), "TF": round(tf, 1), "frac": round(tf / 157.3, 3), "rel_err": err}
+        # yardstick: torch.matmul (hipBLASLt / rocBLAS fp32) on the same operands
+        out = torch.empty_like(ref)
+        for _ in range(2):
+            torch.matmul(Am, Bmm, out=out)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.reps):
+            torch.matmul(Am, Bmm, out=out)
+        e1.record()
+        torch.cuda.synchronize()
+        t_us = e0.elapsed_time(e1) / a.reps * 1e3
+        res[name] = {"us": round(ms / c * 1e3, 1), "TF": round(tf, 1), "frac": round(tf / 157.3, 3), "rel_err": err,
+                     "torch_us": round(t_us, 1), "torch_TF": round(2.0 * M * N * K / (t_us * 1e-6) / 1e12, 1)}
         print(name, json.dumps(res[name]), flush=True)
     print(json.dumps({"remap": os.environ.get("SRK_GEMM_REMAP", "1"), "shapes": res}))
 

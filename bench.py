@@ -49,6 +49,8 @@ from speechrecognitionproject_amd.optim import Adam, FlatParams       # noqa: E4
 from speechrecognitionproject_amd.synthetic import synthetic_clips    # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3     # MI355X_MICROARCH.md, dense fp32 matrix (= vector) peak
+PEAK_LP_MFMA_TFLOPS = 2500.0      # MI355X_MICROARCH.md, dense bf16 / fp16 MFMA peak (no sparsity)
+FP16_LOSS_SCALE = 1024.0          # static loss scale of the fp16 mode (unscaled in the Adam kernel)
 PEAK_HBM_GBS = 8000.0             # MI355X HBM3E spec
 MFCC_BYTES_PER_CLIP = 71956       # 64,000 in + 7,956 out
 # FlopCounterMode on the reference modules (cnn_bgru / spec_cnn: on the oracle restatements)
@@ -69,7 +71,8 @@ CFG = {"mfcc_bgru": "cfg2 mfcc_bgru: on-device MFCC[39x51] + 2-layer BiGRU(512) 
 FEATURE = {"mfcc_bgru": ("mfcc", 71956), "fbanks_cnn": ("fbank", 111040), "spec_bgru": ("spec", 126916),
            "mfrn_bgru": ("mfcc", 71956), "spec_cnn": ("spec", 126916)}
 MATRIX_KERNELS = ("gru_fwd_seq", "gru_bwd_seq", "gru_fwd_step", "gru_bwd_step", "gemm_f32",
-                  "conv_fwd", "conv_dgrad", "conv_wgrad")
+                  "conv_fwd", "conv_dgrad", "conv_wgrad", "gemm_bf16", "gemm_f16", "gru_fwd_seq_lp", "gru_bwd_seq_lp")
+LP_KERNELS = ("gemm_bf16", "gemm_f16", "gru_fwd_seq_lp", "gru_bwd_seq_lp")
 OTHER_KERNELS = ("mfcc", "fbank", "spec", "noise_mix", "adam", "batchnorm_fwd", "batchnorm_bwd", "conv1_pool_fwd",
                  "conv1_pool_wgrad",
                  "maxpool_fwd", "maxpool_bwd")
@@ -162,6 +165,9 @@ def main():
     ap.add_argument("--model", default="mfcc_bgru")
     ap.add_argument("--pool", type=int, default=4, help="distinct pre-staged batches per rank")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--precision", default="fp32", choices=sorted(_lib.PRECISIONS),
+                    help="matrix-core operand precision (fp32 = the reference's arithmetic; bf16 / fp16 "
+                         "operands with fp32 accumulation)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true")
     ap.add_argument("--no-feature-roofline", "--no-mfcc-roofline", dest="no_feature_roofline", action="store_true")
@@ -170,12 +176,14 @@ def main():
     rank, world, local = parallel.init_from_env()
     features.require_gpu()
     _lib.lib()
+    _lib.set_matmul_precision(args.precision)
+    loss_scale = FP16_LOSS_SCALE if args.precision == "fp16" else 1.0
     dev = torch.device("cuda", local)
     torch.manual_seed(0)
     model = build_model(args.model).to(dev)
     flat = FlatParams(model.parameters())
     opt = Adam(model.parameters(), lr=1e-4, flat=flat)
-    opt.grad_scale = 1.0 / world
+    opt.grad_scale = 1.0 / (world * loss_scale)
     parallel.broadcast_flat(flat)
     crit = CrossEntropyLoss()
 
@@ -205,7 +213,7 @@ def main():
         opt.zero_grad()
         out = model(inputs(i))
         loss = crit(out, lab[i % args.pool])
-        loss.backward()
+        (loss * loss_scale if loss_scale != 1.0 else loss).backward()
         parallel.allreduce_grads(flat)
         opt.step()
         return loss
@@ -250,16 +258,17 @@ def main():
         dom = max(mm, key=lambda k: mm[k]["ms_total"])
         k = mm[dom]
         tf = k["work"] / (k["ms_total"] * 1e-3) / 1e12
-        roof = {"bound": "mfma", "kernel": dom, "achieved": round(tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(tf / PEAK_FP32_MFMA_TFLOPS, 4),
-                "traffic": pmc_traffic(dom) if args.model == "mfcc_bgru" else None, "traffic_unit": "bytes/launch",
+        peak = PEAK_LP_MFMA_TFLOPS if dom in LP_KERNELS else PEAK_FP32_MFMA_TFLOPS
+        roof = {"bound": "mfma", "kernel": dom, "achieved": round(tf, 2), "peak": peak,
+                "unit": "TFLOP/s", "frac": round(tf / peak, 4),
+                "traffic": pmc_traffic(dom) if args.model == "mfcc_bgru" and args.precision == "fp32" else None, "traffic_unit": "bytes/launch",
                 "avg_launch_ms": round(k["ms_total"] / k["launches"], 5),
                 "flops_per_launch": k["work"] / k["launches"]}
     res = {
         "metric": "utterances/sec (1 s @16 kHz) MFCC+CNN-BiGRU train step",
         "value": round(value, 2), "unit": "utt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SURVEY.md §8d clip mix, pre-staged in HBM)",
+        "vs_baseline": None, "dtype": args.precision, "data": "synthetic (SURVEY.md §8d clip mix, pre-staged in HBM)",
         "config": {"workload": "%s, CE, backward, Adam (full training.py step), per-GPU batch %d"
                                % (CFG[args.model], B), "model": args.model,
                    "global_batch": world * B, "clip_samples": 16000, "parallelism": "dp%d" % world},

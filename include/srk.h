@@ -45,7 +45,10 @@ int srk_init(int device);              /* build + upload constant tables on `dev
 int srk_prof_enable(int on);
 int srk_prof_read(const char* name, int64_t* count, double* total_ms, double* total_work);
 /* Runtime options: "gru_persistent" (default 1) = run each GRU layer's recurrence as ONE
- * persistent launch with W_hh resident in LDS (0 = one launch per time step).              */
+ * persistent launch with W_hh resident in LDS (0 = one launch per time step);
+ * "matmul_precision" (default 0) = operand precision of the matrix-core kernels (GEMM, GRU
+ * recurrence): 0 fp32 (exact, the reference's arithmetic), 1 bf16, 2 fp16 — operands rounded to
+ * nearest-even on chip, fp32 accumulation, fp32 tensors in and out (BASELINE.json cfg2 / cfg5). */
 int srk_set_option(const char* name, int64_t value);
 /* Number of bounded spin-waits of the persistent kernels that gave up (synchronizes the
  * device; must stay 0 — a non-zero value means a co-residency assumption failed).  -1 on error. */

@@ -117,6 +117,26 @@ def set_option(name, value):
     call("srk_set_option", name.encode(), int(value))
 
 
+PRECISIONS = {"fp32": 0, "bf16": 1, "fp16": 2}
+_precision = "fp32"
+
+
+def set_matmul_precision(name):
+    """Operand precision of the matrix-core kernels (GEMMs, GRU recurrence): "fp32" (default,
+    exact fp32 MFMA = the reference's arithmetic), "bf16" or "fp16" (operands rounded on chip,
+    fp32 accumulation, fp32 tensors in and out).  Process-wide, like torch's matmul precision
+    switch; the models' constructors and state_dicts are unchanged."""
+    global _precision
+    if name not in PRECISIONS:
+        raise ValueError("matmul precision must be one of %s, got %r" % (sorted(PRECISIONS), name))
+    set_option("matmul_precision", PRECISIONS[name])
+    _precision = name
+
+
+def matmul_precision():
+    return _precision
+
+
 def spin_timeouts():
     """Persistent-kernel spin waits that gave up since load (synchronizes; must stay 0)."""
     return int(lib().srk_spin_timeouts())

@@ -37,6 +37,40 @@ struct KernelArgs {
   float* rs_partial;     // [splits][M] when split and rowsum requested
 };
 
+// Epilogue shared by the tile kernels.  32x32 accumulator: col = lane & 31,
+// row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).  Split-K launches write the raw fp32 slab.
+template <int TM, int TN>
+__device__ __forceinline__ void store_acc(const KernelArgs& ka, const f32x16 (&acc)[TM][TN], int split, int64_t m0,
+                                          int64_t n0, int wm0, int wn0, int lane, int64_t z) {
+  const GemmDesc& d = ka.d;
+  const int lh = lane >> 5, lc = lane & 31;
+  const bool split_mode = ka.partial != nullptr;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t col = n0 + wn0 + j * 32 + lc;
+      if (col >= d.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row >= d.M) continue;
+        if (split_mode) {
+          ka.partial[((int64_t)split * d.M + row) * d.N + col] = acc[i][j][r];
+          continue;
+        }
+        float* C = d.C + z * d.sC;
+        float v = d.alpha * acc[i][j][r];
+        if (d.bias_mode == 1) v += d.bias[col];
+        else if (d.bias_mode == 2) v += d.bias[row];
+        float* c = C + row * d.ldc + col;
+        if (d.beta != 0.f) v += d.beta * *c;
+        *c = v;
+      }
+    }
+  }
+}
+
 // NW = waves per workgroup: 4 (2 x 2, each wave (BM/2) x (BN/2)) or 8 (2 x 4, each (BM/2) x (BN/4):
 // twice the waves per SIMD to cover the k-tile barrier / staging phases).
 #ifndef SRK_GEMM_PREFETCH
@@ -249,32 +283,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_f32_kernel(KernelArgs ka) {
   }
   }   // register staging
 
-  const bool split_mode = ka.partial != nullptr;
-  // epilogue.  32x32 accumulator: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int64_t col = n0 + wn0 + j * 32 + lc;
-      if (col >= d.N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row >= d.M) continue;
-        if (split_mode) {
-          ka.partial[((int64_t)split * d.M + row) * d.N + col] = acc[i][j][r];
-          continue;
-        }
-        float* C = d.C + z * d.sC;
-        float v = d.alpha * acc[i][j][r];
-        if (d.bias_mode == 1) v += d.bias[col];
-        else if (d.bias_mode == 2) v += d.bias[row];
-        float* c = C + row * d.ldc + col;
-        if (d.beta != 0.f) v += d.beta * *c;
-        *c = v;
-      }
-    }
-  }
+  store_acc<TM, TN>(ka, acc, split, m0, n0, wm0, wn0, lane, z);
   if (do_rs) {
     float* red = smem;
     __syncthreads();
@@ -286,7 +295,211 @@ __global__ __launch_bounds__(NW * 64) void gemm_f32_kernel(KernelArgs ka) {
       for (int p = 0; p < RSP; ++p) t += red[p * BM + tid];
       const int64_t row = m0 + tid;
       if (row < d.M) {
-        if (split_mode) ka.rs_partial[(int64_t)split * d.M + row] = t;
+        if (ka.partial) ka.rs_partial[(int64_t)split * d.M + row] = t;
+        else d.rowsum[row] = d.rowsum_beta != 0.f ? d.rowsum_beta * d.rowsum[row] + t : t;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ bf16 / fp16 operands
+// Reduced-precision matrix-core GEMM (srk_set_option "matmul_precision" 1 / 2): the same fp32
+// tensors in HBM, rounded to bf16 / fp16 (nearest-even, v_cvt_pk_*_f32) when a k-tile is staged into
+// LDS, multiplied by v_mfma_f32_32x32x16_{bf16,f16} (1024 FLOP/clk/SIMD = 16x the fp32 MFMA) into
+// fp32 accumulators; the epilogue, split-K slabs and fused row sums stay fp32 (row sums are taken
+// from the fp32 staging registers, before rounding).
+//
+// Tile 128 x 128 x 64, 4 waves (2 x 2, each 64 x 64 = 2 x 2 MFMA tiles).  LDS images are
+// k-contiguous for BOTH operands: [row][64 + 8] 16-bit elements (a 144-B pitch: a fragment
+// ds_read_b128 of 32 rows hits 16 distinct bank quads per lane group).  A lane's MFMA operand is 8
+// consecutive k of one row (k = 16 s + 8 (lane >> 5) + j), one ds_read_b128.  Staging unit per
+// thread: k-contiguous operand -> 8 consecutive k of one row (2 float4 loads, 1 pack); row-contiguous
+// operand -> 8 k x 4 rows (8 float4 loads, transposed in registers into 4 packs).
+template <bool F16>
+struct LpOps;
+template <>
+struct LpOps<false> {
+  typedef __bf16 e8 __attribute__((ext_vector_type(8)));
+  __device__ static __forceinline__ f32x16 mma(e8 a, e8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <>
+struct LpOps<true> {
+  typedef _Float16 e8 __attribute__((ext_vector_type(8)));
+  __device__ static __forceinline__ f32x16 mma(e8 a, e8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+typedef float v8f __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kLpBM = 128, kLpBN = 128, kLpBK = 64;
+constexpr int kLpPitchQ = kLpBK / 8 + 1;            // image row pitch in 16-B quads (72 elements)
+constexpr int kLpImgQ = 128 * kLpPitchQ;            // quads per 128-row image
+
+template <bool TA, bool TB, bool VEC, bool F16>
+__global__ __launch_bounds__(256, 2) void gemm_lp_kernel(KernelArgs ka) {
+  using Ops = LpOps<F16>;
+  using e8 = typename Ops::e8;
+  constexpr int BM = kLpBM, BN = kLpBN, BK = kLpBK, TM = 2, TN = 2;
+  constexpr bool AKC = !TA, BKC = TB;
+  __shared__ __attribute__((aligned(16))) u32x4 smem[2 * 2 * kLpImgQ];   // [stage][A | B] images
+  const GemmDesc& d = ka.d;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int split, tm, tn;
+  map_tile(ka.nblk, ka.tiles, ka.tiles_m, ka.tiles_n, ka.group_m, ka.remap != 0, split, tm, tn);
+  const int64_t z = blockIdx.z;
+  const float* __restrict__ A = d.A + z * d.sA;
+  const float* __restrict__ B = d.B + z * d.sB;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kb0 = split * ka.kchunk;
+  const int64_t ke = (kb0 + ka.kchunk < d.K) ? kb0 + ka.kchunk : d.K;
+  const int wm0 = (wave >> 1) * (BM / 2), wn0 = (wave & 1) * (BN / 2);
+  const bool do_rs = d.rowsum != nullptr && tn == 0;
+  const int kq = tid & 7;          // the thread's 8-deep k chunk of a tile (both unit kinds)
+
+  // staging registers: 8 float4 per operand (KC: 4 units x 2;  !KC: one 8 k x 4 row unit)
+  v4f ra[8], rb[8];
+  // Loads are CLAMPED (rows >= rows -> last row group, k >= ke -> last k) and never predicated; the
+  // k tail is zeroed at LDS-store time in BOTH images (a clamped duplicate may overflow fp16).
+  auto load_op = [&](v4f (&r)[8], const float* __restrict__ P, int64_t ld, bool kc, int64_t rows, int64_t r0,
+                     int64_t k0) {
+    if (kc) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t row = r0 + (tid >> 3) + 32 * u;
+        const float* q = P + (row < rows ? row : rows - 1) * ld;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int64_t k = k0 + kq * 8 + 4 * h;
+          if (VEC) {
+            r[2 * u + h] = ld4(q + (k < ke - 3 ? k : ke - 4));
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) r[2 * u + h][e] = q[k + e < ke ? k + e : ke - 1];
+          }
+        }
+      }
+    } else {
+      const int64_t col = r0 + (tid >> 3) * 4;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int64_t k = k0 + kq * 8 + e;
+        const float* q = P + (k < ke ? k : ke - 1) * ld;
+        if (VEC) {
+          r[e] = ld4(q + (col < rows ? col : rows - 4));
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) r[e][c] = q[col + c < rows ? col + c : rows - 1];
+        }
+      }
+    }
+  };
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};   // fused row sums (A only): KC rows tid/8 + 32 u, !KC rows 4 (tid/8) + c
+  auto store_op = [&](const v4f (&r)[8], u32x4* img, bool kc, int64_t k0, bool rowsum) {
+    const int64_t kbase = k0 + kq * 8;
+    const bool tail = kbase + 8 > ke;
+    if (kc) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v8f v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (tail && kbase + e >= ke) ? 0.f : r[2 * u + (e >> 2)][e & 3];
+        if (rowsum) {
+          float t = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t += v[e];
+          rs[u] += t;
+        }
+        img[((tid >> 3) + 32 * u) * kLpPitchQ + kq] = __builtin_bit_cast(u32x4, __builtin_convertvector(v, e8));
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        v8f v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (tail && kbase + e >= ke) ? 0.f : r[e][c];
+        if (rowsum) {
+          float t = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t += v[e];
+          rs[c] += t;
+        }
+        img[((tid >> 3) * 4 + c) * kLpPitchQ + kq] = __builtin_bit_cast(u32x4, __builtin_convertvector(v, e8));
+      }
+    }
+  };
+  auto load_tile = [&](int64_t k0) {
+    load_op(ra, A, d.lda, AKC, d.M, m0, k0);
+    load_op(rb, B, d.ldb, BKC, d.N, n0, k0);
+  };
+  auto store_tile = [&](int buf, int64_t k0) {
+    u32x4* As = smem + buf * 2 * kLpImgQ;
+    store_op(ra, As, AKC, k0, do_rs);
+    store_op(rb, As + kLpImgQ, BKC, k0, false);
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int lh = lane >> 5, lc = lane & 31;
+  const int64_t nk = ke > kb0 ? (ke - kb0 + BK - 1) / BK : 0;
+  if (nk > 0) {
+    load_tile(kb0);
+    store_tile(0, kb0);
+  }
+  __syncthreads();
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    const int cur = (int)(kt & 1);
+    if (kt + 1 < nk) load_tile(kb0 + (kt + 1) * BK);
+    const u32x4* As = smem + cur * 2 * kLpImgQ;
+    const u32x4* Bs = As + kLpImgQ;
+    u32x4 fa[2][TM], fb[2][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[0][i] = As[(wm0 + i * 32 + lc) * kLpPitchQ + lh];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[0][j] = Bs[(wn0 + j * 32 + lc) * kLpPitchQ + lh];
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int c = ks & 1;
+      if (ks + 1 < BK / 16) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[c ^ 1][i] = As[(wm0 + i * 32 + lc) * kLpPitchQ + 2 * (ks + 1) + lh];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[c ^ 1][j] = Bs[(wn0 + j * 32 + lc) * kLpPitchQ + 2 * (ks + 1) + lh];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = Ops::mma(__builtin_bit_cast(e8, fa[c][i]), __builtin_bit_cast(e8, fb[c][j]), acc[i][j]);
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);   // the next tile's LDS store after this tile's MFMAs
+    if (kt + 1 < nk) store_tile(cur ^ 1, kb0 + (kt + 1) * BK);
+    __syncthreads();
+  }
+  store_acc<TM, TN>(ka, acc, split, m0, n0, wm0, wn0, lane, z);
+  if (do_rs) {   // deterministic: partials [k chunk][row] in LDS, summed in chunk order
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) red[kq * BM + (AKC ? (tid >> 3) + 32 * u : (tid >> 3) * 4 + u)] = rs[u];
+    __syncthreads();
+    if (tid < BM) {
+      float t = 0.f;
+#pragma unroll
+      for (int p = 0; p < 8; ++p) t += red[p * BM + tid];
+      const int64_t row = m0 + tid;
+      if (row < d.M) {
+        if (ka.partial) ka.rs_partial[(int64_t)split * d.M + row] = t;
         else d.rowsum[row] = d.rowsum_beta != 0.f ? d.rowsum_beta * d.rowsum[row] + t : t;
       }
     }
@@ -372,16 +585,14 @@ int env_int(const char* name, int dflt) {
   return v && *v ? atoi(v) : dflt;
 }
 
-template <bool TA, bool TB, int BM, int BN, int BK>
-int launch(const GemmDesc& d, hipStream_t s, bool vec) {
+// Grid, split-K and scratch for one launch of a BM x BN x BK tile kernel with `per_cu` resident
+// workgroups per CU; fills ka and returns the split count (tile::choose_splits).
+int plan_launch(const GemmDesc& d, int BM, int BN, int BK, int per_cu, KernelArgs& ka, int* splits_out) {
   const int64_t tm = (d.M + BM - 1) / BM, tn = (d.N + BN - 1) / BN;
   SRK_REQUIRE(tm * tn <= (INT32_MAX >> 5) && d.batch <= 65535, SRK_ERR_INVALID, "gemm: grid too large");
   static const int remap = env_int("SRK_GEMM_REMAP", 1);
-  constexpr int lds = 2 * 4 * (Img<!TA, BM, BK>::FLOATS + Img<TB, BN, BK>::FLOATS);
-  constexpr int per_cu0 = (160 * 1024) / lds < 8 ? (160 * 1024) / lds : 8;
-  constexpr int per_cu = per_cu0 > 0 ? per_cu0 : 1;
   const int64_t slots = (int64_t)kCUs * per_cu;
-  KernelArgs ka{};
+  ka = KernelArgs{};
   ka.d = d;
   ka.tiles_m = (int)tm;
   ka.tiles_n = (int)tn;
@@ -389,8 +600,7 @@ int launch(const GemmDesc& d, hipStream_t s, bool vec) {
   ka.group_m = 8;
   ka.remap = remap;
   // Split K when the output grid leaves resident slots idle and K is long (tile::choose_splits).
-  const int splits0 = d.batch == 1 ? choose_splits(tm * tn, d.K, BK, slots, 16) : 1;
-  int splits = splits0;
+  int splits = d.batch == 1 ? choose_splits(tm * tn, d.K, BK, slots, 16) : 1;
   ka.kchunk = splits > 1 ? ((d.K + splits - 1) / splits + BK - 1) / BK * BK : std::max<int64_t>(d.K, 1);
   if (splits > 1) splits = (int)((d.K + ka.kchunk - 1) / ka.kchunk);
   ka.nblk = ka.tiles * splits;
@@ -401,6 +611,33 @@ int launch(const GemmDesc& d, hipStream_t s, bool vec) {
     ka.partial = scratch;
     ka.rs_partial = d.rowsum ? scratch + (size_t)splits * d.M * d.N : nullptr;
   }
+  *splits_out = splits;
+  return SRK_OK;
+}
+
+// After a split launch: the deterministic slab reduction (+ epilogue) and the row-sum reduction.
+int finish_splits(const GemmDesc& d, const KernelArgs& ka, int splits, hipStream_t s) {
+  SRK_CHECK_HIP(hipGetLastError());
+  if (splits > 1) {
+    const int64_t n = d.M * d.N;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, ka.partial,
+                       splits);
+    if (d.rowsum)
+      hipLaunchKernelGGL(rowsum_reduce_kernel, dim3((unsigned)((d.M + 255) / 256)), dim3(256), 0, s, d.rowsum,
+                         d.rowsum_beta, ka.rs_partial, d.M, splits);
+    SRK_CHECK_HIP(hipGetLastError());
+  }
+  return SRK_OK;
+}
+
+template <bool TA, bool TB, int BM, int BN, int BK>
+int launch(const GemmDesc& d, hipStream_t s, bool vec) {
+  constexpr int lds = 2 * 4 * (Img<!TA, BM, BK>::FLOATS + Img<TB, BN, BK>::FLOATS);
+  constexpr int per_cu0 = (160 * 1024) / lds < 8 ? (160 * 1024) / lds : 8;
+  constexpr int per_cu = per_cu0 > 0 ? per_cu0 : 1;
+  KernelArgs ka;
+  int splits = 1;
+  if (int rc = plan_launch(d, BM, BN, BK, per_cu, ka, &splits)) return rc;
   ProfScope prof("gemm_f32", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
   // 8 waves (4 per SIMD at 2 workgroups / CU) cover the k-tile staging + barrier phases better
   // (measured: weight-gradient GEMMs +4..17 %); the x W^T projection shape keeps 4.
@@ -426,21 +663,30 @@ int launch(const GemmDesc& d, hipStream_t s, bool vec) {
       else hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, BM, BN, BK, false, 4>), grid, dim3(256), 0, s, ka);
     }
   }
-  SRK_CHECK_HIP(hipGetLastError());
-  if (splits > 1) {
-    const int64_t n = d.M * d.N;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, ka.partial,
-                       splits);
-    if (d.rowsum)
-      hipLaunchKernelGGL(rowsum_reduce_kernel, dim3((unsigned)((d.M + 255) / 256)), dim3(256), 0, s, d.rowsum,
-                         d.rowsum_beta, ka.rs_partial, d.M, splits);
-    SRK_CHECK_HIP(hipGetLastError());
+  return finish_splits(d, ka, splits, s);
+}
+
+template <bool TA, bool TB>
+int launch_lp(const GemmDesc& d, hipStream_t s, bool vec, bool f16) {
+  KernelArgs ka;
+  int splits = 1;
+  if (int rc = plan_launch(d, kLpBM, kLpBN, kLpBK, 2, ka, &splits)) return rc;
+  ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
+  const dim3 grid((unsigned)ka.nblk, 1, (unsigned)d.batch);
+  if (f16) {
+    if (vec) hipLaunchKernelGGL((gemm_lp_kernel<TA, TB, true, true>), grid, dim3(256), 0, s, ka);
+    else hipLaunchKernelGGL((gemm_lp_kernel<TA, TB, false, true>), grid, dim3(256), 0, s, ka);
+  } else {
+    if (vec) hipLaunchKernelGGL((gemm_lp_kernel<TA, TB, true, false>), grid, dim3(256), 0, s, ka);
+    else hipLaunchKernelGGL((gemm_lp_kernel<TA, TB, false, false>), grid, dim3(256), 0, s, ka);
   }
-  return SRK_OK;
+  return finish_splits(d, ka, splits, s);
 }
 
 template <bool TA, bool TB>
 int dispatch_tile(const GemmDesc& d, hipStream_t s, bool vec) {
+  const int prec = d.prec >= 0 ? d.prec : matmul_prec();
+  if (prec != kPrecF32) return launch_lp<TA, TB>(d, s, vec, prec == kPrecF16);
   // 256 x 128 tiles (one 8-wave workgroup per CU, 110 KB of LDS) halve the L2 -> CU operand
   // traffic per flop of the 128 x 128 tile; used when the grid still fills the chip several times
   static const int tile_env = env_int("SRK_GEMM_TILE", 0);

@@ -27,6 +27,8 @@
 // Every spin is bounded: a workgroup that waits ~2 s gives up, bumps g_spin_timeouts (read by
 // srk_spin_timeouts(); the tests assert it stays 0) and carries on, so a fault can never hang the
 // GPU.
+#include <mutex>
+
 #include "gru_internal.h"
 
 namespace srk {
@@ -368,27 +370,342 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
   }
 }
 
+// ------------------------------------------------------------------ bf16 / fp16 operands
+// The same two kernels with the recurrent matmul on v_mfma_f32_16x16x32_{bf16,f16} (16x the fp32
+// MFMA rate; srk_set_option "matmul_precision" 1 / 2): the W_hh slice is held in LDS rounded to
+// 16 bits (half the bytes), the hand-off carries h (fwd) / dg (bwd) rounded to 16 bits in
+// fragment order — a 1 KB chunk per (16-row block, 32-wide k block): lane l holds the 8 k
+// 32 kb + 8 (l >> 4) + j of row l & 15, one 16-B load per MFMA — and everything else (gates,
+// cell update, the register carries, y, dgi, dgh) stays fp32.  A 16-unit slice s fills half of
+// k block s / 2 (lane quarter-rows q = 2 (s & 1) + {0, 1}), 8 units per 16-B store.
+template <bool F16>
+struct RecOps;
+template <>
+struct RecOps<false> {
+  typedef __bf16 e8 __attribute__((ext_vector_type(8)));
+  __device__ static __forceinline__ f32x4 mma(e8 a, e8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <>
+struct RecOps<true> {
+  typedef _Float16 e8 __attribute__((ext_vector_type(8)));
+  __device__ static __forceinline__ f32x4 mma(e8 a, e8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+typedef float v8f __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool F16>
+__device__ __forceinline__ u32x4 pack8(v8f v) {
+  return __builtin_bit_cast(u32x4, __builtin_convertvector(v, typename RecOps<F16>::e8));
+}
+__device__ __forceinline__ v8f cat8(v4f lo, v4f hi) { return v8f{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w}; }
+
+// row pitches in 16-bit elements (+16: a ds_read_b128 B-fragment of 16 rows x 4 quarter-rows hits
+// 16 distinct bank quads per lane group)
+template <int H> constexpr int lp_fwd_wpe() { return H + 16; }
+template <int H> constexpr int lp_bwd_wpe() { return 3 * H + 16; }
+
+// LDS: W slice [48][H + 16] (16-bit; gate g, unit jj -> row g*16 + jj), then hT [64][20] fp32.
+template <int H, bool F16>
+__global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs a) {
+  using Ops = RecOps<F16>;
+  using e8 = typename Ops::e8;
+  constexpr int WPQ = lp_fwd_wpe<H>() / 8, HTP = kUnits + 4, NKB = H / 32;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  u32x4* Ws = reinterpret_cast<u32x4*>(smem);
+  float* hT = smem + 3 * kUnits * WPQ * 4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
+  int dir, group, slice;
+  map_block(a.G, H / kUnits, dir, group, slice);
+  const int T = a.T, j0 = slice * kUnits, j = j0 + lr;
+  const int b0 = a.b_begin + group * kRows;
+  const int b_last = a.b_end - 1;
+  unsigned* cnt = a.counters + (dir * a.G + group) * 16;
+
+  {  // this slice of W_hh[dir], rounded to 16 bits -> LDS (read once per layer)
+    const float* W = a.w_hh + (size_t)dir * 3 * H * H;
+    for (int v = tid; v < 3 * kUnits * (H / 8); v += 256) {
+      const int c = v / (H / 8), kq = v % (H / 8), g = c / kUnits, jj = c % kUnits;
+      const float* src = W + (size_t)(g * H + j0 + jj) * H + kq * 8;
+      Ws[c * WPQ + kq] = pack8<F16>(cat8(ld4(src), ld4(src + 4)));
+    }
+  }
+  const float bhr = a.b_hh[dir * 3 * H + j], bhz = a.b_hh[dir * 3 * H + H + j], bhn = a.b_hh[dir * 3 * H + 2 * H + j];
+  __syncthreads();
+
+  const int Gp = a.G;
+  const __amdgpu_buffer_rsrc_t rx = rsrc(a.xbuf + (size_t)dir * 2 * Gp * 64 * H);   // 16-bit [2][Gp][4][H/32][64][8]
+  float hreg[4] = {0.f, 0.f, 0.f, 0.f};
+
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? step : T - 1 - step;
+    stamp(a, step, 0);
+    float gr[4], gz[4], gn[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = min(b0 + wave * 16 + lq * 4 + r, b_last);
+      const float* gi = a.gi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
+      gr[r] = gi[j];
+      gz[r] = gi[H + j];
+      gn[r] = gi[2 * H + j];
+    }
+    f32x4 acc[3];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (step > 0) {
+      wait_count(cnt, (unsigned)(H / kUnits) * step);
+      stamp(a, step, 1);
+      const unsigned base = (unsigned)(((((size_t)((step - 1) & 1) * Gp + group) * 4 + wave) * NKB * 64 + lane) * 16);
+      const int rot = slice % NKB;   // per-slice k rotation, see the fp32 kernel
+      v4f hv[NKB];
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) hv[kb] = ld4_sc1(rx, base + ((kb + rot) & (NKB - 1)) * 1024);
+      __builtin_amdgcn_sched_barrier(0);
+      u32x4 wv[2][3];
+#pragma unroll
+      for (int g = 0; g < 3; ++g) wv[0][g] = Ws[(g * kUnits + lr) * WPQ + rot * 4 + lq];
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) {
+        const int c = kb & 1;
+        if (kb + 1 < NKB) {
+          const int kn = (kb + 1 + rot) & (NKB - 1);
+#pragma unroll
+          for (int g = 0; g < 3; ++g) wv[c ^ 1][g] = Ws[(g * kUnits + lr) * WPQ + kn * 4 + lq];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const e8 hf = __builtin_bit_cast(e8, hv[kb]);
+#pragma unroll
+        for (int g = 0; g < 3; ++g) acc[g] = Ops::mma(hf, __builtin_bit_cast(e8, wv[c][g]), acc[g]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (a.trace) {
+        asm volatile("" ::"v"(acc[0][0]), "v"(acc[1][0]), "v"(acc[2][0]));
+        stamp(a, step, 2);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = wave * 16 + lq * 4 + r, b = b0 + rl;
+      const float ghn = acc[2][r] + bhn;
+      const float rg = sigmoidf_(gr[r] + (acc[0][r] + bhr));
+      const float zg = sigmoidf_(gz[r] + (acc[1][r] + bhz));
+      const float ng = tanhf(gn[r] + rg * ghn);
+      const float h = (1.0f - zg) * ng + zg * hreg[r];
+      hreg[r] = h;
+      hT[rl * HTP + lr] = h;
+      if (b <= b_last) {
+        float* gs = a.gates + (((size_t)dir * T + t) * a.B + b) * 4 * H;
+        gs[j] = rg;
+        gs[H + j] = zg;
+        gs[2 * H + j] = ng;
+        gs[3 * H + j] = ghn;
+      }
+    }
+    __syncthreads();
+    stamp(a, step, 3);
+    {  // y (fp32): thread = (row tid/4, units 4*(tid%4) .. +3)
+      const int rl = tid >> 2, uq = (tid & 3) * 4, b = b0 + rl;
+      if (b <= b_last) st4(a.y + ((size_t)b * T + t) * 2 * H + dir * H + j0 + uq, ld4(hT + rl * HTP + uq));
+    }
+    if (step + 1 < T && tid < 128) {   // hand-off (16-bit): thread = (row tid/2, units 8*(tid%2) .. +7)
+      const int rl = tid >> 1, half = tid & 1;
+      if (b0 + rl <= b_last) {
+        const float* src = hT + rl * HTP + 8 * half;
+        const int l = (2 * (slice & 1) + half) * 16 + (rl & 15);
+        st4_sc1(rx, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB + (slice >> 1)) * 64 + l) * 16,
+                __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))));
+      }
+    }
+    arrive(cnt);
+    stamp(a, step, 4);
+  }
+}
+
+// LDS: W^T slice [16][3H + 16] (16-bit; unit jj, gate row c), then the dg transpose tile [64][3][20].
+template <int H, bool F16>
+__global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs a) {
+  using Ops = RecOps<F16>;
+  using e8 = typename Ops::e8;
+  constexpr int WPQ = lp_bwd_wpe<H>() / 8, DTP = kUnits + 4, NKB = 3 * H / 32, CH = 16;
+  static_assert(NKB % CH == 0, "chunking");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  u32x4* Wt = reinterpret_cast<u32x4*>(smem);
+  float* dT = smem + kUnits * WPQ * 4;   // [64][3][DTP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
+  int dir, group, slice;
+  map_block(a.G, H / kUnits, dir, group, slice);
+  const int T = a.T, B = a.B, j0 = slice * kUnits, j = j0 + lr;
+  const int b0 = a.b_begin + group * kRows;
+  const int b_last = a.b_end - 1;
+  unsigned* cnt = a.counters + (dir * a.G + group) * 16;
+
+  {  // W_hh[dir][c][j0 .. j0+15], all 3H rows c, transposed [jj][c] in 8-deep c packs
+    const float* W = a.w_hh + (size_t)dir * 3 * H * H;
+    for (int v = tid; v < (3 * H / 8) * (kUnits / 4); v += 256) {
+      const int cb = v / (kUnits / 4), jq = (v % (kUnits / 4)) * 4;
+      v4f w[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) w[e] = ld4(W + (size_t)(cb * 8 + e) * H + j0 + jq);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        Wt[(jq + u) * WPQ + cb] = pack8<F16>(v8f{w[0][u], w[1][u], w[2][u], w[3][u], w[4][u], w[5][u], w[6][u], w[7][u]});
+    }
+  }
+  __syncthreads();
+
+  float* dgh_dir = a.dgh + (size_t)dir * B * T * 3 * H;
+  const int Gp = a.G;
+  const __amdgpu_buffer_rsrc_t rg_ = rsrc(a.xbuf + (size_t)dir * 2 * Gp * 64 * 3 * H);   // 16-bit [2][Gp][4][3H/32][64][8]
+  float dhz[4] = {0.f, 0.f, 0.f, 0.f};
+
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? T - 1 - step : step;
+    const int tprev = dir == 0 ? t - 1 : t + 1;
+    const bool edge = (step == T - 1);
+    stamp(a, step, 0);
+    float g_r[4], g_z[4], g_n[4], g_h[4], dyv[4], hpv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = min(b0 + wave * 16 + lq * 4 + r, b_last);
+      const float* gs = a.gates + (((size_t)dir * T + t) * B + b) * 4 * H;
+      g_r[r] = gs[j];
+      g_z[r] = gs[H + j];
+      g_n[r] = gs[2 * H + j];
+      g_h[r] = gs[3 * H + j];
+      dyv[r] = a.dy[((size_t)b * T + t) * 2 * H + dir * H + j];
+      hpv[r] = edge ? 0.f : a.y_in[((size_t)b * T + tprev) * 2 * H + dir * H + j];
+    }
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    if (step > 0) {
+      wait_count(cnt, (unsigned)(H / kUnits) * step);
+      stamp(a, step, 1);
+      const unsigned base = (unsigned)(((((size_t)((step - 1) & 1) * Gp + group) * 4 + wave) * NKB * 64 + lane) * 16);
+      const int rot = (slice * (NKB / (H / kUnits))) % NKB;
+      auto kr = [&](int i) { const int v = i + rot; return v >= NKB ? v - NKB : v; };
+      v4f dv[2][CH];
+#pragma unroll
+      for (int kb = 0; kb < CH; ++kb) dv[0][kb] = ld4_sc1(rg_, base + kr(kb) * 1024);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ch = 0; ch < NKB / CH; ++ch) {
+        const int cur = ch & 1;
+        if (ch + 1 < NKB / CH) {
+#pragma unroll
+          for (int kb = 0; kb < CH; ++kb) dv[cur ^ 1][kb] = ld4_sc1(rg_, base + kr((ch + 1) * CH + kb) * 1024);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        u32x4 wv[2];
+        wv[0] = Wt[lr * WPQ + kr(ch * CH) * 4 + lq];
+#pragma unroll
+        for (int kb = 0; kb < CH; ++kb) {
+          const int c = kb & 1;
+          if (kb + 1 < CH) wv[c ^ 1] = Wt[lr * WPQ + kr(ch * CH + kb + 1) * 4 + lq];
+          __builtin_amdgcn_sched_barrier(0);
+          acc[c] = Ops::mma(__builtin_bit_cast(e8, dv[cur][kb]), __builtin_bit_cast(e8, wv[c]), acc[c]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (a.trace) {
+        asm volatile("" ::"v"(acc[0][0]), "v"(acc[1][0]));
+        stamp(a, step, 2);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = wave * 16 + lq * 4 + r, b = b0 + rl;
+      float dh = dyv[r];
+      if (step > 0) dh += (acc[0][r] + acc[1][r]) + dhz[r];
+      const float rg = g_r[r], zg = g_z[r], ng = g_n[r], ghn = g_h[r], hp = hpv[r];
+      const float dn = dh * (1.0f - zg);
+      const float daz = dh * (hp - ng) * zg * (1.0f - zg);
+      const float dan = dn * (1.0f - ng * ng);
+      const float dar = dan * ghn * rg * (1.0f - rg);
+      dhz[r] = dh * zg;
+      dT[(rl * 3 + 0) * DTP + lr] = dar;
+      dT[(rl * 3 + 1) * DTP + lr] = daz;
+      dT[(rl * 3 + 2) * DTP + lr] = dan * rg;
+      if (b <= b_last) {
+        float* dgi = a.dgi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
+        dgi[j] = dar;
+        dgi[H + j] = daz;
+        dgi[2 * H + j] = dan;
+      }
+    }
+    __syncthreads();
+    stamp(a, step, 3);
+    // dgh (fp32, the dW_hh GEMM operand): as the fp32 kernel; the edge step goes to dgh_edge
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int v = tid + i * 256, rl = v / 12, g = (v % 12) / 4, uq = (v % 4) * 4, b = b0 + rl;
+      if (b > b_last) continue;
+      const v4f val = ld4(dT + (rl * 3 + g) * DTP + uq);
+      if (!edge) {
+        st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + j0 + uq, val);
+      } else {
+        st4(a.dgh_edge + ((size_t)dir * B + b) * 3 * H + g * H + j0 + uq, val);
+        st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + j0 + uq, v4f{0.f, 0.f, 0.f, 0.f});
+      }
+    }
+    if (!edge) {   // hand-off (16-bit): 64 rows x 3 gates x 2 halves of 8 units
+      for (int v = tid; v < 64 * 3 * 2; v += 256) {
+        const int rl = v / 6, g = (v % 6) >> 1, half = v & 1;
+        if (b0 + rl > b_last) continue;
+        const float* src = dT + (rl * 3 + g) * DTP + 8 * half;
+        const int l = (2 * (slice & 1) + half) * 16 + (rl & 15);
+        const int kb = g * (H / 32) + (slice >> 1);
+        st4_sc1(rg_, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB + kb) * 64 + l) * 16,
+                __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))));
+      }
+    }
+    arrive(cnt);
+    stamp(a, step, 4);
+  }
+}
+
+size_t lds_bytes(int H, bool backward, int prec) {
+  if (prec == kPrecF32) return backward ? bwd_lds_bytes(H) : fwd_lds_bytes(H);
+  const size_t need = backward ? (size_t)kUnits * (3 * H + 16) * 2 + 64 * 3 * (kUnits + 4) * 4
+                               : (size_t)3 * kUnits * (H + 16) * 2 + 64 * (kUnits + 4) * 4;
+  // the sc1 hand-off is the form measured at ONE workgroup per CU (MI355X_MICROARCH.md, "Valid
+  // forms" row 1): reserve more than half of the 160 KB so a second workgroup never fits
+  return std::max<size_t>(need, 96 * 1024);
+}
+
 template <int H>
-int occupancy_ok(bool backward, int grid, size_t lds) {
-  static int cus = -1, occ_f = -1, occ_b = -1;
+const void* kernel_ptr(bool backward, int prec) {
+  if (prec == kPrecBF16)
+    return backward ? reinterpret_cast<const void*>(gru_bwd_persistent_lp_kernel<H, false>)
+                    : reinterpret_cast<const void*>(gru_fwd_persistent_lp_kernel<H, false>);
+  if (prec == kPrecF16)
+    return backward ? reinterpret_cast<const void*>(gru_bwd_persistent_lp_kernel<H, true>)
+                    : reinterpret_cast<const void*>(gru_fwd_persistent_lp_kernel<H, true>);
+  return backward ? reinterpret_cast<const void*>(gru_bwd_persistent_kernel<H>)
+                  : reinterpret_cast<const void*>(gru_fwd_persistent_kernel<H>);
+}
+
+template <int H>
+int occupancy_ok(bool backward, int prec, int grid) {
+  static std::mutex mu;
+  static int cus = -1, occ[2][3] = {{-1, -1, -1}, {-1, -1, -1}};
+  std::lock_guard<std::mutex> lk(mu);
   if (cus < 0) {
     int dev = 0;
     SRK_CHECK_HIP(hipGetDevice(&dev));
     hipDeviceProp_t p;
     SRK_CHECK_HIP(hipGetDeviceProperties(&p, dev));
     cus = p.multiProcessorCount;
-    SRK_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_fwd_persistent_kernel<H>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)fwd_lds_bytes(H)));
-    SRK_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_bwd_persistent_kernel<H>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd_lds_bytes(H)));
-    SRK_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, gru_fwd_persistent_kernel<H>, 256,
-                                                               fwd_lds_bytes(H)));
-    SRK_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_b, gru_bwd_persistent_kernel<H>, 256,
-                                                               bwd_lds_bytes(H)));
   }
-  (void)lds;
-  const int occ = backward ? occ_b : occ_f;
-  return (occ >= 1 && grid <= cus) ? 1 : 0;   // one workgroup per CU: the sc1 hand-off form measured
+  int& o = occ[backward ? 1 : 0][prec];
+  if (o < 0) {
+    const void* k = kernel_ptr<H>(backward, prec);
+    const size_t lds = lds_bytes(H, backward, prec);
+    SRK_CHECK_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    SRK_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, 256, lds));
+  }
+  return (o >= 1 && grid <= cus) ? 1 : 0;   // one workgroup per CU: the sc1 hand-off form measured
 }
 
 }  // namespace
@@ -408,7 +725,7 @@ int gru_persistent_supported(int64_t B, int64_t T, int64_t H, bool backward) {
   if ((double)B * T * 3 * H * 4 >= 2147483647.0 || (double)B * T * 2 * H * 4 >= 2147483647.0) return 0;
   const int64_t G = std::min<int64_t>((B + kRows - 1) / kRows, gmax);
   const int grid = (int)(2 * G * (H / kUnits));
-  const int ok = occupancy_ok<512>(backward, grid, backward ? bwd_lds_bytes(512) : fwd_lds_bytes(512));
+  const int ok = occupancy_ok<512>(backward, matmul_prec(), grid);
   return ok < 0 ? 0 : ok;
 }
 
@@ -416,6 +733,7 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
   const int gmax = gru_persistent_groups(a.H);
   SRK_REQUIRE(gmax > 0 && a.H == 512, SRK_ERR_INVALID, "gru persistent: unsupported H");
   const int rows_per_launch = gmax * kRows;
+  const int prec = matmul_prec();
   for (int c0 = 0; c0 < a.B; c0 += rows_per_launch) {
     GruPArgs ac = a;
     ac.trace = g_opt_gru_trace;
@@ -424,13 +742,11 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     ac.G = (ac.b_end - c0 + kRows - 1) / kRows;
     SRK_CHECK_HIP(hipMemsetAsync(ac.counters, 0, (size_t)kCounterFloats * 4, s));
     const dim3 grid((unsigned)(2 * ac.G * (a.H / kUnits)));
-    if (!backward) {
-      ProfScope prof("gru_fwd_seq", s, 2.0 * 2.0 * (double)(ac.b_end - c0) * 3 * a.H * a.H * (a.T - 1));
-      hipLaunchKernelGGL(gru_fwd_persistent_kernel<512>, grid, dim3(256), fwd_lds_bytes(512), s, ac);
-    } else {
-      ProfScope prof("gru_bwd_seq", s, 2.0 * 2.0 * (double)(ac.b_end - c0) * 3 * a.H * a.H * (a.T - 1));
-      hipLaunchKernelGGL(gru_bwd_persistent_kernel<512>, grid, dim3(256), bwd_lds_bytes(512), s, ac);
-    }
+    const double flops = 2.0 * 2.0 * (double)(ac.b_end - c0) * 3 * a.H * a.H * (a.T - 1);
+    ProfScope prof(backward ? (prec == kPrecF32 ? "gru_bwd_seq" : "gru_bwd_seq_lp")
+                            : (prec == kPrecF32 ? "gru_fwd_seq" : "gru_fwd_seq_lp"), s, flops);
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(kernel_ptr<512>(backward, prec))), grid,
+                       dim3(256), lds_bytes(512, backward, prec), s, ac);
     SRK_CHECK_HIP(hipGetLastError());
   }
   return SRK_OK;

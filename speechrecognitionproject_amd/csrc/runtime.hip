@@ -7,6 +7,7 @@
 //  * DCT-II ortho [:13]    librosa.filters.dct / scipy.fftpack.dct(norm='ortho')
 //  * windows               np.hamming(400) (model_fbanks_cnn.py:41), periodic Hann(640)
 //                          (librosa stft), periodic Tukey(640, 0.25) (scipy spectrogram)
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <mutex>
@@ -18,6 +19,8 @@
 namespace srk {
 
 int g_opt_gru_persistent = 1;
+static std::atomic<int> g_opt_matmul_prec{kPrecF32};
+int matmul_prec() { return g_opt_matmul_prec.load(std::memory_order_relaxed); }
 unsigned long long* g_opt_gru_trace = nullptr;
 
 static thread_local std::string g_last_error;
@@ -270,6 +273,11 @@ int srk_set_option(const char* name, int64_t value) {
   const std::string n(name);
   if (n == "gru_persistent") {
     srk::g_opt_gru_persistent = value != 0;
+    return SRK_OK;
+  }
+  if (n == "matmul_precision") {   // 0 fp32, 1 bf16, 2 fp16 matrix-core operands (fp32 accumulate)
+    SRK_REQUIRE(value >= 0 && value <= 2, SRK_ERR_INVALID, "matmul_precision must be 0, 1 or 2");
+    srk::g_opt_matmul_prec.store((int)value);
     return SRK_OK;
   }
   if (n == "gru_trace_ptr") {   // diagnostics: device buffer of 8 x u64 per (workgroup, step), 0 = off

@@ -69,6 +69,12 @@ struct DeviceTables {
 // Returns the tables for the current HIP device, building them on first use.
 int get_tables(const DeviceTables** out);
 
+// Matrix-core operand precision of the GEMM-shaped kernels (srk_set_option "matmul_precision"):
+// 0 = fp32 (exact fp32 MFMA, the reference's arithmetic), 1 = bf16, 2 = fp16 operands (rounded to
+// nearest-even when staged into LDS) with fp32 accumulation and fp32 inputs / outputs.
+enum MatmulPrec { kPrecF32 = 0, kPrecBF16 = 1, kPrecF16 = 2 };
+int matmul_prec();
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // RAII event pair around one kernel launch (prof.hip); inert unless srk_prof_enable(1).

@@ -20,7 +20,7 @@
 
 #include <stdint.h>
 
-#define SRK_ABI_VERSION 1
+#define SRK_ABI_VERSION 2
 
 #ifdef __cplusplus
 extern "C" {
@@ -134,8 +134,9 @@ int srk_augment(const int16_t* pcm, int64_t n_clips, const int16_t* bank, int64_
 int srk_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
                  int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc,
                  const float* bias, int bias_mode, void* stream);
-/* The same GEMM (alpha, beta, no bias) that also writes rowsum[m] = sum_k op(A)[m, k]: the weight
- * and bias gradients of a Linear in one pass (dW = dY^T X, db = sum over the batch of dY).   */
+/* The same GEMM (alpha, beta, no bias) that also writes rowsum[m] = beta * rowsum[m] +
+ * sum_k op(A)[m, k]: the weight and bias gradients of a Linear in one pass (dW = dY^T X,
+ * db = sum over the batch of dY); beta = 1 accumulates both into existing .grad buffers.     */
 int srk_gemm_rowsum_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
                         int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc,
                         float* rowsum, void* stream);
@@ -150,15 +151,17 @@ int srk_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out
  * w_hh [2][3H][H], b_ih [2][3H], b_hh [2][3H].  H must be a multiple of 128.
  * ws (fwd, kept until the backward): srk_gru_workspace_floats(.., backward=0) floats;
  * ws (bwd scratch): srk_gru_workspace_floats(.., backward=1) floats.
- * Backward OVERWRITES dw_ih, dw_hh, db_ih, db_hh (same stacked layouts) and dx [B, T, in]
- * (dx may be NULL when the input needs no gradient).                                        */
+ * Backward writes dx [B, T, in] (NULL when the input needs no gradient) and OVERWRITES
+ * (accumulate = 0) or ADDS TO (accumulate = 1: autograd's .grad accumulation, done in the GEMM
+ * epilogues) dw_ih, dw_hh, db_ih, db_hh (same stacked layouts).                             */
 int64_t srk_gru_workspace_floats(int64_t B, int64_t T, int64_t in, int64_t H, int backward);
 int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t H, const float* w_ih,
                       const float* w_hh, const float* b_ih, const float* b_hh, float* y, float* ws,
                       void* stream);
 int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t H, const float* w_ih,
                       const float* w_hh, const float* y, const float* ws_fwd, const float* dy, float* dx,
-                      float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, float* ws, void* stream);
+                      float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, int accumulate, float* ws,
+                      void* stream);
 
 /* ---------------------------------------------------------------- K6: convolution / pooling
  * nn.Conv2d / nn.Conv1d (zero padding ph/pw, stride sh/sw, no dilation/groups) as implicit GEMM

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime before libsrk.so)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SRK_LIB") or os.path.join(_HERE, "libsrk.so")   # SRK_LIB: experiment builds
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "srk.h")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -43,7 +43,7 @@ _SIGS = {
     "srk_colsum_f32": [_P, _I64, _I64, _I64, _P, _F, _P],
     "srk_gru_workspace_floats": [_I64, _I64, _I64, _I64, _I],
     "srk_gru_layer_fwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P],
-    "srk_gru_layer_bwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "srk_gru_layer_bwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     "srk_conv2d_workspace_floats": [_I64, _I64, _I64, _I64],
     "srk_conv2d_nhwc_fwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P,
                             _P],

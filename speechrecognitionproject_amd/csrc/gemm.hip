@@ -769,7 +769,7 @@ extern "C" int srk_gemm_rowsum_f32(int trans_a, int trans_b, int64_t M, int64_t 
   d.A = A; d.lda = lda; d.ta = trans_a != 0;
   d.B = B; d.ldb = ldb; d.tb = trans_b != 0;
   d.C = C; d.ldc = ldc; d.alpha = alpha; d.beta = beta;
-  d.rowsum = rowsum;
+  d.rowsum = rowsum; d.rowsum_beta = beta;
   return srk::gemm_f32(d, srk::as_stream(stream));
   SRK_API_END
 }

@@ -360,7 +360,8 @@ int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
 
 int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t H, const float* w_ih,
                       const float* w_hh, const float* y, const float* ws_fwd, const float* dy, float* dx,
-                      float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, float* ws, void* stream) {
+                      float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, int accumulate, float* ws,
+                      void* stream) {
   SRK_API_BEGIN
   if (int rc = srk::check_dims(B, T, in, H)) return rc;
   SRK_REQUIRE(x && w_ih && w_hh && y && ws_fwd && dy && dw_ih && dw_hh && db_ih && db_hh && ws, SRK_ERR_INVALID,
@@ -394,13 +395,14 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
   }
 
   int rc;
+  const float beta = accumulate ? 1.f : 0.f;   // autograd .grad accumulation in the GEMM epilogues
   {  // dW_ih_cat[6H, in] = dgi^T [6H, BT] * x [BT, in]; db_ih fused as the row sums of dgi^T
     GemmDesc g;
     g.M = 6 * H; g.N = in; g.K = BT;
     g.A = dgi; g.lda = 6 * H; g.ta = true;
     g.B = x; g.ldb = in;
-    g.C = dw_ih; g.ldc = in;
-    g.rowsum = db_ih;
+    g.C = dw_ih; g.ldc = in; g.beta = beta;
+    g.rowsum = db_ih; g.rowsum_beta = beta;
     if ((rc = srk::gemm_f32(g, s))) return rc;
   }
   for (int dir = 0; dir < 2; ++dir) {
@@ -414,11 +416,11 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
     g.ta = true; g.lda = 3 * H; g.ldb = 2 * H;
     g.A = dir == 0 ? dg + 3 * H : dg;
     g.B = dir == 0 ? y + dir * H : y + 2 * H + dir * H;
-    g.C = dw_hh + (size_t)dir * 3 * H * H; g.ldc = H;
-    g.rowsum = dbh;
+    g.C = dw_hh + (size_t)dir * 3 * H * H; g.ldc = H; g.beta = beta;
+    g.rowsum = dbh; g.rowsum_beta = beta;
     if (g.K > 0) {
       if ((rc = srk::gemm_f32(g, s))) return rc;
-    } else {
+    } else if (!accumulate) {
       SRK_CHECK_HIP(hipMemsetAsync(g.C, 0, sizeof(float) * 3 * H * H, s));
       SRK_CHECK_HIP(hipMemsetAsync(dbh, 0, sizeof(float) * 3 * H, s));
     }

@@ -20,14 +20,41 @@ def _check_cuda(*ts):
 
 
 # ----------------------------------------------------------------------------- GRU
+def _adjacent(a, b):
+    """b starts right where a ends in one storage (FlatParams lays BiGRU twins out this way)."""
+    return (a.is_contiguous() and b.is_contiguous() and a.dtype == b.dtype and a.shape == b.shape
+            and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
+            and b.data_ptr() == a.data_ptr() + a.numel() * a.element_size())
+
+
+def _dir_pair(a, b):
+    """The [2, ...] stacked tensor of a direction pair: a view when adjacent, else a copy."""
+    if _adjacent(a, b):
+        return a.as_strided((2,) + tuple(a.shape), (a.numel(),) + tuple(a.stride()))
+    return torch.stack([a, b])
+
+
+def _grad_pair(a, b):
+    """The stacked .grad of a direction pair to ACCUMULATE into in place (autograd's own
+    accumulation, fused into the kernels' epilogues), or None when the grads are not adjacent
+    buffers (then the gradient is returned to autograd as usual)."""
+    ga, gb = a.grad, b.grad
+    if ga is None or gb is None or not _adjacent(ga, gb):
+        return None
+    return _dir_pair(ga, gb)
+
+
 class _GRULayerFn(torch.autograd.Function):
-    """One bidirectional GRU layer (srk_gru_layer_fwd / srk_gru_layer_bwd)."""
+    """One bidirectional GRU layer (srk_gru_layer_fwd / srk_gru_layer_bwd) over the direction
+    pairs (weight_ih_lN, weight_ih_lN_reverse), ... of the parameters themselves."""
 
     @staticmethod
-    def forward(ctx, x, w_ih, w_hh, b_ih, b_hh):
+    def forward(ctx, x, w_ih_f, w_ih_r, w_hh_f, w_hh_r, b_ih_f, b_ih_r, b_hh_f, b_hh_r):
         B, T, IN = x.shape
-        H = w_hh.shape[-1]
+        H = w_hh_f.shape[-1]
         x = x.contiguous()
+        w_ih, w_hh = _dir_pair(w_ih_f, w_ih_r), _dir_pair(w_hh_f, w_hh_r)
+        b_ih, b_hh = _dir_pair(b_ih_f, b_ih_r), _dir_pair(b_hh_f, b_hh_r)
         _check_cuda(x, w_ih, w_hh, b_ih, b_hh)
         y = torch.empty((B, T, 2 * H), device=x.device, dtype=torch.float32)
         ws = torch.empty(int(_lib.lib().srk_gru_workspace_floats(B, T, IN, H, 0)), device=x.device)
@@ -35,22 +62,31 @@ class _GRULayerFn(torch.autograd.Function):
              stream_ptr())
         ctx.save_for_backward(x, w_ih, w_hh, y, ws)
         ctx.dims = (B, T, IN, H)
+        ctx.params = (w_ih_f, w_ih_r, w_hh_f, w_hh_r, b_ih_f, b_ih_r, b_hh_f, b_hh_r)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w_ih, w_hh, y, ws = ctx.saved_tensors
         B, T, IN, H = ctx.dims
+        P = ctx.params
         dy = dy.contiguous()
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
-        dw_ih, dw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
-        db_ih = torch.empty((2, 3 * H), device=x.device)
-        db_hh = torch.empty((2, 3 * H), device=x.device)
+        targets = [_grad_pair(P[2 * i], P[2 * i + 1]) for i in range(4)]
+        acc = all(t is not None for t in targets) and all(ctx.needs_input_grad[1:])
+        if acc:   # accumulate straight into the parameters' .grad (FlatParams)
+            dw_ih, dw_hh, db_ih, db_hh = targets
+        else:
+            dw_ih, dw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
+            db_ih = torch.empty((2, 3 * H), device=x.device)
+            db_hh = torch.empty((2, 3 * H), device=x.device)
         ws2 = torch.empty(int(_lib.lib().srk_gru_workspace_floats(B, T, IN, H, 1)), device=x.device)
         call("srk_gru_layer_bwd", ptr(x), B, T, IN, H, ptr(w_ih), ptr(w_hh), ptr(y), ptr(ws), ptr(dy),
-             ptr(dx) if dx is not None else None, ptr(dw_ih), ptr(dw_hh), ptr(db_ih), ptr(db_hh), ptr(ws2),
+             ptr(dx) if dx is not None else None, ptr(dw_ih), ptr(dw_hh), ptr(db_ih), ptr(db_hh), int(acc), ptr(ws2),
              stream_ptr())
-        return dx, dw_ih, dw_hh, db_ih, db_hh
+        if acc:
+            return (dx,) + (None,) * 8
+        return (dx, dw_ih[0], dw_ih[1], dw_hh[0], dw_hh[1], db_ih[0], db_ih[1], db_hh[0], db_hh[1])
 
 
 class BiGRU(tnn.Module):
@@ -72,17 +108,19 @@ class BiGRU(tnn.Module):
                                     ("bias_ih", (3 * H,)), ("bias_hh", (3 * H,))):
                     p = tnn.Parameter(torch.empty(shape).uniform_(-k, k))
                     setattr(self, "%s_l%d%s" % (name, layer, sfx), p)
+            for name in ("weight_ih", "weight_hh", "bias_ih", "bias_hh"):   # FlatParams layout hint
+                getattr(self, "%s_l%d" % (name, layer))._srk_pair = getattr(self, "%s_l%d_reverse" % (name, layer))
 
-    def _stacked(self, name, layer):
-        return torch.stack([getattr(self, "%s_l%d" % (name, layer)), getattr(self, "%s_l%d_reverse" % (name, layer))])
+    def _pairs(self, layer):
+        return [getattr(self, "%s_l%d%s" % (name, layer, sfx))
+                for name in ("weight_ih", "weight_hh", "bias_ih", "bias_hh") for sfx in ("", "_reverse")]
 
     def forward(self, x):
         require_gpu()
         h = x
         finals = []
         for layer in range(self.num_layers):
-            h = _GRULayerFn.apply(h, self._stacked("weight_ih", layer), self._stacked("weight_hh", layer),
-                                  self._stacked("bias_ih", layer), self._stacked("bias_hh", layer))
+            h = _GRULayerFn.apply(h, *self._pairs(layer))
             H = self.hidden_size
             finals += [h[:, -1, :H], h[:, 0, H:]]
         return h, torch.stack(finals)
@@ -96,6 +134,7 @@ class _LinearFn(torch.autograd.Function):
         if x.dim() != 2 or x.stride(1) != 1:
             x = x.contiguous()
         _check_cuda(x, w, b)
+        w_param = w
         w = w.contiguous()
         M, K = x.shape
         N = w.shape[0]
@@ -104,6 +143,7 @@ class _LinearFn(torch.autograd.Function):
              ptr(b) if b is not None else None, 1 if b is not None else 0, stream_ptr())
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
+        ctx.params = (w_param, b)
         return y
 
     @staticmethod
@@ -118,17 +158,29 @@ class _LinearFn(torch.autograd.Function):
             dx = torch.empty((M, K), device=x.device)
             call("srk_gemm_f32", 0, 0, M, K, N, 1.0, ptr(dy), N, ptr(w), K, 0.0, ptr(dx), K, None, 0, s)
         want_db = ctx.has_bias and ctx.needs_input_grad[2]
+        # accumulate straight into the parameters' existing .grad buffers (beta = 1, fused into the
+        # GEMM epilogue) instead of returning a fresh gradient for autograd to add
+        wp, bp = ctx.params
+        gw = wp.grad if wp.grad is not None and wp.grad.is_contiguous() else None
+        gb = bp.grad if bp is not None and bp.grad is not None and bp.grad.is_contiguous() else None
+        acc = gw is not None and (not want_db or gb is not None)
         if ctx.needs_input_grad[1]:
-            dw = torch.empty((N, K), device=x.device)
+            dw = gw if acc else torch.empty((N, K), device=x.device)
+            beta = 1.0 if acc else 0.0
             if want_db:   # dW = dy^T x with db = row sums of dy^T fused into the same kernel
-                db = torch.empty((N,), device=x.device)
-                call("srk_gemm_rowsum_f32", 1, 0, N, K, M, 1.0, ptr(dy), N, ptr(x), x.stride(0), 0.0, ptr(dw), K,
+                db = gb if acc else torch.empty((N,), device=x.device)
+                call("srk_gemm_rowsum_f32", 1, 0, N, K, M, 1.0, ptr(dy), N, ptr(x), x.stride(0), beta, ptr(dw), K,
                      ptr(db), s)
             else:
-                call("srk_gemm_f32", 1, 0, N, K, M, 1.0, ptr(dy), N, ptr(x), x.stride(0), 0.0, ptr(dw), K, None, 0, s)
+                call("srk_gemm_f32", 1, 0, N, K, M, 1.0, ptr(dy), N, ptr(x), x.stride(0), beta, ptr(dw), K, None, 0,
+                     s)
+        else:
+            acc = False
         if want_db and db is None:
             db = torch.empty((N,), device=x.device)
             call("srk_colsum_f32", ptr(dy), M, N, N, ptr(db), 0.0, s)
+        if acc:
+            return dx, None, None
         return dx, dw, db
 
 

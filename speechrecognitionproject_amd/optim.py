@@ -16,7 +16,22 @@ _ALIGN = 64   # floats
 class FlatParams:
     def __init__(self, params, device=None):
         require_gpu()
-        self.params = [p for p in params if p.requires_grad]
+        # a parameter may name a partner to be laid out right behind it (``_srk_pair``: the
+        # reverse-direction twin of a BiGRU weight), so the kernels see the stacked pair as ONE
+        # [2, ...] tensor in place — no per-step torch.stack / unbind copies
+        ps = [p for p in params if p.requires_grad]
+        ids = {id(p) for p in ps}
+        order, seen = [], set()
+        for p in ps:
+            if id(p) in seen:
+                continue
+            order.append(p)
+            seen.add(id(p))
+            q = getattr(p, "_srk_pair", None)
+            if q is not None and id(q) in ids and id(q) not in seen:
+                order.append(q)
+                seen.add(id(q))
+        self.params = order
         device = device or self.params[0].device
         offs, n = [], 0
         for p in self.params:

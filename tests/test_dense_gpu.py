@@ -166,3 +166,41 @@ def test_bigru_persistent_matches_per_step_and_torch(gpu, B, T):
         gr = ref.weight_hh_l0.grad
         gm = dict(mine.named_parameters())["weight_hh_l0"].grad.cpu()
         assert (gm - gr).abs().max() / gr.abs().max() <= 1e-4
+
+
+def test_flat_grads_accumulate_in_place(gpu):
+    """FlatParams lays each BiGRU direction pair out back to back, so the layer sees the stacked
+    weights as one tensor and the backward ADDS into the .grad views (beta = 1 epilogues) instead
+    of handing autograd fresh gradients: two backward passes must give exactly twice one pass,
+    and the result must equal the returned-gradient path of a module without FlatParams."""
+    torch.manual_seed(7)
+    B, T, IN, H = 40, 5, 39, 512
+    ref = _ref_gru(IN, H, 2)
+    plain = snn.BiGRU(IN, H, num_layers=2).cuda()
+    plain.load_state_dict(ref.state_dict())
+    fc_plain = snn.Linear(2 * H, 12).cuda()
+    flat_net = torch.nn.ModuleDict({"gru": snn.BiGRU(IN, H, num_layers=2), "fc": snn.Linear(2 * H, 12)}).cuda()
+    flat_net["gru"].load_state_dict(ref.state_dict())
+    flat_net["fc"].load_state_dict(fc_plain.state_dict())
+    flat = FlatParams(flat_net.parameters())
+    g = flat_net["gru"]
+    assert g.weight_ih_l0_reverse.data_ptr() == g.weight_ih_l0.data_ptr() + g.weight_ih_l0.numel() * 4
+    x = torch.randn(B, T, IN, device="cuda")
+    lab = torch.randint(0, 12, (B,), device="cuda")
+
+    def loss_of(gru, fc):
+        y, _ = gru(x)
+        return snn.CrossEntropyLoss()(fc(y[:, -1, :]), lab)
+
+    loss_of(plain, fc_plain).backward()
+    flat.zero_grad()
+    loss_of(flat_net["gru"], flat_net["fc"]).backward()
+    one = flat.grad.clone()
+    loss_of(flat_net["gru"], flat_net["fc"]).backward()
+    assert torch.allclose(flat.grad, 2 * one, rtol=1e-5, atol=1e-9)
+    named = dict(flat_net["gru"].named_parameters())
+    for n, p in plain.named_parameters():
+        d = (named[n].grad - 2 * p.grad).abs().max().item()
+        assert d <= 1e-5 * (1 + p.grad.abs().max().item()), n
+    assert (flat_net["fc"].weight.grad - 2 * fc_plain.weight.grad).abs().max().item() <= 1e-6
+    assert (flat_net["fc"].bias.grad - 2 * fc_plain.bias.grad).abs().max().item() <= 1e-6

@@ -1,7 +1,10 @@
 """GEMM micro-benchmark: the fp32 GEMM shapes of one model_mfcc_bgru train step (B = 256, T = 51,
 H = 512), timed with srk_prof events and checked against torch fp32 matmul on the same device.
 
-    python tools/gemm_bench.py [--reps 10]      (env SRK_GEMM_REMAP=0 disables the XCD remap)
+    python tools/gemm_bench.py [--reps 10] [--precision fp32|bf16|fp16]
+                                                 (env SRK_GEMM_REMAP=0 disables the XCD remap)
+With --precision bf16 / fp16 the yardstick is torch.matmul on operands already converted to that
+dtype (hipBLASLt reading 16-bit operands; ours reads the fp32 tensors and rounds on chip).
 """
 import argparse
 import ctypes
@@ -30,7 +33,12 @@ SHAPES = [
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp16"])
     a = ap.parse_args()
+    _lib.set_matmul_precision(a.precision)
+    pname = {"fp32": "gemm_f32", "bf16": "gemm_bf16", "fp16": "gemm_f16"}[a.precision]
+    peak = 157.3 if a.precision == "fp32" else 2500.0
+    tdt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[a.precision]
     torch.backends.cuda.matmul.allow_tf32 = False
     dev = torch.device("cuda")
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -50,15 +58,16 @@ def main():
         _lib.prof_enable(True)
         for _ in range(a.reps):
             fn()
-        c, ms, w = _lib.prof_read("gemm_f32")
+        c, ms, w = _lib.prof_read(pname)
         _lib.prof_enable(False)
         Am = (A.view(K, lda)[:, :M].t() if ta else A.view(M, lda)[:, :K])
         Bmm = (Bm.view(N, ldb)[:, :K].t() if tb else Bm.view(K, ldb)[:, :N])
-        ref = Am @ Bmm
+        ref = Am.to(tdt).float() @ Bmm.to(tdt).float()
         err = float((C.view(M, N) - ref).abs().max() / ref.abs().max())
         tf = w / (ms * 1e-3) / 1e12
         # yardstick: torch.matmul (hipBLASLt / rocBLAS fp32) on the same operands
-        out = torch.empty_like(ref)
+        Am, Bmm = Am.to(tdt), Bmm.to(tdt)
+        out = torch.empty(ref.shape, device=dev, dtype=tdt)
         for _ in range(2):
             torch.matmul(Am, Bmm, out=out)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -68,7 +77,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         t_us = e0.elapsed_time(e1) / a.reps * 1e3
-        res[name] = {"us": round(ms / c * 1e3, 1), "TF": round(tf, 1), "frac": round(tf / 157.3, 3), "rel_err": err,
+        res[name] = {"us": round(ms / c * 1e3, 1), "TF": round(tf, 1), "frac": round(tf / peak, 3), "rel_err": err,
                      "torch_us": round(t_us, 1), "torch_TF": round(2.0 * M * N * K / (t_us * 1e-6) / 1e12, 1)}
         print(name, json.dumps(res[name]), flush=True)
     print(json.dumps({"remap": os.environ.get("SRK_GEMM_REMAP", "1"), "shapes": res}))

@@ -24,9 +24,15 @@ on the device from raw 1-s 16 kHz PCM (K1), then model_mfcc_bgru's 2-layer BiGRU
 cross-entropy, backward and Adam — the full training.py:85-91 step.  Clips are pre-staged in HBM
 (the timed region starts with inputs resident).  "value" = clips processed by all ranks / time.
 
+--precision fp32 (default: exact fp32 MFMA, the reference's arithmetic) | bf16 | fp16 selects the
+matrix-core operand precision (srk_set_option "matmul_precision"; fp16 adds a static loss scale).
+With fp32, the same line also carries "bf16": the identical step re-timed with bf16 operands
+(BASELINE.json names bf16 for cfg2), with its own roofline against the dense bf16 peak.
+
 Measurement extras on the same line:
   roofline     — the dominant kernel of the timed steps, timed live with HIP events on its launch
-                 stream (srk_prof_*), algorithmic flops / avg launch time vs the fp32 MFMA peak;
+                 stream (srk_prof_*), algorithmic flops / avg launch time vs the MFMA peak of its
+                 operand type (fp32 157.3 TF, bf16/fp16 2.5 PF dense);
   mfcc_roofline— K1 alone on 65,536 clips (HBM-bound): algorithmic bytes / time vs 8 TB/s;
   cpu_baseline — the CPU restatement (oracle/: numpy MFCC per clip + torch-CPU GRU step) timed on
                  this host's cores on a bounded sample (rank 0, N = 1 only).
@@ -168,6 +174,8 @@ def main():
     ap.add_argument("--precision", default="fp32", choices=sorted(_lib.PRECISIONS),
                     help="matrix-core operand precision (fp32 = the reference's arithmetic; bf16 / fp16 "
                          "operands with fp32 accumulation)")
+    ap.add_argument("--no-lowprec", dest="lowprec", action="store_false",
+                    help="skip the extra bf16 measurement reported under \"bf16\" on the same line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true")
     ap.add_argument("--no-feature-roofline", "--no-mfcc-roofline", dest="no_feature_roofline", action="store_true")
@@ -176,14 +184,12 @@ def main():
     rank, world, local = parallel.init_from_env()
     features.require_gpu()
     _lib.lib()
-    _lib.set_matmul_precision(args.precision)
-    loss_scale = FP16_LOSS_SCALE if args.precision == "fp16" else 1.0
+    loss_scale = 1.0
     dev = torch.device("cuda", local)
     torch.manual_seed(0)
     model = build_model(args.model).to(dev)
     flat = FlatParams(model.parameters())
     opt = Adam(model.parameters(), lr=1e-4, flat=flat)
-    opt.grad_scale = 1.0 / (world * loss_scale)
     parallel.broadcast_flat(flat)
     crit = CrossEntropyLoss()
 
@@ -218,52 +224,71 @@ def main():
         opt.step()
         return loss
 
-    for i in range(args.warmup):
-        loss = step(i)
-    torch.cuda.synchronize()
-    if not torch.isfinite(loss).item():
-        raise SystemExit("non-finite loss during warm-up")
-    if world > 1:
-        torch.distributed.barrier()
-    if not args.no_prof:
-        _lib.prof_enable(True)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        el = float(t.item())
-    final_loss = float(loss.item())
+    def timed(precision):
+        """W warm-up + K timed steps at one matrix precision -> (seconds, kernel records, loss)."""
+        nonlocal loss_scale
+        _lib.set_matmul_precision(precision)
+        loss_scale = FP16_LOSS_SCALE if precision == "fp16" else 1.0
+        opt.grad_scale = 1.0 / (world * loss_scale)
+        for i in range(args.warmup):
+            loss = step(i)
+        torch.cuda.synchronize()
+        if not torch.isfinite(loss).item():
+            raise SystemExit("non-finite loss during warm-up")
+        if world > 1:
+            torch.distributed.barrier()
+        if not args.no_prof:
+            _lib.prof_enable(True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            loss = step(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        kernels = {}
+        if not args.no_prof:
+            for name in MATRIX_KERNELS + OTHER_KERNELS:
+                c, ms, w = _lib.prof_read(name)
+                if c:
+                    kernels[name] = {"launches": c, "ms_total": round(ms, 3), "work": w}
+            _lib.prof_enable(False)
+        return el, kernels, float(loss.item())
 
-    kernels = {}
-    if not args.no_prof:
-        for name in MATRIX_KERNELS + OTHER_KERNELS:
-            c, ms, w = _lib.prof_read(name)
-            if c:
-                kernels[name] = {"launches": c, "ms_total": round(ms, 3), "work": w}
-        _lib.prof_enable(False)
-
-    if rank != 0:
-        return
-    value = world * B * args.steps / el
-    roof = None
-    mm = {k: v for k, v in kernels.items() if k in MATRIX_KERNELS}
-    if mm:
+    def roofline(kernels, traffic_ok):
+        mm = {k: v for k, v in kernels.items() if k in MATRIX_KERNELS}
+        if not mm:
+            return None
         dom = max(mm, key=lambda k: mm[k]["ms_total"])
         k = mm[dom]
         tf = k["work"] / (k["ms_total"] * 1e-3) / 1e12
         peak = PEAK_LP_MFMA_TFLOPS if dom in LP_KERNELS else PEAK_FP32_MFMA_TFLOPS
-        roof = {"bound": "mfma", "kernel": dom, "achieved": round(tf, 2), "peak": peak,
+        return {"bound": "mfma", "kernel": dom, "achieved": round(tf, 2), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(tf / peak, 4),
-                "traffic": pmc_traffic(dom) if args.model == "mfcc_bgru" and args.precision == "fp32" else None, "traffic_unit": "bytes/launch",
+                "traffic": pmc_traffic(dom) if traffic_ok else None, "traffic_unit": "bytes/launch",
                 "avg_launch_ms": round(k["ms_total"] / k["launches"], 5),
                 "flops_per_launch": k["work"] / k["launches"]}
+
+    el, kernels, final_loss = timed(args.precision)
+    # the same step with 16-bit matrix-core operands (BASELINE.json cfg2 names bf16), same line
+    lp = None
+    if args.lowprec and args.precision == "fp32":
+        lp_el, lp_kernels, lp_loss = timed("bf16")
+        lp = {"dtype": "bf16", "value": round(world * B * args.steps / lp_el, 2),
+              "ms_per_step": round(lp_el / args.steps * 1e3, 3), "final_loss": round(lp_loss, 5),
+              "roofline": roofline(lp_kernels, False),
+              "kernels": {k: {"launches": v["launches"], "ms_total": v["ms_total"]} for k, v in lp_kernels.items()}}
+        _lib.set_matmul_precision(args.precision)
+
+    if rank != 0:
+        return
+    value = world * B * args.steps / el
+    roof = roofline(kernels, args.model == "mfcc_bgru" and args.precision == "fp32")
     res = {
         "metric": "utterances/sec (1 s @16 kHz) MFCC+CNN-BiGRU train step",
         "value": round(value, 2), "unit": "utt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -277,6 +302,8 @@ def main():
         "roofline": roof,
         "kernels": {k: {"launches": v["launches"], "ms_total": v["ms_total"]} for k, v in kernels.items()},
     }
+    if lp is not None:
+        res["bf16"] = lp
     if not args.no_feature_roofline and args.model in FEATURE:
         res["feature_roofline"] = feature_roofline(args.model)
     if world == 1 and not args.no_cpu_baseline:

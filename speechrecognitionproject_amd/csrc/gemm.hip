@@ -334,17 +334,43 @@ struct LpOps<true> {
 typedef float v8f __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kLpBM = 128, kLpBN = 128, kLpBK = 64;
+constexpr int kLpBK = 64;
 constexpr int kLpPitchQ = kLpBK / 8 + 1;            // image row pitch in 16-B quads (72 elements)
-constexpr int kLpImgQ = 128 * kLpPitchQ;            // quads per 128-row image
 
-template <bool TA, bool TB, bool VEC, bool F16>
-__global__ __launch_bounds__(256, 2) void gemm_lp_kernel(KernelArgs ka) {
+// Staging of one operand tile (ROWS x 64 k, fp32 in HBM) by NT threads.  Unit = KW consecutive k
+// (KW = 8 -> one 16-B pack, KW = 4 -> one 8-B half pack) of 1 row (k-contiguous operand, 2 or 1
+// float4 loads) or of 4 rows (row-contiguous operand: KW float4 loads transposed in registers into
+// 4 packs).  Consecutive lanes walk k (LDS stores of 8 / 16 lanes fill one 128-B row chunk).
+template <bool KC, int ROWS, int NT>
+struct LpStage {
+  static constexpr int UNITS8 = KC ? ROWS * (kLpBK / 8) : (ROWS / 4) * (kLpBK / 8);
+  static constexpr int KW = UNITS8 >= NT ? 8 : 4;
+  static constexpr int KCH = kLpBK / KW;                      // k chunks per row
+  static constexpr int UNITS = KC ? ROWS * KCH : (ROWS / 4) * KCH;
+  static constexpr int U = UNITS / NT;                        // units per thread
+  static constexpr int V = KC ? U * KW / 4 : U * KW;          // float4 registers per thread
+  static constexpr int RS = KC ? U : 4 * U;                   // rows per thread (fused row sums)
+  static_assert(UNITS % NT == 0 && U >= 1, "staging must divide evenly");
+};
+
+template <int BM, int BN>
+constexpr int lp_per_cu() { return 2 * (BM + BN) * kLpPitchQ * 16 <= 80 * 1024 ? 2 : 1; }
+
+template <bool TA, bool TB, int BM, int BN, int NW, bool VEC, bool F16, int PF>
+__global__ __launch_bounds__(NW * 64, (lp_per_cu<BM, BN>())) void gemm_lp_kernel(KernelArgs ka) {
   using Ops = LpOps<F16>;
   using e8 = typename Ops::e8;
-  constexpr int BM = kLpBM, BN = kLpBN, BK = kLpBK, TM = 2, TN = 2;
+  typedef typename LpOps<F16>::e8 e8_t;
+  typedef __attribute__((ext_vector_type(4))) typename std::conditional<F16, _Float16, __bf16>::type e4;
+  constexpr int NT = NW * 64, BK = kLpBK;
+  constexpr int WM = (NW == 4) ? 2 : (BM >= 256 ? 4 : 2), WN = NW / WM;
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  static_assert(TM >= 1 && TN >= 1, "bad wave grid");
   constexpr bool AKC = !TA, BKC = TB;
-  __shared__ __attribute__((aligned(16))) u32x4 smem[2 * 2 * kLpImgQ];   // [stage][A | B] images
+  using SA = LpStage<AKC, BM, NT>;
+  using SB = LpStage<BKC, BN, NT>;
+  constexpr int IMGA = BM * kLpPitchQ, IMGB = BN * kLpPitchQ;   // quads
+  __shared__ __attribute__((aligned(16))) u32x4 smem[2 * (IMGA + IMGB)];   // [stage][A | B] images
   const GemmDesc& d = ka.d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int split, tm, tn;
@@ -355,89 +381,160 @@ __global__ __launch_bounds__(256, 2) void gemm_lp_kernel(KernelArgs ka) {
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t kb0 = split * ka.kchunk;
   const int64_t ke = (kb0 + ka.kchunk < d.K) ? kb0 + ka.kchunk : d.K;
-  const int wm0 = (wave >> 1) * (BM / 2), wn0 = (wave & 1) * (BN / 2);
+  const int wm0 = (wave / WN) * (BM / WM), wn0 = (wave % WN) * (BN / WN);
   const bool do_rs = d.rowsum != nullptr && tn == 0;
-  const int kq = tid & 7;          // the thread's 8-deep k chunk of a tile (both unit kinds)
 
-  // staging registers: 8 float4 per operand (KC: 4 units x 2;  !KC: one 8 k x 4 row unit)
-  v4f ra[8], rb[8];
-  // Loads are CLAMPED (rows >= rows -> last row group, k >= ke -> last k) and never predicated; the
-  // k tail is zeroed at LDS-store time in BOTH images (a clamped duplicate may overflow fp16).
-  auto load_op = [&](v4f (&r)[8], const float* __restrict__ P, int64_t ld, bool kc, int64_t rows, int64_t r0,
-                     int64_t k0) {
-    if (kc) {
+  v4f ra[PF][SA::V], rb[PF][SB::V];
+  // Loads are CLAMPED (rows >= rows -> last row / row group, k >= ke -> last k) and never
+  // predicated; the k tail is zeroed at LDS-store time in BOTH images (a clamped duplicate may
+  // overflow fp16).
+  // Full k-tiles of VEC shapes load through buffer instructions: a per-thread 32-bit VGPR byte
+  // offset fixed for the whole k loop (rows clamped once) + the k-tile's uniform byte offset in an
+  // SGPR, so no per-load address arithmetic lands on the VALU (which the on-chip bf16 conversion
+  // already keeps busy).  The host guarantees both operands' byte extents are < 2^31 for VEC.
+  auto rsrc_of = [](const float* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rsA = rsrc_of(A), rsB = rsrc_of(B);
+  unsigned voA[SA::U], voB[SB::U];
+  auto init_voff = [&](auto S_, unsigned* vo, int64_t ld, int64_t rows, int64_t r0) {
+    using S = decltype(S_);
+    constexpr bool KC = std::is_same<S, SA>::value ? AKC : BKC;
+    const int kc = tid % S::KCH;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t row = r0 + (tid >> 3) + 32 * u;
+    for (int u = 0; u < S::U; ++u) {
+      const int un = tid / S::KCH + u * (NT / S::KCH);
+      if (KC) {
+        const int64_t row = r0 + un < rows ? r0 + un : rows - 1;
+        vo[u] = (unsigned)((row * ld + kc * S::KW) * 4);
+      } else {
+        const int64_t col = r0 + un * 4 < rows ? r0 + un * 4 : rows - 4;
+        vo[u] = (unsigned)((kc * S::KW * ld + col) * 4);
+      }
+    }
+  };
+  if (VEC) {
+    init_voff(SA{}, voA, d.lda, d.M, m0);
+    init_voff(SB{}, voB, d.ldb, d.N, n0);
+  }
+  auto load_fast = [&](auto S_, v4f* r, __amdgpu_buffer_rsrc_t rs, const unsigned* vo, int64_t ld, int64_t k0) {
+    using S = decltype(S_);
+    constexpr bool KC = std::is_same<S, SA>::value ? AKC : BKC;
+    constexpr int KW = S::KW;
+#pragma unroll
+    for (int u = 0; u < S::U; ++u) {
+      if (KC) {
+#pragma unroll
+        for (int h = 0; h < KW / 4; ++h)
+          r[u * (KW / 4) + h] = __builtin_bit_cast(
+              v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo[u] + 16 * h), (int)(k0 * 4), 0));
+      } else {
+#pragma unroll
+        for (int e = 0; e < KW; ++e)
+          r[u * KW + e] = __builtin_bit_cast(
+              v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo[u], (int)((k0 + e) * ld * 4), 0));
+      }
+    }
+  };
+  // Generic (tail tiles, unaligned shapes): CLAMPED addresses (rows >= rows -> last row / row group,
+  // k >= ke -> last k), never predicated; the k tail is zeroed at LDS-store time in BOTH images (a
+  // clamped duplicate may overflow fp16).
+  auto load_op = [&](auto S_, v4f* r, const float* __restrict__ P, int64_t ld, int64_t rows, int64_t r0, int64_t k0) {
+    using S = decltype(S_);
+    constexpr bool KC = std::is_same<S, SA>::value ? AKC : BKC;
+    constexpr int KW = S::KW, KCH = S::KCH;
+    const int kc = tid % KCH;
+#pragma unroll
+    for (int u = 0; u < S::U; ++u) {
+      const int un = tid / KCH + u * (NT / KCH);   // row (KC) or row group (!KC) of unit u
+      if (KC) {
+        const int64_t row = r0 + un;
         const float* q = P + (row < rows ? row : rows - 1) * ld;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int64_t k = k0 + kq * 8 + 4 * h;
+        for (int h = 0; h < KW / 4; ++h) {
+          const int64_t k = k0 + kc * KW + 4 * h;
           if (VEC) {
-            r[2 * u + h] = ld4(q + (k < ke - 3 ? k : ke - 4));
+            r[u * (KW / 4) + h] = ld4(q + (k < ke - 3 ? k : ke - 4));
           } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) r[2 * u + h][e] = q[k + e < ke ? k + e : ke - 1];
+            for (int e = 0; e < 4; ++e) r[u * (KW / 4) + h][e] = q[k + e < ke ? k + e : ke - 1];
+          }
+        }
+      } else {
+        const int64_t col = r0 + un * 4;
+#pragma unroll
+        for (int e = 0; e < KW; ++e) {
+          const int64_t k = k0 + kc * KW + e;
+          const float* q = P + (k < ke ? k : ke - 1) * ld;
+          if (VEC) {
+            r[u * KW + e] = ld4(q + (col < rows ? col : rows - 4));
+          } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) r[u * KW + e][c] = q[col + c < rows ? col + c : rows - 1];
           }
         }
       }
-    } else {
-      const int64_t col = r0 + (tid >> 3) * 4;
+    }
+  };
+  float rs[SA::RS];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int64_t k = k0 + kq * 8 + e;
-        const float* q = P + (k < ke ? k : ke - 1) * ld;
-        if (VEC) {
-          r[e] = ld4(q + (col < rows ? col : rows - 4));
+  for (int i = 0; i < SA::RS; ++i) rs[i] = 0.f;
+  auto store_op = [&](auto S_, auto MASK_, const v4f* r, u32x4* img, int64_t k0, bool rowsum) {
+    using S = decltype(S_);
+    constexpr bool KC = std::is_same<S, SA>::value ? AKC : BKC;
+    constexpr bool MASK = decltype(MASK_)::value;   // tail k-tile: zero k >= ke
+    constexpr int KW = S::KW, KCH = S::KCH;
+    const int kc = tid % KCH;
+    const int64_t kbase = k0 + kc * KW;
+    char* base = reinterpret_cast<char*>(img);
+#pragma unroll
+    for (int u = 0; u < S::U; ++u) {
+      const int un = tid / KCH + u * (NT / KCH);
+#pragma unroll
+      for (int c = 0; c < (KC ? 1 : 4); ++c) {
+        float v[KW];
+#pragma unroll
+        for (int e = 0; e < KW; ++e) {
+          const float x = KC ? r[u * (KW / 4) + (e >> 2)][e & 3] : r[u * KW + e][c];
+          v[e] = (MASK && kbase + e >= ke) ? 0.f : x;
+        }
+        if (rowsum) {
+          float t = 0.f;
+#pragma unroll
+          for (int e = 0; e < KW; ++e) t += v[e];
+          rs[KC ? u : 4 * u + c] += t;
+        }
+        const int row = KC ? un : 4 * un + c;
+        char* dst = base + (size_t)row * kLpPitchQ * 16 + kc * KW * 2;
+        if constexpr (KW == 8) {
+          const v8f w{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
+          *reinterpret_cast<u32x4*>(dst) = __builtin_bit_cast(u32x4, __builtin_convertvector(w, e8_t));
         } else {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) r[e][c] = q[col + c < rows ? col + c : rows - 1];
+          const v4f w{v[0], v[1], v[2], v[3]};
+          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<u32x2*>(dst) = __builtin_bit_cast(u32x2, __builtin_convertvector(w, e4));
         }
       }
     }
   };
-  float rs[4] = {0.f, 0.f, 0.f, 0.f};   // fused row sums (A only): KC rows tid/8 + 32 u, !KC rows 4 (tid/8) + c
-  auto store_op = [&](const v4f (&r)[8], u32x4* img, bool kc, int64_t k0, bool rowsum) {
-    const int64_t kbase = k0 + kq * 8;
-    const bool tail = kbase + 8 > ke;
-    if (kc) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        v8f v;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (tail && kbase + e >= ke) ? 0.f : r[2 * u + (e >> 2)][e & 3];
-        if (rowsum) {
-          float t = 0.f;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) t += v[e];
-          rs[u] += t;
-        }
-        img[((tid >> 3) + 32 * u) * kLpPitchQ + kq] = __builtin_bit_cast(u32x4, __builtin_convertvector(v, e8));
-      }
+  auto load_tile = [&](int st, int64_t k0) {
+    if (VEC && k0 + BK <= ke) {   // uniform branch
+      load_fast(SA{}, ra[st], rsA, voA, d.lda, k0);
+      load_fast(SB{}, rb[st], rsB, voB, d.ldb, k0);
     } else {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        v8f v;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (tail && kbase + e >= ke) ? 0.f : r[e][c];
-        if (rowsum) {
-          float t = 0.f;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) t += v[e];
-          rs[c] += t;
-        }
-        img[((tid >> 3) * 4 + c) * kLpPitchQ + kq] = __builtin_bit_cast(u32x4, __builtin_convertvector(v, e8));
-      }
+      load_op(SA{}, ra[st], A, d.lda, d.M, m0, k0);
+      load_op(SB{}, rb[st], B, d.ldb, d.N, n0, k0);
     }
   };
-  auto load_tile = [&](int64_t k0) {
-    load_op(ra, A, d.lda, AKC, d.M, m0, k0);
-    load_op(rb, B, d.ldb, BKC, d.N, n0, k0);
-  };
-  auto store_tile = [&](int buf, int64_t k0) {
-    u32x4* As = smem + buf * 2 * kLpImgQ;
-    store_op(ra, As, AKC, k0, do_rs);
-    store_op(rb, As + kLpImgQ, BKC, k0, false);
+  auto store_tile = [&](int st, int buf, int64_t k0) {
+    u32x4* As = smem + buf * (IMGA + IMGB);
+    if (k0 + BK <= ke) {   // uniform branch: only a split's last k-tile needs the k-tail mask
+      store_op(SA{}, std::false_type{}, ra[st], As, k0, do_rs);
+      store_op(SB{}, std::false_type{}, rb[st], As + IMGA, k0, false);
+    } else {
+      store_op(SA{}, std::true_type{}, ra[st], As, k0, do_rs);
+      store_op(SB{}, std::true_type{}, rb[st], As + IMGA, k0, false);
+    }
   };
 
   f32x16 acc[TM][TN];
@@ -450,16 +547,9 @@ __global__ __launch_bounds__(256, 2) void gemm_lp_kernel(KernelArgs ka) {
 
   const int lh = lane >> 5, lc = lane & 31;
   const int64_t nk = ke > kb0 ? (ke - kb0 + BK - 1) / BK : 0;
-  if (nk > 0) {
-    load_tile(kb0);
-    store_tile(0, kb0);
-  }
-  __syncthreads();
-  for (int64_t kt = 0; kt < nk; ++kt) {
-    const int cur = (int)(kt & 1);
-    if (kt + 1 < nk) load_tile(kb0 + (kt + 1) * BK);
-    const u32x4* As = smem + cur * 2 * kLpImgQ;
-    const u32x4* Bs = As + kLpImgQ;
+  auto mma_tile = [&](int buf) {
+    const u32x4* As = smem + buf * (IMGA + IMGB);
+    const u32x4* Bs = As + IMGA;
     u32x4 fa[2][TM], fb[2][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) fa[0][i] = As[(wm0 + i * 32 + lc) * kLpPitchQ + lh];
@@ -481,26 +571,56 @@ __global__ __launch_bounds__(256, 2) void gemm_lp_kernel(KernelArgs ka) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = Ops::mma(__builtin_bit_cast(e8, fa[c][i]), __builtin_bit_cast(e8, fb[c][j]), acc[i][j]);
     }
+  };
+
+  if (nk > 0) load_tile(0, kb0);
+  if (PF == 2 && nk > 1) load_tile(1 % PF, kb0 + BK);
+  if (nk > 0) store_tile(0, 0, kb0);
+  __syncthreads();
+  // k-tile kt: LDS buffer kt & 1, register set kt % PF (static: the loop is unrolled by 2)
+  auto step = [&](auto P_, int64_t kt) {
+    constexpr int P = decltype(P_)::value;
+    if (PF == 2) {
+      if (kt + 2 < nk) load_tile(P % PF, kb0 + (kt + 2) * BK);   // set P was stored last step
+    } else {
+      if (kt + 1 < nk) load_tile(0, kb0 + (kt + 1) * BK);
+    }
+    mma_tile(P);
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);   // the next tile's LDS store after this tile's MFMAs
-    if (kt + 1 < nk) store_tile(cur ^ 1, kb0 + (kt + 1) * BK);
+    if (kt + 1 < nk) store_tile((P ^ 1) % PF, P ^ 1, kb0 + (kt + 1) * BK);
     __syncthreads();
+  };
+  for (int64_t kt = 0; kt < nk; kt += 2) {
+    step(std::integral_constant<int, 0>{}, kt);
+    if (kt + 1 < nk) step(std::integral_constant<int, 1>{}, kt + 1);
   }
   store_acc<TM, TN>(ka, acc, split, m0, n0, wm0, wn0, lane, z);
   if (do_rs) {   // deterministic: partials [k chunk][row] in LDS, summed in chunk order
+    constexpr int KCH = SA::KCH;
     float* red = reinterpret_cast<float*>(smem);
+    static_assert(KCH * BM * 4 <= (int)sizeof(smem), "row-sum scratch");
     __syncthreads();
+    const int kc = tid % KCH;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) red[kq * BM + (AKC ? (tid >> 3) + 32 * u : (tid >> 3) * 4 + u)] = rs[u];
+    for (int u = 0; u < SA::U; ++u) {
+      const int un = tid / KCH + u * (NT / KCH);
+      if (AKC) {
+        red[kc * BM + un] = rs[u];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) red[kc * BM + 4 * un + c] = rs[4 * u + c];
+      }
+    }
     __syncthreads();
-    if (tid < BM) {
-      float t = 0.f;
+    for (int t = tid; t < BM; t += NT) {
+      float sum = 0.f;
 #pragma unroll
-      for (int p = 0; p < 8; ++p) t += red[p * BM + tid];
-      const int64_t row = m0 + tid;
+      for (int p = 0; p < KCH; ++p) sum += red[p * BM + t];
+      const int64_t row = m0 + t;
       if (row < d.M) {
-        if (ka.partial) ka.rs_partial[(int64_t)split * d.M + row] = t;
-        else d.rowsum[row] = d.rowsum_beta != 0.f ? d.rowsum_beta * d.rowsum[row] + t : t;
+        if (ka.partial) ka.rs_partial[(int64_t)split * d.M + row] = sum;
+        else d.rowsum[row] = d.rowsum_beta != 0.f ? d.rowsum_beta * d.rowsum[row] + sum : sum;
       }
     }
   }
@@ -666,21 +786,45 @@ int launch(const GemmDesc& d, hipStream_t s, bool vec) {
   return finish_splits(d, ka, splits, s);
 }
 
-template <bool TA, bool TB>
-int launch_lp(const GemmDesc& d, hipStream_t s, bool vec, bool f16) {
+template <bool TA, bool TB, int BM, int BN, int NW, int PF>
+int launch_lp_cfg(const GemmDesc& d, hipStream_t s, bool vec, bool f16) {
+  constexpr int per_cu = lp_per_cu<BM, BN>();
+  // buffer-instruction byte offsets are 32-bit: VEC also needs both operands' extents < 2^31 B
+  const double ext_a = (double)(d.ta ? d.K : d.M) * d.lda * 4, ext_b = (double)(d.tb ? d.N : d.K) * d.ldb * 4;
+  if (ext_a >= 2147483648.0 || ext_b >= 2147483648.0 || d.batch != 1) vec = false;
   KernelArgs ka;
   int splits = 1;
-  if (int rc = plan_launch(d, kLpBM, kLpBN, kLpBK, 2, ka, &splits)) return rc;
+  if (int rc = plan_launch(d, BM, BN, kLpBK, per_cu, ka, &splits)) return rc;
   ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
-  const dim3 grid((unsigned)ka.nblk, 1, (unsigned)d.batch);
+  const dim3 grid((unsigned)ka.nblk, 1, (unsigned)d.batch), block(NW * 64);
   if (f16) {
-    if (vec) hipLaunchKernelGGL((gemm_lp_kernel<TA, TB, true, true>), grid, dim3(256), 0, s, ka);
-    else hipLaunchKernelGGL((gemm_lp_kernel<TA, TB, false, true>), grid, dim3(256), 0, s, ka);
+    if (vec) hipLaunchKernelGGL((gemm_lp_kernel<TA, TB, BM, BN, NW, true, true, PF>), grid, block, 0, s, ka);
+    else hipLaunchKernelGGL((gemm_lp_kernel<TA, TB, BM, BN, NW, false, true, PF>), grid, block, 0, s, ka);
   } else {
-    if (vec) hipLaunchKernelGGL((gemm_lp_kernel<TA, TB, true, false>), grid, dim3(256), 0, s, ka);
-    else hipLaunchKernelGGL((gemm_lp_kernel<TA, TB, false, false>), grid, dim3(256), 0, s, ka);
+    if (vec) hipLaunchKernelGGL((gemm_lp_kernel<TA, TB, BM, BN, NW, true, false, PF>), grid, block, 0, s, ka);
+    else hipLaunchKernelGGL((gemm_lp_kernel<TA, TB, BM, BN, NW, false, false, PF>), grid, block, 0, s, ka);
   }
   return finish_splits(d, ka, splits, s);
+}
+
+// Tile configuration of the bf16 / fp16 GEMM (SRK_LP_CFG selects one for A/B measurements):
+//   1: 128 x 128, 4 waves, 1 k-tile of register prefetch (2 workgroups / CU)
+//   2: 128 x 128, 4 waves, 2 k-tiles in flight
+//   3: 256 x 128, 8 waves (4 x 2, 64 x 64 each), 1 k-tile (1 workgroup / CU)
+//   4: 256 x 128, 8 waves, 2 k-tiles in flight
+//   5: 128 x 128, 8 waves (2 x 4, 64 x 32 each), 2 k-tiles in flight
+template <bool TA, bool TB>
+int launch_lp(const GemmDesc& d, hipStream_t s, bool vec, bool f16) {
+  static const int cfg_env = env_int("SRK_LP_CFG", 0);
+  int cfg = cfg_env;
+  if (!cfg) cfg = 1;
+  switch (cfg) {
+    case 2: return launch_lp_cfg<TA, TB, 128, 128, 4, 2>(d, s, vec, f16);
+    case 3: return launch_lp_cfg<TA, TB, 256, 128, 8, 1>(d, s, vec, f16);
+    case 4: return launch_lp_cfg<TA, TB, 256, 128, 8, 2>(d, s, vec, f16);
+    case 5: return launch_lp_cfg<TA, TB, 128, 128, 8, 2>(d, s, vec, f16);
+    default: return launch_lp_cfg<TA, TB, 128, 128, 4, 1>(d, s, vec, f16);
+  }
 }
 
 template <bool TA, bool TB>

@@ -104,6 +104,38 @@ __device__ __forceinline__ void map_block(int G, int S, int& dir, int& group, in
   group = pair % G;
 }
 
+// The saved gates (r, z, n, W_hn h + b_hn) of a lane's 4 cells, stored AFTER the step's arrival:
+// nothing in this launch reads them, so their write latency leaves the step-to-step chain.
+__device__ __forceinline__ void store_gates(const GruPArgs& a, const float (&gsv)[4][4], int dir, int t, int brow0,
+                                            int b_last, int j) {
+  const int H = a.H;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int b = brow0 + r;
+    if (b > b_last) continue;
+    float* gs = a.gates + (((size_t)dir * a.T + t) * a.B + b) * 4 * H;
+    gs[j] = gsv[r][0];
+    gs[H + j] = gsv[r][1];
+    gs[2 * H + j] = gsv[r][2];
+    gs[3 * H + j] = gsv[r][3];
+  }
+}
+
+// The input-projection gradients dgi (dar, daz, dan) of a lane's 4 cells, likewise after the arrival.
+__device__ __forceinline__ void store_dgi(const GruPArgs& a, const float (&dv)[4][3], int dir, int t, int brow0,
+                                          int b_last, int j) {
+  const int H = a.H;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int b = brow0 + r;
+    if (b > b_last) continue;
+    float* dgi = a.dgi + ((size_t)b * a.T + t) * 6 * H + dir * 3 * H;
+    dgi[j] = dv[r][0];
+    dgi[H + j] = dv[r][1];
+    dgi[2 * H + j] = dv[r][2];
+  }
+}
+
 // ------------------------------------------------------------------ forward
 // LDS: W slice [48][H + 4] (gate g, unit jj -> row g*16 + jj), then the h transpose tile [64][20].
 template <int H>
@@ -134,6 +166,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
   const int Gp = a.G;   // 64-row groups in this launch (the hand-off buffer is padded to Gp * 64 rows)
   const __amdgpu_buffer_rsrc_t rx = rsrc(a.xbuf + (size_t)dir * 2 * Gp * 64 * H);   // [2][Gp][4][H/16][64][4]
   float hreg[4] = {0.f, 0.f, 0.f, 0.f};                 // h_{t-1} of the lane's own 4 cells
+  float gsv[4][4];                                      // this step's gates, stored after the arrival
 
   for (int step = 0; step < T; ++step) {
     const int t = dir == 0 ? step : T - 1 - step;
@@ -206,28 +239,25 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
       const float h = (1.0f - zg) * ng + zg * hreg[r];
       hreg[r] = h;
       hT[rl * HTP + lr] = h;
-      if (b <= b_last) {
-        float* gs = a.gates + (((size_t)dir * T + t) * a.B + b) * 4 * H;
-        gs[j] = rg;
-        gs[H + j] = zg;
-        gs[2 * H + j] = ng;
-        gs[3 * H + j] = ghn;
-      }
+      gsv[r][0] = rg;
+      gsv[r][1] = zg;
+      gsv[r][2] = ng;
+      gsv[r][3] = ghn;
     }
     __syncthreads();
     stamp(a, step, 3);
-    {  // h_t -> the hand-off buffer (write-through) and y: thread = (row tid/4, units 4*(tid%4) .. +3)
-      const int rl = tid >> 2, uq = (tid & 3) * 4, b = b0 + rl;
-      if (b <= b_last) {
-        const v4f hv4 = ld4(hT + rl * HTP + uq);
-        if (step + 1 < T)   // fragment slot (row block rl/16, k block = slice, lane = (uq/4)*16 + rl%16)
-          st4_sc1(rx, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB * 64 + slice * 64 +
-                                  (uq >> 2) * 16 + (rl & 15)) * 16), hv4);
-        st4(a.y + ((size_t)b * T + t) * 2 * H + dir * H + j0 + uq, hv4);
-      }
+    v4f hv4;
+    const int yrl = tid >> 2, yuq = (tid & 3) * 4;
+    {  // h_t -> the hand-off buffer (write-through): thread = (row tid/4, units 4*(tid%4) .. +3)
+      hv4 = ld4(hT + yrl * HTP + yuq);
+      if (step + 1 < T && b0 + yrl <= b_last)   // fragment slot (row block rl/16, k block = slice, lane = (uq/4)*16 + rl%16)
+        st4_sc1(rx, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (yrl >> 4)) * NKB * 64 + slice * 64 +
+                                (yuq >> 2) * 16 + (yrl & 15)) * 16), hv4);
     }
-    arrive(cnt);
+    arrive(cnt);   // waits for the hand-off stores only: y and the gates go out after it (no consumer in this launch)
     stamp(a, step, 4);
+    if (b0 + yrl <= b_last) st4(a.y + ((size_t)(b0 + yrl) * T + t) * 2 * H + dir * H + j0 + yuq, hv4);
+    store_gates(a, gsv, dir, t, b0 + wave * 16 + lq * 4, b_last, j);
   }
 }
 
@@ -266,6 +296,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
   const int Gp = a.G;
   const __amdgpu_buffer_rsrc_t rg_ = rsrc(a.xbuf + (size_t)dir * 2 * Gp * 64 * 3 * H);   // [2][Gp][4][3H/16][64][4]
   float dhz[4] = {0.f, 0.f, 0.f, 0.f};
+  float dgv[4][3];   // this step's dgi, stored after the arrival
 
   for (int step = 0; step < T; ++step) {
     const int t = dir == 0 ? T - 1 - step : step;
@@ -339,34 +370,39 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
       dT[(rl * 3 + 0) * DTP + lr] = dar;
       dT[(rl * 3 + 1) * DTP + lr] = daz;
       dT[(rl * 3 + 2) * DTP + lr] = dan * rg;
-      if (b <= b_last) {
-        float* dgi = a.dgi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
-        dgi[j] = dar;
-        dgi[H + j] = daz;
-        dgi[2 * H + j] = dan;
-      }
+      dgv[r][0] = dar;
+      dgv[r][1] = daz;
+      dgv[r][2] = dan;
     }
     __syncthreads();
     stamp(a, step, 3);
     // dgh row slice (gates x 16 units) of 64 rows: 768 float4, 3 per thread.  Interior steps go
-    // write-through into dgh (the next step's operand); the edge step has no consumer: it goes to
-    // dgh_edge and zeroes its dgh row (kept out of the dW_hh GEMM, see srk_gru_layer_bwd).
+    // write-through into the hand-off buffer (the next step's operand) before the arrival, and to
+    // dgh (the dW_hh GEMM's operand) after it; the edge step has no consumer: it goes to dgh_edge
+    // and zeroes its dgh row (kept out of the dW_hh GEMM, see srk_gru_layer_bwd).
+    v4f val[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int v = tid + i * 256, rl = v / 12, g = (v % 12) / 4, uq = (v % 4) * 4, b = b0 + rl;
+      val[i] = ld4(dT + (rl * 3 + g) * DTP + uq);
+      if (b > b_last || edge) continue;
+      st4_sc1(rg_, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB * 64 +
+                               (g * (H / 16) + slice) * 64 + (uq >> 2) * 16 + (rl & 15)) * 16), val[i]);
+    }
+    arrive(cnt);
+    stamp(a, step, 4);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int v = tid + i * 256, rl = v / 12, g = (v % 12) / 4, uq = (v % 4) * 4, b = b0 + rl;
       if (b > b_last) continue;
-      const v4f val = ld4(dT + (rl * 3 + g) * DTP + uq);
       if (!edge) {
-        st4_sc1(rg_, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB * 64 +
-                                 (g * (H / 16) + slice) * 64 + (uq >> 2) * 16 + (rl & 15)) * 16), val);
-        st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + j0 + uq, val);
+        st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + j0 + uq, val[i]);
       } else {
-        st4(a.dgh_edge + ((size_t)dir * B + b) * 3 * H + g * H + j0 + uq, val);
+        st4(a.dgh_edge + ((size_t)dir * B + b) * 3 * H + g * H + j0 + uq, val[i]);
         st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + j0 + uq, v4f{0.f, 0.f, 0.f, 0.f});
       }
     }
-    arrive(cnt);
-    stamp(a, step, 4);
+    store_dgi(a, dgv, dir, t, b0 + wave * 16 + lq * 4, b_last, j);
   }
 }
 
@@ -439,6 +475,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
   const int Gp = a.G;
   const __amdgpu_buffer_rsrc_t rx = rsrc(a.xbuf + (size_t)dir * 2 * Gp * 64 * H);   // 16-bit [2][Gp][4][H/32][64][8]
   float hreg[4] = {0.f, 0.f, 0.f, 0.f};
+  float gsv[4][4];
 
   for (int step = 0; step < T; ++step) {
     const int t = dir == 0 ? step : T - 1 - step;
@@ -496,20 +533,15 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
       const float h = (1.0f - zg) * ng + zg * hreg[r];
       hreg[r] = h;
       hT[rl * HTP + lr] = h;
-      if (b <= b_last) {
-        float* gs = a.gates + (((size_t)dir * T + t) * a.B + b) * 4 * H;
-        gs[j] = rg;
-        gs[H + j] = zg;
-        gs[2 * H + j] = ng;
-        gs[3 * H + j] = ghn;
-      }
+      gsv[r][0] = rg;
+      gsv[r][1] = zg;
+      gsv[r][2] = ng;
+      gsv[r][3] = ghn;
     }
     __syncthreads();
     stamp(a, step, 3);
-    {  // y (fp32): thread = (row tid/4, units 4*(tid%4) .. +3)
-      const int rl = tid >> 2, uq = (tid & 3) * 4, b = b0 + rl;
-      if (b <= b_last) st4(a.y + ((size_t)b * T + t) * 2 * H + dir * H + j0 + uq, ld4(hT + rl * HTP + uq));
-    }
+    const int yrl = tid >> 2, yuq = (tid & 3) * 4;   // y (fp32): thread = (row tid/4, units 4*(tid%4) .. +3)
+    const v4f yv = ld4(hT + yrl * HTP + yuq);
     if (step + 1 < T && tid < 128) {   // hand-off (16-bit): thread = (row tid/2, units 8*(tid%2) .. +7)
       const int rl = tid >> 1, half = tid & 1;
       if (b0 + rl <= b_last) {
@@ -519,8 +551,10 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
                 __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))));
       }
     }
-    arrive(cnt);
+    arrive(cnt);   // the hand-off only: y and the gates go out after it
     stamp(a, step, 4);
+    if (b0 + yrl <= b_last) st4(a.y + ((size_t)(b0 + yrl) * T + t) * 2 * H + dir * H + j0 + yuq, yv);
+    store_gates(a, gsv, dir, t, b0 + wave * 16 + lq * 4, b_last, j);
   }
 }
 
@@ -560,6 +594,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
   const int Gp = a.G;
   const __amdgpu_buffer_rsrc_t rg_ = rsrc(a.xbuf + (size_t)dir * 2 * Gp * 64 * 3 * H);   // 16-bit [2][Gp][4][3H/32][64][8]
   float dhz[4] = {0.f, 0.f, 0.f, 0.f};
+  float dgv[4][3];
 
   for (int step = 0; step < T; ++step) {
     const int t = dir == 0 ? T - 1 - step : step;
@@ -627,27 +662,17 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
       dT[(rl * 3 + 0) * DTP + lr] = dar;
       dT[(rl * 3 + 1) * DTP + lr] = daz;
       dT[(rl * 3 + 2) * DTP + lr] = dan * rg;
-      if (b <= b_last) {
-        float* dgi = a.dgi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
-        dgi[j] = dar;
-        dgi[H + j] = daz;
-        dgi[2 * H + j] = dan;
-      }
+      dgv[r][0] = dar;
+      dgv[r][1] = daz;
+      dgv[r][2] = dan;
     }
     __syncthreads();
     stamp(a, step, 3);
-    // dgh (fp32, the dW_hh GEMM operand): as the fp32 kernel; the edge step goes to dgh_edge
+    v4f val[3];   // dgh (fp32, the dW_hh GEMM operand), stored after the arrival
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const int v = tid + i * 256, rl = v / 12, g = (v % 12) / 4, uq = (v % 4) * 4, b = b0 + rl;
-      if (b > b_last) continue;
-      const v4f val = ld4(dT + (rl * 3 + g) * DTP + uq);
-      if (!edge) {
-        st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + j0 + uq, val);
-      } else {
-        st4(a.dgh_edge + ((size_t)dir * B + b) * 3 * H + g * H + j0 + uq, val);
-        st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + j0 + uq, v4f{0.f, 0.f, 0.f, 0.f});
-      }
+      const int v = tid + i * 256, rl = v / 12, g = (v % 12) / 4, uq = (v % 4) * 4;
+      val[i] = ld4(dT + (rl * 3 + g) * DTP + uq);
     }
     if (!edge) {   // hand-off (16-bit): 64 rows x 3 gates x 2 halves of 8 units
       for (int v = tid; v < 64 * 3 * 2; v += 256) {
@@ -660,8 +685,20 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
                 __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))));
       }
     }
-    arrive(cnt);
+    arrive(cnt);   // the hand-off only: dgh, dgh_edge and dgi go out after it
     stamp(a, step, 4);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int v = tid + i * 256, rl = v / 12, g = (v % 12) / 4, uq = (v % 4) * 4, b = b0 + rl;
+      if (b > b_last) continue;
+      if (!edge) {
+        st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + j0 + uq, val[i]);
+      } else {
+        st4(a.dgh_edge + ((size_t)dir * B + b) * 3 * H + g * H + j0 + uq, val[i]);
+        st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + j0 + uq, v4f{0.f, 0.f, 0.f, 0.f});
+      }
+    }
+    store_dgi(a, dgv, dir, t, b0 + wave * 16 + lq * 4, b_last, j);
   }
 }
 

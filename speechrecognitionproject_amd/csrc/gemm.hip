@@ -807,7 +807,7 @@ int launch_lp_cfg(const GemmDesc& d, hipStream_t s, bool vec, bool f16) {
   return finish_splits(d, ka, splits, s);
 }
 
-// Tile configuration of the bf16 / fp16 GEMM (SRK_LP_CFG selects one for A/B measurements):
+// Tile configuration of the bf16 / fp16 GEMM (SRK_LP_CFG overrides the choice for A/B measurements):
 //   1: 128 x 128, 4 waves, 1 k-tile of register prefetch (2 workgroups / CU)
 //   2: 128 x 128, 4 waves, 2 k-tiles in flight
 //   3: 256 x 128, 8 waves (4 x 2, 64 x 64 each), 1 k-tile (1 workgroup / CU)
@@ -817,7 +817,9 @@ template <bool TA, bool TB>
 int launch_lp(const GemmDesc& d, hipStream_t s, bool vec, bool f16) {
   static const int cfg_env = env_int("SRK_LP_CFG", 0);
   int cfg = cfg_env;
-  if (!cfg) cfg = 1;
+  // measured (profiles/r01zf_gemm_bench_bf16_cfg*.txt): 256 x 128 tiles win whenever an operand is
+  // row-contiguous (dx, dW: 12-25 %), the 128 x 128 tile on the x W^T projection (both k-contiguous)
+  if (!cfg) cfg = (d.M >= 1024 && !(!TA && TB)) ? 3 : 1;
   switch (cfg) {
     case 2: return launch_lp_cfg<TA, TB, 128, 128, 4, 2>(d, s, vec, f16);
     case 3: return launch_lp_cfg<TA, TB, 256, 128, 8, 1>(d, s, vec, f16);

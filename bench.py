@@ -77,8 +77,10 @@ CFG = {"mfcc_bgru": "cfg2 mfcc_bgru: on-device MFCC[39x51] + 2-layer BiGRU(512) 
 FEATURE = {"mfcc_bgru": ("mfcc", 71956), "fbanks_cnn": ("fbank", 111040), "spec_bgru": ("spec", 126916),
            "mfrn_bgru": ("mfcc", 71956), "spec_cnn": ("spec", 126916)}
 MATRIX_KERNELS = ("gru_fwd_seq", "gru_bwd_seq", "gru_fwd_step", "gru_bwd_step", "gemm_f32",
-                  "conv_fwd", "conv_dgrad", "conv_wgrad", "gemm_bf16", "gemm_f16", "gru_fwd_seq_lp", "gru_bwd_seq_lp")
-LP_KERNELS = ("gemm_bf16", "gemm_f16", "gru_fwd_seq_lp", "gru_bwd_seq_lp")
+                  "conv_fwd", "conv_dgrad", "conv_wgrad", "gemm_bf16", "gemm_f16", "gru_fwd_seq_lp", "gru_bwd_seq_lp",
+                  "conv_fwd_lp", "conv_dgrad_lp", "conv_wgrad_lp")
+LP_KERNELS = ("gemm_bf16", "gemm_f16", "gru_fwd_seq_lp", "gru_bwd_seq_lp", "conv_fwd_lp", "conv_dgrad_lp",
+              "conv_wgrad_lp")
 OTHER_KERNELS = ("mfcc", "fbank", "spec", "noise_mix", "adam", "batchnorm_fwd", "batchnorm_bwd", "conv1_pool_fwd",
                  "conv1_pool_wgrad",
                  "maxpool_fwd", "maxpool_bwd")

@@ -77,18 +77,75 @@ __device__ __forceinline__ int64_t a_offset(const ConvArgs& c, const Pix& p, con
   return ok ? (((int64_t)p.n * c.H + hi) * c.W + wi) * c.Ci + t.ch : 0;
 }
 
+// ------------------------------------------------------------------ 16-bit operand images
+// (matmul_precision bf16 / fp16): the staged fp32 float4s are rounded to 4 x 16 bit and stored as
+// ONE 8-B write each, in the orientation they were gathered:
+//   k-contiguous A (fwd / dgrad):  [row][BK + 8]       fragment = ds_read_b128 (8 consecutive k)
+//   row-contiguous A (wgrad), B:   [k][kTrPitch]       fragment = 2 x ds_read_b64_tr_b16 (the
+//       hardware transpose read: lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3;
+//       lane i receives column i of the 4 rows), pitch 160 = 32 (mod 128) elements, so each
+//       32-lane half reads 4 rows x 64 B on 64 distinct banks.
+typedef float v8f_ __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+constexpr int kTrPitch = 160;
+
+template <int LP> struct ConvLp;
+template <> struct ConvLp<1> {
+  typedef __bf16 e8 __attribute__((ext_vector_type(8)));
+  typedef __bf16 e4 __attribute__((ext_vector_type(4)));
+  __device__ static __forceinline__ f32x16 mma(u32x4_ a, u32x4_ b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(e8, a), __builtin_bit_cast(e8, b), c, 0, 0, 0);
+  }
+};
+template <> struct ConvLp<2> {
+  typedef _Float16 e8 __attribute__((ext_vector_type(8)));
+  typedef _Float16 e4 __attribute__((ext_vector_type(4)));
+  __device__ static __forceinline__ f32x16 mma(u32x4_ a, u32x4_ b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(e8, a), __builtin_bit_cast(e8, b), c, 0, 0, 0);
+  }
+};
+
+// 16-bit image of one operand: element offset of a staged float4 (same walk as Img::store_off) and
+// the 32x32x16 MFMA fragment of operand rows c0 + (lane & 31), k = kk + 8 (lane >> 5) + 0..7.
+template <bool KC, int ROWS, int BK>
+struct Img16 {
+  static constexpr int P = KC ? BK + 8 : kTrPitch;
+  static constexpr int ELEMS = KC ? ROWS * P : BK * P;
+  static_assert(KC || ROWS <= kTrPitch, "transposed image pitch");
+  __device__ static __forceinline__ int store_off(int vi) {
+    return KC ? (vi / (BK / 4)) * P + (vi % (BK / 4)) * 4 : (vi / (ROWS / 4)) * P + (vi % (ROWS / 4)) * 4;
+  }
+  __device__ static __forceinline__ u32x4_ frag(const unsigned short* img, int c0, int kk, int lane) {
+    if (KC) return *reinterpret_cast<const u32x4_*>(img + (c0 + (lane & 31)) * P + kk + 8 * (lane >> 5));
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    const unsigned short* a = img + (kk + 8 * (lane >> 5) + q) * P + c0 + 16 * ((lane >> 4) & 1) + 4 * p;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 4 * P));
+    const u32x2_ l2 = __builtin_bit_cast(u32x2_, lo), h2 = __builtin_bit_cast(u32x2_, hi);
+    return u32x4_{l2.x, l2.y, h2.x, h2.y};
+  }
+};
+
 // VEC: the 4 elements of a staged A float4 share one pixel and one (kh, kw) — channel count % 4 == 0
 // (fwd / wgrad: Ci, dgrad: Co).  VECB: the B operand's N % 4 == 0 (16-B loads along n).
-template <int MODE, int BM, int BN, int BK, bool VEC, bool VECB>
+// LP: 0 = fp32 operands (v_mfma_f32_32x32x2_f32), 1 / 2 = bf16 / fp16 operands rounded at LDS-store
+// time (v_mfma_f32_32x32x16_{bf16,f16}, Img16 images), fp32 gathers, masks and epilogue alike.
+template <int MODE, int BM, int BN, int BK, bool VEC, bool VECB, int LP = 0>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   constexpr int NT = 256;
   constexpr bool AKC = MODE != kWgrad;   // A k-contiguous (channels along k) for fwd / dgrad
   using IA = Img<AKC, BM, BK>;
   using IB = Img<false, BN, BK>;         // B = row-major [K][N] (Wt / Wd / dY)
+  using JA = Img16<AKC, BM, BK>;
+  using JB = Img16<false, BN, BK>;
   constexpr int VA = BM * BK / 4 / NT, VB = BN * BK / 4 / NT;
   constexpr int TM = BM / 64, TN = BN / 64;
   static_assert(VA >= 1 && VB >= 1 && TM >= 1 && TN >= 1 && VA * 4 <= 32, "bad tile");
-  __shared__ __attribute__((aligned(16))) float smem[2 * (IA::FLOATS + IB::FLOATS)];
+  constexpr int STAGE_FLOATS = LP ? (JA::ELEMS + JB::ELEMS + 1) / 2 : IA::FLOATS + IB::FLOATS;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE_FLOATS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int split, tm, tn;
   map_tile(c.nblk, c.tiles, c.tiles_m, c.tiles_n, c.group_m, true, split, tm, tn);
@@ -183,7 +240,35 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
       bmask |= (k < ke ? 1u : 0u) << i;
     }
   };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
   auto store_tile = [&](int buf) {
+    if constexpr (LP != 0) {
+      using E4 = typename ConvLp<LP>::e4;
+      unsigned short* As = reinterpret_cast<unsigned short*>(smem + buf * STAGE_FLOATS);
+      unsigned short* Bs = As + JA::ELEMS;
+#pragma unroll
+      for (int i = 0; i < VA; ++i) {
+        v4f v = ra[i];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (amask >> (4 * i + e)) & 1u ? v[e] : 0.f;
+        *reinterpret_cast<u32x2_*>(As + JA::store_off(tid + i * NT)) =
+            __builtin_bit_cast(u32x2_, __builtin_convertvector(v, E4));
+      }
+#pragma unroll
+      for (int i = 0; i < VB; ++i) {
+        const v4f v = (bmask >> i) & 1u ? rb[i] : v4f{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<u32x2_*>(Bs + JB::store_off(tid + i * NT)) =
+            __builtin_bit_cast(u32x2_, __builtin_convertvector(v, E4));
+      }
+      return;
+    }
     float* As = smem + buf * (IA::FLOATS + IB::FLOATS);
     float* Bs = As + IA::FLOATS;
 #pragma unroll
@@ -199,14 +284,31 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
       st4(Bs + IB::store_off(tid + i * NT), v);
     }
   };
-
-  f32x16 acc[TM][TN];
+  // 16-bit stage: BK / 16 k-steps, fragments of the next step read ahead of this step's MFMAs
+  auto mma_lp = [&](int buf) {
+    const unsigned short* As = reinterpret_cast<const unsigned short*>(smem + buf * STAGE_FLOATS);
+    const unsigned short* Bs = As + JA::ELEMS;
+    u32x4_ fa[2][TM], fb[2][TN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) fa[0][i] = JA::frag(As, wm0 + i * 32, 0, lane);
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < TN; ++j) fb[0][j] = JB::frag(Bs, wn0 + j * 32, 0, lane);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int cb = ks & 1;
+      if (ks + 1 < BK / 16) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[cb ^ 1][i] = JA::frag(As, wm0 + i * 32, 16 * (ks + 1), lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[cb ^ 1][j] = JB::frag(Bs, wn0 + j * 32, 16 * (ks + 1), lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = ConvLp<LP == 0 ? 1 : LP>::mma(fa[cb][i], fb[cb][j], acc[i][j]);
+    }
+  };
 
   const int64_t nk = ke > kb0 ? (ke - kb0 + BK - 1) / BK : 0;
   if (nk > 0) {
@@ -217,8 +319,12 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   for (int64_t kt = 0; kt < nk; ++kt) {
     const int cur = (int)(kt & 1);
     if (kt + 1 < nk) load_tile(kb0 + (kt + 1) * BK);
-    const float* As = smem + cur * (IA::FLOATS + IB::FLOATS);
-    mma_stage<IA, IB, TM, TN, BK>(As, As + IA::FLOATS, acc, wm0, wn0, lane);
+    if constexpr (LP != 0) {
+      mma_lp(cur);
+    } else {
+      const float* As = smem + cur * (IA::FLOATS + IB::FLOATS);
+      mma_stage<IA, IB, TM, TN, BK>(As, As + IA::FLOATS, acc, wm0, wn0, lane);
+    }
     asm volatile("" ::: "memory");      // keep the stage-k+1 LDS store (and its vmcnt wait)
     __builtin_amdgcn_sched_barrier(0);   // after this stage's MFMAs
     if (kt + 1 < nk) store_tile(cur ^ 1);
@@ -375,22 +481,31 @@ int conv_scratch(size_t floats, float** out) {
   return SRK_OK;
 }
 
+template <int MODE, int BM, int BN, int BK, int LP>
+void launch_conv_p(const ConvArgs& c, dim3 grid, hipStream_t s, bool vec, bool vecb) {
+  if (vec && vecb) hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, true, true, LP>), grid, dim3(256), 0, s, c);
+  else if (vecb) hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, false, true, LP>), grid, dim3(256), 0, s, c);
+  else hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, false, false, LP>), grid, dim3(256), 0, s, c);
+}
+
 template <int MODE, int BM, int BN>
-void launch_conv(const ConvArgs& c, dim3 grid, hipStream_t s, bool vec, bool vecb) {
-  if (vec && vecb) hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, 32, true, true>), grid, dim3(256), 0, s, c);
-  else if (vecb) hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, 32, false, true>), grid, dim3(256), 0, s, c);
-  else hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, 32, false, false>), grid, dim3(256), 0, s, c);
+void launch_conv(const ConvArgs& c, dim3 grid, hipStream_t s, bool vec, bool vecb, int prec) {
+  if (prec == kPrecBF16) launch_conv_p<MODE, BM, BN, 64, 1>(c, grid, s, vec, vecb);
+  else if (prec == kPrecF16) launch_conv_p<MODE, BM, BN, 64, 2>(c, grid, s, vec, vecb);
+  else launch_conv_p<MODE, BM, BN, 32, 0>(c, grid, s, vec, vecb);
 }
 
 template <int MODE>
 int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
-  constexpr int BK = 32;
+  const int prec = matmul_prec();
+  const int BK = prec == kPrecF32 ? 32 : 64;   // 16-bit: 64-deep k-tiles (4 MFMA k-steps per barrier)
   // tile: 128 x 128 unless the GEMM is narrow (N <= 64: 128 x 64) or small (64 x 64)
   int BM = 128, BN = c.Nn <= 64 ? 64 : 128;
   if (((c.M + 127) / 128) * ((c.Nn + BN - 1) / BN) < 64 && c.K < 2048) { BM = 64; BN = 64; }
   const int64_t tm = (c.M + BM - 1) / BM, tn = (c.Nn + BN - 1) / BN;
   SRK_REQUIRE(tm * tn <= (INT32_MAX >> 9), SRK_ERR_INVALID, "conv: grid too large");
-  const int lds = 2 * 4 * ((MODE != kWgrad ? BM * (BK + 4) : BK * (BM + 8)) + BK * (BN + 8));
+  const int lds = prec == kPrecF32 ? 2 * 4 * ((MODE != kWgrad ? BM * (BK + 4) : BK * (BM + 8)) + BK * (BN + 8))
+                                   : 2 * 2 * ((MODE != kWgrad ? BM * (BK + 8) : BK * kTrPitch) + BK * kTrPitch);
   const int64_t slots = (int64_t)kCUs * std::min(8, (160 * 1024) / lds);
   // weight-gradient GEMMs reduce over every pixel (K up to millions) onto a few hundred tiles:
   // allow deep splits there (deterministic slab reduction)
@@ -410,11 +525,12 @@ int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
   const int chans = MODE == kDgrad ? c.Co : c.Ci;
   const bool vecb = c.Nn % 4 == 0;
   const bool vec = (chans % 4 == 0) && vecb;
-  ProfScope prof(name, s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
+  ProfScope prof(prec == kPrecF32 ? name : (MODE == kFwd ? "conv_fwd_lp" : MODE == kDgrad ? "conv_dgrad_lp" : "conv_wgrad_lp"),
+                 s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
   const dim3 grid((unsigned)c.nblk);
-  if (BM == 64) launch_conv<MODE, 64, 64>(c, grid, s, vec, vecb);
-  else if (BN == 64) launch_conv<MODE, 128, 64>(c, grid, s, vec, vecb);
-  else launch_conv<MODE, 128, 128>(c, grid, s, vec, vecb);
+  if (BM == 64) launch_conv<MODE, 64, 64>(c, grid, s, vec, vecb, prec);
+  else if (BN == 64) launch_conv<MODE, 128, 64>(c, grid, s, vec, vecb, prec);
+  else launch_conv<MODE, 128, 128>(c, grid, s, vec, vecb, prec);
   SRK_CHECK_HIP(hipGetLastError());
   if (splits > 1) {
     const int64_t n = c.M * c.Nn;
@@ -490,7 +606,8 @@ int srk_conv2d_nhwc_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t
     g.A = dy; g.lda = Co;
     g.B = ws; g.ldb = Co; g.tb = true;
     g.C = dx; g.ldc = KW * Ci;
-    srk::ProfScope prof("conv_dgrad", s, 2.0 * (double)g.M * (double)g.N * (double)g.K);
+    srk::ProfScope prof(srk::matmul_prec() == srk::kPrecF32 ? "conv_dgrad" : "conv_dgrad_lp", s,
+                        2.0 * (double)g.M * (double)g.N * (double)g.K);
     if ((rc = srk::gemm_f32(g, s))) return rc;
   } else if (dx) {
     hipLaunchKernelGGL(srk::weight_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, (int)Co,

@@ -155,14 +155,17 @@ def test_bigru_lowprec_grads_close_to_fp32(prec):
 
 
 # ----------------------------------------------------------------------------- whole models
-@pytest.mark.parametrize("name", ["mfcc_bgru", "spec_bgru"])
+@pytest.mark.parametrize("name", ["mfcc_bgru", "spec_bgru", "fbanks_cnn", "resnet_bgru", "spec_cnn", "cnn_bgru",
+                                  "mfrn_bgru"])
 def test_model_lowprec_logits_vs_reference_golden(prec, name):
+    import importlib
     from conftest import golden
     from oracle import models as OM
     from tolerances import LOGITS_REL_LOWPREC, rel_err
     from speechrecognitionproject_amd import nn as snn
-    from speechrecognitionproject_amd.models import model_mfcc_bgru, model_spec_bgru
-    mod, ocls = {"mfcc_bgru": (model_mfcc_bgru, OM.MfccBGRU), "spec_bgru": (model_spec_bgru, OM.SpecBGRU)}[name]
+    ocls = {"mfcc_bgru": OM.MfccBGRU, "spec_bgru": OM.SpecBGRU, "fbanks_cnn": OM.FbanksCNN,
+            "resnet_bgru": OM.ResnetBGRU, "spec_cnn": OM.SpecCNN, "cnn_bgru": OM.CnnBGRU, "mfrn_bgru": OM.MfrnBGRU}[name]
+    mod = importlib.import_module("speechrecognitionproject_amd.models.model_" + name)
     g = golden(name + "_golden.npz")
     net = mod.Network().cuda()
     net.load_state_dict(OM.seeded_state_dict(ocls(), 0))
@@ -173,4 +176,52 @@ def test_model_lowprec_logits_vs_reference_golden(prec, name):
     assert rel_err(out.detach().cpu().numpy(), g["logits"]) <= LOGITS_REL_LOWPREC
     assert abs(loss.item() - float(g["loss"])) <= LOGITS_REL_LOWPREC * max(1.0, abs(float(g["loss"])))
     for p in net.parameters():
-        assert torch.isfinite(p.grad).all()
+        assert p.grad is None or torch.isfinite(p.grad).all()
+
+
+# ----------------------------------------------------------------------------- convolutions
+CONV_LP = [  # N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw  (fbanks_cnn layers, resnet 1-D strided, odd edges)
+    (2, 98, 40, 64, 128, 1, 7, 0, 3, 1, 1),
+    (2, 98, 10, 128, 256, 1, 10, 0, 0, 1, 1),
+    (3, 98, 1, 256, 512, 7, 1, 3, 0, 1, 1),
+    (2, 9, 11, 5, 7, 3, 2, 1, 0, 1, 1),
+    (4, 17, 13, 12, 36, 3, 3, 1, 1, 1, 1),
+    (2, 1, 1000, 64, 128, 1, 15, 0, 7, 1, 2),
+    (2, 1, 16000, 1, 64, 1, 80, 0, 38, 1, 16),
+]
+
+
+@pytest.mark.parametrize("shape", CONV_LP)
+def test_conv_lowprec_exact_rounding(prec, shape):
+    """Implicit-GEMM conv fwd / dgrad / wgrad with 16-bit operands == the float64 convolution of
+    the host-rounded operands (x, w for fwd; dy, w for dgrad; x, dy for wgrad)."""
+    import torch.nn.functional as F
+    from speechrecognitionproject_amd import nn as snn
+    N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw = shape
+    g = torch.Generator().manual_seed(N * 100 + Co + KW)
+    x = torch.randn(N, Ci, H, W, generator=g)
+    w = torch.randn(Co, Ci, KH, KW, generator=g) / (Ci * KH * KW) ** 0.5
+    b = torch.randn(Co, generator=g)
+    xm = x.permute(0, 2, 3, 1).contiguous().cuda().requires_grad_(True)
+    wm, bm = w.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+    _lib.prof_enable(1)
+    ym = snn._Conv2dNHWCFn.apply(xm, wm, bm, (ph, pw), (sh, sw))
+    gy = torch.randn(ym.permute(0, 3, 1, 2).shape, generator=g)
+    (ym * gy.permute(0, 2, 3, 1).cuda()).sum().backward()
+    torch.cuda.synchronize()
+    n_lp = _lib.prof_read("conv_fwd_lp")[0] + _lib.prof_read("conv_wgrad_lp")[0]
+    _lib.prof_enable(0)
+    assert n_lp >= 2, "the 16-bit conv kernels did not run"
+    xr, wr, gr = _rounded(x, prec), _rounded(w, prec), _rounded(gy, prec)
+    y_ref = F.conv2d(xr, wr, b.double(), stride=(sh, sw), padding=(ph, pw))
+    dx_ref = torch.nn.grad.conv2d_input(x.shape, wr, gr, stride=(sh, sw), padding=(ph, pw))
+    dw_ref = torch.nn.grad.conv2d_weight(xr, w.shape, gr, stride=(sh, sw), padding=(ph, pw))
+    K = Ci * KH * KW
+
+    def close(out, ref, k):
+        # fp32 accumulation of k rounded products; only the summation order differs
+        return (out.double() - ref).abs().max().item() <= 1e-5 * (1 + ref.abs().max().item()) * max(1.0, (k / 256) ** 0.5)
+
+    assert close(ym.detach().permute(0, 3, 1, 2).cpu(), y_ref, K)
+    assert close(xm.grad.permute(0, 3, 1, 2).cpu(), dx_ref, Co * KH * KW)
+    assert close(wm.grad.cpu(), dw_ref, N * y_ref.shape[2] * y_ref.shape[3])

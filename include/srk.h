@@ -140,6 +140,12 @@ int srk_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, floa
 int srk_gemm_rowsum_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
                         int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc,
                         float* rowsum, void* stream);
+/* The same GEMM on 16-bit operands already in memory (bf16 or fp16 as set by matmul_precision,
+ * which must not be fp32): A / B hold raw 16-bit values, leading dimensions in elements; fp32
+ * accumulation, C / bias fp32.  Needs 16-B aligned rows whose lengths are multiples of 8.      */
+int srk_gemm_16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha, const uint16_t* A,
+                int64_t lda, const uint16_t* B, int64_t ldb, float beta, float* C, int64_t ldc,
+                const float* bias, int bias_mode, void* stream);
 /* out[n] = beta * out[n] + sum_m X[m, n]  (bias gradients).                                 */
 int srk_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, float beta, void* stream);
 
@@ -153,7 +159,9 @@ int srk_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out
  * ws (bwd scratch): srk_gru_workspace_floats(.., backward=1) floats.
  * Backward writes dx [B, T, in] (NULL when the input needs no gradient) and OVERWRITES
  * (accumulate = 0) or ADDS TO (accumulate = 1: autograd's .grad accumulation, done in the GEMM
- * epilogues) dw_ih, dw_hh, db_ih, db_hh (same stacked layouts).                             */
+ * epilogues) dw_ih, dw_hh, db_ih, db_hh (same stacked layouts).  The backward must run at the
+ * matmul_precision of its forward (with bf16 / fp16 the forward workspace carries the 16-bit
+ * operands of the backward's GEMMs).                                                          */
 int64_t srk_gru_workspace_floats(int64_t B, int64_t T, int64_t in, int64_t H, int backward);
 int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t H, const float* w_ih,
                       const float* w_hh, const float* b_ih, const float* b_hh, float* y, float* ws,

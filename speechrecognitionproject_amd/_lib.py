@@ -40,6 +40,7 @@ _SIGS = {
     "srk_softmax_ensemble": [_P, _I64, _I64, _I64, _P, _P, _P, _P],
     "srk_gemm_f32": [_I, _I, _I64, _I64, _I64, _F, _P, _I64, _P, _I64, _F, _P, _I64, _P, _I, _P],
     "srk_gemm_rowsum_f32": [_I, _I, _I64, _I64, _I64, _F, _P, _I64, _P, _I64, _F, _P, _I64, _P, _P],
+    "srk_gemm_16": [_I, _I, _I64, _I64, _I64, _F, _P, _I64, _P, _I64, _F, _P, _I64, _P, _I, _P],
     "srk_colsum_f32": [_P, _I64, _I64, _I64, _P, _F, _P],
     "srk_gru_workspace_floats": [_I64, _I64, _I64, _I64, _I],
     "srk_gru_layer_fwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P],
@@ -135,6 +136,26 @@ def set_matmul_precision(name):
 
 def matmul_precision():
     return _precision
+
+
+class precision_scope:
+    """Run a block at a given matmul precision (restored after): autograd backward passes use the
+    precision their forward ran at (the 16-bit GRU backward reads 16-bit operands its forward
+    wrote)."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        self.prev = _precision
+        if self.name != self.prev:
+            set_matmul_precision(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        if _precision != self.prev:
+            set_matmul_precision(self.prev)
+        return False
 
 
 def spin_timeouts():

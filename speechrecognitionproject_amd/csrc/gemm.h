@@ -21,6 +21,11 @@ struct GemmDesc {
   float* rowsum = nullptr; float rowsum_beta = 0.f;
   // matrix-core operand precision (MatmulPrec); -1 = the process setting (srk_set_option)
   int prec = -1;
+  // 16-bit operands already in memory (bf16 / fp16 per `prec`, same layouts and leading dimensions
+  // in elements): when BOTH are set they replace A / B and no rounding happens on chip (half the
+  // operand bytes).  No fused row sums on this path.
+  const uint16_t* A16 = nullptr;
+  const uint16_t* B16 = nullptr;
 };
 
 // Enqueue on `stream`; returns SRK_OK or an srk_status.

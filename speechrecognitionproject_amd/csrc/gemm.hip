@@ -626,6 +626,179 @@ __global__ __launch_bounds__(NW * 64, (lp_per_cu<BM, BN>())) void gemm_lp_kernel
   }
 }
 
+// ------------------------------------------------------------------ 16-bit operands in memory
+// Both operands already bf16 / fp16 in HBM (GemmDesc::A16 / B16, written by their producers): every
+// staged 16-B unit is 8 elements that go to LDS unchanged, so the tile moves HALF the bytes of the
+// on-chip-rounding kernel above and spends no VALU on conversion.
+//   k-contiguous operand:   unit = 8 consecutive k of one row  -> image [row][64 + 8], fragment =
+//                           one ds_read_b128;
+//   row-contiguous operand: unit = 8 consecutive rows at one k -> image [k][ROWS + 32] (pitch = 32
+//                           mod 128 elements), fragment = 2 x ds_read_b64_tr_b16 (hardware transpose).
+// VEC only (host-checked): 16-B aligned bases, leading dimensions % 8 == 0, K % 8 (k-contiguous) and
+// rows % 8 (row-contiguous) == 0, so a unit is wholly valid or wholly invalid; invalid units are
+// clamped loads zeroed at LDS-store time (k tail), or feed discarded outputs (rows).
+typedef short s16x4_ __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+
+template <bool KC, int ROWS>
+struct H16Img {
+  static constexpr int P = KC ? kLpBK + 8 : ROWS + 32;      // elements
+  static constexpr int ELEMS = KC ? ROWS * P : kLpBK * P;
+  static_assert(KC || P % 128 == 32, "transposed image pitch");
+  __device__ static __forceinline__ u32x4 frag(const unsigned short* img, int c0, int kk, int lane) {
+    if (KC) return *reinterpret_cast<const u32x4*>(img + (c0 + (lane & 31)) * P + kk + 8 * (lane >> 5));
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    const unsigned short* a = img + (kk + 8 * (lane >> 5) + q) * P + c0 + 16 * ((lane >> 4) & 1) + 4 * p;
+    typedef __attribute__((address_space(3))) s16x4_ lds_s16x4;
+    const s16x4_ lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a));
+    const s16x4_ hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 4 * P));
+    const u32x2_ l2 = __builtin_bit_cast(u32x2_, lo), h2 = __builtin_bit_cast(u32x2_, hi);
+    return u32x4{l2.x, l2.y, h2.x, h2.y};
+  }
+};
+
+template <bool TA, bool TB, int BM, int BN>
+constexpr int h16_per_cu() { return 2 * 2 * (H16Img<!TA, BM>::ELEMS + H16Img<TB, BN>::ELEMS) <= 80 * 1024 ? 2 : 1; }
+
+template <bool TA, bool TB, int BM, int BN, int NW, bool F16>
+__global__ __launch_bounds__(NW * 64, (h16_per_cu<TA, TB, BM, BN>())) void gemm_h16_kernel(KernelArgs ka) {
+  using Ops = LpOps<F16>;
+  using e8 = typename Ops::e8;
+  constexpr int NT = NW * 64, BK = kLpBK;
+  constexpr int WM = (NW == 4) ? 2 : (BM >= 256 ? 4 : 2), WN = NW / WM;
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr bool AKC = !TA, BKC = TB;
+  using IA = H16Img<AKC, BM>;
+  using IB = H16Img<BKC, BN>;
+  constexpr int UA = BM * 8 / NT, UB = BN * 8 / NT;   // 16-B units per thread per operand
+  static_assert(UA >= 1 && UB >= 1 && BM * 8 % NT == 0 && BN * 8 % NT == 0, "staging");
+  constexpr int STAGE = IA::ELEMS + IB::ELEMS;         // 16-bit elements per stage
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * STAGE];
+  const GemmDesc& d = ka.d;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int split, tm, tn;
+  map_tile(ka.nblk, ka.tiles, ka.tiles_m, ka.tiles_n, ka.group_m, ka.remap != 0, split, tm, tn);
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kb0 = split * ka.kchunk;
+  const int64_t ke = (kb0 + ka.kchunk < d.K) ? kb0 + ka.kchunk : d.K;
+  const int wm0 = (wave / WN) * (BM / WM), wn0 = (wave % WN) * (BN / WN);
+  auto rsrc_of = [](const uint16_t* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p), (short)0, 0x7fffffff, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rsA = rsrc_of(d.A16), rsB = rsrc_of(d.B16);
+
+  // per-unit fixed byte offset (rows clamped once), LDS element offset and k offset within the tile
+  unsigned voA[UA], voB[UB];
+  int ldsA[UA], ldsB[UB], kuA[UA], kuB[UB];
+  auto init = [&](auto KC_, auto ROWS_, unsigned* vo, int* lo, int* ku, int64_t ld, int64_t rows, int64_t r0) {
+    constexpr bool KC = decltype(KC_)::value;
+    constexpr int ROWS = decltype(ROWS_)::value;
+    constexpr int U = ROWS * 8 / NT;
+    using I = H16Img<KC, ROWS>;
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      const int u = tid + i * NT;
+      if (KC) {   // row u / 8, k chunk u % 8
+        const int row = u >> 3, kc = u & 7;
+        const int64_t r = r0 + row < rows ? r0 + row : rows - 1;
+        vo[i] = (unsigned)((r * ld + kc * 8) * 2);
+        lo[i] = row * I::P + kc * 8;
+        ku[i] = kc * 8;
+      } else {    // k u / (ROWS / 8), row chunk u % (ROWS / 8)
+        const int k = u / (ROWS / 8), rc = u % (ROWS / 8);
+        const int64_t c = r0 + rc * 8 < rows ? r0 + rc * 8 : rows - 8;
+        vo[i] = (unsigned)((k * ld + c) * 2);
+        lo[i] = k * I::P + rc * 8;
+        ku[i] = k;
+      }
+    }
+  };
+  init(std::integral_constant<bool, AKC>{}, std::integral_constant<int, BM>{}, voA, ldsA, kuA, d.lda, d.M, m0);
+  init(std::integral_constant<bool, BKC>{}, std::integral_constant<int, BN>{}, voB, ldsB, kuB, d.ldb, d.N, n0);
+
+  u32x4 ra[UA], rb[UB];
+  auto load_tile = [&](int64_t k0) {
+    // k-contiguous: k advances along the row (+2 B per k); row-contiguous: a k row is ld elements
+    const int64_t kc0 = k0 < ke ? k0 : 0;
+#pragma unroll
+    for (int i = 0; i < UA; ++i) {
+      const bool ok = kc0 + kuA[i] < ke;
+      const int64_t kk = ok ? kc0 : 0;   // clamped: an invalid unit re-reads a valid one, zeroed at store
+      const int soff = AKC ? (int)(kk * 2) : (int)(kk * d.lda * 2);
+      ra[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)voA[i], soff, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < UB; ++i) {
+      const bool ok = kc0 + kuB[i] < ke;
+      const int64_t kk = ok ? kc0 : 0;
+      const int soff = BKC ? (int)(kk * 2) : (int)(kk * d.ldb * 2);
+      rb[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsB, (int)voB[i], soff, 0));
+    }
+  };
+  auto store_tile = [&](int buf, int64_t k0) {
+    unsigned short* As = smem + buf * STAGE;
+    unsigned short* Bs = As + IA::ELEMS;
+    const bool tail = k0 + BK > ke;   // uniform
+#pragma unroll
+    for (int i = 0; i < UA; ++i) {
+      const u32x4 v = (tail && k0 + kuA[i] >= ke) ? u32x4{0u, 0u, 0u, 0u} : ra[i];
+      *reinterpret_cast<u32x4*>(As + ldsA[i]) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < UB; ++i) {
+      const u32x4 v = (tail && k0 + kuB[i] >= ke) ? u32x4{0u, 0u, 0u, 0u} : rb[i];
+      *reinterpret_cast<u32x4*>(Bs + ldsB[i]) = v;
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int64_t nk = ke > kb0 ? (ke - kb0 + BK - 1) / BK : 0;
+  if (nk > 0) {
+    load_tile(kb0);
+    store_tile(0, kb0);
+  }
+  __syncthreads();
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    const int cur = (int)(kt & 1);
+    if (kt + 1 < nk) load_tile(kb0 + (kt + 1) * BK);
+    const unsigned short* As = smem + cur * STAGE;
+    const unsigned short* Bs = As + IA::ELEMS;
+    u32x4 fa[2][TM], fb[2][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[0][i] = IA::frag(As, wm0 + i * 32, 0, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[0][j] = IB::frag(Bs, wn0 + j * 32, 0, lane);
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int c = ks & 1;
+      if (ks + 1 < BK / 16) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[c ^ 1][i] = IA::frag(As, wm0 + i * 32, 16 * (ks + 1), lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[c ^ 1][j] = IB::frag(Bs, wn0 + j * 32, 16 * (ks + 1), lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = Ops::mma(__builtin_bit_cast(e8, fa[c][i]), __builtin_bit_cast(e8, fb[c][j]), acc[i][j]);
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 1 < nk) store_tile(cur ^ 1, kb0 + (kt + 1) * BK);
+    __syncthreads();
+  }
+  store_acc<TM, TN>(ka, acc, split, m0, n0, wm0, wn0, lane, 0);
+}
+
 // Sums the split-K slabs in split order and applies the GEMM epilogue.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmDesc d, const float* __restrict__ partial, int splits) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -829,6 +1002,27 @@ int launch_lp(const GemmDesc& d, hipStream_t s, bool vec, bool f16) {
   }
 }
 
+template <bool TA, bool TB, int BM, int BN, int NW>
+int launch_h16_cfg(const GemmDesc& d, hipStream_t s, bool f16) {
+  constexpr int per_cu = h16_per_cu<TA, TB, BM, BN>();
+  KernelArgs ka;
+  int splits = 1;
+  if (int rc = plan_launch(d, BM, BN, kLpBK, per_cu, ka, &splits)) return rc;
+  ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K);
+  const dim3 grid((unsigned)ka.nblk), block(NW * 64);
+  if (f16) hipLaunchKernelGGL((gemm_h16_kernel<TA, TB, BM, BN, NW, true>), grid, block, 0, s, ka);
+  else hipLaunchKernelGGL((gemm_h16_kernel<TA, TB, BM, BN, NW, false>), grid, block, 0, s, ka);
+  return finish_splits(d, ka, splits, s);
+}
+
+template <bool TA, bool TB>
+int launch_h16(const GemmDesc& d, hipStream_t s, bool f16) {
+  static const int cfg_env = env_int("SRK_H16_CFG", 0);
+  const int cfg = cfg_env ? cfg_env : (d.M >= 1024 && !(!TA && TB) ? 3 : 1);
+  if (cfg == 3) return launch_h16_cfg<TA, TB, 256, 128, 8>(d, s, f16);
+  return launch_h16_cfg<TA, TB, 128, 128, 4>(d, s, f16);
+}
+
 template <bool TA, bool TB>
 int dispatch_tile(const GemmDesc& d, hipStream_t s, bool vec) {
   const int prec = d.prec >= 0 ? d.prec : matmul_prec();
@@ -849,6 +1043,23 @@ int dispatch_tile(const GemmDesc& d, hipStream_t s, bool vec) {
 int gemm_f32(const GemmDesc& d, hipStream_t s) {
   SRK_REQUIRE(d.M >= 0 && d.N >= 0 && d.K >= 0 && d.batch >= 1, SRK_ERR_INVALID, "gemm: bad shape");
   if (d.M == 0 || d.N == 0) return SRK_OK;
+  if (d.A16 || d.B16) {   // 16-bit operands in memory
+    const int prec = d.prec >= 0 ? d.prec : matmul_prec();
+    SRK_REQUIRE(d.A16 && d.B16 && d.C && prec != kPrecF32 && d.batch == 1 && !d.rowsum, SRK_ERR_INVALID,
+                "gemm: 16-bit operands need both A16 / B16, a 16-bit precision, batch 1 and no row sums");
+    const double ext_a = (double)(d.ta ? d.K : d.M) * d.lda * 2, ext_b = (double)(d.tb ? d.N : d.K) * d.ldb * 2;
+    SRK_REQUIRE((uintptr_t)d.A16 % 16 == 0 && (uintptr_t)d.B16 % 16 == 0 && d.lda % 8 == 0 && d.ldb % 8 == 0 &&
+                    ((d.ta && d.M % 8 == 0) || (!d.ta && d.K % 8 == 0)) &&
+                    ((d.tb && d.K % 8 == 0) || (!d.tb && d.N % 8 == 0)) && ext_a < 2147483648.0 &&
+                    ext_b < 2147483648.0,
+                SRK_ERR_INVALID, "gemm: 16-bit operands need 16-B aligned rows of 8-element multiples");
+    SRK_REQUIRE(d.K > 0, SRK_ERR_INVALID, "gemm: 16-bit operands need K > 0");
+    const bool f16 = prec == kPrecF16;
+    if (!d.ta && !d.tb) return launch_h16<false, false>(d, s, f16);
+    if (!d.ta && d.tb) return launch_h16<false, true>(d, s, f16);
+    if (d.ta && !d.tb) return launch_h16<true, false>(d, s, f16);
+    return launch_h16<true, true>(d, s, f16);
+  }
   SRK_REQUIRE(d.C && (d.K == 0 || (d.A && d.B)), SRK_ERR_INVALID, "gemm: null operand");
   SRK_REQUIRE(d.bias_mode == 0 || d.bias, SRK_ERR_INVALID, "gemm: bias_mode without bias");
   SRK_REQUIRE(!d.rowsum || d.batch == 1, SRK_ERR_INVALID, "gemm: rowsum needs batch == 1");
@@ -924,5 +1135,21 @@ extern "C" int srk_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx,
   SRK_API_BEGIN
   SRK_REQUIRE(M >= 0 && N >= 0 && (N == 0 || (X && out)), SRK_ERR_INVALID, "colsum: bad args");
   return srk::colsum_f32(X, M, N, ldx, out, beta, srk::as_stream(stream));
+  SRK_API_END
+}
+
+extern "C" int srk_gemm_16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha, const uint16_t* A,
+                           int64_t lda, const uint16_t* B, int64_t ldb, float beta, float* C, int64_t ldc,
+                           const float* bias, int bias_mode, void* stream) {
+  SRK_API_BEGIN
+  srk::GemmDesc d;
+  d.M = M; d.N = N; d.K = K;
+  d.A16 = A; d.lda = lda; d.ta = trans_a != 0;
+  d.B16 = B; d.ldb = ldb; d.tb = trans_b != 0;
+  d.C = C; d.ldc = ldc; d.alpha = alpha; d.beta = beta;
+  d.bias = bias; d.bias_mode = bias_mode;
+  SRK_REQUIRE(bias_mode >= 0 && bias_mode <= 2, SRK_ERR_INVALID, "gemm: bias_mode must be 0, 1 or 2");
+  SRK_REQUIRE(srk::matmul_prec() != srk::kPrecF32, SRK_ERR_INVALID, "gemm_16: set matmul_precision to bf16 / fp16");
+  return srk::gemm_f32(d, srk::as_stream(stream));
   SRK_API_END
 }

@@ -295,6 +295,86 @@ int check_dims(int64_t B, int64_t T, int64_t in, int64_t H) {
   return SRK_OK;
 }
 
+// Input widths that are not a multiple of 4 (the 39 MFCC features of model_mfcc_bgru.py:25):
+// the input-projection GEMMs run on a copy of x / W_ih padded with zero columns to a multiple of
+// 4, so they take the 16-B vector (and LDS-DMA / buffer-load) paths; a zero column adds exact
+// zeros to every dot product.  dW_ih is produced at the padded width and its first `in` columns
+// are written (or added) into the caller's tensor.
+__global__ void pad_cols_kernel(const float* __restrict__ src, int64_t rows, int cols, float* __restrict__ dst,
+                                int colsp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * colsp) return;
+  const int64_t r = i / colsp;
+  const int c = (int)(i - r * colsp);
+  dst[i] = c < cols ? src[r * cols + c] : 0.f;
+}
+__global__ void unpad_cols_kernel(const float* __restrict__ src, int64_t rows, int colsp, float* __restrict__ dst,
+                                  int cols, int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * cols) return;
+  const int64_t r = i / cols;
+  const int c = (int)(i - r * cols);
+  const float v = src[r * colsp + c];
+  dst[i] = accumulate ? dst[i] + v : v;
+}
+// bf16 / fp16 mode: fp32 [rows][cols] -> 16-bit [rows][colsp] (zero columns past cols), rounded to
+// nearest-even — the GEMM operands of the layer that are not produced by the recurrence kernels.
+template <bool F16>
+__global__ void to16_kernel(const float* __restrict__ src, int64_t rows, int cols, uint16_t* __restrict__ dst,
+                            int colsp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * colsp) return;
+  const int64_t r = i / colsp;
+  const int c = (int)(i - r * colsp);
+  const float v = c < cols ? src[r * cols + c] : 0.f;
+  if (F16) {
+    const _Float16 h = (_Float16)v;
+    dst[i] = __builtin_bit_cast(uint16_t, h);
+  } else {
+    const __bf16 h = (__bf16)v;
+    dst[i] = __builtin_bit_cast(uint16_t, h);
+  }
+}
+int to16(const float* src, int64_t rows, int64_t cols, uint16_t* dst, int64_t colsp, hipStream_t s) {
+  const int64_t n = rows * colsp;
+  if (matmul_prec() == kPrecF16)
+    hipLaunchKernelGGL(to16_kernel<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, rows, (int)cols,
+                       dst, (int)colsp);
+  else
+    hipLaunchKernelGGL(to16_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, rows, (int)cols,
+                       dst, (int)colsp);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+}
+// Bias gradients from the 16-bit backward kernel's partials [part][2 dir][4][H] (sums of dar, daz,
+// dan, dan * r), summed over the valid (chunk, group) parts in order: db_ih = (dar, daz, dan),
+// db_hh = (dar, daz, dan * r); `accumulate` adds into the caller's tensors.
+__global__ void dbias_reduce_kernel(const float* __restrict__ part, int nparts, int B, int H, float* __restrict__ db_ih,
+                                    float* __restrict__ db_hh, int accumulate) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over [2 dir][3][H]
+  if (i >= 2 * 3 * H) return;
+  const int dir = i / (3 * H), g = (i / H) % 3, j = i % H;
+  float si = 0.f, sh = 0.f;
+  for (int p = 0; p < nparts; ++p) {
+    if ((p / 4) * 256 + (p % 4) * 64 >= B) continue;   // (chunk, group) without rows
+    const float* q = part + ((size_t)p * 2 + dir) * 4 * H;
+    si += q[g * H + j];
+    sh += q[(g == 2 ? 3 : g) * H + j];
+  }
+  db_ih[i] = accumulate ? db_ih[i] + si : si;
+  db_hh[i] = accumulate ? db_hh[i] + sh : sh;
+}
+
+inline int64_t pad4(int64_t v) { return (v + 3) / 4 * 4; }
+inline bool padded_in(int64_t in) { return in % 4 != 0; }
+int pad_cols(const float* src, int64_t rows, int64_t cols, float* dst, hipStream_t s) {
+  const int64_t n = rows * pad4(cols);
+  hipLaunchKernelGGL(pad_cols_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, rows, (int)cols, dst,
+                     (int)pad4(cols));
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+}
+
 }  // namespace
 }  // namespace srk
 
@@ -315,9 +395,43 @@ static int64_t xbuf_rows(int64_t B) { return std::min<int64_t>((B + 63) / 64 * 6
 static int64_t fwd_counter_off(int64_t B, int64_t T, int64_t H) { return fwd_xbuf_off(B, T, H) + 4 * xbuf_rows(B) * H; }
 static int64_t bwd_counter_off(int64_t B, int64_t T, int64_t H) { return bwd_xbuf_off(B, T, H) + 12 * xbuf_rows(B) * H; }
 
+// After the counters, for an input width that is not a multiple of 4 (srk::padded_in):
+//   fwd: x padded [B*T][in4] (kept for the backward's dW_ih) | W_ih padded [6H][in4]
+//   bwd: W_ih padded [6H][in4] | dW_ih padded [6H][in4] | dx padded [B*T][in4]
+static int64_t pad_off(int64_t B, int64_t T, int64_t H, int backward) {
+  return ((backward ? bwd_counter_off(B, T, H) : fwd_counter_off(B, T, H)) + srk::kCounterFloats + 63) / 64 * 64;
+}
+
+// Then the bf16 / fp16 ("h16") region, used when the 16-bit persistent kernels run (use_h16):
+//   fwd: x16 [B*T][in8] | W_ih16 [6H][in8] | y16 [B*T][2H]          (16-bit, kept for the backward)
+//   bwd: bias partials [4 * chunks][2][4][H] | dW_ih [6H][in8] | dx [B*T][in8]   (fp32; the last two
+//        only when in8 != in); dgi16 / dgh16 alias the fp32 dgi region (unused in this mode).
+static int64_t pad_end(int64_t B, int64_t T, int64_t in, int64_t H, int backward) {
+  int64_t e = pad_off(B, T, H, backward) + 64;
+  if (srk::padded_in(in)) {
+    const int64_t in4 = srk::pad4(in);
+    e += (backward ? 2 * 6 * H * in4 + B * T * in4 : B * T * in4 + 6 * H * in4) + 64;
+  }
+  return (e + 63) / 64 * 64;
+}
+static int64_t up64(int64_t v) { return (v + 63) / 64 * 64; }
+static int64_t in8_of(int64_t in) { return (in + 7) / 8 * 8; }
+static int64_t h16_floats(int64_t B, int64_t T, int64_t in, int64_t H, int backward) {
+  const int64_t in8 = in8_of(in), BT = B * T;
+  if (!backward) return up64(BT * in8 / 2 + 1) + up64(6 * H * in8 / 2 + 1) + up64(BT * 2 * H / 2 + 1);
+  const int64_t chunks = (B + 255) / 256;
+  return up64(chunks * 4 * 2 * 4 * H) + (in8 != in ? up64(6 * H * in8) + up64(BT * in8) : 0);
+}
+// The 16-bit path: a 16-bit precision, the persistent kernels (both directions of the layer), and
+// 32-bit byte offsets for the 16-bit GEMM operands.
+static bool use_h16(int64_t B, int64_t T, int64_t in, int64_t H) {
+  return srk::matmul_prec() != srk::kPrecF32 && srk::g_opt_gru_persistent &&
+         srk::gru_persistent_supported(B, T, H, false) && srk::gru_persistent_supported(B, T, H, true) &&
+         (double)B * T * 6 * H * 2 < 2147483647.0 && (double)B * T * in8_of(in) * 2 < 2147483647.0;
+}
+
 int64_t srk_gru_workspace_floats(int64_t B, int64_t T, int64_t in, int64_t H, int backward) {
-  (void)in;
-  return (backward ? bwd_counter_off(B, T, H) : fwd_counter_off(B, T, H)) + srk::kCounterFloats + 64;
+  return pad_end(B, T, in, H, backward) + (H == 512 ? h16_floats(B, T, in, H, backward) + 64 : 0);
 }
 
 int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t H, const float* w_ih,
@@ -328,10 +442,44 @@ int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
   hipStream_t s = srk::as_stream(stream);
   float* gi = ws;
   float* gates = ws + B * T * 6 * H;
+  uint16_t* y16 = nullptr;
+  if (use_h16(B, T, in, H)) {   // 16-bit operands in memory: x, W_ih rounded once, h written by the kernel
+    const int64_t in8 = in8_of(in), BT = B * T;
+    uint16_t* x16 = reinterpret_cast<uint16_t*>(ws + pad_end(B, T, in, H, 0));
+    uint16_t* w16 = x16 + 2 * up64(BT * in8 / 2 + 1);
+    y16 = w16 + 2 * up64(6 * H * in8 / 2 + 1);
+    if (int rc = srk::to16(x, BT, in, x16, in8, s)) return rc;
+    if (int rc = srk::to16(w_ih, 6 * H, in, w16, in8, s)) return rc;
+    GemmDesc g;   // gi[B*T, 6H] = x16 * W16^T + b_ih
+    g.M = BT; g.N = 6 * H; g.K = in8;
+    g.A16 = x16; g.lda = in8;
+    g.B16 = w16; g.ldb = in8; g.tb = true;
+    g.C = gi; g.ldc = 6 * H;
+    g.bias = b_ih; g.bias_mode = 1;
+    if (int rc = srk::gemm_f32(g, s)) return rc;
+    srk::GruPArgs p{};
+    p.B = (int)B; p.T = (int)T; p.H = (int)H;
+    p.gi = gi; p.w_hh = w_hh; p.b_hh = b_hh; p.y = y; p.gates = gates; p.y16 = y16;
+    p.xbuf = ws + fwd_xbuf_off(B, T, H);
+    p.counters = reinterpret_cast<unsigned*>(ws + fwd_counter_off(B, T, H));
+    return srk::gru_persistent_launch(p, false, s);
+  }
+  const float* xa = x;
+  const float* wa = w_ih;
+  int64_t ink = in;
+  if (srk::padded_in(in)) {   // zero-pad the input width to a multiple of 4 (vector GEMM paths)
+    ink = srk::pad4(in);
+    float* xp = ws + pad_off(B, T, H, 0);
+    float* wp = xp + B * T * ink;
+    if (int rc = srk::pad_cols(x, B * T, in, xp, s)) return rc;
+    if (int rc = srk::pad_cols(w_ih, 6 * H, in, wp, s)) return rc;
+    xa = xp;
+    wa = wp;
+  }
   GemmDesc g;   // gi[B*T, 6H] = x[B*T, in] * W_ih_cat[6H, in]^T + b_ih_cat
-  g.M = B * T; g.N = 6 * H; g.K = in;
-  g.A = x; g.lda = in;
-  g.B = w_ih; g.ldb = in; g.tb = true;
+  g.M = B * T; g.N = 6 * H; g.K = ink;
+  g.A = xa; g.lda = ink;
+  g.B = wa; g.ldb = ink; g.tb = true;
   g.C = gi; g.ldc = 6 * H;
   g.bias = b_ih; g.bias_mode = 1;
   if (int rc = srk::gemm_f32(g, s)) return rc;
@@ -368,6 +516,75 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
               "gru_bwd: null pointer");
   hipStream_t s = srk::as_stream(stream);
   const int64_t BT = B * T;
+  if (use_h16(B, T, in, H)) {
+    // 16-bit path: the kernel writes dgi16 / dgh16 (aliasing the fp32 dgi region) and the bias-
+    // gradient partials; every GEMM reads 16-bit operands (x16 / W16 / y16 from the forward).
+    const int64_t in8 = in8_of(in);
+    const uint16_t* x16 = reinterpret_cast<const uint16_t*>(ws_fwd + pad_end(B, T, in, H, 0));
+    const uint16_t* w16 = x16 + 2 * up64(BT * in8 / 2 + 1);
+    const uint16_t* y16 = w16 + 2 * up64(6 * H * in8 / 2 + 1);
+    uint16_t* dgi16 = reinterpret_cast<uint16_t*>(ws);
+    uint16_t* dgh16 = dgi16 + BT * 6 * H;
+    float* part = ws + pad_end(B, T, in, H, 1);
+    const int64_t chunks = (B + 255) / 256;
+    float* dwpad = part + up64(chunks * 4 * 2 * 4 * H);
+    float* dxpad = dwpad + up64(6 * H * in8);
+    srk::GruPArgs p{};
+    p.B = (int)B; p.T = (int)T; p.H = (int)H;
+    p.w_hh = w_hh; p.y_in = y; p.gates = const_cast<float*>(ws_fwd + BT * 6 * H); p.dy = dy;
+    p.dgi16 = dgi16; p.dgh16 = dgh16; p.dbias = part;
+    p.xbuf = ws + bwd_xbuf_off(B, T, H);
+    p.counters = reinterpret_cast<unsigned*>(ws + bwd_counter_off(B, T, H));
+    int rc;
+    if ((rc = srk::gru_persistent_launch(p, true, s))) return rc;
+    hipLaunchKernelGGL(srk::dbias_reduce_kernel, dim3((unsigned)((6 * H + 255) / 256)), dim3(256), 0, s, part,
+                       (int)(chunks * 4), (int)B, (int)H, db_ih, db_hh, accumulate);
+    SRK_CHECK_HIP(hipGetLastError());
+    const float beta = accumulate ? 1.f : 0.f;
+    {  // dW_ih [6H, in] = dgi16^T x16
+      GemmDesc g;
+      g.M = 6 * H; g.N = in8; g.K = BT;
+      g.A16 = dgi16; g.lda = 6 * H; g.ta = true;
+      g.B16 = x16; g.ldb = in8;
+      g.C = in8 == in ? dw_ih : dwpad; g.ldc = in8; g.beta = in8 == in ? beta : 0.f;
+      if ((rc = srk::gemm_f32(g, s))) return rc;
+      if (in8 != in) {
+        const int64_t n = 6 * H * in;
+        hipLaunchKernelGGL(srk::unpad_cols_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dwpad, 6 * H,
+                           (int)in8, dw_ih, (int)in, (int)accumulate);
+        SRK_CHECK_HIP(hipGetLastError());
+      }
+    }
+    for (int dir = 0; dir < 2; ++dir) {   // dW_hh[dir] = dgh16[dir]^T h_prev16 (edge rows of dgh16 are zero)
+      const uint16_t* dg = dgh16 + (size_t)dir * BT * 3 * H;
+      GemmDesc g;
+      g.M = 3 * H; g.N = H; g.K = BT - 1;
+      g.ta = true; g.lda = 3 * H; g.ldb = 2 * H;
+      g.A16 = dir == 0 ? dg + 3 * H : dg;
+      g.B16 = dir == 0 ? y16 + dir * H : y16 + 2 * H + dir * H;
+      g.C = dw_hh + (size_t)dir * 3 * H * H; g.ldc = H; g.beta = beta;
+      if (g.K > 0) {
+        if ((rc = srk::gemm_f32(g, s))) return rc;
+      } else if (!accumulate) {
+        SRK_CHECK_HIP(hipMemsetAsync(g.C, 0, sizeof(float) * 3 * H * H, s));
+      }
+    }
+    if (dx) {   // dx [BT, in] = dgi16 W16
+      GemmDesc g;
+      g.M = BT; g.N = in8; g.K = 6 * H;
+      g.A16 = dgi16; g.lda = 6 * H;
+      g.B16 = w16; g.ldb = in8;
+      g.C = in8 == in ? dx : dxpad; g.ldc = in8;
+      if ((rc = srk::gemm_f32(g, s))) return rc;
+      if (in8 != in) {
+        const int64_t n = BT * in;
+        hipLaunchKernelGGL(srk::unpad_cols_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dxpad, BT,
+                           (int)in8, dx, (int)in, 0);
+        SRK_CHECK_HIP(hipGetLastError());
+      }
+    }
+    return SRK_OK;
+  }
   float* dgi = ws;
   float* dgh = dgi + BT * 6 * H;
   float* dgh_edge = dgh + 2 * BT * 3 * H;
@@ -396,14 +613,25 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
 
   int rc;
   const float beta = accumulate ? 1.f : 0.f;   // autograd .grad accumulation in the GEMM epilogues
+  const bool pad = srk::padded_in(in);
+  const int64_t in4 = srk::pad4(in);
+  float* wpad = pad ? ws + pad_off(B, T, H, 1) : nullptr;   // [6H][in4]
+  float* dwpad = pad ? wpad + 6 * H * in4 : nullptr;         // [6H][in4]
+  float* dxpad = pad ? dwpad + 6 * H * in4 : nullptr;        // [BT][in4]
   {  // dW_ih_cat[6H, in] = dgi^T [6H, BT] * x [BT, in]; db_ih fused as the row sums of dgi^T
     GemmDesc g;
-    g.M = 6 * H; g.N = in; g.K = BT;
+    g.M = 6 * H; g.N = pad ? in4 : in; g.K = BT;
     g.A = dgi; g.lda = 6 * H; g.ta = true;
-    g.B = x; g.ldb = in;
-    g.C = dw_ih; g.ldc = in; g.beta = beta;
+    g.B = pad ? ws_fwd + pad_off(B, T, H, 0) : x; g.ldb = pad ? in4 : in;   // the forward's padded x
+    g.C = pad ? dwpad : dw_ih; g.ldc = pad ? in4 : in; g.beta = pad ? 0.f : beta;
     g.rowsum = db_ih; g.rowsum_beta = beta;
     if ((rc = srk::gemm_f32(g, s))) return rc;
+    if (pad) {
+      const int64_t n = 6 * H * in;
+      hipLaunchKernelGGL(srk::unpad_cols_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dwpad, 6 * H,
+                         (int)in4, dw_ih, (int)in, (int)accumulate);
+      SRK_CHECK_HIP(hipGetLastError());
+    }
   }
   for (int dir = 0; dir < 2; ++dir) {
     // dW_hh[dir][3H, H] = sum_(b,t) dgh[b][t]^T h_prev[b][t]; h_prev of row (b,t) is y row (b,t-1)
@@ -428,11 +656,18 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
   }
   if (dx) {  // dx[BT, in] = dgi[BT, 6H] * W_ih_cat[6H, in]
     GemmDesc g;
-    g.M = BT; g.N = in; g.K = 6 * H;
+    g.M = BT; g.N = pad ? in4 : in; g.K = 6 * H;
     g.A = dgi; g.lda = 6 * H;
-    g.B = w_ih; g.ldb = in;
-    g.C = dx; g.ldc = in;
+    if (pad && (rc = srk::pad_cols(w_ih, 6 * H, in, wpad, s))) return rc;
+    g.B = pad ? wpad : w_ih; g.ldb = pad ? in4 : in;
+    g.C = pad ? dxpad : dx; g.ldc = pad ? in4 : in;
     if ((rc = srk::gemm_f32(g, s))) return rc;
+    if (pad) {
+      const int64_t n = BT * in;
+      hipLaunchKernelGGL(srk::unpad_cols_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dxpad, BT,
+                         (int)in4, dx, (int)in, 0);
+      SRK_CHECK_HIP(hipGetLastError());
+    }
   }
   return SRK_OK;
   SRK_API_END

@@ -27,6 +27,14 @@ struct GruPArgs {
   float* dgh_edge;       // bwd: [2][B][3H]
   float* xbuf;           // hand-off ping-pong: fwd h [2 dir][2][B][H], bwd dg [2 dir][2][B][3H]
   unsigned* counters;    // kCounterFloats words
+  int flags;             // 1: per-producer step flags [2][G][32] (sc1 stores) instead of arrival counters
+  // 16-bit operand outputs of the bf16 / fp16 kernels (nullptr = off), for the GEMMs of the layer:
+  uint16_t* y16;         // fwd: h [B][T][2H] rounded to 16 bit
+  uint16_t* dgi16;       // bwd: dgi [B*T][6H] (replaces the fp32 dgi)
+  uint16_t* dgh16;       // bwd: dgh [2][B][T][3H], edge rows zero (replaces dgh / dgh_edge)
+  float* dbias;          // bwd with dgi16: bias-gradient partials [chunk * G + group][2 dir][4][H]
+                         //   (sum over t and the group's rows of dar, daz, dan, dan * r)
+  int chunk;             // index of this launch's 64*G-row batch chunk
   unsigned long long* trace;   // optional per-(workgroup, step) timestamps (tools/gru_trace.py)
 };
 

@@ -27,6 +27,8 @@
 // Every spin is bounded: a workgroup that waits ~2 s gives up, bumps g_spin_timeouts (read by
 // srk_spin_timeouts(); the tests assert it stays 0) and carries on, so a fault can never hang the
 // GPU.
+#include <cstdlib>
+#include <type_traits>
 #include <mutex>
 
 #include "gru_internal.h"
@@ -81,6 +83,44 @@ __device__ __forceinline__ void arrive(unsigned* cnt) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Per-producer flags (a.flags): producer (dir, group, slice) stores step + 1 into ITS word of
+// [2][G][32] after every storing wave drained (one lane, behind the workgroup barrier: an sc1
+// store); the consumer's wave 0 polls all S words of its (dir, group) at once (lane i <-> slice i,
+// sc1 loads) until every one is >= step, then the workgroup meets.  MI355X_MICROARCH.md "Valid
+// forms" row 1 (a sharded flag, every shard polled).  Replaces the atomic add at the memory side.
+__device__ __forceinline__ void sync_wait(const GruPArgs& a, unsigned* cnt, int dir, int group, int S, int step) {
+  if (!a.flags) {
+    wait_count(cnt, (unsigned)S * step);
+    return;
+  }
+  if (threadIdx.x < 64) {
+    unsigned* f = a.counters + (dir * a.G + group) * 32;
+    const int lane = threadIdx.x;
+    unsigned spins = 0;
+    while (true) {
+      const unsigned v = lane < S ? __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xffffffffu;
+      if (__all(v >= (unsigned)step)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins >= kSpinLimit) {
+        if (lane == 0) atomicAdd(&g_spin_timeouts, 1ull);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ void sync_arrive(const GruPArgs& a, unsigned* cnt, int dir, int group, int slice, int step) {
+  if (!a.flags) {
+    arrive(cnt);
+    return;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(a.counters + (dir * a.G + group) * 32 + slice, (unsigned)(step + 1), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Diagnostics (tools/gru_trace.py): thread 0 stamps s_memrealtime (100 MHz) at step start (0), after
@@ -185,7 +225,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
 #pragma unroll
     for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (step > 0) {
-      wait_count(cnt, (unsigned)(H / kUnits) * step);
+      sync_wait(a, cnt, dir, group, H / kUnits, step);
       stamp(a, step, 1);
       // h_{t-1}[row 16 wave + lr][k], k = 16 kb + 4 lq + s  (k-permuted: one b128 feeds 4 MFMAs)
       // fragment chunk (group, row block = wave, k block) of the previous step's buffer; lane = lane
@@ -254,7 +294,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
         st4_sc1(rx, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (yrl >> 4)) * NKB * 64 + slice * 64 +
                                 (yuq >> 2) * 16 + (yrl & 15)) * 16), hv4);
     }
-    arrive(cnt);   // waits for the hand-off stores only: y and the gates go out after it (no consumer in this launch)
+    sync_arrive(a, cnt, dir, group, slice, step);   // waits for the hand-off stores only: y and the gates go out after it (no consumer in this launch)
     stamp(a, step, 4);
     if (b0 + yrl <= b_last) st4(a.y + ((size_t)(b0 + yrl) * T + t) * 2 * H + dir * H + j0 + yuq, hv4);
     store_gates(a, gsv, dir, t, b0 + wave * 16 + lq * 4, b_last, j);
@@ -319,7 +359,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
     }
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     if (step > 0) {
-      wait_count(cnt, (unsigned)(H / kUnits) * step);
+      sync_wait(a, cnt, dir, group, H / kUnits, step);
       stamp(a, step, 1);
       const unsigned base = (unsigned)(((((size_t)((step - 1) & 1) * Gp + group) * 4 + wave) * NKB * 64 + lane) * 16);
       // k rotation per slice (see the forward kernel): block index kr(i) = (i + rot) mod NKB
@@ -389,7 +429,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
       st4_sc1(rg_, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB * 64 +
                                (g * (H / 16) + slice) * 64 + (uq >> 2) * 16 + (rl & 15)) * 16), val[i]);
     }
-    arrive(cnt);
+    sync_arrive(a, cnt, dir, group, slice, step);
     stamp(a, step, 4);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -493,7 +533,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
 #pragma unroll
     for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (step > 0) {
-      wait_count(cnt, (unsigned)(H / kUnits) * step);
+      sync_wait(a, cnt, dir, group, H / kUnits, step);
       stamp(a, step, 1);
       const unsigned base = (unsigned)(((((size_t)((step - 1) & 1) * Gp + group) * 4 + wave) * NKB * 64 + lane) * 16);
       const int rot = slice % NKB;   // per-slice k rotation, see the fp32 kernel
@@ -551,9 +591,17 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
                 __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))));
       }
     }
-    arrive(cnt);   // the hand-off only: y and the gates go out after it
+    sync_arrive(a, cnt, dir, group, slice, step);   // the hand-off only: y and the gates go out after it
     stamp(a, step, 4);
-    if (b0 + yrl <= b_last) st4(a.y + ((size_t)(b0 + yrl) * T + t) * 2 * H + dir * H + j0 + yuq, yv);
+    if (b0 + yrl <= b_last) {
+      st4(a.y + ((size_t)(b0 + yrl) * T + t) * 2 * H + dir * H + j0 + yuq, yv);
+      if (a.y16) {   // the layer's 16-bit copy of h for its weight-gradient GEMM (4 units = 8 B)
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        typedef __attribute__((ext_vector_type(4))) typename std::conditional<F16, _Float16, __bf16>::type e4;
+        *reinterpret_cast<u32x2*>(a.y16 + ((size_t)(b0 + yrl) * T + t) * 2 * H + dir * H + j0 + yuq) =
+            __builtin_bit_cast(u32x2, __builtin_convertvector(yv, e4));
+      }
+    }
     store_gates(a, gsv, dir, t, b0 + wave * 16 + lq * 4, b_last, j);
   }
 }
@@ -595,6 +643,9 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
   const __amdgpu_buffer_rsrc_t rg_ = rsrc(a.xbuf + (size_t)dir * 2 * Gp * 64 * 3 * H);   // 16-bit [2][Gp][4][3H/32][64][8]
   float dhz[4] = {0.f, 0.f, 0.f, 0.f};
   float dgv[4][3];
+  const bool h16 = a.dgi16 != nullptr;   // 16-bit dgi / dgh outputs + in-kernel bias gradients
+  float* dI = dT + 64 * 3 * DTP;         // [64][DTP]: dan (dgi's third gate; dT holds dan * r there)
+  float sb[4] = {0.f, 0.f, 0.f, 0.f};    // sums of dar, daz, dan, dan * r over t and the lane's rows
 
   for (int step = 0; step < T; ++step) {
     const int t = dir == 0 ? T - 1 - step : step;
@@ -615,7 +666,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
     }
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     if (step > 0) {
-      wait_count(cnt, (unsigned)(H / kUnits) * step);
+      sync_wait(a, cnt, dir, group, H / kUnits, step);
       stamp(a, step, 1);
       const unsigned base = (unsigned)(((((size_t)((step - 1) & 1) * Gp + group) * 4 + wave) * NKB * 64 + lane) * 16);
       const int rot = (slice * (NKB / (H / kUnits))) % NKB;
@@ -665,6 +716,15 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
       dgv[r][0] = dar;
       dgv[r][1] = daz;
       dgv[r][2] = dan;
+      if (h16) {
+        dI[rl * DTP + lr] = dan;
+        if (b <= b_last) {
+          sb[0] += dar;
+          sb[1] += daz;
+          sb[2] += dan;
+          sb[3] += dan * rg;
+        }
+      }
     }
     __syncthreads();
     stamp(a, step, 3);
@@ -685,8 +745,23 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
                 __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))));
       }
     }
-    arrive(cnt);   // the hand-off only: dgh, dgh_edge and dgi go out after it
+    sync_arrive(a, cnt, dir, group, slice, step);   // the hand-off only: dgh, dgh_edge and dgi go out after it
     stamp(a, step, 4);
+    if (h16) {   // 16-bit dgh (edge rows zero) and dgi: (row, gate, 8 units) = one 16-B store each
+      for (int v = tid; v < 64 * 3 * 2 * 2; v += 256) {
+        const int which = v / 384, w = v % 384, rl = w / 6, g = (w % 6) >> 1, half = w & 1, b = b0 + rl;
+        if (b > b_last) continue;
+        const float* src = which == 0 || g < 2 ? dT + (rl * 3 + g) * DTP + 8 * half : dI + rl * DTP + 8 * half;
+        v4f pk = __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4))));
+        if (which == 0) {
+          if (edge) pk = v4f{0.f, 0.f, 0.f, 0.f};
+          *reinterpret_cast<v4f*>(a.dgh16 + (((size_t)dir * B + b) * T + t) * 3 * H + g * H + j0 + 8 * half) = pk;
+        } else {
+          *reinterpret_cast<v4f*>(a.dgi16 + ((size_t)b * T + t) * 6 * H + dir * 3 * H + g * H + j0 + 8 * half) = pk;
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int v = tid + i * 256, rl = v / 12, g = (v % 12) / 4, uq = (v % 4) * 4, b = b0 + rl;
@@ -700,11 +775,30 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
     }
     store_dgi(a, dgv, dir, t, b0 + wave * 16 + lq * 4, b_last, j);
   }
+  if (h16) {   // bias-gradient partials: lanes lr, lr + 16, lr + 32, lr + 48, then the 4 waves in order
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      sb[q] += __shfl_xor(sb[q], 16);
+      sb[q] += __shfl_xor(sb[q], 32);
+    }
+    __syncthreads();
+    if (lq == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dT[(wave * 4 + q) * 16 + lr] = sb[q];
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const int q = tid >> 4, u = tid & 15;
+      const float v = ((dT[(0 * 4 + q) * 16 + u] + dT[(1 * 4 + q) * 16 + u]) + dT[(2 * 4 + q) * 16 + u]) +
+                      dT[(3 * 4 + q) * 16 + u];
+      a.dbias[(((size_t)(a.chunk * 4 + group) * 2 + dir) * 4 + q) * H + j0 + u] = v;
+    }
+  }
 }
 
 size_t lds_bytes(int H, bool backward, int prec) {
   if (prec == kPrecF32) return backward ? bwd_lds_bytes(H) : fwd_lds_bytes(H);
-  const size_t need = backward ? (size_t)kUnits * (3 * H + 16) * 2 + 64 * 3 * (kUnits + 4) * 4
+  const size_t need = backward ? (size_t)kUnits * (3 * H + 16) * 2 + 64 * 4 * (kUnits + 4) * 4
                                : (size_t)3 * kUnits * (H + 16) * 2 + 64 * (kUnits + 4) * 4;
   // the sc1 hand-off is the form measured at ONE workgroup per CU (MI355X_MICROARCH.md, "Valid
   // forms" row 1): reserve more than half of the 160 KB so a second workgroup never fits
@@ -774,9 +868,12 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
   for (int c0 = 0; c0 < a.B; c0 += rows_per_launch) {
     GruPArgs ac = a;
     ac.trace = g_opt_gru_trace;
+    static const int flags_env = [] { const char* v = getenv("SRK_GRU_FLAGS"); return v && *v ? atoi(v) : 0; }();
+    ac.flags = flags_env;
     ac.b_begin = c0;
     ac.b_end = std::min(a.B, c0 + rows_per_launch);
     ac.G = (ac.b_end - c0 + kRows - 1) / kRows;
+    ac.chunk = c0 / rows_per_launch;
     SRK_CHECK_HIP(hipMemsetAsync(ac.counters, 0, (size_t)kCounterFloats * 4, s));
     const dim3 grid((unsigned)(2 * ac.G * (a.H / kUnits)));
     const double flops = 2.0 * 2.0 * (double)(ac.b_end - c0) * 3 * a.H * a.H * (a.T - 1);

@@ -63,6 +63,7 @@ class _GRULayerFn(torch.autograd.Function):
         ctx.save_for_backward(x, w_ih, w_hh, y, ws)
         ctx.dims = (B, T, IN, H)
         ctx.params = (w_ih_f, w_ih_r, w_hh_f, w_hh_r, b_ih_f, b_ih_r, b_hh_f, b_hh_r)
+        ctx.prec = _lib.matmul_precision()   # the backward runs at its forward's precision
         return y
 
     @staticmethod
@@ -81,9 +82,10 @@ class _GRULayerFn(torch.autograd.Function):
             db_ih = torch.empty((2, 3 * H), device=x.device)
             db_hh = torch.empty((2, 3 * H), device=x.device)
         ws2 = torch.empty(int(_lib.lib().srk_gru_workspace_floats(B, T, IN, H, 1)), device=x.device)
-        call("srk_gru_layer_bwd", ptr(x), B, T, IN, H, ptr(w_ih), ptr(w_hh), ptr(y), ptr(ws), ptr(dy),
-             ptr(dx) if dx is not None else None, ptr(dw_ih), ptr(dw_hh), ptr(db_ih), ptr(db_hh), int(acc), ptr(ws2),
-             stream_ptr())
+        with _lib.precision_scope(ctx.prec):
+            call("srk_gru_layer_bwd", ptr(x), B, T, IN, H, ptr(w_ih), ptr(w_hh), ptr(y), ptr(ws), ptr(dy),
+                 ptr(dx) if dx is not None else None, ptr(dw_ih), ptr(dw_hh), ptr(db_ih), ptr(db_hh), int(acc),
+                 ptr(ws2), stream_ptr())
         if acc:
             return (dx,) + (None,) * 8
         return (dx, dw_ih[0], dw_ih[1], dw_hh[0], dw_hh[1], db_ih[0], db_ih[1], db_hh[0], db_hh[1])

@@ -225,3 +225,36 @@ def test_conv_lowprec_exact_rounding(prec, shape):
     assert close(ym.detach().permute(0, 3, 1, 2).cpu(), y_ref, K)
     assert close(xm.grad.permute(0, 3, 1, 2).cpu(), dx_ref, Co * KH * KW)
     assert close(wm.grad.cpu(), dw_ref, N * y_ref.shape[2] * y_ref.shape[3])
+
+
+# ----------------------------------------------------------------------------- 16-bit operands in memory
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(8, 8, 8), (40, 24, 72), (136, 264, 200), (304, 128, 1024), (256, 128, 8192),
+                                   (1000, 520, 64)])
+def test_gemm_16bit_operands(prec, ta, tb, M, N, K):
+    """srk_gemm_16: operands already bf16 / fp16 in memory == float64 product of those values."""
+    g = torch.Generator().manual_seed(M * 5 + N * 3 + K)
+    dt = TORCH_DT[prec]
+    A = torch.randn((K, M) if ta else (M, K), generator=g).to(dt)
+    B = torch.randn((N, K) if tb else (K, N), generator=g).to(dt)
+    C0 = torch.randn(M, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    opA = (A.T if ta else A).double()
+    opB = (B.T if tb else B).double()
+    ref = 0.5 * (opA @ opB) + 2.0 * C0.double() + bias.double()
+    Ad, Bd, Cd, bd = A.cuda(), B.cuda(), C0.clone().cuda(), bias.cuda()
+    _lib.prof_enable(1)
+    call("srk_gemm_16", ta, tb, M, N, K, 0.5, ptr(Ad), Ad.shape[1], ptr(Bd), Bd.shape[1], 2.0, ptr(Cd), N,
+         ptr(bd), 1, stream_ptr())
+    torch.cuda.synchronize()
+    assert _lib.prof_read("gemm_f16" if prec == "fp16" else "gemm_bf16")[0] == 1
+    _lib.prof_enable(0)
+    scale = (opA.abs() @ opB.abs()).max().item()
+    assert (Cd.cpu().double() - ref).abs().max().item() <= 2e-6 * (1 + scale)
+
+
+def test_gemm_16bit_rejects_misaligned(prec):
+    A = torch.zeros(16, 12, dtype=TORCH_DT[prec], device="cuda")
+    C = torch.zeros(16, 16, device="cuda")
+    with pytest.raises(_lib.SrkError):
+        call("srk_gemm_16", 0, 1, 16, 16, 12, 1.0, ptr(A), 12, ptr(A), 12, 0.0, ptr(C), 16, None, 0, stream_ptr())

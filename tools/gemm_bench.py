@@ -34,6 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp16"])
+    ap.add_argument("--h16", action="store_true", help="operands pre-converted to 16 bit (srk_gemm_16)")
     a = ap.parse_args()
     _lib.set_matmul_precision(a.precision)
     pname = {"fp32": "gemm_f32", "bf16": "gemm_bf16", "fp16": "gemm_f16"}[a.precision]
@@ -52,6 +53,17 @@ def main():
         args = (ta, tb, M, N, K, 1.0, A.data_ptr(), lda, Bm.data_ptr(), ldb, 0.0, C.data_ptr(), N)
         fn = lambda: _lib.call("srk_gemm_rowsum_f32", *args, rs.data_ptr(), stream) if ta else \
             _lib.call("srk_gemm_f32", *args, None, 0, stream)
+        if a.h16 and (M % 8 or N % 8 or K % 8):   # srk_gemm_16 needs 8-element multiples
+            continue
+        if a.h16:   # 16-bit operands in memory (leading dims rounded up to 8 elements)
+            lda8, ldb8 = (lda + 7) // 8 * 8, (ldb + 7) // 8 * 8
+            A16 = torch.zeros((K if ta else M), lda8, device=dev, dtype=tdt)
+            A16[:, :lda] = A.view(-1, lda).to(tdt)
+            B16 = torch.zeros((N if tb else K), ldb8, device=dev, dtype=tdt)
+            B16[:, :ldb] = Bm.view(-1, ldb).to(tdt)
+            Kp = K if (ta or K % 8 == 0) and (not tb or K % 8 == 0) else (K + 7) // 8 * 8
+            args16 = (ta, tb, M, N, Kp, 1.0, A16.data_ptr(), lda8, B16.data_ptr(), ldb8, 0.0, C.data_ptr(), N)
+            fn = lambda: _lib.call("srk_gemm_16", *args16, None, 0, stream)
         for _ in range(2):
             fn()
         torch.cuda.synchronize()

@@ -450,16 +450,20 @@ int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
     y16 = w16 + 2 * up64(6 * H * in8 / 2 + 1);
     if (int rc = srk::to16(x, BT, in, x16, in8, s)) return rc;
     if (int rc = srk::to16(w_ih, 6 * H, in, w16, in8, s)) return rc;
-    GemmDesc g;   // gi[B*T, 6H] = x16 * W16^T + b_ih
-    g.M = BT; g.N = 6 * H; g.K = in8;
-    g.A16 = x16; g.lda = in8;
-    g.B16 = w16; g.ldb = in8; g.tb = true;
-    g.C = gi; g.ldc = 6 * H;
-    g.bias = b_ih; g.bias_mode = 1;
-    if (int rc = srk::gemm_f32(g, s)) return rc;
+    const bool fuse = in <= srk::kFusedIn;   // the kernel projects the input itself (no gi GEMM)
+    if (!fuse) {
+      GemmDesc g;   // gi[B*T, 6H] = x16 * W16^T + b_ih
+      g.M = BT; g.N = 6 * H; g.K = in8;
+      g.A16 = x16; g.lda = in8;
+      g.B16 = w16; g.ldb = in8; g.tb = true;
+      g.C = gi; g.ldc = 6 * H;
+      g.bias = b_ih; g.bias_mode = 1;
+      if (int rc = srk::gemm_f32(g, s)) return rc;
+    }
     srk::GruPArgs p{};
     p.B = (int)B; p.T = (int)T; p.H = (int)H;
     p.gi = gi; p.w_hh = w_hh; p.b_hh = b_hh; p.y = y; p.gates = gates; p.y16 = y16;
+    if (fuse) { p.x_in = x; p.w_ih = w_ih; p.b_ih = b_ih; p.in = (int)in; }
     p.xbuf = ws + fwd_xbuf_off(B, T, H);
     p.counters = reinterpret_cast<unsigned*>(ws + fwd_counter_off(B, T, H));
     return srk::gru_persistent_launch(p, false, s);
@@ -476,17 +480,22 @@ int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
     xa = xp;
     wa = wp;
   }
-  GemmDesc g;   // gi[B*T, 6H] = x[B*T, in] * W_ih_cat[6H, in]^T + b_ih_cat
-  g.M = B * T; g.N = 6 * H; g.K = ink;
-  g.A = xa; g.lda = ink;
-  g.B = wa; g.ldb = ink; g.tb = true;
-  g.C = gi; g.ldc = 6 * H;
-  g.bias = b_ih; g.bias_mode = 1;
-  if (int rc = srk::gemm_f32(g, s)) return rc;
-  if (srk::g_opt_gru_persistent && srk::gru_persistent_supported(B, T, H, false)) {
+  const bool persistent = srk::g_opt_gru_persistent && srk::gru_persistent_supported(B, T, H, false);
+  const bool fuse = persistent && in <= srk::kFusedIn;   // the kernel projects the input itself
+  if (!fuse) {
+    GemmDesc g;   // gi[B*T, 6H] = x[B*T, in] * W_ih_cat[6H, in]^T + b_ih_cat
+    g.M = B * T; g.N = 6 * H; g.K = ink;
+    g.A = xa; g.lda = ink;
+    g.B = wa; g.ldb = ink; g.tb = true;
+    g.C = gi; g.ldc = 6 * H;
+    g.bias = b_ih; g.bias_mode = 1;
+    if (int rc = srk::gemm_f32(g, s)) return rc;
+  }
+  if (persistent) {
     srk::GruPArgs p{};
     p.B = (int)B; p.T = (int)T; p.H = (int)H;
     p.gi = gi; p.w_hh = w_hh; p.b_hh = b_hh; p.y = y; p.gates = gates;
+    if (fuse) { p.x_in = x; p.w_ih = w_ih; p.b_ih = b_ih; p.in = (int)in; }
     p.xbuf = ws + fwd_xbuf_off(B, T, H);
     p.counters = reinterpret_cast<unsigned*>(ws + fwd_counter_off(B, T, H));
     return srk::gru_persistent_launch(p, false, s);

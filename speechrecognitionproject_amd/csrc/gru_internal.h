@@ -10,6 +10,7 @@ namespace srk {
 // Arrival counters of the persistent kernels: [2 directions][groups <= 4] at a 64-B stride,
 // zeroed by a hipMemsetAsync of exactly this block before every launch.
 constexpr int kCounterFloats = 256;
+constexpr int kFusedIn = 64;   // widest layer input whose projection the forward kernels fuse
 
 struct GruPArgs {
   int B, T, H;
@@ -35,6 +36,12 @@ struct GruPArgs {
   float* dbias;          // bwd with dgi16: bias-gradient partials [chunk * G + group][2 dir][4][H]
                          //   (sum over t and the group's rows of dar, daz, dan, dan * r)
   int chunk;             // index of this launch's 64*G-row batch chunk
+  // fused small input projection (in <= kFusedIn, the 39 MFCC features of model_mfcc_bgru.py:25):
+  // with x_in set the forward kernels compute gi_t = x_t W_ih^T + b_ih themselves (gi unused)
+  const float* x_in;     // [B][T][in]
+  const float* w_ih;     // [2][3H][in]
+  const float* b_ih;     // [2][3H]
+  int in;
   unsigned long long* trace;   // optional per-(workgroup, step) timestamps (tools/gru_trace.py)
 };
 

@@ -176,14 +176,75 @@ __device__ __forceinline__ void store_dgi(const GruPArgs& a, const float (&dv)[4
   }
 }
 
+// ------------------------------------------------------------------ fused input projection
+// For inputs of <= kFusedIn features the forward kernels compute the step's input projection for
+// their 64 rows x 48 gate units on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: lane = (row lr,
+// k-quad lq), the same output layout as the recurrent accumulators), from x_t (global, L2-resident)
+// and an LDS copy of the W_ih slice, BEFORE the step's wait: it does not depend on h and runs in
+// the hand-off latency.  RND rounds both operands to bf16 / fp16 first (the 16-bit kernels' GEMM
+// semantics: 16-bit operands, fp32 accumulation).
+constexpr int kXP = kFusedIn + 1;   // LDS pitch of the W_ih slice (odd: conflict-free column reads)
+
+template <int RND>
+__device__ __forceinline__ float rnd16(float v) {
+  if (RND == 1) return (float)(__bf16)v;
+  if (RND == 2) return (float)(_Float16)v;
+  return v;
+}
+
+template <int RND>
+__device__ __forceinline__ void stage_wih(const GruPArgs& a, float* Wx, int dir, int j0, int H) {
+  const float* W = a.w_ih + (size_t)dir * 3 * H * a.in;
+  for (int v = threadIdx.x; v < 3 * kUnits * kFusedIn; v += 256) {
+    const int c = v / kFusedIn, k = v % kFusedIn, g = c / kUnits, jj = c % kUnits;
+    Wx[c * kXP + k] = k < a.in ? rnd16<RND>(W[(size_t)(g * H + j0 + jj) * a.in + k]) : 0.f;
+  }
+}
+
+// x_t of the lane's row (k = 4 m + lq); issued one step ahead so the loads are in flight during the
+// previous step
+__device__ __forceinline__ void load_x(const GruPArgs& a, int t, int brow, int lq, float (&xv)[kFusedIn / 4]) {
+  const float* xr = a.x_in + ((size_t)brow * a.T + t) * a.in;
+#pragma unroll
+  for (int m = 0; m < kFusedIn / 4; ++m) {
+    const int k = 4 * m + lq;
+    xv[m] = (4 * m < a.in && k < a.in) ? xr[k] : 0.f;
+  }
+}
+
+template <int RND>
+__device__ __forceinline__ void fused_gi(const GruPArgs& a, const float* Wx, const float (&xv0)[kFusedIn / 4], int lr,
+                                         int lq, float bir, float biz, float bin, float (&gr)[4], float (&gz)[4],
+                                         float (&gn)[4]) {
+  float xv[kFusedIn / 4];
+#pragma unroll
+  for (int m = 0; m < kFusedIn / 4; ++m) xv[m] = rnd16<RND>(xv0[m]);
+  f32x4 ax[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int m = 0; m < kFusedIn / 4; ++m) {
+    if (4 * m >= a.in) break;   // uniform
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+      ax[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[m], Wx[(g * kUnits + lr) * kXP + 4 * m + lq], ax[g], 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    gr[r] = ax[0][r] + bir;
+    gz[r] = ax[1][r] + biz;
+    gn[r] = ax[2][r] + bin;
+  }
+}
+
 // ------------------------------------------------------------------ forward
 // LDS: W slice [48][H + 4] (gate g, unit jj -> row g*16 + jj), then the h transpose tile [64][20].
 template <int H>
 __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) {
   constexpr int WP = H + 4, HTP = kUnits + 4, NKB = H / 16;
+  constexpr int RNDX = 0;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Ws = smem;
   float* hT = smem + 3 * kUnits * WP;
+  float* Wx = hT + 64 * HTP;   // fused input projection: W_ih slice [48][kXP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
   int dir, group, slice;
   map_block(a.G, H / kUnits, dir, group, slice);
@@ -199,6 +260,12 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
       st4(Ws + c * WP + kq, ld4(W + (size_t)(g * H + j0 + jj) * H + kq));
     }
   }
+  const bool fused = a.x_in != nullptr;
+  if (fused) stage_wih<RNDX>(a, Wx, dir, j0, H);
+  float xnext[kFusedIn / 4];   // x of the next step (fused projection), loaded a step ahead
+  if (fused) load_x(a, dir == 0 ? 0 : a.T - 1, min(a.b_begin + group * kRows + wave * 16 + lr, a.b_end - 1), lq, xnext);
+  const float bir = fused ? a.b_ih[dir * 3 * H + j] : 0.f, biz = fused ? a.b_ih[dir * 3 * H + H + j] : 0.f,
+              bin = fused ? a.b_ih[dir * 3 * H + 2 * H + j] : 0.f;
   const float bhr = a.b_hh[dir * 3 * H + j], bhz = a.b_hh[dir * 3 * H + H + j], bhn = a.b_hh[dir * 3 * H + 2 * H + j];
   __syncthreads();
 
@@ -213,13 +280,18 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
     const int tprev = dir == 0 ? t - 1 : t + 1;
     stamp(a, step, 0);
     float gr[4], gz[4], gn[4];
+    if (fused) {   // this step's input projection, before the wait (independent of h)
+      fused_gi<RNDX>(a, Wx, xnext, lr, lq, bir, biz, bin, gr, gz, gn);
+      if (step + 1 < T) load_x(a, dir == 0 ? t + 1 : t - 1, min(b0 + wave * 16 + lr, b_last), lq, xnext);
+    } else {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {   // input projections of the lane's cells (written by an earlier launch)
-      const int b = min(b0 + wave * 16 + lq * 4 + r, b_last);
-      const float* gi = a.gi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
-      gr[r] = gi[j];
-      gz[r] = gi[H + j];
-      gn[r] = gi[2 * H + j];
+      for (int r = 0; r < 4; ++r) {   // input projections of the lane's cells (written by an earlier launch)
+        const int b = min(b0 + wave * 16 + lq * 4 + r, b_last);
+        const float* gi = a.gi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
+        gr[r] = gi[j];
+        gz[r] = gi[H + j];
+        gn[r] = gi[2 * H + j];
+      }
     }
     f32x4 acc[3];
 #pragma unroll
@@ -490,9 +562,11 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
   using Ops = RecOps<F16>;
   using e8 = typename Ops::e8;
   constexpr int WPQ = lp_fwd_wpe<H>() / 8, HTP = kUnits + 4, NKB = H / 32;
+  constexpr int RNDX = F16 ? 2 : 1;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   u32x4* Ws = reinterpret_cast<u32x4*>(smem);
   float* hT = smem + 3 * kUnits * WPQ * 4;
+  float* Wx = hT + 64 * HTP;   // fused input projection: W_ih slice [48][kXP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
   int dir, group, slice;
   map_block(a.G, H / kUnits, dir, group, slice);
@@ -509,6 +583,12 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
       Ws[c * WPQ + kq] = pack8<F16>(cat8(ld4(src), ld4(src + 4)));
     }
   }
+  const bool fused = a.x_in != nullptr;
+  if (fused) stage_wih<RNDX>(a, Wx, dir, j0, H);
+  float xnext[kFusedIn / 4];   // x of the next step (fused projection), loaded a step ahead
+  if (fused) load_x(a, dir == 0 ? 0 : a.T - 1, min(a.b_begin + group * kRows + wave * 16 + lr, a.b_end - 1), lq, xnext);
+  const float bir = fused ? a.b_ih[dir * 3 * H + j] : 0.f, biz = fused ? a.b_ih[dir * 3 * H + H + j] : 0.f,
+              bin = fused ? a.b_ih[dir * 3 * H + 2 * H + j] : 0.f;
   const float bhr = a.b_hh[dir * 3 * H + j], bhz = a.b_hh[dir * 3 * H + H + j], bhn = a.b_hh[dir * 3 * H + 2 * H + j];
   __syncthreads();
 
@@ -521,13 +601,18 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
     const int t = dir == 0 ? step : T - 1 - step;
     stamp(a, step, 0);
     float gr[4], gz[4], gn[4];
+    if (fused) {   // this step's input projection, before the wait (independent of h)
+      fused_gi<RNDX>(a, Wx, xnext, lr, lq, bir, biz, bin, gr, gz, gn);
+      if (step + 1 < T) load_x(a, dir == 0 ? t + 1 : t - 1, min(b0 + wave * 16 + lr, b_last), lq, xnext);
+    } else {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = min(b0 + wave * 16 + lq * 4 + r, b_last);
-      const float* gi = a.gi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
-      gr[r] = gi[j];
-      gz[r] = gi[H + j];
-      gn[r] = gi[2 * H + j];
+      for (int r = 0; r < 4; ++r) {   // input projections of the lane's cells (written by an earlier launch)
+        const int b = min(b0 + wave * 16 + lq * 4 + r, b_last);
+        const float* gi = a.gi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
+        gr[r] = gi[j];
+        gz[r] = gi[H + j];
+        gn[r] = gi[2 * H + j];
+      }
     }
     f32x4 acc[3];
 #pragma unroll
@@ -799,7 +884,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
 size_t lds_bytes(int H, bool backward, int prec) {
   if (prec == kPrecF32) return backward ? bwd_lds_bytes(H) : fwd_lds_bytes(H);
   const size_t need = backward ? (size_t)kUnits * (3 * H + 16) * 2 + 64 * 4 * (kUnits + 4) * 4
-                               : (size_t)3 * kUnits * (H + 16) * 2 + 64 * (kUnits + 4) * 4;
+                               : (size_t)3 * kUnits * (H + 16) * 2 + 64 * (kUnits + 4) * 4 + 48 * kXP * 4;
   // the sc1 hand-off is the form measured at ONE workgroup per CU (MI355X_MICROARCH.md, "Valid
   // forms" row 1): reserve more than half of the 160 KB so a second workgroup never fits
   return std::max<size_t>(need, 96 * 1024);
@@ -841,7 +926,7 @@ int occupancy_ok(bool backward, int prec, int grid) {
 
 }  // namespace
 
-size_t fwd_lds_bytes(int H) { return (size_t)(3 * 16 * (H + 4) + 64 * 20) * 4; }
+size_t fwd_lds_bytes(int H) { return (size_t)(3 * 16 * (H + 4) + 64 * 20 + 48 * kXP) * 4; }
 size_t bwd_lds_bytes(int H) { return (size_t)(16 * (3 * H + 4) + 64 * 3 * 20) * 4; }
 
 int gru_persistent_groups(int64_t H) {

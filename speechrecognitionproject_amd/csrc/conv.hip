@@ -22,6 +22,20 @@ using namespace tile;
 
 enum { kFwd = 0, kDgrad = 1, kWgrad = 2 };
 
+// Division by a launch-invariant divisor as multiply-high + add + shift (Granlund & Montgomery,
+// "Division by invariant integers using multiplication", 1994): the gathers split staged k / m
+// indices into (pixel, tap, channel) every k-tile, and integer division is a long software
+// sequence on the VALU.  Exact for n < 2^31 (run_conv_gemm checks M, K < 2^31).
+struct FastDiv {
+  unsigned d = 1, m = 1, l = 0;
+  FastDiv() = default;
+  __host__ explicit FastDiv(unsigned dv) : d(dv) {
+    while ((1ull << l) < dv) ++l;
+    m = (unsigned)(((1ull << 32) * ((1ull << l) - dv)) / dv + 1);
+  }
+  __device__ __forceinline__ unsigned div(unsigned n) const { return (__umulhi(n, m) + n) >> l; }
+};
+
 struct ConvArgs {
   int N, H, W, Ci, Ho, Wo, Co, KH, KW, ph, pw, sh, sw;
   const float* x;      // [N][H][W][Ci]
@@ -33,6 +47,8 @@ struct ConvArgs {
   int tiles_m, tiles_n, tiles, nblk, group_m;
   int64_t kchunk;
   float* partial;      // split-K slabs
+  // divisors of the gathers (host-set): pixel grid (cols, rows), channels, KW, strides (dgrad)
+  FastDiv fd_w, fd_h, fd_c, fd_kw, fd_sh, fd_sw;
 };
 
 // Implicit-GEMM operand gathers.  Each returns the ELEMENT OFFSET of the value (clamped to 0 when
@@ -44,23 +60,23 @@ struct ConvArgs {
 //   wgrad A[m = (kh,kw,ci)][k = pixel (n,ho,wo)] = X[n, ho*sh+kh-ph, wo*sw+kw-pw, ci]
 struct Pix { int n, a, b; bool ok; };   // pixel (n, row, col) + "row index < rows"
 
-__device__ __forceinline__ Pix split_pix(int64_t p, int64_t rows, int Hh, int Ww) {
+__device__ __forceinline__ Pix split_pix(int64_t p, int64_t rows, const FastDiv& fw, const FastDiv& fh) {
   Pix q;
   q.ok = p < rows;
-  const int64_t pc = q.ok ? p : 0;
-  q.b = (int)(pc % Ww);
-  const int64_t u = pc / Ww;
-  q.a = (int)(u % Hh);
-  q.n = (int)(u / Hh);
+  const unsigned pc = q.ok ? (unsigned)p : 0u;
+  const unsigned u = fw.div(pc), v = fh.div(u);
+  q.b = (int)(pc - u * fw.d);
+  q.a = (int)(u - v * fh.d);
+  q.n = (int)v;
   return q;
 }
 struct Tap { int kh, kw, ch; };   // k (or wgrad m) = (kh, kw, channel)
-__device__ __forceinline__ Tap split_tap(int64_t k, int C, int KW) {
+__device__ __forceinline__ Tap split_tap(int64_t k, const FastDiv& fc, const FastDiv& fkw) {
+  const unsigned kk = (unsigned)k, u = fc.div(kk), v = fkw.div(u);
   Tap t;
-  t.ch = (int)(k % C);
-  const int64_t u = k / C;
-  t.kw = (int)(u % KW);
-  t.kh = (int)(u / KW);
+  t.ch = (int)(kk - u * fc.d);
+  t.kw = (int)(u - v * fkw.d);
+  t.kh = (int)v;
   return t;
 }
 
@@ -68,7 +84,7 @@ template <int MODE>
 __device__ __forceinline__ int64_t a_offset(const ConvArgs& c, const Pix& p, const Tap& t, bool& ok) {
   if (MODE == kDgrad) {
     const int ht = p.a + c.ph - t.kh, wt = p.b + c.pw - t.kw;
-    const int ho = ht / c.sh, wo = wt / c.sw;
+    const int ho = (int)c.fd_sh.div(ht > 0 ? (unsigned)ht : 0u), wo = (int)c.fd_sw.div(wt > 0 ? (unsigned)wt : 0u);
     ok = ok && p.ok && ht >= 0 && wt >= 0 && ho * c.sh == ht && wo * c.sw == wt && ho < c.Ho && wo < c.Wo;
     return ok ? (((int64_t)p.n * c.Ho + ho) * c.Wo + wo) * c.Co + t.ch : 0;
   }
@@ -155,8 +171,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   const int wm0 = (wave >> 1) * (BM / 2), wn0 = (wave & 1) * (BN / 2);
   const float* __restrict__ Asrc = MODE == kDgrad ? c.dy : c.x;
   const float* __restrict__ Bsrc = MODE == kWgrad ? c.dy : c.wmat;
-  const int Cch = MODE == kDgrad ? c.Co : c.Ci;   // channel count along A's k (fwd/dgrad) or m (wgrad)
-  const int Hh = MODE == kDgrad ? c.H : c.Ho, Ww = MODE == kDgrad ? c.W : c.Wo;   // pixel grid of A's rows / k
+  // pixel / tap splits by the host-set divisors: fd_w, fd_h = the pixel grid of A's rows (fwd / dgrad)
+  // or k (wgrad); fd_c = the channel count along A's k (fwd / dgrad) or m (wgrad); fd_kw = KW
 
   // fwd / dgrad: this thread's A rows are fixed for the whole k loop (decomposed once);
   // wgrad: its A "rows" (= taps m) are fixed instead.
@@ -166,11 +182,11 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   if (AKC) {
     aq = (tid % (BK / 4)) * 4;
 #pragma unroll
-    for (int i = 0; i < VA; ++i) prow[i] = split_pix(m0 + (tid + i * NT) / (BK / 4), c.M, Hh, Ww);
+    for (int i = 0; i < VA; ++i) prow[i] = split_pix(m0 + (tid + i * NT) / (BK / 4), c.M, c.fd_w, c.fd_h);
   } else {
     aq = (tid % (BM / 4)) * 4;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) mtap[e] = split_tap(m0 + aq + e < c.M ? m0 + aq + e : 0, Cch, c.KW);
+    for (int e = 0; e < 4; ++e) mtap[e] = split_tap(m0 + aq + e < c.M ? m0 + aq + e : 0, c.fd_c, c.fd_kw);
   }
 
   v4f ra[VA], rb[VB];
@@ -181,7 +197,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
     if (AKC) {   // 4 consecutive k = (kh, kw, ch .. ch+3) of one pixel row
       const int64_t k = k0 + aq;
       if (VEC) {
-        const Tap t = split_tap(k < ke ? k : 0, Cch, c.KW);
+        const Tap t = split_tap(k < ke ? k : 0, c.fd_c, c.fd_kw);
 #pragma unroll
         for (int i = 0; i < VA; ++i) {
           bool ok = k < ke;
@@ -193,7 +209,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int64_t ke_ = k + e;
-          const Tap t = split_tap(ke_ < ke ? ke_ : 0, Cch, c.KW);
+          const Tap t = split_tap(ke_ < ke ? ke_ : 0, c.fd_c, c.fd_kw);
 #pragma unroll
           for (int i = 0; i < VA; ++i) {
             bool ok = ke_ < ke;
@@ -207,7 +223,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
 #pragma unroll
       for (int i = 0; i < VA; ++i) {
         const int64_t k = k0 + (tid + i * NT) / (BM / 4);
-        const Pix p = split_pix(k < ke ? k : 0, c.K, Hh, Ww);
+        const Pix p = split_pix(k < ke ? k : 0, c.K, c.fd_w, c.fd_h);
         if (VEC) {
           bool ok = k < ke && m0 + aq < c.M;
           const int64_t off = a_offset<MODE>(c, p, mtap[0], ok);
@@ -523,6 +539,13 @@ int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
     if (int rc = conv_scratch((size_t)splits * c.M * c.Nn, &c.partial)) return rc;
   }
   const int chans = MODE == kDgrad ? c.Co : c.Ci;
+  SRK_REQUIRE(c.M < INT32_MAX && c.K < INT32_MAX, SRK_ERR_INVALID, "conv: implicit-GEMM extent >= 2^31");
+  c.fd_w = FastDiv((unsigned)(MODE == kDgrad ? c.W : c.Wo));
+  c.fd_h = FastDiv((unsigned)(MODE == kDgrad ? c.H : c.Ho));
+  c.fd_c = FastDiv((unsigned)chans);
+  c.fd_kw = FastDiv((unsigned)c.KW);
+  c.fd_sh = FastDiv((unsigned)c.sh);
+  c.fd_sw = FastDiv((unsigned)c.sw);
   const bool vecb = c.Nn % 4 == 0;
   const bool vec = (chans % 4 == 0) && vecb;
   ProfScope prof(prec == kPrecF32 ? name : (MODE == kFwd ? "conv_fwd_lp" : MODE == kDgrad ? "conv_dgrad_lp" : "conv_wgrad_lp"),

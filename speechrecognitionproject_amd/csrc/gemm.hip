@@ -717,23 +717,32 @@ __global__ __launch_bounds__(NW * 64, (h16_per_cu<TA, TB, BM, BN>())) void gemm_
   init(std::integral_constant<bool, BKC>{}, std::integral_constant<int, BN>{}, voB, ldsB, kuB, d.ldb, d.N, n0);
 
   u32x4 ra[UA], rb[UB];
+  // k-contiguous: k advances along the row (+2 B per k); row-contiguous: a k row is ld elements.
+  // Full k-tiles (a uniform test) carry the k offset in the scalar soffset; only the k tail uses
+  // per-lane offsets, where an invalid unit re-reads a valid one (k 0 of its row / k row ke - 1) and
+  // is zeroed at LDS-store time.  (A per-lane soffset would make the compiler waterfall every load.)
+  auto load_op = [&](auto KC_, auto U_, __amdgpu_buffer_rsrc_t rs, const unsigned* vo, const int* ku, int64_t ld,
+                     u32x4* r, int64_t k0) {
+    constexpr bool KC = decltype(KC_)::value;
+    constexpr int U = decltype(U_)::value;
+    const int64_t step = KC ? 2 : ld * 2;   // bytes per k
+    if (k0 + BK <= ke) {
+      const int soff = (int)(k0 * step);
+#pragma unroll
+      for (int i = 0; i < U; ++i)
+        r[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo[i], soff, 0));
+    } else {
+#pragma unroll
+      for (int i = 0; i < U; ++i) {
+        const int64_t off = k0 + ku[i] < ke ? (int64_t)vo[i] + k0 * step
+                                            : (KC ? (int64_t)vo[i] - ku[i] * 2 : (int64_t)vo[i] + ((ke - 1) - ku[i]) * step);
+        r[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
+      }
+    }
+  };
   auto load_tile = [&](int64_t k0) {
-    // k-contiguous: k advances along the row (+2 B per k); row-contiguous: a k row is ld elements
-    const int64_t kc0 = k0 < ke ? k0 : 0;
-#pragma unroll
-    for (int i = 0; i < UA; ++i) {
-      const bool ok = kc0 + kuA[i] < ke;
-      const int64_t kk = ok ? kc0 : 0;   // clamped: an invalid unit re-reads a valid one, zeroed at store
-      const int soff = AKC ? (int)(kk * 2) : (int)(kk * d.lda * 2);
-      ra[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)voA[i], soff, 0));
-    }
-#pragma unroll
-    for (int i = 0; i < UB; ++i) {
-      const bool ok = kc0 + kuB[i] < ke;
-      const int64_t kk = ok ? kc0 : 0;
-      const int soff = BKC ? (int)(kk * 2) : (int)(kk * d.ldb * 2);
-      rb[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsB, (int)voB[i], soff, 0));
-    }
+    load_op(std::integral_constant<bool, AKC>{}, std::integral_constant<int, UA>{}, rsA, voA, kuA, d.lda, ra, k0);
+    load_op(std::integral_constant<bool, BKC>{}, std::integral_constant<int, UB>{}, rsB, voB, kuB, d.ldb, rb, k0);
   };
   auto store_tile = [&](int buf, int64_t k0) {
     unsigned short* As = smem + buf * STAGE;
@@ -1018,8 +1027,12 @@ int launch_h16_cfg(const GemmDesc& d, hipStream_t s, bool f16) {
 template <bool TA, bool TB>
 int launch_h16(const GemmDesc& d, hipStream_t s, bool f16) {
   static const int cfg_env = env_int("SRK_H16_CFG", 0);
-  const int cfg = cfg_env ? cfg_env : (d.M >= 1024 && !(!TA && TB) ? 3 : 1);
+  // measured (profiles/r01zk_gemm_h16_cfg*.txt): 256 x 256 on x W^T and on the weight gradients
+  // (TA != TB: gi 143 vs 148 us, dW_ih 128 vs 137), 256 x 128 on dx (204 tiles of 256 x 256 leave
+  // CUs idle: 255 vs 147 us), 128 x 128 below 1024 rows
+  const int cfg = cfg_env ? cfg_env : d.M < 1024 ? 1 : (TA != TB && d.N >= 256) ? 4 : 3;
   if (cfg == 3) return launch_h16_cfg<TA, TB, 256, 128, 8>(d, s, f16);
+  if (cfg == 4) return launch_h16_cfg<TA, TB, 256, 256, 8>(d, s, f16);
   return launch_h16_cfg<TA, TB, 128, 128, 4>(d, s, f16);
 }
 

@@ -51,6 +51,11 @@ constexpr unsigned kSpinLimit = 1u << 24;   // x s_sleep(2) (~128 clk) ~= 2 s at
 __device__ __forceinline__ v4f ld4(const float* p) { return *reinterpret_cast<const v4f*>(p); }
 __device__ __forceinline__ void st4(float* p, v4f v) { *reinterpret_cast<v4f*>(p) = v; }
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+// 16-bit kernels: the hardware exp / reciprocal forms (v_exp_f32, v_rcp_f32: ~1 ulp, far inside the
+// 16-bit operand tolerance) keep the cell epilogue short on the step-to-step chain; the fp32 kernels
+// keep the libm forms.
+__device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float tanh_fast(float x) { return 2.0f * sigmoid_fast(2.0f * x) - 1.0f; }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
@@ -652,9 +657,9 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
     for (int r = 0; r < 4; ++r) {
       const int rl = wave * 16 + lq * 4 + r, b = b0 + rl;
       const float ghn = acc[2][r] + bhn;
-      const float rg = sigmoidf_(gr[r] + (acc[0][r] + bhr));
-      const float zg = sigmoidf_(gz[r] + (acc[1][r] + bhz));
-      const float ng = tanhf(gn[r] + rg * ghn);
+      const float rg = sigmoid_fast(gr[r] + (acc[0][r] + bhr));
+      const float zg = sigmoid_fast(gz[r] + (acc[1][r] + bhz));
+      const float ng = tanh_fast(gn[r] + rg * ghn);
       const float h = (1.0f - zg) * ng + zg * hreg[r];
       hreg[r] = h;
       hT[rl * HTP + lr] = h;

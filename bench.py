@@ -15,9 +15,14 @@
   spec_cnn    SURVEY.md §8f rank 3: on-device log spectrogram[49x321] + 4 Conv2d + pools + dropout + 2 FC,
               512 per GPU
 
-For N > 1 the driver launches one process per GPU with torch.distributed.run; each rank takes its
-own shard of synthetic clips (weak scaling: per-GPU batch fixed) and the flat gradient buffer is
-all-reduced through RCCL once per step.  Rank 0 prints ONE JSON line.
+For N > 1 one process runs per GPU: under torch.distributed.run (WORLD_SIZE set) each process is a
+rank; started plainly as `python bench.py --gpus N` it re-launches itself through
+torch.distributed.run (127.0.0.1, a free port) BEFORE touching the GPU and exits with the
+launcher's code.  Each rank asserts the world size equals --gpus, takes its own shard of synthetic
+clips (weak scaling: per-GPU batch fixed) and the flat gradient buffer is all-reduced through RCCL
+once per step.  Rank 0 prints ONE JSON line.  --cpu-plumbing runs the launcher / rendezvous /
+barrier / max-over-ranks timing / JSON path over gloo with a CPU all-reduce as the "step" (no GPU,
+no measurement: the CPU test of the multi-rank harness).
 
 Workload (BASELINE.json configs[1], reference shapes per SURVEY.md §0.1): MFCC [39 x 51] computed
 on the device from raw 1-s 16 kHz PCM (K1), then model_mfcc_bgru's 2-layer BiGRU(39->512) + FC,
@@ -34,14 +39,17 @@ Measurement extras on the same line:
                  stream (srk_prof_*), algorithmic flops / avg launch time vs the MFMA peak of its
                  operand type (fp32 157.3 TF, bf16/fp16 2.5 PF dense);
   mfcc_roofline— K1 alone on 65,536 clips (HBM-bound): algorithmic bytes / time vs 8 TB/s;
-  cpu_baseline — the CPU restatement (oracle/: numpy MFCC per clip + torch-CPU GRU step) timed on
-                 this host's cores on a bounded sample (rank 0, N = 1 only).
+  cpu_baseline — the CPU restatement (oracle/: numpy features per clip + torch-CPU train step) timed
+                 on this host's cores (every core this process may use, plus a
+                 1-thread figure) on a bounded sample at the config's batch (rank 0, N = 1 only);
+                 "cfg1" = BASELINE.json configs[0]: the MFCC restatement alone on 32 clips.
 """
 import argparse
 import json
 import os
 import sys
 import time
+import types
 
 import numpy as np
 import torch
@@ -97,36 +105,73 @@ def build_model(name):
     return importlib.import_module("speechrecognitionproject_amd.models.model_%s" % name).Network()
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except Exception:
+        return "unknown"
+
+
 def cpu_baseline(model_name, batch, seconds):
-    """The oracle CPU path on a bounded sample: per-clip numpy features + torch-CPU train step."""
+    """SURVEY.md §8d CPU baseline: the oracle CPU path (per-clip numpy features exactly as the
+    reference's forward loops, torch-CPU fp32 model fwd/bwd + Adam) on this host, single process:
+    (1) every core this process may use, train steps at the config's batch until `seconds`;
+    (2) the same code pinned to 1 thread, one train step on a 32-clip sample (a full-batch
+    1-thread step would take minutes); (3) "cfg1" (BASELINE.json configs[0]): the MFCC
+    restatement alone on 32 clips, clips/s."""
+    from oracle import features as OF
     from oracle import models as OM
-    threads = max(1, min(16, os.cpu_count() or 1))
-    torch.set_num_threads(threads)
     cls = {"mfcc_bgru": OM.MfccBGRU, "spec_bgru": OM.SpecBGRU, "fbanks_cnn": OM.FbanksCNN,
            "resnet_bgru": OM.ResnetBGRU, "mfrn_bgru": OM.MfrnBGRU, "cnn_bgru": OM.CnnBGRU,
            "spec_cnn": OM.SpecCNN}[model_name]
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    prev_threads = torch.get_num_threads()
     torch.manual_seed(0)
     net = cls()
     opt = torch.optim.Adam(net.parameters(), lr=1e-4)
-    x, y = synthetic_clips(batch, seed=99)
-    xt, yt = torch.from_numpy(x), torch.from_numpy(y)
-    OM.train_step(net, xt, yt, optimizer=opt)      # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        OM.train_step(net, xt, yt, optimizer=opt)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 50:
-            break
-    cpu = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            cpu = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
-    except Exception:
-        pass
-    return {"value": round(n * batch / el, 2), "unit": "utt/s", "cores": threads, "kind": "port",
-            "sample": "%d train steps x %d clips (%s CPU restatement: per-clip numpy features + torch-CPU "
-                      "fp32 model fwd/bwd + Adam), %.1f s, %s" % (n, batch, model_name, el, cpu)}
+
+    def run(n_clips, threads, budget, max_steps):
+        torch.set_num_threads(threads)
+        x, y = synthetic_clips(n_clips, seed=99)
+        xt, yt = torch.from_numpy(x), torch.from_numpy(y)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            OM.train_step(net, xt, yt, optimizer=opt)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget or n >= max_steps:
+                return n, el
+
+    run(min(batch, 32), cores, 0.0, 1)                        # warm-up (allocator, thread pool)
+    n, el = run(batch, cores, seconds, 50)
+    # 1 thread: the config batch when one step fits ~seconds, else the largest multiple of 32 that does
+    n1, el1 = run(32, 1, 0.0, 1)
+    b1 = int(min(batch, max(32, (seconds / (el1 / 32)) // 32 * 32)))
+    if b1 > 32:
+        n1, el1 = run(b1, 1, 0.0, 1)
+    # cfg1: MFCC restatement on 32 clips, serial per clip like the reference's forward (:31-32)
+    x32, _ = synthetic_clips(32, seed=98)
+    reps, t0 = 0, time.perf_counter()
+    while reps < 3 or time.perf_counter() - t0 < 1.0:
+        for c in x32:
+            OF.compute_mfcc(c)
+        reps += 1
+    el_mfcc = (time.perf_counter() - t0) / reps
+    torch.set_num_threads(prev_threads)
+    cpu = _cpu_model()
+    return {"value": round(n * batch / el, 2), "unit": "utt/s", "cores": cores, "kind": "port",
+            "sample": "%d train steps x %d clips (the config batch; %s CPU restatement: per-clip numpy features + "
+                      "torch-CPU fp32 fwd/bwd + Adam), %.1f s on %d threads, %s (os.cpu_count() = %s)"
+                      % (n, batch, model_name, el, cores, cpu, os.cpu_count()),
+            "one_thread": {"value": round(n1 * b1 / el1, 2), "unit": "utt/s", "cores": 1,
+                           "sample": "%d train step x %d clips, %.1f s" % (n1, b1, el1)},
+            "cfg1": {"value": round(32 / el_mfcc, 2), "unit": "clips/s", "cores": 1,
+                     "sample": "BASELINE.json configs[0]: MFCC[39x51] restatement (numpy, float64 librosa-0.6 "
+                               "semantics) on 32 x 1-s clips, serial, %.4f s per pass (mean of %d)" % (el_mfcc, reps)}}
 
 
 def pmc_traffic(kernel):
@@ -164,6 +209,52 @@ def feature_roofline(model_name, n_clips=65536):
             "clips_per_launch": n_clips, "ms_per_launch": round(ms / cnt, 4), "bytes_per_clip": per_clip}
 
 
+def _relaunch(args):
+    """`bench.py --gpus N` outside torch.distributed.run: start N ranks through it (a child
+    process; nothing here has touched the GPU) and return its exit code."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log("bench: launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    return subprocess.run(cmd).returncode
+
+
+PARAMS = {"mfcc_bgru": 6435852, "fbanks_cnn": 1439244, "spec_bgru": 7302156, "resnet_bgru": 27494573}
+
+
+def plumbing(args, rank, world):
+    """--cpu-plumbing: the multi-rank harness on CPU (gloo): a flat-buffer all-reduce of the model's
+    gradient size as the step, the same barrier / max-over-ranks timing and rank-0 JSON line."""
+    import torch.distributed as dist
+    grad = torch.ones(PARAMS.get(args.model, 1 << 20))
+    for _ in range(args.warmup):
+        parallel.allreduce_grads(types.SimpleNamespace(grad=grad))
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        parallel.allreduce_grads(types.SimpleNamespace(grad=grad))
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "cpu plumbing check (not a measurement)", "value": None, "unit": "utt/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "none (gloo all-reduce only)",
+                          "config": {"workload": "plumbing", "model": args.model, "parallelism": "dp%d" % world}}),
+              flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -181,9 +272,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true")
     ap.add_argument("--no-feature-roofline", "--no-mfcc-roofline", dest="no_feature_roofline", action="store_true")
+    ap.add_argument("--cpu-plumbing", action="store_true",
+                    help="exercise the N-rank launch / timing / JSON path over gloo on CPU (no GPU; no measurement)")
     args = ap.parse_args()
 
-    rank, world, local = parallel.init_from_env()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_relaunch(args))
+    rank, world, local = parallel.init_from_env(backend="gloo" if args.cpu_plumbing else None)
+    if world != args.gpus:
+        raise SystemExit("bench: --gpus %d but the process group has %d ranks" % (args.gpus, world))
+    if args.cpu_plumbing:
+        plumbing(args, rank, world)
+        return
     features.require_gpu()
     _lib.lib()
     loss_scale = 1.0
@@ -287,6 +387,8 @@ def main():
               "kernels": {k: {"launches": v["launches"], "ms_total": v["ms_total"]} for k, v in lp_kernels.items()}}
         _lib.set_matmul_precision(args.precision)
 
+    # a persistent kernel that timed out invalidates every number above: fail loudly
+    _lib.check_health(sync=True)
     if rank != 0:
         return
     value = world * B * args.steps / el
@@ -309,7 +411,7 @@ def main():
     if not args.no_feature_roofline and args.model in FEATURE:
         res["feature_roofline"] = feature_roofline(args.model)
     if world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(args.model, 32, args.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(args.model, B, args.cpu_seconds)
     print(json.dumps(res), flush=True)
 
 

@@ -31,6 +31,7 @@ enum srk_status {
   SRK_ERR_INVALID = -1,   /* bad argument (shape, null pointer, unsupported option) */
   SRK_ERR_HIP = -2,       /* a HIP runtime call failed */
   SRK_ERR_INTERNAL = -3,  /* anything else (host exception) */
+  SRK_ERR_TIMEOUT = -4,   /* a persistent kernel's bounded spin-wait gave up: results are invalid */
 };
 
 /* ---------------------------------------------------------------- library / device */
@@ -53,6 +54,12 @@ int srk_set_option(const char* name, int64_t value);
 /* Number of bounded spin-waits of the persistent kernels that gave up (synchronizes the
  * device; must stay 0 — a non-zero value means a co-residency assumption failed).  -1 on error. */
 int64_t srk_spin_timeouts(void);
+/* Fatal-timeout check: SRK_OK, or SRK_ERR_TIMEOUT (sticky until srk_health_reset) once any
+ * persistent-kernel spin-wait has given up.  Reads a host-pinned word the kernels raise, so with
+ * sync = 0 it costs no device synchronization (it sees timeouts of work the GPU has reached);
+ * sync = 1 synchronizes the device first.  Option "gru_spin_limit" (test hook) shortens the wait. */
+int srk_health_check(int sync);
+int srk_health_reset(void);
 
 /* ---------------------------------------------------------------- feature extraction
  * pcm: float32 [n_clips, 16000], int16-valued (NOT scaled to +-1), exactly what

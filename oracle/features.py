@@ -60,7 +60,14 @@ def fbank_matrix():
 _FBANK = None
 
 
-def filter_banks(sample):
+def fbank_frame_index():
+    """int64[98, 400] sample index read by (frame f, tap n): ``160 f + n`` into the pre-emphasised,
+    zero-appended signal (model_fbanks_cnn.py:32-40; max 15919, so the 80 appended zeros are never
+    read)."""
+    return FB_FRAME_STEP * np.arange(FB_NUM_FRAMES)[:, None] + np.arange(FB_FRAME_LEN)[None, :]
+
+
+def filter_banks(sample, index=None):
     """float32[16000] PCM (int16-valued) -> float32[98, 120] log-mel (dB), time x mel.
 
     Restates models/model_fbanks_cnn.py:15-66.  Precision follows numpy exactly: the
@@ -74,7 +81,7 @@ def filter_banks(sample):
     emph = np.append(signal[0], signal[1:] - np.float32(FB_PRE_EMPHASIS) * signal[:-1])   # :21
     pad_len = FB_NUM_FRAMES * FB_FRAME_STEP + FB_FRAME_LEN                              # :32
     pad = np.append(emph, np.zeros(pad_len - len(emph)))                                 # :33-34 -> f64
-    idx = (np.arange(FB_FRAME_LEN)[None, :] + FB_FRAME_STEP * np.arange(FB_NUM_FRAMES)[:, None])
+    idx = fbank_frame_index() if index is None else index
     frames = pad[idx] * np.hamming(FB_FRAME_LEN)                                         # :36-41
     mag = np.abs(np.fft.rfft(frames, FB_NFFT))                                           # :43
     pow_frames = (1.0 / FB_NFFT) * mag ** 2                                              # :44
@@ -105,7 +112,13 @@ def tukey_window(n=SPEC_NPERSEG, alpha=0.25):
     return w[:n]
 
 
-def compute_spec(sample, transposed=False):
+def spec_frame_index():
+    """int64[49, 640] sample index of (frame f, tap n): ``320 f + n`` (scipy.signal.spectrogram with
+    nperseg=640, noverlap=320: no padding, the last 320 samples' second half never starts a frame)."""
+    return (SPEC_NPERSEG - SPEC_NOVERLAP) * np.arange(SPEC_NUM_FRAMES)[:, None] + np.arange(SPEC_NPERSEG)[None, :]
+
+
+def compute_spec(sample, transposed=False, index=None):
     """float32[16000] -> float32[321, 49] (freq x time); [49, 321] if ``transposed``
     (models/model_spec_cnn.py:14 applies ``.T``).
 
@@ -116,7 +129,7 @@ def compute_spec(sample, transposed=False):
     """
     x = np.asarray(sample, dtype=np.float64)
     w = tukey_window()
-    idx = np.arange(SPEC_NPERSEG)[None, :] + (SPEC_NPERSEG - SPEC_NOVERLAP) * np.arange(SPEC_NUM_FRAMES)[:, None]
+    idx = spec_frame_index() if index is None else index
     spec = np.abs(np.fft.rfft(x[idx] * w, SPEC_NPERSEG)) ** 2
     spec *= 1.0 / (SR * np.sum(w * w))
     spec[:, 1:-1] *= 2.0
@@ -187,15 +200,32 @@ _MEL = None
 _DCT = None
 
 
-def mfcc13(sample):
-    """librosa.feature.mfcc(audio, 16000, n_mfcc=13, n_fft=640, hop_length=320) -> f64[13, 51]."""
+def mfcc_frame_index():
+    """int64[51, 640] ORIGINAL-clip sample index of (frame f, tap n) under librosa's
+    ``stft(center=True, pad_mode='reflect')``: ``src = 320 f + n - 320`` into
+    ``np.pad(x, 320, 'reflect')``, i.e. src < 0 -> -src and src > 15999 -> 31998 - src
+    (p[:3] = x[320, 319, 318], p[-3:] = x[15681, 15680, 15679])."""
+    src = MFCC_HOP * np.arange(MFCC_NUM_FRAMES)[:, None] + np.arange(MFCC_NFFT)[None, :] - MFCC_NFFT // 2
+    src = np.where(src < 0, -src, src)
+    return np.where(src > SEQ_LENGTH - 1, 2 * (SEQ_LENGTH - 1) - src, src)
+
+
+def mfcc13(sample, index=None):
+    """librosa.feature.mfcc(audio, 16000, n_mfcc=13, n_fft=640, hop_length=320) -> f64[13, 51].
+
+    ``index`` (test hook): an alternative [51, 640] table of original-clip sample indices in place
+    of :func:`mfcc_frame_index` (used to show that the parity tests reject a wrong index table)."""
     global _MEL, _DCT
     if _MEL is None:
         _MEL, _DCT = mel_matrix(), dct_matrix()
     y = np.asarray(sample, dtype=np.float32)
-    p = np.pad(y, MFCC_NFFT // 2, mode="reflect")                       # stft(center=True, 'reflect')
-    idx = np.arange(MFCC_NFFT)[None, :] + MFCC_HOP * np.arange(MFCC_NUM_FRAMES)[:, None]
-    frames = p[idx].astype(np.float64) * hann_periodic()                 # f64 window * f32 frames
+    if index is None:
+        p = np.pad(y, MFCC_NFFT // 2, mode="reflect")                   # stft(center=True, 'reflect')
+        idx = np.arange(MFCC_NFFT)[None, :] + MFCC_HOP * np.arange(MFCC_NUM_FRAMES)[:, None]
+        fr = p[idx]
+    else:
+        fr = y[index]
+    frames = fr.astype(np.float64) * hann_periodic()                     # f64 window * f32 frames
     stft = np.fft.rfft(frames, axis=1).astype(np.complex64)              # stored complex64 (0.6)
     S = (np.abs(stft) ** 2).T                                            # f32 [321, 51]
     mel = _MEL @ S                                                       # f64 [128, 51]
@@ -204,9 +234,9 @@ def mfcc13(sample):
     return _DCT @ db                                                     # [13, 51] f64
 
 
-def compute_mfcc(sample):
+def compute_mfcc(sample, index=None):
     """float32[16000] -> float32[39, 51] = [mfcc; d mfcc; dd mfcc] (model_mfcc_bgru.py:11-19)."""
-    m = mfcc13(sample)
+    m = mfcc13(sample, index)
     d = np.gradient(m, axis=1)                                           # :14
     dd = np.gradient(d, axis=1)                                          # :16
     return np.concatenate((m, d, dd)).astype(np.float32)                # :15-18

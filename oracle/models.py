@@ -76,6 +76,19 @@ class SpecBGRU(nn.Module):
         return self.fc(out[:, -1, :])
 
 
+class MaskDropout(nn.Module):
+    """``nn.Dropout(p)`` with the Bernoulli(1 - p) keep mask supplied instead of drawn:
+    y = x * keep / (1 - p) in training mode, identity in eval (the draw the reference's
+    model_fbanks_cnn.py:79,98 would make is exported into the golden fixture instead)."""
+
+    def __init__(self, keep, p=0.5):
+        super().__init__()
+        self.keep, self.p = torch.as_tensor(keep, dtype=torch.float32), p
+
+    def forward(self, x):
+        return x * self.keep / (1.0 - self.p) if self.training else x
+
+
 # ---------------------------------------------------------------- model_fbanks_cnn.py:68-102
 class FbanksCNN(nn.Module):
     def __init__(self):

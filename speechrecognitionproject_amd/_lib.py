@@ -31,6 +31,8 @@ _SIGS = {
                       ctypes.POINTER(ctypes.c_double)],
     "srk_set_option": [ctypes.c_char_p, _I64],
     "srk_spin_timeouts": [],
+    "srk_health_check": [_I],
+    "srk_health_reset": [],
     "srk_fbank_fwd": [_P, _I64, _P, _P],
     "srk_mfcc_fwd": [_P, _I64, _P, _I, _P],
     "srk_spec_fwd": [_P, _I64, _P, _I, _P],
@@ -161,6 +163,12 @@ class precision_scope:
 def spin_timeouts():
     """Persistent-kernel spin waits that gave up since load (synchronizes; must stay 0)."""
     return int(lib().srk_spin_timeouts())
+
+
+def check_health(sync=False):
+    """Raise SrkError if a persistent kernel's spin-wait has ever timed out (its results are
+    invalid).  sync=False reads a host-pinned word without synchronizing the device."""
+    call("srk_health_check", 1 if sync else 0)
 
 
 def header_symbols():

@@ -43,6 +43,8 @@ struct GruPArgs {
   const float* b_ih;     // [2][3H]
   int in;
   unsigned long long* trace;   // optional per-(workgroup, step) timestamps (tools/gru_trace.py)
+  unsigned* health;      // host-pinned, device-mapped word: set when a spin-wait gives up (srk_health_check)
+  unsigned spin_limit;   // s_sleep polls before a wait gives up (~2 s by default)
 };
 
 size_t fwd_lds_bytes(int H);
@@ -55,5 +57,9 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s);
 // Runtime options (srk_set_option): persistent GRU recurrence on/off (default on).
 extern int g_opt_gru_persistent;
 extern unsigned long long* g_opt_gru_trace;   // device buffer or nullptr
+extern unsigned g_opt_gru_spin_limit;          // 0 = default (~2 s); test hook "gru_spin_limit"
+// Host-pinned health word (device-mapped pointer in *dev): non-zero once any persistent-kernel
+// spin-wait has given up; read without a device synchronization by srk_health_check.
+int health_word(unsigned** host, unsigned** dev);
 
 }  // namespace srk

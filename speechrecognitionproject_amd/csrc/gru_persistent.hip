@@ -25,8 +25,10 @@
 // must be resident at once; the host checks the occupancy query against the CU count and falls
 // back to the per-step kernels otherwise, and splits larger batches into 64*G-row chunk launches.
 // Every spin is bounded: a workgroup that waits ~2 s gives up, bumps g_spin_timeouts (read by
-// srk_spin_timeouts(); the tests assert it stays 0) and carries on, so a fault can never hang the
-// GPU.
+// srk_spin_timeouts()) and raises the host-pinned health word, then carries on so a fault can never
+// hang the GPU.  The results of that launch are invalid, so a timeout is FATAL to the caller:
+// srk_health_check() (no device sync) returns SRK_ERR_TIMEOUT from then on; the optimizer step,
+// training.py's loss flush and bench.py check it and raise.
 #include <cstdlib>
 #include <type_traits>
 #include <mutex>
@@ -69,13 +71,20 @@ __device__ __forceinline__ void st4_sc1(__amdgpu_buffer_rsrc_t r, unsigned byte_
 
 // One lane of the workgroup waits until *cnt >= target (relaxed agent-scope = sc1 load), then
 // the whole workgroup passes a barrier.  Bounded.
-__device__ __forceinline__ void wait_count(unsigned* cnt, unsigned target) {
+// A wait that gave up: count it and raise the host-visible health word (a vector store to
+// host-coherent memory at system scope).
+__device__ __forceinline__ void spin_gave_up(const GruPArgs& a) {
+  atomicAdd(&g_spin_timeouts, 1ull);
+  if (a.health) __hip_atomic_store(a.health, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void wait_count(const GruPArgs& a, unsigned* cnt, unsigned target) {
   if (threadIdx.x == 0) {
     unsigned spins = 0;
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins >= kSpinLimit) {
-        atomicAdd(&g_spin_timeouts, 1ull);
+      if (++spins >= a.spin_limit) {
+        spin_gave_up(a);
         break;
       }
     }
@@ -97,7 +106,7 @@ __device__ __forceinline__ void arrive(unsigned* cnt) {
 // forms" row 1 (a sharded flag, every shard polled).  Replaces the atomic add at the memory side.
 __device__ __forceinline__ void sync_wait(const GruPArgs& a, unsigned* cnt, int dir, int group, int S, int step) {
   if (!a.flags) {
-    wait_count(cnt, (unsigned)S * step);
+    wait_count(a, cnt, (unsigned)S * step);
     return;
   }
   if (threadIdx.x < 64) {
@@ -108,8 +117,8 @@ __device__ __forceinline__ void sync_wait(const GruPArgs& a, unsigned* cnt, int 
       const unsigned v = lane < S ? __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xffffffffu;
       if (__all(v >= (unsigned)step)) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins >= kSpinLimit) {
-        if (lane == 0) atomicAdd(&g_spin_timeouts, 1ull);
+      if (++spins >= a.spin_limit) {
+        if (lane == 0) spin_gave_up(a);
         break;
       }
     }
@@ -958,6 +967,9 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
   for (int c0 = 0; c0 < a.B; c0 += rows_per_launch) {
     GruPArgs ac = a;
     ac.trace = g_opt_gru_trace;
+    unsigned* health_host = nullptr;
+    if (int rc = health_word(&health_host, &ac.health)) return rc;
+    ac.spin_limit = g_opt_gru_spin_limit ? g_opt_gru_spin_limit : kSpinLimit;
     static const int flags_env = [] { const char* v = getenv("SRK_GRU_FLAGS"); return v && *v ? atoi(v) : 0; }();
     ac.flags = flags_env;
     ac.b_begin = c0;
@@ -977,6 +989,50 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
 }
 
 }  // namespace srk
+
+namespace srk {
+int health_word(unsigned** host, unsigned** dev) {
+  static std::mutex mu;
+  static unsigned* h = nullptr;
+  static unsigned* d = nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!h) {
+    void* p = nullptr;
+    SRK_CHECK_HIP(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
+    *static_cast<volatile unsigned*>(p) = 0;
+    void* dp = nullptr;
+    SRK_CHECK_HIP(hipHostGetDevicePointer(&dp, p, 0));
+    h = static_cast<unsigned*>(p);
+    d = static_cast<unsigned*>(dp);
+  }
+  *host = h;
+  *dev = d;
+  return SRK_OK;
+}
+}  // namespace srk
+
+extern "C" int srk_health_check(int sync) {
+  SRK_API_BEGIN
+  if (sync) SRK_CHECK_HIP(hipDeviceSynchronize());
+  unsigned *h = nullptr, *d = nullptr;
+  if (int rc = srk::health_word(&h, &d)) return rc;
+  const unsigned v = __atomic_load_n(h, __ATOMIC_ACQUIRE);
+  SRK_REQUIRE(v == 0, SRK_ERR_TIMEOUT,
+              "a persistent GRU kernel's spin-wait timed out (its workgroups were not all co-resident): "
+              "the recurrence results since then are invalid");
+  return SRK_OK;
+  SRK_API_END
+}
+
+extern "C" int srk_health_reset(void) {
+  SRK_API_BEGIN
+  SRK_CHECK_HIP(hipDeviceSynchronize());
+  unsigned *h = nullptr, *d = nullptr;
+  if (int rc = srk::health_word(&h, &d)) return rc;
+  __atomic_store_n(h, 0u, __ATOMIC_RELEASE);
+  return SRK_OK;
+  SRK_API_END
+}
 
 extern "C" int64_t srk_spin_timeouts(void) {
   unsigned long long v = 0;

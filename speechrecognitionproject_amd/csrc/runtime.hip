@@ -22,6 +22,7 @@ int g_opt_gru_persistent = 1;
 static std::atomic<int> g_opt_matmul_prec{kPrecF32};
 int matmul_prec() { return g_opt_matmul_prec.load(std::memory_order_relaxed); }
 unsigned long long* g_opt_gru_trace = nullptr;
+unsigned g_opt_gru_spin_limit = 0;
 
 static thread_local std::string g_last_error;
 
@@ -278,6 +279,11 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "matmul_precision") {   // 0 fp32, 1 bf16, 2 fp16 matrix-core operands (fp32 accumulate)
     SRK_REQUIRE(value >= 0 && value <= 2, SRK_ERR_INVALID, "matmul_precision must be 0, 1 or 2");
     srk::g_opt_matmul_prec.store((int)value);
+    return SRK_OK;
+  }
+  if (n == "gru_spin_limit") {   // test hook: polls before a persistent wait gives up (0 = ~2 s default)
+    SRK_REQUIRE(value >= 0 && value <= 0xffffffffLL, SRK_ERR_INVALID, "gru_spin_limit out of range");
+    srk::g_opt_gru_spin_limit = (unsigned)value;
     return SRK_OK;
   }
   if (n == "gru_trace_ptr") {   // diagnostics: device buffer of 8 x u64 per (workgroup, step), 0 = off

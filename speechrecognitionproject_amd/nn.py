@@ -34,11 +34,24 @@ def _dir_pair(a, b):
     return torch.stack([a, b])
 
 
+def _flat_grad(p):
+    """p.grad when p is owned by a FlatParams (optim.py) and its .grad is still that buffer's view:
+    the one case where a backward may accumulate into .grad in place (beta = 1 in the GEMM
+    epilogue) and hand autograd None.  Any other parameter (plain torch optimizers, DDP,
+    torch.autograd.grad) gets its gradient returned to autograd as usual, so AccumulateGrad and
+    its hooks run."""
+    flat = getattr(p, "_srk_flat", None)
+    g = p.grad
+    if flat is None or g is None or not flat.owns_grad(p):
+        return None
+    return g
+
+
 def _grad_pair(a, b):
-    """The stacked .grad of a direction pair to ACCUMULATE into in place (autograd's own
-    accumulation, fused into the kernels' epilogues), or None when the grads are not adjacent
-    buffers (then the gradient is returned to autograd as usual)."""
-    ga, gb = a.grad, b.grad
+    """The stacked .grad of a FlatParams-owned direction pair to ACCUMULATE into in place
+    (autograd's own accumulation, fused into the kernels' epilogues), or None (then the gradient
+    is returned to autograd as usual)."""
+    ga, gb = _flat_grad(a), _flat_grad(b)
     if ga is None or gb is None or not _adjacent(ga, gb):
         return None
     return _dir_pair(ga, gb)
@@ -163,8 +176,8 @@ class _LinearFn(torch.autograd.Function):
         # accumulate straight into the parameters' existing .grad buffers (beta = 1, fused into the
         # GEMM epilogue) instead of returning a fresh gradient for autograd to add
         wp, bp = ctx.params
-        gw = wp.grad if wp.grad is not None and wp.grad.is_contiguous() else None
-        gb = bp.grad if bp is not None and bp.grad is not None and bp.grad.is_contiguous() else None
+        gw = _flat_grad(wp)
+        gb = _flat_grad(bp) if bp is not None else None
         acc = gw is not None and (not want_db or gb is not None)
         if ctx.needs_input_grad[1]:
             dw = gw if acc else torch.empty((N, K), device=x.device)
@@ -425,21 +438,58 @@ class _DropoutFn(torch.autograd.Function):
         return dx, None, None
 
 
+class _DropoutMaskFn(torch.autograd.Function):
+    """y = x * keep / (1 - p) with a caller-supplied uint8 keep mask (srk_dropout_apply both ways)."""
+
+    @staticmethod
+    def forward(ctx, x, keep, scale):
+        x = x.contiguous()
+        _check_cuda(x, keep)
+        y = torch.empty_like(x)
+        call("srk_dropout_apply", ptr(x), ptr(keep), x.numel(), float(scale), ptr(y), stream_ptr())
+        ctx.save_for_backward(keep)
+        ctx.scale = scale
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (keep,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        call("srk_dropout_apply", ptr(dy), ptr(keep), dy.numel(), float(ctx.scale), ptr(dx), stream_ptr())
+        return dx, None, None
+
+
 class Dropout(tnn.Module):
     """nn.Dropout(p=0.5): identity in eval mode; in training a Bernoulli(1-p) mask from a
-    counter-based hash seeded per call (seed advances every forward)."""
+    counter-based hash.  The per-call seed is drawn from torch's default generator (so
+    ``torch.manual_seed`` governs the masks, as it does the reference's nn.Dropout) and folded with
+    the data-parallel rank, so ranks holding different clips draw independent masks.
 
-    def __init__(self, p=0.5, seed=0):
+    ``set_mask(keep)`` supplies the keep mask (uint8, the input's shape) for the NEXT training
+    forward instead of drawing one — how the parity tests replay a mask exported from the
+    reference (tests/golden/fbanks_cnn_train_golden.npz)."""
+
+    def __init__(self, p=0.5):
         super().__init__()
         self.p = p
-        self._seed = int(seed) * 1000003 + 12345
-        self._calls = 0
+        self._keep = None
+
+    def set_mask(self, keep):
+        self._keep = keep
 
     def forward(self, x):
         if not self.training or self.p == 0.0:
             return x
-        self._calls += 1
-        return _DropoutFn.apply(x, self.p, (self._seed + self._calls * 0x9E3779B1) & ((1 << 63) - 1))
+        if self._keep is not None:
+            keep, self._keep = self._keep.to(device=x.device, dtype=torch.uint8).contiguous(), None
+            if keep.shape != x.shape:
+                raise ValueError("Dropout.set_mask: mask shape %s != input shape %s" % (tuple(keep.shape), tuple(x.shape)))
+            return _DropoutMaskFn.apply(x, keep, 1.0 / (1.0 - self.p))
+        seed = int(torch.randint(0, 1 << 62, (1,)).item())
+        rank = torch.distributed.get_rank() if torch.distributed.is_available() and torch.distributed.is_initialized() else 0
+        seed = (seed ^ (rank * 0x9E3779B97F4A7C15)) & ((1 << 63) - 1)
+        return _DropoutFn.apply(x, self.p, seed)
 
 
 # ----------------------------------------------------------------------------- batch norm

@@ -7,7 +7,7 @@ tensor 256-byte aligned) and points ``p.grad`` at views of ONE gradient buffer, 
 """
 import torch
 
-from ._lib import call
+from ._lib import call, check_health
 from .features import ptr, require_gpu, stream_ptr
 
 _ALIGN = 64   # floats
@@ -47,6 +47,15 @@ class FlatParams:
                 self.data[o:o + k].copy_(p.data.reshape(-1))
                 p.data = self.data[o:o + k].view_as(p)
                 p.grad = self.grad[o:o + k].view_as(p)
+                p._srk_flat = self    # the layers may accumulate into this .grad in place (nn.py)
+        self._slot = {id(p): o for p, o in zip(self.params, offs)}
+
+    def owns_grad(self, p):
+        """p.grad is (still) this buffer's view for p."""
+        o = self._slot.get(id(p))
+        g = p.grad
+        return (o is not None and g is not None and g.is_contiguous()
+                and g.data_ptr() == self.grad.data_ptr() + o * self.grad.element_size())
 
     def zero_grad(self):
         self.grad.zero_()
@@ -83,4 +92,7 @@ class Adam(torch.optim.Optimizer):
         call("srk_adam_step", ptr(f.data), ptr(f.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq), f.numel,
              float(g["lr"]), float(b1), float(b2), float(g["eps"]), self.step_count, float(self.grad_scale),
              stream_ptr())
+        # a persistent kernel that timed out produced invalid gradients: fail loudly (a host-pinned
+        # word, no device sync; it sees every timeout of the work the GPU has reached so far)
+        check_health(sync=False)
         return loss

@@ -7,6 +7,7 @@ north_star.  Ranks are launched by ``torch.distributed.run`` (RANK / LOCAL_RANK 
 MASTER_ADDR / MASTER_PORT in the environment).  On a CPU-only host the same code runs over gloo
 (tests/test_parallel.py).
 """
+import datetime
 import os
 
 import torch
@@ -25,7 +26,10 @@ def init_from_env(backend=None):
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+        # a long timeout: rank 0 alone runs the reference's per-epoch accuracy passes while the other
+        # ranks wait at a barrier (training.py)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=int(os.environ.get("SRK_DIST_TIMEOUT", "7200"))))
     elif torch.cuda.is_available():
         torch.cuda.set_device(local)
     return rank, world, local
@@ -33,6 +37,11 @@ def init_from_env(backend=None):
 
 def world_size():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def barrier():
+    if world_size() > 1:
+        dist.barrier()
 
 
 def broadcast_flat(flat):

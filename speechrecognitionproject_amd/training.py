@@ -24,6 +24,7 @@ import torch
 from torch.utils.data import DataLoader
 
 from . import parallel
+from ._lib import check_health
 from .nn import CrossEntropyLoss
 from .optim import Adam, FlatParams
 
@@ -100,6 +101,19 @@ def main(argv=None):
         else:
             loader = DataLoader(data, batch_size=args.batch_size, shuffle=True, drop_last=False)
         pending = []
+
+        def flush():
+            # every rank drains its buffered losses (and fails loudly on a persistent-kernel
+            # timeout); only rank 0 writes the reference's loss file (training.py:94-95)
+            nonlocal pending
+            vals = torch.stack(pending).tolist() if pending else []
+            check_health(sync=True)
+            if rank == 0 and vals:
+                with open(loss_file, 'a') as f:
+                    for v in vals:
+                        f.write(str(v) + '\n')
+            pending = []
+
         for batch in loader:
             optimizer.zero_grad()
             outputs = model(batch['audio'])
@@ -108,18 +122,15 @@ def main(argv=None):
             parallel.allreduce_grads(flat)
             optimizer.step()
             pending.append(loss.detach())
-            if len(pending) >= args.log_every and rank == 0:
-                with open(loss_file, 'a') as f:
-                    for v in torch.stack(pending).tolist():
-                        f.write(str(v) + '\n')
-                pending = []
-        if pending and rank == 0:
-            with open(loss_file, 'a') as f:
-                for v in torch.stack(pending).tolist():
-                    f.write(str(v) + '\n')
+            if len(pending) >= args.log_every:
+                flush()
+        flush()
         if not args.no_eval and rank == 0:
             mod.accuracy(model, valset, os.path.join(args.output_path, 'val_' + key + '.txt'), 4)
             mod.accuracy(model, data, os.path.join(args.output_path, 'train_' + key + '.txt'), 4)
+            check_health(sync=True)
+        if world > 1:
+            parallel.barrier()    # the other ranks wait here (long timeout), not inside a collective
         epoch += 1
         if hasattr(data, 'resample_unknown_class'):
             data.resample_unknown_class()

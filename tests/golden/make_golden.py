@@ -88,12 +88,26 @@ if ONLY:
     np.savez_compressed = _savez_only
 
 
-def model_golden(name, net, x, labels, train_mode=False):
+class _MaskDropout(torch.nn.Module):
+    """Stands in for the reference's ``nn.Dropout`` (model_fbanks_cnn.py:79,98) with an exported
+    Bernoulli(1 - p) keep mask: y = x * keep / (1 - p), what nn.Dropout computes for that draw."""
+
+    def __init__(self, keep, p=0.5):
+        super().__init__()
+        self.keep, self.p = keep, p
+
+    def forward(self, x):
+        return x * self.keep / (1.0 - self.p) if self.training else x
+
+
+def model_golden(name, net, x, labels, train_mode=False, dropout_keep=None):
     if ONLY and name not in ONLY:
         return
     sd = OM.seeded_state_dict(net, seed=0)
     net.load_state_dict(sd)
     net.train(train_mode)
+    if dropout_keep is not None:
+        net.dropout = _MaskDropout(torch.from_numpy(dropout_keep.astype(np.float32)))
     opt = torch.optim.Adam(net.parameters(), lr=1e-4)
     before = {k: v.detach().clone() for k, v in net.named_parameters()}
     opt.zero_grad()
@@ -104,6 +118,8 @@ def model_golden(name, net, x, labels, train_mode=False):
     opt.step()
     rec = {"pcm": x, "labels": labels, "logits": out.detach().numpy(), "loss": np.float32(loss.item()),
            "train_mode": np.int64(train_mode), "names": np.array(list(grads.keys()))}
+    if dropout_keep is not None:
+        rec["dropout_keep"] = dropout_keep.astype(np.uint8)
     for k in grads:
         gi, gv = sample_entries(grads[k])
         di, dv = sample_entries(dict(net.named_parameters())[k].detach() - before[k])
@@ -252,6 +268,9 @@ def main():
     x, y = synthetic_clips(4, seed=5)
     torch.manual_seed(0)
     model_golden("fbanks_cnn_golden.npz", R_fb.Network(), x, y, train_mode=False)
+    # train mode: dropout on [B, 512] after maxpool3 with an exported keep mask
+    keep = (np.random.default_rng(55).random((4, 512)) >= 0.5).astype(np.uint8)
+    model_golden("fbanks_cnn_train_golden.npz", R_fb.Network(), x, y, train_mode=True, dropout_keep=keep)
     model_golden("mfcc_bgru_golden.npz", R_mb.Network(), x, y)
     model_golden("spec_bgru_golden.npz", R_sb.Network(), x, y)
     x2, y2 = synthetic_clips(2, seed=6)

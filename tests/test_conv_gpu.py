@@ -119,13 +119,33 @@ def test_dropout_mask(gpu):
     assert d(x) is x
 
 
-def test_fbanks_cnn_vs_reference_golden(gpu):
-    g = golden("fbanks_cnn_golden.npz")
+def test_dropout_follows_torch_seed(gpu):
+    d = snn.Dropout(0.5).cuda()
+    x = torch.ones(4096, device="cuda")
+    torch.manual_seed(3)
+    a = d(x)
+    torch.manual_seed(3)
+    b = d(x)
+    assert torch.equal(a, b)
+    keep = (torch.arange(4096, device="cuda") % 3 == 0).to(torch.uint8)
+    d.set_mask(keep)
+    assert torch.equal(d(x), keep.float() * 2.0)
+    assert not torch.equal(d(x), keep.float() * 2.0)     # the supplied mask is used once
+
+
+@pytest.mark.parametrize("fixture", ["fbanks_cnn_golden.npz", "fbanks_cnn_train_golden.npz"])
+def test_fbanks_cnn_vs_reference_golden(gpu, fixture):
+    # the train-mode fixture replays the reference's dropout (model_fbanks_cnn.py:79,98) with the
+    # keep mask it exported, through srk_dropout_apply
+    g = golden(fixture)
     net = model_fbanks_cnn.Network().cuda()
     ref_sd = OM.seeded_state_dict(OM.FbanksCNN(), 0)
     assert list(net.state_dict().keys()) == list(ref_sd.keys())
     net.load_state_dict(ref_sd)
     net.train(bool(g["train_mode"]))
+    if "dropout_keep" in g:
+        assert net.training
+        net.dropout.set_mask(torch.from_numpy(g["dropout_keep"]))
     params = dict(net.named_parameters())
     before = {k: v.detach().clone() for k, v in params.items()}
     opt = Adam(net.parameters(), lr=1e-4)

@@ -103,7 +103,9 @@ def _emulate_bigru(x, sd, H, L, prec):
     return h_in
 
 
-@pytest.mark.parametrize("B,T,IN,L", [(70, 9, 39, 2), (256, 6, 321, 1)])
+# B = 300 / 512: more rows than one persistent launch holds (256), so the recurrence runs as two
+# batch-chunk launches (b_begin > 0) — the path cfg4 / cfg5 take at their per-GPU batch of 512
+@pytest.mark.parametrize("B,T,IN,L", [(70, 9, 39, 2), (256, 6, 321, 1), (300, 5, 39, 2), (512, 4, 321, 1)])
 def test_bigru_lowprec_forward_matches_emulation(prec, B, T, IN, L):
     from tolerances import GRU_LOWPREC_EMU_ABS
     from speechrecognitionproject_amd import nn as snn
@@ -126,9 +128,10 @@ def test_bigru_lowprec_forward_matches_emulation(prec, B, T, IN, L):
     assert _lib.spin_timeouts() == 0
 
 
-def test_bigru_lowprec_grads_close_to_fp32(prec):
+@pytest.mark.parametrize("B", [96, 512])
+def test_bigru_lowprec_grads_close_to_fp32(prec, B):
     from speechrecognitionproject_amd import nn as snn
-    B, T, IN, H, L = 96, 8, 39, 512, 2
+    T, IN, H, L = 8, 39, 512, 2
     torch.manual_seed(4)
     ref = torch.nn.GRU(IN, H, num_layers=L, bidirectional=True, batch_first=True)
     mine = snn.BiGRU(IN, H, num_layers=L).cuda()
@@ -177,6 +180,39 @@ def test_model_lowprec_logits_vs_reference_golden(prec, name):
     assert abs(loss.item() - float(g["loss"])) <= LOGITS_REL_LOWPREC * max(1.0, abs(float(g["loss"])))
     for p in net.parameters():
         assert p.grad is None or torch.isfinite(p.grad).all()
+
+
+@pytest.mark.parametrize("name,precision,B", [("mfcc_bgru", "bf16", 256), ("spec_bgru", "fp16", 512),
+                                              ("fbanks_cnn", "bf16", 512), ("spec_bgru", "bf16", 300)])
+def test_model_lowprec_at_config_batch(gpu, name, precision, B):
+    """BASELINE.json's configs at their own per-GPU batch (cfg2 bf16 B=256, cfg5 fp16 B=512, cfg3 in
+    bf16 at B=512): logits of the 16-bit mode vs the fp32 CPU oracle (<= 2e-2) and vs the fp32 HIP
+    path on the same clips; the persistent recurrence must not have timed out."""
+    import importlib
+    from oracle import models as OM
+    from tolerances import LOGITS_REL, LOGITS_REL_LOWPREC, rel_err
+    from speechrecognitionproject_amd.synthetic import synthetic_clips
+    ocls = {"mfcc_bgru": OM.MfccBGRU, "spec_bgru": OM.SpecBGRU, "fbanks_cnn": OM.FbanksCNN}[name]
+    mod = importlib.import_module("speechrecognitionproject_amd.models.model_" + name)
+    sd = OM.seeded_state_dict(ocls(), 0)
+    x, _ = synthetic_clips(B, seed=31, clip=30000)
+    net = mod.Network().cuda().eval()
+    net.load_state_dict(sd)
+    ref = ocls()
+    ref.load_state_dict(sd)
+    with torch.no_grad():
+        want = ref.eval()(torch.from_numpy(x)).numpy()
+        xd = torch.from_numpy(x).cuda()
+        fp32 = net(xd).cpu().numpy()
+        try:
+            _lib.set_matmul_precision(precision)
+            lp = net(xd).cpu().numpy()
+        finally:
+            _lib.set_matmul_precision("fp32")
+    assert rel_err(fp32, want) <= LOGITS_REL
+    assert rel_err(lp, want) <= LOGITS_REL_LOWPREC, rel_err(lp, want)
+    assert rel_err(lp, fp32) <= LOGITS_REL_LOWPREC
+    assert _lib.spin_timeouts() == 0
 
 
 # ----------------------------------------------------------------------------- convolutions

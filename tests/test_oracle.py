@@ -80,12 +80,15 @@ def test_noise_mix_oracle_vs_reference():
 @pytest.mark.parametrize("name,cls", [("fbanks_cnn", OM.FbanksCNN), ("mfcc_bgru", OM.MfccBGRU),
                                       ("spec_bgru", OM.SpecBGRU), ("resnet_bgru", OM.ResnetBGRU),
                                       ("mfrn_bgru", OM.MfrnBGRU), ("cnn_bgru", OM.CnnBGRU),
-                                      ("spec_cnn", OM.SpecCNN), ("analyst", OM.Analyst)])
+                                      ("spec_cnn", OM.SpecCNN), ("analyst", OM.Analyst),
+                                      ("fbanks_cnn_train", OM.FbanksCNN)])
 def test_model_oracle_vs_reference(name, cls):
     g = golden(name + "_golden.npz")
     net = cls()
     net.load_state_dict(OM.seeded_state_dict(net, 0))
     net.train(bool(g["train_mode"]))
+    if "dropout_keep" in g:
+        net.dropout = OM.MaskDropout(g["dropout_keep"])
     params = dict(net.named_parameters())
     before = {k: v.detach().clone() for k, v in params.items()}
     out, loss, _ = OM.train_step(net, torch.from_numpy(g["pcm"]), torch.from_numpy(g["labels"]))
@@ -96,3 +99,25 @@ def test_model_oracle_vs_reference(name, cls):
         assert rel_err(gv, g["gval__" + k]) <= 1e-4, k
         dv = (params[k].detach() - before[k]).reshape(-1).numpy()[g["gidx__" + k]]
         assert np.abs(dv - g["dval__" + k]).max() <= 2e-6, k
+
+
+def test_frame_index_tables():
+    # SURVEY.md Appendix A "Frame/window index tables", stated as integer arithmetic and checked
+    # against the padding / framing numpy itself performs in the reference's code paths
+    T = OF.mfcc_frame_index()
+    assert T.shape == (51, 640) and T.min() == 0 and T.max() == 15999
+    y = np.random.default_rng(4).normal(size=16000).astype(np.float32)
+    p = np.pad(y, 320, mode="reflect")                                   # librosa stft(center=True)
+    assert np.array_equal(y[T], p[np.arange(640)[None] + 320 * np.arange(51)[:, None]])
+    assert list(p[:3]) == list(y[[320, 319, 318]]) and list(p[-3:]) == list(y[[15681, 15680, 15679]])
+    assert np.array_equal(OF.compute_mfcc(y), OF.compute_mfcc(y, T))
+    F = OF.fbank_frame_index()
+    assert F.shape == (98, 400) and F.max() == 15919 and np.array_equal(F[:, 0], 160 * np.arange(98))
+    assert np.array_equal(OF.filter_banks(y), OF.filter_banks(y, F))
+    S = OF.spec_frame_index()
+    assert S.shape == (49, 640) and S.max() == 15999 and np.array_equal(S[:, 0], 320 * np.arange(49))
+    assert np.array_equal(OF.compute_spec(y), OF.compute_spec(y, index=S))
+    # the golden fbank / spec vectors (reference outputs) are reproduced through the explicit tables
+    g = golden("fbank_golden.npz")
+    for c, ref in zip(g["pcm"], g["out"]):
+        assert np.array_equal(OF.filter_banks(c, F), ref)

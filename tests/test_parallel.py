@@ -162,3 +162,30 @@ def test_dp_equivalence_gpu_kernels(gpu):
     # batch only by fp32 summation order
     diff = (res[0] - flat.data.cpu()).abs()
     assert (diff <= 2e-6).float().mean().item() >= 0.999
+
+
+def test_bench_relaunches_itself_for_gpus_n():
+    """`python bench.py --gpus 2` (no WORLD_SIZE) starts 2 ranks through torch.distributed.run and
+    rank 0 prints one JSON line with n_gpus == 2 (CPU: --cpu-plumbing, gloo, no GPU work)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--cpu-plumbing"], capture_output=True, text=True, timeout=300, env=env, cwd=repo)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["config"]["parallelism"] == "dp2"
+
+
+def test_bench_rejects_world_size_mismatch():
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--cpu-plumbing"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=repo)
+    assert r.returncode != 0 and "process group has 1 ranks" in r.stderr

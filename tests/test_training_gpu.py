@@ -66,3 +66,24 @@ def test_training_on_wav_tree(gpu, tmp_path, loader):
     losses = [float(l) for l in open(out / "loss_w.txt")]
     assert len(losses) == 2 * 3 and all(np.isfinite(losses))      # 18 commands + 12 unknown + 12 silence = 42
     assert len(open(out / "val_w.txt").readlines()) == 2
+
+
+def test_spin_timeout_is_fatal(gpu, tmp_path):
+    """A persistent-kernel spin-wait that gives up must stop training (its results are invalid),
+    not continue silently.  The test hook "gru_spin_limit" = 1 makes every wait that is not
+    satisfied on its first poll give up; training.py must exit non-zero with the SrkError."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from speechrecognitionproject_amd import _lib\n"
+            "from speechrecognitionproject_amd.training import main\n"
+            "_lib.set_option('gru_spin_limit', 1)\n"
+            "main(['-key', 'x', '--model', 'mfcc_bgru', '--synthetic', '64', '--batch-size', '64', '--no-eval', "
+            "'--output-path', %r])\n") % (repo, str(tmp_path))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0, r.stdout + r.stderr
+    assert "SrkError" in r.stderr and "timed out" in r.stderr, r.stderr[-2000:]
+    # and in this (healthy) process the check passes
+    from speechrecognitionproject_amd import _lib
+    _lib.check_health(sync=True)

@@ -125,10 +125,15 @@ def cpu_baseline(model_name, batch, seconds):
     cls = {"mfcc_bgru": OM.MfccBGRU, "spec_bgru": OM.SpecBGRU, "fbanks_cnn": OM.FbanksCNN,
            "resnet_bgru": OM.ResnetBGRU, "mfrn_bgru": OM.MfrnBGRU, "cnn_bgru": OM.CnnBGRU,
            "spec_cnn": OM.SpecCNN}[model_name]
+    # the CPU share this process may use: OMP_NUM_THREADS where the host sets it (the GPU box gives
+    # each GPU 16 CPUs under a quota while affinity / os.cpu_count() show the whole machine — more
+    # threads than the quota only thrash), else the affinity mask
     try:
-        cores = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
+        affinity = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    cores = max(1, min(affinity, int(omp))) if omp.isdigit() else affinity
     prev_threads = torch.get_num_threads()
     torch.manual_seed(0)
     net = cls()
@@ -146,8 +151,10 @@ def cpu_baseline(model_name, batch, seconds):
             if el >= budget or n >= max_steps:
                 return n, el
 
+    log("cpu_baseline: %s on %d threads" % (model_name, cores))
     run(min(batch, 32), cores, 0.0, 1)                        # warm-up (allocator, thread pool)
     n, el = run(batch, cores, seconds, 50)
+    log("cpu_baseline: %d steps x %d clips in %.1f s; 1-thread leg" % (n, batch, el))
     # 1 thread: the config batch when one step fits ~seconds, else the largest multiple of 32 that does
     n1, el1 = run(32, 1, 0.0, 1)
     b1 = int(min(batch, max(32, (seconds / (el1 / 32)) // 32 * 32)))
@@ -165,8 +172,8 @@ def cpu_baseline(model_name, batch, seconds):
     cpu = _cpu_model()
     return {"value": round(n * batch / el, 2), "unit": "utt/s", "cores": cores, "kind": "port",
             "sample": "%d train steps x %d clips (the config batch; %s CPU restatement: per-clip numpy features + "
-                      "torch-CPU fp32 fwd/bwd + Adam), %.1f s on %d threads, %s (os.cpu_count() = %s)"
-                      % (n, batch, model_name, el, cores, cpu, os.cpu_count()),
+                      "torch-CPU fp32 fwd/bwd + Adam), %.1f s on %d threads, %s (affinity %d CPUs, os.cpu_count() = %s, "
+                      "OMP_NUM_THREADS = %s)" % (n, batch, model_name, el, cores, cpu, affinity, os.cpu_count(), omp or "unset"),
             "one_thread": {"value": round(n1 * b1 / el1, 2), "unit": "utt/s", "cores": 1,
                            "sample": "%d train step x %d clips, %.1f s" % (n1, b1, el1)},
             "cfg1": {"value": round(32 / el_mfcc, 2), "unit": "clips/s", "cores": 1,
@@ -329,6 +336,7 @@ def main():
     def timed(precision):
         """W warm-up + K timed steps at one matrix precision -> (seconds, kernel records, loss)."""
         nonlocal loss_scale
+        log("bench: %s %s, %d warm-up + %d timed steps" % (args.model, precision, args.warmup, args.steps))
         _lib.set_matmul_precision(precision)
         loss_scale = FP16_LOSS_SCALE if precision == "fp16" else 1.0
         opt.grad_scale = 1.0 / (world * loss_scale)
@@ -409,6 +417,7 @@ def main():
     if lp is not None:
         res["bf16"] = lp
     if not args.no_feature_roofline and args.model in FEATURE:
+        log("bench: feature roofline")
         res["feature_roofline"] = feature_roofline(args.model)
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.model, B, args.cpu_seconds)

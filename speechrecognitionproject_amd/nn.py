@@ -444,7 +444,9 @@ class _DropoutMaskFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, keep, scale):
         x = x.contiguous()
-        _check_cuda(x, keep)
+        _check_cuda(x)
+        if keep.device != x.device or keep.dtype != torch.uint8 or keep.numel() != x.numel():
+            raise _lib.SrkError("dropout keep mask must be a uint8 tensor of the input's size on its device")
         y = torch.empty_like(x)
         call("srk_dropout_apply", ptr(x), ptr(keep), x.numel(), float(scale), ptr(y), stream_ptr())
         ctx.save_for_backward(keep)

@@ -13,6 +13,13 @@
 * noise-mix (K4), frame/window indexing, dataset PCM: bit-exact.
 * logits: ||d||_inf / ||ref||_inf <= 1e-4 in fp32 mode; <= 2e-2 with bf16 / fp16 matrix-core
   operands (matmul_precision "bf16" / "fp16", SURVEY.md Appendix A, stated separately).
+  Spectrogram-fed models on tonal clips: the reference's own arithmetic (scipy's complex64
+  spectrogram) and the float64 restatement already differ by up to 2.5e-3 in logits (bins deep
+  under a tone's peak are float32 noise, and the GRU reads them as features; measured at B=512,
+  tests/test_lowprec_gpu.py).  There each clip is held to 1e-4 + 4 x that clip's own
+  reference-vs-restatement spread (logits_ok) — the HIP spectrogram is a third float32 rounding of
+  the same float64 quantity, so its distance to the restatement is of the reference's order, not
+  bounded by it — and the model half alone (the oracle model fed the HIP features) to 1e-4.
 * bf16 / fp16 GRU forward vs a float64 emulation of the same operand rounding: <= 2e-3 absolute on
   y (h in [-1, 1]; a rounding flip of one operand moves a gate pre-activation by ~1e-4).
 """
@@ -60,3 +67,35 @@ def spec_ok(out, ref):
 
 def rel_err(out, ref):
     return float(np.abs(np.asarray(out) - np.asarray(ref)).max() / max(np.abs(np.asarray(ref)).max(), 1e-30))
+
+
+def spec_reference_spread(oracle_net, pcm, oracle_logits):
+    """Per-clip |logits(scipy complex64 features) - logits(float64 restatement)|_inf / ||ref||_inf:
+    the float32 spread of the reference's OWN spectrogram (models/model_spec_bgru.py:11-17 calls
+    scipy.signal.spectrogram, which is importable here and on the GPU box) fed to the same oracle
+    model.  oracle_net: an oracle.models spec model (features in [B, 321, 49] via .features)."""
+    import scipy.signal as ss
+    import torch
+
+    def scipy_spec(c):
+        _, _, S = ss.spectrogram(c, fs=16000, nperseg=640, noverlap=320, detrend=False)
+        return np.log(S.astype(np.float32) + np.float32(1e-10))
+
+    feats = torch.from_numpy(np.stack([scipy_spec(c) for c in pcm]))
+    with torch.no_grad():
+        out, _ = oracle_net.gru(feats.transpose(1, 2))
+        alt = oracle_net.fc(out[:, -1, :]).numpy()
+    scale = max(np.abs(oracle_logits).max(), 1e-30)
+    return np.abs(alt - oracle_logits).max(axis=1) / scale
+
+
+def logits_ok(out, ref, spread=None):
+    """fp32-mode logits, per clip: ||d||_inf / ||ref||_inf <= LOGITS_REL (+ 4 x the reference's own
+    float32 spread of that clip when given) -> (ok, worst (clip, err, bound))."""
+    out = np.asarray(out, np.float64)
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(out - ref).max(axis=1) / max(np.abs(ref).max(), 1e-30)
+    bound = LOGITS_REL + (4.0 * np.asarray(spread) if spread is not None else 0.0)
+    bound = np.broadcast_to(bound, err.shape)
+    i = int(np.argmax(err - bound))
+    return bool((err <= bound).all()), (i, float(err[i]), float(bound[i]))

@@ -271,14 +271,7 @@ __global__ __launch_bounds__(256, 4) void spec_kernel(const float* __restrict__ 
   }
 }
 
-// ------------------------------------------------------------------------- K1 MFCC (v2)
-// Workgroup = 4 waves, persistent over clips (grid-stride), 2 workgroups per CU: the pass-A
-// twiddles and the Hann window are staged in LDS once per workgroup; the 16-tap mel windows
-// (filters lane and lane+64, [q][128] so a wave's loads coalesce), the untangle twiddles and the
-// DCT rows are read through L1.  Per clip the waves split the 17 chunks of 3 frames; the
-// per-clip top_db max is combined across the waves through LDS.
-constexpr int kMfWaves = 4;   // 2 workgroups (8 waves) per CU: LDS = 80,096 B each
-
+// ------------------------------------------------------------------------- K1 MFCC
 __device__ __forceinline__ void mfcc_load_chunk(const float* __restrict__ x, int c, int lane, v2f (&raw)[20]) {
   const int fa = lane >> 4, j = lane & 15;
   const int gf = 3 * c + (fa < 3 ? fa : 0);
@@ -296,141 +289,221 @@ __device__ __forceinline__ void mfcc_load_chunk(const float* __restrict__ x, int
   }
 }
 
-// 2 workgroups per CU need <= 256 VGPRs (no AGPR spill-over): waves_per_eu(2) and no prefetch
-// of the next chunk (measured: prefetch + 1 wave/SIMD 7.2 ms, prefetch + spills 4.95 ms, no
-// prefetch 4.65 ms per 65,536 clips).
-__global__ __launch_bounds__(64 * kMfWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void mfcc2_kernel(const float* __restrict__ pcm, float* __restrict__ out,
-                                                              int layout, int64_t n_clips, DeviceTables t) {
-  __shared__ v2f tbuf[kMfWaves][3 * 340];
-  __shared__ float pbuf[kMfWaves][3 * 321];
-  __shared__ __attribute__((aligned(16))) float db[51 * 132];   // row pitch 132: conflict-free b128 reads
-  __shared__ v2f s_tw[20 * 16];   // W320^(j k1) at [k1][j]
-  __shared__ float s_hann[640];
-  __shared__ float red[kMfWaves];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < 320; i += 64 * kMfWaves)
-    s_tw[i] = *reinterpret_cast<const v2f*>(t.tw320 + ((i >> 4) * (i & 15)));   // [k1][j]
-  for (int i = threadIdx.x; i < 640; i += 64 * kMfWaves) s_hann[i] = t.hann640f[i];
-  __syncthreads();
-  // mel windows / DCT / untangle twiddles stay in global memory (L1/L2-resident, coalesced)
-  const int lo0 = t.mel16_lo[lane], lo1 = t.mel16_lo[lane + 64];
-  const float* w0 = t.mel16_wt + lane;        // [q][128] layout: w0[q * 128]
-  const float* w1 = t.mel16_wt + lane + 64;
-  const v2f* __restrict__ s_post = reinterpret_cast<const v2f*>(t.post640);
-  const int fa = lane >> 4, j = lane & 15;
-  v2f* tb = tbuf[wave];
-  float* pb = pbuf[wave];
+// ------------------------------------------------------------------------- K1 MFCC (v3)
+// Workgroup = 4 waves, persistent over clips, 2 workgroups per CU (67.4 KB LDS each).  Per clip the
+// waves split the 17 chunks of 3 frames; per chunk and wave, all in registers except two LDS
+// round trips:
+//   pass A  lane (frame, j): 20-point DFT of the windowed samples, twiddle, LDS transpose;
+//   pass B  lane (frame, k1): 16-point DFT -> Z[k1 + 20 k2] in registers; the packed-real untangle
+//           pairs Z[k] with Z[320 - k], held by lane (frame, 20 - k1) at k2' = 15 - k2: ONE
+//           ds_bpermute per float instead of an LDS spectrum write + two reads; |X[k]|^2 -> LDS;
+//   mel     each lane owns a narrow (<= 3 bins) and a wide (<= 15 bins) filter: 18 taps read from LDS
+//           with immediate offsets (window starts chosen bank-conflict-free, runtime.hip), weights in
+//           registers; power_to_db -> the clip's dB image in LDS.
+// Lane constants (window, mel weights) stay in registers for the whole kernel; the twiddles are read
+// from LDS.
+// After one workgroup barrier (the clip's top_db max), the DCT-II runs on the fp32 matrix cores:
+// C[16 x 64] = DCT[16 x 128] . max(dB, floor)[128 x 64], one 16-frame column tile per wave
+// (v_mfma_f32_16x16x4_f32, exact fp32 products), then the deltas and the store.
+constexpr int kM3Waves = 4;
+constexpr int kM3DbP = 132;   // dB image [frame][band] pitch (16-B rows)
+constexpr int kM3CP = 52;     // coefficient image [13][52]
 
+__device__ __forceinline__ float bperm(int src_byte, float v) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(src_byte, __float_as_int(v)));
+}
+
+typedef float f32x4_ __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __restrict__ pcm, float* __restrict__ out,
+                                                                  int layout, int64_t n_clips, DeviceTables t) {
+  __shared__ __attribute__((aligned(16))) v2f tbuf[kM3Waves][3 * 340];
+  __shared__ __attribute__((aligned(16))) float db[51 * kM3DbP];
+  __shared__ v2f s_tw[20 * 16];   // W320^(j k1) at [k1][j]
+  __shared__ v2f s_post[320];     // W640^k (untangle twiddles)
+  __shared__ float cbuf[13 * kM3CP];
+  __shared__ float red[kM3Waves];
+  // the wave index in an SGPR: the chunk loop and its reflect / tail branches stay scalar
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int fa = lane >> 4, j = lane & 15;           // pass A
+  const int fb = lane / 20, k1b = lane - 20 * fb;    // pass B (fb == 3: lanes 60..63 idle)
+  for (int i = threadIdx.x; i < 320; i += 64 * kM3Waves)
+    s_tw[i] = *reinterpret_cast<const v2f*>(t.tw320 + ((i >> 4) * (i & 15)));
+  v2f win[20];
+#pragma unroll
+  for (int i = 0; i < 20; ++i) win[i] = *reinterpret_cast<const v2f*>(t.hann640f + 2 * (j + 16 * i));
+  for (int i = threadIdx.x; i < 320; i += 64 * kM3Waves) s_post[i] = *reinterpret_cast<const v2f*>(t.post640 + i);
+  const int4 mlo = t.melq_lo[lane];   // {window start a, window start b, filter a, filter b}
+  float mw[18];
+#pragma unroll
+  for (int q = 0; q < 18; ++q) mw[q] = 0.25f * t.melq_w[q * 64 + lane];   // the LDS holds 4 |X|^2
+  const int pbyte = 4 * (fb < 3 ? fb * 20 + (k1b == 0 ? 0 : 20 - k1b) : lane);
+  // pin the lane constants in registers: left alone, the compiler re-loads these invariant table
+  // entries from global memory inside the chunk loop and waits on them there
+#pragma unroll
+  for (int i = 0; i < 20; ++i) asm volatile("" : "+v"(win[i]));
+#pragma unroll
+  for (int q = 0; q < 18; ++q) asm volatile("" : "+v"(mw[q]));
+  __syncthreads();
+  v2f* tb = tbuf[wave];
+  float* pb = reinterpret_cast<float*>(tb);   // |X|^2 [3][321] over the transpose slice
+
+  // One chunk of 3 frames: consumes `cur` (its samples) and issues the loads of the wave's next
+  // chunk into `nxt` right after the 20-point DFTs, so they overlap pass B, the untangle and the mel
+  // reduction.  The two register buffers alternate between consecutive steps (no copies: a copy
+  // would force the wait early); only wave 0, with an odd chunk count (5 of 17), swaps once per clip.
+  auto step = [&](v2f (&cur)[20], v2f (&nxt)[20], int64_t clip, int c, float& vmax) {
+    v2f a[20];
+#pragma unroll
+    for (int i = 0; i < 20; ++i) a[i] = cur[i] * win[i];
+    dft20v(a);
+    if (fa < 3) {
+#pragma unroll
+      for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? cm2(a[k1], s_tw[k1 * 16 + j]) : a[0];
+    }
+    {  // next: this clip's chunk c + 4, else the next clip's chunk `wave` (past the end: a re-read)
+      const bool more = c + kM3Waves < 17;
+      int64_t nclip = more ? clip : clip + gridDim.x;
+      nclip = nclip < n_clips ? nclip : clip;
+      mfcc_load_chunk(pcm + nclip * kPcmLen, more ? c + kM3Waves : wave, lane, nxt);
+    }
+    wave_lds_fence();
+    // lanes 60..63 (fb = 3) duplicate frame 2's reads and park their results in the unused tail
+    // of the slice (3 * 321 + 303 < 2 * 1020 floats): no divergent branches in this phase
+    v2f b[16];
+    const int fbr = fb < 3 ? fb : 2;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) b[jj] = tb[fbr * 340 + k1b * 17 + jj];
+    dft16v(b);
+    wave_lds_fence();
+    // untangle the packed real FFT: X[k] = E + W640^k O, E = (Z[k] + Z*[320-k]) / 2,
+    // O = -i (Z[k] - Z*[320-k]) / 2; lane k1 = 0 holds both of its pairs (Z[20 k2], Z[20 (16 - k2)]).
+    // With A = Z[k], B = Z[320-k], W640^k = (c, s):  2 X = S + c U + s (-U.y, U.x),
+    // S = (A.x + B.x, A.y - B.y), U = (A.y + B.y, B.x - A.x).  The LDS holds |2 X|^2 = 4 |X|^2; the
+    // factor 1/4 is folded into the mel weights (exact).
+    // all 32 partner values are requested before any is used (the LDS crossbar latency overlaps);
+    // the arithmetic is scalar (packed fp32 issues at half rate and needs swizzle moves here)
+    float Bx[16], By[16];
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) {
+      Bx[k2] = bperm(pbyte, b[15 - k2].x);
+      By[k2] = bperm(pbyte, b[15 - k2].y);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the 32 requests ahead of their consumers
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) {
+      const float ax = b[k2].x, ay = b[k2].y;
+      const float bx = k1b == 0 ? b[(16 - k2) & 15].x : Bx[k2];
+      const float by = k1b == 0 ? b[(16 - k2) & 15].y : By[k2];
+      const float sx = ax + bx, sy = ay - by, ux = ay + by, uy = bx - ax;
+      const v2f w = s_post[k1b + 20 * k2];
+      const float xr = fmaf(-w.y, uy, fmaf(w.x, ux, sx));
+      const float xi = fmaf(w.y, ux, fmaf(w.x, uy, sy));
+      pb[fb * 321 + k1b + 20 * k2] = fmaf(xr, xr, xi * xi);
+    }
+    if (fb < 3 && k1b == 0) {
+      const float ny = 2.0f * (b[0].x - b[0].y);   // 2 X[320] = 2 (Re Z[0] - Im Z[0])
+      pb[fb * 321 + 320] = ny * ny;
+    }
+    wave_lds_fence();
+    // Slaney mel (the lane's narrow and wide filter) -> power_to_db(ref = 1, amin = 1e-10).  The 18
+    // taps of frame ff + 1 are requested before frame ff's sums run (LDS latency off the chain).
+    const int f0 = 3 * c;
+    const int nf = f0 + 3 <= 51 ? 3 : 51 - f0;   // uniform
+    float pv[2][18];
+    auto read_taps = [&](int ff, float (&v)[18]) {
+      const float* p = pb + ff * 321;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) v[q] = p[mlo.x + q];
+#pragma unroll
+      for (int q = 0; q < 15; ++q) v[3 + q] = p[mlo.y + q];
+    };
+    read_taps(0, pv[0]);
+#pragma unroll
+    for (int ff = 0; ff < 3; ++ff) {
+      if (ff >= nf) break;   // uniform
+      if (ff + 1 < nf) read_taps(ff + 1, pv[(ff + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      const float* v = pv[ff & 1];
+      float s0 = mw[0] * v[0], s1 = mw[3] * v[3], s2 = mw[4] * v[4];
+      s0 = fmaf(mw[1], v[1], s0);
+      s0 = fmaf(mw[2], v[2], s0);
+#pragma unroll
+      for (int q = 5; q < 18; q += 2) {
+        s1 = fmaf(mw[q], v[q], s1);
+        if (q + 1 < 18) s2 = fmaf(mw[q + 1], v[q + 1], s2);
+      }
+      s1 += s2;
+      const float v0 = s0 > 1e-10f ? 10.0f * fast_log10(s0) : -100.0f;
+      const float v1 = s1 > 1e-10f ? 10.0f * fast_log10(s1) : -100.0f;
+      db[(f0 + ff) * kM3DbP + mlo.z] = v0;
+      db[(f0 + ff) * kM3DbP + mlo.w] = v1;
+      vmax = fmaxf(vmax, fmaxf(v0, v1));
+    }
+    wave_lds_fence();
+  };
+
+  v2f rawA[20], rawB[20];
+  if ((int64_t)blockIdx.x < n_clips) mfcc_load_chunk(pcm + (int64_t)blockIdx.x * kPcmLen, wave, lane, rawA);
+  const int nsteps = (17 - wave + kM3Waves - 1) / kM3Waves;   // 5 for wave 0, else 4 (uniform)
   for (int64_t clip = blockIdx.x; clip < n_clips; clip += gridDim.x) {
-    const float* __restrict__ x = pcm + clip * kPcmLen;
     float vmax = -INFINITY;
-    for (int c = wave; c < 17; c += kMfWaves) {
-      v2f raw[20];
-      mfcc_load_chunk(x, c, lane, raw);
-      const int f0 = 3 * c;
-      v2f a[20];
-#pragma unroll
-      for (int i = 0; i < 20; ++i) {
-        const v2f w = *reinterpret_cast<const v2f*>(s_hann + 2 * (j + 16 * i));
-        a[i] = raw[i] * w;
-      }
-      // pass A: 20-point DFTs + twiddle, transpose through LDS
-      dft20v(a);
-      if (fa < 3) {
-#pragma unroll
-        for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? cm2(a[k1], s_tw[k1 * 16 + j]) : a[0];
-      }
-      wave_lds_fence();
-      // pass B: 16-point DFTs -> natural-order spectra (overwrite the transpose slice)
-      const int fb = lane / 20, k1 = lane % 20;
-      v2f b[16];
-      if (fb < 3) {
-#pragma unroll
-        for (int jj = 0; jj < 16; ++jj) b[jj] = tb[fb * 340 + k1 * 17 + jj];
-      }
-      dft16v(b);
-      wave_lds_fence();
-      if (fb < 3) {
-#pragma unroll
-        for (int k2 = 0; k2 < 16; ++k2) tb[fb * 320 + k1 + 20 * k2] = b[k2];
-      }
-      wave_lds_fence();
-      // untangle the packed real FFT -> |X[k]|^2, k = 0..320
-#pragma unroll
-      for (int f = 0; f < 3; ++f) {
-#pragma unroll
-        for (int m = 0; m < 6; ++m) {
-          const int k = lane + 64 * m;
-          if (k <= 320) {
-            const v2f A = tb[f * 320 + (k == 320 ? 0 : k)];
-            const v2f Bz = tb[f * 320 + (k == 0 ? 0 : 320 - k)];
-            const v2f Bc = v2f{Bz.x, -Bz.y};
-            const v2f e = 0.5f * (A + Bc), o = mi2(0.5f * (A - Bc));
-            const v2f X = e + cm2(s_post[k], o);
-            pb[f * 321 + k] = X.x * X.x + X.y * X.y;
-          }
-        }
-      }
-      wave_lds_fence();
-      // Slaney mel (two 16-tap filters per lane) -> power_to_db(ref=1, amin=1e-10)
-#pragma unroll
-      for (int f = 0; f < 3; ++f) {
-        const float* p = pb + f * 321;
-        float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          s0 = fmaf(w0[q * 128], p[lo0 + q], s0);
-          s1 = fmaf(w1[q * 128], p[lo1 + q], s1);
-        }
-        const float v0 = s0 > 1e-10f ? 10.0f * fast_log10(s0) : -100.0f;
-        const float v1 = s1 > 1e-10f ? 10.0f * fast_log10(s1) : -100.0f;
-        db[(f0 + f) * 132 + lane] = v0;
-        db[(f0 + f) * 132 + lane + 64] = v1;
-        vmax = fmaxf(vmax, fmaxf(v0, v1));
-      }
-      wave_lds_fence();
+    for (int k = 0; k < nsteps; k += 2) {
+      step(rawA, rawB, clip, wave + kM3Waves * k, vmax);
+      if (k + 1 < nsteps) step(rawB, rawA, clip, wave + kM3Waves * (k + 1), vmax);
     }
     vmax = wave_max(vmax);
     if (lane == 0) red[wave] = vmax;
     __syncthreads();
     float mx = red[0];
 #pragma unroll
-    for (int w = 1; w < kMfWaves; ++w) mx = fmaxf(mx, red[w]);
+    for (int w = 1; w < kM3Waves; ++w) mx = fmaxf(mx, red[w]);
     const float floor_db = mx - 80.0f;
-    float* C = reinterpret_cast<float*>(&tbuf[0][0]);   // 13 x 51 coefficients
-    float* D = C + 13 * 51;                             // deltas
-    for (int it = threadIdx.x; it < 13 * 51; it += 64 * kMfWaves) {
-      const int cc = it / 51, f = it % 51;
-      const float* d = db + f * 132;
-      const float* w = t.dct + cc * 128;
-      v4f acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-      for (int k = 0; k < 128; k += 4) {
-        const v4f dv = *reinterpret_cast<const v4f*>(d + k);
-        const v4f wv = *reinterpret_cast<const v4f*>(w + k);
-        acc.x = fmaf(wv.x, fmaxf(dv.x, floor_db), acc.x);
-        acc.y = fmaf(wv.y, fmaxf(dv.y, floor_db), acc.y);
-        acc.z = fmaf(wv.z, fmaxf(dv.z, floor_db), acc.z);
-        acc.w = fmaf(wv.w, fmaxf(dv.w, floor_db), acc.w);
+    {  // DCT-II (ortho, 13 rows) on the matrix cores: wave = frames [16 wave, 16 wave + 16)
+      const int row = lane & 15, kq = 4 * (lane >> 4);
+      const int fr = min(16 * wave + row, 50);
+      const float* dr = db + fr * kM3DbP + kq;
+      const float* ar = t.dct + min(row, 12) * 128 + kq;
+      f32x4_ acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) {
+        const v4f bv = *reinterpret_cast<const v4f*>(dr + 16 * kb);
+        v4f av = *reinterpret_cast<const v4f*>(ar + 16 * kb);
+        if (row >= 13) av = v4f{0.f, 0.f, 0.f, 0.f};
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, fmaxf(bv.x, floor_db), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, fmaxf(bv.y, floor_db), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, fmaxf(bv.z, floor_db), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, fmaxf(bv.w, floor_db), acc, 0, 0, 0);
       }
-      C[it] = (acc.x + acc.y) + (acc.z + acc.w);
+      // acc[r] = C[coef 4 (lane >> 4) + r][frame 16 wave + (lane & 15)]
+      const int fo = 16 * wave + row;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int coef = kq + r;
+        if (coef < 13 && fo < 51) cbuf[coef * kM3CP + fo] = acc[r];
+      }
     }
     __syncthreads();
+    // np.gradient (edge_order 1) twice, then [C; dC; ddC] in the requested layout
     auto grad = [](const float* r, int f) {
       return f == 0 ? r[1] - r[0] : (f == 50 ? r[50] - r[49] : (r[f + 1] - r[f - 1]) * 0.5f);
     };
-    for (int it = threadIdx.x; it < 13 * 51; it += 64 * kMfWaves) D[it] = grad(C + (it / 51) * 51, it % 51);
-    __syncthreads();
+    auto grad2 = [&](const float* r, int f) {
+      return f == 0 ? grad(r, 1) - grad(r, 0)
+                    : (f == 50 ? grad(r, 50) - grad(r, 49) : (grad(r, f + 1) - grad(r, f - 1)) * 0.5f);
+    };
     float* o = out + clip * 39 * 51;
-    for (int it = threadIdx.x; it < 39 * 51; it += 64 * kMfWaves) {
-      const int row = it / 51, f = it % 51;
-      float v;
-      if (row < 13) v = C[row * 51 + f];
-      else if (row < 26) v = D[(row - 13) * 51 + f];
-      else v = grad(D + (row - 26) * 51, f);
-      if (layout == 0) o[row * 51 + f] = v; else o[f * 39 + row] = v;
+    for (int it = threadIdx.x; it < 39 * 51; it += 64 * kM3Waves) {
+      int rw, f;
+      if (layout == 0) { rw = it / 51; f = it - 51 * rw; } else { f = it / 39; rw = it - 39 * f; }
+      const int cr = rw < 13 ? rw : (rw < 26 ? rw - 13 : rw - 26);
+      const float* r = cbuf + cr * kM3CP;
+      o[it] = rw < 13 ? r[f] : (rw < 26 ? grad(r, f) : grad2(r, f));
     }
-    __syncthreads();   // tbuf / db are reused by the next clip
+    if (nsteps & 1) {   // wave 0: the next clip's first chunk landed in rawB (long since)
+#pragma unroll
+      for (int i = 0; i < 20; ++i) rawA[i] = rawB[i];
+    }
   }
 }
 
@@ -520,8 +593,8 @@ int srk_mfcc_fwd(const float* pcm, int64_t n_clips, float* out, int layout, void
   const DeviceTables* t = nullptr;
   if (int rc = srk::get_tables(&t)) return rc;
   srk::ProfScope prof("mfcc", srk::as_stream(stream), 71956.0 * (double)n_clips);     // 64000 + 7956 B/clip
-  const int64_t grid = std::min<int64_t>(n_clips, 256 * 4);   // persistent over clips
-  hipLaunchKernelGGL(srk::mfcc2_kernel, dim3((unsigned)grid), dim3(64 * srk::kMfWaves), 0,
+  const int64_t grid = std::min<int64_t>(n_clips, 256 * 2);   // persistent over clips, 2 per CU
+  hipLaunchKernelGGL(srk::mfcc3_kernel, dim3((unsigned)grid), dim3(64 * srk::kM3Waves), 0,
                      srk::as_stream(stream), pcm, out, layout, n_clips, *t);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;

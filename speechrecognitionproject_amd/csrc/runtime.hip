@@ -8,6 +8,7 @@
 //  * windows               np.hamming(400) (model_fbanks_cnn.py:41), periodic Hann(640)
 //                          (librosa stft), periodic Tukey(640, 0.25) (scipy spectrogram)
 #include <atomic>
+#include <functional>
 #include <cmath>
 #include <cstdarg>
 #include <mutex>
@@ -218,6 +219,55 @@ int build_tables(DeviceTables& t) {
     for (int m = 0; m < 128; ++m)
       for (int q = 0; q < 16; ++q) wt[q * 128 + m] = wv[m * 16 + q];
     if ((rc = upload(&t.mel16_wt, wt))) return rc;
+    // lane pairs for mfcc3_kernel.  Lane l owns one narrow filter (0..63, <= 3 bins) read as a 3-bin
+    // window and one wide filter (64..127, <= 15 bins) read as a 15-bin window.  ds_read_b32 serves
+    // lanes 0-31 and 32-63 as two groups over 32 banks: the narrow filters go to the groups by halves,
+    // the wide ones alternately, and each wide window's start (free within [last - 14, first]) is
+    // matched so that the 32 starts of a group are distinct mod 32 — every tap read conflict-free
+    // (a plain lane = filter layout costs 3x on those 15 reads).
+    const std::vector<double> mel = slaney_mel();
+    int first[128], last[128];
+    for (int m = 0; m < 128; ++m) {
+      first[m] = last[m] = -1;
+      for (int k = 0; k < 321; ++k)
+        if (mel[(size_t)m * 321 + k] != 0.0) { if (first[m] < 0) first[m] = k; last[m] = k; }
+      SRK_REQUIRE(first[m] >= 0 && last[m] - first[m] < (m < 64 ? 3 : 15), SRK_ERR_INTERNAL,
+                  "mel filter %d does not fit its lane window", m);
+    }
+    std::vector<int4> qlo(64);
+    std::vector<float> qw(18 * 64, 0.f);
+    for (int g = 0; g < 2; ++g) {
+      int wide[32], start[32], owner[32];
+      for (int i = 0; i < 32; ++i) { wide[i] = 64 + 2 * i + g; start[i] = first[wide[i]]; }
+      for (int r = 0; r < 32; ++r) owner[r] = -1;
+      // Kuhn's augmenting paths: filter i -> a start s in [max(0, last - 14), min(first, 306)], residue s % 32
+      std::vector<int> seen(32);
+      std::function<bool(int)> assign = [&](int i) {
+        const int f = wide[i];
+        for (int s0 = std::max(0, last[f] - 14); s0 <= std::min(first[f], 321 - 15); ++s0) {
+          const int r = s0 % 32;
+          if (seen[r]) continue;
+          seen[r] = 1;
+          if (owner[r] < 0 || assign(owner[r])) { owner[r] = i; start[i] = s0; return true; }
+        }
+        return false;
+      };
+      bool ok = true;
+      for (int i = 0; i < 32 && ok; ++i) { std::fill(seen.begin(), seen.end(), 0); ok = assign(i); }
+      if (!ok)   // still correct, only slower: plain starts
+        for (int i = 0; i < 32; ++i) start[i] = first[wide[i]];
+      for (int i = 0; i < 32; ++i) {
+        const int l = 32 * g + i, fa = 32 * g + i, fb = wide[i];
+        qlo[l] = int4{first[fa], start[i], fa, fb};
+        for (int q = 0; q < 3; ++q)
+          if (first[fa] + q <= last[fa]) qw[q * 64 + l] = (float)mel[(size_t)fa * 321 + first[fa] + q];
+        for (int q = 0; q < 15; ++q) {
+          const int k = start[i] + q;
+          if (k >= first[fb] && k <= last[fb]) qw[(3 + q) * 64 + l] = (float)mel[(size_t)fb * 321 + k];
+        }
+      }
+    }
+    if ((rc = upload(&t.melq_lo, qlo)) || (rc = upload(&t.melq_w, qw))) return rc;
   }
 
   std::vector<float> dct(13 * 128);

@@ -63,6 +63,10 @@ struct DeviceTables {
   // Slaney mel as fixed 16-tap windows (zero-padded, start clamped so lo+16 <= bins)
   int* mel16_lo = nullptr; float* mel16_w = nullptr;   // [128], [128][16]
   float* mel16_wt = nullptr;                           // [16][128] (lane-coalesced)
+  // Slaney mel as 64 lane pairs (a narrow filter <= 3 bins, a wide one <= 15 bins, bank-conflict-free
+  // window starts; runtime.hip): {start_a, start_b, filter_a, filter_b} and [18][64] weights
+  // (taps 0..2 from start_a, taps 3..17 from start_b)
+  int4* melq_lo = nullptr; float* melq_w = nullptr;
   double spec_scale = 0.0;     // 1 / (fs * sum(w^2)) for the Tukey window
 };
 

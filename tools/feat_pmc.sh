@@ -1,0 +1,22 @@
+#!/bin/bash
+# VALU / LDS / cycle counters of the feature kernels (K1-K3) on 65,536 clips, one rocprofv3 pass per
+# counter group (<= 8 SQ counters each), then the summary table.
+#   gpurun --timeout 600 -- bash tools/feat_pmc.sh TAG
+set -o pipefail
+TAG=${1:-feat}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+ROOT=$(pwd)
+i=0
+for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC" \
+           "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+  i=$((i+1))
+  for k in ${KERNELS:-mfcc fbank spec}; do
+    timeout -k 10 120 rocprofv3 --kernel-trace --pmc $pmc -d "$ROOT/$OUT/p${i}_$k" -o run -- \
+      python3 tools/mfcc_only.py $k 65536 > "$OUT/p${i}_$k.log" 2>&1 || { echo "pass $i $k failed"; tail -5 "$OUT/p${i}_$k.log"; exit 1; }
+    echo "pass $i $k ok"
+  done
+done
+python3 tools/pmc_table.py "$OUT" > "$OUT/summary.txt" && cat "$OUT/summary.txt"

@@ -279,6 +279,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true")
     ap.add_argument("--no-feature-roofline", "--no-mfcc-roofline", dest="no_feature_roofline", action="store_true")
+    ap.add_argument("--no-overlap", dest="overlap", action="store_false",
+                    help="N > 1: one blocking all-reduce after backward instead of bucketed all-reduces overlapped "
+                         "with it (parallel.GradReducer)")
+    ap.add_argument("--bucket-mb", type=float, default=8.0, help="gradient bucket size of the overlapped all-reduce")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="BatchNorm statistics over the global batch of all ranks (SyncBatchNorm1d; resnet_bgru, "
+                         "cnn_bgru, mfrn_bgru)")
     ap.add_argument("--cpu-plumbing", action="store_true",
                     help="exercise the N-rank launch / timing / JSON path over gloo on CPU (no GPU; no measurement)")
     args = ap.parse_args()
@@ -297,9 +304,13 @@ def main():
     dev = torch.device("cuda", local)
     torch.manual_seed(0)
     model = build_model(args.model).to(dev)
+    if args.sync_bn:
+        from speechrecognitionproject_amd.nn import convert_sync_batchnorm
+        model = convert_sync_batchnorm(model)
     flat = FlatParams(model.parameters())
     opt = Adam(model.parameters(), lr=1e-4, flat=flat)
     parallel.broadcast_flat(flat)
+    reducer = parallel.GradReducer(flat, bucket_mb=args.bucket_mb) if (world > 1 and args.overlap) else None
     crit = CrossEntropyLoss()
 
     B = args.batch or DEFAULT_BATCH[args.model]
@@ -326,10 +337,15 @@ def main():
 
     def step(i):
         opt.zero_grad()
+        if reducer is not None:
+            reducer.begin()
         out = model(inputs(i))
         loss = crit(out, lab[i % args.pool])
         (loss * loss_scale if loss_scale != 1.0 else loss).backward()
-        parallel.allreduce_grads(flat)
+        if reducer is not None:
+            reducer.finish()        # bucketed all-reduces launched during backward
+        else:
+            parallel.allreduce_grads(flat)
         opt.step()
         return loss
 
@@ -408,7 +424,10 @@ def main():
         "vs_baseline": None, "dtype": args.precision, "data": "synthetic (SURVEY.md §8d clip mix, pre-staged in HBM)",
         "config": {"workload": "%s, CE, backward, Adam (full training.py step), per-GPU batch %d"
                                % (CFG[args.model], B), "model": args.model,
-                   "global_batch": world * B, "clip_samples": 16000, "parallelism": "dp%d" % world},
+                   "global_batch": world * B, "clip_samples": 16000, "parallelism": "dp%d" % world,
+                   "allreduce": ("bucketed %.0f MB, overlapped with backward" % args.bucket_mb
+                                 if reducer is not None else ("one flat buffer after backward" if world > 1 else None)),
+                   "sync_bn": bool(args.sync_bn)},
         "model_tflops": round(value * TRAIN_GFLOP_PER_UTT.get(args.model, 0) / 1e3, 2),
         "final_loss": round(final_loss, 5),
         "roofline": roof,

@@ -226,6 +226,29 @@ int srk_batchnorm_fwd(const float* x, int64_t M, int64_t C, const float* gamma, 
 int srk_batchnorm_bwd(const float* x, const float* y, const float* dy, int64_t M, int64_t C, const float* gamma,
                       const float* save_mean, const float* save_invstd, int training, int relu, float* dx,
                       float* dgamma, float* dbeta, float* dresidual, void* stream);
+/* SyncBatchNorm pieces (torch.nn.SyncBatchNorm semantics: training statistics over the global
+ * batch of all data-parallel ranks; model_resnet_bgru.py's BatchNorm1d layers under DP).  Forward:
+ * srk_batchnorm_stats (this rank's count, mean, M2 per channel -> stats [3][C]), the caller gathers
+ * every rank's triple ([world][3][C], rank order), srk_batchnorm_combine (Chan's combination in rank
+ * order: identical on every rank; running stats with the global unbiased variance; total_count [1]
+ * = the global row count, nullable), then
+ * srk_batchnorm_apply.  Backward: srk_batchnorm_bwd_reduce (this rank's sums [2][C] = sum g,
+ * sum g * xhat, g = dy * act'(y): also its dbeta / dgamma contributions), the caller sums them over
+ * ranks, srk_batchnorm_bwd_dx with the combine's total_count (device).  The C-ABI replaces the fused
+ * srk_batchnorm_fwd / _bwd statistics step only; layouts as srk_batchnorm_fwd.                    */
+int srk_batchnorm_stats(const float* x, int64_t M, int64_t C, float* stats, void* stream);
+int srk_batchnorm_combine(const float* stats_all, int world, int64_t C, float eps, float momentum,
+                          float* running_mean, float* running_var, float* save_mean, float* save_invstd,
+                          float* total_count, void* stream);
+int srk_batchnorm_apply(const float* x, int64_t M, int64_t C, const float* save_mean, const float* save_invstd,
+                        const float* gamma, const float* beta, const float* residual, int relu, float* y,
+                        void* stream);
+int srk_batchnorm_bwd_reduce(const float* x, const float* y, const float* dy, int64_t M, int64_t C,
+                             const float* save_mean, const float* save_invstd, int relu, float* sums, void* stream);
+int srk_batchnorm_bwd_dx(const float* x, const float* y, const float* dy, int64_t M, int64_t C,
+                         const float* total_count, const float* gamma, const float* save_mean,
+                         const float* save_invstd, const float* sums, int relu, float* dx, float* dresidual,
+                         void* stream);
 
 /* ---------------------------------------------------------------- K7/K8: step ops
  * Cross-entropy, mean over the batch (nn.CrossEntropyLoss, training.py:73,87):

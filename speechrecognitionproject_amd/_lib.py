@@ -59,6 +59,11 @@ _SIGS = {
     "srk_maxpool_nhwc_bwd": [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P],
     "srk_batchnorm_fwd": [_P, _I64, _I64, _P, _P, _F, _F, _I, _P, _P, _P, _I, _P, _P, _P, _P],
     "srk_batchnorm_bwd": [_P, _P, _P, _I64, _I64, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P],
+    "srk_batchnorm_stats": [_P, _I64, _I64, _P, _P],
+    "srk_batchnorm_combine": [_P, _I, _I64, _F, _F, _P, _P, _P, _P, _P, _P],
+    "srk_batchnorm_apply": [_P, _I64, _I64, _P, _P, _P, _P, _P, _I, _P, _P],
+    "srk_batchnorm_bwd_reduce": [_P, _P, _P, _I64, _I64, _P, _P, _I, _P, _P],
+    "srk_batchnorm_bwd_dx": [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P, _I, _P, _P, _P],
     "srk_cross_entropy": [_P, _P, _I64, _I64, _P, _P, _P, _P],
     "srk_adam_step": [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _I64, _F, _P],
     "srk_dropout_fwd": [_P, _I64, _F, ctypes.c_uint64, _P, _P, _P],

@@ -203,7 +203,8 @@ __global__ void bn_dgamma_kernel(const float* __restrict__ p0, const float* __re
 __global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ dy,
                              int64_t M, int C, const float* __restrict__ mean, const float* __restrict__ invstd,
                              const float* __restrict__ gamma, const float* __restrict__ dbeta,
-                             const float* __restrict__ dgamma, int relu, int train, float* __restrict__ dx,
+                             const float* __restrict__ dgamma, int relu, int train, float m_norm,
+                             const float* __restrict__ m_norm_dev, float* __restrict__ dx,
                              float* __restrict__ dres) {
   const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i4 * 4 >= M * C) return;
@@ -220,11 +221,51 @@ __global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restric
   const v4f is = ld4(invstd + c), ga = ld4(gamma + c);
   if (train) {
     const v4f xhat = (ld4(x + o) - ld4(mean + c)) * is;
-    const float inv_m = 1.0f / (float)M;
+    const float mn = m_norm_dev ? m_norm_dev[0] : m_norm;   // rows the statistics span (all ranks' for SyncBN)
+    const float inv_m = 1.0f / mn;
     const v4f db = ld4(dbeta + c), dg = ld4(dgamma + c);
-    st4(dx + o, ga * is * inv_m * ((float)M * gr - db - xhat * dg));
+    st4(dx + o, ga * is * inv_m * (mn * gr - db - xhat * dg));
   } else {
     st4(dx + o, ga * is * gr);
+  }
+}
+
+// ---- SyncBatchNorm pieces (torch.nn.SyncBatchNorm over data-parallel ranks).  One rank's (count,
+// mean, M2) per channel from the chunk partials; the ranks' triples are gathered by the caller and
+// combined in rank order (Chan, fixed order: every rank computes identical statistics).
+__global__ void bn_local_stats_kernel(const float* __restrict__ pmean, const float* __restrict__ pm2, BnGeom g,
+                                      float* __restrict__ stats) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= g.C) return;
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  for (int k = 0; k < g.chunks; ++k) {
+    const int64_t r0 = (int64_t)k * g.rows_per_chunk;
+    const float nb = (float)((r0 + g.rows_per_chunk < g.M ? g.rows_per_chunk : g.M - r0));
+    chan(n, mu, m2, nb, pmean[(int64_t)k * g.C + c], pm2[(int64_t)k * g.C + c]);
+  }
+  stats[c] = n;
+  stats[g.C + c] = mu;
+  stats[2 * g.C + c] = m2;
+}
+
+__global__ void bn_combine_kernel(const float* __restrict__ all, int world, int C, float eps, float momentum,
+                                  float* __restrict__ running_mean, float* __restrict__ running_var,
+                                  float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ total) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  for (int r = 0; r < world; ++r) {
+    const float* s = all + (size_t)r * 3 * C;
+    chan(n, mu, m2, s[c], s[C + c], s[2 * C + c]);
+  }
+  const float var = n > 0.f ? m2 / n : 0.f;
+  if (c == 0 && total) total[0] = n;
+  mean[c] = mu;
+  invstd[c] = 1.0f / sqrtf(var + eps);
+  if (running_mean) {
+    const float unbiased = n > 1.f ? m2 / (n - 1.f) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mu;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
   }
 }
 
@@ -306,7 +347,95 @@ int srk_batchnorm_bwd(const float* x, const float* y, const float* dy, int64_t M
                      part + (size_t)g.chunks * C, g.chunks, (int)C, dbeta, dgamma);
   const int64_t n4 = M * C / 4;
   hipLaunchKernelGGL(srk::bn_dx_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, y, dy, M, (int)C,
-                     save_mean, save_invstd, gamma, dbeta, dgamma, relu, training, dx, dresidual);
+                     save_mean, save_invstd, gamma, dbeta, dgamma, relu, training, (float)M, nullptr, dx, dresidual);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_batchnorm_stats(const float* x, int64_t M, int64_t C, float* stats, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(M > 0 && C > 0 && C % 4 == 0 && C <= (1 << 24), SRK_ERR_INVALID,
+              "batchnorm_stats: bad shape (C % 4 == 0 required)");
+  SRK_REQUIRE(M < (1LL << 24), SRK_ERR_INVALID, "batchnorm_stats: > 2^24 rows per rank (fp32 counts)");
+  SRK_REQUIRE(x && stats, SRK_ERR_INVALID, "batchnorm_stats: null pointer");
+  hipStream_t s = srk::as_stream(stream);
+  srk::ProfScope prof("batchnorm_fwd", s, 4.0 * (double)M * C);
+  const srk::BnGeom g = srk::bn_geom(M, (int)C);
+  float* part = nullptr;
+  if (int rc = srk::bn_scratch((size_t)2 * g.chunks * C, &part)) return rc;
+  hipLaunchKernelGGL(srk::bn_stats_kernel, dim3((unsigned)((g.C4 + g.CQ - 1) / g.CQ), (unsigned)g.chunks), dim3(256), 0,
+                     s, x, g, part, part + (size_t)g.chunks * C);
+  hipLaunchKernelGGL(srk::bn_local_stats_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
+                     part + (size_t)g.chunks * C, g, stats);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_batchnorm_combine(const float* stats_all, int world, int64_t C, float eps, float momentum,
+                          float* running_mean, float* running_var, float* save_mean, float* save_invstd,
+                          float* total_count, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(world >= 1 && C > 0, SRK_ERR_INVALID, "batchnorm_combine: bad shape");
+  SRK_REQUIRE(stats_all && save_mean && save_invstd && ((running_mean == nullptr) == (running_var == nullptr)),
+              SRK_ERR_INVALID, "batchnorm_combine: null pointer");
+  hipStream_t s = srk::as_stream(stream);
+  hipLaunchKernelGGL(srk::bn_combine_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, stats_all, world,
+                     (int)C, eps, momentum, running_mean, running_var, save_mean, save_invstd, total_count);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_batchnorm_apply(const float* x, int64_t M, int64_t C, const float* save_mean, const float* save_invstd,
+                        const float* gamma, const float* beta, const float* residual, int relu, float* y,
+                        void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(M > 0 && C > 0 && C % 4 == 0, SRK_ERR_INVALID, "batchnorm_apply: bad shape (C % 4 == 0 required)");
+  SRK_REQUIRE(x && save_mean && save_invstd && gamma && beta && y, SRK_ERR_INVALID, "batchnorm_apply: null pointer");
+  hipStream_t s = srk::as_stream(stream);
+  srk::ProfScope prof("batchnorm_fwd", s, 8.0 * (double)M * C);
+  const int64_t n4 = M * C / 4;
+  hipLaunchKernelGGL(srk::bn_apply_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, M, (int)C,
+                     save_mean, save_invstd, gamma, beta, residual, relu, y);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_batchnorm_bwd_reduce(const float* x, const float* y, const float* dy, int64_t M, int64_t C,
+                             const float* save_mean, const float* save_invstd, int relu, float* sums, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(M > 0 && C > 0 && C % 4 == 0, SRK_ERR_INVALID, "batchnorm_bwd_reduce: bad shape");
+  SRK_REQUIRE(x && y && dy && save_mean && save_invstd && sums, SRK_ERR_INVALID, "batchnorm_bwd_reduce: null pointer");
+  hipStream_t s = srk::as_stream(stream);
+  srk::ProfScope prof("batchnorm_bwd", s, 12.0 * (double)M * C);
+  const srk::BnGeom g = srk::bn_geom(M, (int)C);
+  float* part = nullptr;
+  if (int rc = srk::bn_scratch((size_t)2 * g.chunks * C, &part)) return rc;
+  hipLaunchKernelGGL(srk::bn_bwd_partial_kernel, dim3((unsigned)((g.C4 + g.CQ - 1) / g.CQ), (unsigned)g.chunks),
+                     dim3(256), 0, s, x, y, dy, g, save_mean, save_invstd, relu, part, part + (size_t)g.chunks * C);
+  hipLaunchKernelGGL(srk::bn_dgamma_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
+                     part + (size_t)g.chunks * C, g.chunks, (int)C, sums, sums + C);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_batchnorm_bwd_dx(const float* x, const float* y, const float* dy, int64_t M, int64_t C,
+                         const float* total_count, const float* gamma, const float* save_mean,
+                         const float* save_invstd, const float* sums, int relu, float* dx, float* dresidual,
+                         void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(M > 0 && C > 0 && C % 4 == 0, SRK_ERR_INVALID, "batchnorm_bwd_dx: bad shape");
+  SRK_REQUIRE(x && y && dy && total_count && gamma && save_mean && save_invstd && sums && (dx || dresidual),
+              SRK_ERR_INVALID, "batchnorm_bwd_dx: null pointer");
+  hipStream_t s = srk::as_stream(stream);
+  srk::ProfScope prof("batchnorm_bwd", s, 16.0 * (double)M * C);
+  const int64_t n4 = M * C / 4;
+  hipLaunchKernelGGL(srk::bn_dx_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, y, dy, M, (int)C,
+                     save_mean, save_invstd, gamma, sums, sums + C, relu, 1, 0.f, total_count, dx, dresidual);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END

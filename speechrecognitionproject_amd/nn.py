@@ -47,6 +47,12 @@ def _flat_grad(p):
     return g
 
 
+def _reducer_of(p):
+    """The overlapped gradient all-reduce (parallel.GradReducer) attached to p's FlatParams, if any."""
+    flat = getattr(p, "_srk_flat", None)
+    return getattr(flat, "reducer", None) if flat is not None else None
+
+
 def _grad_pair(a, b):
     """The stacked .grad of a FlatParams-owned direction pair to ACCUMULATE into in place
     (autograd's own accumulation, fused into the kernels' epilogues), or None (then the gradient
@@ -77,6 +83,9 @@ class _GRULayerFn(torch.autograd.Function):
         ctx.dims = (B, T, IN, H)
         ctx.params = (w_ih_f, w_ih_r, w_hh_f, w_hh_r, b_ih_f, b_ih_r, b_hh_f, b_hh_r)
         ctx.prec = _lib.matmul_precision()   # the backward runs at its forward's precision
+        red = _reducer_of(w_ih_f)
+        if red is not None and any(ctx.needs_input_grad):
+            red.persistent_pending(1)      # collectives wait until this layer's recurrence is enqueued
         return y
 
     @staticmethod
@@ -99,6 +108,11 @@ class _GRULayerFn(torch.autograd.Function):
             call("srk_gru_layer_bwd", ptr(x), B, T, IN, H, ptr(w_ih), ptr(w_hh), ptr(y), ptr(ws), ptr(dy),
                  ptr(dx) if dx is not None else None, ptr(dw_ih), ptr(dw_hh), ptr(db_ih), ptr(db_hh), int(acc),
                  ptr(ws2), stream_ptr())
+        red = _reducer_of(P[0])
+        if red is not None:
+            red.persistent_done()
+            if acc:
+                red.mark_ready(P)
         if acc:
             return (dx,) + (None,) * 8
         return (dx, dw_ih[0], dw_ih[1], dw_hh[0], dw_hh[1], db_ih[0], db_ih[1], db_hh[0], db_hh[1])
@@ -195,6 +209,9 @@ class _LinearFn(torch.autograd.Function):
             db = torch.empty((N,), device=x.device)
             call("srk_colsum_f32", ptr(dy), M, N, N, ptr(db), 0.0, s)
         if acc:
+            red = _reducer_of(wp)
+            if red is not None:
+                red.mark_ready([wp] + ([bp] if bp is not None else []))
             return dx, None, None
         return dx, dw, db
 
@@ -549,3 +566,94 @@ class BatchNorm1d(tnn.Module):
             self.num_batches_tracked.add_(1)
         return _BatchNormFn.apply(x, self.weight, self.bias, residual, self.running_mean, self.running_var,
                                   self.training, self.momentum, self.eps, relu)
+
+
+# ----------------------------------------------------------------------------- synchronized batch norm
+class _SyncBatchNormFn(torch.autograd.Function):
+    """Training-mode BatchNorm over the GLOBAL batch of all data-parallel ranks (torch.nn.SyncBatchNorm
+    semantics): this rank's (count, mean, M2) per channel are all-gathered and combined in rank order
+    on the device (identical statistics on every rank); the backward all-reduces (sum g, sum g * xhat)
+    for dx, while dgamma / dbeta keep this rank's contribution (the data-parallel gradient all-reduce
+    sums them, as for any parameter)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, momentum, eps, relu, group):
+        import torch.distributed as dist
+        x = x.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        _check_cuda(x, gamma, beta, residual)
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        # all-gather as an all-reduce of rank-owned slots (x + 0 is exact; works on every backend)
+        allst = torch.zeros((world, 3 * C), device=x.device)
+        call("srk_batchnorm_stats", ptr(x), M, C, ptr(allst[rank]), stream_ptr())
+        dist.all_reduce(allst, op=dist.ReduceOp.SUM, group=group)
+        mean = torch.empty(C, device=x.device)
+        invstd = torch.empty(C, device=x.device)
+        total = torch.empty(1, device=x.device)
+        call("srk_batchnorm_combine", ptr(allst), world, C, float(eps), float(momentum), ptr(running_mean),
+             ptr(running_var), ptr(mean), ptr(invstd), ptr(total), stream_ptr())
+        y = torch.empty_like(x)
+        res = residual.contiguous() if residual is not None else None
+        call("srk_batchnorm_apply", ptr(x), M, C, ptr(mean), ptr(invstd), ptr(gamma), ptr(beta),
+             ptr(res) if res is not None else None, int(relu), ptr(y), stream_ptr())
+        ctx.save_for_backward(x, y, gamma, mean, invstd, total)
+        ctx.flags = (int(relu), residual is not None)
+        ctx.group = group
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        import torch.distributed as dist
+        x, y, gamma, mean, invstd, total = ctx.saved_tensors
+        relu, has_res = ctx.flags
+        C = x.shape[-1]
+        M = x.numel() // C
+        dy = dy.contiguous()
+        sums = torch.empty(2 * C, device=x.device)
+        call("srk_batchnorm_bwd_reduce", ptr(x), ptr(y), ptr(dy), M, C, ptr(mean), ptr(invstd), relu, ptr(sums),
+             stream_ptr())
+        dbeta, dgamma = sums[:C].clone(), sums[C:].clone()     # this rank's contributions
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=ctx.group)
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dres = torch.empty_like(x) if has_res and ctx.needs_input_grad[3] else None
+        if dx is not None or dres is not None:
+            call("srk_batchnorm_bwd_dx", ptr(x), ptr(y), ptr(dy), M, C, ptr(total), ptr(gamma), ptr(mean), ptr(invstd),
+                 ptr(sums), relu, ptr(dx) if dx is not None else None, ptr(dres) if dres is not None else None,
+                 stream_ptr())
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None
+
+
+class SyncBatchNorm1d(BatchNorm1d):
+    """BatchNorm1d whose training statistics span every data-parallel rank (torch.nn.SyncBatchNorm).
+    Same parameters / buffers / state_dict keys as BatchNorm1d; eval mode and a world of 1 take the
+    plain BatchNorm1d path.  Build one with ``convert_sync_batchnorm(model)``."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, process_group=None):
+        super().__init__(num_features, eps, momentum)
+        self.process_group = process_group
+
+    def forward(self, x, residual=None, relu=False):
+        import torch.distributed as dist
+        if not (self.training and dist.is_available() and dist.is_initialized()
+                and dist.get_world_size(self.process_group) > 1):
+            return super().forward(x, residual=residual, relu=relu)
+        require_gpu()
+        self.num_batches_tracked.add_(1)
+        return _SyncBatchNormFn.apply(x, self.weight, self.bias, residual, self.running_mean, self.running_var,
+                                      self.momentum, self.eps, relu, self.process_group)
+
+
+def convert_sync_batchnorm(module, process_group=None):
+    """Replace every BatchNorm1d of ``module`` by a SyncBatchNorm1d sharing its parameters and
+    buffers (torch.nn.SyncBatchNorm.convert_sync_batchnorm).  Call before FlatParams / the optimizer."""
+    out = module
+    if isinstance(module, BatchNorm1d) and not isinstance(module, SyncBatchNorm1d):
+        out = SyncBatchNorm1d(module.num_features, module.eps, module.momentum, process_group)
+        out.weight, out.bias = module.weight, module.bias
+        out.running_mean, out.running_var = module.running_mean, module.running_var
+        out.num_batches_tracked = module.num_batches_tracked
+        out.train(module.training)
+    for name, child in module.named_children():
+        out.add_module(name, convert_sync_batchnorm(child, process_group))
+    return out

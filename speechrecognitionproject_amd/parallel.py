@@ -57,6 +57,109 @@ def allreduce_grads(flat):
         dist.all_reduce(flat.grad, op=dist.ReduceOp.SUM)
 
 
+class GradReducer:
+    """Bucketed all-reduce of a FlatParams gradient buffer, overlapped with the backward pass
+    (SURVEY.md §8e "overlap it with the backward pass").
+
+    The flat buffer is cut into contiguous buckets of ~bucket_mb, built from the END of the
+    parameter list (backward produces the last layers' gradients first).  A bucket's
+    ``all_reduce(SUM, async_op=True)`` is launched as soon as every parameter in it has its
+    gradient: autograd's post-accumulate hook for layers that return gradients, ``mark_ready`` from
+    the GRU / Linear backward that accumulate into the buffer in place (nn.py).  The collective runs
+    on the process group's own stream, which first waits for the compute stream, so it overlaps the
+    backward work enqueued after it.
+
+    Persistent kernels need every workgroup co-resident (csrc/gru_persistent.hip): a collective
+    kernel sharing the CUs with one could starve it.  Each GRU layer forward calls
+    ``persistent_pending(+1)``; its backward calls ``persistent_done`` right after enqueueing the
+    recurrence: until the last such backward is enqueued, ready buckets are held (a collective
+    launched afterwards waits for that kernel on the compute stream).  ``finish()`` launches what
+    is left in bucket order (identical on every rank) and makes the compute stream wait for all."""
+
+    def __init__(self, flat, bucket_mb=8.0, group=None):
+        self.flat, self.group = flat, group
+        cap = max(1, int(bucket_mb * (1 << 20) / 4))
+        groups, cur, size = [], [], 0
+        for off, p in sorted(zip(flat.offsets, flat.params), key=lambda t: t[0], reverse=True):
+            cur.append((off, p))
+            size += p.numel()
+            if size >= cap:
+                groups.append(cur)
+                cur, size = [], 0
+        if cur:
+            groups.append(cur)
+        # contiguous cover of the buffer (alignment padding included): the first bucket ends at numel,
+        # each later one where the previous one starts, the last one starts at 0
+        self.buckets, end = [], flat.numel
+        for gi, g in enumerate(groups):
+            start = 0 if gi == len(groups) - 1 else min(off for off, _ in g)
+            self.buckets.append((start, end, [p for _, p in g]))
+            end = start
+        self.bucket_of = {}
+        for i, (_, _, ps) in enumerate(self.buckets):
+            for p in ps:
+                self.bucket_of[id(p)] = i
+        self.hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in flat.params]
+        flat.reducer = self
+        self.begin()
+
+    def begin(self):
+        """Reset per-step state; call before the forward pass of each step."""
+        self.remaining = [len(ps) for _, _, ps in self.buckets]
+        self.launched = [False] * len(self.buckets)
+        self.works = []
+        self.pending = 0
+        self.held = []
+
+    def persistent_pending(self, n=1):
+        self.pending += n
+
+    def persistent_done(self):
+        self.pending = max(0, self.pending - 1)
+        if self.pending == 0:
+            held, self.held = self.held, []
+            for i in held:
+                self._launch(i)
+
+    def _hook(self, p):
+        self.mark_ready([p])
+
+    def mark_ready(self, params):
+        for p in params:
+            i = self.bucket_of.get(id(p))
+            if i is None:
+                continue
+            self.remaining[i] -= 1
+            if self.remaining[i] == 0:
+                if self.pending > 0:
+                    self.held.append(i)
+                else:
+                    self._launch(i)
+
+    def _launch(self, i):
+        if self.launched[i]:
+            return
+        self.launched[i] = True
+        lo, hi, _ = self.buckets[i]
+        if world_size() > 1:
+            self.works.append(dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
+                                              async_op=True))
+
+    def finish(self):
+        """Launch every bucket not launched yet (in bucket order) and wait for all of them."""
+        self.pending = 0
+        for i in range(len(self.buckets)):
+            self._launch(i)
+        for w in self.works:
+            w.wait()
+        self.works = []
+
+    def remove(self):
+        for h in self.hooks:
+            h.remove()
+        self.flat.reducer = None
+
+
 def shard_indices(n_items, rank, world, seed, epoch=0):
     """DistributedSampler-equivalent: a seeded permutation, rank r takes every world-th item
     starting at r (padded by wrap-around so every rank gets the same count)."""

@@ -44,6 +44,10 @@ def parse(argv=None):
     p.add_argument('--reduce', type=int, default=0, help='reduce_dataset(n) like training.py:66-67')
     p.add_argument('--log-every', type=int, default=1, help='write buffered loss lines every n steps')
     p.add_argument('--no-eval', action='store_true')
+    p.add_argument('--sync-bn', action='store_true',
+                   help='data-parallel: BatchNorm statistics over the global batch (SyncBatchNorm1d)')
+    p.add_argument('--no-overlap', dest='overlap', action='store_false',
+                   help='data-parallel: one all-reduce after backward instead of overlapped buckets')
     p.add_argument('--loader', choices=('device', 'torch'), default='device',
                    help='WAV datasets: device = native batched decode + K10 on-device augmentation '
                         '(DeviceBatchLoader); torch = per-item Dataset.__getitem__ through DataLoader')
@@ -75,10 +79,14 @@ def main(argv=None):
 
     torch.manual_seed(0)
     model = mod.Network().to(device)
+    if args.sync_bn:
+        from .nn import convert_sync_batchnorm
+        model = convert_sync_batchnorm(model)
     flat = FlatParams(model.parameters())
     optimizer = Adam(model.parameters(), lr=lr, flat=flat)
     optimizer.grad_scale = 1.0 / world
     parallel.broadcast_flat(flat)
+    reducer = parallel.GradReducer(flat) if (world > 1 and args.overlap) else None
     scheduler = torch.optim.lr_scheduler.ExponentialLR(optimizer, 0.87)
     criterion = CrossEntropyLoss()
     os.makedirs(args.output_path, exist_ok=True)
@@ -116,10 +124,15 @@ def main(argv=None):
 
         for batch in loader:
             optimizer.zero_grad()
+            if reducer is not None:
+                reducer.begin()
             outputs = model(batch['audio'])
             loss = criterion(outputs, batch['label'].to(device))
             loss.backward()
-            parallel.allreduce_grads(flat)
+            if reducer is not None:
+                reducer.finish()
+            else:
+                parallel.allreduce_grads(flat)
             optimizer.step()
             pending.append(loss.detach())
             if len(pending) >= args.log_every:

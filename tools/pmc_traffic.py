@@ -14,12 +14,14 @@ import json
 import os
 import sqlite3
 
-GROUPS = {  # srk_prof name -> substring of the rocprof kernel symbol
-    "gemm_f32": "gemm_f32_kernel", "gru_fwd_seq": "gru_fwd_persistent_kernel",
-    "gru_bwd_seq": "gru_bwd_persistent_kernel", "gru_fwd_step": "gru_fwd_step_kernel",
-    "gru_bwd_step": "gru_bwd_step_kernel", "mfcc": "mfcc2_kernel", "fbank": "fbank_kernel", "spec": "spec_kernel",
-    "conv_fwd": "conv_gemm_kernel<0", "conv_dgrad": "conv_gemm_kernel<1", "conv_wgrad": "conv_gemm_kernel<2",
-    "adam": "adam_kernel", "noise_mix": "noise_mix_kernel",
+GROUPS = {  # srk_prof name -> substrings of the rocprof kernel symbols it covers
+    "gemm_f32": ("gemm_f32_kernel",), "gemm_bf16": ("gemm_h16_kernel", "gemm_lp_kernel"),
+    "gru_fwd_seq": ("gru_fwd_persistent_kernel",), "gru_bwd_seq": ("gru_bwd_persistent_kernel",),
+    "gru_fwd_seq_lp": ("gru_fwd_persistent_lp_kernel",), "gru_bwd_seq_lp": ("gru_bwd_persistent_lp_kernel",),
+    "gru_fwd_step": ("gru_fwd_step_kernel",), "gru_bwd_step": ("gru_bwd_step_kernel",),
+    "mfcc": ("mfcc3_kernel", "mfcc2_kernel"), "fbank": ("fbank_kernel",), "spec": ("spec_kernel",),
+    "conv_fwd": ("conv_gemm_kernel<0",), "conv_dgrad": ("conv_gemm_kernel<1",), "conv_wgrad": ("conv_gemm_kernel<2",),
+    "adam": ("adam_kernel",), "noise_mix": ("noise_mix_kernel",),
 }
 
 
@@ -29,8 +31,8 @@ def collect(d, counter):
     out = {}
     for name, n, tot in c.execute("select kernel_name, count(*), sum(value) from counters_collection where "
                                   "counter_name = ? group by kernel_name", (counter,)):
-        for g, sub in GROUPS.items():
-            if sub in name:
+        for g, subs in GROUPS.items():
+            if any(sub in name for sub in subs):
                 a = out.setdefault(g, [0, 0.0])
                 a[0] += n
                 a[1] += tot

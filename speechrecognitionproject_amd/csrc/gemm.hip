@@ -808,6 +808,275 @@ __global__ __launch_bounds__(NW * 64, (h16_per_cu<TA, TB, BM, BN>())) void gemm_
   store_acc<TM, TN>(ka, acc, split, m0, n0, wm0, wn0, lane, 0);
 }
 
+// ------------------------------------------------------------------ 16-bit operands: LDS-DMA ping-pong
+// gemm_g16_kernel: the same contract as gemm_h16_kernel (16-bit A16 / B16 in HBM, fp32 accumulation,
+// split-K slabs), restructured so the matrix pipe never waits on staging:
+//
+//  * 256 x 256 output tile, 8 waves = two GROUPS of 4 (group g = wave >> 2 owns A rows 128 g .. +128;
+//    wave w & 3 owns columns 64 (w & 3) .. +64), 128 x 64 outputs per wave as 4 x 2 32x32x16 MFMA tiles;
+//  * the k loop is a sequence of PHASES, one per 16-deep k-step (8 MFMAs = 256 cycles per wave, all 8
+//    accumulators once); a phase is a LOAD section (the k-step's 6 fragments — 4 A row blocks, 2 B
+//    column blocks — plus part of a later K-tile's LDS-DMA issue) and an MFMA section, each closed
+//    by a raw s_barrier.  The two groups run one section apart (group 1 takes one extra barrier up
+//    front, group 0 one at the end): while one group's waves multiply, the other group's waves — one
+//    per SIMD in each group — read LDS, so each SIMD's matrix pipe alternates between its two waves;
+//  * operands reach LDS by buffer_load_dwordx4 ... lds (LDS-DMA, no VGPR round trip) into lane-linear
+//    half-tile images (8 KB: 128 rows x 32 k, or 32 k x 128 rows) swizzled on the SOURCE address; a
+//    k-tail or out-of-range unit is read past the descriptor's num_records, i.e. as 16 zero bytes, so
+//    the products are exact zeros; per lane one fixed offset, the K-tile's k in the scalar soffset;
+//  * a ring of NST K-tile stages of 32 k (32 KB each; NST = 4 measured faster than 5): K-tile t + NST - 1
+//    is issued into the stage of K-tile t - 1 in K-tile t's two phases (A halves, then B halves) —
+//    that stage's last reads retired before the previous barrier (every load section waits
+//    lgkmcnt(0) before its barrier) — and K-tile t + 1 is retired by a counted vmcnt in K-tile t's
+//    last load section, NST - 2 K-tiles after its issue (~2 x 256 MFMA cycles x 2 (NST - 1) of
+//    latency cover).  MI355X_MICROARCH.md / cdna_hip_programming.md rules: raw s_barrier, never
+//    __syncthreads() while a DMA is in flight; one __shared__ array; the DMA is inline asm, so the
+//    compiler knows of no pending LDS write and inserts no vmcnt(0) before the fragment reads (with
+//    the builtin it did, before every ds_read_b64_tr_b16, draining the ring every K-tile);
+//  * the epilogue stages each wave's accumulators through the (then idle) LDS and writes 16-B rows.
+//
+// KC image (operand k-contiguous in HBM): [128 rows][4 units of 8 k] (64-B rows), unit slot
+//   kc ^ ((row >> 2) & 3); a 32x32x16 fragment (lane: row l & 31, 8 k at 8 (l >> 5)) is one
+//   conflict-free ds_read_b128 (the 4 rows sharing a bank row per 16-lane group get 4 slots).
+// TR image (row-contiguous): [32 k][16 units of 8 rows] (256-B rows), unit slot u ^ ((k & 3) << 2);
+//   a fragment is 2 x ds_read_b64_tr_b16 whose 4 k-rows per half-wave land on 4 distinct 64-B groups.
+constexpr int kG16BK = 32;
+template <bool KC>
+struct G16Half {
+  static constexpr int ELEMS = 128 * kG16BK;   // 8 KB
+  static constexpr int PIECES = ELEMS / 512;   // 1-KB DMA pieces (one wave-instruction each)
+  // element offset of logical (row, k); the 16-B unit holding it is whole, so fragments stay contiguous
+  __device__ static __forceinline__ int off(int row, int k) {
+    if (KC) return row * kG16BK + ((((k >> 3) ^ ((row >> 2) & 3))) << 3) + (k & 7);
+    return k * 128 + ((((row >> 3) ^ ((k & 3) << 2))) << 3) + (row & 7);
+  }
+  // 32x32x16 operand fragment for rows r0 .. r0 + 31 (within the half), k = kk .. kk + 15
+  __device__ static __forceinline__ u32x4 frag(const unsigned short* img, int r0, int kk, int lane) {
+    if (KC) return *reinterpret_cast<const u32x4*>(img + off(r0 + (lane & 31), kk + 8 * (lane >> 5)));
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    const int k = kk + 8 * (lane >> 5) + q, row = r0 + 16 * ((lane >> 4) & 1) + 4 * p;
+    typedef __attribute__((address_space(3))) s16x4_ lds_s16x4;
+    const s16x4_ lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + off(row, k)));
+    const s16x4_ hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + off(row, k + 4)));
+    const u32x2_ l2 = __builtin_bit_cast(u32x2_, lo), h2 = __builtin_bit_cast(u32x2_, hi);
+    return u32x4{l2.x, l2.y, h2.x, h2.y};
+  }
+  // The unit lane `lane` of DMA piece `piece` brings into this half image, for the K-tile at k0 = 0:
+  // its byte offset from the operand base, the k offset kk of that unit within the K-tile, and
+  // whether its rows are in range.  A K-tile at k0 adds k0 * KSTEP bytes (the buffer load's soffset).
+  __device__ static __forceinline__ void src(int piece, int lane, int64_t r0, int64_t rows, int64_t ld, unsigned& voff,
+                                             int& kk, bool& row_ok) {
+    const int p = piece * 64 + lane;
+    if (KC) {   // p = row * 4 + slot
+      const int row = p >> 2, kc = (p & 3) ^ ((row >> 2) & 3);
+      voff = (unsigned)(((r0 + row) * ld + kc * 8) * 2);
+      kk = kc * 8;
+      row_ok = r0 + row < rows;
+    } else {    // p = k * 16 + slot
+      const int k = p >> 4, u = (p & 15) ^ ((k & 3) << 2);
+      voff = (unsigned)((k * ld + r0 + u * 8) * 2);
+      kk = k;
+      row_ok = r0 + u * 8 < rows;
+    }
+  }
+  __device__ static __forceinline__ int64_t kstep_bytes(int64_t ld) { return KC ? 2 : 2 * ld; }
+};
+
+#ifndef SRK_G16_STAGES
+#define SRK_G16_STAGES 4
+#endif
+constexpr int kG16Stages = SRK_G16_STAGES;
+static_assert(kG16Stages >= 4 && kG16Stages <= 5, "g16 ring: 4..5 stages of 32 KB (the epilogue needs 128 KB)");
+
+template <bool TA, bool TB, bool F16>
+__global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
+  using Ops = LpOps<F16>;
+  using e8 = typename Ops::e8;
+  constexpr int BK = kG16BK, NST = kG16Stages;
+  constexpr bool AKC = !TA, BKC = TB;
+  using HA = G16Half<AKC>;
+  using HB = G16Half<BKC>;
+  constexpr int HALF = HA::ELEMS;                 // 16-bit elements per half image
+  constexpr int STAGE = 4 * HALF;                 // A0 A1 B0 B1 = 32 KB
+  static_assert(NST * STAGE * 2 >= 8 * 4096 * 4, "the epilogue stages 128 KB of fp32 through the ring");
+  __shared__ __attribute__((aligned(1024))) unsigned short smem[NST * STAGE];   // the only LDS object
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  // raw workgroup barrier (no vmcnt drain: DMAs stay in flight across it); the empty asm statements
+  // keep the compiler from moving LDS reads across it
+  auto bar = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  const GemmDesc& d = ka.d;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = wave >> 2, wc = wave & 3;
+  int split, tm, tn;
+  map_tile(ka.nblk, ka.tiles, ka.tiles_m, ka.tiles_n, ka.group_m, ka.remap != 0, split, tm, tn);
+  const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
+  const int64_t kb0 = split * ka.kchunk;
+  const int64_t ke = (kb0 + ka.kchunk < d.K) ? kb0 + ka.kchunk : d.K;
+  const int nk = ke > kb0 ? (int)((ke - kb0 + BK - 1) / BK) : 0;
+
+  // LDS-DMA by buffer_load_dwordx4 ... lds (inline asm: the compiler knows of no pending LDS write, so
+  // it inserts no vmcnt(0) before the fragment reads — with the global_load_lds builtin it did, before
+  // every ds_read_b64_tr_b16, draining the ring every K-tile).  Per lane a fixed 32-bit byte offset
+  // (rows clamped once); the K-tile's k0 goes in the scalar soffset; a unit outside the rows or past
+  // the split's k end gets an offset beyond num_records, which the buffer range check turns into 16
+  // zero bytes.  M0 = the piece's LDS base (saved and restored around the DMA).
+  typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+  auto rsrc16 = [](const uint16_t* p) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    return u32x4s{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)a),
+                  (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)), 0x7ffffff0u, 0x00020000u};
+  };
+  const u32x4s rsA = rsrc16(d.A16), rsB = rsrc16(d.B16);
+  constexpr unsigned kOOB = 0x80000000u;
+  unsigned vo[4];
+  int kk[4];
+  bool rok[4];
+  G16Half<AKC>::src(wave, lane, m0, d.M, d.lda, vo[0], kk[0], rok[0]);
+  G16Half<AKC>::src(wave, lane, m0 + 128, d.M, d.lda, vo[1], kk[1], rok[1]);
+  G16Half<BKC>::src(wave, lane, n0, d.N, d.ldb, vo[2], kk[2], rok[2]);
+  G16Half<BKC>::src(wave, lane, n0 + 128, d.N, d.ldb, vo[3], kk[3], rok[3]);
+  const int64_t ksA = G16Half<AKC>::kstep_bytes(d.lda), ksB = G16Half<BKC>::kstep_bytes(d.ldb);
+  const unsigned lds0 =
+      (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ptr)smem + (unsigned)wave * 1024u);
+  auto dma = [&](int t, int h) {   // K-tile t, half image h (0, 1: A rows; 2, 3: B columns)
+    const int64_t k0 = kb0 + (int64_t)t * BK;
+    const bool full = k0 + BK <= ke;   // uniform: only a split's last K-tile has a k tail
+    const unsigned v = (rok[h] && (full || k0 + kk[h] < ke)) ? vo[h] : kOOB;
+    const unsigned soff = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(k0 * (h < 2 ? ksA : ksB)));
+    const unsigned ldsa = lds0 + (unsigned)(((t % NST) * STAGE + h * HALF) * 2);
+    unsigned keep;
+    if (h < 2)
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(v), "s"(rsA), "s"(ldsa), "s"(soff)
+                   : "memory");
+    else
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(v), "s"(rsB), "s"(ldsa), "s"(soff)
+                   : "memory");
+  };
+  auto dma_a = [&](int t) { dma(t, 0); dma(t, 1); };   // K-tile t's A halves (2 DMA instructions per wave)
+  auto dma_b = [&](int t) { dma(t, 2); dma(t, 3); };   // K-tile t's B halves
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // prologue: K-tiles 0 .. NST - 2 in flight (4 DMA instructions per wave each), tile 0 retired
+  for (int t = 0; t < NST - 1; ++t)
+    if (t < nk) {
+      dma_a(t);
+      dma_b(t);
+    }
+  // vmcnt wants an immediate: retire tile 0, leaving min(nk - 1, NST - 2) tiles in flight
+  auto retire_keep = [](int tiles_in_flight) {
+    if (tiles_in_flight >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (tiles_in_flight == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (tiles_in_flight == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  retire_keep(min(nk - 1, NST - 2));
+  bar();
+  if (grp == 1) bar();   // the groups run one section apart
+
+  const int bh = wc >> 1, bc0 = (wc & 1) * 64;   // this wave's B half image and its column base there
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned short* S = smem + (kt % NST) * STAGE;
+    const unsigned short* As = S + grp * HALF;
+    const unsigned short* Bs = S + (2 + bh) * HALF;
+    const int tn_ = kt + NST - 1;   // the K-tile issued during this one (into K-tile kt - 1's stage)
+#pragma unroll
+    for (int q = 0; q < BK / 16; ++q) {
+      // ---- load section: k-step q's fragments (4 A row blocks, 2 B column blocks)
+      u32x4 fa[4], fb[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = HA::frag(As, i * 32, 16 * q, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = HB::frag(Bs, bc0 + j * 32, 16 * q, lane);
+#if !(defined(SRK_G16_EXP) && SRK_G16_EXP == 1)   // experiment builds only: no DMA after the prologue
+      if (tn_ < nk) {
+        if (q == 0) dma_a(tn_);
+        else dma_b(tn_);
+      }
+#endif
+#if !(defined(SRK_G16_EXP) && SRK_G16_EXP == 2)   // experiment builds only: DMA never waited for in the loop
+      if (q == BK / 16 - 1) retire_keep(min(nk - 1 - (kt + 1), NST - 2));   // K-tile kt + 1 landed (this wave's part)
+#endif
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this section's fragments are in registers
+      bar();
+      // ---- MFMA section: 8 independent accumulators, one k-step
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = Ops::mma(__builtin_bit_cast(e8, fa[i]), __builtin_bit_cast(e8, fb[j]), acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+    }
+  }
+  if (grp == 0) bar();   // equal barrier counts; every wave is past its last LDS read and DMA wait
+
+  // ---- epilogue through LDS: each wave stages 64 x 64 fp32 of its 128 x 64 block per pass (16 KB,
+  // 8 waves = 128 KB of the ring), then writes rows as 16-B vectors (4 rows x 256 B per instruction)
+  // instead of the accumulator layout's 4-B scalar stores
+#if defined(SRK_G16_EXP) && SRK_G16_EXP == 3   // experiment builds only: no C stores (kept live)
+  if (d.alpha != 12345.f) return;
+#endif
+  float* st = reinterpret_cast<float*>(smem) + wave * 4096;
+  const bool split_mode = ka.partial != nullptr;
+  float* C = split_mode ? ka.partial + (int64_t)split * d.M * d.N : d.C;
+  const int64_t ldc = split_mode ? d.N : d.ldc;
+  const bool vec = (ldc % 4 == 0) && ((uintptr_t)C % 16 == 0);
+  const int lh = lane >> 5, lc = lane & 31;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          st[(i2 * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * 64 + j * 32 + lc] = acc[2 * h + i2][j][r];
+#pragma unroll 4
+    for (int v = 0; v < 16; ++v) {
+      const int rl = v * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+      const int64_t row = m0 + grp * 128 + h * 64 + rl, col = n0 + wc * 64 + c4;
+      if (row >= d.M || col >= d.N) continue;
+      v4f x = *reinterpret_cast<const v4f*>(st + rl * 64 + c4);
+      float* c = C + row * ldc + col;
+      if (!split_mode) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x[e] *= d.alpha;
+          if (d.bias_mode == 1) x[e] += col + e < d.N ? d.bias[col + e] : 0.f;
+          else if (d.bias_mode == 2) x[e] += d.bias[row];
+        }
+      }
+      if (vec && col + 3 < d.N) {
+        if (!split_mode && d.beta != 0.f) x += d.beta * *reinterpret_cast<const v4f*>(c);
+        *reinterpret_cast<v4f*>(c) = x;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (col + e >= d.N) break;
+          float y = x[e];
+          if (!split_mode && d.beta != 0.f) y += d.beta * c[e];
+          c[e] = y;
+        }
+      }
+    }
+  }
+}
+
 // Sums the split-K slabs in split order and applies the GEMM epilogue.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmDesc d, const float* __restrict__ partial, int splits) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -889,7 +1158,8 @@ int env_int(const char* name, int dflt) {
 
 // Grid, split-K and scratch for one launch of a BM x BN x BK tile kernel with `per_cu` resident
 // workgroups per CU; fills ka and returns the split count (tile::choose_splits).
-int plan_launch(const GemmDesc& d, int BM, int BN, int BK, int per_cu, KernelArgs& ka, int* splits_out) {
+int plan_launch(const GemmDesc& d, int BM, int BN, int BK, int per_cu, KernelArgs& ka, int* splits_out,
+                bool allow_split = true) {
   const int64_t tm = (d.M + BM - 1) / BM, tn = (d.N + BN - 1) / BN;
   SRK_REQUIRE(tm * tn <= (INT32_MAX >> 5) && d.batch <= 65535, SRK_ERR_INVALID, "gemm: grid too large");
   static const int remap = env_int("SRK_GEMM_REMAP", 1);
@@ -902,7 +1172,7 @@ int plan_launch(const GemmDesc& d, int BM, int BN, int BK, int per_cu, KernelArg
   ka.group_m = 8;
   ka.remap = remap;
   // Split K when the output grid leaves resident slots idle and K is long (tile::choose_splits).
-  int splits = d.batch == 1 ? choose_splits(tm * tn, d.K, BK, slots, 16) : 1;
+  int splits = (d.batch == 1 && allow_split) ? choose_splits(tm * tn, d.K, BK, slots, 16) : 1;
   ka.kchunk = splits > 1 ? ((d.K + splits - 1) / splits + BK - 1) / BK * BK : std::max<int64_t>(d.K, 1);
   if (splits > 1) splits = (int)((d.K + ka.kchunk - 1) / ka.kchunk);
   ka.nblk = ka.tiles * splits;
@@ -1025,8 +1295,26 @@ int launch_h16_cfg(const GemmDesc& d, hipStream_t s, bool f16) {
 }
 
 template <bool TA, bool TB>
+int launch_g16(const GemmDesc& d, hipStream_t s, bool f16) {
+  KernelArgs ka;
+  int splits = 1;
+  // split K only when the 256 x 256 output grid leaves more than half of the CUs idle: the slabs
+  // (M x N fp32 per split, written and re-read) cost more than a partly filled round otherwise
+  const int64_t tiles = ((d.M + 255) / 256) * ((d.N + 255) / 256);
+  if (int rc = plan_launch(d, 256, 256, kG16BK, 1, ka, &splits, tiles * 2 < kCUs)) return rc;
+  ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K);
+  const dim3 grid((unsigned)ka.nblk), block(512);
+  if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true>), grid, block, 0, s, ka);
+  else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false>), grid, block, 0, s, ka);
+  return finish_splits(d, ka, splits, s);
+}
+
+template <bool TA, bool TB>
 int launch_h16(const GemmDesc& d, hipStream_t s, bool f16) {
   static const int cfg_env = env_int("SRK_H16_CFG", 0);
+  // the LDS-DMA ping-pong kernel wherever its 256 x 256 tile fills the chip (srk option overrides)
+  const int kern = g_opt_gemm16_kernel ? g_opt_gemm16_kernel : (d.M >= 1024 && d.N >= 256 ? 2 : 1);
+  if (kern == 2 || cfg_env == 5) return launch_g16<TA, TB>(d, s, f16);
   // measured (profiles/r01zk_gemm_h16_cfg*.txt): 256 x 256 on x W^T and on the weight gradients
   // (TA != TB: gi 143 vs 148 us, dW_ih 128 vs 137), 256 x 128 on dx (204 tiles of 256 x 256 leave
   // CUs idle: 255 vs 147 us), 128 x 128 below 1024 rows

@@ -79,6 +79,10 @@ int get_tables(const DeviceTables** out);
 enum MatmulPrec { kPrecF32 = 0, kPrecBF16 = 1, kPrecF16 = 2 };
 int matmul_prec();
 
+// Kernel of the 16-bit-operand GEMM (srk_set_option "gemm16_kernel", A/B measurements and tests):
+// 0 = by shape, 1 = register-staged gemm_h16_kernel, 2 = LDS-DMA ping-pong gemm_g16_kernel.
+extern int g_opt_gemm16_kernel;
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // RAII event pair around one kernel launch (prof.hip); inert unless srk_prof_enable(1).

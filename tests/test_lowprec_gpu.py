@@ -304,6 +304,33 @@ def test_gemm_16bit_operands(prec, ta, tb, M, N, K):
     assert (Cd.cpu().double() - ref).abs().max().item() <= 2e-6 * (1 + scale)
 
 
+@pytest.mark.parametrize("kernel", [1, 2])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0)])
+@pytest.mark.parametrize("M,N,K", [(1288, 776, 1352), (1032, 264, 4104), (2048, 512, 64), (1536, 1024, 1000)])
+def test_gemm_16bit_kernels_at_tile_edges(prec, kernel, ta, tb, M, N, K):
+    """Both 16-bit-operand GEMM kernels (register-staged / LDS-DMA ping-pong, srk option
+    gemm16_kernel) on shapes with partial 256-row / -column tiles, k tails (K % 64 != 0),
+    split-K and a single K-tile == float64 product of the 16-bit values."""
+    g = torch.Generator().manual_seed(M + 7 * N + 11 * K + ta)
+    dt = TORCH_DT[prec]
+    A = torch.randn((K, M) if ta else (M, K), generator=g).to(dt)
+    B = torch.randn((N, K) if tb else (K, N), generator=g).to(dt)
+    C0 = torch.randn(M, N, generator=g)
+    opA = (A.T if ta else A).double()
+    opB = (B.T if tb else B).double()
+    ref = opA @ opB + C0.double()
+    Ad, Bd, Cd = A.cuda(), B.cuda(), C0.clone().cuda()
+    _lib.set_option("gemm16_kernel", kernel)
+    try:
+        call("srk_gemm_16", ta, tb, M, N, K, 1.0, ptr(Ad), Ad.shape[1], ptr(Bd), Bd.shape[1], 1.0, ptr(Cd), N,
+             None, 0, stream_ptr())
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_option("gemm16_kernel", 0)
+    scale = (opA.abs() @ opB.abs()).max().item()
+    assert (Cd.cpu().double() - ref).abs().max().item() <= 2e-6 * (1 + scale)
+
+
 def test_gemm_16bit_rejects_misaligned(prec):
     A = torch.zeros(16, 12, dtype=TORCH_DT[prec], device="cuda")
     C = torch.zeros(16, 16, device="cuda")

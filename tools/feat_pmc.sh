@@ -19,4 +19,4 @@ for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD S
     echo "pass $i $k ok"
   done
 done
-python3 tools/pmc_table.py "$OUT" > "$OUT/summary.txt" && cat "$OUT/summary.txt"
+python3 tools/pmc_table.py "$OUT" > "$OUT/summary.txt" && rm -rf "$OUT"/p[0-9]* && cat "$OUT/summary.txt"

@@ -7,9 +7,11 @@
 
 namespace srk {
 
-// Arrival counters of the persistent kernels: [2 directions][groups <= 4] at a 64-B stride,
+// Arrival counters / per-producer flags of the persistent kernels ([2 directions][groups <= 4] at a
+// 64-B stride, or [2][G][32] flags) in words 0..255, the XCD census in words kCensusOff..+8;
 // zeroed by a hipMemsetAsync of exactly this block before every launch.
-constexpr int kCounterFloats = 256;
+constexpr int kCounterFloats = 512;
+constexpr int kCensusOff = 256;
 constexpr int kFusedIn = 64;   // widest layer input whose projection the forward kernels fuse
 
 struct GruPArgs {
@@ -29,6 +31,7 @@ struct GruPArgs {
   float* xbuf;           // hand-off ping-pong: fwd h [2 dir][2][B][H], bwd dg [2 dir][2][B][3H]
   unsigned* counters;    // kCounterFloats words
   int flags;             // 1: per-producer step flags [2][G][32] (sc1 stores) instead of arrival counters
+  int xcd_local;         // 1: try the XCD-local hand-off (census at launch; plain stores kept in the XCD's L2)
   // 16-bit operand outputs of the bf16 / fp16 kernels (nullptr = off), for the GEMMs of the layer:
   uint16_t* y16;         // fwd: h [B][T][2H] rounded to 16 bit
   uint16_t* dgi16;       // bwd: dgi [B*T][6H] (replaces the fp32 dgi)
@@ -58,6 +61,7 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s);
 extern int g_opt_gru_persistent;
 extern unsigned long long* g_opt_gru_trace;   // device buffer or nullptr
 extern unsigned g_opt_gru_spin_limit;          // 0 = default (~2 s); test hook "gru_spin_limit"
+extern int g_opt_gru_xcd_local;                // XCD-local hand-off when the census allows (default 1)
 // Host-pinned health word (device-mapped pointer in *dev): non-zero once any persistent-kernel
 // spin-wait has given up; read without a device synchronization by srk_health_check.
 int health_word(unsigned** host, unsigned** dev);

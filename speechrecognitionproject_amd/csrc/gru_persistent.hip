@@ -104,8 +104,9 @@ __device__ __forceinline__ void arrive(unsigned* cnt) {
 // store); the consumer's wave 0 polls all S words of its (dir, group) at once (lane i <-> slice i,
 // sc1 loads) until every one is >= step, then the workgroup meets.  MI355X_MICROARCH.md "Valid
 // forms" row 1 (a sharded flag, every shard polled).  Replaces the atomic add at the memory side.
-__device__ __forceinline__ void sync_wait(const GruPArgs& a, unsigned* cnt, int dir, int group, int S, int step) {
-  if (!a.flags) {
+__device__ __forceinline__ void sync_wait(const GruPArgs& a, unsigned* cnt, int dir, int group, int S, int step,
+                                          bool local) {
+  if (!a.flags && !local) {
     wait_count(a, cnt, (unsigned)S * step);
     return;
   }
@@ -125,16 +126,28 @@ __device__ __forceinline__ void sync_wait(const GruPArgs& a, unsigned* cnt, int 
   }
   __syncthreads();
 }
-__device__ __forceinline__ void sync_arrive(const GruPArgs& a, unsigned* cnt, int dir, int group, int slice, int step) {
-  if (!a.flags) {
+__device__ __forceinline__ void sync_arrive(const GruPArgs& a, unsigned* cnt, int dir, int group, int slice, int step,
+                                            bool local) {
+  if (!a.flags && !local) {
     arrive(cnt);
     return;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_store(a.counters + (dir * a.G + group) * 32 + slice, (unsigned)(step + 1), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    unsigned* f = a.counters + (dir * a.G + group) * 32 + slice;
+    if (local)   // XCD-local: a plain store, kept in the XCD's L2 where the consumers' sc1 polls read it
+      __builtin_amdgcn_raw_buffer_store_b32((unsigned)(step + 1), rsrc(reinterpret_cast<const float*>(f)), 0, 0, 0);
+    else
+      __hip_atomic_store(f, (unsigned)(step + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Hand-off payload store: write-through (sc1) in the placement-independent protocol; a plain store
+// in the XCD-local one (the line stays in the XCD's L2, where every consumer's sc1 load finds it).
+__device__ __forceinline__ void st4_ho(__amdgpu_buffer_rsrc_t r, unsigned byte_off, v4f v, bool local) {
+  if (local) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)byte_off, 0, 0);
+  else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)byte_off, 0, kSc1);
 }
 
 // Diagnostics (tools/gru_trace.py): thread 0 stamps s_memrealtime (100 MHz) at step start (0), after
@@ -156,6 +169,52 @@ __device__ __forceinline__ void map_block(int G, int S, int& dir, int& group, in
   slice = wgid % S;
   dir = pair / G;
   group = pair % G;
+}
+
+// Placement.  Default: map_block (speed-only XCD affinity; every hand-off byte goes write-through,
+// MI355X_MICROARCH.md "Valid forms" row 1, correct under any placement).  With xcd_local and a full
+// 256-workgroup grid, a census first asks the hardware which XCD each workgroup runs on
+// (HW_REG_XCC_ID) and hands out slots per XCD; when every XCD holds exactly 32 workgroups, XCD x
+// runs (direction, group) pair x — then producers and consumers of a pair provably share one L2, the
+// hand-off bytes and flags are PLAIN stores that stay in that L2 (no write-through to the Infinity
+// Cache and back) and consumers keep reading them with sc1 (L1-bypassing) loads.  Otherwise every
+// workgroup (they all read the same final census) falls back to the default protocol.
+__device__ __forceinline__ void place(const GruPArgs& a, int S, int& dir, int& group, int& slice, bool& local) {
+  __shared__ int info[2];
+  const int nwg = 2 * a.G * S;
+  if (a.xcd_local && nwg == 256) {
+    if (threadIdx.x == 0) {
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+      unsigned* cen = a.counters + kCensusOff;
+      const unsigned slot = __hip_atomic_fetch_add(cen + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(cen + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned spins = 0;
+      while (__hip_atomic_load(cen + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nwg) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins >= a.spin_limit) {
+          spin_gave_up(a);
+          break;
+        }
+      }
+      bool even = true;
+      for (int x = 0; x < 8; ++x)
+        even = even && __hip_atomic_load(cen + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nwg / 8);
+      info[0] = even ? (int)xcc : -1;
+      info[1] = (int)slot;
+    }
+    __syncthreads();
+    const int pair = __builtin_amdgcn_readfirstlane(info[0]);
+    if (pair >= 0) {
+      local = true;
+      dir = pair / a.G;
+      group = pair % a.G;
+      slice = __builtin_amdgcn_readfirstlane(info[1]);
+      return;
+    }
+  }
+  local = false;
+  map_block(a.G, S, dir, group, slice);
 }
 
 // The saved gates (r, z, n, W_hn h + b_hn) of a lane's 4 cells, stored AFTER the step's arrival:
@@ -261,7 +320,8 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
   float* Wx = hT + 64 * HTP;   // fused input projection: W_ih slice [48][kXP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
   int dir, group, slice;
-  map_block(a.G, H / kUnits, dir, group, slice);
+  bool local;
+  place(a, H / kUnits, dir, group, slice, local);
   const int T = a.T, j0 = slice * kUnits, j = j0 + lr;
   const int b0 = a.b_begin + group * kRows;
   const int b_last = a.b_end - 1;
@@ -311,7 +371,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
 #pragma unroll
     for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (step > 0) {
-      sync_wait(a, cnt, dir, group, H / kUnits, step);
+      sync_wait(a, cnt, dir, group, H / kUnits, step, local);
       stamp(a, step, 1);
       // h_{t-1}[row 16 wave + lr][k], k = 16 kb + 4 lq + s  (k-permuted: one b128 feeds 4 MFMAs)
       // fragment chunk (group, row block = wave, k block) of the previous step's buffer; lane = lane
@@ -377,10 +437,10 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
     {  // h_t -> the hand-off buffer (write-through): thread = (row tid/4, units 4*(tid%4) .. +3)
       hv4 = ld4(hT + yrl * HTP + yuq);
       if (step + 1 < T && b0 + yrl <= b_last)   // fragment slot (row block rl/16, k block = slice, lane = (uq/4)*16 + rl%16)
-        st4_sc1(rx, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (yrl >> 4)) * NKB * 64 + slice * 64 +
-                                (yuq >> 2) * 16 + (yrl & 15)) * 16), hv4);
+        st4_ho(rx, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (yrl >> 4)) * NKB * 64 + slice * 64 +
+                                (yuq >> 2) * 16 + (yrl & 15)) * 16), hv4, local);
     }
-    sync_arrive(a, cnt, dir, group, slice, step);   // waits for the hand-off stores only: y and the gates go out after it (no consumer in this launch)
+    sync_arrive(a, cnt, dir, group, slice, step, local);   // waits for the hand-off stores only: y and the gates go out after it (no consumer in this launch)
     stamp(a, step, 4);
     if (b0 + yrl <= b_last) st4(a.y + ((size_t)(b0 + yrl) * T + t) * 2 * H + dir * H + j0 + yuq, hv4);
     store_gates(a, gsv, dir, t, b0 + wave * 16 + lq * 4, b_last, j);
@@ -399,7 +459,8 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
   float* dT = smem + kUnits * WP;   // [64][3][DTP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
   int dir, group, slice;
-  map_block(a.G, H / kUnits, dir, group, slice);
+  bool local;
+  place(a, H / kUnits, dir, group, slice, local);
   const int T = a.T, B = a.B, j0 = slice * kUnits, j = j0 + lr;
   const int b0 = a.b_begin + group * kRows;
   const int b_last = a.b_end - 1;
@@ -445,7 +506,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
     }
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     if (step > 0) {
-      sync_wait(a, cnt, dir, group, H / kUnits, step);
+      sync_wait(a, cnt, dir, group, H / kUnits, step, local);
       stamp(a, step, 1);
       const unsigned base = (unsigned)(((((size_t)((step - 1) & 1) * Gp + group) * 4 + wave) * NKB * 64 + lane) * 16);
       // k rotation per slice (see the forward kernel): block index kr(i) = (i + rot) mod NKB
@@ -512,10 +573,10 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
       const int v = tid + i * 256, rl = v / 12, g = (v % 12) / 4, uq = (v % 4) * 4, b = b0 + rl;
       val[i] = ld4(dT + (rl * 3 + g) * DTP + uq);
       if (b > b_last || edge) continue;
-      st4_sc1(rg_, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB * 64 +
-                               (g * (H / 16) + slice) * 64 + (uq >> 2) * 16 + (rl & 15)) * 16), val[i]);
+      st4_ho(rg_, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB * 64 +
+                               (g * (H / 16) + slice) * 64 + (uq >> 2) * 16 + (rl & 15)) * 16), val[i], local);
     }
-    sync_arrive(a, cnt, dir, group, slice, step);
+    sync_arrive(a, cnt, dir, group, slice, step, local);
     stamp(a, step, 4);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -583,7 +644,8 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
   float* Wx = hT + 64 * HTP;   // fused input projection: W_ih slice [48][kXP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
   int dir, group, slice;
-  map_block(a.G, H / kUnits, dir, group, slice);
+  bool local;
+  place(a, H / kUnits, dir, group, slice, local);
   const int T = a.T, j0 = slice * kUnits, j = j0 + lr;
   const int b0 = a.b_begin + group * kRows;
   const int b_last = a.b_end - 1;
@@ -632,7 +694,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
 #pragma unroll
     for (int g = 0; g < 3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (step > 0) {
-      sync_wait(a, cnt, dir, group, H / kUnits, step);
+      sync_wait(a, cnt, dir, group, H / kUnits, step, local);
       stamp(a, step, 1);
       const unsigned base = (unsigned)(((((size_t)((step - 1) & 1) * Gp + group) * 4 + wave) * NKB * 64 + lane) * 16);
       const int rot = slice % NKB;   // per-slice k rotation, see the fp32 kernel
@@ -686,11 +748,11 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
       if (b0 + rl <= b_last) {
         const float* src = hT + rl * HTP + 8 * half;
         const int l = (2 * (slice & 1) + half) * 16 + (rl & 15);
-        st4_sc1(rx, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB + (slice >> 1)) * 64 + l) * 16,
-                __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))));
+        st4_ho(rx, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB + (slice >> 1)) * 64 + l) * 16,
+                __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))), local);
       }
     }
-    sync_arrive(a, cnt, dir, group, slice, step);   // the hand-off only: y and the gates go out after it
+    sync_arrive(a, cnt, dir, group, slice, step, local);   // the hand-off only: y and the gates go out after it
     stamp(a, step, 4);
     if (b0 + yrl <= b_last) {
       st4(a.y + ((size_t)(b0 + yrl) * T + t) * 2 * H + dir * H + j0 + yuq, yv);
@@ -717,7 +779,8 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
   float* dT = smem + kUnits * WPQ * 4;   // [64][3][DTP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
   int dir, group, slice;
-  map_block(a.G, H / kUnits, dir, group, slice);
+  bool local;
+  place(a, H / kUnits, dir, group, slice, local);
   const int T = a.T, B = a.B, j0 = slice * kUnits, j = j0 + lr;
   const int b0 = a.b_begin + group * kRows;
   const int b_last = a.b_end - 1;
@@ -765,7 +828,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
     }
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     if (step > 0) {
-      sync_wait(a, cnt, dir, group, H / kUnits, step);
+      sync_wait(a, cnt, dir, group, H / kUnits, step, local);
       stamp(a, step, 1);
       const unsigned base = (unsigned)(((((size_t)((step - 1) & 1) * Gp + group) * 4 + wave) * NKB * 64 + lane) * 16);
       const int rot = (slice * (NKB / (H / kUnits))) % NKB;
@@ -840,11 +903,11 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
         const float* src = dT + (rl * 3 + g) * DTP + 8 * half;
         const int l = (2 * (slice & 1) + half) * 16 + (rl & 15);
         const int kb = g * (H / 32) + (slice >> 1);
-        st4_sc1(rg_, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB + kb) * 64 + l) * 16,
-                __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))));
+        st4_ho(rg_, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB + kb) * 64 + l) * 16,
+                __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))), local);
       }
     }
-    sync_arrive(a, cnt, dir, group, slice, step);   // the hand-off only: dgh, dgh_edge and dgi go out after it
+    sync_arrive(a, cnt, dir, group, slice, step, local);   // the hand-off only: dgh, dgh_edge and dgi go out after it
     stamp(a, step, 4);
     if (h16) {   // 16-bit dgh (edge rows zero) and dgi: (row, gate, 8 units) = one 16-B store each
       for (int v = tid; v < 64 * 3 * 2 * 2; v += 256) {
@@ -972,6 +1035,7 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     ac.spin_limit = g_opt_gru_spin_limit ? g_opt_gru_spin_limit : kSpinLimit;
     static const int flags_env = [] { const char* v = getenv("SRK_GRU_FLAGS"); return v && *v ? atoi(v) : 0; }();
     ac.flags = flags_env;
+    ac.xcd_local = g_opt_gru_xcd_local;
     ac.b_begin = c0;
     ac.b_end = std::min(a.B, c0 + rows_per_launch);
     ac.G = (ac.b_end - c0 + kRows - 1) / kRows;

@@ -25,6 +25,7 @@ static std::atomic<int> g_opt_matmul_prec{kPrecF32};
 int matmul_prec() { return g_opt_matmul_prec.load(std::memory_order_relaxed); }
 unsigned long long* g_opt_gru_trace = nullptr;
 unsigned g_opt_gru_spin_limit = 0;
+int g_opt_gru_xcd_local = 1;
 
 static thread_local std::string g_last_error;
 
@@ -340,6 +341,10 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "gru_spin_limit") {   // test hook: polls before a persistent wait gives up (0 = ~2 s default)
     SRK_REQUIRE(value >= 0 && value <= 0xffffffffLL, SRK_ERR_INVALID, "gru_spin_limit out of range");
     srk::g_opt_gru_spin_limit = (unsigned)value;
+    return SRK_OK;
+  }
+  if (n == "gru_xcd_local") {   // persistent GRU: XCD-local hand-off when every XCD hosts one (dir, group)
+    srk::g_opt_gru_xcd_local = value != 0;
     return SRK_OK;
   }
   if (n == "gru_trace_ptr") {   // diagnostics: device buffer of 8 x u64 per (workgroup, step), 0 = off

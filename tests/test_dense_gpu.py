@@ -129,6 +129,39 @@ def test_colsum_large(gpu):
     assert (out.cpu().double() - X.double().sum(0)).abs().max() <= 1e-3
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("B,T,IN", [(256, 51, 24), (512, 19, 1024), (200, 9, 24)])
+def test_bigru_xcd_local_handoff_is_bitwise_identical(gpu, prec, B, T, IN):
+    """The persistent recurrence with the XCD-local hand-off (census of HW_REG_XCC_ID, plain stores
+    kept in the XCD's L2; option gru_xcd_local, default on) produces bitwise the same outputs and
+    gradients as the placement-independent write-through protocol: each (direction, group, slice)
+    does the same arithmetic in the same order, only which workgroup runs it changes.  B = 512 runs
+    two 256-row chunk launches (census per launch); B = 200 has a partial grid (no census: fallback)."""
+    from speechrecognitionproject_amd import _lib
+    H = 512
+    torch.manual_seed(11)
+    mine = snn.BiGRU(IN, H, num_layers=1).cuda()
+    x = torch.randn(B, T, IN)
+    w = torch.randn(B, T, 2 * H)
+    outs = {}
+    try:
+        _lib.set_matmul_precision(prec)
+        for mode in (1, 0):
+            _lib.set_option("gru_xcd_local", mode)
+            for _ in range(2):   # twice: the census and the flags must reset between launches
+                mine.zero_grad()
+                xm = x.cuda().requires_grad_(True)
+                ym, _ = mine(xm)
+                (ym * w.cuda()).sum().backward()
+            outs[mode] = [ym.detach().cpu(), xm.grad.cpu()] + [p.grad.cpu() for p in mine.parameters()]
+    finally:
+        _lib.set_option("gru_xcd_local", 1)
+        _lib.set_matmul_precision("fp32")
+    assert _lib.spin_timeouts() == 0
+    for i, (a, b) in enumerate(zip(outs[1], outs[0])):
+        assert torch.equal(a, b), i
+
+
 @pytest.mark.parametrize("B,T", [(1, 6), (67, 13), (256, 51), (300, 7)])
 def test_bigru_persistent_matches_per_step_and_torch(gpu, B, T):
     """The one-launch persistent recurrence (H = 512) agrees with the per-step kernels (same cell

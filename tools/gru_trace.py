@@ -15,7 +15,7 @@ import torch  # noqa: E402
 from speechrecognitionproject_amd import _lib  # noqa: E402
 from speechrecognitionproject_amd import nn as snn  # noqa: E402
 
-B, T, IN, H = int(os.environ.get("B", 256)), 51, 1024, 512
+B, T, IN, H = int(os.environ.get("B", 256)), 51, int(os.environ.get("IN", 1024)), 512
 nwg = 256
 _lib.set_matmul_precision(os.environ.get("PREC", "fp32"))   # bf16 / fp16: the 16-bit recurrence kernels
 res = {}
@@ -40,6 +40,25 @@ for name, b in (("fwd", fwd), ("bwd", bwd)):
     pub = (ts[:, 1:, 4] - ts[:, 1:, 3]).mean().item()
     step = ((ts[:, -1, 4] - ts[:, 0, 0]) / T).mean().item()
     start_skew = (ts[:, 0, 0].max() - ts[:, 0, 0].min()).item()
+    # group membership (csrc/gru_persistent.hip map_block): the 32 slices of a (direction, 64-row group)
+    G, S = nwg // 64, 32
+    q, r = nwg >> 3, nwg & 7
+    grp = []
+    for b in range(nwg):
+        xcd = b & 7
+        wgid = (xcd * (q + 1) if xcd < r else r * (q + 1) + (xcd - r) * q) + (b >> 3)
+        grp.append(wgid // S)
+    grp = torch.tensor(grp)
+    spread, prop = [], []
+    for g in range(2 * G):
+        m = grp == g
+        pubs = ts[m][:, :, 4]                              # [32, T] publish stamps
+        spread.append((pubs.max(0).values - pubs.min(0).values)[:-1])
+        # wait done at step s + 1 minus the group's LAST publish of step s: flag propagation
+        prop.append(ts[m][:, 1:, 1] - pubs.max(0).values[None, :-1])
+    spread, prop = torch.cat(spread), torch.cat(prop)
     res[name] = {"us_per_step": round(step, 2), "wait": round(wait, 2), "loads_mfma": round(mfma, 2),
-                 "epilogue": round(epi, 2), "publish": round(pub, 2), "launch_skew_us": round(start_skew, 2)}
+                 "epilogue": round(epi, 2), "publish": round(pub, 2), "launch_skew_us": round(start_skew, 2),
+                 "publish_spread_us": round(spread.mean().item(), 2),
+                 "last_publish_to_wait_done_us": round(prop.mean().item(), 2)}
 print(json.dumps(res))

@@ -51,7 +51,8 @@ int srk_prof_read(const char* name, int64_t* count, double* total_ms, double* to
  * recurrence): 0 fp32 (exact, the reference's arithmetic), 1 bf16, 2 fp16 — operands rounded to
  * nearest-even on chip, fp32 accumulation, fp32 tensors in and out (BASELINE.json cfg2 / cfg5);
  * "gemm16_kernel" (default 0 = by shape) = the 16-bit-operand GEMM kernel: 1 register-staged,
- * 2 LDS-DMA ping-pong (same results up to fp32 summation order; for A/B measurements and tests). */
+ * 2 LDS-DMA ping-pong (same results up to fp32 summation order; for A/B measurements and tests);
+ * "gemm32_kernel" (default 0 = by shape) = the same choice for the fp32 GEMM. */
 int srk_set_option(const char* name, int64_t value);
 /* Number of bounded spin-waits of the persistent kernels that gave up (synchronizes the
  * device; must stay 0 — a non-zero value means a co-residency assumption failed).  -1 on error. */

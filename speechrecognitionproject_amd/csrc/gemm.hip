@@ -808,6 +808,60 @@ __global__ __launch_bounds__(NW * 64, (h16_per_cu<TA, TB, BM, BN>())) void gemm_
   store_acc<TM, TN>(ka, acc, split, m0, n0, wm0, wn0, lane, 0);
 }
 
+// Epilogue of the ping-pong kernels (gemm_g16_kernel, gemm_p32_kernel): each wave stages 64 x 64
+// fp32 of its 128 x 64 accumulator block per pass through LDS (16 KB per wave, 128 KB for the 8
+// waves; the K ring is idle by then), then writes rows as 16-B vectors (4 rows x 256 B per
+// instruction) instead of the 32x32 accumulator layout's 4-B scalar stores.  Split-K launches write
+// the raw slab; otherwise alpha, bias and beta are applied.
+__device__ __forceinline__ void pp_epilogue(const KernelArgs& ka, const f32x16 (&acc)[4][2], float* lds, int split,
+                                            int64_t m0, int64_t n0, int grp, int wc, int wave, int lane) {
+  const GemmDesc& d = ka.d;
+  float* st = lds + wave * 4096;
+  const bool split_mode = ka.partial != nullptr;
+  float* C = split_mode ? ka.partial + (int64_t)split * d.M * d.N : d.C;
+  const int64_t ldc = split_mode ? d.N : d.ldc;
+  const bool vec = (ldc % 4 == 0) && ((uintptr_t)C % 16 == 0);
+  const int lh = lane >> 5, lc = lane & 31;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          st[(i2 * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * 64 + j * 32 + lc] = acc[2 * h + i2][j][r];
+#pragma unroll 4
+    for (int v = 0; v < 16; ++v) {
+      const int rl = v * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+      const int64_t row = m0 + grp * 128 + h * 64 + rl, col = n0 + wc * 64 + c4;
+      if (row >= d.M || col >= d.N) continue;
+      v4f x = *reinterpret_cast<const v4f*>(st + rl * 64 + c4);
+      float* c = C + row * ldc + col;
+      if (!split_mode) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x[e] *= d.alpha;
+          if (d.bias_mode == 1) x[e] += col + e < d.N ? d.bias[col + e] : 0.f;
+          else if (d.bias_mode == 2) x[e] += d.bias[row];
+        }
+      }
+      if (vec && col + 3 < d.N) {
+        if (!split_mode && d.beta != 0.f) x += d.beta * *reinterpret_cast<const v4f*>(c);
+        *reinterpret_cast<v4f*>(c) = x;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (col + e >= d.N) break;
+          float y = x[e];
+          if (!split_mode && d.beta != 0.f) y += d.beta * c[e];
+          c[e] = y;
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ 16-bit operands: LDS-DMA ping-pong
 // gemm_g16_kernel: the same contract as gemm_h16_kernel (16-bit A16 / B16 in HBM, fp32 accumulation,
 // split-K slabs), restructured so the matrix pipe never waits on staging:
@@ -1025,53 +1079,194 @@ __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
   }
   if (grp == 0) bar();   // equal barrier counts; every wave is past its last LDS read and DMA wait
 
-  // ---- epilogue through LDS: each wave stages 64 x 64 fp32 of its 128 x 64 block per pass (16 KB,
-  // 8 waves = 128 KB of the ring), then writes rows as 16-B vectors (4 rows x 256 B per instruction)
-  // instead of the accumulator layout's 4-B scalar stores
+  // ---- epilogue (the ring is idle now): pp_epilogue
 #if defined(SRK_G16_EXP) && SRK_G16_EXP == 3   // experiment builds only: no C stores (kept live)
   if (d.alpha != 12345.f) return;
 #endif
-  float* st = reinterpret_cast<float*>(smem) + wave * 4096;
-  const bool split_mode = ka.partial != nullptr;
-  float* C = split_mode ? ka.partial + (int64_t)split * d.M * d.N : d.C;
-  const int64_t ldc = split_mode ? d.N : d.ldc;
-  const bool vec = (ldc % 4 == 0) && ((uintptr_t)C % 16 == 0);
-  const int lh = lane >> 5, lc = lane & 31;
+  pp_epilogue(ka, acc, reinterpret_cast<float*>(smem), split, m0, n0, grp, wc, wave, lane);
+}
+
+// ------------------------------------------------------------------ fp32: LDS-DMA ping-pong
+// gemm_p32_kernel: the exact-fp32 GEMM (v_mfma_f32_32x32x2_f32) on the structure of gemm_g16_kernel —
+// 256 x 256 tiles, two 4-wave groups running one section apart behind raw barriers, a ring of four
+// 16-deep K-tiles (32 KB each) filled by inline-asm buffer_load ... lds with zero-filled edges, and
+// the LDS-staged epilogue.  A phase is one 8-deep k block: its load section reads 6 fragments (4 A
+// row blocks, 2 B column blocks, 4 k per lane each: the k order inside a block is permuted so lanes of
+// half h take k = 8 kb + 4 h + s at sub-step s, as in the register-staged kernel) and issues 2 DMA
+// pieces; its MFMA section is 32 MFMAs = 2,048 cycles per wave.  The register-staged gemm_f32_kernel
+// keeps the matrix pipe 64-76 % busy at the clock it holds (PMC, profiles/r02c_gemm_f32_pmc.txt; its
+// waves park ~28 % of their cycles at the per-K-tile drain and barrier); this structure gains 6-7 %
+// on the dx / dW_ih shapes and loses on the x W^T projection, so it is used for the former only —
+// the fp32 matrix pipe, not the staging, is what binds both.  Row sums of op(A) (the dW GEMMs' fused bias gradient) come from the A
+// fragments of the column-0 waves.
+//
+// KC image (k-contiguous operand): [128 rows][4 units of 4 k] (64-B rows), unit slot u ^ ((row >> 2) & 3):
+//   a fragment (row l & 31, 4 k at unit 2 kb + (l >> 5)) is one conflict-free ds_read_b128.
+// TR image (row-contiguous operand): [16 k][128 rows] (512-B rows), unswizzled: a fragment is 4
+//   ds_read_b32 of 32 consecutive rows per half-wave (the halves on k rows 4 apart).
+constexpr int kP32BK = 16;
+template <bool KC>
+struct P32Half {
+  static constexpr int FLOATS = 128 * kP32BK;   // 8 KB
+  __device__ static __forceinline__ v4f frag(const float* img, int r0, int kb, int lane) {
+    const int row = r0 + (lane & 31), h = lane >> 5;
+    if (KC) return *reinterpret_cast<const v4f*>(img + row * kP32BK + (((2 * kb + h) ^ ((row >> 2) & 3)) << 2));
+    const float* q = img + (8 * kb + 4 * h) * 128 + row;
+    return v4f{q[0], q[128], q[256], q[384]};
+  }
+  // lane's unit of DMA piece `piece` (1 KB = 64 units of 16 B) for the K-tile at k0 = 0: byte offset,
+  // k offset within the K-tile, rows in range
+  __device__ static __forceinline__ void src(int piece, int lane, int64_t r0, int64_t rows, int64_t ld, unsigned& voff,
+                                             int& kk, bool& row_ok) {
+    const int p = piece * 64 + lane;
+    if (KC) {   // p = row * 4 + slot
+      const int row = p >> 2, kc = (p & 3) ^ ((row >> 2) & 3);
+      voff = (unsigned)(((r0 + row) * ld + kc * 4) * 4);
+      kk = kc * 4;
+      row_ok = r0 + row < rows;
+    } else {    // p = k * 32 + unit (4 rows)
+      const int k = p >> 5, u = p & 31;
+      voff = (unsigned)((k * ld + r0 + u * 4) * 4);
+      kk = k;
+      row_ok = r0 + u * 4 < rows;
+    }
+  }
+  __device__ static __forceinline__ int64_t kstep_bytes(int64_t ld) { return KC ? 4 : 4 * ld; }
+};
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(512, 1) void gemm_p32_kernel(KernelArgs ka) {
+  constexpr int BK = kP32BK, NST = 4;
+  constexpr bool AKC = !TA, BKC = TB;
+  using HA = P32Half<AKC>;
+  using HB = P32Half<BKC>;
+  constexpr int HALF = HA::FLOATS;
+  constexpr int STAGE = 4 * HALF;   // A0 A1 B0 B1 = 32 KB
+  __shared__ __attribute__((aligned(1024))) float smem[NST * STAGE];   // 128 KB, the only LDS object
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  auto bar = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  const GemmDesc& d = ka.d;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = wave >> 2, wc = wave & 3;
+  int split, tm, tn;
+  map_tile(ka.nblk, ka.tiles, ka.tiles_m, ka.tiles_n, ka.group_m, ka.remap != 0, split, tm, tn);
+  const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
+  const int64_t kb0 = split * ka.kchunk;
+  const int64_t ke = (kb0 + ka.kchunk < d.K) ? kb0 + ka.kchunk : d.K;
+  const int nk = ke > kb0 ? (int)((ke - kb0 + BK - 1) / BK) : 0;
+
+  typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+  auto rsrc32 = [](const float* p) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    return u32x4s{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)a),
+                  (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)), 0x7ffffff0u, 0x00020000u};
+  };
+  const u32x4s rsA = rsrc32(d.A), rsB = rsrc32(d.B);
+  constexpr unsigned kOOB = 0x80000000u;
+  unsigned vo[4];
+  int kk[4];
+  bool rok[4];
+  P32Half<AKC>::src(wave, lane, m0, d.M, d.lda, vo[0], kk[0], rok[0]);
+  P32Half<AKC>::src(wave, lane, m0 + 128, d.M, d.lda, vo[1], kk[1], rok[1]);
+  P32Half<BKC>::src(wave, lane, n0, d.N, d.ldb, vo[2], kk[2], rok[2]);
+  P32Half<BKC>::src(wave, lane, n0 + 128, d.N, d.ldb, vo[3], kk[3], rok[3]);
+  const int64_t ksA = P32Half<AKC>::kstep_bytes(d.lda), ksB = P32Half<BKC>::kstep_bytes(d.ldb);
+  const unsigned lds0 =
+      (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ptr)smem + (unsigned)wave * 1024u);
+  auto dma = [&](int t, int h) {   // K-tile t, half image h (0, 1: A rows; 2, 3: B columns)
+    const int64_t k0 = kb0 + (int64_t)t * BK;
+    const bool full = k0 + BK <= ke;
+    const unsigned v = (rok[h] && (full || k0 + kk[h] < ke)) ? vo[h] : kOOB;
+    const unsigned soff = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(k0 * (h < 2 ? ksA : ksB)));
+    const unsigned ldsa = lds0 + (unsigned)(((t % NST) * STAGE + h * HALF) * 4);
+    unsigned keep;
+    if (h < 2)
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(v), "s"(rsA), "s"(ldsa), "s"(soff)
+                   : "memory");
+    else
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(v), "s"(rsB), "s"(ldsa), "s"(soff)
+                   : "memory");
+  };
+  auto dma_a = [&](int t) { dma(t, 0); dma(t, 1); };
+  auto dma_b = [&](int t) { dma(t, 2); dma(t, 3); };
+  auto retire_keep = [](int tiles_in_flight) {   // retire all but the youngest tiles (4 DMAs each)
+    if (tiles_in_flight >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (tiles_in_flight == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  f32x16 acc[4][2];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int i2 = 0; i2 < 2; ++i2)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const bool do_rs = d.rowsum != nullptr && tn == 0 && wc == 0;   // one wave per 128 rows
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+
+  for (int t = 0; t < NST - 1; ++t)
+    if (t < nk) {
+      dma_a(t);
+      dma_b(t);
+    }
+  retire_keep(min(nk - 1, NST - 2));
+  bar();
+  if (grp == 1) bar();
+
+  const int bh = wc >> 1, bc0 = (wc & 1) * 64;
+  for (int kt = 0; kt < nk; ++kt) {
+    const float* S = smem + (kt % NST) * STAGE;
+    const float* As = S + grp * HALF;
+    const float* Bs = S + (2 + bh) * HALF;
+    const int tn_ = kt + NST - 1;
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          st[(i2 * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * 64 + j * 32 + lc] = acc[2 * h + i2][j][r];
-#pragma unroll 4
-    for (int v = 0; v < 16; ++v) {
-      const int rl = v * 4 + (lane >> 4), c4 = (lane & 15) * 4;
-      const int64_t row = m0 + grp * 128 + h * 64 + rl, col = n0 + wc * 64 + c4;
-      if (row >= d.M || col >= d.N) continue;
-      v4f x = *reinterpret_cast<const v4f*>(st + rl * 64 + c4);
-      float* c = C + row * ldc + col;
-      if (!split_mode) {
+    for (int q = 0; q < BK / 8; ++q) {
+      v4f fa[4], fb[2];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          x[e] *= d.alpha;
-          if (d.bias_mode == 1) x[e] += col + e < d.N ? d.bias[col + e] : 0.f;
-          else if (d.bias_mode == 2) x[e] += d.bias[row];
-        }
+      for (int i = 0; i < 4; ++i) fa[i] = HA::frag(As, i * 32, q, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = HB::frag(Bs, bc0 + j * 32, q, lane);
+      if (tn_ < nk) {
+        if (q == 0) dma_a(tn_);
+        else dma_b(tn_);
       }
-      if (vec && col + 3 < d.N) {
-        if (!split_mode && d.beta != 0.f) x += d.beta * *reinterpret_cast<const v4f*>(c);
-        *reinterpret_cast<v4f*>(c) = x;
-      } else {
+      if (q == BK / 8 - 1) retire_keep(min(nk - 1 - (kt + 1), NST - 2));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bar();
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (col + e >= d.N) break;
-          float y = x[e];
-          if (!split_mode && d.beta != 0.f) y += d.beta * c[e];
-          c[e] = y;
-        }
+      for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][ss], fb[j][ss], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (do_rs) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rs[i] += (fa[i][0] + fa[i][1]) + (fa[i][2] + fa[i][3]);
+      }
+      bar();
+    }
+  }
+  if (grp == 0) bar();
+
+  pp_epilogue(ka, acc, smem, split, m0, n0, grp, wc, wave, lane);
+  if (do_rs) {   // lanes l and l + 32 hold the two k halves of row (l & 31) of each row block
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float t = rs[i] + __shfl_xor(rs[i], 32);
+      const int64_t row = m0 + grp * 128 + i * 32 + (lane & 31);
+      if (lane < 32 && row < d.M) {
+        if (ka.partial) ka.rs_partial[(int64_t)split * d.M + row] = t;
+        else d.rowsum[row] = d.rowsum_beta != 0.f ? d.rowsum_beta * d.rowsum[row] + t : t;
       }
     }
   }
@@ -1325,9 +1520,28 @@ int launch_h16(const GemmDesc& d, hipStream_t s, bool f16) {
 }
 
 template <bool TA, bool TB>
+int launch_p32(const GemmDesc& d, hipStream_t s) {
+  KernelArgs ka;
+  int splits = 1;
+  const int64_t tiles = ((d.M + 255) / 256) * ((d.N + 255) / 256);
+  if (int rc = plan_launch(d, 256, 256, kP32BK, 1, ka, &splits, tiles * 2 < kCUs)) return rc;
+  ProfScope prof("gemm_f32", s, 2.0 * (double)d.M * (double)d.N * (double)d.K);
+  hipLaunchKernelGGL((gemm_p32_kernel<TA, TB>), dim3((unsigned)ka.nblk), dim3(512), 0, s, ka);
+  return finish_splits(d, ka, splits, s);
+}
+
+template <bool TA, bool TB>
 int dispatch_tile(const GemmDesc& d, hipStream_t s, bool vec) {
   const int prec = d.prec >= 0 ? d.prec : matmul_prec();
   if (prec != kPrecF32) return launch_lp<TA, TB>(d, s, vec, prec == kPrecF16);
+  // the LDS-DMA ping-pong kernel where a 256 x 256 grid fills the chip (16-B units, 32-bit buffer
+  // offsets, batch 1); srk option gemm32_kernel: 1 register-staged, 2 ping-pong
+  const double ext_a = (double)(d.ta ? d.K : d.M) * d.lda * 4, ext_b = (double)(d.tb ? d.N : d.K) * d.ldb * 4;
+  const bool p32_ok = vec && d.batch == 1 && ext_a < 2147483000.0 && ext_b < 2147483000.0;
+  // measured (tools/gemm_bench.py, cfg2 shapes): ping-pong 6-7 % faster on dx (NN) and dW_ih (TN),
+  // 8 % slower on the x W^T projection (NT) and on the 12-tile dW_hh grid (split 16)
+  const int kern32 = g_opt_gemm32_kernel ? g_opt_gemm32_kernel : (!TB && d.M >= 2048 && d.N >= 1024 ? 2 : 1);
+  if (p32_ok && kern32 == 2) return launch_p32<TA, TB>(d, s);
   // 256 x 128 tiles (one 8-wave workgroup per CU, 110 KB of LDS) halve the L2 -> CU operand
   // traffic per flop of the 128 x 128 tile; used when the grid still fills the chip several times
   static const int tile_env = env_int("SRK_GEMM_TILE", 0);

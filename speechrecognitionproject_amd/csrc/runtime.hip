@@ -21,6 +21,7 @@ namespace srk {
 
 int g_opt_gru_persistent = 1;
 int g_opt_gemm16_kernel = 0;
+int g_opt_gemm32_kernel = 0;
 static std::atomic<int> g_opt_matmul_prec{kPrecF32};
 int matmul_prec() { return g_opt_matmul_prec.load(std::memory_order_relaxed); }
 unsigned long long* g_opt_gru_trace = nullptr;
@@ -336,6 +337,11 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "gemm16_kernel") {   // 0 by shape, 1 register-staged, 2 LDS-DMA ping-pong (16-bit operands)
     SRK_REQUIRE(value >= 0 && value <= 2, SRK_ERR_INVALID, "gemm16_kernel must be 0, 1 or 2");
     srk::g_opt_gemm16_kernel = (int)value;
+    return SRK_OK;
+  }
+  if (n == "gemm32_kernel") {   // 0 by shape, 1 register-staged, 2 LDS-DMA ping-pong (fp32 operands)
+    SRK_REQUIRE(value >= 0 && value <= 2, SRK_ERR_INVALID, "gemm32_kernel must be 0, 1 or 2");
+    srk::g_opt_gemm32_kernel = (int)value;
     return SRK_OK;
   }
   if (n == "gru_spin_limit") {   // test hook: polls before a persistent wait gives up (0 = ~2 s default)

@@ -82,6 +82,9 @@ int matmul_prec();
 // Kernel of the 16-bit-operand GEMM (srk_set_option "gemm16_kernel", A/B measurements and tests):
 // 0 = by shape, 1 = register-staged gemm_h16_kernel, 2 = LDS-DMA ping-pong gemm_g16_kernel.
 extern int g_opt_gemm16_kernel;
+// Kernel of the fp32 GEMM (srk_set_option "gemm32_kernel"): 0 = by shape, 1 = register-staged
+// gemm_f32_kernel, 2 = LDS-DMA ping-pong gemm_p32_kernel.
+extern int g_opt_gemm32_kernel;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -100,6 +100,39 @@ def test_adam_matches_torch(gpu):
         assert (a.detach() - b.detach().cpu()).abs().max() <= 1e-5, n
 
 
+@pytest.mark.parametrize("kernel", [1, 2])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(1288, 776, 1352), (1032, 264, 4100), (2048, 512, 16), (1536, 516, 13056)])
+def test_gemm_f32_kernels_at_tile_edges(gpu, kernel, ta, tb, M, N, K):
+    """Both fp32 GEMM kernels (register-staged / LDS-DMA ping-pong, srk option gemm32_kernel) on
+    shapes with partial 256-row / -column tiles, k tails (K % 16 != 0), a single K-tile and split-K,
+    with alpha, beta and a bias, and the fused row sums of op(A) (the dW GEMMs' bias gradient)."""
+    from speechrecognitionproject_amd import _lib
+    g = torch.Generator().manual_seed(M + 3 * N + 7 * K + 11 * ta + 13 * tb)
+    A = torch.randn((K, M) if ta else (M, K), generator=g)
+    B = torch.randn((N, K) if tb else (K, N), generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    opA, opB = (A.T if ta else A).double(), (B.T if tb else B).double()
+    ref = 0.5 * (opA @ opB) + 2.0 * C0.double() + bias.double()
+    tol = 1e-5 * (1 + (opA.abs() @ opB.abs()).max().item())
+    Ad, Bd = A.cuda(), B.cuda()
+    _lib.set_option("gemm32_kernel", kernel)
+    try:
+        Cd = C0.clone().cuda()
+        call("srk_gemm_f32", ta, tb, M, N, K, 0.5, ptr(Ad), Ad.shape[1], ptr(Bd), Bd.shape[1], 2.0, ptr(Cd), N,
+             ptr(bias.cuda()), 1, stream_ptr())
+        Cr = torch.zeros(M, N, device="cuda")
+        rs = torch.full((M,), 3.0, device="cuda")
+        call("srk_gemm_rowsum_f32", ta, tb, M, N, K, 1.0, ptr(Ad), Ad.shape[1], ptr(Bd), Bd.shape[1], 1.0, ptr(Cr),
+             N, ptr(rs), stream_ptr())   # beta = 1 on C (zero-initialised below) and on the row sums
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_option("gemm32_kernel", 0)
+    assert (Cd.cpu().double() - ref).abs().max().item() <= tol
+    assert (rs.cpu().double() - (3.0 + opA.sum(1))).abs().max().item() <= 1e-3 * (1 + K ** 0.5)
+
+
 @pytest.mark.parametrize("ta", [0, 1])
 @pytest.mark.parametrize("M,N,K", [(96, 64, 13056), (3072, 39, 4999), (12, 1024, 256)])
 def test_gemm_rowsum_splitk(gpu, ta, M, N, K):

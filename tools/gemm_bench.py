@@ -37,9 +37,11 @@ def main():
     ap.add_argument("--h16", action="store_true", help="operands pre-converted to 16 bit (srk_gemm_16)")
     ap.add_argument("--kernel16", type=int, default=0,
                     help="srk option gemm16_kernel: 0 by shape, 1 register-staged, 2 LDS-DMA ping-pong")
+    ap.add_argument("--kernel32", type=int, default=0, help="srk option gemm32_kernel (the same for fp32)")
     a = ap.parse_args()
     _lib.set_matmul_precision(a.precision)
     _lib.call("srk_set_option", b"gemm16_kernel", a.kernel16)
+    _lib.call("srk_set_option", b"gemm32_kernel", a.kernel32)
     pname = {"fp32": "gemm_f32", "bf16": "gemm_bf16", "fp16": "gemm_f16"}[a.precision]
     peak = 157.3 if a.precision == "fp32" else 2500.0
     tdt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[a.precision]
@@ -95,7 +97,7 @@ def main():
         res[name] = {"us": round(ms / c * 1e3, 1), "TF": round(tf, 1), "frac": round(tf / peak, 3), "rel_err": err,
                      "torch_us": round(t_us, 1), "torch_TF": round(2.0 * M * N * K / (t_us * 1e-6) / 1e12, 1)}
         print(name, json.dumps(res[name]), flush=True)
-    print(json.dumps({"remap": os.environ.get("SRK_GEMM_REMAP", "1"), "kernel16": a.kernel16, "shapes": res}))
+    print(json.dumps({"remap": os.environ.get("SRK_GEMM_REMAP", "1"), "kernel16": a.kernel16, "kernel32": a.kernel32, "shapes": res}))
 
 
 if __name__ == "__main__":

@@ -15,7 +15,7 @@ for pmc in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
            "GRBM_GUI_ACTIVE GRBM_COUNT" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -k 10 120 rocprofv3 --kernel-trace --pmc $pmc -d "$ROOT/$OUT/p${i}_gemm" -o run -- \
-    python3 tools/gemm_bench.py --precision bf16 --h16 --kernel16 $K16 --reps 3 > "$OUT/p${i}.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p${i}.log"; exit 1; }
+    python3 tools/gemm_bench.py --precision ${PREC:-bf16} $([ "${PREC:-bf16}" = fp32 ] || echo --h16) --kernel16 $K16 --reps 3 > "$OUT/p${i}.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p${i}.log"; exit 1; }
   echo "pass $i ok"
 done
 python3 tools/pmc_table.py "$OUT" > "$OUT/summary.txt" && rm -rf "$OUT"/p[0-9]*_gemm && cat "$OUT/summary.txt"

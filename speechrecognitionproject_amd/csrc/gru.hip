@@ -349,14 +349,15 @@ int to16(const float* src, int64_t rows, int64_t cols, uint16_t* dst, int64_t co
 // Bias gradients from the 16-bit backward kernel's partials [part][2 dir][4][H] (sums of dar, daz,
 // dan, dan * r), summed over the valid (chunk, group) parts in order: db_ih = (dar, daz, dan),
 // db_hh = (dar, daz, dan * r); `accumulate` adds into the caller's tensors.
-__global__ void dbias_reduce_kernel(const float* __restrict__ part, int nparts, int B, int H, float* __restrict__ db_ih,
-                                    float* __restrict__ db_hh, int accumulate) {
+__global__ void dbias_reduce_kernel(const float* __restrict__ part, int nparts, int B, int H, int rows_per_part,
+                                    float* __restrict__ db_ih, float* __restrict__ db_hh, int accumulate) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over [2 dir][3][H]
   if (i >= 2 * 3 * H) return;
   const int dir = i / (3 * H), g = (i / H) % 3, j = i % H;
+  const int per_chunk = 256 / rows_per_part;
   float si = 0.f, sh = 0.f;
   for (int p = 0; p < nparts; ++p) {
-    if ((p / 4) * 256 + (p % 4) * 64 >= B) continue;   // (chunk, group) without rows
+    if ((p / per_chunk) * 256 + (p % per_chunk) * rows_per_part >= B) continue;   // (chunk, group) without rows
     const float* q = part + ((size_t)p * 2 + dir) * 4 * H;
     si += q[g * H + j];
     sh += q[(g == 2 ? 3 : g) * H + j];
@@ -404,7 +405,7 @@ static int64_t pad_off(int64_t B, int64_t T, int64_t H, int backward) {
 
 // Then the bf16 / fp16 ("h16") region, used when the 16-bit persistent kernels run (use_h16):
 //   fwd: x16 [B*T][in8] | W_ih16 [6H][in8] | y16 [B*T][2H]          (16-bit, kept for the backward)
-//   bwd: bias partials [4 * chunks][2][4][H] | dW_ih [6H][in8] | dx [B*T][in8]   (fp32; the last two
+//   bwd: bias partials [8 * chunks][2][4][H] | dW_ih [6H][in8] | dx [B*T][in8]   (fp32; the last two
 //        only when in8 != in); dgi16 / dgh16 alias the fp32 dgi region (unused in this mode).
 static int64_t pad_end(int64_t B, int64_t T, int64_t in, int64_t H, int backward) {
   int64_t e = pad_off(B, T, H, backward) + 64;
@@ -420,7 +421,7 @@ static int64_t h16_floats(int64_t B, int64_t T, int64_t in, int64_t H, int backw
   const int64_t in8 = in8_of(in), BT = B * T;
   if (!backward) return up64(BT * in8 / 2 + 1) + up64(6 * H * in8 / 2 + 1) + up64(BT * 2 * H / 2 + 1);
   const int64_t chunks = (B + 255) / 256;
-  return up64(chunks * 4 * 2 * 4 * H) + (in8 != in ? up64(6 * H * in8) + up64(BT * in8) : 0);
+  return up64(chunks * 8 * 2 * 4 * H) + (in8 != in ? up64(6 * H * in8) + up64(BT * in8) : 0);   // <= 8 parts per chunk
 }
 // The 16-bit path: a 16-bit precision, the persistent kernels (both directions of the layer), and
 // 32-bit byte offsets for the 16-bit GEMM operands.
@@ -536,7 +537,7 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
     uint16_t* dgh16 = dgi16 + BT * 6 * H;
     float* part = ws + pad_end(B, T, in, H, 1);
     const int64_t chunks = (B + 255) / 256;
-    float* dwpad = part + up64(chunks * 4 * 2 * 4 * H);
+    float* dwpad = part + up64(chunks * 8 * 2 * 4 * H);
     float* dxpad = dwpad + up64(6 * H * in8);
     srk::GruPArgs p{};
     p.B = (int)B; p.T = (int)T; p.H = (int)H;
@@ -546,8 +547,9 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
     p.counters = reinterpret_cast<unsigned*>(ws + bwd_counter_off(B, T, H));
     int rc;
     if ((rc = srk::gru_persistent_launch(p, true, s))) return rc;
+    const int prows = srk::gru_bias_part_rows();
     hipLaunchKernelGGL(srk::dbias_reduce_kernel, dim3((unsigned)((6 * H + 255) / 256)), dim3(256), 0, s, part,
-                       (int)(chunks * 4), (int)B, (int)H, db_ih, db_hh, accumulate);
+                       (int)(chunks * (256 / prows)), (int)B, (int)H, prows, db_ih, db_hh, accumulate);
     SRK_CHECK_HIP(hipGetLastError());
     const float beta = accumulate ? 1.f : 0.f;
     {  // dW_ih [6H, in] = dgi16^T x16

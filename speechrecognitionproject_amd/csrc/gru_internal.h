@@ -36,7 +36,7 @@ struct GruPArgs {
   uint16_t* y16;         // fwd: h [B][T][2H] rounded to 16 bit
   uint16_t* dgi16;       // bwd: dgi [B*T][6H] (replaces the fp32 dgi)
   uint16_t* dgh16;       // bwd: dgh [2][B][T][3H], edge rows zero (replaces dgh / dgh_edge)
-  float* dbias;          // bwd with dgi16: bias-gradient partials [chunk * G + group][2 dir][4][H]
+  float* dbias;          // bwd with dgi16: bias-gradient partials [chunk * (256 / rows per group) + group][2 dir][4][H]
                          //   (sum over t and the group's rows of dar, daz, dan, dan * r)
   int chunk;             // index of this launch's 64*G-row batch chunk
   // fused small input projection (in <= kFusedIn, the 39 MFCC features of model_mfcc_bgru.py:25):
@@ -62,6 +62,9 @@ extern int g_opt_gru_persistent;
 extern unsigned long long* g_opt_gru_trace;   // device buffer or nullptr
 extern unsigned g_opt_gru_spin_limit;          // 0 = default (~2 s); test hook "gru_spin_limit"
 extern int g_opt_gru_xcd_local;                // XCD-local hand-off when the census allows (default 1)
+extern int g_opt_gru_lp2;                      // 16-bit recurrence on 32 x 32 workgroups (default 1)
+// Batch rows per bias-gradient partial of the 16-bit backward kernel (32 or 64; 256-row launch chunks).
+int gru_bias_part_rows();
 // Host-pinned health word (device-mapped pointer in *dev): non-zero once any persistent-kernel
 // spin-wait has given up; read without a device synchronization by srk_health_check.
 int health_word(unsigned** host, unsigned** dev);

@@ -158,6 +158,12 @@ __device__ __forceinline__ void stamp(const GruPArgs& a, int step, int i) {
     a.trace[((size_t)blockIdx.x * a.T + step) * 8 + i] = __builtin_amdgcn_s_memrealtime();
 }
 
+// Diagnostics: the workgroup's (direction, group) pair and slice, in trace slot 5 of its step 0.
+__device__ __forceinline__ void trace_id(const GruPArgs& a, int dir, int group, int slice) {
+  if (a.trace && threadIdx.x == 0)
+    a.trace[(size_t)blockIdx.x * a.T * 8 + 5] = ((unsigned long long)(dir * a.G + group) << 8) | (unsigned)slice;
+}
+
 // (direction, group, slice) of this workgroup: the S slices of one (direction, group) pair are
 // dealt to blocks of ONE XCD (blocks b, b+8, ... share an XCD under round-robin dispatch), so the
 // handed-off rows stay in that XCD's L2.  Speed only; the protocol does not depend on it.
@@ -175,7 +181,8 @@ __device__ __forceinline__ void map_block(int G, int S, int& dir, int& group, in
 // MI355X_MICROARCH.md "Valid forms" row 1, correct under any placement).  With xcd_local and a full
 // 256-workgroup grid, a census first asks the hardware which XCD each workgroup runs on
 // (HW_REG_XCC_ID) and hands out slots per XCD; when every XCD holds exactly 32 workgroups, XCD x
-// runs (direction, group) pair x — then producers and consumers of a pair provably share one L2, the
+// runs (direction, group) pairs x * 32 / S .. (S slices per pair: one pair of 32 slices, or two of
+// 16) — then producers and consumers of a pair provably share one L2, the
 // hand-off bytes and flags are PLAIN stores that stay in that L2 (no write-through to the Infinity
 // Cache and back) and consumers keep reading them with sc1 (L1-bypassing) loads.  Otherwise every
 // workgroup (they all read the same final census) falls back to the default protocol.
@@ -204,12 +211,14 @@ __device__ __forceinline__ void place(const GruPArgs& a, int S, int& dir, int& g
       info[1] = (int)slot;
     }
     __syncthreads();
-    const int pair = __builtin_amdgcn_readfirstlane(info[0]);
-    if (pair >= 0) {
+    const int xcc = __builtin_amdgcn_readfirstlane(info[0]);
+    if (xcc >= 0) {   // XCD x hosts pairs x * (32 / S) .. : 32 workgroups = 32 / S whole (direction, group) pairs
+      const int slot = __builtin_amdgcn_readfirstlane(info[1]);
+      const int pair = xcc * (32 / S) + slot / S;
       local = true;
       dir = pair / a.G;
       group = pair % a.G;
-      slice = __builtin_amdgcn_readfirstlane(info[1]);
+      slice = slot % S;
       return;
     }
   }
@@ -322,6 +331,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
   int dir, group, slice;
   bool local;
   place(a, H / kUnits, dir, group, slice, local);
+  trace_id(a, dir, group, slice);
   const int T = a.T, j0 = slice * kUnits, j = j0 + lr;
   const int b0 = a.b_begin + group * kRows;
   const int b_last = a.b_end - 1;
@@ -461,6 +471,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
   int dir, group, slice;
   bool local;
   place(a, H / kUnits, dir, group, slice, local);
+  trace_id(a, dir, group, slice);
   const int T = a.T, B = a.B, j0 = slice * kUnits, j = j0 + lr;
   const int b0 = a.b_begin + group * kRows;
   const int b_last = a.b_end - 1;
@@ -646,6 +657,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
   int dir, group, slice;
   bool local;
   place(a, H / kUnits, dir, group, slice, local);
+  trace_id(a, dir, group, slice);
   const int T = a.T, j0 = slice * kUnits, j = j0 + lr;
   const int b0 = a.b_begin + group * kRows;
   const int b_last = a.b_end - 1;
@@ -781,6 +793,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
   int dir, group, slice;
   bool local;
   place(a, H / kUnits, dir, group, slice, local);
+  trace_id(a, dir, group, slice);
   const int T = a.T, B = a.B, j0 = slice * kUnits, j = j0 + lr;
   const int b0 = a.b_begin + group * kRows;
   const int b_last = a.b_end - 1;
@@ -958,6 +971,432 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
   }
 }
 
+// ------------------------------------------------------------------ 16-bit operands, 32 x 32 workgroups
+// The bf16 / fp16 recurrence with workgroup = (direction, 32 batch rows, 32 hidden units) instead of
+// (direction, 64 rows, 16 units): the same MFMA work per workgroup, but every consumer reads half the
+// hand-off (32 rows x H instead of 64 x H: the L2 -> CU broadcast that sets the step time,
+// profiles/r02*_gru_trace*) and each wave depends on 8 producers instead of 32.
+//  * wave w = (row block rb = w & 1, k half kh = w >> 1): 16 rows x all 96 gate columns (fwd) or both
+//    16-unit column blocks (bwd), over HALF of k — the k blocks of producers 8 kh .. 8 kh + 7 (slice s
+//    owns units 32 s .. 32 s + 31 = k block s of h, blocks g * 16 + s of the 3H-wide dg);
+//  * the two k halves are combined through LDS in a fixed order (kh = 0 part + kh = 1 part, IEEE
+//    addition commutes), after which wave (rb, kh) owns units 32 s + 16 kh .. + 16 of its rows: the
+//    cell epilogue is the 64 x 16 kernels' per-lane layout;
+//  * a wave waits only for its 8 producers (per-wave polls of per-producer flags in the XCD-local /
+//    flag protocols; the group counter otherwise), loads its 8 (fwd) or 24 (bwd) fragment chunks and
+//    runs 48 MFMAs;
+//  * hand-off chunks [buffer][group][rb][k block][lane][8 x 16-bit] (1 KB each): a producer writes 2
+//    (fwd: k block s) or 6 (bwd: g * 16 + s); flags [2 dir][G][16] (<= 256 words).
+// The backward kernel needs the 16-bit outputs (dgi16 / dgh16 / bias partials [chunk * 8 + group]).
+constexpr int kRows2 = 32, kUnits2 = 32;
+
+__device__ __forceinline__ void lp2_wait(const GruPArgs& a, int dir, int group, int first, int count, int step,
+                                         bool per) {
+  const int lane = threadIdx.x & 63;
+  unsigned spins = 0;
+  if (per) {   // per-producer flags, this wave's producers only
+    unsigned* fl = a.counters + (dir * a.G + group) * 16 + first;
+    while (true) {
+      const unsigned v = lane < count ? __hip_atomic_load(fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : 0xffffffffu;
+      if (__all(v >= (unsigned)step)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins >= a.spin_limit) {
+        if (lane == 0) spin_gave_up(a);
+        break;
+      }
+    }
+  } else {     // the group's arrival counter (16 producers per step)
+    unsigned* cnt = a.counters + (dir * a.G + group) * 16;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 16u * (unsigned)step) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins >= a.spin_limit) {
+        if (lane == 0) spin_gave_up(a);
+        break;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void lp2_arrive(const GruPArgs& a, int dir, int group, int slice, int step, bool per,
+                                           bool local) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (per) {
+      unsigned* f = a.counters + (dir * a.G + group) * 16 + slice;
+      if (local)
+        __builtin_amdgcn_raw_buffer_store_b32((unsigned)(step + 1), rsrc(reinterpret_cast<const float*>(f)), 0, 0, 0);
+      else
+        __hip_atomic_store(f, (unsigned)(step + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_fetch_add(a.counters + (dir * a.G + group) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int H> constexpr int lp2_fwd_wpq() { return (H + 16) / 8; }
+template <int H> constexpr int lp2_bwd_wpq() { return (3 * H + 16) / 8; }
+constexpr int kXP2 = 20;   // pitch of the k-half exchange tiles (16 columns + 4: conflict-free b32 writes)
+
+// LDS: W slice [96][H + 16] 16-bit (row g * 32 + jj) | hT [32][36] fp32 | W_ih slice [96][kXP] fp32 |
+// exchange [4 waves][3][16][kXP2] fp32
+template <int H, bool F16>
+__global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs a) {
+  using Ops = RecOps<F16>;
+  using e8 = typename Ops::e8;
+  constexpr int U = kUnits2, S = H / U, WPQ = lp2_fwd_wpq<H>(), HTP = U + 4, NKB = H / 32, KH = NKB / 2;
+  constexpr int RNDX = F16 ? 2 : 1;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  u32x4* Ws = reinterpret_cast<u32x4*>(smem);
+  float* hT = smem + 3 * U * WPQ * 4;
+  float* Wx = hT + kRows2 * HTP;
+  float* X = Wx + 3 * U * kXP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
+  const int rb = wave & 1, kh = wave >> 1;
+  int dir, group, slice;
+  bool local;
+  place(a, S, dir, group, slice, local);
+  trace_id(a, dir, group, slice);
+  const bool per = a.flags || local;
+  const int T = a.T, j0 = slice * U, ju = kh * 16 + lr, j = j0 + ju;
+  const int b0 = a.b_begin + group * kRows2, b_last = a.b_end - 1, rbase = b0 + rb * 16;
+
+  {  // this slice of W_hh[dir] (3 gates x 32 units), rounded to 16 bits -> LDS
+    const float* W = a.w_hh + (size_t)dir * 3 * H * H;
+    for (int v = tid; v < 3 * U * (H / 8); v += 256) {
+      const int c = v / (H / 8), kq = v % (H / 8), g = c / U, jj = c % U;
+      const float* src = W + (size_t)(g * H + j0 + jj) * H + kq * 8;
+      Ws[c * WPQ + kq] = pack8<F16>(cat8(ld4(src), ld4(src + 4)));
+    }
+  }
+  const bool fused = a.x_in != nullptr;
+  if (fused) {   // W_ih slice (rows g * 32 + jj), rounded like the GEMM operands
+    const float* W = a.w_ih + (size_t)dir * 3 * H * a.in;
+    for (int v = tid; v < 3 * U * kFusedIn; v += 256) {
+      const int c = v / kFusedIn, k = v % kFusedIn, g = c / U, jj = c % U;
+      Wx[c * kXP + k] = k < a.in ? rnd16<RNDX>(W[(size_t)(g * H + j0 + jj) * a.in + k]) : 0.f;
+    }
+  }
+  float xnext[kFusedIn / 4];
+  if (fused) load_x(a, dir == 0 ? 0 : T - 1, min(rbase + lr, b_last), lq, xnext);
+  const float bir = fused ? a.b_ih[dir * 3 * H + j] : 0.f, biz = fused ? a.b_ih[dir * 3 * H + H + j] : 0.f,
+              bin = fused ? a.b_ih[dir * 3 * H + 2 * H + j] : 0.f;
+  const float bhr = a.b_hh[dir * 3 * H + j], bhz = a.b_hh[dir * 3 * H + H + j], bhn = a.b_hh[dir * 3 * H + 2 * H + j];
+  __syncthreads();
+
+  const int Gp = a.G;
+  const __amdgpu_buffer_rsrc_t rx = rsrc(a.xbuf + (size_t)dir * 2 * Gp * kRows2 * H);   // 16-bit [2][Gp][2][NKB][64][8]
+  float hreg[4] = {0.f, 0.f, 0.f, 0.f};
+  float gsv[4][4];
+
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? step : T - 1 - step;
+    stamp(a, step, 0);
+    float gr[4], gz[4], gn[4];
+    if (fused) {   // the lane's input projections (rows rbase + 4 lq + r, unit j), before the wait
+      float xv[kFusedIn / 4];
+#pragma unroll
+      for (int m = 0; m < kFusedIn / 4; ++m) xv[m] = rnd16<RNDX>(xnext[m]);
+      f32x4 ax[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int m = 0; m < kFusedIn / 4; ++m) {
+        if (4 * m >= a.in) break;   // uniform
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+          ax[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[m], Wx[(g * U + kh * 16 + lr) * kXP + 4 * m + lq], ax[g], 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gr[r] = ax[0][r] + bir;
+        gz[r] = ax[1][r] + biz;
+        gn[r] = ax[2][r] + bin;
+      }
+      if (step + 1 < T) load_x(a, dir == 0 ? t + 1 : t - 1, min(rbase + lr, b_last), lq, xnext);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = min(rbase + lq * 4 + r, b_last);
+        const float* gi = a.gi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
+        gr[r] = gi[j];
+        gz[r] = gi[H + j];
+        gn[r] = gi[2 * H + j];
+      }
+    }
+    float full[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    if (step > 0) {
+      lp2_wait(a, dir, group, kh * KH, KH, step, per);
+      stamp(a, step, 1);
+      const unsigned base =
+          (unsigned)((((((size_t)((step - 1) & 1) * Gp + group) * 2 + rb) * NKB + kh * KH) * 64 + lane) * 16);
+      v4f hv[KH];
+#pragma unroll
+      for (int i = 0; i < KH; ++i) hv[i] = ld4_sc1(rx, base + i * 1024);
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 acc[6];
+#pragma unroll
+      for (int cb = 0; cb < 6; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      u32x4 wv[2][6];
+#pragma unroll
+      for (int cb = 0; cb < 6; ++cb) wv[0][cb] = Ws[((cb >> 1) * U + (cb & 1) * 16 + lr) * WPQ + (kh * KH) * 4 + lq];
+#pragma unroll
+      for (int i = 0; i < KH; ++i) {
+        const int c = i & 1;
+        if (i + 1 < KH) {
+#pragma unroll
+          for (int cb = 0; cb < 6; ++cb)
+            wv[c ^ 1][cb] = Ws[((cb >> 1) * U + (cb & 1) * 16 + lr) * WPQ + (kh * KH + i + 1) * 4 + lq];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const e8 hf = __builtin_bit_cast(e8, hv[i]);
+#pragma unroll
+        for (int cb = 0; cb < 6; ++cb) acc[cb] = Ops::mma(hf, __builtin_bit_cast(e8, wv[c][cb]), acc[cb]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // k halves: hand the partner (same rows, other kh) the column blocks it owns, take ours.  kh is
+      // wave-uniform: one static code path per value (an acc index computed from kh would make the
+      // compiler select registers with compare / cndmask chains)
+      float* Xw = X + wave * (3 * 16 * kXP2);
+      const float* Xp = X + (wave ^ 2) * (3 * 16 * kXP2);
+      auto exchange = [&](auto KH_) {
+        constexpr int K = decltype(KH_)::value;
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Xw[(g * 16 + 4 * lq + r) * kXP2 + lr] = acc[2 * g + (1 - K)][r];
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float o = acc[2 * g + K][r], p = Xp[(g * 16 + 4 * lq + r) * kXP2 + lr];
+            full[g][r] = K == 0 ? o + p : p + o;   // always (kh 0 part) + (kh 1 part)
+          }
+      };
+      if (__builtin_amdgcn_readfirstlane(kh) == 0) exchange(std::integral_constant<int, 0>{});
+      else exchange(std::integral_constant<int, 1>{});
+      if (a.trace) {
+        asm volatile("" ::"v"(full[0][0]), "v"(full[1][0]), "v"(full[2][0]));
+        stamp(a, step, 2);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = rb * 16 + lq * 4 + r;
+      const float ghn = full[2][r] + bhn;
+      const float rg = sigmoid_fast(gr[r] + (full[0][r] + bhr));
+      const float zg = sigmoid_fast(gz[r] + (full[1][r] + bhz));
+      const float ng = tanh_fast(gn[r] + rg * ghn);
+      const float h = (1.0f - zg) * ng + zg * hreg[r];
+      hreg[r] = h;
+      hT[rl * HTP + ju] = h;
+      gsv[r][0] = rg;
+      gsv[r][1] = zg;
+      gsv[r][2] = ng;
+      gsv[r][3] = ghn;
+    }
+    __syncthreads();
+    stamp(a, step, 3);
+    if (step + 1 < T && tid < 128) {   // hand-off (16-bit): chunk (rb', k block = slice), lane l: row l & 15, 8 units
+      const int rbp = tid >> 6, l = tid & 63, row = rbp * 16 + (l & 15);
+      if (b0 + row <= b_last) {
+        const float* src = hT + row * HTP + 8 * (l >> 4);
+        st4_ho(rx, (unsigned)((((((size_t)(step & 1) * Gp + group) * 2 + rbp) * NKB + slice) * 64 + l) * 16),
+               __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))), local);
+      }
+    }
+    lp2_arrive(a, dir, group, slice, step, per, local);   // the hand-off only: y and the gates go out after it
+    stamp(a, step, 4);
+    {
+      const int row = tid >> 3, u4 = (tid & 7) * 4;   // y (fp32, + the 16-bit copy): 32 rows x 32 units
+      if (b0 + row <= b_last) {
+        const v4f yv = ld4(hT + row * HTP + u4);
+        st4(a.y + ((size_t)(b0 + row) * T + t) * 2 * H + dir * H + j0 + u4, yv);
+        if (a.y16) {
+          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+          typedef __attribute__((ext_vector_type(4))) typename std::conditional<F16, _Float16, __bf16>::type e4;
+          *reinterpret_cast<u32x2*>(a.y16 + ((size_t)(b0 + row) * T + t) * 2 * H + dir * H + j0 + u4) =
+              __builtin_bit_cast(u32x2, __builtin_convertvector(yv, e4));
+        }
+      }
+    }
+    store_gates(a, gsv, dir, t, rbase + lq * 4, b_last, j);
+  }
+}
+
+// LDS: W^T slice [32][3H + 16] 16-bit (unit jj, gate row c) | dT [32][3][36] | dI [32][36] |
+// exchange [4 waves][16][kXP2] | bias partials [4 waves][4][16]
+template <int H, bool F16>
+__global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs a) {
+  using Ops = RecOps<F16>;
+  using e8 = typename Ops::e8;
+  constexpr int U = kUnits2, S = H / U, WPQ = lp2_bwd_wpq<H>(), DTP = U + 4, NKB = 3 * H / 32, KS = S / 2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  u32x4* Wt = reinterpret_cast<u32x4*>(smem);
+  float* dT = smem + U * WPQ * 4;              // [32][3][DTP]
+  float* dI = dT + kRows2 * 3 * DTP;           // [32][DTP]: dan (dgi's third gate; dT holds dan * r)
+  float* X = dI + kRows2 * DTP;                // [4][16][kXP2]
+  float* red = X + 4 * 16 * kXP2;              // [4][4][16]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
+  const int rb = wave & 1, kh = wave >> 1;
+  int dir, group, slice;
+  bool local;
+  place(a, S, dir, group, slice, local);
+  trace_id(a, dir, group, slice);
+  const bool per = a.flags || local;
+  const int T = a.T, B = a.B, j0 = slice * U, ju = kh * 16 + lr, j = j0 + ju;
+  const int b0 = a.b_begin + group * kRows2, b_last = a.b_end - 1, rbase = b0 + rb * 16;
+
+  {  // W_hh[dir][c][j0 .. j0+31] for all 3H rows c, transposed [jj][c] in 8-deep c packs
+    const float* W = a.w_hh + (size_t)dir * 3 * H * H;
+    for (int v = tid; v < (3 * H / 8) * (U / 4); v += 256) {
+      const int cb = v / (U / 4), jq = (v % (U / 4)) * 4;
+      v4f w[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) w[e] = ld4(W + (size_t)(cb * 8 + e) * H + j0 + jq);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        Wt[(jq + u) * WPQ + cb] = pack8<F16>(v8f{w[0][u], w[1][u], w[2][u], w[3][u], w[4][u], w[5][u], w[6][u], w[7][u]});
+    }
+  }
+  __syncthreads();
+
+  const int Gp = a.G;
+  const __amdgpu_buffer_rsrc_t rg_ = rsrc(a.xbuf + (size_t)dir * 2 * Gp * kRows2 * 3 * H);   // 16-bit [2][Gp][2][NKB][64][8]
+  float dhz[4] = {0.f, 0.f, 0.f, 0.f};
+  float sb[4] = {0.f, 0.f, 0.f, 0.f};   // sums of dar, daz, dan, dan * r over t and the lane's rows
+
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? T - 1 - step : step;
+    const int tprev = dir == 0 ? t - 1 : t + 1;
+    const bool edge = (step == T - 1);
+    stamp(a, step, 0);
+    float g_r[4], g_z[4], g_n[4], g_h[4], dyv[4], hpv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = min(rbase + lq * 4 + r, b_last);
+      const float* gs = a.gates + (((size_t)dir * T + t) * B + b) * 4 * H;
+      g_r[r] = gs[j];
+      g_z[r] = gs[H + j];
+      g_n[r] = gs[2 * H + j];
+      g_h[r] = gs[3 * H + j];
+      dyv[r] = a.dy[((size_t)b * T + t) * 2 * H + dir * H + j];
+      hpv[r] = edge ? 0.f : a.y_in[((size_t)b * T + tprev) * 2 * H + dir * H + j];
+    }
+    float full[4] = {0.f, 0.f, 0.f, 0.f};
+    if (step > 0) {
+      lp2_wait(a, dir, group, kh * KS, KS, step, per);
+      stamp(a, step, 1);
+      const unsigned base = (unsigned)(((((size_t)((step - 1) & 1) * Gp + group) * 2 + rb) * NKB * 64 + lane) * 16);
+      v4f dv[3 * KS];   // dv[3 i + g] = k block g * 16 + kh * KS + i (gate g of producer kh * KS + i)
+#pragma unroll
+      for (int i = 0; i < KS; ++i)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) dv[3 * i + g] = ld4_sc1(rg_, base + (g * 16 + kh * KS + i) * 1024);
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      auto blk = [&](int n) { return (n % 3) * 16 + kh * KS + n / 3; };
+      u32x4 wv[2][2];
+#pragma unroll
+      for (int ub = 0; ub < 2; ++ub) wv[0][ub] = Wt[(ub * 16 + lr) * WPQ + blk(0) * 4 + lq];
+#pragma unroll
+      for (int n = 0; n < 3 * KS; ++n) {
+        const int c = n & 1;
+        if (n + 1 < 3 * KS) {
+#pragma unroll
+          for (int ub = 0; ub < 2; ++ub) wv[c ^ 1][ub] = Wt[(ub * 16 + lr) * WPQ + blk(n + 1) * 4 + lq];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ub = 0; ub < 2; ++ub) acc[ub] = Ops::mma(__builtin_bit_cast(e8, dv[n]), __builtin_bit_cast(e8, wv[c][ub]), acc[ub]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      float* Xw = X + wave * 16 * kXP2;   // the partner's unit block (static per kh, see the forward)
+      const float* Xp = X + (wave ^ 2) * 16 * kXP2;
+      auto exchange = [&](auto KH_) {
+        constexpr int K = decltype(KH_)::value;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Xw[(4 * lq + r) * kXP2 + lr] = acc[1 - K][r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float o = acc[K][r], p = Xp[(4 * lq + r) * kXP2 + lr];
+          full[r] = K == 0 ? o + p : p + o;
+        }
+      };
+      if (__builtin_amdgcn_readfirstlane(kh) == 0) exchange(std::integral_constant<int, 0>{});
+      else exchange(std::integral_constant<int, 1>{});
+      if (a.trace) {
+        asm volatile("" ::"v"(full[0]));
+        stamp(a, step, 2);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = rb * 16 + lq * 4 + r, b = b0 + rl;
+      float dh = dyv[r];
+      if (step > 0) dh += full[r] + dhz[r];
+      const float rg = g_r[r], zg = g_z[r], ng = g_n[r], ghn = g_h[r], hp = hpv[r];
+      const float dn = dh * (1.0f - zg);
+      const float daz = dh * (hp - ng) * zg * (1.0f - zg);
+      const float dan = dn * (1.0f - ng * ng);
+      const float dar = dan * ghn * rg * (1.0f - rg);
+      dhz[r] = dh * zg;
+      dT[(rl * 3 + 0) * DTP + ju] = dar;
+      dT[(rl * 3 + 1) * DTP + ju] = daz;
+      dT[(rl * 3 + 2) * DTP + ju] = dan * rg;
+      dI[rl * DTP + ju] = dan;
+      if (b <= b_last) {
+        sb[0] += dar;
+        sb[1] += daz;
+        sb[2] += dan;
+        sb[3] += dan * rg;
+      }
+    }
+    __syncthreads();
+    stamp(a, step, 3);
+    if (!edge) {   // hand-off (16-bit): chunks (rb', k block g * 16 + slice), lane l: row l & 15, 8 units
+      for (int v = tid; v < 6 * 64; v += 256) {
+        const int c = v >> 6, rbp = c / 3, g = c % 3, l = v & 63, row = rbp * 16 + (l & 15);
+        if (b0 + row > b_last) continue;
+        const float* src = dT + (row * 3 + g) * DTP + 8 * (l >> 4);
+        st4_ho(rg_, (unsigned)((((((size_t)(step & 1) * Gp + group) * 2 + rbp) * NKB + g * 16 + slice) * 64 + l) * 16),
+               __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))), local);
+      }
+    }
+    lp2_arrive(a, dir, group, slice, step, per, local);   // the hand-off only: dgh16 / dgi16 go out after it
+    stamp(a, step, 4);
+    for (int v = tid; v < 2 * 32 * 3 * 4; v += 256) {   // 16-bit dgh (edge rows zero) and dgi: (row, gate, 8 units)
+      const int which = v / 384, w = v % 384, row = w / 12, g = (w % 12) >> 2, q8 = w & 3, b = b0 + row;
+      if (b > b_last) continue;
+      const float* src = which == 0 || g < 2 ? dT + (row * 3 + g) * DTP + 8 * q8 : dI + row * DTP + 8 * q8;
+      v4f pk = __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4))));
+      if (which == 0) {
+        if (edge) pk = v4f{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<v4f*>(a.dgh16 + (((size_t)dir * B + b) * T + t) * 3 * H + g * H + j0 + 8 * q8) = pk;
+      } else {
+        *reinterpret_cast<v4f*>(a.dgi16 + ((size_t)b * T + t) * 6 * H + dir * 3 * H + g * H + j0 + 8 * q8) = pk;
+      }
+    }
+  }
+  // bias-gradient partials: lanes lr, lr + 16, lr + 32, lr + 48, then the two row-block waves in order
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    sb[q] += __shfl_xor(sb[q], 16);
+    sb[q] += __shfl_xor(sb[q], 32);
+  }
+  if (lq == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[(wave * 4 + q) * 16 + lr] = sb[q];
+  }
+  __syncthreads();
+  if (tid < 128) {
+    const int k2 = tid >> 6, q = (tid >> 4) & 3, u = tid & 15;   // waves (rb 0, k2) = 2 k2 and (rb 1, k2) = 2 k2 + 1
+    const float v = red[((2 * k2) * 4 + q) * 16 + u] + red[((2 * k2 + 1) * 4 + q) * 16 + u];
+    a.dbias[(((size_t)(a.chunk * 8 + group) * 2 + dir) * 4 + q) * H + j0 + k2 * 16 + u] = v;
+  }
+}
+
 size_t lds_bytes(int H, bool backward, int prec) {
   if (prec == kPrecF32) return backward ? bwd_lds_bytes(H) : fwd_lds_bytes(H);
   const size_t need = backward ? (size_t)kUnits * (3 * H + 16) * 2 + 64 * 4 * (kUnits + 4) * 4
@@ -965,6 +1404,38 @@ size_t lds_bytes(int H, bool backward, int prec) {
   // the sc1 hand-off is the form measured at ONE workgroup per CU (MI355X_MICROARCH.md, "Valid
   // forms" row 1): reserve more than half of the 160 KB so a second workgroup never fits
   return std::max<size_t>(need, 96 * 1024);
+}
+
+size_t lp2_lds_bytes(int H, bool backward) {
+  const size_t need = backward ? (size_t)kUnits2 * ((3 * H + 16) / 8) * 16 + (size_t)kRows2 * 3 * (kUnits2 + 4) * 4 +
+                                     (size_t)kRows2 * (kUnits2 + 4) * 4 + 4 * 16 * kXP2 * 4 + 4 * 4 * 16 * 4
+                               : (size_t)3 * kUnits2 * ((H + 16) / 8) * 16 + (size_t)kRows2 * (kUnits2 + 4) * 4 +
+                                     (size_t)3 * kUnits2 * kXP * 4 + 4 * 3 * 16 * kXP2 * 4;
+  return std::max<size_t>(need, 96 * 1024);   // one workgroup per CU (see lds_bytes)
+}
+
+template <int H>
+const void* lp2_kernel_ptr(bool backward, int prec) {
+  if (prec == kPrecF16)
+    return backward ? reinterpret_cast<const void*>(gru_bwd_persistent_lp2_kernel<H, true>)
+                    : reinterpret_cast<const void*>(gru_fwd_persistent_lp2_kernel<H, true>);
+  return backward ? reinterpret_cast<const void*>(gru_bwd_persistent_lp2_kernel<H, false>)
+                  : reinterpret_cast<const void*>(gru_fwd_persistent_lp2_kernel<H, false>);
+}
+
+template <int H>
+int lp2_occupancy_ok(bool backward, int prec) {
+  static std::mutex mu;
+  static int occ[2][3] = {{-1, -1, -1}, {-1, -1, -1}};
+  std::lock_guard<std::mutex> lk(mu);
+  int& o = occ[backward ? 1 : 0][prec];
+  if (o < 0) {
+    const void* k = lp2_kernel_ptr<H>(backward, prec);
+    const size_t lds = lp2_lds_bytes(H, backward);
+    SRK_CHECK_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    SRK_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, 256, lds));
+  }
+  return o >= 1 ? 1 : 0;
 }
 
 template <int H>
@@ -1018,15 +1489,24 @@ int gru_persistent_supported(int64_t B, int64_t T, int64_t H, bool backward) {
   if ((double)B * T * 3 * H * 4 >= 2147483647.0 || (double)B * T * 2 * H * 4 >= 2147483647.0) return 0;
   const int64_t G = std::min<int64_t>((B + kRows - 1) / kRows, gmax);
   const int grid = (int)(2 * G * (H / kUnits));
-  const int ok = occupancy_ok<512>(backward, matmul_prec(), grid);
+  const int prec = matmul_prec();
+  int ok = occupancy_ok<512>(backward, prec, grid);
+  if (ok > 0 && prec != kPrecF32 && g_opt_gru_lp2) ok = lp2_occupancy_ok<512>(backward, prec);
   return ok < 0 ? 0 : ok;
 }
+
+int gru_bias_part_rows() { return (matmul_prec() != kPrecF32 && g_opt_gru_lp2) ? kRows2 : kRows; }
 
 int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
   const int gmax = gru_persistent_groups(a.H);
   SRK_REQUIRE(gmax > 0 && a.H == 512, SRK_ERR_INVALID, "gru persistent: unsupported H");
   const int rows_per_launch = gmax * kRows;
   const int prec = matmul_prec();
+  // 16-bit operands: the 32 x 32 workgroup kernels (the backward one writes the 16-bit outputs only)
+  const bool lp2 = prec != kPrecF32 && g_opt_gru_lp2 && (!backward || a.dgi16 != nullptr);
+  const int rows_g = lp2 ? kRows2 : kRows, slices = lp2 ? a.H / kUnits2 : a.H / kUnits;
+  if (lp2 && lp2_occupancy_ok<512>(backward, prec) <= 0)
+    SRK_REQUIRE(false, SRK_ERR_INVALID, "gru persistent: the 32 x 32 kernels do not fit one workgroup per CU");
   for (int c0 = 0; c0 < a.B; c0 += rows_per_launch) {
     GruPArgs ac = a;
     ac.trace = g_opt_gru_trace;
@@ -1038,15 +1518,19 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     ac.xcd_local = g_opt_gru_xcd_local;
     ac.b_begin = c0;
     ac.b_end = std::min(a.B, c0 + rows_per_launch);
-    ac.G = (ac.b_end - c0 + kRows - 1) / kRows;
+    ac.G = (ac.b_end - c0 + rows_g - 1) / rows_g;
     ac.chunk = c0 / rows_per_launch;
     SRK_CHECK_HIP(hipMemsetAsync(ac.counters, 0, (size_t)kCounterFloats * 4, s));
-    const dim3 grid((unsigned)(2 * ac.G * (a.H / kUnits)));
+    const dim3 grid((unsigned)(2 * ac.G * slices));
     const double flops = 2.0 * 2.0 * (double)(ac.b_end - c0) * 3 * a.H * a.H * (a.T - 1);
     ProfScope prof(backward ? (prec == kPrecF32 ? "gru_bwd_seq" : "gru_bwd_seq_lp")
                             : (prec == kPrecF32 ? "gru_fwd_seq" : "gru_fwd_seq_lp"), s, flops);
-    hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(kernel_ptr<512>(backward, prec))), grid,
-                       dim3(256), lds_bytes(512, backward, prec), s, ac);
+    if (lp2)
+      hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(lp2_kernel_ptr<512>(backward, prec))),
+                         grid, dim3(256), lp2_lds_bytes(512, backward), s, ac);
+    else
+      hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(kernel_ptr<512>(backward, prec))), grid,
+                         dim3(256), lds_bytes(512, backward, prec), s, ac);
     SRK_CHECK_HIP(hipGetLastError());
   }
   return SRK_OK;

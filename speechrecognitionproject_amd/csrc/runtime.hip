@@ -27,6 +27,7 @@ int matmul_prec() { return g_opt_matmul_prec.load(std::memory_order_relaxed); }
 unsigned long long* g_opt_gru_trace = nullptr;
 unsigned g_opt_gru_spin_limit = 0;
 int g_opt_gru_xcd_local = 1;
+int g_opt_gru_lp2 = 1;
 
 static thread_local std::string g_last_error;
 
@@ -351,6 +352,10 @@ int srk_set_option(const char* name, int64_t value) {
   }
   if (n == "gru_xcd_local") {   // persistent GRU: XCD-local hand-off when every XCD hosts one (dir, group)
     srk::g_opt_gru_xcd_local = value != 0;
+    return SRK_OK;
+  }
+  if (n == "gru_lp_32x32") {   // 16-bit recurrence: 32 x 32 workgroups (1) or 64 rows x 16 units (0)
+    srk::g_opt_gru_lp2 = value != 0;
     return SRK_OK;
   }
   if (n == "gru_trace_ptr") {   // diagnostics: device buffer of 8 x u64 per (workgroup, step), 0 = off

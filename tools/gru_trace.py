@@ -40,19 +40,13 @@ for name, b in (("fwd", fwd), ("bwd", bwd)):
     pub = (ts[:, 1:, 4] - ts[:, 1:, 3]).mean().item()
     step = ((ts[:, -1, 4] - ts[:, 0, 0]) / T).mean().item()
     start_skew = (ts[:, 0, 0].max() - ts[:, 0, 0].min()).item()
-    # group membership (csrc/gru_persistent.hip map_block): the 32 slices of a (direction, 64-row group)
-    G, S = nwg // 64, 32
-    q, r = nwg >> 3, nwg & 7
-    grp = []
-    for b in range(nwg):
-        xcd = b & 7
-        wgid = (xcd * (q + 1) if xcd < r else r * (q + 1) + (xcd - r) * q) + (b >> 3)
-        grp.append(wgid // S)
-    grp = torch.tensor(grp)
+    # group membership: the (direction, group) pair each workgroup ran, recorded by the kernel (trace_id)
+    grp = (b.view(nwg, T, 8)[:, 0, 5].cpu() >> 8)
+    npairs = int(grp.max().item()) + 1
     spread, prop = [], []
-    for g in range(2 * G):
+    for g in range(npairs):
         m = grp == g
-        pubs = ts[m][:, :, 4]                              # [32, T] publish stamps
+        pubs = ts[m][:, :, 4]                              # [slices, T] publish stamps
         spread.append((pubs.max(0).values - pubs.min(0).values)[:-1])
         # wait done at step s + 1 minus the group's LAST publish of step s: flag propagation
         prop.append(ts[m][:, 1:, 1] - pubs.max(0).values[None, :-1])

@@ -15,9 +15,10 @@ import os
 import sqlite3
 
 GROUPS = {  # srk_prof name -> substrings of the rocprof kernel symbols it covers
-    "gemm_f32": ("gemm_f32_kernel",), "gemm_bf16": ("gemm_h16_kernel", "gemm_lp_kernel"),
+    "gemm_f32": ("gemm_f32_kernel", "gemm_p32_kernel"), "gemm_bf16": ("gemm_h16_kernel", "gemm_lp_kernel", "gemm_g16_kernel"),
     "gru_fwd_seq": ("gru_fwd_persistent_kernel",), "gru_bwd_seq": ("gru_bwd_persistent_kernel",),
-    "gru_fwd_seq_lp": ("gru_fwd_persistent_lp_kernel",), "gru_bwd_seq_lp": ("gru_bwd_persistent_lp_kernel",),
+    "gru_fwd_seq_lp": ("gru_fwd_persistent_lp_kernel", "gru_fwd_persistent_lp2_kernel"),
+    "gru_bwd_seq_lp": ("gru_bwd_persistent_lp_kernel", "gru_bwd_persistent_lp2_kernel"),
     "gru_fwd_step": ("gru_fwd_step_kernel",), "gru_bwd_step": ("gru_bwd_step_kernel",),
     "mfcc": ("mfcc3_kernel", "mfcc2_kernel"), "fbank": ("fbank_kernel",), "spec": ("spec_kernel",),
     "conv_fwd": ("conv_gemm_kernel<0",), "conv_dgrad": ("conv_gemm_kernel<1",), "conv_wgrad": ("conv_gemm_kernel<2",),

@@ -315,13 +315,30 @@ __device__ __forceinline__ float bperm(int src_byte, float v) {
 
 typedef float f32x4_ __attribute__((ext_vector_type(4)));
 
+// Diagnostic build only (tools/build_variant.sh ... -DSRK_MFCC_STAMPS): per-wave s_memtime phase
+// totals, read back by srk_debug_mfcc_stamps (tools/mfcc_stamps.py).  Never in the product build.
+#ifdef SRK_MFCC_STAMPS
+constexpr int kStampPhases = 10;
+__device__ unsigned long long g_mfcc_stamps[512 * kM3Waves * kStampPhases];
+#define MFCC_STAMP(p)                                                   \
+  do {                                                                  \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
+    st_acc[p] += t_ - st_last;                                          \
+    st_last = t_;                                                       \
+  } while (0)
+#else
+#define MFCC_STAMP(p) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __restrict__ pcm, float* __restrict__ out,
                                                                   int layout, int64_t n_clips, DeviceTables t) {
   __shared__ __attribute__((aligned(16))) v2f tbuf[kM3Waves][3 * 340];
+  constexpr int DBP = kM3DbP;
   __shared__ __attribute__((aligned(16))) float db[51 * kM3DbP];
   __shared__ v2f s_tw[20 * 16];   // W320^(j k1) at [k1][j]
   __shared__ v2f s_post[320];     // W640^k (untangle twiddles)
-  __shared__ float cbuf[13 * kM3CP];
+  __shared__ float cbuf[2][13 * kM3CP];                         // coefficient images, alternating clips
+  __shared__ __attribute__((aligned(16))) float s_dct[13 * 128];   // DCT-II rows (ortho)
   __shared__ float red[kM3Waves];
   // the wave index in an SGPR: the chunk loop and its reflect / tail branches stay scalar
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -333,6 +350,7 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
 #pragma unroll
   for (int i = 0; i < 20; ++i) win[i] = *reinterpret_cast<const v2f*>(t.hann640f + 2 * (j + 16 * i));
   for (int i = threadIdx.x; i < 320; i += 64 * kM3Waves) s_post[i] = *reinterpret_cast<const v2f*>(t.post640 + i);
+  for (int i = threadIdx.x; i < 13 * 128; i += 64 * kM3Waves) s_dct[i] = t.dct[i];
   const int4 mlo = t.melq_lo[lane];   // {window start a, window start b, filter a, filter b}
   float mw[18];
 #pragma unroll
@@ -347,25 +365,38 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
   __syncthreads();
   v2f* tb = tbuf[wave];
   float* pb = reinterpret_cast<float*>(tb);   // |X|^2 [3][321] over the transpose slice
+#ifdef SRK_MFCC_STAMPS
+  unsigned long long st_acc[kStampPhases] = {}, st_last = __builtin_amdgcn_s_memtime();
+#endif
 
-  // One chunk of 3 frames: consumes `cur` (its samples) and issues the loads of the wave's next
-  // chunk into `nxt` right after the 20-point DFTs, so they overlap pass B, the untangle and the mel
-  // reduction.  The two register buffers alternate between consecutive steps (no copies: a copy
-  // would force the wait early); only wave 0, with an odd chunk count (5 of 17), swaps once per clip.
-  auto step = [&](v2f (&cur)[20], v2f (&nxt)[20], int64_t clip, int c, float& vmax) {
+  // Chunk order: wave w takes chunks (w + 4 k + 2) mod 17, k < nsteps, so the wave with the fifth
+  // chunk (wave 0) holds none of the two reflect-padded edge chunks (0 and 16, the dearer loads).
+  const int nsteps = (17 - wave + kM3Waves - 1) / kM3Waves;   // 5 for wave 0, else 4 (uniform)
+  auto chunk_of = [&](int k) { return (wave + kM3Waves * k + 2) % 17; };
+  // One chunk of 3 frames (the wave's k-th): consumes `raw` (its samples) and, right after the
+  // 20-point DFTs, re-fills it with the wave's next chunk (this clip's, else the next clip's first),
+  // so those loads overlap pass B, the untangle and the mel reduction.
+  auto step = [&](v2f (&raw)[20], int64_t clip, int k, float& vmax) {
+    const int c = chunk_of(k);
     v2f a[20];
 #pragma unroll
-    for (int i = 0; i < 20; ++i) a[i] = cur[i] * win[i];
+    for (int i = 0; i < 20; ++i) a[i] = raw[i] * win[i];
+    // the 19 twiddles are read before the DFT: read between the transpose stores, each one would
+    // wait out its own LDS round trip (the compiler keeps loads behind stores it cannot disambiguate)
+    v2f tw[19];
+#pragma unroll
+    for (int k1 = 1; k1 < 20; ++k1) tw[k1 - 1] = s_tw[k1 * 16 + j];
     dft20v(a);
     if (fa < 3) {
 #pragma unroll
-      for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? cm2(a[k1], s_tw[k1 * 16 + j]) : a[0];
+      for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? cm2(a[k1], tw[k1 - 1]) : a[0];
     }
-    {  // next: this clip's chunk c + 4, else the next clip's chunk `wave` (past the end: a re-read)
-      const bool more = c + kM3Waves < 17;
+    MFCC_STAMP(0);
+    {  // next: this clip's next chunk, else the next clip's first (past the end: a re-read)
+      const bool more = k + 1 < nsteps;
       int64_t nclip = more ? clip : clip + gridDim.x;
       nclip = nclip < n_clips ? nclip : clip;
-      mfcc_load_chunk(pcm + nclip * kPcmLen, more ? c + kM3Waves : wave, lane, nxt);
+      mfcc_load_chunk(pcm + nclip * kPcmLen, chunk_of(more ? k + 1 : 0), lane, raw);
     }
     wave_lds_fence();
     // lanes 60..63 (fb = 3) duplicate frame 2's reads and park their results in the unused tail
@@ -376,36 +407,42 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
     for (int jj = 0; jj < 16; ++jj) b[jj] = tb[fbr * 340 + k1b * 17 + jj];
     dft16v(b);
     wave_lds_fence();
-    // untangle the packed real FFT: X[k] = E + W640^k O, E = (Z[k] + Z*[320-k]) / 2,
-    // O = -i (Z[k] - Z*[320-k]) / 2; lane k1 = 0 holds both of its pairs (Z[20 k2], Z[20 (16 - k2)]).
-    // With A = Z[k], B = Z[320-k], W640^k = (c, s):  2 X = S + c U + s (-U.y, U.x),
-    // S = (A.x + B.x, A.y - B.y), U = (A.y + B.y, B.x - A.x).  The LDS holds |2 X|^2 = 4 |X|^2; the
-    // factor 1/4 is folded into the mel weights (exact).
-    // all 32 partner values are requested before any is used (the LDS crossbar latency overlaps);
-    // the arithmetic is scalar (packed fp32 issues at half rate and needs swizzle moves here)
-    float Bx[16], By[16];
+    MFCC_STAMP(1);
+    // untangle the packed real FFT: with A = Z[k], B = Z[320 - k], W = W640^k,
+    //   2 E = (A.x + B.x, A.y - B.y) = S,  2 O = -i (A - B*) = (A.y + B.y, B.x - A.x) = U,
+    //   2 X[k] = S + W U,  2 X[320 - k] = (S - W U)*,
+    // so one (A, B) pair gives two bins.  Lane (frame, k1) pairs its k2 < 8 with the partner lane
+    // (frame, 20 - k1) at 15 - k2 (ds_bpermute), which in turn covers the other 8; k1 = 0 and 10 pair
+    // inside the lane, and k1 = 0 also takes the self-paired bin 160.  The LDS holds |2 X|^2 = 4 |X|^2;
+    // the factor 1/4 is folded into the mel weights (exact).
+    float Bx[8], By[8];
+    v2f wpost[8];   // untangle twiddles, requested with the partner values (not between the stores)
 #pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) {
+    for (int k2 = 0; k2 < 8; ++k2) wpost[k2] = s_post[k1b + 20 * k2];
+    const v2f w160 = s_post[160];
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
       Bx[k2] = bperm(pbyte, b[15 - k2].x);
       By[k2] = bperm(pbyte, b[15 - k2].y);
     }
-    __builtin_amdgcn_sched_barrier(0);   // keep the 32 requests ahead of their consumers
+    __builtin_amdgcn_sched_barrier(0);   // keep the 24 requests ahead of their consumers
+    float* pf = pb + fb * 321;
+    auto two_bins = [&](float ax, float ay, float bx, float by, v2f w, int k) {
+      const float sx = ax + bx, sy = ay - by, ux = ay + by, uy = bx - ax;
+      const float wr = fmaf(w.x, ux, -(w.y * uy)), wi = fmaf(w.y, ux, w.x * uy);
+      const float r1 = sx + wr, i1 = sy + wi, r2 = sx - wr, i2 = sy - wi;
+      pf[320 - k] = fmaf(r2, r2, i2 * i2);   // first: bin 160 pairs with itself, |S + W U|^2 stands
+      pf[k] = fmaf(r1, r1, i1 * i1);
+    };
 #pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) {
-      const float ax = b[k2].x, ay = b[k2].y;
+    for (int k2 = 0; k2 < 8; ++k2) {
       const float bx = k1b == 0 ? b[(16 - k2) & 15].x : Bx[k2];
       const float by = k1b == 0 ? b[(16 - k2) & 15].y : By[k2];
-      const float sx = ax + bx, sy = ay - by, ux = ay + by, uy = bx - ax;
-      const v2f w = s_post[k1b + 20 * k2];
-      const float xr = fmaf(-w.y, uy, fmaf(w.x, ux, sx));
-      const float xi = fmaf(w.y, ux, fmaf(w.x, uy, sy));
-      pb[fb * 321 + k1b + 20 * k2] = fmaf(xr, xr, xi * xi);
+      two_bins(b[k2].x, b[k2].y, bx, by, wpost[k2], k1b + 20 * k2);
     }
-    if (fb < 3 && k1b == 0) {
-      const float ny = 2.0f * (b[0].x - b[0].y);   // 2 X[320] = 2 (Re Z[0] - Im Z[0])
-      pb[fb * 321 + 320] = ny * ny;
-    }
+    if (k1b == 0) two_bins(b[8].x, b[8].y, b[8].x, b[8].y, w160, 160);
     wave_lds_fence();
+    MFCC_STAMP(2);
     // Slaney mel (the lane's narrow and wide filter) -> power_to_db(ref = 1, amin = 1e-10).  The 18
     // taps of frame ff + 1 are requested before frame ff's sums run (LDS latency off the chain).
     const int f0 = 3 * c;
@@ -436,25 +473,68 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
       s1 += s2;
       const float v0 = s0 > 1e-10f ? 10.0f * fast_log10(s0) : -100.0f;
       const float v1 = s1 > 1e-10f ? 10.0f * fast_log10(s1) : -100.0f;
-      db[(f0 + ff) * kM3DbP + mlo.z] = v0;
-      db[(f0 + ff) * kM3DbP + mlo.w] = v1;
+      db[(f0 + ff) * DBP + mlo.z] = v0;
+      db[(f0 + ff) * DBP + mlo.w] = v1;
       vmax = fmaxf(vmax, fmaxf(v0, v1));
     }
     wave_lds_fence();
+    MFCC_STAMP(3);
   };
 
-  v2f rawA[20], rawB[20];
-  if ((int64_t)blockIdx.x < n_clips) mfcc_load_chunk(pcm + (int64_t)blockIdx.x * kPcmLen, wave, lane, rawA);
-  const int nsteps = (17 - wave + kM3Waves - 1) / kM3Waves;   // 5 for wave 0, else 4 (uniform)
-  for (int64_t clip = blockIdx.x; clip < n_clips; clip += gridDim.x) {
+  // [C; dC; ddC] of one clip from its coefficient image: np.gradient (edge_order 1) twice.  Item =
+  // (coefficient, block of 4 frames), 13 x 13 items over `nthr` threads; an item reads the 8 image
+  // values its frames and their 2-frame neighbourhoods need.
+  auto emit = [&](const float* cb, int64_t clip, int tid, int nthr) {
+    float* o = out + clip * 39 * 51;
+    for (int it = tid; it < 13 * 13; it += nthr) {
+      int cr, fb4;
+      if (layout == 0) { cr = it / 13; fb4 = it - 13 * cr; } else { fb4 = it / 13; cr = it - 13 * fb4; }
+      const int f0 = 4 * fb4;
+      const float* r = cb + cr * kM3CP;
+      float w[8];   // frames f0 - 2 .. f0 + 5, clamped
+#pragma unroll
+      for (int u = 0; u < 8; ++u) w[u] = r[min(max(f0 - 2 + u, 0), 50)];
+      auto G = [&](int p, int u) {   // gradient at frame p = f0 - 2 + u
+        return p == 0 ? w[u + 1] - w[u] : (p == 50 ? w[u] - w[u - 1] : (w[u + 1] - w[u - 1]) * 0.5f);
+      };
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int f = f0 + q;
+        if (f > 50) break;
+        const float g0 = G(f, q + 2);
+        const float g2 = f == 0 ? G(f + 1, q + 3) - g0
+                                : (f == 50 ? g0 - G(f - 1, q + 1) : (G(f + 1, q + 3) - G(f - 1, q + 1)) * 0.5f);
+        if (layout == 0) {
+          o[cr * 51 + f] = w[q + 2];
+          o[(13 + cr) * 51 + f] = g0;
+          o[(26 + cr) * 51 + f] = g2;
+        } else {
+          o[f * 39 + cr] = w[q + 2];
+          o[f * 39 + 13 + cr] = g0;
+          o[f * 39 + 26 + cr] = g2;
+        }
+      }
+    }
+  };
+
+  // Per clip: the 17 chunks (wave 0 takes 5, the others 4), then the top_db max, the DCT into
+  // cbuf[clip parity] and the barrier that frees db.  The previous clip's output is written from
+  // its coefficient image by waves 1..3 while wave 0 runs its fifth chunk, off the barrier.
+  v2f raw[20];
+  if ((int64_t)blockIdx.x < n_clips) mfcc_load_chunk(pcm + (int64_t)blockIdx.x * kPcmLen, chunk_of(0), lane, raw);
+  int par = 0;
+  for (int64_t clip = blockIdx.x; clip < n_clips; clip += gridDim.x, par ^= 1) {
     float vmax = -INFINITY;
-    for (int k = 0; k < nsteps; k += 2) {
-      step(rawA, rawB, clip, wave + kM3Waves * k, vmax);
-      if (k + 1 < nsteps) step(rawB, rawA, clip, wave + kM3Waves * (k + 1), vmax);
+    for (int k = 0; k < nsteps; ++k) step(raw, clip, k, vmax);
+    if (wave > 0 && clip != (int64_t)blockIdx.x) {
+      emit(cbuf[par ^ 1], clip - gridDim.x, threadIdx.x - 64, 64 * (kM3Waves - 1));
+      MFCC_STAMP(8);
     }
     vmax = wave_max(vmax);
     if (lane == 0) red[wave] = vmax;
+    MFCC_STAMP(4);
     __syncthreads();
+    MFCC_STAMP(5);
     float mx = red[0];
 #pragma unroll
     for (int w = 1; w < kM3Waves; ++w) mx = fmaxf(mx, red[w]);
@@ -462,8 +542,8 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
     {  // DCT-II (ortho, 13 rows) on the matrix cores: wave = frames [16 wave, 16 wave + 16)
       const int row = lane & 15, kq = 4 * (lane >> 4);
       const int fr = min(16 * wave + row, 50);
-      const float* dr = db + fr * kM3DbP + kq;
-      const float* ar = t.dct + min(row, 12) * 128 + kq;
+      const float* dr = db + fr * DBP + kq;
+      const float* ar = s_dct + min(row, 12) * 128 + kq;
       f32x4_ acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kb = 0; kb < 8; ++kb) {
@@ -480,31 +560,26 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int coef = kq + r;
-        if (coef < 13 && fo < 51) cbuf[coef * kM3CP + fo] = acc[r];
+        if (coef < 13 && fo < 51) cbuf[par][coef * kM3CP + fo] = acc[r];
       }
     }
-    __syncthreads();
-    // np.gradient (edge_order 1) twice, then [C; dC; ddC] in the requested layout
-    auto grad = [](const float* r, int f) {
-      return f == 0 ? r[1] - r[0] : (f == 50 ? r[50] - r[49] : (r[f + 1] - r[f - 1]) * 0.5f);
-    };
-    auto grad2 = [&](const float* r, int f) {
-      return f == 0 ? grad(r, 1) - grad(r, 0)
-                    : (f == 50 ? grad(r, 50) - grad(r, 49) : (grad(r, f + 1) - grad(r, f - 1)) * 0.5f);
-    };
-    float* o = out + clip * 39 * 51;
-    for (int it = threadIdx.x; it < 39 * 51; it += 64 * kM3Waves) {
-      int rw, f;
-      if (layout == 0) { rw = it / 51; f = it - 51 * rw; } else { f = it / 39; rw = it - 39 * f; }
-      const int cr = rw < 13 ? rw : (rw < 26 ? rw - 13 : rw - 26);
-      const float* r = cbuf + cr * kM3CP;
-      o[it] = rw < 13 ? r[f] : (rw < 26 ? grad(r, f) : grad2(r, f));
-    }
-    if (nsteps & 1) {   // wave 0: the next clip's first chunk landed in rawB (long since)
-#pragma unroll
-      for (int i = 0; i < 20; ++i) rawA[i] = rawB[i];
-    }
+    MFCC_STAMP(6);
+    __syncthreads();   // cbuf[par] complete; db free for the next clip
+    MFCC_STAMP(7);
   }
+  {  // the last clip's output, all waves
+    const int64_t nmine = ((int64_t)blockIdx.x < n_clips) ? (n_clips - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+    if (nmine > 0) emit(cbuf[par ^ 1], blockIdx.x + (nmine - 1) * gridDim.x, threadIdx.x, 64 * kM3Waves);
+    MFCC_STAMP(8);
+  }
+#ifdef SRK_MFCC_STAMPS
+  if (lane == 0) {
+    unsigned long long* d = g_mfcc_stamps + ((size_t)blockIdx.x * kM3Waves + wave) * kStampPhases;
+#pragma unroll
+    for (int p = 0; p < kStampPhases - 1; ++p) d[p] = st_acc[p];
+    d[kStampPhases - 1] = 1;
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------- K4 noise mix
@@ -545,6 +620,14 @@ __global__ void noise_mix_kernel(const int16_t* __restrict__ pcm, const int16_t*
 using srk::DeviceTables;
 
 extern "C" {
+
+#ifdef SRK_MFCC_STAMPS
+int srk_debug_mfcc_stamps(unsigned long long* host, int64_t n) {
+  const int64_t cap = 512 * srk::kM3Waves * srk::kStampPhases;
+  if (n > cap) n = cap;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(srk::g_mfcc_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int srk_fbank_fwd(const float* pcm, int64_t n_clips, float* out, void* stream) {
   SRK_API_BEGIN

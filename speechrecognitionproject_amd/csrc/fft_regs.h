@@ -19,14 +19,6 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ v2f cm2(v2f a, v2f b) { return v2f{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
 __device__ __forceinline__ v2f mi2(v2f a) { return v2f{a.y, -a.x}; }   // -i * a
 
-__device__ constexpr float kW20[4][5][2] = {
-  {{1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}},
-  {{1.f, 0.f}, {9.510565163e-01f, -3.090169944e-01f}, {8.090169944e-01f, -5.877852523e-01f},
-   {5.877852523e-01f, -8.090169944e-01f}, {3.090169944e-01f, -9.510565163e-01f}},
-  {{1.f, 0.f}, {8.090169944e-01f, -5.877852523e-01f}, {3.090169944e-01f, -9.510565163e-01f},
-   {-3.090169944e-01f, -9.510565163e-01f}, {-8.090169944e-01f, -5.877852523e-01f}},
-  {{1.f, 0.f}, {5.877852523e-01f, -8.090169944e-01f}, {-3.090169944e-01f, -9.510565163e-01f},
-   {-9.510565163e-01f, -3.090169944e-01f}, {-8.090169944e-01f, 5.877852523e-01f}}};
 __device__ constexpr float kW16[4][4][2] = {
   {{1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}, {1.f, 0.f}},
   {{1.f, 0.f}, {9.238795325e-01f, -3.826834324e-01f}, {7.071067812e-01f, -7.071067812e-01f},
@@ -56,24 +48,35 @@ __device__ __forceinline__ void dft5v(v2f& a0, v2f& a1, v2f& a2, v2f& a3, v2f& a
   a3 = b2 - mi2(q2);
 }
 
-// in-place 20-point forward DFT, natural order in and out (i = 4p + q, k = k1 + 5 k2)
+// in-place 20-point forward DFT, natural order in and out.  Good-Thomas prime-factor form (20 = 4 x 5,
+// coprime): input n = (5 n1 + 4 n2) mod 20, output k = (5 k1 + 16 k2) mod 20, so that
+// W20^(n k) = W4^(n1 k1) W5^(n2 k2) and no twiddles sit between the 4- and the 5-point stages.
 __device__ __forceinline__ void dft20v(v2f (&a)[20]) {
-  v2f b[4][5];
+  v2f y[5][4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    v2f t0 = a[q], t1 = a[4 + q], t2 = a[8 + q], t3 = a[12 + q], t4 = a[16 + q];
-    dft5v(t0, t1, t2, t3, t4);
-    b[q][0] = t0; b[q][1] = t1; b[q][2] = t2; b[q][3] = t3; b[q][4] = t4;
-#pragma unroll
-    for (int k1 = 1; k1 < 5; ++k1)
-      if (q > 0) b[q][k1] = cm2(b[q][k1], v2f{kW20[q][k1][0], kW20[q][k1][1]});
+  for (int n2 = 0; n2 < 5; ++n2) {
+    v2f t0 = a[(4 * n2) % 20], t1 = a[(5 + 4 * n2) % 20], t2 = a[(10 + 4 * n2) % 20], t3 = a[(15 + 4 * n2) % 20];
+    dft4v(t0, t1, t2, t3);
+    y[n2][0] = t0; y[n2][1] = t1; y[n2][2] = t2; y[n2][3] = t3;
   }
 #pragma unroll
-  for (int k1 = 0; k1 < 5; ++k1) {
-    v2f u0 = b[0][k1], u1 = b[1][k1], u2 = b[2][k1], u3 = b[3][k1];
-    dft4v(u0, u1, u2, u3);
-    a[k1] = u0; a[k1 + 5] = u1; a[k1 + 10] = u2; a[k1 + 15] = u3;
+  for (int k1 = 0; k1 < 4; ++k1) {
+    v2f u0 = y[0][k1], u1 = y[1][k1], u2 = y[2][k1], u3 = y[3][k1], u4 = y[4][k1];
+    dft5v(u0, u1, u2, u3, u4);
+    a[(5 * k1) % 20] = u0; a[(5 * k1 + 16) % 20] = u1; a[(5 * k1 + 32) % 20] = u2;
+    a[(5 * k1 + 48) % 20] = u3; a[(5 * k1 + 64) % 20] = u4;
   }
+}
+
+// a * W16^(q k1) for compile-time q, k1: W16^4 = -i and W16^{2,6} = (+-1 - i) / sqrt(2) take adds and
+// one packed multiply instead of a complex product
+__device__ __forceinline__ v2f tw16(v2f a, int q, int k1) {
+  constexpr float c = 7.071067812e-01f;
+  const int m = q * k1;
+  if (m == 4) return mi2(a);
+  if (m == 2) return c * v2f{a.x + a.y, a.y - a.x};
+  if (m == 6) return c * v2f{a.y - a.x, -(a.x + a.y)};
+  return cm2(a, v2f{kW16[q][k1][0], kW16[q][k1][1]});
 }
 
 // in-place 16-point forward DFT (j = 4p + q, k = k1 + 4 k2)
@@ -86,7 +89,7 @@ __device__ __forceinline__ void dft16v(v2f (&a)[16]) {
     b[q][0] = t0; b[q][1] = t1; b[q][2] = t2; b[q][3] = t3;
 #pragma unroll
     for (int k1 = 1; k1 < 4; ++k1)
-      if (q > 0) b[q][k1] = cm2(b[q][k1], v2f{kW16[q][k1][0], kW16[q][k1][1]});
+      if (q > 0) b[q][k1] = tw16(b[q][k1], q, k1);
   }
 #pragma unroll
   for (int k1 = 0; k1 < 4; ++k1) {

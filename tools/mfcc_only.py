@@ -7,6 +7,9 @@ which = sys.argv[1] if len(sys.argv) > 1 else "mfcc"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
 x, _ = synthetic_clips(1024, seed=123)
 xd = torch.from_numpy(x).cuda().repeat(n // 1024, 1)
+# the models' layouts (bench.py feature_roofline): MFCC time-major, spectrogram transposed
+fn = {"mfcc": lambda x: K.mfcc(x, time_major=True), "spec": lambda x: K.spec(x, transposed=True),
+      "fbank": K.fbank}[which]
 for _ in range(3):
-    getattr(K, which)(xd)
+    fn(xd)
 torch.cuda.synchronize()

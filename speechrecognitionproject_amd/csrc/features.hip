@@ -60,7 +60,7 @@ struct FbankTables {
 __global__ __launch_bounds__(256, 4) void fbank_kernel(const float* __restrict__ pcm, float* __restrict__ out,
                                                        int64_t n_clips, FbankTables t) {
   __shared__ v2f sbuf[4][4 * 272];   // per wave: 4 frames x (16 x 17) transpose, reused for spectra / power
-  __shared__ double s_win[400];
+  __shared__ __attribute__((aligned(16))) double s_win[400];
   __shared__ v2f s_tw[16 * 16];      // W256^(j k1) at [k1][j]
   __shared__ v2f s_post[257];        // W512^k
   __shared__ float s_pw[kFbPairs * kFbPairTaps];
@@ -89,20 +89,32 @@ __global__ __launch_bounds__(256, 4) void fbank_kernel(const float* __restrict__
     const bool live = gf < 98;
     const float* __restrict__ x = pcm + clip * kPcmLen + 160 * (live ? gf : 0);
     // pre-emphasis (fp32, numpy's two roundings) x Hamming (fp64, :33-41), DC / Nyquist sums in fp64
+    // every lane loads (dead lanes read in-clip samples) and the products are masked after: with the
+    // loads under the condition the compiler serialises their waits
+    v2f xv[13];
+    float xm[13];
+#pragma unroll
+    for (int i = 0; i < 13; ++i) {
+      const int n = j + 16 * i;
+      xv[i] = *reinterpret_cast<const v2f*>(x + 2 * n);
+      xm[i] = x[(n == 0 && !(live && gf > 0)) ? 0 : 2 * n - 1];   // x[-1] only inside the clip
+    }
     v2f a[16];
     double dc = 0.0, ny = 0.0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       a[i] = v2f{0.f, 0.f};
       const int n = j + 16 * i;
-      if (i < 13 && n < 200 && live) {
+      if (i < 13) {
 #pragma clang fp contract(off)
-        const v2f xv = *reinterpret_cast<const v2f*>(x + 2 * n);
         const bool first = (gf == 0 && n == 0);
-        const float xm = first ? 0.f : x[2 * n - 1];
-        const float e0 = first ? xv.x : xv.x - 0.97f * xm;
-        const float e1 = xv.y - 0.97f * xv.x;
-        const double d0 = (double)e0 * s_win[2 * n], d1 = (double)e1 * s_win[2 * n + 1];
+        const float e0 = first ? xv[i].x : xv[i].x - 0.97f * xm[i];
+        const float e1 = xv[i].y - 0.97f * xv[i].x;
+        const double2 w = *reinterpret_cast<const double2*>(s_win + 2 * (n < 200 ? n : 199));
+        double d0 = (double)e0 * w.x, d1 = (double)e1 * w.y;
+        const bool valid = live && n < 200;
+        d0 = valid ? d0 : 0.0;
+        d1 = valid ? d1 : 0.0;
         a[i] = v2f{(float)d0, (float)d1};
         dc += d0 + d1;
         ny += d0 - d1;
@@ -112,8 +124,15 @@ __global__ __launch_bounds__(256, 4) void fbank_kernel(const float* __restrict__
     ny = group16_sum(ny);
     // pass A: 16-point DFT over i, twiddle W256^(j k1), transpose
     dft16v(a);
+    tb[f * 272 + j] = a[0];
 #pragma unroll
-    for (int k1 = 0; k1 < 16; ++k1) tb[f * 272 + k1 * 17 + j] = k1 ? cm2(a[k1], s_tw[k1 * 16 + j]) : a[0];
+    for (int g = 1; g < 16; g += 5) {   // twiddles read 5 at a time ahead of their stores (3 LDS round trips)
+      v2f tw[5];
+#pragma unroll
+      for (int u = 0; u < 5; ++u) tw[u] = s_tw[(g + u) * 16 + j];
+#pragma unroll
+      for (int u = 0; u < 5; ++u) tb[f * 272 + (g + u) * 17 + j] = cm2(a[g + u], tw[u]);
+    }
     wave_lds_fence();
     // pass B: lane = (f, k1): 16-point DFT over j -> Z[k1 + 16 k2]
     v2f b[16];
@@ -193,7 +212,7 @@ struct SpecTables {
 __global__ __launch_bounds__(256, 4) void spec_kernel(const float* __restrict__ pcm, float* __restrict__ out,
                                                       int64_t n_clips, int transposed, SpecTables t) {
   __shared__ v2f sbuf[4][3 * 340];
-  __shared__ double s_win[640];
+  __shared__ __attribute__((aligned(16))) double s_win[640];
   __shared__ v2f s_tw[20 * 16];      // W320^(j k1) at [k1][j]
   __shared__ v2f s_post[321];        // W640^k
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -214,13 +233,23 @@ __global__ __launch_bounds__(256, 4) void spec_kernel(const float* __restrict__ 
     const int gf = 3 * c + fa;
     const bool live = fa < 3 && gf < 49;
     const float* __restrict__ x = pcm + clip * kPcmLen + 320 * (live ? gf : 0);
+    // every lane loads (a dead lane's x is frame 0 of the clip) and the products are masked after:
+    // with the loads under the `live` condition the compiler serialises 40 load / LDS waits
+    v2f xv[20];
+#pragma unroll
+    for (int i = 0; i < 20; ++i) xv[i] = *reinterpret_cast<const v2f*>(x + 2 * (j + 16 * i));
+    v2f tw[19];   // pass-A twiddles, read ahead of the transpose stores
+#pragma unroll
+    for (int k1 = 1; k1 < 20; ++k1) tw[k1 - 1] = s_tw[k1 * 16 + j];
     v2f a[20];
     double dc = 0.0, ny = 0.0;
 #pragma unroll
     for (int i = 0; i < 20; ++i) {
-      const v2f xv = *reinterpret_cast<const v2f*>(x + 2 * (j + 16 * i));
       const int n = j + 16 * i;
-      const double d0 = live ? (double)xv.x * s_win[2 * n] : 0.0, d1 = live ? (double)xv.y * s_win[2 * n + 1] : 0.0;
+      const double2 w = *reinterpret_cast<const double2*>(s_win + 2 * n);
+      double d0 = (double)xv[i].x * w.x, d1 = (double)xv[i].y * w.y;
+      d0 = live ? d0 : 0.0;
+      d1 = live ? d1 : 0.0;
       a[i] = v2f{(float)d0, (float)d1};
       dc += d0 + d1;
       ny += d0 - d1;
@@ -230,7 +259,7 @@ __global__ __launch_bounds__(256, 4) void spec_kernel(const float* __restrict__ 
     dft20v(a);
     if (fa < 3) {
 #pragma unroll
-      for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? cm2(a[k1], s_tw[k1 * 16 + j]) : a[0];
+      for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? cm2(a[k1], tw[k1 - 1]) : a[0];
     }
     wave_lds_fence();
     v2f b[16];

@@ -243,6 +243,20 @@ __device__ __forceinline__ void store_gates(const GruPArgs& a, const float (&gsv
   }
 }
 
+// The 16-bit 32 x 32 kernels keep the saved gates unit-interleaved, [dir][t][b][H][4]: one 16-B store
+// per cell here and one 16-B load in the backward kernel instead of four dword accesses each.
+__device__ __forceinline__ void store_gates_il(const GruPArgs& a, const float (&gsv)[4][4], int dir, int t, int brow0,
+                                               int b_last, int j) {
+  const int H = a.H;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int b = brow0 + r;
+    if (b > b_last) continue;
+    float* gs = a.gates + (((size_t)dir * a.T + t) * a.B + b) * 4 * H;
+    *reinterpret_cast<v4f*>(gs + 4 * j) = v4f{gsv[r][0], gsv[r][1], gsv[r][2], gsv[r][3]};
+  }
+}
+
 // The input-projection gradients dgi (dar, daz, dan) of a lane's 4 cells, likewise after the arrival.
 __device__ __forceinline__ void store_dgi(const GruPArgs& a, const float (&dv)[4][3], int dir, int t, int brow0,
                                           int b_last, int j) {
@@ -1056,26 +1070,51 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs
   const int rb = wave & 1, kh = wave >> 1;
   int dir, group, slice;
   bool local;
+  stamp(a, 0, 6);   // kernel entry (prologue = slot 0 - slot 6 of step 0)
   place(a, S, dir, group, slice, local);
   trace_id(a, dir, group, slice);
   const bool per = a.flags || local;
   const int T = a.T, j0 = slice * U, ju = kh * 16 + lr, j = j0 + ju;
   const int b0 = a.b_begin + group * kRows2, b_last = a.b_end - 1, rbase = b0 + rb * 16;
 
-  {  // this slice of W_hh[dir] (3 gates x 32 units), rounded to 16 bits -> LDS
+  {  // this slice of W_hh[dir] (3 gates x 32 units), rounded to 16 bits -> LDS; loads issued 8 packs
+     // at a time ahead of their stores (the prologue is a chain of L2 round trips otherwise)
     const float* W = a.w_hh + (size_t)dir * 3 * H * H;
-    for (int v = tid; v < 3 * U * (H / 8); v += 256) {
-      const int c = v / (H / 8), kq = v % (H / 8), g = c / U, jj = c % U;
-      const float* src = W + (size_t)(g * H + j0 + jj) * H + kq * 8;
-      Ws[c * WPQ + kq] = pack8<F16>(cat8(ld4(src), ld4(src + 4)));
+    constexpr int NV = 3 * U * (H / 8), NB = 8;
+    static_assert(NV % (256 * NB) == 0, "prologue batches");
+    for (int v0 = tid; v0 < NV; v0 += 256 * NB) {
+      v4f w[NB][2];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int v = v0 + 256 * u, c = v / (H / 8), kq = v % (H / 8), g = c / U, jj = c % U;
+        const float* src = W + (size_t)(g * H + j0 + jj) * H + kq * 8;
+        w[u][0] = ld4(src);
+        w[u][1] = ld4(src + 4);
+      }
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int v = v0 + 256 * u, c = v / (H / 8), kq = v % (H / 8);
+        Ws[c * WPQ + kq] = pack8<F16>(cat8(w[u][0], w[u][1]));
+      }
     }
   }
   const bool fused = a.x_in != nullptr;
-  if (fused) {   // W_ih slice (rows g * 32 + jj), rounded like the GEMM operands
+  if (fused) {   // W_ih slice (rows g * 32 + jj), rounded like the GEMM operands, 8 loads in flight
     const float* W = a.w_ih + (size_t)dir * 3 * H * a.in;
-    for (int v = tid; v < 3 * U * kFusedIn; v += 256) {
-      const int c = v / kFusedIn, k = v % kFusedIn, g = c / U, jj = c % U;
-      Wx[c * kXP + k] = k < a.in ? rnd16<RNDX>(W[(size_t)(g * H + j0 + jj) * a.in + k]) : 0.f;
+    constexpr int NV = 3 * U * kFusedIn, NB = 8;
+    static_assert(NV % (256 * NB) == 0, "prologue batches");
+    for (int v0 = tid; v0 < NV; v0 += 256 * NB) {
+      float w[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int v = v0 + 256 * u, c = v / kFusedIn, k = v % kFusedIn, g = c / U, jj = c % U;
+        w[u] = k < a.in ? W[(size_t)(g * H + j0 + jj) * a.in + k] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int v = v0 + 256 * u, c = v / kFusedIn, k = v % kFusedIn;
+        Wx[c * kXP + k] = rnd16<RNDX>(w[u]);
+      }
     }
   }
   float xnext[kFusedIn / 4];
@@ -1090,10 +1129,49 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs
   float hreg[4] = {0.f, 0.f, 0.f, 0.f};
   float gsv[4][4];
 
+  // y (fp32 + the 16-bit copy) and the saved gates of a step, from hT / gsv, after its arrival.
+  // (Issuing them one step later, behind the next step's hand-off loads, shortens that step's wait --
+  // vmcnt retires in order, so stores ahead of a flag poll hold its answer back -- but their issue
+  // then lands on the MFMA phase: measured slower, DESIGN.md.)
+  auto flush_outputs = [&](int sstep) {
+    const int ts = dir == 0 ? sstep : T - 1 - sstep;
+    const int row = tid >> 3, u4 = (tid & 7) * 4;   // 32 rows x 32 units
+    if (b0 + row <= b_last) {
+      const v4f yv = ld4(hT + row * HTP + u4);
+      st4(a.y + ((size_t)(b0 + row) * T + ts) * 2 * H + dir * H + j0 + u4, yv);
+      if (a.y16) {
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        typedef __attribute__((ext_vector_type(4))) typename std::conditional<F16, _Float16, __bf16>::type e4;
+        *reinterpret_cast<u32x2*>(a.y16 + ((size_t)(b0 + row) * T + ts) * 2 * H + dir * H + j0 + u4) =
+            __builtin_bit_cast(u32x2, __builtin_convertvector(yv, e4));
+      }
+    }
+    if (a.y16) store_gates_il(a, gsv, dir, ts, rbase + lq * 4, b_last, j);   // read by the 16-bit bwd kernel
+    else store_gates(a, gsv, dir, ts, rbase + lq * 4, b_last, j);
+  };
+  float gr[4], gz[4], gn[4];
+  auto load_gi = [&](int t) {   // non-fused: this step's input projections from the gi GEMM
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = min(rbase + lq * 4 + r, b_last);
+      const float* gi = a.gi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
+      gr[r] = gi[j];
+      gz[r] = gi[H + j];
+      gn[r] = gi[2 * H + j];
+    }
+  };
+  // this step's input-side loads (fused: the next step's x), ahead of the wait
+  auto issue_inputs = [&](int step, int t) {
+    if (fused) {
+      if (step + 1 < T) load_x(a, dir == 0 ? t + 1 : t - 1, min(rbase + lr, b_last), lq, xnext);
+    } else {
+      load_gi(t);
+    }
+  };
+
   for (int step = 0; step < T; ++step) {
     const int t = dir == 0 ? step : T - 1 - step;
     stamp(a, step, 0);
-    float gr[4], gz[4], gn[4];
     if (fused) {   // the lane's input projections (rows rbase + 4 lq + r, unit j), before the wait
       float xv[kFusedIn / 4];
 #pragma unroll
@@ -1112,17 +1190,8 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs
         gz[r] = ax[1][r] + biz;
         gn[r] = ax[2][r] + bin;
       }
-      if (step + 1 < T) load_x(a, dir == 0 ? t + 1 : t - 1, min(rbase + lr, b_last), lq, xnext);
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int b = min(rbase + lq * 4 + r, b_last);
-        const float* gi = a.gi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
-        gr[r] = gi[j];
-        gz[r] = gi[H + j];
-        gn[r] = gi[2 * H + j];
-      }
     }
+    issue_inputs(step, t);
     float full[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     if (step > 0) {
       lp2_wait(a, dir, group, kh * KH, KH, step, per);
@@ -1207,20 +1276,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs
     }
     lp2_arrive(a, dir, group, slice, step, per, local);   // the hand-off only: y and the gates go out after it
     stamp(a, step, 4);
-    {
-      const int row = tid >> 3, u4 = (tid & 7) * 4;   // y (fp32, + the 16-bit copy): 32 rows x 32 units
-      if (b0 + row <= b_last) {
-        const v4f yv = ld4(hT + row * HTP + u4);
-        st4(a.y + ((size_t)(b0 + row) * T + t) * 2 * H + dir * H + j0 + u4, yv);
-        if (a.y16) {
-          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-          typedef __attribute__((ext_vector_type(4))) typename std::conditional<F16, _Float16, __bf16>::type e4;
-          *reinterpret_cast<u32x2*>(a.y16 + ((size_t)(b0 + row) * T + t) * 2 * H + dir * H + j0 + u4) =
-              __builtin_bit_cast(u32x2, __builtin_convertvector(yv, e4));
-        }
-      }
-    }
-    store_gates(a, gsv, dir, t, rbase + lq * 4, b_last, j);
+    flush_outputs(step);
   }
 }
 
@@ -1241,6 +1297,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs
   const int rb = wave & 1, kh = wave >> 1;
   int dir, group, slice;
   bool local;
+  stamp(a, 0, 6);   // kernel entry
   place(a, S, dir, group, slice, local);
   trace_id(a, dir, group, slice);
   const bool per = a.flags || local;
@@ -1275,11 +1332,12 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int b = min(rbase + lq * 4 + r, b_last);
-      const float* gs = a.gates + (((size_t)dir * T + t) * B + b) * 4 * H;
-      g_r[r] = gs[j];
-      g_z[r] = gs[H + j];
-      g_n[r] = gs[2 * H + j];
-      g_h[r] = gs[3 * H + j];
+      const float* gs = a.gates + (((size_t)dir * T + t) * B + b) * 4 * H;   // unit-interleaved (store_gates_il)
+      const v4f gv = *reinterpret_cast<const v4f*>(gs + 4 * j);
+      g_r[r] = gv.x;
+      g_z[r] = gv.y;
+      g_n[r] = gv.z;
+      g_h[r] = gv.w;
       dyv[r] = a.dy[((size_t)b * T + t) * 2 * H + dir * H + j];
       hpv[r] = edge ? 0.f : a.y_in[((size_t)b * T + tprev) * 2 * H + dir * H + j];
     }

@@ -39,6 +39,8 @@ for name, b in (("fwd", fwd), ("bwd", bwd)):
     epi = (ts[:, 1:, 3] - ts[:, 1:, 2]).mean().item()
     pub = (ts[:, 1:, 4] - ts[:, 1:, 3]).mean().item()
     step = ((ts[:, -1, 4] - ts[:, 0, 0]) / T).mean().item()
+    prologue = (ts[:, 0, 0] - ts[:, 0, 6]).mean().item() if bool((ts[:, 0, 6] > 0).all()) else float("nan")
+    span = (ts[:, -1, 4].max() - ts[:, 0, 6].min()).item() if bool((ts[:, 0, 6] > 0).all()) else float("nan")
     start_skew = (ts[:, 0, 0].max() - ts[:, 0, 0].min()).item()
     # group membership: the (direction, group) pair each workgroup ran, recorded by the kernel (trace_id)
     grp = (b.view(nwg, T, 8)[:, 0, 5].cpu() >> 8)
@@ -51,7 +53,7 @@ for name, b in (("fwd", fwd), ("bwd", bwd)):
         # wait done at step s + 1 minus the group's LAST publish of step s: flag propagation
         prop.append(ts[m][:, 1:, 1] - pubs.max(0).values[None, :-1])
     spread, prop = torch.cat(spread), torch.cat(prop)
-    res[name] = {"us_per_step": round(step, 2), "wait": round(wait, 2), "loads_mfma": round(mfma, 2),
+    res[name] = {"us_per_step": round(step, 2), "prologue_us": round(prologue, 2), "entry_to_last_publish_us": round(span, 2), "wait": round(wait, 2), "loads_mfma": round(mfma, 2),
                  "epilogue": round(epi, 2), "publish": round(pub, 2), "launch_skew_us": round(start_skew, 2),
                  "publish_spread_us": round(spread.mean().item(), 2),
                  "last_publish_to_wait_done_us": round(prop.mean().item(), 2)}

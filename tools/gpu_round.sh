@@ -20,6 +20,8 @@ timeout -k 10 420 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>
   && for m in fbanks_cnn resnet_bgru spec_bgru mfrn_bgru; do
        timeout -k 10 300 python bench.py --model $m --steps 10 > "$OUT/bench_$m.json" 2> "$OUT/bench_$m.err" || exit 1
      done \
+  && timeout -k 10 300 python bench.py --model spec_bgru --precision fp16 --steps 10 --no-cpu-baseline \
+       > "$OUT/bench_spec_bgru_fp16.json" 2> "$OUT/bench_spec_bgru_fp16.err" \
   && timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof_stats" -o run -- \
        python3 bench.py --no-cpu-baseline > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" \
   && timeout -k 10 180 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$ROOT/$OUT/prof_fetch" -o run -- \

@@ -367,7 +367,8 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
   __shared__ v2f s_tw[20 * 16];   // W320^(j k1) at [k1][j]
   __shared__ v2f s_post[320];     // W640^k (untangle twiddles)
   __shared__ float cbuf[2][13 * kM3CP];                         // coefficient images, alternating clips
-  __shared__ __attribute__((aligned(16))) float s_dct[13 * 128];   // DCT-II rows (ortho)
+  __shared__ __attribute__((aligned(16))) float s_dct[13 * kM3DbP];   // DCT-II rows (ortho), pitch 132: the
+                                                                       // 16-B fragment reads of 16 rows hit distinct banks
   __shared__ float red[kM3Waves];
   // the wave index in an SGPR: the chunk loop and its reflect / tail branches stay scalar
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
 #pragma unroll
   for (int i = 0; i < 20; ++i) win[i] = *reinterpret_cast<const v2f*>(t.hann640f + 2 * (j + 16 * i));
   for (int i = threadIdx.x; i < 320; i += 64 * kM3Waves) s_post[i] = *reinterpret_cast<const v2f*>(t.post640 + i);
-  for (int i = threadIdx.x; i < 13 * 128; i += 64 * kM3Waves) s_dct[i] = t.dct[i];
+  for (int i = threadIdx.x; i < 13 * 128; i += 64 * kM3Waves) s_dct[(i >> 7) * kM3DbP + (i & 127)] = t.dct[i];
   const int4 mlo = t.melq_lo[lane];   // {window start a, window start b, filter a, filter b}
   float mw[18];
 #pragma unroll
@@ -572,7 +573,7 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
       const int row = lane & 15, kq = 4 * (lane >> 4);
       const int fr = min(16 * wave + row, 50);
       const float* dr = db + fr * DBP + kq;
-      const float* ar = s_dct + min(row, 12) * 128 + kq;
+      const float* ar = s_dct + min(row, 12) * kM3DbP + kq;
       f32x4_ acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kb = 0; kb < 8; ++kb) {

@@ -140,8 +140,9 @@ class _Block(nn.Module):
 
 
 class _ResNet1d(nn.Module):
-    def __init__(self, stem=(80, 16, 38), backend=True):
+    def __init__(self, stem=(80, 16, 38), backend=True, mode=0):
         super().__init__()
+        self.mode = mode
         self.inplanes = 64
         k, st, pd = stem
         self.conv1 = nn.Conv1d(1, 64, kernel_size=k, stride=st, padding=pd, bias=False)
@@ -176,6 +177,9 @@ class _ResNet1d(nn.Module):
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         b, _, t = x.shape
         x = self.fc1(x.transpose(1, 2).reshape(b * t, -1))
+        if self.mode == 1:   # model_resnet_bgru.py:113-117: the time steps are the backend's channels
+            x = self.backend_conv1(x.view(b, t, 512))
+            return self.backend_conv2(torch.mean(x, 2))
         return x.view(b, t, 512)
 
 
@@ -195,11 +199,12 @@ class ResnetBGRU(nn.Module):
     def __init__(self, num_features=512, num_layers=2, mode=0):
         super().__init__()
         self.mode = mode
-        self.resnet = _ResNet1d()
+        self.resnet = _ResNet1d(mode=mode)
         self.gru = _GRUHead(num_features, num_layers)
 
-    def forward(self, x):
-        return self.gru(self.resnet(x.float().unsqueeze(1)))
+    def forward(self, x):   # model_resnet_bgru.py:145-150: mode 1 returns the backend head's logits
+        x = self.resnet(x.float().unsqueeze(1))
+        return x if self.mode == 1 else self.gru(x)
 
 
 # ---------------------------------------------------------------- model_mfrn_bgru.py:11-140

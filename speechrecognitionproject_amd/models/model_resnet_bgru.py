@@ -7,15 +7,18 @@ Same constructor ``Network(num_features=512, num_layers=2, mode=0)``, ``state_di
 (including the ``mode == 1`` backend head, :57-71, so reference checkpoints load) and helpers.
 Activations stay channels-last [B, L, C] through the ResNet, so the reference's transpose before
 ``fc1`` (:107-111) is free.  Convolutions = K6, BatchNorm(+residual+ReLU) = K9, GRU = K5.
-``mode == 1`` (the auxiliary backend of the staged training, :113-118) is not implemented on the
-device path and raises.
+``mode == 1`` (the auxiliary backend of the staged training, :57-71, :113-118) runs on the same
+kernels: the fc1 output's 125 time steps are the backend's channels, so the [B, 125, 512] view is
+transposed to channels-last [B, 512, 125] once, then K6 1-D convs, K9 BatchNorm (+ReLU; 250 / 125
+channels on zero-padded float4 groups), the channels-last max-pool, the length mean and two Linear
+layers give [B, 12] logits; the GRU is skipped (:147-149).
 
 BatchNorm under data parallelism uses per-rank batch statistics.
 """
 import torch
 import torch.nn as nn
 
-from ..nn import BatchNorm1d, BiGRU, Conv1d, Linear
+from ..nn import BatchNorm1d, BiGRU, Conv1d, Linear, MaxPool1d, conv1d_nlc
 from ._common import DEVICE, accuracy, class_accuracy   # noqa: F401
 
 
@@ -56,13 +59,15 @@ class ResNet(nn.Module):
         self.layer3 = self._make_layer(block, 256, 2, stride=2)
         self.layer4 = self._make_layer(block, 512, 2, stride=2)
         self.fc1 = Linear(512, 512)
-        # mode == 1 auxiliary head: kept for state_dict compatibility (model_resnet_bgru.py:57-71)
+        # mode == 1 auxiliary head (model_resnet_bgru.py:57-71): same module indices / state_dict keys;
+        # the ReLUs are fused into the BatchNorm kernels in forward
         self.backend_conv1 = nn.Sequential(
-            nn.Conv1d(self.dim, 2 * self.dim, 5, 2, 0, bias=False), nn.BatchNorm1d(2 * self.dim), nn.ReLU(True),
-            nn.MaxPool1d(2, 2),
-            nn.Conv1d(2 * self.dim, 4 * self.dim, 5, 2, 0, bias=False), nn.BatchNorm1d(4 * self.dim), nn.ReLU(True))
+            Conv1d(self.dim, 2 * self.dim, 5, stride=2, padding=0, bias=False), BatchNorm1d(2 * self.dim), nn.ReLU(True),
+            MaxPool1d(2),
+            Conv1d(2 * self.dim, 4 * self.dim, 5, stride=2, padding=0, bias=False), BatchNorm1d(4 * self.dim),
+            nn.ReLU(True))
         self.backend_conv2 = nn.Sequential(
-            nn.Linear(4 * self.dim, self.dim), nn.BatchNorm1d(self.dim), nn.ReLU(True), nn.Linear(self.dim, 12))
+            Linear(4 * self.dim, self.dim), BatchNorm1d(self.dim), nn.ReLU(True), Linear(self.dim, 12))
         for m in self.modules():
             if isinstance(m, (Conv1d, nn.Conv1d)):
                 _kaiming(m)
@@ -84,8 +89,18 @@ class ResNet(nn.Module):
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))   # [B, 125, 512]
         bs, sl, _ = x.shape
         x = self.fc1(x.reshape(bs * sl, -1))
-        if self.mode == 1:
-            raise NotImplementedError("model_resnet_bgru mode=1 backend head is not on the device path")
+        if self.mode == 1:   # :113-117, channels = the sl time steps, length = the 512 features
+            x = x.view(bs, sl, 512).transpose(1, 2).contiguous()     # [B, 512, sl] channels-last
+            conv_a, bn_a, _, pool, conv_b, bn_b, _ = self.backend_conv1
+            # 250 channels run as 252 (float4 groups for K9 and the pool): conv_a gets 2 zero output
+            # filters, BatchNorm keeps them 0, conv_b gets 2 zero input channels
+            pa = (-conv_a.out_channels) % 4
+            wa = torch.cat([conv_a.weight, conv_a.weight.new_zeros((pa,) + tuple(conv_a.weight.shape[1:]))])
+            wb = torch.cat([conv_b.weight, conv_b.weight.new_zeros((conv_b.out_channels, pa, conv_b.kernel_size[0]))], 1)
+            x = bn_a.forward_padded(conv1d_nlc(x, wa, None, conv_a.stride[0]), relu=True)   # [B, 254, 252]
+            x = bn_b(conv1d_nlc(pool(x), wb, None, conv_b.stride[0]), relu=True)           # [B, 62, 500]
+            fc_a, bn_h, _, fc_b = self.backend_conv2
+            return fc_b(bn_h(fc_a(x.mean(1)), relu=True))            # torch.mean(x, 2) of the NCL layout
         return x.view(bs, sl, 512)
 
 

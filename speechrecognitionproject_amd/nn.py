@@ -338,11 +338,15 @@ class Conv1d(tnn.Module):
         self.bias = tnn.Parameter(ref.bias.detach().clone()) if bias else None
 
     def forward(self, x):
-        require_gpu()
-        N, L, C = x.shape
-        y = _Conv2dNHWCFn.apply(x.reshape(N, 1, L, C), self.weight.unsqueeze(2), self.bias, (0, self.padding[0]),
-                                (1, self.stride[0]))
-        return y.reshape(N, y.shape[2], self.out_channels)
+        return conv1d_nlc(x, self.weight, self.bias, self.stride[0], self.padding[0])
+
+
+def conv1d_nlc(x, weight, bias=None, stride=1, padding=0):
+    """K6 1-D convolution of channels-last [N, L, Ci] input with an nn.Conv1d weight [Co, Ci, K]."""
+    require_gpu()
+    N, L, C = x.shape
+    y = _Conv2dNHWCFn.apply(x.reshape(N, 1, L, C), weight.unsqueeze(2), bias, (0, padding), (1, stride))
+    return y.reshape(N, y.shape[2], weight.shape[0])
 
 
 class _Conv1PoolFn(torch.autograd.Function):
@@ -562,10 +566,40 @@ class BatchNorm1d(tnn.Module):
 
     def forward(self, x, residual=None, relu=False):
         require_gpu()
+        if self.num_features % 4:
+            return self.forward_padded(x, residual, relu)[..., :self.num_features]
         if self.training:
             self.num_batches_tracked.add_(1)
         return _BatchNormFn.apply(x, self.weight, self.bias, residual, self.running_mean, self.running_var,
                                   self.training, self.momentum, self.eps, relu)
+
+    def forward_padded(self, x, residual=None, relu=False):
+        """K9 works on float4 channel groups: a channel count that is not a multiple of 4 (the
+        resnet_bgru mode-1 head's 250 / 125) runs on zero-padded channels — their statistics are
+        0 / 0, their outputs beta = 0 — and the result keeps the padding ([..., C rounded up to 4],
+        pad channels 0; `forward` slices it off).  ``x`` may arrive padded already.  The running
+        statistics are updated on padded copies and written back."""
+        require_gpu()
+        if self.training:
+            self.num_batches_tracked.add_(1)
+        C = self.num_features
+        p = (-C) % 4
+        if x.shape[-1] == C + p:
+            xp = x
+        else:
+            assert x.shape[-1] == C, (x.shape, C)
+            xp = tnn.functional.pad(x, (0, p))
+        rp = tnn.functional.pad(residual, (0, C + p - residual.shape[-1])) if residual is not None else None
+        g = torch.cat([self.weight, self.weight.new_ones(p)])
+        b = torch.cat([self.bias, self.bias.new_zeros(p)])
+        rm = torch.cat([self.running_mean, self.running_mean.new_zeros(p)])
+        rv = torch.cat([self.running_var, self.running_var.new_ones(p)])
+        y = _BatchNormFn.apply(xp, g, b, rp, rm, rv, self.training, self.momentum, self.eps, relu)
+        if self.training:
+            with torch.no_grad():
+                self.running_mean.copy_(rm[:C])
+                self.running_var.copy_(rv[:C])
+        return y
 
 
 # ----------------------------------------------------------------------------- synchronized batch norm

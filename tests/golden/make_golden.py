@@ -275,6 +275,8 @@ def main():
     model_golden("spec_bgru_golden.npz", R_sb.Network(), x, y)
     x2, y2 = synthetic_clips(2, seed=6)
     model_golden("resnet_bgru_golden.npz", R_rb.Network(), x2, y2, train_mode=True)
+    torch.manual_seed(0)
+    model_golden("resnet_bgru_mode1_golden.npz", R_rb.Network(mode=1), x2, y2, train_mode=True)
     x3, y3 = synthetic_clips(2, seed=7)
     torch.manual_seed(0)
     model_golden("mfrn_bgru_golden.npz", R_mr.Network(), x3, y3, train_mode=True)

@@ -81,7 +81,8 @@ def test_noise_mix_oracle_vs_reference():
                                       ("spec_bgru", OM.SpecBGRU), ("resnet_bgru", OM.ResnetBGRU),
                                       ("mfrn_bgru", OM.MfrnBGRU), ("cnn_bgru", OM.CnnBGRU),
                                       ("spec_cnn", OM.SpecCNN), ("analyst", OM.Analyst),
-                                      ("fbanks_cnn_train", OM.FbanksCNN)])
+                                      ("fbanks_cnn_train", OM.FbanksCNN),
+                                      ("resnet_bgru_mode1", lambda: OM.ResnetBGRU(mode=1))])
 def test_model_oracle_vs_reference(name, cls):
     g = golden(name + "_golden.npz")
     net = cls()

@@ -44,6 +44,8 @@ def parse(argv=None):
     p.add_argument('--reduce', type=int, default=0, help='reduce_dataset(n) like training.py:66-67')
     p.add_argument('--log-every', type=int, default=1, help='write buffered loss lines every n steps')
     p.add_argument('--no-eval', action='store_true')
+    p.add_argument('--mode', type=int, default=None,
+                   help="Network(mode=...) for plugins that take it (resnet_bgru: 1 = the staged training's backend head)")
     p.add_argument('--sync-bn', action='store_true',
                    help='data-parallel: BatchNorm statistics over the global batch (SyncBatchNorm1d)')
     p.add_argument('--no-overlap', dest='overlap', action='store_false',
@@ -78,7 +80,7 @@ def main(argv=None):
             valset.reduce_dataset(args.reduce)
 
     torch.manual_seed(0)
-    model = mod.Network().to(device)
+    model = (mod.Network() if args.mode is None else mod.Network(mode=args.mode)).to(device)
     if args.sync_bn:
         from .nn import convert_sync_batchnorm
         model = convert_sync_batchnorm(model)

@@ -19,6 +19,15 @@ def test_training_entry_point(gpu, tmp_path, model):
     assert len(open(tmp_path / "train_t.txt").readlines()) == 1
 
 
+def test_training_resnet_bgru_backend_head(gpu, tmp_path):
+    """--mode 1: the staged training's auxiliary head (model_resnet_bgru.py:113-118) end to end."""
+    from speechrecognitionproject_amd.training import main
+    main(["-key", "m", "-lr", "0.0001", "--model", "resnet_bgru", "--mode", "1", "--synthetic", "48",
+          "--batch-size", "16", "--output-path", str(tmp_path), "--log-every", "2"])
+    losses = [float(l) for l in open(tmp_path / "loss_m.txt")]
+    assert len(losses) == 3 and all(np.isfinite(losses))
+
+
 def test_device_noise_mix_matches_numpy(gpu):
     from oracle import features as OF
     from speechrecognitionproject_amd.dataset import DeviceNoiseMix

@@ -32,6 +32,10 @@ __device__ __forceinline__ float wave_max(float v) {
 __device__ __forceinline__ float fast_log10(float x) { return __builtin_amdgcn_logf(x) * 0.30102999566398120f; }
 __device__ __forceinline__ float fast_ln(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
 
+__device__ __forceinline__ float bperm(int src_byte, float v) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(src_byte, __float_as_int(v)));
+}
+
 // sum over the 16 lanes of a frame group (lanes 16f .. 16f+15)
 __device__ __forceinline__ double group16_sum(double v) {
 #pragma unroll
@@ -140,34 +144,43 @@ __global__ __launch_bounds__(256, 4) void fbank_kernel(const float* __restrict__
     for (int jj = 0; jj < 16; ++jj) b[jj] = tb[f * 272 + j * 17 + jj];
     dft16v(b);
     wave_lds_fence();
+    // untangle (as K1): with A = Z[k], B = Z[256 - k], W = W512^k, S = (A.x + B.x, A.y - B.y),
+    // U = (A.y + B.y, B.x - A.x): 2 X[k] = S + W U and 2 X[256 - k] = (S - W U)*.  Lane (f, k1) pairs
+    // its k2 < 8 with lane (f, 16 - k1) at 15 - k2 (ds_bpermute); k1 = 0 and 8 pair inside the lane,
+    // k1 = 0 also takes the self-paired bin 128 and writes the fp64 DC / Nyquist powers for k = 0 / 256.
+    {
+      const int pbyte = 4 * (16 * f + ((16 - j) & 15));
+      float Bx[8], By[8];
+      v2f wpost[8];
 #pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) tb[f * 272 + j + 16 * k2] = b[k2];
-    wave_lds_fence();
-    // untangle -> |X[k]|^2 (k = 0..256) of the 4 frames, held in registers, then written over tb
-    float p[4][5];
+      for (int k2 = 0; k2 < 8; ++k2) wpost[k2] = s_post[j + 16 * k2];
+      const v2f w128 = s_post[128];
 #pragma unroll
-    for (int ff = 0; ff < 4; ++ff) {
-      const double dcf = __shfl(dc, 16 * ff, 64), nyf = __shfl(ny, 16 * ff, 64);
+      for (int k2 = 0; k2 < 8; ++k2) {
+        Bx[k2] = bperm(pbyte, b[15 - k2].x);
+        By[k2] = bperm(pbyte, b[15 - k2].y);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      float* pf = pb + f * 260;
+      auto two_bins = [&](float ax, float ay, float bx, float by, v2f w, int k) {
+        const float sx = ax + bx, sy = ay - by, ux = ay + by, uy = bx - ax;
+        const float wr = fmaf(w.x, ux, -(w.y * uy)), wi = fmaf(w.y, ux, w.x * uy);
+        const float r1 = sx + wr, i1 = sy + wi, r2 = sx - wr, i2 = sy - wi;
+        pf[256 - k] = 0.25f * fmaf(r2, r2, i2 * i2);   // first: bin 128 pairs with itself
+        pf[k] = 0.25f * fmaf(r1, r1, i1 * i1);
+      };
 #pragma unroll
-      for (int m = 0; m < 5; ++m) {
-        const int k = lane + 64 * m;
-        const v2f A = tb[ff * 272 + (k & 255)];
-        const v2f Bz = tb[ff * 272 + ((256 - k) & 255)];
-        const v2f Bc = v2f{Bz.x, -Bz.y};
-        const v2f e = 0.5f * (A + Bc), o = mi2(0.5f * (A - Bc));
-        const v2f X = e + cm2(s_post[min(k, 256)], o);
-        float v = X.x * X.x + X.y * X.y;
-        if (k == 0) v = (float)(dcf * dcf);
-        if (k == 256) v = (float)(nyf * nyf);
-        p[ff][m] = v;
+      for (int k2 = 0; k2 < 8; ++k2) {
+        const float bx = j == 0 ? b[(16 - k2) & 15].x : Bx[k2];
+        const float by = j == 0 ? b[(16 - k2) & 15].y : By[k2];
+        two_bins(b[k2].x, b[k2].y, bx, by, wpost[k2], j + 16 * k2);
+      }
+      if (j == 0) {
+        two_bins(b[8].x, b[8].y, b[8].x, b[8].y, w128, 128);
+        pf[0] = (float)(dc * dc);     // DC / Nyquist from the fp64 sums (the pre-emphasised DC bin
+        pf[256] = (float)(ny * ny);   // cancels in fp32)
       }
     }
-    wave_lds_fence();
-#pragma unroll
-    for (int ff = 0; ff < 4; ++ff)
-#pragma unroll
-      for (int m = 0; m < 5; ++m)
-        if (lane + 64 * m <= 256) pb[ff * 260 + lane + 64 * m] = p[ff][m];
     wave_lds_fence();
     // mel pairs (filter l and 119 - l), |X|^2 / 512 (:44, an exact power of two), eps floor, 20 log10
     if (lane < kFbPairs) {
@@ -338,9 +351,6 @@ constexpr int kM3Waves = 4;
 constexpr int kM3DbP = 132;   // dB image [frame][band] pitch (16-B rows)
 constexpr int kM3CP = 52;     // coefficient image [13][52]
 
-__device__ __forceinline__ float bperm(int src_byte, float v) {
-  return __int_as_float(__builtin_amdgcn_ds_bpermute(src_byte, __float_as_int(v)));
-}
 
 typedef float f32x4_ __attribute__((ext_vector_type(4)));
 

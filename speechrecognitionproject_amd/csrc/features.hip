@@ -185,6 +185,16 @@ __global__ __launch_bounds__(256, 4) void fbank_kernel(const float* __restrict__
     // mel pairs (filter l and 119 - l), |X|^2 / 512 (:44, an exact power of two), eps floor, 20 log10
     if (lane < kFbPairs) {
       float* o = out + (clip * 98 + 4 * c) * 120;
+      // the pair's tap weights, read once per item, split into the two filters (zero elsewhere): a
+      // tap is then one LDS read and two multiply-adds, no per-tap selects
+      float wa[kFbPairTaps], wb[kFbPairTaps];
+#pragma unroll
+      for (int q = 0; q < kFbPairTaps; ++q) {
+        const float w = pw[q];
+        wa[q] = q < meta.y ? w : 0.f;
+        wb[q] = q < meta.y ? 0.f : w;
+      }
+      const int ka = meta.x, kb = meta.z - meta.y;   // tap q reads bin (q < cnt_a ? ka : kb) + q
 #pragma unroll
       for (int ff = 0; ff < 4; ++ff) {
         if (4 * c + ff >= 98) break;
@@ -192,11 +202,9 @@ __global__ __launch_bounds__(256, 4) void fbank_kernel(const float* __restrict__
         float sa = 0.f, sb = 0.f;
 #pragma unroll
         for (int q = 0; q < kFbPairTaps; ++q) {
-          const bool in_a = q < meta.y;
-          const int k = in_a ? meta.x + q : meta.z + (q - meta.y);
-          const float v = pw[q] * pp[min(k, 256)];
-          sa += in_a ? v : 0.f;
-          sb += in_a ? 0.f : v;
+          const float v = pp[min((q < meta.y ? ka : kb) + q, 256)];
+          sa += wa[q] * v;
+          sb += wb[q] * v;
         }
         sa *= (1.0f / 512.0f);
         sb *= (1.0f / 512.0f);

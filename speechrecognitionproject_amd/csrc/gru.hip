@@ -481,7 +481,10 @@ int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
     xa = xp;
     wa = wp;
   }
-  const bool persistent = srk::g_opt_gru_persistent && srk::gru_persistent_supported(B, T, H, false);
+  // both directions of the layer persistent or neither: the persistent fp32 kernels hand the saved
+  // gates over unit-interleaved, the per-step kernels in the plain layout
+  const bool persistent = srk::g_opt_gru_persistent && srk::gru_persistent_supported(B, T, H, false) &&
+                          srk::gru_persistent_supported(B, T, H, true);
   const bool fuse = persistent && in <= srk::kFusedIn;   // the kernel projects the input itself
   if (!fuse) {
     GemmDesc g;   // gi[B*T, 6H] = x[B*T, in] * W_ih_cat[6H, in]^T + b_ih_cat
@@ -606,7 +609,8 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
   a.dy = dy; a.dgi = dgi; a.dgh = dgh; a.dgh_edge = dgh_edge; a.dhz = dhz;
   a.G = (int)((B + srk::kRows - 1) / srk::kRows);
   a.S = (int)(H / srk::kUnits);
-  if (srk::g_opt_gru_persistent && srk::gru_persistent_supported(B, T, H, true)) {
+  if (srk::g_opt_gru_persistent && srk::gru_persistent_supported(B, T, H, false) &&
+      srk::gru_persistent_supported(B, T, H, true)) {   // as the forward decided (the gates' layout)
     srk::GruPArgs p{};
     p.B = (int)B; p.T = (int)T; p.H = (int)H;
     p.w_hh = w_hh; p.y_in = y; p.gates = a.gates; p.dy = dy; p.dgi = dgi; p.dgh = dgh; p.dgh_edge = dgh_edge;

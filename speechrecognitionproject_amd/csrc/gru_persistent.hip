@@ -467,7 +467,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
     sync_arrive(a, cnt, dir, group, slice, step, local);   // waits for the hand-off stores only: y and the gates go out after it (no consumer in this launch)
     stamp(a, step, 4);
     if (b0 + yrl <= b_last) st4(a.y + ((size_t)(b0 + yrl) * T + t) * 2 * H + dir * H + j0 + yuq, hv4);
-    store_gates(a, gsv, dir, t, b0 + wave * 16 + lq * 4, b_last, j);
+    store_gates_il(a, gsv, dir, t, b0 + wave * 16 + lq * 4, b_last, j);   // unit-interleaved: read by gru_bwd_persistent_kernel
   }
 }
 
@@ -521,11 +521,12 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int b = min(b0 + wave * 16 + lq * 4 + r, b_last);
-      const float* gs = a.gates + (((size_t)dir * T + t) * B + b) * 4 * H;
-      g_r[r] = gs[j];
-      g_z[r] = gs[H + j];
-      g_n[r] = gs[2 * H + j];
-      g_h[r] = gs[3 * H + j];
+      const float* gs = a.gates + (((size_t)dir * T + t) * B + b) * 4 * H;   // unit-interleaved (store_gates_il)
+      const v4f gv = *reinterpret_cast<const v4f*>(gs + 4 * j);
+      g_r[r] = gv.x;
+      g_z[r] = gv.y;
+      g_n[r] = gv.z;
+      g_h[r] = gv.w;
       dyv[r] = a.dy[((size_t)b * T + t) * 2 * H + dir * H + j];
       hpv[r] = edge ? 0.f : a.y_in[((size_t)b * T + tprev) * 2 * H + dir * H + j];
     }

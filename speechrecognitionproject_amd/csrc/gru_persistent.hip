@@ -480,7 +480,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
   static_assert(NKB % CH == 0, "chunking");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Wt = smem;
-  float* dT = smem + kUnits * WP;   // [64][3][DTP]
+  float* dT = smem + kUnits * WP;   // [64][4][DTP]: dar, daz, dan * r (the hand-off / dgh), dan (dgi)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
   int dir, group, slice;
   bool local;
@@ -508,7 +508,6 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
   const int Gp = a.G;
   const __amdgpu_buffer_rsrc_t rg_ = rsrc(a.xbuf + (size_t)dir * 2 * Gp * 64 * 3 * H);   // [2][Gp][4][3H/16][64][4]
   float dhz[4] = {0.f, 0.f, 0.f, 0.f};
-  float dgv[4][3];   // this step's dgi, stored after the arrival
 
   for (int step = 0; step < T; ++step) {
     const int t = dir == 0 ? T - 1 - step : step;
@@ -580,12 +579,10 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
       const float dan = dn * (1.0f - ng * ng);
       const float dar = dan * ghn * rg * (1.0f - rg);
       dhz[r] = dh * zg;
-      dT[(rl * 3 + 0) * DTP + lr] = dar;
-      dT[(rl * 3 + 1) * DTP + lr] = daz;
-      dT[(rl * 3 + 2) * DTP + lr] = dan * rg;
-      dgv[r][0] = dar;
-      dgv[r][1] = daz;
-      dgv[r][2] = dan;
+      dT[(rl * 4 + 0) * DTP + lr] = dar;
+      dT[(rl * 4 + 1) * DTP + lr] = daz;
+      dT[(rl * 4 + 2) * DTP + lr] = dan * rg;
+      dT[(rl * 4 + 3) * DTP + lr] = dan;
     }
     __syncthreads();
     stamp(a, step, 3);
@@ -597,7 +594,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int v = tid + i * 256, rl = v / 12, g = (v % 12) / 4, uq = (v % 4) * 4, b = b0 + rl;
-      val[i] = ld4(dT + (rl * 3 + g) * DTP + uq);
+      val[i] = ld4(dT + (rl * 4 + g) * DTP + uq);
       if (b > b_last || edge) continue;
       st4_ho(rg_, (unsigned)(((((size_t)(step & 1) * Gp + group) * 4 + (rl >> 4)) * NKB * 64 +
                                (g * (H / 16) + slice) * 64 + (uq >> 2) * 16 + (rl & 15)) * 16), val[i], local);
@@ -614,8 +611,11 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
         st4(a.dgh_edge + ((size_t)dir * B + b) * 3 * H + g * H + j0 + uq, val[i]);
         st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + j0 + uq, v4f{0.f, 0.f, 0.f, 0.f});
       }
+      // dgi (dar, daz, dan): the same 16-B row pieces from the staged image (a dword store per
+      // cell and gate otherwise)
+      st4(a.dgi + ((size_t)b * T + t) * 6 * H + dir * 3 * H + g * H + j0 + uq,
+          g == 2 ? ld4(dT + (rl * 4 + 3) * DTP + uq) : val[i]);
     }
-    store_dgi(a, dgv, dir, t, b0 + wave * 16 + lq * 4, b_last, j);
   }
 }
 
@@ -1534,7 +1534,7 @@ int occupancy_ok(bool backward, int prec, int grid) {
 }  // namespace
 
 size_t fwd_lds_bytes(int H) { return (size_t)(3 * 16 * (H + 4) + 64 * 20 + 48 * kXP) * 4; }
-size_t bwd_lds_bytes(int H) { return (size_t)(16 * (3 * H + 4) + 64 * 3 * 20) * 4; }
+size_t bwd_lds_bytes(int H) { return (size_t)(16 * (3 * H + 4) + 64 * 4 * 20) * 4; }
 
 int gru_persistent_groups(int64_t H) {
   if (H != 512) return 0;

@@ -357,7 +357,7 @@ __device__ __forceinline__ void mfcc_load_chunk(const float* __restrict__ x, int
 // (v_mfma_f32_16x16x4_f32, exact fp32 products), then the deltas and the store.
 constexpr int kM3Waves = 4;
 constexpr int kM3DbP = 132;   // dB image [frame][band] pitch (16-B rows)
-constexpr int kM3CP = 52;     // coefficient image [13][52]
+constexpr int kM3CP = 53;     // coefficient image [13][53] (odd pitch: the delta reads of 13 rows spread over banks)
 
 
 typedef float f32x4_ __attribute__((ext_vector_type(4)));

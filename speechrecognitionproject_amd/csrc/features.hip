@@ -80,7 +80,8 @@ __global__ __launch_bounds__(256, 4) void fbank_kernel(const float* __restrict__
   }
   __syncthreads();
   v2f* tb = sbuf[wave];
-  float* pb = reinterpret_cast<float*>(tb);   // power [4][260] after the untangle
+  float* pb = reinterpret_cast<float*>(tb);   // power [4][272] after the untangle (pitch = 16 mod 32:
+                                              // two frames' 16-lane stores fill the 32 banks)
   const int pl = lane < kFbPairs ? lane : 0;
   const int4 meta = t.pair_meta[pl];
   const float* pw = s_pw + pl * kFbPairTaps;
@@ -161,7 +162,7 @@ __global__ __launch_bounds__(256, 4) void fbank_kernel(const float* __restrict__
         By[k2] = bperm(pbyte, b[15 - k2].y);
       }
       __builtin_amdgcn_sched_barrier(0);
-      float* pf = pb + f * 260;
+      float* pf = pb + f * 272;
       auto two_bins = [&](float ax, float ay, float bx, float by, v2f w, int k) {
         const float sx = ax + bx, sy = ay - by, ux = ay + by, uy = bx - ax;
         const float wr = fmaf(w.x, ux, -(w.y * uy)), wi = fmaf(w.y, ux, w.x * uy);
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(256, 4) void fbank_kernel(const float* __restrict__
 #pragma unroll
       for (int ff = 0; ff < 4; ++ff) {
         if (4 * c + ff >= 98) break;
-        const float* pp = pb + ff * 260;
+        const float* pp = pb + ff * 272;
         float sa = 0.f, sb = 0.f;
 #pragma unroll
         for (int q = 0; q < kFbPairTaps; ++q) {

@@ -1287,6 +1287,23 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmDesc d, const fl
   *c = v;
 }
 
+// The same with 4 consecutive columns per thread (N % 4 == 0, ldc % 4 == 0, 16-B aligned C): 16-B
+// slab loads and one 16-B store per thread.
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(GemmDesc d, const float* __restrict__ partial, int splits) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, n4 = d.N >> 2;
+  if (q >= d.M * n4) return;
+  const int64_t row = q / n4, col = (q - row * n4) * 4, i = row * d.N + col;
+  const int64_t slab = d.M * d.N;
+  v4f s = *reinterpret_cast<const v4f*>(partial + i);
+  for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const v4f*>(partial + (int64_t)k * slab + i);
+  v4f v = d.alpha * s;
+  if (d.bias_mode == 1) v += *reinterpret_cast<const v4f*>(d.bias + col);
+  else if (d.bias_mode == 2) v += d.bias[row];
+  v4f* c = reinterpret_cast<v4f*>(d.C + row * d.ldc + col);
+  if (d.beta != 0.f) v += d.beta * *c;
+  *c = v;
+}
+
 __global__ void rowsum_reduce_kernel(float* __restrict__ out, float beta, const float* __restrict__ rp, int64_t M,
                                      int splits) {
   const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1387,8 +1404,14 @@ int finish_splits(const GemmDesc& d, const KernelArgs& ka, int splits, hipStream
   SRK_CHECK_HIP(hipGetLastError());
   if (splits > 1) {
     const int64_t n = d.M * d.N;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, ka.partial,
-                       splits);
+    const bool vec4 = d.N % 4 == 0 && d.ldc % 4 == 0 && (uintptr_t)d.C % 16 == 0 &&
+                      (d.bias_mode != 1 || (uintptr_t)d.bias % 16 == 0);
+    if (vec4)
+      hipLaunchKernelGGL(splitk_reduce4_kernel, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, s, d, ka.partial,
+                         splits);
+    else
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, ka.partial,
+                         splits);
     if (d.rowsum)
       hipLaunchKernelGGL(rowsum_reduce_kernel, dim3((unsigned)((d.M + 255) / 256)), dim3(256), 0, s, d.rowsum,
                          d.rowsum_beta, ka.rs_partial, d.M, splits);

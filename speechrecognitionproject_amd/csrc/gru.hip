@@ -335,8 +335,31 @@ __global__ void to16_kernel(const float* __restrict__ src, int64_t rows, int col
     dst[i] = __builtin_bit_cast(uint16_t, h);
   }
 }
+// Dense case (no column padding, 8 | n, 16-B aligned): 8 elements per thread, two 16-B loads and one
+// 16-B store, no index division.
+template <bool F16>
+__global__ void to16_vec8_kernel(const float* __restrict__ src, int64_t n8, uint16_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((ext_vector_type(8))) typename std::conditional<F16, _Float16, __bf16>::type e8;
+  const f4 a = *reinterpret_cast<const f4*>(src + 8 * i), b = *reinterpret_cast<const f4*>(src + 8 * i + 4);
+  const e8 h = __builtin_convertvector((__attribute__((ext_vector_type(8))) float){a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}, e8);
+  *reinterpret_cast<u4*>(dst + 8 * i) = __builtin_bit_cast(u4, h);
+}
+
 int to16(const float* src, int64_t rows, int64_t cols, uint16_t* dst, int64_t colsp, hipStream_t s) {
   const int64_t n = rows * colsp;
+  if (cols == colsp && n % 8 == 0 && (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0) {
+    const int64_t n8 = n / 8;
+    if (matmul_prec() == kPrecF16)
+      hipLaunchKernelGGL(to16_vec8_kernel<true>, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, src, n8, dst);
+    else
+      hipLaunchKernelGGL(to16_vec8_kernel<false>, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, src, n8, dst);
+    SRK_CHECK_HIP(hipGetLastError());
+    return SRK_OK;
+  }
   if (matmul_prec() == kPrecF16)
     hipLaunchKernelGGL(to16_kernel<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, rows, (int)cols,
                        dst, (int)colsp);

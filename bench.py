@@ -91,7 +91,7 @@ LP_KERNELS = ("gemm_bf16", "gemm_f16", "gru_fwd_seq_lp", "gru_bwd_seq_lp", "conv
               "conv_wgrad_lp")
 OTHER_KERNELS = ("mfcc", "fbank", "spec", "noise_mix", "adam", "batchnorm_fwd", "batchnorm_bwd", "conv1_pool_fwd",
                  "conv1_pool_wgrad",
-                 "maxpool_fwd", "maxpool_bwd")
+                 "maxpool_fwd", "maxpool_bwd", "conv_to16")
 
 
 def log(*a):

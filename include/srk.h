@@ -52,7 +52,9 @@ int srk_prof_read(const char* name, int64_t* count, double* total_ms, double* to
  * nearest-even on chip, fp32 accumulation, fp32 tensors in and out (BASELINE.json cfg2 / cfg5);
  * "gemm16_kernel" (default 0 = by shape) = the 16-bit-operand GEMM kernel: 1 register-staged,
  * 2 LDS-DMA ping-pong (same results up to fp32 summation order; for A/B measurements and tests);
- * "gemm32_kernel" (default 0 = by shape) = the same choice for the fp32 GEMM. */
+ * "gemm32_kernel" (default 0 = by shape) = the same choice for the fp32 GEMM;
+ * "conv16_sources" (default 1) = bf16 / fp16 convolutions gather from one pre-rounded 16-bit copy
+ * of their operands (0 = round at LDS-store time; bit-identical results either way). */
 int srk_set_option(const char* name, int64_t value);
 /* Number of bounded spin-waits of the persistent kernels that gave up (synchronizes the
  * device; must stay 0 — a non-zero value means a co-residency assumption failed).  -1 on error. */

@@ -47,6 +47,11 @@ struct ConvArgs {
   int tiles_m, tiles_n, tiles, nblk, group_m;
   int64_t kchunk;
   float* partial;      // split-K slabs
+  // 16-bit operand sources (matmul_precision bf16 / fp16, 8-aligned channel counts): the A source
+  // (x or dy) and B (the weight matrix, or dy for wgrad) pre-rounded once per call, so a gather
+  // moves 8 elements per 16-B load and the LDS store needs no conversion.  Null = fp32 sources.
+  const unsigned short* a16;
+  const unsigned short* b16;
   // divisors of the gathers (host-set): pixel grid (cols, rows), channels, KW, strides (dgrad)
   FastDiv fd_w, fd_h, fd_c, fd_kw, fd_sh, fd_sw;
 };
@@ -133,6 +138,10 @@ struct Img16 {
   __device__ static __forceinline__ int store_off(int vi) {
     return KC ? (vi / (BK / 4)) * P + (vi % (BK / 4)) * 4 : (vi / (ROWS / 4)) * P + (vi % (ROWS / 4)) * 4;
   }
+  // the same for a staged unit of 8 elements (16-bit sources)
+  __device__ static __forceinline__ int store_off8(int vi) {
+    return KC ? (vi / (BK / 8)) * P + (vi % (BK / 8)) * 8 : (vi / (ROWS / 8)) * P + (vi % (ROWS / 8)) * 8;
+  }
   __device__ static __forceinline__ u32x4_ frag(const unsigned short* img, int c0, int kk, int lane) {
     if (KC) return *reinterpret_cast<const u32x4_*>(img + (c0 + (lane & 31)) * P + kk + 8 * (lane >> 5));
     const int q = (lane >> 2) & 3, p = lane & 3;
@@ -149,7 +158,10 @@ struct Img16 {
 // (fwd / wgrad: Ci, dgrad: Co).  VECB: the B operand's N % 4 == 0 (16-B loads along n).
 // LP: 0 = fp32 operands (v_mfma_f32_32x32x2_f32), 1 / 2 = bf16 / fp16 operands rounded at LDS-store
 // time (v_mfma_f32_32x32x16_{bf16,f16}, Img16 images), fp32 gathers, masks and epilogue alike.
-template <int MODE, int BM, int BN, int BK, bool VEC, bool VECB, int LP = 0>
+// S16: 16-bit sources (ConvArgs::a16 / b16, rounded by the same conversion as the LDS-store path,
+// so the MFMA operands are bit-identical): a staged unit is 8 elements = one 16-B load and one
+// 16-B LDS store (needs VEC and VECB with 8-aligned channel counts / N).
+template <int MODE, int BM, int BN, int BK, bool VEC, bool VECB, int LP = 0, bool S16 = false>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   constexpr int NT = 256;
   constexpr bool AKC = MODE != kWgrad;   // A k-contiguous (channels along k) for fwd / dgrad
@@ -157,7 +169,9 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   using IB = Img<false, BN, BK>;         // B = row-major [K][N] (Wt / Wd / dY)
   using JA = Img16<AKC, BM, BK>;
   using JB = Img16<false, BN, BK>;
-  constexpr int VA = BM * BK / 4 / NT, VB = BN * BK / 4 / NT;
+  static_assert(!S16 || (LP != 0 && VEC && VECB), "16-bit sources need the vector gathers");
+  constexpr int EU = S16 ? 8 : 4;        // elements per staged unit
+  constexpr int VA = BM * BK / EU / NT, VB = BN * BK / EU / NT;
   constexpr int TM = BM / 64, TN = BN / 64;
   static_assert(VA >= 1 && VB >= 1 && TM >= 1 && TN >= 1 && VA * 4 <= 32, "bad tile");
   constexpr int STAGE_FLOATS = LP ? (JA::ELEMS + JB::ELEMS + 1) / 2 : IA::FLOATS + IB::FLOATS;
@@ -180,20 +194,55 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   Tap mtap[4];   // wgrad: the taps m0 + aq + e of this thread (fixed for the whole k loop)
   int aq;        // fwd/dgrad: k offset of this thread's float4 in a stage; wgrad: m offset
   if (AKC) {
-    aq = (tid % (BK / 4)) * 4;
+    aq = (tid % (BK / EU)) * EU;
 #pragma unroll
-    for (int i = 0; i < VA; ++i) prow[i] = split_pix(m0 + (tid + i * NT) / (BK / 4), c.M, c.fd_w, c.fd_h);
+    for (int i = 0; i < VA; ++i) prow[i] = split_pix(m0 + (tid + i * NT) / (BK / EU), c.M, c.fd_w, c.fd_h);
   } else {
-    aq = (tid % (BM / 4)) * 4;
+    aq = (tid % (BM / EU)) * EU;
 #pragma unroll
     for (int e = 0; e < 4; ++e) mtap[e] = split_tap(m0 + aq + e < c.M ? m0 + aq + e : 0, c.fd_c, c.fd_kw);
   }
 
-  v4f ra[VA], rb[VB];
-  unsigned amask = 0, bmask = 0;   // bit = element valid (4 per staged float4)
+  v4f ra[VA], rb[VB];   // fp32 staged units (unused, and eliminated, when S16)
+  u32x4_ ha[S16 ? VA : 1], hb[S16 ? VB : 1];   // S16 staged units (8 x 16 bit)
+  unsigned amask = 0, bmask = 0;   // bit = element valid (4 per staged float4; S16: 1 per unit)
   auto load_tile = [&](int64_t k0) {
     amask = 0;
     bmask = 0;
+    if constexpr (S16) {
+      // every unit shares one pixel and one tap (channel counts % 8 == 0) and never straddles ke
+      // (K and the split chunks are multiples of 8)
+      if (AKC) {
+        const int64_t k = k0 + aq;
+        const Tap t = split_tap(k < ke ? k : 0, c.fd_c, c.fd_kw);
+#pragma unroll
+        for (int i = 0; i < VA; ++i) {
+          bool ok = k < ke;
+          const int64_t off = a_offset<MODE>(c, prow[i], t, ok);
+          ha[i] = *reinterpret_cast<const u32x4_*>(c.a16 + off);
+          amask |= (ok ? 1u : 0u) << i;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < VA; ++i) {
+          const int64_t k = k0 + (tid + i * NT) / (BM / EU);
+          const Pix p = split_pix(k < ke ? k : 0, c.K, c.fd_w, c.fd_h);
+          bool ok = k < ke && m0 + aq < c.M;
+          const int64_t off = a_offset<MODE>(c, p, mtap[0], ok);
+          ha[i] = *reinterpret_cast<const u32x4_*>(c.a16 + off);
+          amask |= (ok ? 1u : 0u) << i;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < VB; ++i) {
+        const int vi = tid + i * NT;
+        const int64_t k = k0 + vi / (BN / EU), n = n0 + (vi % (BN / EU)) * EU;
+        const unsigned short* q = c.b16 + (k < ke ? k : ke - 1) * c.Nn;
+        hb[i] = *reinterpret_cast<const u32x4_*>(q + (n < c.Nn ? n : c.Nn - 8));
+        bmask |= (k < ke ? 1u : 0u) << i;
+      }
+      return;
+    }
     if (AKC) {   // 4 consecutive k = (kh, kw, ch .. ch+3) of one pixel row
       const int64_t k = k0 + aq;
       if (VEC) {
@@ -265,6 +314,18 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   auto store_tile = [&](int buf) {
+    if constexpr (S16) {
+      unsigned short* As = reinterpret_cast<unsigned short*>(smem + buf * STAGE_FLOATS);
+      unsigned short* Bs = As + JA::ELEMS;
+      const u32x4_ z = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int i = 0; i < VA; ++i)
+        *reinterpret_cast<u32x4_*>(As + JA::store_off8(tid + i * NT)) = (amask >> i) & 1u ? ha[i] : z;
+#pragma unroll
+      for (int i = 0; i < VB; ++i)
+        *reinterpret_cast<u32x4_*>(Bs + JB::store_off8(tid + i * NT)) = (bmask >> i) & 1u ? hb[i] : z;
+      return;
+    }
     if constexpr (LP != 0) {
       using E4 = typename ConvLp<LP>::e4;
       unsigned short* As = reinterpret_cast<unsigned short*>(smem + buf * STAGE_FLOATS);
@@ -473,18 +534,31 @@ __global__ void zero_kernel(float* __restrict__ p, int64_t n) {
   if (i < n) p[i] = 0.f;
 }
 
+// fp32 -> 16-bit operand copy, 8 elements per thread, by the same conversion the LDS-store path
+// applies (so S16 operands are bit-identical to the fp32-source LP path's)
+template <int LP>
+__global__ void to16_kernel(const float* __restrict__ x, int64_t n8, unsigned short* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  using E4 = typename ConvLp<LP>::e4;
+  const u32x2_ lo = __builtin_bit_cast(u32x2_, __builtin_convertvector(ld4(x + 8 * i), E4));
+  const u32x2_ hi = __builtin_bit_cast(u32x2_, __builtin_convertvector(ld4(x + 8 * i + 4), E4));
+  *reinterpret_cast<u32x4_*>(y + 8 * i) = u32x4_{lo.x, lo.y, hi.x, hi.y};
+}
+
 struct ConvScratch {
   float* p = nullptr;
   size_t floats = 0;
 };
-ConvScratch g_cs[64];
+ConvScratch g_cs[64];     // split-K slabs
+ConvScratch g_cs16[64];   // 16-bit operand sources
 std::mutex g_cs_mu;
 
-int conv_scratch(size_t floats, float** out) {
+int conv_scratch(size_t floats, float** out, ConvScratch* pool = g_cs) {
   int dev = 0;
   SRK_CHECK_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_cs_mu);
-  ConvScratch& s = g_cs[dev & 63];
+  ConvScratch& s = pool[dev & 63];
   if (s.floats < floats) {
     if (s.p) {
       SRK_CHECK_HIP(hipDeviceSynchronize());
@@ -497,8 +571,47 @@ int conv_scratch(size_t floats, float** out) {
   return SRK_OK;
 }
 
+// 16-bit sources (ConvArgs::a16 / b16) for matmul_precision bf16 / fp16 when every channel count is
+// a multiple of 8 and the fp32 tensors are 16-B aligned (option "conv16_sources", default on).
+bool s16_ok(int prec, int64_t Ci, int64_t Co, std::initializer_list<const void*> ptrs) {
+  if (!g_opt_conv16_sources || prec == kPrecF32 || Ci % 8 || Co % 8) return false;
+  for (const void* p : ptrs)
+    if (reinterpret_cast<uintptr_t>(p) % 16) return false;
+  return true;
+}
+
+// rounds cnt fp32 tensors (n[i] % 8 == 0 elements each) into one 16-bit scratch allocation, on s
+int to16_all(int prec, const float* const* src, const int64_t* n, int cnt, unsigned short** dst, hipStream_t s) {
+  size_t off[4], total = 0;
+  double bytes = 0;
+  for (int i = 0; i < cnt; ++i) {
+    off[i] = total;
+    total += (size_t)((n[i] + 63) / 64 * 64);
+    bytes += 6.0 * (double)n[i];
+  }
+  float* base = nullptr;
+  if (int rc = conv_scratch((total + 1) / 2, &base, g_cs16)) return rc;
+  ProfScope prof("conv_to16", s, bytes);
+  for (int i = 0; i < cnt; ++i) {
+    dst[i] = reinterpret_cast<unsigned short*>(base) + off[i];
+    const int64_t n8 = n[i] / 8;
+    SRK_REQUIRE(n[i] % 8 == 0 && (n8 + 255) / 256 < INT32_MAX, SRK_ERR_INTERNAL, "conv: bad 16-bit source size");
+    const dim3 grid((unsigned)((n8 + 255) / 256));
+    if (prec == kPrecBF16) hipLaunchKernelGGL(to16_kernel<1>, grid, dim3(256), 0, s, src[i], n8, dst[i]);
+    else hipLaunchKernelGGL(to16_kernel<2>, grid, dim3(256), 0, s, src[i], n8, dst[i]);
+  }
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+}
+
 template <int MODE, int BM, int BN, int BK, int LP>
 void launch_conv_p(const ConvArgs& c, dim3 grid, hipStream_t s, bool vec, bool vecb) {
+  if constexpr (LP != 0) {
+    if (c.a16) {
+      hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, true, true, LP, true>), grid, dim3(256), 0, s, c);
+      return;
+    }
+  }
   if (vec && vecb) hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, true, true, LP>), grid, dim3(256), 0, s, c);
   else if (vecb) hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, false, true, LP>), grid, dim3(256), 0, s, c);
   else hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, false, false, LP>), grid, dim3(256), 0, s, c);
@@ -548,6 +661,8 @@ int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
   c.fd_sw = FastDiv((unsigned)c.sw);
   const bool vecb = c.Nn % 4 == 0;
   const bool vec = (chans % 4 == 0) && vecb;
+  SRK_REQUIRE(!c.a16 || (prec != kPrecF32 && c.b16 && chans % 8 == 0 && c.Nn % 8 == 0), SRK_ERR_INTERNAL,
+              "conv: 16-bit sources need 8-aligned channels");
   ProfScope prof(prec == kPrecF32 ? name : (MODE == kFwd ? "conv_fwd_lp" : MODE == kDgrad ? "conv_dgrad_lp" : "conv_wgrad_lp"),
                  s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
   const dim3 grid((unsigned)c.nblk);
@@ -599,6 +714,15 @@ int srk_conv2d_nhwc_fwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t
   c.KH = (int)KH; c.KW = (int)KW; c.ph = (int)ph; c.pw = (int)pw; c.sh = (int)sh; c.sw = (int)sw;
   c.x = x; c.wmat = ws; c.out = y; c.bias = bias;
   c.M = N * Ho * Wo; c.Nn = Co; c.K = KH * KW * Ci;
+  const int prec = srk::matmul_prec();
+  if (srk::s16_ok(prec, Ci, Co, {x, ws})) {
+    const float* src[2] = {x, ws};
+    const int64_t n[2] = {N * H * W * Ci, nw};
+    unsigned short* d16[2];
+    if (int rc = srk::to16_all(prec, src, n, 2, d16, s)) return rc;
+    c.a16 = d16[0];
+    c.b16 = d16[1];
+  }
   return srk::run_conv_gemm<srk::kFwd>(c, s, "conv_fwd");
   SRK_API_END
 }
@@ -617,7 +741,20 @@ int srk_conv2d_nhwc_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t
   c.KH = (int)KH; c.KW = (int)KW; c.ph = (int)ph; c.pw = (int)pw; c.sh = (int)sh; c.sw = (int)sw;
   c.x = x; c.dy = dy;
   int rc;
-  if (dx && KH == 1 && ph == 0 && sh == 1 && pw == 0 && KW == W && Wo == 1) {
+  const bool full_width = KH == 1 && ph == 0 && sh == 1 && pw == 0 && KW == W && Wo == 1;
+  const bool dgrad_implicit = dx && !full_width;
+  if (dgrad_implicit)
+    hipLaunchKernelGGL(srk::weight_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, (int)Co,
+                       (int)Ci, (int)KH, (int)KW, 1, ws);
+  // 16-bit sources: x and dY serve both GEMMs, Wd the data gradient (one scratch allocation)
+  unsigned short* d16[3] = {nullptr, nullptr, nullptr};   // x, dY, Wd
+  const int prec = srk::matmul_prec();
+  if (srk::s16_ok(prec, Ci, Co, {x, dy, ws})) {
+    const float* src[3] = {x, dy, ws};
+    const int64_t n[3] = {N * H * W * Ci, N * Ho * Wo * Co, nw};
+    if ((rc = srk::to16_all(prec, src, n, dgrad_implicit ? 3 : 2, d16, s))) return rc;
+  }
+  if (dx && full_width) {
     // A full-width "valid" conv (model_fbanks_cnn.py:74, conv3 1x10 on width 10): every input
     // column meets exactly one tap, so the data gradient is the plain GEMM
     //   dX[(n,h)][(kw,ci)] = dY[(n,h)][co] * Wt[(kw,ci)][co]^T
@@ -632,18 +769,24 @@ int srk_conv2d_nhwc_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t
     srk::ProfScope prof(srk::matmul_prec() == srk::kPrecF32 ? "conv_dgrad" : "conv_dgrad_lp", s,
                         2.0 * (double)g.M * (double)g.N * (double)g.K);
     if ((rc = srk::gemm_f32(g, s))) return rc;
-  } else if (dx) {
-    hipLaunchKernelGGL(srk::weight_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, (int)Co,
-                       (int)Ci, (int)KH, (int)KW, 1, ws);
+  } else if (dgrad_implicit) {
     srk::ConvArgs d = c;
     d.wmat = ws; d.out = dx;
     d.M = N * H * W; d.Nn = Ci; d.K = KH * KW * Co;
+    if (d16[0]) {
+      d.a16 = d16[1];
+      d.b16 = d16[2];
+    }
     if ((rc = srk::run_conv_gemm<srk::kDgrad>(d, s, "conv_dgrad"))) return rc;
   }
   {
     srk::ConvArgs g = c;
     g.out = ws;   // dWt [(kh,kw,ci)][co], then re-laid out into dw
     g.M = KH * KW * Ci; g.Nn = Co; g.K = N * Ho * Wo;
+    if (d16[0]) {
+      g.a16 = d16[0];
+      g.b16 = d16[1];
+    }
     if ((rc = srk::run_conv_gemm<srk::kWgrad>(g, s, "conv_wgrad"))) return rc;
     hipLaunchKernelGGL(srk::weight_grad_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, ws,
                        (int)Co, (int)Ci, (int)KH, (int)KW, dw);

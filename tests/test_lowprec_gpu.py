@@ -278,6 +278,48 @@ def test_conv_lowprec_exact_rounding(prec, shape):
     assert close(wm.grad.cpu(), dw_ref, N * y_ref.shape[2] * y_ref.shape[3])
 
 
+CONV_S16 = [  # 8-aligned channel counts: the pre-rounded 16-bit source path (option conv16_sources)
+    (2, 98, 40, 64, 128, 1, 7, 0, 3, 1, 1),
+    (3, 98, 1, 256, 512, 7, 1, 3, 0, 1, 1),
+    (2, 1, 1000, 64, 128, 1, 15, 0, 7, 1, 2),   # strided: dgrad taps with no exact source
+    (8, 1, 1000, 64, 64, 1, 15, 0, 7, 1, 1),    # wgrad K = 8000 pixels: split-K slabs
+    (3, 1, 125, 512, 512, 1, 15, 0, 7, 1, 1),
+    (2, 5, 7, 8, 24, 3, 3, 1, 1, 1, 1),         # partial 64-row / -column tiles
+    (2, 1, 500, 128, 256, 1, 1, 0, 0, 1, 2),    # 1x1 downsample
+]
+
+
+@pytest.mark.parametrize("shape", CONV_S16)
+def test_conv_16bit_sources_bit_identical(prec, shape):
+    """bf16 / fp16 convs gathering from the pre-rounded 16-bit copy (conv16_sources = 1) give the
+    SAME bits as rounding the fp32 gathers at LDS-store time (0): same rounding, same MFMA order."""
+    from speechrecognitionproject_amd import nn as snn
+    N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw = shape
+    g = torch.Generator().manual_seed(N * 31 + Co + KW)
+    x = torch.randn(N, H, W, Ci, generator=g).cuda()
+    w = (torch.randn(Co, Ci, KH, KW, generator=g) / (Ci * KH * KW) ** 0.5).cuda()
+    b = torch.randn(Co, generator=g).cuda()
+    Ho, Wo = (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
+    gy = torch.randn(N, Ho, Wo, Co, generator=g).cuda()
+    outs = []
+    try:
+        for on in (0, 1):
+            _lib.set_option("conv16_sources", on)
+            xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
+            _lib.prof_enable(1)
+            ym = snn._Conv2dNHWCFn.apply(xm, wm, bm, (ph, pw), (sh, sw))
+            (ym * gy).sum().backward()
+            torch.cuda.synchronize()
+            assert (_lib.prof_read("conv_to16")[0] > 0) == bool(on)
+            _lib.prof_enable(0)
+            outs.append((ym.detach(), xm.grad, wm.grad, bm.grad))
+    finally:
+        _lib.set_option("conv16_sources", 1)
+        _lib.prof_enable(0)
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+
+
 # ----------------------------------------------------------------------------- 16-bit operands in memory
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(8, 8, 8), (40, 24, 72), (136, 264, 200), (304, 128, 1024), (256, 128, 8192),

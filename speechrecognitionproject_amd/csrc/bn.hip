@@ -23,7 +23,12 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 // Work split: a block = 256 threads = CQ channel quads (4 channels each, 16-B accesses) x RP row
 // phases; blockIdx.x walks channel groups of 4*CQ channels, blockIdx.y row chunks.  The chunk count
 // is capped (kMaxChunks) so the per-channel finalize reads a short, fixed-order list of partials.
+// The reduction kernels keep kUnroll rows' 16-B loads in flight per lane (all issued before any is
+// consumed; clamped addresses, masked accumulation in the same row order, so the sums are bitwise
+// those of the one-row loop): with one 4-wave block per CU at C = 64 the one-row loop waited out a
+// full HBM latency per row.
 constexpr int kMaxChunks = 256;
+constexpr int kUnroll = 8;
 
 struct BnGeom {
   int C, C4, CQ, RP;   // channels, channel quads, quads per block, row phases per block
@@ -73,11 +78,22 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
   v4f piv = {0.f, 0.f, 0.f, 0.f};
   if (c4 < g.C4) {
     piv = ld4(x + r0 * g.C + c4 * 4);
-    for (int64_t r = r0 + rp; r < r1; r += g.RP) {
-      const v4f d = ld4(x + r * g.C + c4 * 4) - piv;
-      s1 += d;
-      s2 += d * d;
-      n += 1.f;
+    for (int64_t r = r0 + rp; r < r1; r += kUnroll * g.RP) {
+      v4f v[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t ru = r + u * g.RP;
+        v[u] = ld4(x + (ru < r1 ? ru : r) * g.C + c4 * 4);
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        if (r + u * g.RP < r1) {
+          const v4f d = v[u] - piv;
+          s1 += d;
+          s2 += d * d;
+          n += 1.f;
+        }
+      }
     }
   }
   sn[threadIdx.x] = n;
@@ -122,13 +138,19 @@ __global__ void bn_finalize_kernel(const float* __restrict__ pmean, const float*
   }
 }
 
+template <bool I32>
+__device__ __forceinline__ int chan_of(int64_t o, int C) {
+  return I32 ? (int)((unsigned)o % (unsigned)C) : (int)(o % C);
+}
+
+template <bool I32>
 __global__ void bn_apply_kernel(const float* __restrict__ x, int64_t M, int C, const float* __restrict__ mean,
                                 const float* __restrict__ invstd, const float* __restrict__ gamma,
                                 const float* __restrict__ beta, const float* __restrict__ residual, int relu,
                                 float* __restrict__ y) {
   const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i4 * 4 >= M * C) return;
-  const int c = (int)((i4 * 4) % C);
+  const int c = chan_of<I32>(i4 * 4, C);
   const v4f mu = ld4(mean + c), is = ld4(invstd + c), ga = ld4(gamma + c), be = ld4(beta + c);
   v4f v = (ld4(x + i4 * 4) - mu) * is * ga + be;
   if (residual) v += ld4(residual + i4 * 4);
@@ -161,16 +183,28 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const float* __rest
   v4f a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
   if (c4 < g.C4) {
     const v4f mu = ld4(mean + c4 * 4), is = ld4(invstd + c4 * 4);
-    for (int64_t r = r0 + rp; r < r1; r += g.RP) {
-      const int64_t o = r * g.C + c4 * 4;
-      v4f gr = ld4(dy + o);
-      if (relu) {
-        const v4f yv = ld4(y + o);
+    for (int64_t r = r0 + rp; r < r1; r += kUnroll * g.RP) {
+      v4f vd[kUnroll], vy[kUnroll], vx[kUnroll];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) gr[e] = yv[e] <= 0.f ? 0.f : gr[e];
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t ru = r + u * g.RP;
+        const int64_t o = (ru < r1 ? ru : r) * g.C + c4 * 4;
+        vd[u] = ld4(dy + o);
+        if (relu) vy[u] = ld4(y + o);
+        vx[u] = ld4(x + o);
       }
-      a0 += gr;
-      a1 += gr * ((ld4(x + o) - mu) * is);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        if (r + u * g.RP < r1) {
+          v4f gr = vd[u];
+          if (relu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) gr[e] = vy[u][e] <= 0.f ? 0.f : gr[e];
+          }
+          a0 += gr;
+          a1 += gr * ((vx[u] - mu) * is);
+        }
+      }
     }
   }
   s0[threadIdx.x] = a0;
@@ -200,6 +234,7 @@ __global__ void bn_dgamma_kernel(const float* __restrict__ p0, const float* __re
   dgamma[c] = b;
 }
 
+template <bool I32>
 __global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ dy,
                              int64_t M, int C, const float* __restrict__ mean, const float* __restrict__ invstd,
                              const float* __restrict__ gamma, const float* __restrict__ dbeta,
@@ -209,7 +244,7 @@ __global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restric
   const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i4 * 4 >= M * C) return;
   const int64_t o = i4 * 4;
-  const int c = (int)(o % C);
+  const int c = chan_of<I32>(o, C);
   v4f gr = ld4(dy + o);
   if (relu) {
     const v4f yv = ld4(y + o);
@@ -322,7 +357,7 @@ int srk_batchnorm_fwd(const float* x, int64_t M, int64_t C, const float* gamma, 
                        running_var, (int)C, eps, save_mean, save_invstd);
   }
   const int64_t n4 = M * C / 4;
-  hipLaunchKernelGGL(srk::bn_apply_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, M, (int)C,
+  hipLaunchKernelGGL(M * C < (1LL << 32) ? srk::bn_apply_kernel<true> : srk::bn_apply_kernel<false>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, M, (int)C,
                      save_mean, save_invstd, gamma, beta, residual, relu, y);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
@@ -346,7 +381,7 @@ int srk_batchnorm_bwd(const float* x, const float* y, const float* dy, int64_t M
   hipLaunchKernelGGL(srk::bn_dgamma_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
                      part + (size_t)g.chunks * C, g.chunks, (int)C, dbeta, dgamma);
   const int64_t n4 = M * C / 4;
-  hipLaunchKernelGGL(srk::bn_dx_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, y, dy, M, (int)C,
+  hipLaunchKernelGGL(M * C < (1LL << 32) ? srk::bn_dx_kernel<true> : srk::bn_dx_kernel<false>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, y, dy, M, (int)C,
                      save_mean, save_invstd, gamma, dbeta, dgamma, relu, training, (float)M, nullptr, dx, dresidual);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
@@ -397,7 +432,7 @@ int srk_batchnorm_apply(const float* x, int64_t M, int64_t C, const float* save_
   hipStream_t s = srk::as_stream(stream);
   srk::ProfScope prof("batchnorm_fwd", s, 8.0 * (double)M * C);
   const int64_t n4 = M * C / 4;
-  hipLaunchKernelGGL(srk::bn_apply_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, M, (int)C,
+  hipLaunchKernelGGL(M * C < (1LL << 32) ? srk::bn_apply_kernel<true> : srk::bn_apply_kernel<false>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, M, (int)C,
                      save_mean, save_invstd, gamma, beta, residual, relu, y);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
@@ -434,7 +469,7 @@ int srk_batchnorm_bwd_dx(const float* x, const float* y, const float* dy, int64_
   hipStream_t s = srk::as_stream(stream);
   srk::ProfScope prof("batchnorm_bwd", s, 16.0 * (double)M * C);
   const int64_t n4 = M * C / 4;
-  hipLaunchKernelGGL(srk::bn_dx_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, y, dy, M, (int)C,
+  hipLaunchKernelGGL(M * C < (1LL << 32) ? srk::bn_dx_kernel<true> : srk::bn_dx_kernel<false>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, y, dy, M, (int)C,
                      save_mean, save_invstd, gamma, sums, sums + C, relu, 1, 0.f, total_count, dx, dresidual);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;

@@ -197,6 +197,18 @@ int srk_conv2d_nhwc_fwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t
 int srk_conv2d_nhwc_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co,
                         int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw, const float* dy,
                         float* dx, float* dw, float* db, float* ws, void* stream);
+/* The same pair with the forward's 16-bit copy of x kept for the backward (bf16 / fp16 matmul
+ * precision, Ci and Co multiples of 8, 16-B aligned tensors: the 16-bit operand path).  fwd16
+ * rounds x into x16 (N*H*W*Ci 16-bit elements, 16-B aligned, caller storage) and sets
+ * *x16_written = 1 when that path ran, else 0 (x16 untouched); bwd16 gathers from that copy instead
+ * of rounding x again (x16 null: as srk_conv2d_nhwc_bwd).  The backward must run at the forward's
+ * precision.  Bitwise the results of the plain pair.                                          */
+int srk_conv2d_nhwc_fwd16(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w,
+                          const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh,
+                          int64_t sw, float* y, float* ws, void* x16, int* x16_written, void* stream);
+int srk_conv2d_nhwc_bwd16(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co,
+                          int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw, const float* dy,
+                          float* dx, float* dw, float* db, float* ws, const void* x16, void* stream);
 /* Max pooling, window = stride = (kh, kw), floor mode, channels-last (nn.MaxPool2d((1,3)),
  * ((1,4)) and nn.MaxPool1d(98), model_fbanks_cnn.py:73,75,78).  Backward routes each gradient to
  * the first maximum of its window, as PyTorch does.                                          */

@@ -52,6 +52,10 @@ _SIGS = {
                             _P],
     "srk_conv2d_nhwc_bwd": [_P, _I64, _I64, _I64, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P,
                             _P, _P, _P],
+    "srk_conv2d_nhwc_fwd16": [_P, _I64, _I64, _I64, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P,
+                              _P, ctypes.POINTER(_I), _P],
+    "srk_conv2d_nhwc_bwd16": [_P, _I64, _I64, _I64, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P,
+                              _P, _P, _P, _P],
     "srk_conv1_pool_workspace_floats": [_I64, _I64, _I64],
     "srk_conv1_pool_fwd": [_P, _I64, _I64, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P],
     "srk_conv1_pool_wgrad": [_P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P],

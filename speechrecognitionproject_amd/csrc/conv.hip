@@ -580,20 +580,26 @@ bool s16_ok(int prec, int64_t Ci, int64_t Co, std::initializer_list<const void*>
   return true;
 }
 
-// rounds cnt fp32 tensors (n[i] % 8 == 0 elements each) into one 16-bit scratch allocation, on s
-int to16_all(int prec, const float* const* src, const int64_t* n, int cnt, unsigned short** dst, hipStream_t s) {
+// rounds cnt fp32 tensors (n[i] % 8 == 0 elements each) into 16-bit copies, on s.  dst[i] null on
+// entry: a slice of one scratch allocation; preset: caller storage, converted into unless ready[i]
+// (it already holds this tensor's copy, e.g. the one srk_conv2d_nhwc_fwd16 kept for the backward).
+int to16_all(int prec, const float* const* src, const int64_t* n, int cnt, unsigned short** dst, hipStream_t s,
+             const bool* ready = nullptr) {
   size_t off[4], total = 0;
   double bytes = 0;
   for (int i = 0; i < cnt; ++i) {
     off[i] = total;
-    total += (size_t)((n[i] + 63) / 64 * 64);
-    bytes += 6.0 * (double)n[i];
+    if (!dst[i]) total += (size_t)((n[i] + 63) / 64 * 64);
+    if (!(ready && ready[i])) bytes += 6.0 * (double)n[i];
   }
   float* base = nullptr;
-  if (int rc = conv_scratch((total + 1) / 2, &base, g_cs16)) return rc;
+  if (total) {
+    if (int rc = conv_scratch((total + 1) / 2, &base, g_cs16)) return rc;
+  }
   ProfScope prof("conv_to16", s, bytes);
   for (int i = 0; i < cnt; ++i) {
-    dst[i] = reinterpret_cast<unsigned short*>(base) + off[i];
+    if (ready && ready[i]) continue;
+    if (!dst[i]) dst[i] = reinterpret_cast<unsigned short*>(base) + off[i];
     const int64_t n8 = n[i] / 8;
     SRK_REQUIRE(n[i] % 8 == 0 && (n8 + 255) / 256 < INT32_MAX, SRK_ERR_INTERNAL, "conv: bad 16-bit source size");
     const dim3 grid((unsigned)((n8 + 255) / 256));
@@ -701,7 +707,14 @@ int64_t srk_conv2d_workspace_floats(int64_t Ci, int64_t Co, int64_t KH, int64_t 
 int srk_conv2d_nhwc_fwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w,
                         const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh,
                         int64_t sw, float* y, float* ws, void* stream) {
+  return srk_conv2d_nhwc_fwd16(x, N, H, W, Ci, w, bias, Co, KH, KW, ph, pw, sh, sw, y, ws, nullptr, nullptr, stream);
+}
+
+int srk_conv2d_nhwc_fwd16(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w,
+                          const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh,
+                          int64_t sw, float* y, float* ws, void* x16, int* x16_written, void* stream) {
   SRK_API_BEGIN
+  if (x16_written) *x16_written = 0;
   int64_t Ho, Wo;
   if (int rc = srk::check(N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw, &Ho, &Wo)) return rc;
   SRK_REQUIRE(x && w && y && ws, SRK_ERR_INVALID, "conv fwd: null pointer");
@@ -715,13 +728,14 @@ int srk_conv2d_nhwc_fwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t
   c.x = x; c.wmat = ws; c.out = y; c.bias = bias;
   c.M = N * Ho * Wo; c.Nn = Co; c.K = KH * KW * Ci;
   const int prec = srk::matmul_prec();
-  if (srk::s16_ok(prec, Ci, Co, {x, ws})) {
+  if (srk::s16_ok(prec, Ci, Co, {x, ws, x16})) {
     const float* src[2] = {x, ws};
     const int64_t n[2] = {N * H * W * Ci, nw};
-    unsigned short* d16[2];
+    unsigned short* d16[2] = {static_cast<unsigned short*>(x16), nullptr};   // x16: the caller keeps x's copy
     if (int rc = srk::to16_all(prec, src, n, 2, d16, s)) return rc;
     c.a16 = d16[0];
     c.b16 = d16[1];
+    if (x16 && x16_written) *x16_written = 1;
   }
   return srk::run_conv_gemm<srk::kFwd>(c, s, "conv_fwd");
   SRK_API_END
@@ -730,6 +744,12 @@ int srk_conv2d_nhwc_fwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t
 int srk_conv2d_nhwc_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co,
                         int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw, const float* dy,
                         float* dx, float* dw, float* db, float* ws, void* stream) {
+  return srk_conv2d_nhwc_bwd16(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, sh, sw, dy, dx, dw, db, ws, nullptr, stream);
+}
+
+int srk_conv2d_nhwc_bwd16(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co,
+                          int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw, const float* dy,
+                          float* dx, float* dw, float* db, float* ws, const void* x16, void* stream) {
   SRK_API_BEGIN
   int64_t Ho, Wo;
   if (int rc = srk::check(N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw, &Ho, &Wo)) return rc;
@@ -749,10 +769,12 @@ int srk_conv2d_nhwc_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t
   // 16-bit sources: x and dY serve both GEMMs, Wd the data gradient (one scratch allocation)
   unsigned short* d16[3] = {nullptr, nullptr, nullptr};   // x, dY, Wd
   const int prec = srk::matmul_prec();
-  if (srk::s16_ok(prec, Ci, Co, {x, dy, ws})) {
+  if (srk::s16_ok(prec, Ci, Co, {x, dy, ws, x16})) {
     const float* src[3] = {x, dy, ws};
     const int64_t n[3] = {N * H * W * Ci, N * Ho * Wo * Co, nw};
-    if ((rc = srk::to16_all(prec, src, n, dgrad_implicit ? 3 : 2, d16, s))) return rc;
+    const bool ready[3] = {x16 != nullptr, false, false};   // x16: the forward's copy of x
+    d16[0] = const_cast<unsigned short*>(static_cast<const unsigned short*>(x16));
+    if ((rc = srk::to16_all(prec, src, n, dgrad_implicit ? 3 : 2, d16, s, ready))) return rc;
   }
   if (dx && full_width) {
     // A full-width "valid" conv (model_fbanks_cnn.py:74, conv3 1x10 on width 10): every input

@@ -5,6 +5,8 @@ torch's, so reference ``state_dict`` checkpoints load unchanged
 Every forward/backward runs a HIP kernel through the C ABI; there is no CPU or torch-kernel
 fallback (the GPU and the library are required).
 """
+import ctypes
+
 import torch
 import torch.nn as tnn
 
@@ -287,8 +289,16 @@ class _Conv2dNHWCFn(torch.autograd.Function):
         Ho, Wo = (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
         y = torch.empty((N, Ho, Wo, Co), device=x.device)
         ws = torch.empty(int(_lib.lib().srk_conv2d_workspace_floats(Ci, Co, KH, KW)), device=x.device)
-        call("srk_conv2d_nhwc_fwd", ptr(x), N, H, W, Ci, ptr(w), ptr(b) if b is not None else None, Co, KH, KW,
-             ph, pw, sh, sw, ptr(y), ptr(ws), stream_ptr())
+        # 16-bit matmul precision with 8-aligned channels: keep the forward's 16-bit copy of x for the
+        # backward's gathers (srk_conv2d_nhwc_fwd16; the library reports whether it wrote it)
+        x16, written = None, ctypes.c_int(0)
+        if _lib.matmul_precision() != "fp32" and Ci % 8 == 0 and Co % 8 == 0 and ctx.needs_input_grad[1]:
+            x16 = torch.empty(x.numel(), device=x.device, dtype=torch.int16)
+        call("srk_conv2d_nhwc_fwd16", ptr(x), N, H, W, Ci, ptr(w), ptr(b) if b is not None else None, Co, KH, KW,
+             ph, pw, sh, sw, ptr(y), ptr(ws), ptr(x16) if x16 is not None else None, ctypes.byref(written),
+             stream_ptr())
+        ctx.x16 = x16 if written.value else None
+        ctx.prec = _lib.matmul_precision()
         ctx.save_for_backward(x, w)
         ctx.geom = (padding, stride, b is not None)
         return y
@@ -304,8 +314,11 @@ class _Conv2dNHWCFn(torch.autograd.Function):
         dw = torch.empty_like(w)
         db = torch.empty((Co,), device=x.device) if has_b else None
         ws = torch.empty(int(_lib.lib().srk_conv2d_workspace_floats(Ci, Co, KH, KW)), device=x.device)
-        call("srk_conv2d_nhwc_bwd", ptr(x), N, H, W, Ci, ptr(w), Co, KH, KW, ph, pw, sh, sw, ptr(dy),
-             ptr(dx) if dx is not None else None, ptr(dw), ptr(db) if db is not None else None, ptr(ws), stream_ptr())
+        x16 = ctx.x16 if ctx.prec == _lib.matmul_precision() else None   # a copy in this precision only
+        ctx.x16 = None
+        call("srk_conv2d_nhwc_bwd16", ptr(x), N, H, W, Ci, ptr(w), Co, KH, KW, ph, pw, sh, sw, ptr(dy),
+             ptr(dx) if dx is not None else None, ptr(dw), ptr(db) if db is not None else None, ptr(ws),
+             ptr(x16) if x16 is not None else None, stream_ptr())
         return dx, dw, db, None, None
 
 

@@ -320,6 +320,43 @@ def test_conv_16bit_sources_bit_identical(prec, shape):
         assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize("shape", CONV_S16[:4])
+def test_conv_kept_16bit_copy_matches_plain_abi(prec, shape):
+    """srk_conv2d_nhwc_fwd16 / bwd16 (the autograd path: the forward's 16-bit copy of x kept for the
+    backward) == the plain srk_conv2d_nhwc_fwd / bwd pair called through the C ABI, bitwise; the
+    backward rounds only dY (and the weights) once the copy is kept."""
+    import ctypes
+    N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw = shape
+    g = torch.Generator().manual_seed(N * 7 + Ci + KH)
+    x = torch.randn(N, H, W, Ci, generator=g).cuda()
+    w = (torch.randn(Co, Ci, KH, KW, generator=g) / (Ci * KH * KW) ** 0.5).cuda()
+    Ho, Wo = (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
+    dy = torch.randn(N, Ho, Wo, Co, generator=g).cuda()
+    ws = torch.empty(Ci * Co * KH * KW, device="cuda")
+    y0, dx0, dw0 = torch.empty_like(dy), torch.empty_like(x), torch.empty_like(w)
+    call("srk_conv2d_nhwc_fwd", ptr(x), N, H, W, Ci, ptr(w), None, Co, KH, KW, ph, pw, sh, sw, ptr(y0), ptr(ws),
+         stream_ptr())
+    call("srk_conv2d_nhwc_bwd", ptr(x), N, H, W, Ci, ptr(w), Co, KH, KW, ph, pw, sh, sw, ptr(dy), ptr(dx0), ptr(dw0),
+         None, ptr(ws), stream_ptr())
+    x16 = torch.empty(x.numel(), device="cuda", dtype=torch.int16)
+    written = ctypes.c_int(-1)
+    y1, dx1, dw1 = torch.empty_like(dy), torch.empty_like(x), torch.empty_like(w)
+    call("srk_conv2d_nhwc_fwd16", ptr(x), N, H, W, Ci, ptr(w), None, Co, KH, KW, ph, pw, sh, sw, ptr(y1), ptr(ws),
+         ptr(x16), ctypes.byref(written), stream_ptr())
+    assert written.value == 1
+    x16_expect = x.reshape(-1).to(TORCH_DT[prec]).view(torch.int16)
+    assert torch.equal(x16, x16_expect)   # round-to-nearest-even, as torch's cast
+    _lib.prof_enable(1)
+    call("srk_conv2d_nhwc_bwd16", ptr(x), N, H, W, Ci, ptr(w), Co, KH, KW, ph, pw, sh, sw, ptr(dy), ptr(dx1),
+         ptr(dw1), None, ptr(ws), ptr(x16), stream_ptr())
+    torch.cuda.synchronize()
+    bytes_to16 = _lib.prof_read("conv_to16")[2]
+    _lib.prof_enable(0)
+    assert bytes_to16 == 6.0 * (dy.numel() + w.numel())   # dY and the dgrad weights; x not again
+    for a, b in ((y0, y1), (dx0, dx1), (dw0, dw1)):
+        assert torch.equal(a, b)
+
+
 # ----------------------------------------------------------------------------- 16-bit operands in memory
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(8, 8, 8), (40, 24, 72), (136, 264, 200), (304, 128, 1024), (256, 128, 8192),

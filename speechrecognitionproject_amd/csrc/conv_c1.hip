@@ -25,7 +25,9 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 constexpr int kCo = 64;              // output channels (model_fbanks_cnn.py:72)
 constexpr int kC4 = kCo / 4;         // threads per pixel group (4 channels each)
 constexpr int kPG = 256 / kC4;       // pixel groups per block
-constexpr int kRows = 2;             // image rows per block (per grid-stride step)
+constexpr int kRows = 2;             // image rows per block (forward)
+constexpr int kRowsW = 8;            // image rows per grid-stride step of the weight gradient: the
+                                     // (KH - 1)-row halo and the two barriers amortised over 4x the rows
 constexpr int kWgradBlocks = 1024;   // persistent blocks of the backward (partials: 5.8 MB)
 
 struct C1Args {
@@ -42,9 +44,9 @@ struct C1Args {
 __device__ __forceinline__ bool takes(float v, float m, bool first) { return first || v > m || (v != v && m == m); }
 
 // x rows [h0 - ph, h0 + kRows - 1 + KH - 1 - ph], cols [-pw, W - 1 + KW - 1 - pw] -> LDS, zero padded
-template <int KH, int KW>
+template <int KH, int KW, int ROWS = kRows>
 __device__ __forceinline__ void load_patch(const C1Args& a, int n, int h0, float* patch, int pitch) {
-  constexpr int PR = kRows + KH - 1;
+  constexpr int PR = ROWS + KH - 1;
   const int PC = a.W + KW - 1;
   for (int i = threadIdx.x; i < PR * PC; i += 256) {
     const int r = i / PC, cidx = i % PC;
@@ -108,18 +110,18 @@ __global__ __launch_bounds__(256) void conv1_pool_wgrad_kernel(C1Args a) {
   float* patch = smem;
   const int pitch = a.W + KW - 1 + 1;
   const int c4 = threadIdx.x % kC4, pg = threadIdx.x / kC4;
-  const int hp = (a.H + kRows - 1) / kRows;
+  const int hp = (a.H + kRowsW - 1) / kRowsW;
   const int Wq = a.W / PW;
   v4f acc[T];
 #pragma unroll
   for (int t = 0; t < T; ++t) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
   v4f dbacc = {0.f, 0.f, 0.f, 0.f};
   for (int blk = blockIdx.x; blk < a.N * hp; blk += gridDim.x) {
-    const int n = blk / hp, h0 = (blk % hp) * kRows;
+    const int n = blk / hp, h0 = (blk % hp) * kRowsW;
     __syncthreads();   // previous patch fully consumed
-    load_patch<KH, KW>(a, n, h0, patch, pitch);
+    load_patch<KH, KW, kRowsW>(a, n, h0, patch, pitch);
     __syncthreads();
-    const int rows = min(kRows, a.H - h0);
+    const int rows = min(kRowsW, a.H - h0);
     for (int wi = pg; wi < rows * Wq; wi += kPG) {
       const int r = wi / Wq, wq = wi % Wq;
       const size_t o = (((size_t)n * a.H + h0 + r) * Wq + wq) * kCo + c4 * 4;
@@ -234,9 +236,9 @@ int srk_conv1_pool_wgrad(const float* x, int64_t N, int64_t H, int64_t W, int64_
   a.x = x; a.dy = dy; a.arg = const_cast<uint8_t*>(argmax); a.partial = ws;
   hipStream_t s = srk::as_stream(stream);
   const int T = (int)(KH * KW);
-  const int hp = (int)((H + srk::kRows - 1) / srk::kRows);
+  const int hp = (int)((H + srk::kRowsW - 1) / srk::kRowsW);
   const int blocks = (int)std::min<int64_t>(srk::kWgradBlocks, N * hp);
-  const size_t patch = (size_t)(srk::kRows + KH - 1) * (W + KW) * 4;
+  const size_t patch = (size_t)(srk::kRowsW + KH - 1) * (W + KW) * 4;
   const size_t red = (size_t)4 * srk::kC4 * (T + 1) * 4 * 4;
   srk::ProfScope prof("conv1_pool_wgrad", s, 4.0 * N * H * W + 5.0 * N * H * (W / pool) * Co);
   if (KH == 7)

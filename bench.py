@@ -181,11 +181,12 @@ def cpu_baseline(model_name, batch, seconds):
                                "semantics) on 32 x 1-s clips, serial, %.4f s per pass (mean of %d)" % (el_mfcc, reps)}}
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, model="mfcc_bgru"):
     """HBM bytes per launch of `kernel` from the committed PMC summary of the same bench command
-    (tools/pmc_traffic.py over separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected),
-    or None if no summary is committed."""
-    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    (tools/pmc_traffic.py over separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected):
+    profiles/pmc_traffic.json for the default cfg2 command, pmc_traffic_<model>.json for
+    `--model <model>`; None if no summary is committed."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json" if model == "mfcc_bgru" else "pmc_traffic_%s.json" % model)
     try:
         with open(p) as f:
             v = json.load(f)["bytes_per_launch"].get(kernel)
@@ -396,7 +397,7 @@ def main():
         peak = PEAK_LP_MFMA_TFLOPS if dom in LP_KERNELS else PEAK_FP32_MFMA_TFLOPS
         return {"bound": "mfma", "kernel": dom, "achieved": round(tf, 2), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(tf / peak, 4),
-                "traffic": pmc_traffic(dom) if traffic_ok else None, "traffic_unit": "bytes/launch",
+                "traffic": pmc_traffic(dom, args.model) if traffic_ok else None, "traffic_unit": "bytes/launch",
                 "avg_launch_ms": round(k["ms_total"] / k["launches"], 5),
                 "flops_per_launch": k["work"] / k["launches"]}
 
@@ -407,7 +408,7 @@ def main():
         lp_el, lp_kernels, lp_loss = timed("bf16")
         lp = {"dtype": "bf16", "value": round(world * B * args.steps / lp_el, 2),
               "ms_per_step": round(lp_el / args.steps * 1e3, 3), "final_loss": round(lp_loss, 5),
-              "roofline": roofline(lp_kernels, args.model == "mfcc_bgru"),   # same default command's PMC
+              "roofline": roofline(lp_kernels, True),   # the PMC summary of the same command, if committed
               "kernels": {k: {"launches": v["launches"], "ms_total": v["ms_total"]} for k, v in lp_kernels.items()}}
         _lib.set_matmul_precision(args.precision)
 
@@ -416,7 +417,7 @@ def main():
     if rank != 0:
         return
     value = world * B * args.steps / el
-    roof = roofline(kernels, args.model == "mfcc_bgru" and args.precision == "fp32")
+    roof = roofline(kernels, True)
     res = {
         "metric": "utterances/sec (1 s @16 kHz) MFCC+CNN-BiGRU train step",
         "value": round(value, 2), "unit": "utt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

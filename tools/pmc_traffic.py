@@ -1,6 +1,8 @@
 """Per-launch HBM traffic of the bench kernels from rocprofv3 PMC passes -> profiles/pmc_traffic.json.
 
     python tools/pmc_traffic.py FETCH_DIR WRITE_DIR [-o profiles/pmc_traffic.json]
+    (bench.py reads profiles/pmc_traffic.json for the default cfg2 command and
+    profiles/pmc_traffic_<model>.json for `bench.py --model <model>`)
 
 FETCH_SIZE / WRITE_SIZE come from two separate `rocprofv3 --kernel-trace --pmc ...` runs of the same
 bench command.  Corrections per MI355X_MICROARCH.md (HBM section, gfx950): FETCH_SIZE (KiB) x 2
@@ -12,6 +14,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import sqlite3
 
 GROUPS = {  # srk_prof name -> substrings of the rocprof kernel symbols it covers
@@ -21,9 +24,17 @@ GROUPS = {  # srk_prof name -> substrings of the rocprof kernel symbols it cover
     "gru_bwd_seq_lp": ("gru_bwd_persistent_lp_kernel", "gru_bwd_persistent_lp2_kernel"),
     "gru_fwd_step": ("gru_fwd_step_kernel",), "gru_bwd_step": ("gru_bwd_step_kernel",),
     "mfcc": ("mfcc3_kernel", "mfcc2_kernel"), "fbank": ("fbank_kernel",), "spec": ("spec_kernel",),
-    "conv_fwd": ("conv_gemm_kernel<0",), "conv_dgrad": ("conv_gemm_kernel<1",), "conv_wgrad": ("conv_gemm_kernel<2",),
+    "conv_fwd": (), "conv_dgrad": (), "conv_wgrad": (), "conv_fwd_lp": (), "conv_dgrad_lp": (), "conv_wgrad_lp": (),
     "adam": ("adam_kernel",), "noise_mix": ("noise_mix_kernel",),
 }
+
+
+def _conv_group(name):
+    """conv_gemm_kernel<MODE, BM, BN, BK, VEC, VECB, LP, S16>: MODE 0/1/2 = fwd/dgrad/wgrad, LP != 0 = 16-bit."""
+    m = re.search(r"conv_gemm_kernel<(\d+),[^,]*,[^,]*,[^,]*,[^,]*,[^,]*,\s*(\d+)", name)
+    if not m:
+        return None
+    return ("conv_fwd", "conv_dgrad", "conv_wgrad")[int(m.group(1))] + ("_lp" if m.group(2) != "0" else "")
 
 
 def collect(d, counter):
@@ -32,8 +43,9 @@ def collect(d, counter):
     out = {}
     for name, n, tot in c.execute("select kernel_name, count(*), sum(value) from counters_collection where "
                                   "counter_name = ? group by kernel_name", (counter,)):
+        cg = _conv_group(name)
         for g, subs in GROUPS.items():
-            if any(sub in name for sub in subs):
+            if (g == cg) if cg else any(sub in name for sub in subs):
                 a = out.setdefault(g, [0, 0.0])
                 a[0] += n
                 a[1] += tot

@@ -34,6 +34,21 @@ matrix-core operand precision (srk_set_option "matmul_precision"; fp16 adds a st
 With fp32, the same line also carries "bf16": the identical step re-timed with bf16 operands
 (BASELINE.json names bf16 for cfg2), with its own roofline against the dense bf16 peak.
 
+Step execution: after W warm-up steps the train step is captured once into a HIP graph
+(speechrecognitionproject_amd/graphs.py; per-step host values — the Adam step count and the dropout
+seed — live on the device) and the K timed steps are graph replays, each preceded by a device copy of
+that step's pre-staged batch into the graph's static input.  N > 1: forward + backward are one graph,
+the flat gradient buffer is all-reduced over RCCL between the replay and the Adam launch.
+--no-graph times the eager step instead (N > 1: bucketed all-reduces overlapped with backward).
+The per-kernel HIP-event timers cannot run inside a graph: kernel times ("kernels", "roofline")
+come from a separate eager pass of the same step (--prof-steps, default 5), reported with its own
+"eager_ms_per_step".
+
+Default run (no --model): the cfg2 headline, then compact records under "configs" for BASELINE.json's
+other configs at their per-GPU batch — cfg3 fbanks_cnn fp32 512, cfg4 resnet_bgru fp32 512, cfg5
+spec_bgru fp16 512 with the noise-mix in the step — each with value / ms_per_step / roofline
+(--no-configs skips them).
+
 Measurement extras on the same line:
   roofline     — the dominant kernel of the timed steps, timed live with HIP events on its launch
                  stream (srk_prof_*), algorithmic flops / avg launch time vs the MFMA peak of its
@@ -181,18 +196,22 @@ def cpu_baseline(model_name, batch, seconds):
                                "semantics) on 32 x 1-s clips, serial, %.4f s per pass (mean of %d)" % (el_mfcc, reps)}}
 
 
-def pmc_traffic(kernel, model="mfcc_bgru"):
-    """HBM bytes per launch of `kernel` from the committed PMC summary of the same bench command
-    (tools/pmc_traffic.py over separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected):
-    profiles/pmc_traffic.json for the default cfg2 command, pmc_traffic_<model>.json for
-    `--model <model>`; None if no summary is committed."""
-    p = os.path.join(REPO, "profiles", "pmc_traffic.json" if model == "mfcc_bgru" else "pmc_traffic_%s.json" % model)
+def pmc_traffic(kernel, cmd):
+    """HBM bytes per launch of the kernel category `kernel` from the committed PMC summary of THIS
+    command (tools/pmc_traffic.py over separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes,
+    gfx950-corrected): profiles/pmc_traffic_<model>.json, used only when the command it records
+    (model, per-GPU batch, world size, precisions, options) matches `cmd`; otherwise None."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic_%s.json" % cmd["model"])
     try:
         with open(p) as f:
-            v = json.load(f)["bytes_per_launch"].get(kernel)
-        return None if v is None else v["total"]
-    except (OSError, ValueError, KeyError):
+            doc = json.load(f)
+    except (OSError, ValueError):
         return None
+    rec = doc.get("command") or {}
+    same = (rec.get("model") == cmd["model"] and rec.get("batch") == cmd["batch"] and rec.get("world") == cmd["world"]
+            and cmd["precision"] in rec.get("precisions", ()) and bool(rec.get("sync_bn")) == cmd["sync_bn"])
+    v = doc.get("bytes_per_launch", {}).get(kernel) if same else None
+    return None if v is None else v["total"]
 
 
 def feature_roofline(model_name, n_clips=65536):
@@ -263,13 +282,207 @@ def plumbing(args, rank, world):
               flush=True)
 
 
+EXTRA_CONFIGS = (  # BASELINE.json configs[2..4] at their per-GPU batch (the default run appends them)
+    ("cfg3", "fbanks_cnn", "fp32", 512, 10),
+    ("cfg4", "resnet_bgru", "fp32", 512, 4),
+    ("cfg5", "spec_bgru", "fp16", 512, 20),
+)
+
+
+class Workload:
+    """One model's train step on this rank (per-GPU batch B, `pool` distinct pre-staged batches),
+    timed eagerly or as HIP-graph replays; the rank-0 JSON line is built from run()."""
+
+    def __init__(self, args, model_name, B, rank, world, dev):
+        self.args, self.name, self.B, self.rank, self.world, self.dev = args, model_name, B, rank, world, dev
+        torch.manual_seed(0)
+        model = build_model(model_name).to(dev)
+        if args.sync_bn:
+            from speechrecognitionproject_amd.nn import convert_sync_batchnorm
+            model = convert_sync_batchnorm(model)
+        self.model = model
+        self.flat = FlatParams(model.parameters())
+        self.opt = Adam(model.parameters(), lr=1e-4, flat=self.flat)
+        parallel.broadcast_flat(self.flat)
+        self.reducer = None
+        self.crit = CrossEntropyLoss()
+        self.loss_scale = 1.0
+        pool = args.pool
+        x, y = synthetic_clips(pool * B, seed=1000 + rank, clip=30000 if model_name == "spec_bgru" else 32767)
+        self.lab = torch.from_numpy(y).to(dev).view(pool, B)
+        self.static_lab = self.lab[0].clone()
+        if model_name == "spec_bgru":
+            # cfg5: int16 PCM + resident noise bank; the per-clip (file, offset, gain) draws of
+            # dataset.py:190-193 are made up front (numpy), the mix runs on the device every step.
+            from speechrecognitionproject_amd.synthetic import synthetic_noise_bank, synthetic_noise_draws
+            self.pcm16 = torch.from_numpy(x.astype(np.int16)).to(dev).view(pool, B, -1)
+            self.bank = torch.from_numpy(synthetic_noise_bank()).to(dev)
+            self.draws = [torch.from_numpy(a).to(dev).view(pool, B) for a in synthetic_noise_draws(pool * B, seed=2 + rank)]
+            self.mixed = torch.empty((B, 16000), device=dev)
+            self.static = [self.pcm16[0].clone()] + [d[0].clone() for d in self.draws]
+        else:
+            self.pcm = torch.from_numpy(x).to(dev).view(pool, B, -1)
+            self.static = [self.pcm[0].clone()]
+
+    # ---- inputs
+    def _inputs(self, srcs):
+        if self.name == "spec_bgru":
+            return features.noise_mix(srcs[0], self.bank, srcs[1], srcs[2], srcs[3], out=self.mixed)
+        return srcs[0]
+
+    def _batch(self, i):
+        j = i % self.args.pool
+        if self.name == "spec_bgru":
+            return [self.pcm16[j]] + [d[j] for d in self.draws]
+        return [self.pcm[j]]
+
+    def _feed(self, i):
+        """Copy step i's pre-staged batch into the graph's static inputs (device to device)."""
+        for dst, src in zip(self.static, self._batch(i)):
+            dst.copy_(src, non_blocking=True)
+        self.static_lab.copy_(self.lab[i % self.args.pool], non_blocking=True)
+
+    # ---- the step
+    def _fwd_bwd(self, srcs, lab):
+        self.opt.zero_grad()
+        if self.reducer is not None:
+            self.reducer.begin()
+        out = self.model(self._inputs(srcs))
+        loss = self.crit(out, lab)
+        (loss * self.loss_scale if self.loss_scale != 1.0 else loss).backward()
+        return loss
+
+    def _exchange_and_update(self):
+        if self.reducer is not None:
+            self.reducer.finish()        # bucketed all-reduces launched during backward
+        else:
+            parallel.allreduce_grads(self.flat)
+        self.opt.step()
+
+    def eager_step(self, i):
+        loss = self._fwd_bwd(self._batch(i), self.lab[i % self.args.pool])
+        self._exchange_and_update()
+        return loss
+
+    def _graph_body(self):
+        loss = self._fwd_bwd(self.static, self.static_lab)
+        if self.world == 1:
+            self.opt.step()
+        return loss
+
+    def run(self, precision, steps, warmup, graph):
+        """W warm-up + K timed steps at one matrix precision -> record dict (rank 0 uses it)."""
+        args = self.args
+        log("bench: %s %s B=%d, %d warm-up + %d timed steps%s" % (self.name, precision, self.B, warmup, steps,
+                                                                   " (HIP graph)" if graph else ""))
+        _lib.set_matmul_precision(precision)
+        self.loss_scale = FP16_LOSS_SCALE if precision == "fp16" else 1.0
+        self.opt.grad_scale = 1.0 / (self.world * self.loss_scale)
+        self.reducer = (parallel.GradReducer(self.flat, bucket_mb=args.bucket_mb)
+                        if (self.world > 1 and args.overlap and not graph) else None)
+        g = None
+        if graph:
+            from speechrecognitionproject_amd.graphs import GraphedStep
+            self._feed(0)
+            g = GraphedStep(self._graph_body, warmup=max(2, warmup))
+            loss = g.out
+        else:
+            for i in range(warmup):
+                loss = self.eager_step(i)
+        torch.cuda.synchronize()
+        if not torch.isfinite(loss).item():
+            raise SystemExit("non-finite loss during warm-up")
+        if self.world > 1:
+            torch.distributed.barrier()
+        prof = not args.no_prof and not graph
+        if prof:
+            _lib.prof_enable(True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            if g is not None:
+                self._feed(i)
+                loss = g.replay()
+                if self.world > 1:
+                    self._exchange_and_update()
+            else:
+                loss = self.eager_step(i)
+        torch.cuda.synchronize()
+        if self.world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - t0
+        if self.world > 1:
+            t = torch.tensor([el], device=self.dev, dtype=torch.float64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        final_loss = float(loss.item())
+        if g is not None:
+            g.release()
+            del g
+        eager_ms = None
+        if not args.no_prof and graph:
+            # kernel timers cannot run inside a graph: an eager pass of the same step, timed per kernel
+            self.reducer = None
+            _lib.prof_enable(True)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for i in range(args.prof_steps):
+                self.eager_step(i)
+            torch.cuda.synchronize()
+            eager_ms = (time.perf_counter() - t1) / args.prof_steps * 1e3
+            prof = True
+        kernels, singles = {}, []
+        if prof:
+            for name in MATRIX_KERNELS + OTHER_KERNELS:
+                c, ms, w = _lib.prof_read(name)
+                if c:
+                    kernels[name] = {"launches": c, "ms_total": round(ms, 3), "work": w}
+            singles = _lib.prof_kernels()
+            _lib.prof_enable(False)
+        torch.cuda.empty_cache()
+        cmd = {"model": self.name, "batch": self.B, "world": self.world, "precision": precision,
+               "sync_bn": bool(args.sync_bn)}
+        return {"el": el, "steps": steps, "warmup": warmup, "graph": bool(graph), "final_loss": final_loss,
+                "kernels": kernels, "roofline": roofline(kernels, singles, cmd), "eager_ms": eager_ms,
+                "prof_steps": args.prof_steps if (graph and prof) else steps}
+
+
+def roofline(kernels, singles, cmd):
+    """The dominant matrix-core kernel CATEGORY of the profiled steps (e.g. gemm_f32 = every fp32 GEMM
+    launch) — achieved algorithmic TFLOP/s over its launches vs the MFMA peak of its operand type —
+    plus the largest SINGLE kernel (one kernel template at one shape) and the top 5 by time."""
+    mm = {k: v for k, v in kernels.items() if k in MATRIX_KERNELS}
+    if not mm:
+        return None
+    dom = max(mm, key=lambda k: mm[k]["ms_total"])
+    k = mm[dom]
+    tf = k["work"] / (k["ms_total"] * 1e-3) / 1e12
+    peak = PEAK_LP_MFMA_TFLOPS if dom in LP_KERNELS else PEAK_FP32_MFMA_TFLOPS
+    res = {"bound": "mfma", "kernel": dom, "achieved": round(tf, 2), "peak": peak,
+           "unit": "TFLOP/s", "frac": round(tf / peak, 4),
+           "traffic": pmc_traffic(dom, cmd), "traffic_unit": "bytes/launch",
+           "avg_launch_ms": round(k["ms_total"] / k["launches"], 5),
+           "flops_per_launch": k["work"] / k["launches"]}
+    mat = [r for r in singles if r["name"] in MATRIX_KERNELS and r["work"] > 0]
+    if mat:
+        big = max(mat, key=lambda r: r["ms_total"])
+        btf = big["work"] / (big["ms_total"] * 1e-3) / 1e12
+        bpeak = PEAK_LP_MFMA_TFLOPS if big["name"] in LP_KERNELS else PEAK_FP32_MFMA_TFLOPS
+        res["largest_kernel"] = {"kernel": big["kernel"], "category": big["name"], "launches": big["launches"],
+                                 "avg_launch_ms": round(big["ms_total"] / big["launches"], 5),
+                                 "achieved": round(btf, 2), "peak": bpeak, "frac": round(btf / bpeak, 4)}
+    res["top_kernels"] = [{"kernel": r["kernel"], "launches": r["launches"], "ms_total": round(r["ms_total"], 3)}
+                          for r in sorted(singles, key=lambda r: -r["ms_total"])[:5]]
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None, help="clips per GPU per step (default per model)")
-    ap.add_argument("--model", default="mfcc_bgru")
+    ap.add_argument("--model", default=None, help="default: mfcc_bgru (cfg2) + the other configs under \"configs\"")
     ap.add_argument("--pool", type=int, default=4, help="distinct pre-staged batches per rank")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--precision", default="fp32", choices=sorted(_lib.PRECISIONS),
@@ -277,12 +490,17 @@ def main():
                          "operands with fp32 accumulation)")
     ap.add_argument("--no-lowprec", dest="lowprec", action="store_false",
                     help="skip the extra bf16 measurement reported under \"bf16\" on the same line")
+    ap.add_argument("--no-graph", dest="graph", action="store_false",
+                    help="time eager steps (one host launch per kernel) instead of HIP-graph replays")
+    ap.add_argument("--prof-steps", type=int, default=5, help="eager steps of the per-kernel timing pass (graph mode)")
+    ap.add_argument("--no-configs", dest="configs", action="store_false",
+                    help="skip the cfg3 / cfg4 / cfg5 records of the default run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true")
     ap.add_argument("--no-feature-roofline", "--no-mfcc-roofline", dest="no_feature_roofline", action="store_true")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
-                    help="N > 1: one blocking all-reduce after backward instead of bucketed all-reduces overlapped "
-                         "with it (parallel.GradReducer)")
+                    help="N > 1, eager: one blocking all-reduce after backward instead of bucketed all-reduces "
+                         "overlapped with it (parallel.GradReducer)")
     ap.add_argument("--bucket-mb", type=float, default=8.0, help="gradient bucket size of the overlapped all-reduce")
     ap.add_argument("--sync-bn", action="store_true",
                     help="BatchNorm statistics over the global batch of all ranks (SyncBatchNorm1d; resnet_bgru, "
@@ -290,6 +508,10 @@ def main():
     ap.add_argument("--cpu-plumbing", action="store_true",
                     help="exercise the N-rank launch / timing / JSON path over gloo on CPU (no GPU; no measurement)")
     args = ap.parse_args()
+    default_run = args.model is None
+    args.model = args.model or "mfcc_bgru"
+    if args.model not in DEFAULT_BATCH:
+        raise SystemExit("unknown --model %s" % args.model)
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_relaunch(args))
@@ -301,123 +523,35 @@ def main():
         return
     features.require_gpu()
     _lib.lib()
-    loss_scale = 1.0
     dev = torch.device("cuda", local)
-    torch.manual_seed(0)
-    model = build_model(args.model).to(dev)
-    if args.sync_bn:
-        from speechrecognitionproject_amd.nn import convert_sync_batchnorm
-        model = convert_sync_batchnorm(model)
-    flat = FlatParams(model.parameters())
-    opt = Adam(model.parameters(), lr=1e-4, flat=flat)
-    parallel.broadcast_flat(flat)
-    reducer = parallel.GradReducer(flat, bucket_mb=args.bucket_mb) if (world > 1 and args.overlap) else None
-    crit = CrossEntropyLoss()
-
+    torch.cuda.set_device(dev)
     B = args.batch or DEFAULT_BATCH[args.model]
-    x, y = synthetic_clips(args.pool * B, seed=1000 + rank, clip=30000 if args.model == "spec_bgru" else 32767)
-    lab = torch.from_numpy(y).to(dev).view(args.pool, B)
-    if args.model == "spec_bgru":
-        # cfg5: int16 PCM + resident noise bank; the per-clip (file, offset, gain) draws of
-        # dataset.py:190-193 are made up front (numpy), the mix runs on the device every step.
-        from speechrecognitionproject_amd.synthetic import synthetic_noise_bank, synthetic_noise_draws
-        pcm16 = torch.from_numpy(x.astype(np.int16)).to(dev).view(args.pool, B, -1)
-        bank = torch.from_numpy(synthetic_noise_bank()).to(dev)
-        draws = [torch.from_numpy(a).to(dev).view(args.pool, B)
-                 for a in synthetic_noise_draws(args.pool * B, seed=2 + rank)]
-        mixed = torch.empty((B, 16000), device=dev)
-
-        def inputs(i):
-            j = i % args.pool
-            return features.noise_mix(pcm16[j], bank, draws[0][j], draws[1][j], draws[2][j], out=mixed)
-    else:
-        pcm = torch.from_numpy(x).to(dev).view(args.pool, B, -1)
-
-        def inputs(i):
-            return pcm[i % args.pool]
-
-    def step(i):
-        opt.zero_grad()
-        if reducer is not None:
-            reducer.begin()
-        out = model(inputs(i))
-        loss = crit(out, lab[i % args.pool])
-        (loss * loss_scale if loss_scale != 1.0 else loss).backward()
-        if reducer is not None:
-            reducer.finish()        # bucketed all-reduces launched during backward
-        else:
-            parallel.allreduce_grads(flat)
-        opt.step()
-        return loss
-
-    def timed(precision):
-        """W warm-up + K timed steps at one matrix precision -> (seconds, kernel records, loss)."""
-        nonlocal loss_scale
-        log("bench: %s %s, %d warm-up + %d timed steps" % (args.model, precision, args.warmup, args.steps))
-        _lib.set_matmul_precision(precision)
-        loss_scale = FP16_LOSS_SCALE if precision == "fp16" else 1.0
-        opt.grad_scale = 1.0 / (world * loss_scale)
-        for i in range(args.warmup):
-            loss = step(i)
-        torch.cuda.synchronize()
-        if not torch.isfinite(loss).item():
-            raise SystemExit("non-finite loss during warm-up")
-        if world > 1:
-            torch.distributed.barrier()
-        if not args.no_prof:
-            _lib.prof_enable(True)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            loss = step(i)
-        torch.cuda.synchronize()
-        if world > 1:
-            torch.distributed.barrier()
-        el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el], device=dev, dtype=torch.float64)
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-            el = float(t.item())
-        kernels = {}
-        if not args.no_prof:
-            for name in MATRIX_KERNELS + OTHER_KERNELS:
-                c, ms, w = _lib.prof_read(name)
-                if c:
-                    kernels[name] = {"launches": c, "ms_total": round(ms, 3), "work": w}
-            _lib.prof_enable(False)
-        return el, kernels, float(loss.item())
-
-    def roofline(kernels, traffic_ok):
-        mm = {k: v for k, v in kernels.items() if k in MATRIX_KERNELS}
-        if not mm:
-            return None
-        dom = max(mm, key=lambda k: mm[k]["ms_total"])
-        k = mm[dom]
-        tf = k["work"] / (k["ms_total"] * 1e-3) / 1e12
-        peak = PEAK_LP_MFMA_TFLOPS if dom in LP_KERNELS else PEAK_FP32_MFMA_TFLOPS
-        return {"bound": "mfma", "kernel": dom, "achieved": round(tf, 2), "peak": peak,
-                "unit": "TFLOP/s", "frac": round(tf / peak, 4),
-                "traffic": pmc_traffic(dom, args.model) if traffic_ok else None, "traffic_unit": "bytes/launch",
-                "avg_launch_ms": round(k["ms_total"] / k["launches"], 5),
-                "flops_per_launch": k["work"] / k["launches"]}
-
-    el, kernels, final_loss = timed(args.precision)
+    wl = Workload(args, args.model, B, rank, world, dev)
+    main_rec = wl.run(args.precision, args.steps, args.warmup, args.graph)
     # the same step with 16-bit matrix-core operands (BASELINE.json cfg2 names bf16), same line
-    lp = None
+    lp_rec = None
     if args.lowprec and args.precision == "fp32":
-        lp_el, lp_kernels, lp_loss = timed("bf16")
-        lp = {"dtype": "bf16", "value": round(world * B * args.steps / lp_el, 2),
-              "ms_per_step": round(lp_el / args.steps * 1e3, 3), "final_loss": round(lp_loss, 5),
-              "roofline": roofline(lp_kernels, True),   # the PMC summary of the same command, if committed
-              "kernels": {k: {"launches": v["launches"], "ms_total": v["ms_total"]} for k, v in lp_kernels.items()}}
+        lp_rec = wl.run("bf16", args.steps, args.warmup, args.graph)
+        _lib.set_matmul_precision(args.precision)
+    del wl
+    extras = []
+    if default_run and args.configs:
+        for tag, name, prec, eb, esteps in EXTRA_CONFIGS:
+            w2 = Workload(args, name, eb, rank, world, dev)
+            rec = w2.run(prec, esteps, 2, args.graph)
+            rec.update(tag=tag, name=name, precision=prec, B=eb)
+            extras.append(rec)
+            del w2
+            torch.cuda.empty_cache()
         _lib.set_matmul_precision(args.precision)
 
     # a persistent kernel that timed out invalidates every number above: fail loudly
     _lib.check_health(sync=True)
     if rank != 0:
         return
+    el = main_rec["el"]
     value = world * B * args.steps / el
-    roof = roofline(kernels, True)
+    kern = lambda ks: {k: {"launches": v["launches"], "ms_total": v["ms_total"]} for k, v in ks.items()}
     res = {
         "metric": "utterances/sec (1 s @16 kHz) MFCC+CNN-BiGRU train step",
         "value": round(value, 2), "unit": "utt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -426,16 +560,35 @@ def main():
         "config": {"workload": "%s, CE, backward, Adam (full training.py step), per-GPU batch %d"
                                % (CFG[args.model], B), "model": args.model,
                    "global_batch": world * B, "clip_samples": 16000, "parallelism": "dp%d" % world,
-                   "allreduce": ("bucketed %.0f MB, overlapped with backward" % args.bucket_mb
-                                 if reducer is not None else ("one flat buffer after backward" if world > 1 else None)),
+                   "step_execution": ("HIP graph replay" + (" (forward + backward) + eager RCCL all-reduce + Adam"
+                                                            if world > 1 else " of the whole step")
+                                      if args.graph else "eager"),
+                   "allreduce": (None if world == 1 else "one flat buffer after backward" if (args.graph or not args.overlap)
+                                 else "bucketed %.0f MB, overlapped with backward" % args.bucket_mb),
                    "sync_bn": bool(args.sync_bn)},
         "model_tflops": round(value * TRAIN_GFLOP_PER_UTT.get(args.model, 0) / 1e3, 2),
-        "final_loss": round(final_loss, 5),
-        "roofline": roof,
-        "kernels": {k: {"launches": v["launches"], "ms_total": v["ms_total"]} for k, v in kernels.items()},
+        "final_loss": round(main_rec["final_loss"], 5),
+        "roofline": main_rec["roofline"],
+        "kernels": kern(main_rec["kernels"]),
+        "kernel_timing": ("eager pass of the same step, %d steps, HIP events on the launch stream; eager %.3f ms/step"
+                          % (main_rec["prof_steps"], main_rec["eager_ms"])) if main_rec["eager_ms"] else
+                         "the timed steps, HIP events on the launch stream",
     }
-    if lp is not None:
-        res["bf16"] = lp
+    if lp_rec is not None:
+        res["bf16"] = {"dtype": "bf16", "value": round(world * B * args.steps / lp_rec["el"], 2),
+                       "ms_per_step": round(lp_rec["el"] / args.steps * 1e3, 3),
+                       "eager_ms_per_step": round(lp_rec["eager_ms"], 3) if lp_rec["eager_ms"] else None,
+                       "final_loss": round(lp_rec["final_loss"], 5), "roofline": lp_rec["roofline"],
+                       "kernels": kern(lp_rec["kernels"])}
+    if main_rec["eager_ms"]:
+        res["eager_ms_per_step"] = round(main_rec["eager_ms"], 3)
+    if extras:
+        res["configs"] = [{"config": r["tag"], "workload": CFG[r["name"]], "model": r["name"], "dtype": r["precision"],
+                           "per_gpu_batch": r["B"], "global_batch": world * r["B"], "steps": r["steps"],
+                           "value": round(world * r["B"] * r["steps"] / r["el"], 2), "unit": "utt/s",
+                           "ms_per_step": round(r["el"] / r["steps"] * 1e3, 3),
+                           "eager_ms_per_step": round(r["eager_ms"], 3) if r["eager_ms"] else None,
+                           "final_loss": round(r["final_loss"], 5), "roofline": r["roofline"]} for r in extras]
     if not args.no_feature_roofline and args.model in FEATURE:
         log("bench: feature roofline")
         res["feature_roofline"] = feature_roofline(args.model)

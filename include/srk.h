@@ -43,8 +43,15 @@ int srk_init(int device);              /* build + upload constant tables on `dev
  * "noise_mix", "gemm_f32", "gru_fwd_step", "gru_bwd_step", "adam", ...), the elapsed time and
  * the launches' ALGORITHMIC work (flops for matrix kernels, bytes for streaming kernels).
  * srk_prof_enable synchronizes the device and clears previous records.                     */
+/* Generation of the library's grow-only scratch buffers (split-K slabs, conv / BatchNorm partials):
+ * it changes whenever one is reallocated, which invalidates any HIP graph captured before.         */
+int64_t srk_scratch_generation(void);
 int srk_prof_enable(int on);
 int srk_prof_read(const char* name, int64_t* count, double* total_ms, double* total_work);
+/* Every record since srk_prof_enable grouped by (name, launch detail: kernel template + shape), one
+ * "name\tdetail\tcount\ttotal_ms\ttotal_work\n" line each, NUL-terminated into buf (truncated at
+ * cap bytes); *needed = the full size.  bench.py names the largest single kernel with it. */
+int srk_prof_kernels(char* buf, int64_t cap, int64_t* needed);
 /* Runtime options: "gru_persistent" (default 1) = run each GRU layer's recurrence as ONE
  * persistent launch with W_hh resident in LDS (0 = one launch per time step);
  * "matmul_precision" (default 0) = operand precision of the matrix-core kernels (GEMM, GRU
@@ -277,9 +284,20 @@ int srk_cross_entropy(const float* logits, const int64_t* labels, int64_t B, int
  * step is the 1-based step count after increment; grad is multiplied by grad_scale first.   */
 int srk_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
                   float beta1, float beta2, float eps, int64_t step, float grad_scale, void* stream);
+/* The same step with its per-step values on the device, so a captured HIP graph can replay it:
+ * state is a 4-int64 (32-B) device buffer — int64 step, then floats bc1, sqrt(bc2), lr, 0.  The
+ * caller writes lr (float, byte offset 16); the call advances the step and derives the bias
+ * corrections on the device (double precision, as srk_adam_step's host side).                    */
+int srk_adam_step_state(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float beta1,
+                        float beta2, float eps, int64_t* state, float grad_scale, void* stream);
 /* nn.Dropout(p) training forward: keep[i] = Bernoulli(1-p) from a counter-based hash of
  * (seed, i) (not torch's RNG stream), y = keep ? x / (1-p) : 0.                              */
 int srk_dropout_fwd(const float* x, int64_t n, float p, uint64_t seed, float* y, uint8_t* keep, void* stream);
+/* srk_dropout_fwd with its seed on the device: state = uint64[2] {base, counter}; the mask hashes
+ * base + counter * odd constant, then the call advances state[1] (graph-replayable; nn.Dropout,
+ * model_fbanks_cnn.py:79,98).                                                                    */
+int srk_dropout_fwd_state(const float* x, int64_t n, float p, uint64_t* state, float* y, uint8_t* keep,
+                          void* stream);
 /* y = keep ? x * scale : 0 (dropout with an explicit keep-mask; also its backward).          */
 int srk_dropout_apply(const float* x, const uint8_t* keep, int64_t n, float scale, float* y, void* stream);
 

@@ -29,8 +29,10 @@ _SIGS = {
     "srk_prof_enable": [_I],
     "srk_prof_read": [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
                       ctypes.POINTER(ctypes.c_double)],
+    "srk_prof_kernels": [ctypes.c_char_p, _I64, ctypes.POINTER(ctypes.c_int64)],
     "srk_set_option": [ctypes.c_char_p, _I64],
     "srk_spin_timeouts": [],
+    "srk_scratch_generation": [],
     "srk_health_check": [_I],
     "srk_health_reset": [],
     "srk_fbank_fwd": [_P, _I64, _P, _P],
@@ -71,9 +73,11 @@ _SIGS = {
     "srk_cross_entropy": [_P, _P, _I64, _I64, _P, _P, _P, _P],
     "srk_adam_step": [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _I64, _F, _P],
     "srk_dropout_fwd": [_P, _I64, _F, ctypes.c_uint64, _P, _P, _P],
+    "srk_dropout_fwd_state": [_P, _I64, _F, _P, _P, _P, _P],
+    "srk_adam_step_state": [_P, _P, _P, _P, _I64, _F, _F, _F, _P, _F, _P],
     "srk_dropout_apply": [_P, _P, _I64, _F, _P, _P],
 }
-_RESTYPE = {"srk_last_error": ctypes.c_char_p, "srk_spin_timeouts": ctypes.c_int64, "srk_gru_workspace_floats": ctypes.c_int64,
+_RESTYPE = {"srk_last_error": ctypes.c_char_p, "srk_spin_timeouts": ctypes.c_int64, "srk_scratch_generation": ctypes.c_int64, "srk_gru_workspace_floats": ctypes.c_int64,
             "srk_conv2d_workspace_floats": ctypes.c_int64, "srk_conv1_pool_workspace_floats": ctypes.c_int64}
 
 
@@ -122,6 +126,26 @@ def prof_read(name):
     w = ctypes.c_double(0.0)
     call("srk_prof_read", name.encode(), ctypes.byref(n), ctypes.byref(ms), ctypes.byref(w))
     return int(n.value), float(ms.value), float(w.value)
+
+
+def prof_kernels():
+    """Every recorded launch grouped by (category name, kernel template + shape):
+    [{"name", "kernel", "launches", "ms_total", "work"}]."""
+    need = ctypes.c_int64(0)
+    call("srk_prof_kernels", None, 0, ctypes.byref(need))
+    buf = ctypes.create_string_buffer(int(need.value) + 256)
+    call("srk_prof_kernels", buf, len(buf), ctypes.byref(need))
+    out = []
+    for line in buf.value.decode().splitlines():
+        name, detail, n, ms, work = line.split("\t")
+        out.append({"name": name, "kernel": detail or name, "launches": int(n), "ms_total": float(ms),
+                    "work": float(work)})
+    return out
+
+
+def scratch_generation():
+    """srk_scratch_generation(): changes whenever a library scratch buffer is reallocated."""
+    return int(lib().srk_scratch_generation())
 
 
 def set_option(name, value):

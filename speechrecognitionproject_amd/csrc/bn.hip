@@ -355,6 +355,7 @@ int bn_scratch(size_t floats, float** out) {
     }
     s.floats = floats + floats / 4;
     SRK_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&s.p), s.floats * sizeof(float)));
+    g_scratch_gen.fetch_add(1);
   }
   *out = s.p;
   return SRK_OK;
@@ -509,3 +510,17 @@ int srk_batchnorm_bwd_dx(const float* x, const float* y, const float* dy, int64_
 }
 
 }  // extern "C"
+
+namespace srk {
+int release_bn_scratch() {
+  std::lock_guard<std::mutex> lk(g_bs_mu);
+  SRK_CHECK_HIP(hipDeviceSynchronize());
+  for (BnScratch& s : g_bs) {
+    if (s.p) SRK_CHECK_HIP(hipFree(s.p));
+    s.p = nullptr;
+    s.floats = 0;
+  }
+  g_scratch_gen.fetch_add(1);
+  return SRK_OK;
+}
+}  // namespace srk

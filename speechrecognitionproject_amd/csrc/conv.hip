@@ -566,6 +566,7 @@ int conv_scratch(size_t floats, float** out, ConvScratch* pool = g_cs) {
     }
     s.floats = floats + floats / 4;
     SRK_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&s.p), s.floats * sizeof(float)));
+    g_scratch_gen.fetch_add(1);
   }
   *out = s.p;
   return SRK_OK;
@@ -671,6 +672,8 @@ int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
               "conv: 16-bit sources need 8-aligned channels");
   ProfScope prof(prec == kPrecF32 ? name : (MODE == kFwd ? "conv_fwd_lp" : MODE == kDgrad ? "conv_dgrad_lp" : "conv_wgrad_lp"),
                  s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
+  prof.detail("conv_gemm_kernel<%s,%dx%d%s> %lldx%lldx%lld s%d", MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad",
+              BM, BN, c.a16 ? ",s16" : "", (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
   const dim3 grid((unsigned)c.nblk);
   if (BM == 64) launch_conv<MODE, 64, 64>(c, grid, s, vec, vecb, prec);
   else if (BN == 64) launch_conv<MODE, 128, 64>(c, grid, s, vec, vecb, prec);
@@ -790,6 +793,7 @@ int srk_conv2d_nhwc_bwd16(const float* x, int64_t N, int64_t H, int64_t W, int64
     g.C = dx; g.ldc = KW * Ci;
     srk::ProfScope prof(srk::matmul_prec() == srk::kPrecF32 ? "conv_dgrad" : "conv_dgrad_lp", s,
                         2.0 * (double)g.M * (double)g.N * (double)g.K);
+    prof.detail("conv_dgrad_as_gemm %lldx%lldx%lld", (long long)g.M, (long long)g.N, (long long)g.K);
     if ((rc = srk::gemm_f32(g, s))) return rc;
   } else if (dgrad_implicit) {
     srk::ConvArgs d = c;
@@ -857,3 +861,18 @@ int srk_maxpool_nhwc_bwd(const float* x, const float* dy, int64_t N, int64_t H, 
 }
 
 }  // extern "C"
+
+namespace srk {
+int release_conv_scratch() {
+  std::lock_guard<std::mutex> lk(g_cs_mu);
+  SRK_CHECK_HIP(hipDeviceSynchronize());
+  for (ConvScratch* pool : {g_cs, g_cs16})
+    for (int d = 0; d < 64; ++d) {
+      if (pool[d].p) SRK_CHECK_HIP(hipFree(pool[d].p));
+      pool[d].p = nullptr;
+      pool[d].floats = 0;
+    }
+  g_scratch_gen.fetch_add(1);
+  return SRK_OK;
+}
+}  // namespace srk

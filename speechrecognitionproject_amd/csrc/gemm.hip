@@ -1356,6 +1356,7 @@ int get_scratch(size_t floats, float** out) {
     }
     const size_t want = floats + floats / 4;
     SRK_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&s.p), want * sizeof(float)));
+    g_scratch_gen.fetch_add(1);
     s.floats = want;
   }
   *out = s.p;
@@ -1433,6 +1434,8 @@ int launch(const GemmDesc& d, hipStream_t s, bool vec) {
   // (measured: weight-gradient GEMMs +4..17 %); the x W^T projection shape keeps 4.
   static const int waves_env = env_int("SRK_GEMM_WAVES", 0);
   const int waves = BM == 256 ? 8 : (waves_env ? waves_env : ((!TA && TB) ? 4 : 8));
+  prof.detail("gemm_f32_kernel<%c%c,%dx%d,%dw> %lldx%lldx%lld b%lld s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', BM, BN, waves,
+              (long long)d.M, (long long)d.N, (long long)d.K, (long long)d.batch, splits);
   const dim3 grid((unsigned)ka.nblk, 1, (unsigned)d.batch);
   // LDS-DMA staging (global_load_lds_dwordx4) whenever the 16-B vector conditions hold
   static const int glds_env = env_int("SRK_GEMM_GLDS", 1);
@@ -1466,6 +1469,8 @@ int launch_lp_cfg(const GemmDesc& d, hipStream_t s, bool vec, bool f16) {
   int splits = 1;
   if (int rc = plan_launch(d, BM, BN, kLpBK, per_cu, ka, &splits)) return rc;
   ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
+  prof.detail("gemm_lp_kernel<%c%c,%dx%d> %lldx%lldx%lld s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', BM, BN, (long long)d.M,
+              (long long)d.N, (long long)d.K, splits);
   const dim3 grid((unsigned)ka.nblk, 1, (unsigned)d.batch), block(NW * 64);
   if (f16) {
     if (vec) hipLaunchKernelGGL((gemm_lp_kernel<TA, TB, BM, BN, NW, true, true, PF>), grid, block, 0, s, ka);
@@ -1506,6 +1511,8 @@ int launch_h16_cfg(const GemmDesc& d, hipStream_t s, bool f16) {
   int splits = 1;
   if (int rc = plan_launch(d, BM, BN, kLpBK, per_cu, ka, &splits)) return rc;
   ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K);
+  prof.detail("gemm_h16_kernel<%c%c,%dx%d> %lldx%lldx%lld s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', BM, BN, (long long)d.M,
+              (long long)d.N, (long long)d.K, splits);
   const dim3 grid((unsigned)ka.nblk), block(NW * 64);
   if (f16) hipLaunchKernelGGL((gemm_h16_kernel<TA, TB, BM, BN, NW, true>), grid, block, 0, s, ka);
   else hipLaunchKernelGGL((gemm_h16_kernel<TA, TB, BM, BN, NW, false>), grid, block, 0, s, ka);
@@ -1521,6 +1528,8 @@ int launch_g16(const GemmDesc& d, hipStream_t s, bool f16) {
   const int64_t tiles = ((d.M + 255) / 256) * ((d.N + 255) / 256);
   if (int rc = plan_launch(d, 256, 256, kG16BK, 1, ka, &splits, tiles * 2 < kCUs)) return rc;
   ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K);
+  prof.detail("gemm_g16_kernel<%c%c> %lldx%lldx%lld s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', (long long)d.M, (long long)d.N,
+              (long long)d.K, splits);
   const dim3 grid((unsigned)ka.nblk), block(512);
   if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true>), grid, block, 0, s, ka);
   else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false>), grid, block, 0, s, ka);
@@ -1549,6 +1558,8 @@ int launch_p32(const GemmDesc& d, hipStream_t s) {
   const int64_t tiles = ((d.M + 255) / 256) * ((d.N + 255) / 256);
   if (int rc = plan_launch(d, 256, 256, kP32BK, 1, ka, &splits, tiles * 2 < kCUs)) return rc;
   ProfScope prof("gemm_f32", s, 2.0 * (double)d.M * (double)d.N * (double)d.K);
+  prof.detail("gemm_p32_kernel<%c%c> %lldx%lldx%lld s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', (long long)d.M, (long long)d.N,
+              (long long)d.K, splits);
   hipLaunchKernelGGL((gemm_p32_kernel<TA, TB>), dim3((unsigned)ka.nblk), dim3(512), 0, s, ka);
   return finish_splits(d, ka, splits, s);
 }
@@ -1691,3 +1702,16 @@ extern "C" int srk_gemm_16(int trans_a, int trans_b, int64_t M, int64_t N, int64
   return srk::gemm_f32(d, srk::as_stream(stream));
   SRK_API_END
 }
+
+namespace srk {
+int release_gemm_scratch() {
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  SRK_CHECK_HIP(hipDeviceSynchronize());
+  for (Scratch& s : g_scratch) {
+    if (s.p) SRK_CHECK_HIP(hipFree(s.p));
+    s = Scratch{};
+  }
+  g_scratch_gen.fetch_add(1);
+  return SRK_OK;
+}
+}  // namespace srk

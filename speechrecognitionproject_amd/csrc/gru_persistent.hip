@@ -195,9 +195,17 @@ __device__ __forceinline__ void place(const GruPArgs& a, int S, int& dir, int& g
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
       unsigned* cen = a.counters + kCensusOff;
       const unsigned slot = __hip_atomic_fetch_add(cen + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(cen + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      unsigned spins = 0;
-      while (__hip_atomic_load(cen + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nwg) {
+      // wait for the per-XCD counts themselves to add up to the grid: the counts only grow and sum
+      // to nwg at most, so a sum of nwg means every count read in that pass is final (a separate
+      // total counter would not order the per-XCD adds it counts)
+      unsigned n[8], spins = 0;
+      while (true) {
+        unsigned sum = 0;
+        for (int x = 0; x < 8; ++x) {
+          n[x] = __hip_atomic_load(cen + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          sum += n[x];
+        }
+        if (sum >= (unsigned)nwg) break;
         __builtin_amdgcn_s_sleep(2);
         if (++spins >= a.spin_limit) {
           spin_gave_up(a);
@@ -205,8 +213,7 @@ __device__ __forceinline__ void place(const GruPArgs& a, int S, int& dir, int& g
         }
       }
       bool even = true;
-      for (int x = 0; x < 8; ++x)
-        even = even && __hip_atomic_load(cen + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nwg / 8);
+      for (int x = 0; x < 8; ++x) even = even && n[x] == (unsigned)(nwg / 8);
       info[0] = even ? (int)xcc : -1;
       info[1] = (int)slot;
     }
@@ -1584,6 +1591,8 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     const double flops = 2.0 * 2.0 * (double)(ac.b_end - c0) * 3 * a.H * a.H * (a.T - 1);
     ProfScope prof(backward ? (prec == kPrecF32 ? "gru_bwd_seq" : "gru_bwd_seq_lp")
                             : (prec == kPrecF32 ? "gru_fwd_seq" : "gru_fwd_seq_lp"), s, flops);
+    prof.detail("gru_%s_persistent%s_kernel B%d T%d chunk%d", backward ? "bwd" : "fwd", lp2 ? "_lp2" : (prec == kPrecF32 ? "" : "_lp"),
+                ac.b_end - c0, a.T, ac.chunk);
     if (lp2)
       hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(lp2_kernel_ptr<512>(backward, prec))),
                          grid, dim3(256), lp2_lds_bytes(512, backward), s, ac);

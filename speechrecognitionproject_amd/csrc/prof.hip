@@ -3,7 +3,10 @@
 // the SAME stream; srk_prof_read() waits for the recorded events and sums the elapsed times by
 // kernel name.  Disabled (the default), a ProfScope costs one relaxed atomic load.
 #include <atomic>
+#include <cstdarg>
+#include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -14,7 +17,7 @@ namespace srk {
 namespace {
 
 struct Rec {
-  std::string name;
+  std::string name, detail;
   hipEvent_t a, b;
   double work;
 };
@@ -46,6 +49,7 @@ void recycle_all() {
 }  // namespace
 
 ProfScope::ProfScope(const char* name, hipStream_t s, double work) : name_(name), s_(s), a_(nullptr), work_(work) {
+  detail_[0] = 0;
   if (!g_on.load(std::memory_order_relaxed)) return;
   std::lock_guard<std::mutex> lk(g_mu);
   a_ = take_event();
@@ -58,7 +62,15 @@ ProfScope::~ProfScope() {
   hipEvent_t b = take_event();
   if (!b) return;
   (void)hipEventRecord(b, s_);
-  g_recs.push_back(Rec{name_, static_cast<hipEvent_t>(a_), b, work_});
+  g_recs.push_back(Rec{name_, detail_, static_cast<hipEvent_t>(a_), b, work_});
+}
+
+void ProfScope::detail(const char* fmt, ...) {
+  if (!a_) return;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(detail_, sizeof(detail_), fmt, ap);
+  va_end(ap);
 }
 
 }  // namespace srk
@@ -93,6 +105,40 @@ int srk_prof_read(const char* name, int64_t* count, double* total_ms, double* to
   *count = n;
   *total_ms = tot;
   *total_work = work;
+  return SRK_OK;
+  SRK_API_END
+}
+
+// Every record grouped by (name, detail), as JSON lines "name\tdetail\tcount\tms\twork\n" into buf
+// (NUL-terminated, truncated at cap); *needed = the full length + 1.
+int srk_prof_kernels(char* buf, int64_t cap, int64_t* needed) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(needed && (buf || cap == 0), SRK_ERR_INVALID, "prof_kernels: null pointer");
+  std::lock_guard<std::mutex> lk(srk::g_mu);
+  struct Agg { int64_t n = 0; double ms = 0.0, work = 0.0; };
+  std::map<std::pair<std::string, std::string>, Agg> agg;
+  for (auto& r : srk::g_recs) {
+    SRK_CHECK_HIP(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    SRK_CHECK_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+    Agg& g = agg[{r.name, r.detail}];
+    g.n += 1;
+    g.ms += ms;
+    g.work += r.work;
+  }
+  std::string out;
+  char line[320];
+  for (auto& kv : agg) {
+    snprintf(line, sizeof(line), "%s\t%s\t%lld\t%.6f\t%.6e\n", kv.first.first.c_str(), kv.first.second.c_str(),
+             (long long)kv.second.n, kv.second.ms, kv.second.work);
+    out += line;
+  }
+  *needed = (int64_t)out.size() + 1;
+  if (cap > 0) {
+    const size_t n = std::min<size_t>(out.size(), (size_t)cap - 1);
+    memcpy(buf, out.data(), n);
+    buf[n] = 0;
+  }
   return SRK_OK;
   SRK_API_END
 }

@@ -29,6 +29,7 @@ unsigned long long* g_opt_gru_trace = nullptr;
 unsigned g_opt_gru_spin_limit = 0;
 int g_opt_gru_xcd_local = 1;
 int g_opt_gru_lp2 = 1;
+std::atomic<int64_t> g_scratch_gen{0};
 
 static thread_local std::string g_last_error;
 
@@ -327,6 +328,11 @@ int srk_set_option(const char* name, int64_t value) {
   SRK_API_BEGIN
   SRK_REQUIRE(name, SRK_ERR_INVALID, "set_option: null name");
   const std::string n(name);
+  if (n == "release_scratch") {   // free the library's grow-only scratch buffers (invalidates captured graphs)
+    if (int rc = srk::release_gemm_scratch()) return rc;
+    if (int rc = srk::release_conv_scratch()) return rc;
+    return srk::release_bn_scratch();
+  }
   if (n == "gru_persistent") {
     srk::g_opt_gru_persistent = value != 0;
     return SRK_OK;
@@ -372,3 +378,5 @@ int srk_set_option(const char* name, int64_t value) {
 }
 
 }  // extern "C"
+
+extern "C" int64_t srk_scratch_generation(void) { return srk::g_scratch_gen.load(); }

@@ -1,6 +1,7 @@
 // Internal helpers shared by every translation unit of libsrk.so (gfx950 / CDNA4 only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -81,6 +82,13 @@ int matmul_prec();
 
 // Kernel of the 16-bit-operand GEMM (srk_set_option "gemm16_kernel", A/B measurements and tests):
 // 0 = by shape, 1 = register-staged gemm_h16_kernel, 2 = LDS-DMA ping-pong gemm_g16_kernel.
+// Bumped whenever a library scratch buffer is (re)allocated: a captured HIP graph that refers to the
+// old buffer must not be replayed (srk_scratch_generation; graphs.GraphedStep checks it).
+extern std::atomic<int64_t> g_scratch_gen;
+// Free every grow-only scratch buffer of one pool (device-synchronizing; bumps g_scratch_gen).
+int release_gemm_scratch();
+int release_conv_scratch();
+int release_bn_scratch();
 extern int g_opt_gemm16_kernel;
 // Kernel of the fp32 GEMM (srk_set_option "gemm32_kernel"): 0 = by shape, 1 = register-staged
 // gemm_f32_kernel, 2 = LDS-DMA ping-pong gemm_p32_kernel.
@@ -99,12 +107,16 @@ class ProfScope {
   ~ProfScope();
   ProfScope(const ProfScope&) = delete;
   ProfScope& operator=(const ProfScope&) = delete;
+  // The launch's kernel and shape ("gemm_f32_kernel<NT,256x128> 13056x3072x1024"), printf-style;
+  // srk_prof_kernels groups records by (name, detail).  No-op (no formatting) when profiling is off.
+  void detail(const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 
  private:
   const char* name_;
   hipStream_t s_;
   void* a_;
   double work_;
+  char detail_[96];
 };
 
 }  // namespace srk

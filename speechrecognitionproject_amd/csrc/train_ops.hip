@@ -55,9 +55,9 @@ __global__ __launch_bounds__(256) void mean_kernel(const float* __restrict__ v, 
 //   m = b1*m + (1-b1)*g ; v = b2*v + (1-b2)*g*g
 //   denom = sqrt(v) / sqrt(1 - b2^t) + eps ; p -= (lr / (1 - b1^t)) * m / denom
 // grad_scale multiplies g first (1/world for a summed all-reduce, or 1).
-__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
-                            float bc1, float bc2_sqrt, float grad_scale) {
+__device__ __forceinline__ void adam_body(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                          float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
+                                          float bc1, float bc2_sqrt, float grad_scale) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
   for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
     if (i + 3 < n) {
@@ -89,6 +89,12 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   }
 }
 
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
+                            float bc1, float bc2_sqrt, float grad_scale) {
+  adam_body(p, g, m, v, n, lr, b1, b2, eps, bc1, bc2_sqrt, grad_scale);
+}
+
 // Counter-based Bernoulli mask (splitmix64 of seed ^ index): keep with probability 1 - p.
 __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t i) {
   uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
@@ -106,6 +112,41 @@ __global__ void dropout_fwd_kernel(const float* __restrict__ x, int64_t n, float
   keep[i] = k;
   y[i] = k ? x[i] * scale : 0.f;
 }
+
+// Device-resident optimizer step (graph-replayable): one lane advances the step count and stores the
+// bias corrections the host path would compute (double precision, rounded to float) beside it.
+__global__ void adam_prep_kernel(int64_t* __restrict__ state, float beta1, float beta2) {
+  const int64_t step = state[0] + 1;
+  state[0] = step;
+  float* bc = reinterpret_cast<float*>(state + 1);
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  bc[0] = (float)bc1;
+  bc[1] = (float)sqrt(bc2);
+}
+
+__global__ __launch_bounds__(256) void adam_state_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                         float b1, float b2, float eps,
+                                                         const int64_t* __restrict__ state, float grad_scale) {
+  const float* f = reinterpret_cast<const float*>(state + 1);   // bc1, sqrt(bc2), lr
+  adam_body(p, g, m, v, n, f[2], b1, b2, eps, f[0], f[1], grad_scale);
+}
+
+// Dropout whose seed lives on the device ([base, counter]): the mask of call k hashes base + k, and
+// the counter advances behind the mask kernel — so a captured graph draws a fresh mask per replay.
+__global__ void dropout_state_kernel(const float* __restrict__ x, int64_t n, float p, float scale,
+                                     const uint64_t* __restrict__ state, float* __restrict__ y,
+                                     uint8_t* __restrict__ keep) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t seed = state[0] + 0xD1B54A32D192ED03ull * state[1];
+  const bool k = uniform01(seed, (uint64_t)i) >= p;
+  keep[i] = k;
+  y[i] = k ? x[i] * scale : 0.f;
+}
+
+__global__ void counter_inc_kernel(uint64_t* __restrict__ c) { c[0] += 1; }
 
 __global__ void dropout_kernel(const float* __restrict__ x, const uint8_t* __restrict__ keep, int64_t n, float scale,
                                float* __restrict__ y) {
@@ -150,6 +191,41 @@ int srk_adam_step(float* param, const float* grad, float* exp_avg, float* exp_av
   srk::ProfScope prof("adam", srk::as_stream(stream), 28.0 * (double)n);   // p,g,m,v read + p,m,v written
   hipLaunchKernelGGL(srk::adam_kernel, dim3((unsigned)blocks), dim3(nt), 0, srk::as_stream(stream), param, grad,
                      exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, (float)bc1, (float)std::sqrt(bc2), grad_scale);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_adam_step_state(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float beta1,
+                        float beta2, float eps, int64_t* state, float grad_scale, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(n >= 0 && state, SRK_ERR_INVALID, "adam_state: bad n / null state");
+  if (n == 0) return SRK_OK;
+  SRK_REQUIRE(param && grad && exp_avg && exp_avg_sq, SRK_ERR_INVALID, "adam_state: null pointer");
+  SRK_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0 &&
+              (uintptr_t)state % 8 == 0, SRK_ERR_INVALID, "adam_state: buffers must be 16-byte aligned");
+  hipStream_t s = srk::as_stream(stream);
+  hipLaunchKernelGGL(srk::adam_prep_kernel, dim3(1), dim3(1), 0, s, state, beta1, beta2);
+  const int nt = 256;
+  const int64_t blocks = std::min<int64_t>((n + nt * 4 - 1) / (nt * 4), 256 * 8);
+  srk::ProfScope prof("adam", s, 28.0 * (double)n);   // p,g,m,v read + p,m,v written
+  hipLaunchKernelGGL(srk::adam_state_kernel, dim3((unsigned)blocks), dim3(nt), 0, s, param, grad, exp_avg, exp_avg_sq,
+                     n, beta1, beta2, eps, state, grad_scale);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_dropout_fwd_state(const float* x, int64_t n, float p, uint64_t* state, float* y, uint8_t* keep,
+                          void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(n >= 0 && p >= 0.f && p < 1.f && state && (n == 0 || (x && y && keep)), SRK_ERR_INVALID,
+              "dropout_fwd_state: bad args");
+  if (n == 0) return SRK_OK;
+  hipStream_t s = srk::as_stream(stream);
+  hipLaunchKernelGGL(srk::dropout_state_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n, p,
+                     1.0f / (1.0f - p), state, y, keep);
+  hipLaunchKernelGGL(srk::counter_inc_kernel, dim3(1), dim3(1), 0, s, state + 1);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END

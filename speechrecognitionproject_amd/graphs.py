@@ -1,0 +1,66 @@
+"""HIP-graph replay of a warm-up-stable train step (training.py:83-95 minus its host work).
+
+A train step of this package is a fixed sequence of launches on one stream (the HIP kernels behind
+the C ABI, the persistent GRU's counter memsets, torch's allocator and autograd bookkeeping) whose
+shapes, pointers and host arguments do not change from step to step once the batch shape is fixed:
+the only per-step host values — the Adam step count and the dropout seed — live on the device
+(``optim.Adam.state_dev``, ``nn._dropout_state``).  ``GraphedStep`` records that sequence once into a
+HIP graph (torch.cuda.graph: a private memory pool, capture on a side stream) and then launches the
+whole step with one ``hipGraphLaunch``, removing the per-kernel host launch cost.
+
+Inputs must sit at fixed addresses: the caller copies each batch into ``static`` tensors it passes
+to the step function, then calls ``replay()``.
+
+Constraints (checked by the parity tests, tests/test_graphs_gpu.py): every library scratch buffer must
+already have its final size when the capture starts (the warm-up runs the step at least twice), and
+the per-step kernel timers (srk_prof) stay off during capture and replay; bench.py times kernels in a
+separate eager pass of the same step.
+"""
+import torch
+
+from . import _lib
+
+
+class GraphedStep:
+    """``step()`` -> its output tensor(s), captured after ``warmup`` eager calls on a side stream."""
+
+    def __init__(self, step, warmup=2):
+        """warmup: eager calls of ``step`` on a side stream before the capture (>= 2 so every scratch
+        buffer reaches its size), or 0 when the caller has just run >= 2 eager steps of the same shapes
+        (training.py: real steps on real batches, no repeated step)."""
+        if warmup == 1 or warmup < 0:
+            raise ValueError("GraphedStep: warmup must be 0 (caller warmed up) or >= 2")
+        self.step = step
+        self.graph = None
+        self.out = None
+        if warmup:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(warmup):
+                    self.out = step()
+            torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.generation = _lib.scratch_generation()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = step()
+        torch.cuda.synchronize()
+        if _lib.scratch_generation() != self.generation:
+            raise _lib.SrkError("GraphedStep: a library scratch buffer grew during the capture (warm up longer)")
+
+    def valid(self):
+        """False once a library scratch buffer the graph may refer to has been reallocated."""
+        return self.graph is not None and _lib.scratch_generation() == self.generation
+
+    def replay(self):
+        if not self.valid():
+            raise _lib.SrkError("GraphedStep: the library's scratch buffers were reallocated after the capture "
+                                "(another shape ran in between): capture again")
+        self.graph.replay()
+        return self.out
+
+    def release(self):
+        """Drop the graph and its private memory pool (before other shapes grow shared scratch)."""
+        self.graph = None
+        self.out = None

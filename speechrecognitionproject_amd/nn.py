@@ -451,14 +451,42 @@ class MaxPool1d(tnn.Module):
         return y.reshape(N, L // self.kernel_size, C)
 
 
+_DROPOUT_STATE = {}   # device index -> int64[2] {base seed, call counter} read by srk_dropout_fwd_state
+_MASK63 = (1 << 63) - 1
+
+
+def _dropout_state(device):
+    """The device-resident dropout seed of ``device``.  Outside a graph capture it is re-derived on
+    every call from torch's CUDA generator of that device — (initial seed, Philox offset), the
+    offset then advanced as torch's own dropout would — folded with the data-parallel rank, so
+    ``torch.manual_seed`` governs the masks (as it does the reference's nn.Dropout on the GPU) and
+    the CPU generator (DataLoader shuffles, the reference's numpy/random draws) is never touched.
+    Inside a capture the state is left as the last eager call set it and the kernel's own counter
+    advance gives every graph replay a fresh mask."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _DROPOUT_STATE.get(idx)
+    if st is None:
+        st = torch.zeros(2, dtype=torch.int64, device=device)
+        _DROPOUT_STATE[idx] = st
+    if not torch.cuda.is_current_stream_capturing():
+        gen = torch.cuda.default_generators[idx]
+        seed, off = gen.initial_seed(), gen.get_offset()
+        gen.set_offset(off + 4)
+        rank = torch.distributed.get_rank() if torch.distributed.is_available() and torch.distributed.is_initialized() else 0
+        base = ((seed * 0x9E3779B97F4A7C15) ^ (rank * 0xC2B2AE3D27D4EB4F) ^ (off << 17)) & _MASK63
+        st[0].fill_(base)
+        st[1].fill_(0)
+    return st
+
+
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, p, seed):
+    def forward(ctx, x, p, state):
         x = x.contiguous()
         _check_cuda(x)
         y = torch.empty_like(x)
         keep = torch.empty(x.shape, device=x.device, dtype=torch.uint8)
-        call("srk_dropout_fwd", ptr(x), x.numel(), float(p), int(seed), ptr(y), ptr(keep), stream_ptr())
+        call("srk_dropout_fwd_state", ptr(x), x.numel(), float(p), ptr(state), ptr(y), ptr(keep), stream_ptr())
         ctx.save_for_backward(keep)
         ctx.scale = 1.0 / (1.0 - p)
         return y
@@ -498,9 +526,9 @@ class _DropoutMaskFn(torch.autograd.Function):
 
 class Dropout(tnn.Module):
     """nn.Dropout(p=0.5): identity in eval mode; in training a Bernoulli(1-p) mask from a
-    counter-based hash.  The per-call seed is drawn from torch's default generator (so
-    ``torch.manual_seed`` governs the masks, as it does the reference's nn.Dropout) and folded with
-    the data-parallel rank, so ranks holding different clips draw independent masks.
+    counter-based hash of a device-resident seed (``_dropout_state``: torch's CUDA generator state
+    folded with the data-parallel rank, so ``torch.manual_seed`` governs the masks, ranks holding
+    different clips draw independent masks, and a captured HIP graph draws a new mask per replay).
 
     ``set_mask(keep)`` supplies the keep mask (uint8, the input's shape) for the NEXT training
     forward instead of drawing one — how the parity tests replay a mask exported from the
@@ -522,10 +550,7 @@ class Dropout(tnn.Module):
             if keep.shape != x.shape:
                 raise ValueError("Dropout.set_mask: mask shape %s != input shape %s" % (tuple(keep.shape), tuple(x.shape)))
             return _DropoutMaskFn.apply(x, keep, 1.0 / (1.0 - self.p))
-        seed = int(torch.randint(0, 1 << 62, (1,)).item())
-        rank = torch.distributed.get_rank() if torch.distributed.is_available() and torch.distributed.is_initialized() else 0
-        seed = (seed ^ (rank * 0x9E3779B97F4A7C15)) & ((1 << 63) - 1)
-        return _DropoutFn.apply(x, self.p, seed)
+        return _DropoutFn.apply(x, self.p, _dropout_state(x.device))
 
 
 # ----------------------------------------------------------------------------- batch norm
@@ -577,14 +602,18 @@ class BatchNorm1d(tnn.Module):
         self.register_buffer("running_var", torch.ones(num_features))
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
 
+    def _normalize(self, x, gamma, beta, residual, running_mean, running_var, relu):
+        """The K9 call on float4-aligned channels (SyncBatchNorm1d overrides it)."""
+        return _BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, self.training, self.momentum,
+                                  self.eps, relu)
+
     def forward(self, x, residual=None, relu=False):
         require_gpu()
         if self.num_features % 4:
             return self.forward_padded(x, residual, relu)[..., :self.num_features]
         if self.training:
             self.num_batches_tracked.add_(1)
-        return _BatchNormFn.apply(x, self.weight, self.bias, residual, self.running_mean, self.running_var,
-                                  self.training, self.momentum, self.eps, relu)
+        return self._normalize(x, self.weight, self.bias, residual, self.running_mean, self.running_var, relu)
 
     def forward_padded(self, x, residual=None, relu=False):
         """K9 works on float4 channel groups: a channel count that is not a multiple of 4 (the
@@ -607,7 +636,7 @@ class BatchNorm1d(tnn.Module):
         b = torch.cat([self.bias, self.bias.new_zeros(p)])
         rm = torch.cat([self.running_mean, self.running_mean.new_zeros(p)])
         rv = torch.cat([self.running_var, self.running_var.new_ones(p)])
-        y = _BatchNormFn.apply(xp, g, b, rp, rm, rv, self.training, self.momentum, self.eps, relu)
+        y = self._normalize(xp, g, b, rp, rm, rv, relu)
         if self.training:
             with torch.no_grad():
                 self.running_mean.copy_(rm[:C])
@@ -680,15 +709,15 @@ class SyncBatchNorm1d(BatchNorm1d):
         super().__init__(num_features, eps, momentum)
         self.process_group = process_group
 
-    def forward(self, x, residual=None, relu=False):
+    def _normalize(self, x, gamma, beta, residual, running_mean, running_var, relu):
+        # the padded path (channel counts not a multiple of 4: the resnet_bgru mode-1 head's 250 / 125)
+        # comes through here too, so its statistics span the ranks as well
         import torch.distributed as dist
         if not (self.training and dist.is_available() and dist.is_initialized()
                 and dist.get_world_size(self.process_group) > 1):
-            return super().forward(x, residual=residual, relu=relu)
-        require_gpu()
-        self.num_batches_tracked.add_(1)
-        return _SyncBatchNormFn.apply(x, self.weight, self.bias, residual, self.running_mean, self.running_var,
-                                      self.momentum, self.eps, relu, self.process_group)
+            return super()._normalize(x, gamma, beta, residual, running_mean, running_var, relu)
+        return _SyncBatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, self.momentum, self.eps,
+                                      relu, self.process_group)
 
 
 def convert_sync_batchnorm(module, process_group=None):

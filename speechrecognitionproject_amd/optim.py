@@ -76,11 +76,24 @@ class Adam(torch.optim.Optimizer):
         self.flat = flat if flat is not None else FlatParams(params)
         self.exp_avg = torch.zeros_like(self.flat.data)
         self.exp_avg_sq = torch.zeros_like(self.flat.data)
-        self.step_count = 0
+        self.step_count = 0      # host mirror of the device step count
+        # {int64 step; float bc1, sqrt(bc2), lr, 0} on the device, so a captured HIP graph replays the
+        # step count and follows lr changes (ExponentialLR) made between replays
+        self.state_dev = torch.zeros(4, dtype=torch.int64, device=self.flat.data.device)
+        self._lr_dev = None
         self.grad_scale = 1.0
 
     def zero_grad(self, set_to_none=False):
         self.flat.zero_grad()
+
+    @torch.no_grad()
+    def sync_lr(self):
+        """Write param_groups[0]["lr"] into the device state if it changed (a captured step reads lr
+        there: call this after an lr scheduler step when replaying a graph)."""
+        lr = self.param_groups[0]["lr"]
+        if lr != self._lr_dev and not torch.cuda.is_current_stream_capturing():
+            self.state_dev.view(torch.float32)[4].fill_(float(lr))
+            self._lr_dev = lr
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -89,9 +102,9 @@ class Adam(torch.optim.Optimizer):
         self.step_count += 1
         b1, b2 = g["betas"]
         f = self.flat
-        call("srk_adam_step", ptr(f.data), ptr(f.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq), f.numel,
-             float(g["lr"]), float(b1), float(b2), float(g["eps"]), self.step_count, float(self.grad_scale),
-             stream_ptr())
+        self.sync_lr()
+        call("srk_adam_step_state", ptr(f.data), ptr(f.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq), f.numel,
+             float(b1), float(b2), float(g["eps"]), ptr(self.state_dev), float(self.grad_scale), stream_ptr())
         # a persistent kernel that timed out produced invalid gradients: fail loudly (a host-pinned
         # word, no device sync; it sees every timeout of the work the GPU has reached so far)
         check_health(sync=False)

@@ -13,7 +13,10 @@ synthetic clips when no Kaggle tree is available, ``--data-path/--output-path`` 
 hard-coded paths (:21-24), ``--log-every`` batches loss lines to avoid a host sync per step,
 ``--loader device`` (default for WAV trees) replaces the per-item DataLoader with native batched
 decode + one on-device augmentation launch per batch, and torchrun environments train
-data-parallel (one process per GPU, RCCL all-reduce).
+data-parallel (one process per GPU, RCCL all-reduce).  On one GPU, full-size batches after the
+first two run as replays of a HIP graph of the step (the batch is copied into the graph's static
+input first; a short last batch runs eagerly; ``--no-graph`` disables it) — same arithmetic, bit
+for bit (tests/test_graphs_gpu.py).
 """
 import argparse
 import importlib
@@ -50,6 +53,9 @@ def parse(argv=None):
                    help='data-parallel: BatchNorm statistics over the global batch (SyncBatchNorm1d)')
     p.add_argument('--no-overlap', dest='overlap', action='store_false',
                    help='data-parallel: one all-reduce after backward instead of overlapped buckets')
+    p.add_argument('--no-graph', dest='graph', action='store_false',
+                   help='single GPU: run every step eagerly instead of replaying a HIP graph of the step for '
+                        'full-size batches (speechrecognitionproject_amd/graphs.py)')
     p.add_argument('--loader', choices=('device', 'torch'), default='device',
                    help='WAV datasets: device = native batched decode + K10 on-device augmentation '
                         '(DeviceBatchLoader); torch = per-item Dataset.__getitem__ through DataLoader')
@@ -94,10 +100,33 @@ def main(argv=None):
     os.makedirs(args.output_path, exist_ok=True)
     loss_file = os.path.join(args.output_path, 'loss_' + key + '.txt')
 
+    use_graph = args.graph and world == 1
+    graphed = None          # GraphedStep of a full-batch step (captured after two eager full steps)
+    static = {}
+    full_eager = 0
+
+    def eager_step(x, y):
+        optimizer.zero_grad()
+        if reducer is not None:
+            reducer.begin()
+        outputs = model(x)
+        loss = criterion(outputs, y)
+        loss.backward()
+        if reducer is not None:
+            reducer.finish()
+        else:
+            parallel.allreduce_grads(flat)
+        optimizer.step()
+        return loss
+
+    def graph_body():
+        return eager_step(static['x'], static['y'])
+
     epoch = 0
     while epoch < args.epochs:
         if epoch > 4:
             scheduler.step()
+            optimizer.sync_lr()     # a replayed step reads lr from the device
         sampler = None
         if world > 1:
             idx = parallel.shard_indices(len(data), rank, world, seed=0, epoch=epoch)
@@ -125,18 +154,23 @@ def main(argv=None):
             pending = []
 
         for batch in loader:
-            optimizer.zero_grad()
-            if reducer is not None:
-                reducer.begin()
-            outputs = model(batch['audio'])
-            loss = criterion(outputs, batch['label'].to(device))
-            loss.backward()
-            if reducer is not None:
-                reducer.finish()
+            x, y = batch['audio'], batch['label'].to(device)
+            full = x.shape[0] == args.batch_size
+            if use_graph and full and full_eager >= 2:
+                if not static:
+                    static['x'] = torch.empty(x.shape, dtype=torch.float32, device=device)
+                    static['y'] = torch.empty(y.shape, dtype=y.dtype, device=device)
+                static['x'].copy_(x, non_blocking=True)
+                static['y'].copy_(y, non_blocking=True)
+                if graphed is None or not graphed.valid():
+                    from .graphs import GraphedStep
+                    graphed = GraphedStep(graph_body, warmup=0)   # the eager full steps were the warm-up
+                loss = graphed.replay()
             else:
-                parallel.allreduce_grads(flat)
-            optimizer.step()
-            pending.append(loss.detach())
+                loss = eager_step(x, y)
+                if full:
+                    full_eager += 1
+            pending.append(loss.detach().clone() if graphed is not None and loss is graphed.out else loss.detach())
             if len(pending) >= args.log_every:
                 flush()
         flush()

@@ -26,6 +26,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
 REF = "/root/reference"
 sys.path.insert(0, REPO)
+# the reference tree is read-only: importing it must not leave __pycache__/*.pyc behind
+sys.dont_write_bytecode = True
 
 from oracle import features as OF            # noqa: E402
 from oracle import models as OM              # noqa: E402
@@ -129,6 +131,61 @@ def model_golden(name, net, x, labels, train_mode=False, dropout_keep=None):
         rec["gabs__" + k] = np.float64(grads[k].double().abs().sum())
     np.savez_compressed(os.path.join(HERE, name), **rec)
     print("wrote", name, "logits", out.shape)
+
+
+def eval_helpers_golden(name, R_mod, ocls, seed):
+    """The plugin eval helpers ``accuracy`` / ``class_accuracy`` (model_mfcc_bgru.py:39-82; the same
+    text in every model_*.py) run by the reference on a seeded model in eval mode, recording the
+    files they write.  Clips are kept only where the reference's top-2 logit gap is wide (> 1e-2 of
+    the largest logit), so a 1e-4 logit difference cannot change a prediction.
+    * ``accuracy`` on 3 clips at batchsize 2 (labels: right, wrong, right): the last batch is short
+      and ``total += batchsize`` counts it as 2 -> 2 / 4 = 50.0, appended after an existing line.
+    * ``class_accuracy`` on 36 clips at batchsize 4: clips 0..23 carry labels i % 12 (every class
+      present; the reference divides by each class count) and clips 24..35 carry the reference's
+      own prediction; the file is overwritten."""
+    if ONLY and name not in ONLY:
+        return
+    net = R_mod.Network()
+    sd = OM.seeded_state_dict(ocls(), 0)
+    net.load_state_dict(sd)
+    net.eval()
+    x, _ = synthetic_clips(160, seed=seed)
+    with torch.no_grad():
+        lg = net(torch.from_numpy(x)).numpy()
+    # a random-init model predicts one class for every clip: centre the output bias on these
+    # clips' mean logits so the predictions spread over the classes (stored in the fixture)
+    bias_key = [k for k in sd if k.endswith("bias")][-1]
+    sd[bias_key] = (sd[bias_key].double() - torch.from_numpy(lg.mean(0))).float()
+    net.load_state_dict(sd)
+    with torch.no_grad():
+        lg = net(torch.from_numpy(x)).numpy()
+    top2 = np.sort(lg, axis=1)[:, -2:]
+    wide = np.nonzero(top2[:, 1] - top2[:, 0] > 1e-2 * np.abs(lg).max())[0]
+    assert len(wide) >= 39, len(wide)
+    pred = lg.argmax(1)
+    a_idx = wide[:3]
+    a_lab = np.array([pred[a_idx[0]], (pred[a_idx[1]] + 5) % 12, pred[a_idx[2]]])
+    c_idx = wide[3:39]
+    c_lab = np.concatenate([np.arange(24) % 12, pred[c_idx[24:]]])
+    ds_a = [{"audio": x[i], "label": int(l)} for i, l in zip(a_idx, a_lab)]
+    ds_c = [{"audio": x[i], "label": int(l)} for i, l in zip(c_idx, c_lab)]
+    with tempfile.TemporaryDirectory() as d:
+        fa, fc = d + "/val.txt", d + "/class.txt"
+        with open(fa, "w") as f:
+            f.write("12.5\n")
+        with open(fc, "w") as f:
+            f.write("stale\n")
+        net.train()
+        ret = R_mod.accuracy(net, ds_a, fa, 2)
+        assert net.training
+        R_mod.class_accuracy(net, ds_c, fc, 4)
+        ta, tc = open(fa).read(), open(fc).read()
+    np.savez_compressed(os.path.join(HERE, name), acc_pcm=x[a_idx], acc_labels=a_lab, acc_batch=np.int64(2),
+                        acc_return=np.float64(ret), acc_file=np.array(ta), acc_prior=np.array("12.5\n"),
+                        cls_pcm=x[c_idx], cls_labels=c_lab, cls_batch=np.int64(4), cls_file=np.array(tc),
+                        acc_pred=pred[a_idx], cls_pred=pred[c_idx], bias_key=np.array(bias_key),
+                        bias=sd[bias_key].numpy())
+    print("wrote", name, repr(ta), tc.count("\n"), "lines")
 
 
 def main():
@@ -291,6 +348,10 @@ def main():
     probs = (np.exp(lg) / np.exp(lg).sum(-1, keepdims=True)).reshape(6, 48).astype(np.float32)
     torch.manual_seed(0)
     model_golden("analyst_golden.npz", R_an.Network(), probs, np.array([0, 3, 11, 5, 5, 10]), train_mode=True)
+    # ---- plugin eval helpers (SURVEY.md §8c "Python-harness rows" item 3)
+    torch.manual_seed(0)
+    eval_helpers_golden("eval_helpers_fbanks_cnn_golden.npz", R_fb, OM.FbanksCNN, seed=61)
+    eval_helpers_golden("eval_helpers_mfcc_bgru_golden.npz", R_mb, OM.MfccBGRU, seed=62)
 
 
 if __name__ == "__main__":

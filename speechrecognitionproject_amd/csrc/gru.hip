@@ -408,16 +408,20 @@ extern "C" {
 
 // Both workspaces end with a 64-float-aligned block of kCounterFloats arrival counters (the
 // persistent recurrence kernels' step ordering; see gru_persistent.hip).
-// Before them, 64-float aligned, the persistent kernels' hand-off ping-pong buffer in MFMA-fragment
-// order (fwd: h [2 dir][2][rows][H], bwd: dg [2 dir][2][rows][3H]).
+// Before them, 64-float aligned, the persistent kernels' hand-off ring in MFMA-fragment order
+// (fwd: h [2 dir][kHandoffSlots][rows][H], bwd: dg [2 dir][kHandoffSlots][rows][3H]).
 static int64_t fwd_xbuf_off(int64_t B, int64_t T, int64_t H) { return (B * T * 6 * H + 2 * T * B * 4 * H + 63) / 64 * 64; }
 static int64_t bwd_xbuf_off(int64_t B, int64_t T, int64_t H) {
   return (B * T * 6 * H + 2 * B * T * 3 * H + 2 * B * 3 * H + 2 * B * H + 63) / 64 * 64;
 }
 // (rows padded to the 64-row groups of one launch chunk: <= 256 rows, or B rounded up to 64)
 static int64_t xbuf_rows(int64_t B) { return std::min<int64_t>((B + 63) / 64 * 64, 256); }
-static int64_t fwd_counter_off(int64_t B, int64_t T, int64_t H) { return fwd_xbuf_off(B, T, H) + 4 * xbuf_rows(B) * H; }
-static int64_t bwd_counter_off(int64_t B, int64_t T, int64_t H) { return bwd_xbuf_off(B, T, H) + 12 * xbuf_rows(B) * H; }
+static int64_t fwd_counter_off(int64_t B, int64_t T, int64_t H) {
+  return fwd_xbuf_off(B, T, H) + 2 * srk::kHandoffSlots * xbuf_rows(B) * H;
+}
+static int64_t bwd_counter_off(int64_t B, int64_t T, int64_t H) {
+  return bwd_xbuf_off(B, T, H) + 6 * srk::kHandoffSlots * xbuf_rows(B) * H;
+}
 
 // After the counters, for an input width that is not a multiple of 4 (srk::padded_in):
 //   fwd: x padded [B*T][in4] (kept for the backward's dW_ih) | W_ih padded [6H][in4]

@@ -8,10 +8,14 @@
 namespace srk {
 
 // Arrival counters / per-producer flags of the persistent kernels ([2 directions][groups <= 4] at a
-// 64-B stride, or [2][G][32] flags) in words 0..255, the XCD census in words kCensusOff..+8;
-// zeroed by a hipMemsetAsync of exactly this block before every launch.
-constexpr int kCounterFloats = 512;
-constexpr int kCensusOff = 256;
+// 64-B stride, or [2][G][32] flags: words 0..255; the fp32 two-chain kernels' per-wave flags
+// [2 dir][G][2 chains][2 row blocks][32 slices][2 k halves]: words 0..2047), the XCD census in
+// words kCensusOff..+8; zeroed by a hipMemsetAsync of exactly this block before every launch.
+constexpr int kCounterFloats = 4096;
+constexpr int kCensusOff = 4080;
+// Hand-off ring depth of the persistent kernels (slots per direction in the workspace): the fp32
+// two-chain kernels need 3 (a wave waits only for the producers of its k half, see gru_persistent.hip)
+constexpr int kHandoffSlots = 3;
 constexpr int kFusedIn = 64;   // widest layer input whose projection the forward kernels fuse
 
 struct GruPArgs {
@@ -63,6 +67,7 @@ extern unsigned long long* g_opt_gru_trace;   // device buffer or nullptr
 extern unsigned g_opt_gru_spin_limit;          // 0 = default (~2 s); test hook "gru_spin_limit"
 extern int g_opt_gru_xcd_local;                // XCD-local hand-off when the census allows (default 1)
 extern int g_opt_gru_lp2;                      // 16-bit recurrence on 32 x 32 workgroups (default 1)
+extern int g_opt_gru_dc;                       // fp32 recurrence: two independent row chains per workgroup (default 1)
 // Batch rows per bias-gradient partial of the 16-bit backward kernel (32 or 64; 256-row launch chunks).
 int gru_bias_part_rows();
 // Host-pinned health word (device-mapped pointer in *dev): non-zero once any persistent-kernel

@@ -32,6 +32,7 @@
 #include <cstdlib>
 #include <type_traits>
 #include <mutex>
+#include <utility>
 
 #include "gru_internal.h"
 
@@ -622,6 +623,455 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
       // cell and gate otherwise)
       st4(a.dgi + ((size_t)b * T + t) * 6 * H + dir * 3 * H + g * H + j0 + uq,
           g == 2 ? ld4(dT + (rl * 4 + 3) * DTP + uq) : val[i]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ fp32, two row chains per workgroup
+// The fp32 recurrence is bound by its MFMAs (B = 256: 12.3k MFMA cycles per SIMD per step, 5.1-5.6 us)
+// plus a serial tail the 4-wave kernels above leave the matrix cores idle in: the wait for the
+// slowest producer, the cell epilogue and the publish (~3.5 us of a 10.5 us step, tools/gru_trace.py).
+// Here a workgroup (direction, 64-row group, 16-unit slice — the same 256-workgroup grid and W_hh
+// slice in LDS) runs 8 waves as two INDEPENDENT chains of 32 rows: wave w = (chain c = w >> 2, row
+// block rb, k half kh) multiplies its 16 rows by the 48 gate columns over HALF of k (the h of slices
+// 16 kh .. 16 kh + 15), so each SIMD hosts one wave of each chain and one chain's MFMAs fill the other
+// chain's wait / epilogue / publish.  No workgroup barrier in the step loop:
+//  * a wave polls the per-wave flags of just its producers ((slice, kh') of its chain and row block in
+//    its k half: 32 words) and loads 16 fragment chunks of the hand-off;
+//  * the k-half pair (kh = 0, 1) adds its partial sums through LDS (double-buffered, an LDS flag per
+//    wave) in a fixed order (p0 + p1), after which wave kh owns units 8 kh .. 8 kh + 7 of its rows;
+//  * the owner lanes run the cell update, transpose their 16 x 8 h block through a per-wave LDS tile
+//    into the fragment layout (512 contiguous bytes of the chunk) and publish it with one flag word.
+// Hand-off ring of kHandoffSlots = 3: a producer waits only for its own k half, so without the third
+// slot it could overwrite step s - 1's data while a consumer in the other half still reads it; two
+// steps ahead it cannot (every slice's step s + 1 needed both halves' step s through its k-half pair).
+__device__ __forceinline__ void dc_wave_lds_fence() {   // this wave's LDS writes before its later LDS reads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// diagnostics: wave 4 (chain 1's first wave) stamps its arrival-wait end into trace slot 7
+__device__ __forceinline__ void dc_stamp_chain1(const GruPArgs& a, int step) {
+  if (a.trace && threadIdx.x == 256)
+    a.trace[((size_t)blockIdx.x * a.T + step) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+}
+
+constexpr int kDcXF = 24;   // floats a lane hands its pair partner: 3 gate accumulators x 4 rows (+ the fused projection's)
+
+__device__ __forceinline__ void dc_wait(const GruPArgs& a, const unsigned* f, int step) {
+  const int lane = threadIdx.x & 63;
+  unsigned spins = 0;
+  while (true) {
+    const unsigned v = lane < 32 ? __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xffffffffu;
+    if (__all(v >= (unsigned)step)) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins >= a.spin_limit) {
+      if (lane == 0) spin_gave_up(a);
+      break;
+    }
+  }
+}
+
+// pair barrier of the two k-half waves through an LDS word per wave (monotonic step counts)
+__device__ __forceinline__ void dc_pair_sync(const GruPArgs& a, unsigned* pf, int w, int step) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(pf + w, (unsigned)(step + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  unsigned spins = 0;
+  while (__hip_atomic_load(pf + (w ^ 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)(step + 1)) {
+    __builtin_amdgcn_s_sleep(0);
+    if (++spins >= 4 * a.spin_limit) {
+      if ((threadIdx.x & 63) == 0) spin_gave_up(a);
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ void dc_flag(const GruPArgs& a, unsigned* f, int step, bool local) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) {
+    if (local)
+      __builtin_amdgcn_raw_buffer_store_b32((unsigned)(step + 1), rsrc(reinterpret_cast<const float*>(f)), 0, 0, 0);
+    else
+      __hip_atomic_store(f, (unsigned)(step + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// flags of (dir, group, chain, row block): [32 slices][2 k halves] words
+__device__ __forceinline__ unsigned* dc_flags(const GruPArgs& a, int dir, int group, int c, int rb) {
+  return a.counters + (((dir * a.G + group) * 2 + c) * 2 + rb) * 64;
+}
+
+size_t dc_fwd_lds_floats(int H) { return (size_t)48 * (H + 4) + 16 * 32 * kDcXF + 8 * 128 + 16; }
+
+// LDS: W slice [48][H + 4] | combine [2 c][2 rb][2 parity][2 sender kh][32 slots][kDcXF] |
+// transpose tiles [8 waves][16][8] | pair flags [8]
+template <int H, bool FUSED>
+__global__ __launch_bounds__(512, 1) void gru_fwd_persistent_dc_kernel(GruPArgs a) {
+  constexpr int WP = H + 4, NKB = H / 16, KB2 = NKB / 2;
+  static_assert(KB2 == 16, "the k half is 16 k blocks (H = 512)");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Ws = smem;
+  float* xch = Ws + 48 * WP;
+  float* tp = xch + 16 * 32 * kDcXF;
+  unsigned* pf = reinterpret_cast<unsigned*>(tp + 8 * 128);
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = w >> 2, rb = (w >> 1) & 1, kh = w & 1;
+  const int lr = lane & 15, lq = lane >> 4;
+  int dir, group, slice;
+  bool local;
+  place(a, H / kUnits, dir, group, slice, local);
+  trace_id(a, dir, group, slice);
+  const int T = a.T, j0 = slice * kUnits, j = j0 + lr;
+  const int rbase = a.b_begin + group * kRows + 32 * c + 16 * rb;   // the wave's 16-row block
+  const int b_last = a.b_end - 1;
+  const bool own = (lr >> 3) == kh;   // after the combine this lane's unit belongs to this wave
+
+  {  // this slice of W_hh[dir] -> LDS (read once per layer)
+    const float* W = a.w_hh + (size_t)dir * 3 * H * H;
+    for (int v = tid; v < 3 * kUnits * H / 4; v += 512) {
+      const int cc = v / (H / 4), kq = (v % (H / 4)) * 4, g = cc / kUnits, jj = cc % kUnits;
+      st4(Ws + cc * WP + kq, ld4(W + (size_t)(g * H + j0 + jj) * H + kq));
+    }
+  }
+  if (tid < 8) pf[tid] = 0;
+  // fused input projection (in <= 64): this wave's k half of the input quads, W_ih in registers
+  constexpr bool fused = FUSED;
+  const int nq = fused ? (a.in + 3) / 4 : 0, mh = (nq + 1) / 2;
+  const int m0 = kh ? mh : 0, m1 = kh ? nq : mh;   // quads [m0, m1), at most 8
+  constexpr int NX = FUSED ? 8 : 1;
+  float wx[3][NX];
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int k = 4 * (m0 + i) + lq;
+      wx[g][i] = (fused && m0 + i < m1 && k < a.in) ? a.w_ih[((size_t)dir * 3 * H + g * H + j) * a.in + k] : 0.f;
+    }
+  float xv[NX];
+  auto load_xh = [&](int t) {
+    const float* xr = a.x_in + ((size_t)min(rbase + lr, b_last) * T + t) * a.in;
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int k = 4 * (m0 + i) + lq;
+      xv[i] = (m0 + i < m1 && k < a.in) ? xr[k] : 0.f;
+    }
+  };
+  if constexpr (FUSED) load_xh(dir == 0 ? 0 : T - 1);
+  const float bir = fused ? a.b_ih[dir * 3 * H + j] : 0.f, biz = fused ? a.b_ih[dir * 3 * H + H + j] : 0.f,
+              bin = fused ? a.b_ih[dir * 3 * H + 2 * H + j] : 0.f;
+  const float bhr = a.b_hh[dir * 3 * H + j], bhz = a.b_hh[dir * 3 * H + H + j], bhn = a.b_hh[dir * 3 * H + 2 * H + j];
+  __syncthreads();
+
+  const int Gp = a.G;
+  const __amdgpu_buffer_rsrc_t rx = rsrc(a.xbuf + (size_t)dir * kHandoffSlots * Gp * 64 * H);   // [3][Gp][4][NKB][64][4]
+  unsigned* myflags = dc_flags(a, dir, group, c, rb);
+  const int rot = slice & (KB2 - 1);   // per-slice k rotation within the half (spreads the L2 channels)
+  const int slot_id = (lr & 7) + 8 * lq;
+  float* mytp = tp + w * 128;
+  float hreg[4] = {0.f, 0.f, 0.f, 0.f};
+
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? step : T - 1 - step;
+    stamp(a, step, 0);
+    float gr[4], gz[4], gn[4];
+    f32x4 ax[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    if constexpr (FUSED) {   // this wave's k half of the step's input projection, before the wait
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        if (m0 + i >= m1) break;   // uniform
+#pragma unroll
+        for (int g = 0; g < 3; ++g) ax[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[i], wx[g][i], ax[g], 0, 0, 0);
+      }
+      if (step + 1 < T) load_xh(dir == 0 ? t + 1 : t - 1);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {   // input projections of the lane's cells (written by the gi GEMM)
+        const int b = min(rbase + lq * 4 + r, b_last);
+        const float* gi = a.gi + ((size_t)b * T + t) * 6 * H + dir * 3 * H;
+        gr[r] = gi[j];
+        gz[r] = gi[H + j];
+        gn[r] = gi[2 * H + j];
+      }
+    }
+    f32x4 acc[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    if (step > 0) {
+      dc_wait(a, myflags + 32 * kh, step);
+      stamp(a, step, 1);
+      dc_stamp_chain1(a, step);
+      const unsigned base =
+          (unsigned)((((((size_t)((step - 1) % kHandoffSlots) * Gp + group) * 4 + 2 * c + rb) * NKB + KB2 * kh) * 64 + lane) * 16);
+      v4f hv[KB2];
+#pragma unroll
+      for (int i = 0; i < KB2; ++i) hv[i] = ld4_sc1(rx, base + ((i + rot) & (KB2 - 1)) * 1024);
+      __builtin_amdgcn_sched_barrier(0);
+      v4f wv[2][3];
+#pragma unroll
+      for (int g = 0; g < 3; ++g) wv[0][g] = ld4(Ws + (g * kUnits + lr) * WP + (KB2 * kh + rot) * 16 + 4 * lq);
+#pragma unroll
+      for (int i = 0; i < KB2; ++i) {
+        const int cur = i & 1;
+        if (i + 1 < KB2) {
+          const int kn = KB2 * kh + ((i + 1 + rot) & (KB2 - 1));
+#pragma unroll
+          for (int g = 0; g < 3; ++g) wv[cur ^ 1][g] = ld4(Ws + (g * kUnits + lr) * WP + kn * 16 + 4 * lq);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[i][s], wv[cur][g][s], acc[g], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 12; ++q) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (a.trace) {
+        asm volatile("" ::"v"(acc[0][0]), "v"(acc[1][0]), "v"(acc[2][0]));
+        stamp(a, step, 2);
+      }
+    }
+    // k-half combine: the partner's lanes get this wave's partial sums of their units
+    {
+      const int par = step & 1;
+      float* out = xch + ((((c * 2 + rb) * 2 + par) * 2 + kh) * 32 + slot_id) * kDcXF;
+      const float* in = xch + ((((c * 2 + rb) * 2 + par) * 2 + (kh ^ 1)) * 32 + slot_id) * kDcXF;
+      if (!own) {
+#pragma unroll
+        for (int g = 0; g < 3; ++g) st4(out + 4 * g, v4f{acc[g][0], acc[g][1], acc[g][2], acc[g][3]});
+        if (fused)
+#pragma unroll
+          for (int g = 0; g < 3; ++g) st4(out + 12 + 4 * g, v4f{ax[g][0], ax[g][1], ax[g][2], ax[g][3]});
+      }
+      dc_pair_sync(a, pf, w, step);
+      if (own) {
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          const v4f o = ld4(in + 4 * g);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[g][r] = kh == 0 ? acc[g][r] + o[r] : o[r] + acc[g][r];
+        }
+        if (fused) {
+#pragma unroll
+          for (int g = 0; g < 3; ++g) {
+            const v4f o = ld4(in + 12 + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ax[g][r] = kh == 0 ? ax[g][r] + o[r] : o[r] + ax[g][r];
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            gr[r] = ax[0][r] + bir;
+            gz[r] = ax[1][r] + biz;
+            gn[r] = ax[2][r] + bin;
+          }
+        }
+      }
+    }
+    // cell update of the owner lanes (rows 4 lq + r of the block, unit j), h -> the transpose tile
+    float gsv[4][4];
+    if (own) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ghn = acc[2][r] + bhn;
+        const float rg = sigmoidf_(gr[r] + (acc[0][r] + bhr));
+        const float zg = sigmoidf_(gz[r] + (acc[1][r] + bhz));
+        const float ng = tanhf(gn[r] + rg * ghn);
+        const float h = (1.0f - zg) * ng + zg * hreg[r];
+        hreg[r] = h;
+        mytp[(4 * lq + r) * 8 + (lr & 7)] = h;
+        gsv[r][0] = rg;
+        gsv[r][1] = zg;
+        gsv[r][2] = ng;
+        gsv[r][3] = ghn;
+      }
+    }
+    dc_wave_lds_fence();
+    stamp(a, step, 3);
+    // publish: lane l < 32 = (q = l >> 4, row = l & 15) holds units 8 kh + 4 q .. + 3 of its row; the
+    // chunk (row block, k block = slice) has them at fragment lanes 32 kh + l
+    const int prow = lane & 15, pq = (lane >> 4) & 1;
+    const v4f hv4 = ld4(mytp + prow * 8 + 4 * pq);
+    const bool prow_ok = rbase + prow <= b_last;
+    if (lane < 32 && step + 1 < T && prow_ok)
+      st4_ho(rx, (unsigned)((((((size_t)(step % kHandoffSlots) * Gp + group) * 4 + 2 * c + rb) * NKB + slice) * 64 +
+                             32 * kh + lane) * 16), hv4, local);
+    dc_flag(a, myflags + 2 * slice + kh, step, local);
+    stamp(a, step, 4);
+    if (lane < 32 && prow_ok) st4(a.y + ((size_t)(rbase + prow) * T + t) * 2 * H + dir * H + j0 + 8 * kh + 4 * pq, hv4);
+    if (own) store_gates_il(a, gsv, dir, t, rbase + 4 * lq, b_last, j);
+  }
+}
+
+
+// The backward recurrence in the same two-chain form: wave (c, rb, kh) sums dg_next . W_hh over the
+// k half of slices 16 kh .. 16 kh + 15 (all three gates of each: 48 of the 96 k blocks, 8 chunks in
+// flight per buffer), the pair combines through LDS, the owner lanes (units 8 kh .. 8 kh + 7) run the
+// cell backward and publish (dar, daz, dan * r) of their 16 rows x 8 units into the three gate chunks.
+size_t dc_bwd_lds_floats(int H) { return (size_t)16 * (3 * H + 4) + 16 * 32 * 4 + 8 * 512 + 16; }
+
+template <int H>
+__global__ __launch_bounds__(512, 1) void gru_bwd_persistent_dc_kernel(GruPArgs a) {
+  constexpr int WP = 3 * H + 4, NKB = 3 * H / 16, S = H / kUnits, CH = 8, NCH = 3 * (S / 2) / CH;   // 48 blocks, 6 chunks
+  static_assert(S == 32 && NCH * CH == 48, "H = 512");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Wt = smem;                        // [16 units][3H + 4]
+  float* xch = Wt + 16 * WP;               // [2 c][2 rb][2 parity][2 sender][32 slots][4]
+  float* tp = xch + 16 * 32 * 4;           // [8 waves][16 rows][4 (dar, daz, dan r, dan)][8 units]
+  unsigned* pf = reinterpret_cast<unsigned*>(tp + 8 * 512);
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = w >> 2, rb = (w >> 1) & 1, kh = w & 1;
+  const int lr = lane & 15, lq = lane >> 4;
+  int dir, group, slice;
+  bool local;
+  place(a, S, dir, group, slice, local);
+  trace_id(a, dir, group, slice);
+  const int T = a.T, B = a.B, j0 = slice * kUnits, j = j0 + lr;
+  const int rbase = a.b_begin + group * kRows + 32 * c + 16 * rb;
+  const int b_last = a.b_end - 1;
+  const bool own = (lr >> 3) == kh;
+
+  {  // W_hh[dir][c][j0 .. j0+15] for all 3H rows c, stored transposed [jj][c]
+    const float* W = a.w_hh + (size_t)dir * 3 * H * H;
+    for (int v = tid; v < 3 * H * kUnits / 4; v += 512) {
+      const int cc = v / (kUnits / 4), jq = (v % (kUnits / 4)) * 4;
+      const v4f wv = ld4(W + (size_t)cc * H + j0 + jq);
+      Wt[(jq + 0) * WP + cc] = wv.x;
+      Wt[(jq + 1) * WP + cc] = wv.y;
+      Wt[(jq + 2) * WP + cc] = wv.z;
+      Wt[(jq + 3) * WP + cc] = wv.w;
+    }
+  }
+  if (tid < 8) pf[tid] = 0;
+  __syncthreads();
+
+  float* dgh_dir = a.dgh + (size_t)dir * B * T * 3 * H;
+  const int Gp = a.G;
+  const __amdgpu_buffer_rsrc_t rg_ = rsrc(a.xbuf + (size_t)dir * kHandoffSlots * Gp * 64 * 3 * H);   // [3][Gp][4][NKB][64][4]
+  unsigned* myflags = dc_flags(a, dir, group, c, rb);
+  const int slot_id = (lr & 7) + 8 * lq;
+  float* mytp = tp + w * 512;
+  // the wave's 48 k blocks: i -> gate i / 16, slice 16 kh + ((i + rot) mod 16), k block g * S + slice
+  const int rot = slice & 15;
+  auto kblock = [&](int i) { const int g = i >> 4; return g * S + 16 * kh + (((i & 15) + rot) & 15); };
+  float dhz[4] = {0.f, 0.f, 0.f, 0.f};
+
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? T - 1 - step : step;
+    const int tprev = dir == 0 ? t - 1 : t + 1;
+    const bool edge = (step == T - 1);   // h_prev = 0 here
+    stamp(a, step, 0);
+    float g_r[4], g_z[4], g_n[4], g_h[4], dyv[4], hpv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {   // epilogue operands of the lane's cells (earlier launches)
+      const int b = min(rbase + lq * 4 + r, b_last);
+      const v4f gv = *reinterpret_cast<const v4f*>(a.gates + (((size_t)dir * T + t) * B + b) * 4 * H + 4 * j);
+      g_r[r] = gv.x;
+      g_z[r] = gv.y;
+      g_n[r] = gv.z;
+      g_h[r] = gv.w;
+      dyv[r] = a.dy[((size_t)b * T + t) * 2 * H + dir * H + j];
+      hpv[r] = edge ? 0.f : a.y_in[((size_t)b * T + tprev) * 2 * H + dir * H + j];
+    }
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    if (step > 0) {
+      dc_wait(a, myflags + 32 * kh, step);
+      stamp(a, step, 1);
+      dc_stamp_chain1(a, step);
+      const unsigned base =
+          (unsigned)(((((size_t)((step - 1) % kHandoffSlots) * Gp + group) * 4 + 2 * c + rb) * NKB * 64 + lane) * 16);
+      v4f dv[2][CH];
+#pragma unroll
+      for (int i = 0; i < CH; ++i) dv[0][i] = ld4_sc1(rg_, base + kblock(i) * 1024);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const int cur = ch & 1;
+        if (ch + 1 < NCH) {
+#pragma unroll
+          for (int i = 0; i < CH; ++i) dv[cur ^ 1][i] = ld4_sc1(rg_, base + kblock((ch + 1) * CH + i) * 1024);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        v4f wv[2];
+        wv[0] = ld4(Wt + lr * WP + kblock(ch * CH) * 16 + 4 * lq);
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int cw = i & 1;
+          if (i + 1 < CH) wv[cw ^ 1] = ld4(Wt + lr * WP + kblock(ch * CH + i + 1) * 16 + 4 * lq);
+          __builtin_amdgcn_sched_barrier(0);
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][i].x, wv[cw].x, acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][i].y, wv[cw].y, acc[1], 0, 0, 0);
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][i].z, wv[cw].z, acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[cur][i].w, wv[cw].w, acc[1], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (a.trace) {
+        asm volatile("" ::"v"(acc[0][0]), "v"(acc[1][0]));
+        stamp(a, step, 2);
+      }
+    }
+    // k-half combine (p0 + p1) of the recurrent sum
+    float dsum[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dsum[r] = acc[0][r] + acc[1][r];
+    {
+      const int par = step & 1;
+      float* out = xch + ((((c * 2 + rb) * 2 + par) * 2 + kh) * 32 + slot_id) * 4;
+      const float* in = xch + ((((c * 2 + rb) * 2 + par) * 2 + (kh ^ 1)) * 32 + slot_id) * 4;
+      if (!own) st4(out, v4f{dsum[0], dsum[1], dsum[2], dsum[3]});
+      dc_pair_sync(a, pf, w, step);
+      if (own) {
+        const v4f o = ld4(in);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dsum[r] = kh == 0 ? dsum[r] + o[r] : o[r] + dsum[r];
+      }
+    }
+    if (own) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float dh = dyv[r];
+        if (step > 0) dh += dsum[r] + dhz[r];
+        const float rg = g_r[r], zg = g_z[r], ng = g_n[r], ghn = g_h[r], hp = hpv[r];
+        const float dn = dh * (1.0f - zg);
+        const float daz = dh * (hp - ng) * zg * (1.0f - zg);
+        const float dan = dn * (1.0f - ng * ng);
+        const float dar = dan * ghn * rg * (1.0f - rg);
+        dhz[r] = dh * zg;
+        float* o = mytp + (4 * lq + r) * 32 + (lr & 7);
+        o[0] = dar;
+        o[8] = daz;
+        o[16] = dan * rg;
+        o[24] = dan;
+      }
+    }
+    dc_wave_lds_fence();
+    stamp(a, step, 3);
+    // lane l < 32 = (q, row): units 8 kh + 4 q .. + 3 of its row, for each gate image
+    const int prow = lane & 15, pq = (lane >> 4) & 1;
+    const bool prow_ok = rbase + prow <= b_last;
+    v4f val[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) val[g] = ld4(mytp + prow * 32 + 8 * g + 4 * pq);
+    if (lane < 32 && !edge && prow_ok) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+        st4_ho(rg_, (unsigned)((((((size_t)(step % kHandoffSlots) * Gp + group) * 4 + 2 * c + rb) * NKB + g * S + slice) * 64 +
+                                32 * kh + lane) * 16), val[g], local);
+    }
+    dc_flag(a, myflags + 2 * slice + kh, step, local);
+    stamp(a, step, 4);
+    if (lane < 32 && prow_ok) {
+      const int b = rbase + prow, u = j0 + 8 * kh + 4 * pq;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        if (!edge) {
+          st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + u, val[g]);
+        } else {
+          st4(a.dgh_edge + ((size_t)dir * B + b) * 3 * H + g * H + u, val[g]);
+          st4(dgh_dir + ((size_t)b * T + t) * 3 * H + g * H + u, v4f{0.f, 0.f, 0.f, 0.f});
+        }
+        st4(a.dgi + ((size_t)b * T + t) * 6 * H + dir * 3 * H + g * H + u, g == 2 ? val[3] : val[g]);
+      }
     }
   }
 }
@@ -1517,6 +1967,26 @@ const void* kernel_ptr(bool backward, int prec) {
 }
 
 template <int H>
+int dc_occupancy_ok() {
+  static std::mutex mu;
+  static int occ = -1;
+  std::lock_guard<std::mutex> lk(mu);
+  if (occ < 0) {
+    int o2 = 0;
+    const std::pair<const void*, size_t> ks[3] = {
+        {reinterpret_cast<const void*>(gru_fwd_persistent_dc_kernel<H, false>), dc_fwd_lds_floats(H) * 4},
+        {reinterpret_cast<const void*>(gru_fwd_persistent_dc_kernel<H, true>), dc_fwd_lds_floats(H) * 4},
+        {reinterpret_cast<const void*>(gru_bwd_persistent_dc_kernel<H>), dc_bwd_lds_floats(H) * 4}};
+    for (const auto& k : ks) {
+      SRK_CHECK_HIP(hipFuncSetAttribute(k.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)k.second));
+      SRK_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, k.first, 512, k.second));
+      occ = occ < 0 ? o2 : std::min(occ, o2);
+    }
+  }
+  return occ >= 1 ? 1 : 0;
+}
+
+template <int H>
 int occupancy_ok(bool backward, int prec, int grid) {
   static std::mutex mu;
   static int cus = -1, occ[2][3] = {{-1, -1, -1}, {-1, -1, -1}};
@@ -1573,6 +2043,8 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
   const int rows_g = lp2 ? kRows2 : kRows, slices = lp2 ? a.H / kUnits2 : a.H / kUnits;
   if (lp2 && lp2_occupancy_ok<512>(backward, prec) <= 0)
     SRK_REQUIRE(false, SRK_ERR_INVALID, "gru persistent: the 32 x 32 kernels do not fit one workgroup per CU");
+  // fp32 forward: the two-chain 8-wave kernel (same grid, W slice and outputs)
+  const bool dc = prec == kPrecF32 && g_opt_gru_dc && dc_occupancy_ok<512>() > 0;
   for (int c0 = 0; c0 < a.B; c0 += rows_per_launch) {
     GruPArgs ac = a;
     ac.trace = g_opt_gru_trace;
@@ -1591,9 +2063,16 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     const double flops = 2.0 * 2.0 * (double)(ac.b_end - c0) * 3 * a.H * a.H * (a.T - 1);
     ProfScope prof(backward ? (prec == kPrecF32 ? "gru_bwd_seq" : "gru_bwd_seq_lp")
                             : (prec == kPrecF32 ? "gru_fwd_seq" : "gru_fwd_seq_lp"), s, flops);
-    prof.detail("gru_%s_persistent%s_kernel B%d T%d chunk%d", backward ? "bwd" : "fwd", lp2 ? "_lp2" : (prec == kPrecF32 ? "" : "_lp"),
+    prof.detail("gru_%s_persistent%s_kernel B%d T%d chunk%d", backward ? "bwd" : "fwd",
+                dc ? "_dc" : lp2 ? "_lp2" : (prec == kPrecF32 ? "" : "_lp"),
                 ac.b_end - c0, a.T, ac.chunk);
-    if (lp2)
+    if (dc && backward)
+      hipLaunchKernelGGL((gru_bwd_persistent_dc_kernel<512>), grid, dim3(512), dc_bwd_lds_floats(512) * 4, s, ac);
+    else if (dc && ac.x_in)
+      hipLaunchKernelGGL((gru_fwd_persistent_dc_kernel<512, true>), grid, dim3(512), dc_fwd_lds_floats(512) * 4, s, ac);
+    else if (dc)
+      hipLaunchKernelGGL((gru_fwd_persistent_dc_kernel<512, false>), grid, dim3(512), dc_fwd_lds_floats(512) * 4, s, ac);
+    else if (lp2)
       hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(lp2_kernel_ptr<512>(backward, prec))),
                          grid, dim3(256), lp2_lds_bytes(512, backward), s, ac);
     else

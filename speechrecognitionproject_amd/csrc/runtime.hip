@@ -29,6 +29,7 @@ unsigned long long* g_opt_gru_trace = nullptr;
 unsigned g_opt_gru_spin_limit = 0;
 int g_opt_gru_xcd_local = 1;
 int g_opt_gru_lp2 = 1;
+int g_opt_gru_dc = 1;
 std::atomic<int64_t> g_scratch_gen{0};
 
 static thread_local std::string g_last_error;
@@ -363,6 +364,10 @@ int srk_set_option(const char* name, int64_t value) {
   }
   if (n == "gru_xcd_local") {   // persistent GRU: XCD-local hand-off when every XCD hosts one (dir, group)
     srk::g_opt_gru_xcd_local = value != 0;
+    return SRK_OK;
+  }
+  if (n == "gru_fp32_dual_chain") {   // fp32 recurrence: 8-wave workgroups running two row chains (1) or the 4-wave form (0)
+    srk::g_opt_gru_dc = value != 0;
     return SRK_OK;
   }
   if (n == "gru_lp_32x32") {   // 16-bit recurrence: 32 x 32 workgroups (1) or 64 rows x 16 units (0)

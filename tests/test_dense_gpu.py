@@ -298,3 +298,36 @@ def test_plain_autograd_gets_gradients_without_flatparams(gpu):
     assert len(fired) == 2
     for p, g in zip(params, grads):
         assert torch.allclose(p.grad, 2 * g, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,T,IN", [(256, 51, 39), (256, 13, 1024), (512, 9, 24), (300, 7, 24), (67, 11, 1024), (1, 5, 39)])
+def test_bigru_fp32_dual_chain_matches_four_wave(gpu, B, T, IN):
+    """The fp32 two-chain recurrence kernels, forward and backward (8 waves, k halves combined through
+    LDS, per-wave flags, a 3-slot hand-off ring; option gru_fp32_dual_chain, default on) against the
+    4-wave kernels: the same cell math with the recurrent k sum split in two halves (2e-5 relative), the fused layer-0
+    projection (IN <= 64) and the gi-GEMM path, full / partial / chunked (B = 300, 512) grids; and
+    run twice — bitwise the same both times (deterministic order, flags and ring reset per launch)."""
+    from speechrecognitionproject_amd import _lib
+    H = 512
+    torch.manual_seed(5)
+    mine = snn.BiGRU(IN, H, num_layers=1).cuda()
+    x = torch.randn(B, T, IN)
+    w = torch.randn(B, T, 2 * H)
+    outs = {}
+    try:
+        for mode in (1, 1, 0):
+            _lib.set_option("gru_fp32_dual_chain", mode)
+            mine.zero_grad()
+            xm = x.cuda().requires_grad_(True)
+            ym, _ = mine(xm)
+            (ym * w.cuda()).sum().backward()
+            outs.setdefault(mode, []).append([ym.detach().cpu(), xm.grad.cpu()] + [p.grad.cpu() for p in mine.parameters()])
+    finally:
+        _lib.set_option("gru_fp32_dual_chain", 1)
+    assert _lib.spin_timeouts() == 0
+    for a, b in zip(outs[1][0], outs[1][1]):
+        assert torch.equal(a, b)
+    for i, (a, b) in enumerate(zip(outs[1][0], outs[0][0])):
+        err = float((a - b).abs().max() / (b.abs().max() + 1e-30))
+        assert err <= 2e-5, (i, err)
+

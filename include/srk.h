@@ -71,6 +71,11 @@ int64_t srk_spin_timeouts(void);
  * sync = 0 it costs no device synchronization (it sees timeouts of work the GPU has reached);
  * sync = 1 synchronizes the device first.  Option "gru_spin_limit" (test hook) shortens the wait. */
 int srk_health_check(int sync);
+/* Host-side audit of the persistent GRU's step-ordering words for a batch of B rows at the given
+ * precision (0 fp32, 1 bf16, 2 fp16): *max_word = largest counter / flag word any workgroup of the
+ * planned launches touches, *chunks = launches, *census = first word of the XCD census (must exceed
+ * *max_word).  No GPU needed.                                                                     */
+int srk_gru_audit_words(int64_t B, int precision, int backward, int64_t* max_word, int64_t* chunks, int64_t* census);
 int srk_health_reset(void);
 
 /* ---------------------------------------------------------------- feature extraction

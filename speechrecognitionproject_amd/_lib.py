@@ -33,6 +33,8 @@ _SIGS = {
     "srk_set_option": [ctypes.c_char_p, _I64],
     "srk_spin_timeouts": [],
     "srk_scratch_generation": [],
+    "srk_gru_audit_words": [_I64, _I, _I, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                            ctypes.POINTER(ctypes.c_int64)],
     "srk_health_check": [_I],
     "srk_health_reset": [],
     "srk_fbank_fwd": [_P, _I64, _P, _P],

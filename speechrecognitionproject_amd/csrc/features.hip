@@ -641,7 +641,7 @@ __device__ __forceinline__ float mix_one(short s, double g, short n) {
 }
 
 __global__ void noise_mix_kernel(const int16_t* __restrict__ pcm, const int16_t* __restrict__ bank,
-                                 int64_t bank_len, const int64_t* __restrict__ file_idx,
+                                 int64_t n_files, int64_t bank_len, const int64_t* __restrict__ file_idx,
                                  const int64_t* __restrict__ offs, const double* __restrict__ gains,
                                  int64_t n_clips, float* __restrict__ out) {
   // 8 samples per thread: 16-B int16 loads of pcm, 16-B + 16-B fp32 stores.
@@ -650,7 +650,11 @@ __global__ void noise_mix_kernel(const int16_t* __restrict__ pcm, const int16_t*
   if (i8 >= total8) return;
   const int64_t clip = i8 / (kPcmLen / 8);
   const int s0 = (int)(i8 % (kPcmLen / 8)) * 8;
-  const int16_t* nz = bank + file_idx[clip] * bank_len + offs[clip] + s0;
+  // the host validates the draws before an eager launch; inside a captured graph it cannot read them,
+  // so the file and offset are also clamped here: an invalid draw can never read outside the bank
+  const int64_t f = min(max(file_idx[clip], (int64_t)0), n_files - 1);
+  const int64_t off = min(max(offs[clip], (int64_t)0), bank_len - kPcmLen);
+  const int16_t* nz = bank + f * bank_len + off + s0;
   const double g = gains[clip];
   const short4 a = *reinterpret_cast<const short4*>(pcm + clip * kPcmLen + s0);
   const short4 b = *reinterpret_cast<const short4*>(pcm + clip * kPcmLen + s0 + 4);
@@ -748,7 +752,7 @@ int srk_noise_mix(const int16_t* pcm, const int16_t* bank, int64_t n_files, int6
   const int64_t blocks = (total8 + nt - 1) / nt;
   srk::ProfScope prof("noise_mix", srk::as_stream(stream), 128000.0 * (double)n_clips); // 32000+32000+64000 B/clip
   hipLaunchKernelGGL(srk::noise_mix_kernel, dim3((unsigned)blocks), dim3(nt), 0, srk::as_stream(stream), pcm, bank,
-                     bank_len, file_idx, offset, gain, n_clips, out);
+                     n_files, bank_len, file_idx, offset, gain, n_clips, out);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END

@@ -13,6 +13,14 @@ namespace srk {
 // words kCensusOff..+8; zeroed by a hipMemsetAsync of exactly this block before every launch.
 constexpr int kCounterFloats = 4096;
 constexpr int kCensusOff = 4080;
+// Word indices of the step-ordering state inside that block — host + device, so the kernels and
+// srk_gru_audit_words (a host-side check of every word a launch plan touches) share one arithmetic.
+__host__ __device__ constexpr int pw_counter(int dir, int G, int group) { return (dir * G + group) * 16; }
+__host__ __device__ constexpr int pw_flag64(int dir, int G, int group, int slot) { return (dir * G + group) * 32 + slot; }
+__host__ __device__ constexpr int pw_flag_lp2(int dir, int G, int group, int slot) { return (dir * G + group) * 16 + slot; }
+__host__ __device__ constexpr int pw_flag_dc(int dir, int G, int group, int c, int rb, int slot) {
+  return (((dir * G + group) * 2 + c) * 2 + rb) * 64 + slot;
+}
 // Hand-off ring depth of the persistent kernels (slots per direction in the workspace): the fp32
 // two-chain kernels need 3 (a wave waits only for the producers of its k half, see gru_persistent.hip)
 constexpr int kHandoffSlots = 3;

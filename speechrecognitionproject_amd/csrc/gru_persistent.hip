@@ -112,7 +112,7 @@ __device__ __forceinline__ void sync_wait(const GruPArgs& a, unsigned* cnt, int 
     return;
   }
   if (threadIdx.x < 64) {
-    unsigned* f = a.counters + (dir * a.G + group) * 32;
+    unsigned* f = a.counters + pw_flag64(dir, a.G, group, 0);
     const int lane = threadIdx.x;
     unsigned spins = 0;
     while (true) {
@@ -136,7 +136,7 @@ __device__ __forceinline__ void sync_arrive(const GruPArgs& a, unsigned* cnt, in
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned* f = a.counters + (dir * a.G + group) * 32 + slice;
+    unsigned* f = a.counters + pw_flag64(dir, a.G, group, slice);
     if (local)   // XCD-local: a plain store, kept in the XCD's L2 where the consumers' sc1 polls read it
       __builtin_amdgcn_raw_buffer_store_b32((unsigned)(step + 1), rsrc(reinterpret_cast<const float*>(f)), 0, 0, 0);
     else
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_kernel(GruPArgs a) 
   const int T = a.T, j0 = slice * kUnits, j = j0 + lr;
   const int b0 = a.b_begin + group * kRows;
   const int b_last = a.b_end - 1;
-  unsigned* cnt = a.counters + (dir * a.G + group) * 16;
+  unsigned* cnt = a.counters + pw_counter(dir, a.G, group);
 
   {  // this slice of W_hh[dir] -> LDS (read once per layer)
     const float* W = a.w_hh + (size_t)dir * 3 * H * H;
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_kernel(GruPArgs a) 
   const int T = a.T, B = a.B, j0 = slice * kUnits, j = j0 + lr;
   const int b0 = a.b_begin + group * kRows;
   const int b_last = a.b_end - 1;
-  unsigned* cnt = a.counters + (dir * a.G + group) * 16;
+  unsigned* cnt = a.counters + pw_counter(dir, a.G, group);
 
   {  // W_hh[dir][c][j0 .. j0+15] for all 3H rows c, stored transposed [jj][c]
     const float* W = a.w_hh + (size_t)dir * 3 * H * H;
@@ -700,7 +700,7 @@ __device__ __forceinline__ void dc_flag(const GruPArgs& a, unsigned* f, int step
 
 // flags of (dir, group, chain, row block): [32 slices][2 k halves] words
 __device__ __forceinline__ unsigned* dc_flags(const GruPArgs& a, int dir, int group, int c, int rb) {
-  return a.counters + (((dir * a.G + group) * 2 + c) * 2 + rb) * 64;
+  return a.counters + pw_flag_dc(dir, a.G, group, c, rb, 0);
 }
 
 size_t dc_fwd_lds_floats(int H) { return (size_t)48 * (H + 4) + 16 * 32 * kDcXF + 8 * 128 + 16; }
@@ -1133,7 +1133,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp_kernel(GruPArgs 
   const int T = a.T, j0 = slice * kUnits, j = j0 + lr;
   const int b0 = a.b_begin + group * kRows;
   const int b_last = a.b_end - 1;
-  unsigned* cnt = a.counters + (dir * a.G + group) * 16;
+  unsigned* cnt = a.counters + pw_counter(dir, a.G, group);
 
   {  // this slice of W_hh[dir], rounded to 16 bits -> LDS (read once per layer)
     const float* W = a.w_hh + (size_t)dir * 3 * H * H;
@@ -1269,7 +1269,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp_kernel(GruPArgs 
   const int T = a.T, B = a.B, j0 = slice * kUnits, j = j0 + lr;
   const int b0 = a.b_begin + group * kRows;
   const int b_last = a.b_end - 1;
-  unsigned* cnt = a.counters + (dir * a.G + group) * 16;
+  unsigned* cnt = a.counters + pw_counter(dir, a.G, group);
 
   {  // W_hh[dir][c][j0 .. j0+15], all 3H rows c, transposed [jj][c] in 8-deep c packs
     const float* W = a.w_hh + (size_t)dir * 3 * H * H;
@@ -1467,7 +1467,7 @@ __device__ __forceinline__ void lp2_wait(const GruPArgs& a, int dir, int group, 
   const int lane = threadIdx.x & 63;
   unsigned spins = 0;
   if (per) {   // per-producer flags, this wave's producers only
-    unsigned* fl = a.counters + (dir * a.G + group) * 16 + first;
+    unsigned* fl = a.counters + pw_flag_lp2(dir, a.G, group, first);
     while (true) {
       const unsigned v = lane < count ? __hip_atomic_load(fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                       : 0xffffffffu;
@@ -1479,7 +1479,7 @@ __device__ __forceinline__ void lp2_wait(const GruPArgs& a, int dir, int group, 
       }
     }
   } else {     // the group's arrival counter (16 producers per step)
-    unsigned* cnt = a.counters + (dir * a.G + group) * 16;
+    unsigned* cnt = a.counters + pw_counter(dir, a.G, group);
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 16u * (unsigned)step) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins >= a.spin_limit) {
@@ -1496,13 +1496,13 @@ __device__ __forceinline__ void lp2_arrive(const GruPArgs& a, int dir, int group
   __syncthreads();
   if (threadIdx.x == 0) {
     if (per) {
-      unsigned* f = a.counters + (dir * a.G + group) * 16 + slice;
+      unsigned* f = a.counters + pw_flag_lp2(dir, a.G, group, slice);
       if (local)
         __builtin_amdgcn_raw_buffer_store_b32((unsigned)(step + 1), rsrc(reinterpret_cast<const float*>(f)), 0, 0, 0);
       else
         __hip_atomic_store(f, (unsigned)(step + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      __hip_atomic_fetch_add(a.counters + (dir * a.G + group) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(a.counters + pw_counter(dir, a.G, group), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -2135,3 +2135,52 @@ extern "C" int64_t srk_spin_timeouts(void) {
   if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(srk::g_spin_timeouts), sizeof(v)) != hipSuccess) return -1;
   return (int64_t)v;
 }
+
+// Host-side audit of the step-ordering words (tests/test_gru_audit.py, no GPU needed): plans the
+// launches of gru_persistent_launch for a batch of B rows (256-row chunks, the variant the current
+// options and precision select) and walks every word each workgroup polls, stores or adds to with
+// the kernels' own index helpers.  *max_word = the largest word touched (must stay below the census
+// at kCensusOff), *chunks = launches, *census = kCensusOff.  A fault that depends on the chunk
+// (b_begin > 0) would need a chunk-dependent word: none of these indices involves b_begin.
+extern "C" int srk_gru_audit_words(int64_t B, int precision, int backward, int64_t* max_word, int64_t* chunks,
+                                   int64_t* census) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(B > 0 && max_word && chunks && census && precision >= 0 && precision <= 2, SRK_ERR_INVALID,
+              "gru_audit_words: bad arguments");
+  using namespace srk;
+  const int rows_per_launch = gru_persistent_groups(512) * kRows;
+  const bool lp2 = precision != kPrecF32 && g_opt_gru_lp2;
+  const bool dc = precision == kPrecF32 && g_opt_gru_dc;
+  const int rows_g = lp2 ? kRows2 : kRows, S = lp2 ? 512 / kUnits2 : 512 / kUnits;
+  int64_t mx = -1, n = 0;
+  auto see = [&](int w) { mx = std::max<int64_t>(mx, w); };
+  for (int64_t c0 = 0; c0 < B; c0 += rows_per_launch, ++n) {
+    const int G = (int)((std::min<int64_t>(B, c0 + rows_per_launch) - c0 + rows_g - 1) / rows_g);
+    for (int dir = 0; dir < 2; ++dir)
+      for (int group = 0; group < G; ++group) {
+        see(pw_counter(dir, G, group));
+        if (dc) {
+          for (int c = 0; c < 2; ++c)
+            for (int rb = 0; rb < 2; ++rb)
+              for (int kh = 0; kh < 2; ++kh) {
+                for (int lane = 0; lane < 32; ++lane) see(pw_flag_dc(dir, G, group, c, rb, 32 * kh + lane));   // dc_wait
+                for (int slice = 0; slice < S; ++slice) see(pw_flag_dc(dir, G, group, c, rb, 2 * slice + kh));   // dc_flag
+              }
+        } else if (lp2) {
+          for (int first = 0; first < S; first += 8)
+            for (int lane = 0; lane < 8; ++lane) see(pw_flag_lp2(dir, G, group, first + lane));   // lp2_wait
+          for (int slice = 0; slice < S; ++slice) see(pw_flag_lp2(dir, G, group, slice));          // lp2_arrive
+        } else {
+          for (int lane = 0; lane < S; ++lane) see(pw_flag64(dir, G, group, lane));   // sync_wait
+          for (int slice = 0; slice < S; ++slice) see(pw_flag64(dir, G, group, slice));   // sync_arrive
+        }
+      }
+  }
+  (void)backward;   // the backward kernels use the same words as their forward twins
+  *max_word = mx;
+  *chunks = n;
+  *census = kCensusOff;
+  return SRK_OK;
+  SRK_API_END
+}
+

@@ -80,8 +80,9 @@ def noise_mix(pcm_i16, bank_i16, file_idx, offsets, gains, out=None):
     n = x.shape[0]
     if x.shape != (n, SEQ_LENGTH) or fi.numel() != n or of.numel() != n or g.numel() != n:
         raise SrkError("noise_mix: inconsistent shapes")
-    # host-side bounds check of the draws (the kernel trusts them)
-    if n and (int(of.min()) < 0 or int(of.max()) > bank.shape[1] - SEQ_LENGTH or int(fi.min()) < 0
+    # host-side bounds check of the draws (skipped inside a HIP-graph capture, where reading them back
+    # is not possible; the kernel clamps them into the bank either way)
+    if n and not torch.cuda.is_current_stream_capturing() and (int(of.min()) < 0 or int(of.max()) > bank.shape[1] - SEQ_LENGTH or int(fi.min()) < 0
               or int(fi.max()) >= bank.shape[0]):
         raise SrkError("noise_mix: file index / offset out of range")
     out = torch.empty((n, SEQ_LENGTH), device=dev, dtype=torch.float32) if out is None else out

@@ -26,8 +26,8 @@ class GraphedStep:
 
     def __init__(self, step, warmup=2):
         """warmup: eager calls of ``step`` on a side stream before the capture (>= 2 so every scratch
-        buffer reaches its size), or 0 when the caller has just run >= 2 eager steps of the same shapes
-        (training.py: real steps on real batches, no repeated step)."""
+        buffer reaches its size), or 0 when the caller has just run >= 2 steps of the same shapes on a
+        side stream itself (training.py: real steps on real batches, no repeated step)."""
         if warmup == 1 or warmup < 0:
             raise ValueError("GraphedStep: warmup must be 0 (caller warmed up) or >= 2")
         self.step = step
@@ -40,6 +40,9 @@ class GraphedStep:
                 for _ in range(warmup):
                     self.out = step()
             torch.cuda.current_stream().wait_stream(side)
+        # drop the warm-up's output: its autograd graph would keep the side stream's AccumulateGrad
+        # nodes alive into the capture
+        self.out = None
         torch.cuda.synchronize()
         self.generation = _lib.scratch_generation()
         self.graph = torch.cuda.CUDAGraph()

@@ -107,6 +107,7 @@ class GradReducer:
         """Reset per-step state; call before the forward pass of each step."""
         self.remaining = [len(ps) for _, _, ps in self.buckets]
         self.launched = [False] * len(self.buckets)
+        self.ready = set()
         self.works = []
         self.pending = 0
         self.held = []
@@ -125,10 +126,15 @@ class GradReducer:
         self.mark_ready([p])
 
     def mark_ready(self, params):
+        # idempotent per step: a layer that accumulates into .grad in place calls mark_ready after
+        # enqueueing its GEMMs, and autograd STILL runs that parameter's post-accumulate hook (with no
+        # gradient to add) afterwards; counting both would declare a bucket complete while some of
+        # its gradients are still to be computed and launch its all-reduce too early
         for p in params:
             i = self.bucket_of.get(id(p))
-            if i is None:
+            if i is None or id(p) in self.ready:
                 continue
+            self.ready.add(id(p))
             self.remaining[i] -= 1
             if self.remaining[i] == 0:
                 if self.pending > 0:

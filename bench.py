@@ -34,10 +34,10 @@ matrix-core operand precision (srk_set_option "matmul_precision"; fp16 adds a st
 With fp32, the same line also carries "bf16": the identical step re-timed with bf16 operands
 (BASELINE.json names bf16 for cfg2), with its own roofline against the dense bf16 peak.
 
-Step execution: after W warm-up steps the train step is captured once into a HIP graph
+Step execution: after W warm-up steps the train step is captured into HIP graphs
 (speechrecognitionproject_amd/graphs.py; per-step host values — the Adam step count and the dropout
-seed — live on the device) and the K timed steps are graph replays, each preceded by a device copy of
-that step's pre-staged batch into the graph's static input.  N > 1: forward + backward are one graph,
+seed — live on the device), one per pre-staged batch slot sharing one memory pool, and the K timed
+steps are graph replays.  N > 1: forward + backward are one graph,
 the flat gradient buffer is all-reduced over RCCL between the replay and the Adam launch.
 --no-graph times the eager step instead (N > 1: bucketed all-reduces overlapped with backward).
 The per-kernel HIP-event timers cannot run inside a graph: kernel times ("kernels", "roofline")
@@ -310,7 +310,6 @@ class Workload:
         pool = args.pool
         x, y = synthetic_clips(pool * B, seed=1000 + rank, clip=30000 if model_name == "spec_bgru" else 32767)
         self.lab = torch.from_numpy(y).to(dev).view(pool, B)
-        self.static_lab = self.lab[0].clone()
         if model_name == "spec_bgru":
             # cfg5: int16 PCM + resident noise bank; the per-clip (file, offset, gain) draws of
             # dataset.py:190-193 are made up front (numpy), the mix runs on the device every step.
@@ -319,10 +318,8 @@ class Workload:
             self.bank = torch.from_numpy(synthetic_noise_bank()).to(dev)
             self.draws = [torch.from_numpy(a).to(dev).view(pool, B) for a in synthetic_noise_draws(pool * B, seed=2 + rank)]
             self.mixed = torch.empty((B, 16000), device=dev)
-            self.static = [self.pcm16[0].clone()] + [d[0].clone() for d in self.draws]
         else:
             self.pcm = torch.from_numpy(x).to(dev).view(pool, B, -1)
-            self.static = [self.pcm[0].clone()]
 
     # ---- inputs
     def _inputs(self, srcs):
@@ -335,12 +332,6 @@ class Workload:
         if self.name == "spec_bgru":
             return [self.pcm16[j]] + [d[j] for d in self.draws]
         return [self.pcm[j]]
-
-    def _feed(self, i):
-        """Copy step i's pre-staged batch into the graph's static inputs (device to device)."""
-        for dst, src in zip(self.static, self._batch(i)):
-            dst.copy_(src, non_blocking=True)
-        self.static_lab.copy_(self.lab[i % self.args.pool], non_blocking=True)
 
     # ---- the step
     def _fwd_bwd(self, srcs, lab):
@@ -365,7 +356,8 @@ class Workload:
         return loss
 
     def _graph_body(self):
-        loss = self._fwd_bwd(self.static, self.static_lab)
+        j = self._slot
+        loss = self._fwd_bwd(self._batch(j), self.lab[j])
         if self.world == 1:
             self.opt.step()
         return loss
@@ -380,12 +372,17 @@ class Workload:
         self.opt.grad_scale = 1.0 / (self.world * self.loss_scale)
         self.reducer = (parallel.GradReducer(self.flat, bucket_mb=args.bucket_mb)
                         if (self.world > 1 and args.overlap and not graph) else None)
-        g = None
+        graphs = []
         if graph:
+            # one graph per pre-staged batch slot, sharing one memory pool: each reads its own resident
+            # batch (no per-step input copy); the first capture's warm-up covers the others
             from speechrecognitionproject_amd.graphs import GraphedStep
-            self._feed(0)
-            g = GraphedStep(self._graph_body, warmup=max(2, warmup))
-            loss = g.replay()        # one untimed replay: the captured step runs once before timing
+            for j in range(args.pool):
+                self._slot = j
+                graphs.append(GraphedStep(self._graph_body, warmup=max(2, warmup) if j == 0 else 0,
+                                          pool=graphs[0].pool() if graphs else None))
+            for g in graphs:
+                loss = g.replay()    # one untimed replay of each: every captured step runs once before timing
         else:
             for i in range(warmup):
                 loss = self.eager_step(i)
@@ -400,9 +397,8 @@ class Workload:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(steps):
-            if g is not None:
-                self._feed(i)
-                loss = g.replay()
+            if graphs:
+                loss = graphs[i % args.pool].replay()
                 if self.world > 1:
                     self._exchange_and_update()
             else:
@@ -416,9 +412,9 @@ class Workload:
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             el = float(t.item())
         final_loss = float(loss.item())
-        if g is not None:
+        for g in graphs:
             g.release()
-            del g
+        del graphs
         eager_ms = None
         if not args.no_prof and graph:
             # kernel timers cannot run inside a graph: an eager pass of the same step, timed per kernel

@@ -9,7 +9,9 @@ HIP graph (torch.cuda.graph: a private memory pool, capture on a side stream) an
 whole step with one ``hipGraphLaunch``, removing the per-kernel host launch cost.
 
 Inputs must sit at fixed addresses: the caller copies each batch into ``static`` tensors it passes
-to the step function, then calls ``replay()``.
+to the step function, then calls ``replay()`` — or, when the batches are already resident (bench.py's
+pre-staged pool), captures one graph per batch slot sharing one memory pool, which avoids the copy
+(a device-to-device ``copy_`` goes through a DMA engine: measured +0.3-0.7 ms per 16 MB batch).
 
 Constraints (checked by the parity tests, tests/test_graphs_gpu.py): every library scratch buffer must
 already have its final size when the capture starts (the warm-up runs the step at least twice), and
@@ -24,7 +26,7 @@ from . import _lib
 class GraphedStep:
     """``step()`` -> its output tensor(s), captured after ``warmup`` eager calls on a side stream."""
 
-    def __init__(self, step, warmup=2):
+    def __init__(self, step, warmup=2, pool=None):
         """warmup: eager calls of ``step`` on a side stream before the capture (>= 2 so every scratch
         buffer reaches its size), or 0 when the caller has just run >= 2 steps of the same shapes on a
         side stream itself (training.py: real steps on real batches, no repeated step)."""
@@ -46,11 +48,16 @@ class GraphedStep:
         torch.cuda.synchronize()
         self.generation = _lib.scratch_generation()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, pool=pool):
             self.out = step()
         torch.cuda.synchronize()
         if _lib.scratch_generation() != self.generation:
             raise _lib.SrkError("GraphedStep: a library scratch buffer grew during the capture (warm up longer)")
+
+    def pool(self):
+        """The graph's private memory pool: graphs captured with it share memory (replay them one at
+        a time, as a training loop does)."""
+        return self.graph.pool()
 
     def valid(self):
         """False once a library scratch buffer the graph may refer to has been reallocated."""

@@ -657,6 +657,14 @@ __device__ __forceinline__ void dc_stamp_chain1(const GruPArgs& a, int step) {
     a.trace[((size_t)blockIdx.x * a.T + step) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
 }
 
+// optional phase offset between the two chains: chain 1 starts a.dc_offset ticks late
+__device__ __forceinline__ void dc_chain_delay(const GruPArgs& a, int c) {
+  if (c == 1 && a.dc_offset) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < a.dc_offset) __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 constexpr int kDcXF = 24;   // floats a lane hands its pair partner: 3 gate accumulators x 4 rows (+ the fused projection's)
 
 __device__ __forceinline__ void dc_wait(const GruPArgs& a, const unsigned* f, int step) {
@@ -763,6 +771,7 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_persistent_dc_kernel(GruPArgs 
               bin = fused ? a.b_ih[dir * 3 * H + 2 * H + j] : 0.f;
   const float bhr = a.b_hh[dir * 3 * H + j], bhz = a.b_hh[dir * 3 * H + H + j], bhn = a.b_hh[dir * 3 * H + 2 * H + j];
   __syncthreads();
+  dc_chain_delay(a, c);
 
   const int Gp = a.G;
   const __amdgpu_buffer_rsrc_t rx = rsrc(a.xbuf + (size_t)dir * kHandoffSlots * Gp * 64 * H);   // [3][Gp][4][NKB][64][4]
@@ -873,9 +882,16 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_persistent_dc_kernel(GruPArgs 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float ghn = acc[2][r] + bhn;
-        const float rg = sigmoidf_(gr[r] + (acc[0][r] + bhr));
-        const float zg = sigmoidf_(gz[r] + (acc[1][r] + bhz));
-        const float ng = tanhf(gn[r] + rg * ghn);
+        float rg, zg, ng;
+        if (a.fast_cell) {
+          rg = sigmoid_fast(gr[r] + (acc[0][r] + bhr));
+          zg = sigmoid_fast(gz[r] + (acc[1][r] + bhz));
+          ng = tanh_fast(gn[r] + rg * ghn);
+        } else {
+          rg = sigmoidf_(gr[r] + (acc[0][r] + bhr));
+          zg = sigmoidf_(gz[r] + (acc[1][r] + bhz));
+          ng = tanhf(gn[r] + rg * ghn);
+        }
         const float h = (1.0f - zg) * ng + zg * hreg[r];
         hreg[r] = h;
         mytp[(4 * lq + r) * 8 + (lr & 7)] = h;
@@ -943,6 +959,7 @@ __global__ __launch_bounds__(512, 1) void gru_bwd_persistent_dc_kernel(GruPArgs 
   }
   if (tid < 8) pf[tid] = 0;
   __syncthreads();
+  dc_chain_delay(a, c);
 
   float* dgh_dir = a.dgh + (size_t)dir * B * T * 3 * H;
   const int Gp = a.G;
@@ -2054,6 +2071,8 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     static const int flags_env = [] { const char* v = getenv("SRK_GRU_FLAGS"); return v && *v ? atoi(v) : 0; }();
     ac.flags = flags_env;
     ac.xcd_local = g_opt_gru_xcd_local;
+    ac.dc_offset = g_opt_gru_dc_offset;
+    ac.fast_cell = g_opt_gru_fast_cell;
     ac.b_begin = c0;
     ac.b_end = std::min(a.B, c0 + rows_per_launch);
     ac.G = (ac.b_end - c0 + rows_g - 1) / rows_g;

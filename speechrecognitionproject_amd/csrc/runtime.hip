@@ -30,6 +30,8 @@ unsigned g_opt_gru_spin_limit = 0;
 int g_opt_gru_xcd_local = 1;
 int g_opt_gru_lp2 = 1;
 int g_opt_gru_dc = 1;
+unsigned g_opt_gru_dc_offset = 200;
+int g_opt_gru_fast_cell = 1;
 std::atomic<int64_t> g_scratch_gen{0};
 
 static thread_local std::string g_last_error;
@@ -368,6 +370,15 @@ int srk_set_option(const char* name, int64_t value) {
   }
   if (n == "gru_fp32_dual_chain") {   // fp32 recurrence: 8-wave workgroups running two row chains (1) or the 4-wave form (0)
     srk::g_opt_gru_dc = value != 0;
+    return SRK_OK;
+  }
+  if (n == "gru_dc_offset_ns") {   // fp32 two-chain kernels: delay chain 1's start (phase offset between the chains)
+    SRK_REQUIRE(value >= 0 && value <= 1000000, SRK_ERR_INVALID, "gru_dc_offset_ns out of range");
+    srk::g_opt_gru_dc_offset = (unsigned)(value / 10);
+    return SRK_OK;
+  }
+  if (n == "gru_fp32_fast_cell") {   // fp32 two-chain forward: v_exp_f32 / v_rcp_f32 cell nonlinearities
+    srk::g_opt_gru_fast_cell = value != 0;
     return SRK_OK;
   }
   if (n == "gru_lp_32x32") {   // 16-bit recurrence: 32 x 32 workgroups (1) or 64 rows x 16 units (0)

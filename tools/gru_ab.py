@@ -17,7 +17,10 @@ import torch  # noqa: E402
 from speechrecognitionproject_amd import _lib  # noqa: E402
 from speechrecognitionproject_amd import nn as snn  # noqa: E402
 
-VARIANTS = {"dc": {"gru_fp32_dual_chain": 1}, "4wave": {"gru_fp32_dual_chain": 0}}
+VARIANTS = {"dc": {"gru_fp32_dual_chain": 1, "gru_dc_offset_ns": 0, "gru_fp32_fast_cell": 0},
+            "dc_off2us": {"gru_dc_offset_ns": 2000}, "dc_off4us": {"gru_dc_offset_ns": 4000},
+            "dc_fast": {"gru_dc_offset_ns": 0, "gru_fp32_fast_cell": 1},
+            "4wave": {"gru_fp32_dual_chain": 0, "gru_fp32_fast_cell": 0}}
 
 
 def run(B, T, IN, reps, opts):
@@ -56,6 +59,8 @@ def main():
         for IN in (39, 1024):
             print(name, "IN=%d" % IN, json.dumps(run(a.B, a.T, IN, a.reps, opts)), flush=True)
     _lib.set_option("gru_fp32_dual_chain", 1)
+    _lib.set_option("gru_dc_offset_ns", 0)
+    _lib.set_option("gru_fp32_fast_cell", 0)
 
 
 if __name__ == "__main__":

@@ -1,8 +1,9 @@
 """Per-launch HBM traffic of the bench kernels from rocprofv3 PMC passes -> profiles/pmc_traffic.json.
 
-    python tools/pmc_traffic.py FETCH_DIR WRITE_DIR [-o profiles/pmc_traffic.json]
-    (bench.py reads profiles/pmc_traffic.json for the default cfg2 command and
-    profiles/pmc_traffic_<model>.json for `bench.py --model <model>`)
+    python tools/pmc_traffic.py FETCH_DIR WRITE_DIR --model M --batch B --precisions fp32,bf16 \
+        -o profiles/pmc_traffic_M.json
+    (bench.py reads profiles/pmc_traffic_<model>.json and uses it only when the recorded command —
+    model, per-GPU batch, world size, precisions, options — matches the running one)
 
 FETCH_SIZE / WRITE_SIZE come from two separate `rocprofv3 --kernel-trace --pmc ...` runs of the same
 bench command.  Corrections per MI355X_MICROARCH.md (HBM section, gfx950): FETCH_SIZE (KiB) x 2
@@ -19,7 +20,8 @@ import sqlite3
 
 GROUPS = {  # srk_prof name -> substrings of the rocprof kernel symbols it covers
     "gemm_f32": ("gemm_f32_kernel", "gemm_p32_kernel"), "gemm_bf16": ("gemm_h16_kernel", "gemm_lp_kernel", "gemm_g16_kernel"),
-    "gru_fwd_seq": ("gru_fwd_persistent_kernel",), "gru_bwd_seq": ("gru_bwd_persistent_kernel",),
+    "gru_fwd_seq": ("gru_fwd_persistent_kernel", "gru_fwd_persistent_dc_kernel"),
+    "gru_bwd_seq": ("gru_bwd_persistent_kernel", "gru_bwd_persistent_dc_kernel"),
     "gru_fwd_seq_lp": ("gru_fwd_persistent_lp_kernel", "gru_fwd_persistent_lp2_kernel"),
     "gru_bwd_seq_lp": ("gru_bwd_persistent_lp_kernel", "gru_bwd_persistent_lp2_kernel"),
     "gru_fwd_step": ("gru_fwd_step_kernel",), "gru_bwd_step": ("gru_bwd_step_kernel",),
@@ -56,11 +58,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch")
     ap.add_argument("write")
-    ap.add_argument("-o", default="profiles/pmc_traffic.json")
+    ap.add_argument("-o", required=True)
     ap.add_argument("--source", default="")
+    ap.add_argument("--model", required=True)
+    ap.add_argument("--batch", type=int, required=True)
+    ap.add_argument("--precisions", default="fp32", help="comma list: the precisions the command timed")
+    ap.add_argument("--world", type=int, default=1)
+    ap.add_argument("--sync-bn", action="store_true")
     a = ap.parse_args()
     f, w = collect(a.fetch, "FETCH_SIZE"), collect(a.write, "WRITE_SIZE")
+    # bench.py reports this traffic only for a command with the same model / batch / world / options
     res = {"source": a.source, "correction": "FETCH_SIZE KiB x 2 x 1024 + WRITE_SIZE KiB x 1024 (gfx950)",
+           "command": {"model": a.model, "batch": a.batch, "world": a.world, "precisions": a.precisions.split(","),
+                       "sync_bn": bool(a.sync_bn)},
            "bytes_per_launch": {}}
     for g in sorted(set(f) & set(w)):
         fb = 2.0 * 1024.0 * f[g][1] / f[g][0]

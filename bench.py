@@ -231,9 +231,31 @@ def feature_roofline(model_name, n_clips=65536):
     cnt, ms, work = _lib.prof_read(name)
     _lib.prof_enable(False)
     gbs = work / (ms * 1e-3) / 1e9
-    return {"kernel": name, "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
-            "clips_per_launch": n_clips, "ms_per_launch": round(ms / cnt, 4), "bytes_per_clip": per_clip}
+    res = {"kernel": name, "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+           "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+           "clips_per_launch": n_clips, "ms_per_launch": round(ms / cnt, 4), "bytes_per_clip": per_clip}
+    res.update(feature_pmc(name, n_clips))
+    return res
+
+
+def feature_pmc(name, n_clips):
+    """HBM bytes and SQ counters of this feature launch from profiles/pmc_feature.json
+    (tools/feat_pmc.sh: rocprofv3 PMC passes over tools/mfcc_only.py, the same kernel, layout and
+    clip count), used only when the recorded clip count matches."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_feature.json")
+    try:
+        with open(path) as fh:
+            rec = json.load(fh)
+    except (OSError, ValueError):
+        return {}
+    ent = rec.get("kernels", {}).get(name)
+    if rec.get("clips_per_launch") != n_clips or not ent or "traffic_per_launch" not in ent:
+        return {}
+    pc = ent.get("per_clip", {})
+    return {"traffic": ent["traffic_per_launch"], "traffic_per_clip": ent["traffic_per_clip"],
+            "sq_insts_valu_per_clip": pc.get("SQ_INSTS_VALU"), "sq_wait_inst_any_per_clip": pc.get("SQ_WAIT_INST_ANY"),
+            "sq_wave_cycles_per_clip": pc.get("SQ_WAVE_CYCLES"),
+            "pmc_source": "profiles/pmc_feature.json (%s)" % rec.get("source", "")}
 
 
 def _relaunch(args):

@@ -1386,6 +1386,8 @@ int plan_launch(const GemmDesc& d, int BM, int BN, int BK, int per_cu, KernelArg
   ka.remap = remap;
   // Split K when the output grid leaves resident slots idle and K is long (tile::choose_splits).
   int splits = (d.batch == 1 && allow_split) ? choose_splits(tm * tn, d.K, BK, slots, 16) : 1;
+  static const int splits_env = env_int("SRK_GEMM_SPLITS", 0);   // A/B measurements only
+  if (splits_env > 0 && d.batch == 1 && d.K >= (int64_t)splits_env * 4 * BK) splits = splits_env;
   ka.kchunk = splits > 1 ? ((d.K + splits - 1) / splits + BK - 1) / BK * BK : std::max<int64_t>(d.K, 1);
   if (splits > 1) splits = (int)((d.K + ka.kchunk - 1) / ka.kchunk);
   ka.nblk = ka.tiles * splits;

@@ -414,8 +414,8 @@ static int64_t fwd_xbuf_off(int64_t B, int64_t T, int64_t H) { return (B * T * 6
 static int64_t bwd_xbuf_off(int64_t B, int64_t T, int64_t H) {
   return (B * T * 6 * H + 2 * B * T * 3 * H + 2 * B * 3 * H + 2 * B * H + 63) / 64 * 64;
 }
-// (rows padded to the 64-row groups of one launch chunk: <= 256 rows, or B rounded up to 64)
-static int64_t xbuf_rows(int64_t B) { return std::min<int64_t>((B + 63) / 64 * 64, 256); }
+// (rows padded to the 64-row groups of one launch chunk: <= 512 rows, or B rounded up to 64)
+static int64_t xbuf_rows(int64_t B) { return std::min<int64_t>((B + 63) / 64 * 64, 512); }
 static int64_t fwd_counter_off(int64_t B, int64_t T, int64_t H) {
   return fwd_xbuf_off(B, T, H) + 2 * srk::kHandoffSlots * xbuf_rows(B) * H;
 }
@@ -577,7 +577,7 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
     p.counters = reinterpret_cast<unsigned*>(ws + bwd_counter_off(B, T, H));
     int rc;
     if ((rc = srk::gru_persistent_launch(p, true, s))) return rc;
-    const int prows = srk::gru_bias_part_rows();
+    const int prows = srk::gru_bias_part_rows(B);
     hipLaunchKernelGGL(srk::dbias_reduce_kernel, dim3((unsigned)((6 * H + 255) / 256)), dim3(256), 0, s, part,
                        (int)(chunks * (256 / prows)), (int)B, (int)H, prows, db_ih, db_hh, accumulate);
     SRK_CHECK_HIP(hipGetLastError());

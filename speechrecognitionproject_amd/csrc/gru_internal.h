@@ -76,12 +76,13 @@ extern int g_opt_gru_persistent;
 extern unsigned long long* g_opt_gru_trace;   // device buffer or nullptr
 extern unsigned g_opt_gru_spin_limit;          // 0 = default (~2 s); test hook "gru_spin_limit"
 extern int g_opt_gru_xcd_local;                // XCD-local hand-off when the census allows (default 1)
+extern int g_opt_gru_lp_wide;                 // 16-bit recurrence over > 256 rows: 64-row workgroups, one launch (default 1)
 extern int g_opt_gru_lp2;                      // 16-bit recurrence on 32 x 32 workgroups (default 1)
 extern int g_opt_gru_dc;                       // fp32 recurrence: two independent row chains per workgroup (default 1)
 extern unsigned g_opt_gru_dc_offset;            // chain-1 start delay (ticks of 10 ns), default 200 (2 us)
 extern int g_opt_gru_fast_cell;                 // fp32 two-chain forward: hardware exp / rcp cell math (default 1)
 // Batch rows per bias-gradient partial of the 16-bit backward kernel (32 or 64; 256-row launch chunks).
-int gru_bias_part_rows();
+int gru_bias_part_rows(int64_t B);
 // Host-pinned health word (device-mapped pointer in *dev): non-zero once any persistent-kernel
 // spin-wait has given up; read without a device synchronization by srk_health_check.
 int health_word(unsigned** host, unsigned** dev);

@@ -1528,21 +1528,25 @@ template <int H> constexpr int lp2_fwd_wpq() { return (H + 16) / 8; }
 template <int H> constexpr int lp2_bwd_wpq() { return (3 * H + 16) / 8; }
 constexpr int kXP2 = 20;   // pitch of the k-half exchange tiles (16 columns + 4: conflict-free b32 writes)
 
-// LDS: W slice [96][H + 16] 16-bit (row g * 32 + jj) | hT [32][36] fp32 | W_ih slice [96][kXP] fp32 |
-// exchange [4 waves][3][16][kXP2] fp32
-template <int H, bool F16>
-__global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs a) {
+// RB row blocks of 16 per workgroup (2 x RB waves: wave = kh * RB + rb): RB = 2 is the 32 x 32
+// workgroup; RB = 4 (64 rows, 8 waves, the same W slice in LDS) runs a 512-row batch in ONE launch
+// where RB = 2 needs two chunks one after the other.  Per row the arithmetic is the same.
+template <int RB> constexpr int lp2_fused_in() { return RB == 2 ? kFusedIn : 40; }   // RB = 4: LDS fits 40
+// LDS: W slice [96][H + 16] 16-bit (row g * 32 + jj) | hT [16 RB][36] fp32 | W_ih slice [96][KF + 1] fp32 |
+// exchange [2 RB waves][3][16][kXP2] fp32
+template <int H, bool F16, int RB>
+__global__ __launch_bounds__(128 * RB, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs a) {
   using Ops = RecOps<F16>;
   using e8 = typename Ops::e8;
   constexpr int U = kUnits2, S = H / U, WPQ = lp2_fwd_wpq<H>(), HTP = U + 4, NKB = H / 32, KH = NKB / 2;
-  constexpr int RNDX = F16 ? 2 : 1;
+  constexpr int RNDX = F16 ? 2 : 1, NT = 128 * RB, ROWS = 16 * RB, KF = lp2_fused_in<RB>(), XP = KF + 1;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   u32x4* Ws = reinterpret_cast<u32x4*>(smem);
   float* hT = smem + 3 * U * WPQ * 4;
-  float* Wx = hT + kRows2 * HTP;
-  float* X = Wx + 3 * U * kXP;
+  float* Wx = hT + ROWS * HTP;
+  float* X = Wx + 3 * U * XP;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
-  const int rb = wave & 1, kh = wave >> 1;
+  const int rb = wave % RB, kh = wave / RB;
   int dir, group, slice;
   bool local;
   stamp(a, 0, 6);   // kernel entry (prologue = slot 0 - slot 6 of step 0)
@@ -1550,25 +1554,25 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs
   trace_id(a, dir, group, slice);
   const bool per = a.flags || local;
   const int T = a.T, j0 = slice * U, ju = kh * 16 + lr, j = j0 + ju;
-  const int b0 = a.b_begin + group * kRows2, b_last = a.b_end - 1, rbase = b0 + rb * 16;
+  const int b0 = a.b_begin + group * ROWS, b_last = a.b_end - 1, rbase = b0 + rb * 16;
 
   {  // this slice of W_hh[dir] (3 gates x 32 units), rounded to 16 bits -> LDS; loads issued 8 packs
      // at a time ahead of their stores (the prologue is a chain of L2 round trips otherwise)
     const float* W = a.w_hh + (size_t)dir * 3 * H * H;
-    constexpr int NV = 3 * U * (H / 8), NB = 8;
-    static_assert(NV % (256 * NB) == 0, "prologue batches");
-    for (int v0 = tid; v0 < NV; v0 += 256 * NB) {
+    constexpr int NV = 3 * U * (H / 8), NB = 2048 / NT;
+    static_assert(NV % (NT * NB) == 0, "prologue batches");
+    for (int v0 = tid; v0 < NV; v0 += NT * NB) {
       v4f w[NB][2];
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
-        const int v = v0 + 256 * u, c = v / (H / 8), kq = v % (H / 8), g = c / U, jj = c % U;
+        const int v = v0 + NT * u, c = v / (H / 8), kq = v % (H / 8), g = c / U, jj = c % U;
         const float* src = W + (size_t)(g * H + j0 + jj) * H + kq * 8;
         w[u][0] = ld4(src);
         w[u][1] = ld4(src + 4);
       }
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
-        const int v = v0 + 256 * u, c = v / (H / 8), kq = v % (H / 8);
+        const int v = v0 + NT * u, c = v / (H / 8), kq = v % (H / 8);
         Ws[c * WPQ + kq] = pack8<F16>(cat8(w[u][0], w[u][1]));
       }
     }
@@ -1576,19 +1580,18 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs
   const bool fused = a.x_in != nullptr;
   if (fused) {   // W_ih slice (rows g * 32 + jj), rounded like the GEMM operands, 8 loads in flight
     const float* W = a.w_ih + (size_t)dir * 3 * H * a.in;
-    constexpr int NV = 3 * U * kFusedIn, NB = 8;
-    static_assert(NV % (256 * NB) == 0, "prologue batches");
-    for (int v0 = tid; v0 < NV; v0 += 256 * NB) {
+    constexpr int NV = 3 * U * KF, NB = 2048 / NT;   // the last batch is partial for RB = 4
+    for (int v0 = tid; v0 < NV; v0 += NT * NB) {
       float w[NB];
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
-        const int v = v0 + 256 * u, c = v / kFusedIn, k = v % kFusedIn, g = c / U, jj = c % U;
+        const int v = min(v0 + NT * u, NV - 1), c = v / KF, k = v % KF, g = c / U, jj = c % U;
         w[u] = k < a.in ? W[(size_t)(g * H + j0 + jj) * a.in + k] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
-        const int v = v0 + 256 * u, c = v / kFusedIn, k = v % kFusedIn;
-        Wx[c * kXP + k] = rnd16<RNDX>(w[u]);
+        const int v = v0 + NT * u, c = v / KF, k = v % KF;
+        if (v < NV) Wx[c * XP + k] = rnd16<RNDX>(w[u]);
       }
     }
   }
@@ -1600,7 +1603,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs
   __syncthreads();
 
   const int Gp = a.G;
-  const __amdgpu_buffer_rsrc_t rx = rsrc(a.xbuf + (size_t)dir * 2 * Gp * kRows2 * H);   // 16-bit [2][Gp][2][NKB][64][8]
+  const __amdgpu_buffer_rsrc_t rx = rsrc(a.xbuf + (size_t)dir * 2 * Gp * ROWS * H);   // 16-bit [2][Gp][RB][NKB][64][8]
   float hreg[4] = {0.f, 0.f, 0.f, 0.f};
   float gsv[4][4];
 
@@ -1653,11 +1656,11 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs
       for (int m = 0; m < kFusedIn / 4; ++m) xv[m] = rnd16<RNDX>(xnext[m]);
       f32x4 ax[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-      for (int m = 0; m < kFusedIn / 4; ++m) {
+      for (int m = 0; m < KF / 4; ++m) {
         if (4 * m >= a.in) break;   // uniform
 #pragma unroll
         for (int g = 0; g < 3; ++g)
-          ax[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[m], Wx[(g * U + kh * 16 + lr) * kXP + 4 * m + lq], ax[g], 0, 0, 0);
+          ax[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[m], Wx[(g * U + kh * 16 + lr) * XP + 4 * m + lq], ax[g], 0, 0, 0);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1672,7 +1675,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs
       lp2_wait(a, dir, group, kh * KH, KH, step, per);
       stamp(a, step, 1);
       const unsigned base =
-          (unsigned)((((((size_t)((step - 1) & 1) * Gp + group) * 2 + rb) * NKB + kh * KH) * 64 + lane) * 16);
+          (unsigned)((((((size_t)((step - 1) & 1) * Gp + group) * RB + rb) * NKB + kh * KH) * 64 + lane) * 16);
       v4f hv[KH];
 #pragma unroll
       for (int i = 0; i < KH; ++i) hv[i] = ld4_sc1(rx, base + i * 1024);
@@ -1701,7 +1704,7 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs
       // wave-uniform: one static code path per value (an acc index computed from kh would make the
       // compiler select registers with compare / cndmask chains)
       float* Xw = X + wave * (3 * 16 * kXP2);
-      const float* Xp = X + (wave ^ 2) * (3 * 16 * kXP2);
+      const float* Xp = X + (wave ^ RB) * (3 * 16 * kXP2);
       auto exchange = [&](auto KH_) {
         constexpr int K = decltype(KH_)::value;
 #pragma unroll
@@ -1741,11 +1744,11 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs
     }
     __syncthreads();
     stamp(a, step, 3);
-    if (step + 1 < T && tid < 128) {   // hand-off (16-bit): chunk (rb', k block = slice), lane l: row l & 15, 8 units
+    if (step + 1 < T && tid < 64 * RB) {   // hand-off (16-bit): chunk (rb', k block = slice), lane l: row l & 15, 8 units
       const int rbp = tid >> 6, l = tid & 63, row = rbp * 16 + (l & 15);
       if (b0 + row <= b_last) {
         const float* src = hT + row * HTP + 8 * (l >> 4);
-        st4_ho(rx, (unsigned)((((((size_t)(step & 1) * Gp + group) * 2 + rbp) * NKB + slice) * 64 + l) * 16),
+        st4_ho(rx, (unsigned)((((((size_t)(step & 1) * Gp + group) * RB + rbp) * NKB + slice) * 64 + l) * 16),
                __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))), local);
       }
     }
@@ -1755,21 +1758,22 @@ __global__ __launch_bounds__(256, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs
   }
 }
 
-// LDS: W^T slice [32][3H + 16] 16-bit (unit jj, gate row c) | dT [32][3][36] | dI [32][36] |
-// exchange [4 waves][16][kXP2] | bias partials [4 waves][4][16]
-template <int H, bool F16>
-__global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs a) {
+// LDS: W^T slice [32][3H + 16] 16-bit (unit jj, gate row c) | dT [16 RB][3][36] | dI [16 RB][36] |
+// exchange [2 RB waves][16][kXP2] | bias partials [2 RB waves][4][16]
+template <int H, bool F16, int RB>
+__global__ __launch_bounds__(128 * RB, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs a) {
   using Ops = RecOps<F16>;
   using e8 = typename Ops::e8;
   constexpr int U = kUnits2, S = H / U, WPQ = lp2_bwd_wpq<H>(), DTP = U + 4, NKB = 3 * H / 32, KS = S / 2;
+  constexpr int NT = 128 * RB, ROWS = 16 * RB, NW = 2 * RB;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   u32x4* Wt = reinterpret_cast<u32x4*>(smem);
-  float* dT = smem + U * WPQ * 4;              // [32][3][DTP]
-  float* dI = dT + kRows2 * 3 * DTP;           // [32][DTP]: dan (dgi's third gate; dT holds dan * r)
-  float* X = dI + kRows2 * DTP;                // [4][16][kXP2]
-  float* red = X + 4 * 16 * kXP2;              // [4][4][16]
+  float* dT = smem + U * WPQ * 4;              // [ROWS][3][DTP]
+  float* dI = dT + ROWS * 3 * DTP;             // [ROWS][DTP]: dan (dgi's third gate; dT holds dan * r)
+  float* X = dI + ROWS * DTP;                  // [NW][16][kXP2]
+  float* red = X + NW * 16 * kXP2;             // [NW][4][16]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
-  const int rb = wave & 1, kh = wave >> 1;
+  const int rb = wave % RB, kh = wave / RB;
   int dir, group, slice;
   bool local;
   stamp(a, 0, 6);   // kernel entry
@@ -1777,11 +1781,11 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs
   trace_id(a, dir, group, slice);
   const bool per = a.flags || local;
   const int T = a.T, B = a.B, j0 = slice * U, ju = kh * 16 + lr, j = j0 + ju;
-  const int b0 = a.b_begin + group * kRows2, b_last = a.b_end - 1, rbase = b0 + rb * 16;
+  const int b0 = a.b_begin + group * ROWS, b_last = a.b_end - 1, rbase = b0 + rb * 16;
 
   {  // W_hh[dir][c][j0 .. j0+31] for all 3H rows c, transposed [jj][c] in 8-deep c packs
     const float* W = a.w_hh + (size_t)dir * 3 * H * H;
-    for (int v = tid; v < (3 * H / 8) * (U / 4); v += 256) {
+    for (int v = tid; v < (3 * H / 8) * (U / 4); v += NT) {
       const int cb = v / (U / 4), jq = (v % (U / 4)) * 4;
       v4f w[8];
 #pragma unroll
@@ -1794,7 +1798,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs
   __syncthreads();
 
   const int Gp = a.G;
-  const __amdgpu_buffer_rsrc_t rg_ = rsrc(a.xbuf + (size_t)dir * 2 * Gp * kRows2 * 3 * H);   // 16-bit [2][Gp][2][NKB][64][8]
+  const __amdgpu_buffer_rsrc_t rg_ = rsrc(a.xbuf + (size_t)dir * 2 * Gp * ROWS * 3 * H);   // 16-bit [2][Gp][RB][NKB][64][8]
   float dhz[4] = {0.f, 0.f, 0.f, 0.f};
   float sb[4] = {0.f, 0.f, 0.f, 0.f};   // sums of dar, daz, dan, dan * r over t and the lane's rows
 
@@ -1820,7 +1824,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs
     if (step > 0) {
       lp2_wait(a, dir, group, kh * KS, KS, step, per);
       stamp(a, step, 1);
-      const unsigned base = (unsigned)(((((size_t)((step - 1) & 1) * Gp + group) * 2 + rb) * NKB * 64 + lane) * 16);
+      const unsigned base = (unsigned)(((((size_t)((step - 1) & 1) * Gp + group) * RB + rb) * NKB * 64 + lane) * 16);
       v4f dv[3 * KS];   // dv[3 i + g] = k block g * 16 + kh * KS + i (gate g of producer kh * KS + i)
 #pragma unroll
       for (int i = 0; i < KS; ++i)
@@ -1845,7 +1849,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs
         __builtin_amdgcn_sched_barrier(0);
       }
       float* Xw = X + wave * 16 * kXP2;   // the partner's unit block (static per kh, see the forward)
-      const float* Xp = X + (wave ^ 2) * 16 * kXP2;
+      const float* Xp = X + (wave ^ RB) * 16 * kXP2;
       auto exchange = [&](auto KH_) {
         constexpr int K = decltype(KH_)::value;
 #pragma unroll
@@ -1889,18 +1893,18 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs
     __syncthreads();
     stamp(a, step, 3);
     if (!edge) {   // hand-off (16-bit): chunks (rb', k block g * 16 + slice), lane l: row l & 15, 8 units
-      for (int v = tid; v < 6 * 64; v += 256) {
+      for (int v = tid; v < 3 * RB * 64; v += NT) {
         const int c = v >> 6, rbp = c / 3, g = c % 3, l = v & 63, row = rbp * 16 + (l & 15);
         if (b0 + row > b_last) continue;
         const float* src = dT + (row * 3 + g) * DTP + 8 * (l >> 4);
-        st4_ho(rg_, (unsigned)((((((size_t)(step & 1) * Gp + group) * 2 + rbp) * NKB + g * 16 + slice) * 64 + l) * 16),
+        st4_ho(rg_, (unsigned)((((((size_t)(step & 1) * Gp + group) * RB + rbp) * NKB + g * 16 + slice) * 64 + l) * 16),
                __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4)))), local);
       }
     }
     lp2_arrive(a, dir, group, slice, step, per, local);   // the hand-off only: dgh16 / dgi16 go out after it
     stamp(a, step, 4);
-    for (int v = tid; v < 2 * 32 * 3 * 4; v += 256) {   // 16-bit dgh (edge rows zero) and dgi: (row, gate, 8 units)
-      const int which = v / 384, w = v % 384, row = w / 12, g = (w % 12) >> 2, q8 = w & 3, b = b0 + row;
+    for (int v = tid; v < 2 * ROWS * 3 * 4; v += NT) {   // 16-bit dgh (edge rows zero) and dgi: (row, gate, 8 units)
+      const int which = v / (ROWS * 12), w = v % (ROWS * 12), row = w / 12, g = (w % 12) >> 2, q8 = w & 3, b = b0 + row;
       if (b > b_last) continue;
       const float* src = which == 0 || g < 2 ? dT + (row * 3 + g) * DTP + 8 * q8 : dI + row * DTP + 8 * q8;
       v4f pk = __builtin_bit_cast(v4f, pack8<F16>(cat8(ld4(src), ld4(src + 4))));
@@ -1912,7 +1916,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs
       }
     }
   }
-  // bias-gradient partials: lanes lr, lr + 16, lr + 32, lr + 48, then the two row-block waves in order
+  // bias-gradient partials: lanes lr, lr + 16, lr + 32, lr + 48, then the RB row-block waves in order
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     sb[q] += __shfl_xor(sb[q], 16);
@@ -1924,8 +1928,10 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs
   }
   __syncthreads();
   if (tid < 128) {
-    const int k2 = tid >> 6, q = (tid >> 4) & 3, u = tid & 15;   // waves (rb 0, k2) = 2 k2 and (rb 1, k2) = 2 k2 + 1
-    const float v = red[((2 * k2) * 4 + q) * 16 + u] + red[((2 * k2 + 1) * 4 + q) * 16 + u];
+    const int k2 = tid >> 6, q = (tid >> 4) & 3, u = tid & 15;   // waves (rb, k2) = RB k2 + rb
+    float v = red[((RB * k2) * 4 + q) * 16 + u];
+#pragma unroll
+    for (int r = 1; r < RB; ++r) v += red[((RB * k2 + r) * 4 + q) * 16 + u];
     a.dbias[(((size_t)(a.chunk * 8 + group) * 2 + dir) * 4 + q) * H + j0 + k2 * 16 + u] = v;
   }
 }
@@ -1939,34 +1945,42 @@ size_t lds_bytes(int H, bool backward, int prec) {
   return std::max<size_t>(need, 96 * 1024);
 }
 
-size_t lp2_lds_bytes(int H, bool backward) {
-  const size_t need = backward ? (size_t)kUnits2 * ((3 * H + 16) / 8) * 16 + (size_t)kRows2 * 3 * (kUnits2 + 4) * 4 +
-                                     (size_t)kRows2 * (kUnits2 + 4) * 4 + 4 * 16 * kXP2 * 4 + 4 * 4 * 16 * 4
-                               : (size_t)3 * kUnits2 * ((H + 16) / 8) * 16 + (size_t)kRows2 * (kUnits2 + 4) * 4 +
-                                     (size_t)3 * kUnits2 * kXP * 4 + 4 * 3 * 16 * kXP2 * 4;
+size_t lp2_lds_bytes(int H, bool backward, int RB) {
+  const size_t rows = 16 * RB, nw = 2 * RB, xp = (RB == 2 ? kFusedIn : 40) + 1;
+  const size_t need = backward ? (size_t)kUnits2 * ((3 * H + 16) / 8) * 16 + rows * 3 * (kUnits2 + 4) * 4 +
+                                     rows * (kUnits2 + 4) * 4 + nw * 16 * kXP2 * 4 + nw * 4 * 16 * 4
+                               : (size_t)3 * kUnits2 * ((H + 16) / 8) * 16 + rows * (kUnits2 + 4) * 4 +
+                                     (size_t)3 * kUnits2 * xp * 4 + nw * 3 * 16 * kXP2 * 4;
   return std::max<size_t>(need, 96 * 1024);   // one workgroup per CU (see lds_bytes)
 }
 
 template <int H>
-const void* lp2_kernel_ptr(bool backward, int prec) {
+const void* lp2_kernel_ptr(bool backward, int prec, int RB) {
+  if (RB == 4) {
+    if (prec == kPrecF16)
+      return backward ? reinterpret_cast<const void*>(gru_bwd_persistent_lp2_kernel<H, true, 4>)
+                      : reinterpret_cast<const void*>(gru_fwd_persistent_lp2_kernel<H, true, 4>);
+    return backward ? reinterpret_cast<const void*>(gru_bwd_persistent_lp2_kernel<H, false, 4>)
+                    : reinterpret_cast<const void*>(gru_fwd_persistent_lp2_kernel<H, false, 4>);
+  }
   if (prec == kPrecF16)
-    return backward ? reinterpret_cast<const void*>(gru_bwd_persistent_lp2_kernel<H, true>)
-                    : reinterpret_cast<const void*>(gru_fwd_persistent_lp2_kernel<H, true>);
-  return backward ? reinterpret_cast<const void*>(gru_bwd_persistent_lp2_kernel<H, false>)
-                  : reinterpret_cast<const void*>(gru_fwd_persistent_lp2_kernel<H, false>);
+    return backward ? reinterpret_cast<const void*>(gru_bwd_persistent_lp2_kernel<H, true, 2>)
+                    : reinterpret_cast<const void*>(gru_fwd_persistent_lp2_kernel<H, true, 2>);
+  return backward ? reinterpret_cast<const void*>(gru_bwd_persistent_lp2_kernel<H, false, 2>)
+                  : reinterpret_cast<const void*>(gru_fwd_persistent_lp2_kernel<H, false, 2>);
 }
 
 template <int H>
-int lp2_occupancy_ok(bool backward, int prec) {
+int lp2_occupancy_ok(bool backward, int prec, int RB = 2) {
   static std::mutex mu;
-  static int occ[2][3] = {{-1, -1, -1}, {-1, -1, -1}};
+  static int occ[2][2][3] = {{{-1, -1, -1}, {-1, -1, -1}}, {{-1, -1, -1}, {-1, -1, -1}}};
   std::lock_guard<std::mutex> lk(mu);
-  int& o = occ[backward ? 1 : 0][prec];
+  int& o = occ[RB == 4 ? 1 : 0][backward ? 1 : 0][prec];
   if (o < 0) {
-    const void* k = lp2_kernel_ptr<H>(backward, prec);
-    const size_t lds = lp2_lds_bytes(H, backward);
+    const void* k = lp2_kernel_ptr<H>(backward, prec, RB);
+    const size_t lds = lp2_lds_bytes(H, backward, RB);
     SRK_CHECK_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    SRK_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, 256, lds));
+    SRK_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, 128 * RB, lds));
   }
   return o >= 1 ? 1 : 0;
 }
@@ -2048,16 +2062,28 @@ int gru_persistent_supported(int64_t B, int64_t T, int64_t H, bool backward) {
   return ok < 0 ? 0 : ok;
 }
 
-int gru_bias_part_rows() { return (matmul_prec() != kPrecF32 && g_opt_gru_lp2) ? kRows2 : kRows; }
+// 16-bit recurrence over more than 256 rows: the 64-row workgroups (RB = 4) run up to 512 rows per
+// launch instead of 256-row chunks one after the other (a fused input projection needs in <= 40)
+bool lp2_wide(int64_t B, int prec, bool backward, int in_fused) {
+  return prec != kPrecF32 && g_opt_gru_lp2 && g_opt_gru_lp_wide && B > 256 && in_fused <= 40 &&
+         lp2_occupancy_ok<512>(backward, prec, 4) > 0;
+}
+
+int gru_bias_part_rows(int64_t B) {
+  const int prec = matmul_prec();
+  if (lp2_wide(B, prec, true, 0)) return 64;
+  return (prec != kPrecF32 && g_opt_gru_lp2) ? kRows2 : kRows;
+}
 
 int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
   const int gmax = gru_persistent_groups(a.H);
   SRK_REQUIRE(gmax > 0 && a.H == 512, SRK_ERR_INVALID, "gru persistent: unsupported H");
-  const int rows_per_launch = gmax * kRows;
   const int prec = matmul_prec();
+  const bool wide = lp2_wide(a.B, prec, backward, a.x_in ? a.in : 0) && (!backward || a.dgi16 != nullptr);
+  const int rows_per_launch = wide ? 512 : gmax * kRows;
   // 16-bit operands: the 32 x 32 workgroup kernels (the backward one writes the 16-bit outputs only)
   const bool lp2 = prec != kPrecF32 && g_opt_gru_lp2 && (!backward || a.dgi16 != nullptr);
-  const int rows_g = lp2 ? kRows2 : kRows, slices = lp2 ? a.H / kUnits2 : a.H / kUnits;
+  const int rows_g = wide ? 64 : lp2 ? kRows2 : kRows, slices = lp2 ? a.H / kUnits2 : a.H / kUnits;
   if (lp2 && lp2_occupancy_ok<512>(backward, prec) <= 0)
     SRK_REQUIRE(false, SRK_ERR_INVALID, "gru persistent: the 32 x 32 kernels do not fit one workgroup per CU");
   // fp32 forward: the two-chain 8-wave kernel (same grid, W slice and outputs)
@@ -2083,7 +2109,7 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     ProfScope prof(backward ? (prec == kPrecF32 ? "gru_bwd_seq" : "gru_bwd_seq_lp")
                             : (prec == kPrecF32 ? "gru_fwd_seq" : "gru_fwd_seq_lp"), s, flops);
     prof.detail("gru_%s_persistent%s_kernel B%d T%d chunk%d", backward ? "bwd" : "fwd",
-                dc ? "_dc" : lp2 ? "_lp2" : (prec == kPrecF32 ? "" : "_lp"),
+                dc ? "_dc" : wide ? "_lp2w" : lp2 ? "_lp2" : (prec == kPrecF32 ? "" : "_lp"),
                 ac.b_end - c0, a.T, ac.chunk);
     if (dc && backward)
       hipLaunchKernelGGL((gru_bwd_persistent_dc_kernel<512>), grid, dim3(512), dc_bwd_lds_floats(512) * 4, s, ac);
@@ -2092,8 +2118,8 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     else if (dc)
       hipLaunchKernelGGL((gru_fwd_persistent_dc_kernel<512, false>), grid, dim3(512), dc_fwd_lds_floats(512) * 4, s, ac);
     else if (lp2)
-      hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(lp2_kernel_ptr<512>(backward, prec))),
-                         grid, dim3(256), lp2_lds_bytes(512, backward), s, ac);
+      hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(lp2_kernel_ptr<512>(backward, prec, wide ? 4 : 2))),
+                         grid, dim3(wide ? 512 : 256), lp2_lds_bytes(512, backward, wide ? 4 : 2), s, ac);
     else
       hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(kernel_ptr<512>(backward, prec))), grid,
                          dim3(256), lds_bytes(512, backward, prec), s, ac);
@@ -2167,10 +2193,11 @@ extern "C" int srk_gru_audit_words(int64_t B, int precision, int backward, int64
   SRK_REQUIRE(B > 0 && max_word && chunks && census && precision >= 0 && precision <= 2, SRK_ERR_INVALID,
               "gru_audit_words: bad arguments");
   using namespace srk;
-  const int rows_per_launch = gru_persistent_groups(512) * kRows;
   const bool lp2 = precision != kPrecF32 && g_opt_gru_lp2;
+  const bool wide = lp2 && g_opt_gru_lp_wide && B > 256;   // as lp2_wide (occupancy aside)
+  const int rows_per_launch = wide ? 512 : gru_persistent_groups(512) * kRows;
   const bool dc = precision == kPrecF32 && g_opt_gru_dc;
-  const int rows_g = lp2 ? kRows2 : kRows, S = lp2 ? 512 / kUnits2 : 512 / kUnits;
+  const int rows_g = wide ? 64 : lp2 ? kRows2 : kRows, S = lp2 ? 512 / kUnits2 : 512 / kUnits;
   int64_t mx = -1, n = 0;
   auto see = [&](int w) { mx = std::max<int64_t>(mx, w); };
   for (int64_t c0 = 0; c0 < B; c0 += rows_per_launch, ++n) {

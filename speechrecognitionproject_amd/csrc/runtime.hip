@@ -29,6 +29,7 @@ unsigned long long* g_opt_gru_trace = nullptr;
 unsigned g_opt_gru_spin_limit = 0;
 int g_opt_gru_xcd_local = 1;
 int g_opt_gru_lp2 = 1;
+int g_opt_gru_lp_wide = 1;
 int g_opt_gru_dc = 1;
 unsigned g_opt_gru_dc_offset = 200;
 int g_opt_gru_fast_cell = 1;
@@ -379,6 +380,10 @@ int srk_set_option(const char* name, int64_t value) {
   }
   if (n == "gru_fp32_fast_cell") {   // fp32 two-chain forward: v_exp_f32 / v_rcp_f32 cell nonlinearities
     srk::g_opt_gru_fast_cell = value != 0;
+    return SRK_OK;
+  }
+  if (n == "gru_lp_wide") {   // 16-bit recurrence over > 256 rows: 64-row workgroups in one launch (1) or 256-row chunks (0)
+    srk::g_opt_gru_lp_wide = value != 0;
     return SRK_OK;
   }
   if (n == "gru_lp_32x32") {   // 16-bit recurrence: 32 x 32 workgroups (1) or 64 rows x 16 units (0)

@@ -331,3 +331,56 @@ def test_bigru_fp32_dual_chain_matches_four_wave(gpu, B, T, IN):
         err = float((a - b).abs().max() / (b.abs().max() + 1e-30))
         assert err <= 2e-5, (i, err)
 
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("B,T,IN", [(512, 9, 39), (512, 6, 1024), (300, 7, 39), (1024, 5, 48), (448, 5, 24)])
+def test_bigru_lowprec_wide_matches_chunked(gpu, prec, B, T, IN):
+    """16-bit recurrence over more than 256 rows: the 64-row workgroup kernels (8 waves, one launch of
+    up to 512 rows; option gru_lp_wide, default on) against the 32-row kernels run as 256-row chunks
+    one after the other.  Each row runs the same source arithmetic, but the two instantiations are
+    compiled separately and the compiler's multiply-add contraction in the cell is free to differ:
+    step 0 (h_prev = 0) is bitwise equal, later steps differ at fp32 rounding level, amplified by the
+    16-bit hand-off (measured <= 1.3e-4 on outputs of magnitude <= 1).  Bounds: outputs 5e-4 absolute,
+    gradients 2e-3 relative (norm-wise), and each mode bitwise reproducible run to run.  IN = 48 keeps
+    the fused forward on the chunked kernel (the wide one fuses inputs of <= 40) while the backward
+    runs wide; B = 1024 is two wide launches (bias partials of chunk 1); B = 448 a partial grid."""
+    from speechrecognitionproject_amd import _lib
+    H = 512
+    torch.manual_seed(12)
+    mine = snn.BiGRU(IN, H, num_layers=1).cuda()
+    x = torch.randn(B, T, IN)
+    w = torch.randn(B, T, 2 * H)
+    outs = {}
+    try:
+        _lib.set_matmul_precision(prec)
+        for mode in (1, 1, 0):
+            _lib.set_option("gru_lp_wide", mode)
+            _lib.prof_enable(True)
+            mine.zero_grad()
+            xm = x.cuda().requires_grad_(True)
+            ym, _ = mine(xm)
+            (ym * w.cuda()).sum().backward()
+            torch.cuda.synchronize()
+            kinds = {r["kernel"].split(" ")[0] for r in _lib.prof_kernels() if r["name"].startswith("gru_")}
+            _lib.prof_enable(False)
+            outs.setdefault(mode, []).append(([ym.detach().cpu(), xm.grad.cpu()],
+                                              dict((n, p.grad.cpu()) for n, p in mine.named_parameters()), kinds))
+    finally:
+        _lib.set_option("gru_lp_wide", 1)
+        _lib.set_matmul_precision("fp32")
+    assert _lib.spin_timeouts() == 0
+    assert "gru_bwd_persistent_lp2w_kernel" in outs[1][0][2] and "gru_bwd_persistent_lp2w_kernel" not in outs[0][0][2]
+    assert ("gru_fwd_persistent_lp2w_kernel" in outs[1][0][2]) == (IN != 48)
+    (a0, g0, _), (a1, g1, _) = outs[1]
+    (c0, h0, _), = outs[0]
+    for a, b in zip(a0, a1):
+        assert torch.equal(a, b)
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
+    if IN != 48:   # step 0 of each direction: no recurrent term, bitwise equal
+        assert torch.equal(a0[0][:, 0, :H], c0[0][:, 0, :H]) and torch.equal(a0[0][:, -1, H:], c0[0][:, -1, H:])
+    assert float((a0[0] - c0[0]).abs().max()) <= 5e-4
+    for a, b in [(a0[1], c0[1])] + [(g0[n], h0[n]) for n in g0]:
+        err = float((a - b).norm() / b.norm())
+        assert err <= 2e-3, err

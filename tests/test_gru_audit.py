@@ -17,10 +17,13 @@ def _audit(B, prec, backward=0):
     return mx.value, n.value, cen.value
 
 
-@pytest.mark.parametrize("opts", [{"gru_fp32_dual_chain": 1, "gru_lp_32x32": 1},
-                                  {"gru_fp32_dual_chain": 0, "gru_lp_32x32": 0}])
+@pytest.mark.parametrize("opts", [{"gru_fp32_dual_chain": 1, "gru_lp_32x32": 1, "gru_lp_wide": 1},
+                                  {"gru_fp32_dual_chain": 1, "gru_lp_32x32": 1, "gru_lp_wide": 0},
+                                  {"gru_fp32_dual_chain": 0, "gru_lp_32x32": 0, "gru_lp_wide": 0}])
 @pytest.mark.parametrize("prec", [0, 1, 2])
 def test_flag_words_below_census_and_chunk_independent(opts, prec):
+    # 16-bit with gru_lp_wide: batches over 256 rows run as 512-row launches of 64-row workgroups
+    wide = prec != 0 and opts["gru_lp_32x32"] and opts["gru_lp_wide"]
     try:
         for k, v in opts.items():
             _lib.set_option(k, v)
@@ -28,9 +31,10 @@ def test_flag_words_below_census_and_chunk_independent(opts, prec):
         for B in (1, 63, 64, 200, 256, 300, 512, 1000, 4096):
             mx, n, cen = _audit(B, prec)
             assert 0 <= mx < cen, (B, mx, cen)
-            assert n == (B + 255) // 256
+            assert n == ((B + 511) // 512 if wide and B > 256 else (B + 255) // 256)
             if B % 256 == 0:
                 assert mx == first[0]          # every full chunk touches the same words
     finally:
         _lib.set_option("gru_fp32_dual_chain", 1)
         _lib.set_option("gru_lp_32x32", 1)
+        _lib.set_option("gru_lp_wide", 1)

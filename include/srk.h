@@ -170,6 +170,13 @@ int srk_gemm_rowsum_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t 
 int srk_gemm_16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha, const uint16_t* A,
                 int64_t lda, const uint16_t* B, int64_t ldb, float beta, float* C, int64_t ldc,
                 const float* bias, int bias_mode, void* stream);
+/* Batched form of srk_gemm_16 (no bias): for z < batch, C + z sC = alpha op(A + z sA) op(B + z sB)
+ * + beta (C + z sC); strides in elements, multiples of 8 (sC of 4).  The BiGRU backward's two
+ * recurrent weight gradients (nn.GRU weight_hh_l{k}{,_reverse}.grad, models/model_mfcc_bgru.py:25)
+ * run as one batch-2 launch.                                                                  */
+int srk_gemm_16_batched(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha,
+                        const uint16_t* A, int64_t lda, int64_t sA, const uint16_t* B, int64_t ldb,
+                        int64_t sB, float beta, float* C, int64_t ldc, int64_t sC, int batch, void* stream);
 /* out[n] = beta * out[n] + sum_m X[m, n]  (bias gradients).                                 */
 int srk_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, float beta, void* stream);
 

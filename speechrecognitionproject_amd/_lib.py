@@ -47,6 +47,7 @@ _SIGS = {
     "srk_gemm_f32": [_I, _I, _I64, _I64, _I64, _F, _P, _I64, _P, _I64, _F, _P, _I64, _P, _I, _P],
     "srk_gemm_rowsum_f32": [_I, _I, _I64, _I64, _I64, _F, _P, _I64, _P, _I64, _F, _P, _I64, _P, _P],
     "srk_gemm_16": [_I, _I, _I64, _I64, _I64, _F, _P, _I64, _P, _I64, _F, _P, _I64, _P, _I, _P],
+    "srk_gemm_16_batched": [_I, _I, _I64, _I64, _I64, _F, _P, _I64, _I64, _P, _I64, _I64, _F, _P, _I64, _I64, _I, _P],
     "srk_colsum_f32": [_P, _I64, _I64, _I64, _P, _F, _P],
     "srk_gru_workspace_floats": [_I64, _I64, _I64, _I64, _I],
     "srk_gru_layer_fwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P],

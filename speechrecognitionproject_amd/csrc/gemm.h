@@ -19,6 +19,7 @@ struct GemmDesc {
   int batch = 1; int64_t sA = 0, sB = 0, sC = 0;
   // optional fused row sums of op(A): rowsum[m] = rowsum_beta * rowsum[m] + sum_k op(A)[m, k]
   float* rowsum = nullptr; float rowsum_beta = 0.f;
+  int64_t sRS = 0;   // batched launches: batch z's row sums at rowsum + z sRS
   // matrix-core operand precision (MatmulPrec); -1 = the process setting (srk_set_option)
   int prec = -1;
   // 16-bit operands already in memory (bf16 / fp16 per `prec`, same layouts and leading dimensions

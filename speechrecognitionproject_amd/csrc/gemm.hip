@@ -814,11 +814,13 @@ __global__ __launch_bounds__(NW * 64, (h16_per_cu<TA, TB, BM, BN>())) void gemm_
 // instruction) instead of the 32x32 accumulator layout's 4-B scalar stores.  Split-K launches write
 // the raw slab; otherwise alpha, bias and beta are applied.
 __device__ __forceinline__ void pp_epilogue(const KernelArgs& ka, const f32x16 (&acc)[4][2], float* lds, int split,
-                                            int64_t m0, int64_t n0, int grp, int wc, int wave, int lane) {
+                                            int64_t m0, int64_t n0, int grp, int wc, int wave, int lane,
+                                            int64_t z = 0) {
   const GemmDesc& d = ka.d;
   float* st = lds + wave * 4096;
   const bool split_mode = ka.partial != nullptr;
-  float* C = split_mode ? ka.partial + (int64_t)split * d.M * d.N : d.C;
+  // batched launches: batch z's slabs follow batch z - 1's ([batch][splits][M][N])
+  float* C = split_mode ? ka.partial + (z * (ka.nblk / ka.tiles) + split) * d.M * d.N : d.C + z * d.sC;
   const int64_t ldc = split_mode ? d.N : d.ldc;
   const bool vec = (ldc % 4 == 0) && ((uintptr_t)C % 16 == 0);
   const int lh = lane >> 5, lc = lane & 31;
@@ -983,7 +985,8 @@ __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
     return u32x4s{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)a),
                   (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)), 0x7ffffff0u, 0x00020000u};
   };
-  const u32x4s rsA = rsrc16(d.A16), rsB = rsrc16(d.B16);
+  const int64_t z = blockIdx.y;   // batch index (grid.y = batch; strides sA / sB in elements)
+  const u32x4s rsA = rsrc16(d.A16 + z * d.sA), rsB = rsrc16(d.B16 + z * d.sB);
   constexpr unsigned kOOB = 0x80000000u;
   unsigned vo[4];
   int kk[4];
@@ -1083,7 +1086,7 @@ __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
 #if defined(SRK_G16_EXP) && SRK_G16_EXP == 3   // experiment builds only: no C stores (kept live)
   if (d.alpha != 12345.f) return;
 #endif
-  pp_epilogue(ka, acc, reinterpret_cast<float*>(smem), split, m0, n0, grp, wc, wave, lane);
+  pp_epilogue(ka, acc, reinterpret_cast<float*>(smem), split, m0, n0, grp, wc, wave, lane, z);
 }
 
 // ------------------------------------------------------------------ fp32: LDS-DMA ping-pong
@@ -1164,7 +1167,8 @@ __global__ __launch_bounds__(512, 1) void gemm_p32_kernel(KernelArgs ka) {
     return u32x4s{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)a),
                   (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)), 0x7ffffff0u, 0x00020000u};
   };
-  const u32x4s rsA = rsrc32(d.A), rsB = rsrc32(d.B);
+  const int64_t z = blockIdx.y;   // batch index (grid.y = batch)
+  const u32x4s rsA = rsrc32(d.A + z * d.sA), rsB = rsrc32(d.B + z * d.sB);
   constexpr unsigned kOOB = 0x80000000u;
   unsigned vo[4];
   int kk[4];
@@ -1258,24 +1262,29 @@ __global__ __launch_bounds__(512, 1) void gemm_p32_kernel(KernelArgs ka) {
   }
   if (grp == 0) bar();
 
-  pp_epilogue(ka, acc, smem, split, m0, n0, grp, wc, wave, lane);
+  pp_epilogue(ka, acc, smem, split, m0, n0, grp, wc, wave, lane, z);
   if (do_rs) {   // lanes l and l + 32 hold the two k halves of row (l & 31) of each row block
+    const int splits = ka.nblk / ka.tiles;
+    float* rsum = d.rowsum + z * d.sRS;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float t = rs[i] + __shfl_xor(rs[i], 32);
       const int64_t row = m0 + grp * 128 + i * 32 + (lane & 31);
       if (lane < 32 && row < d.M) {
-        if (ka.partial) ka.rs_partial[(int64_t)split * d.M + row] = t;
-        else d.rowsum[row] = d.rowsum_beta != 0.f ? d.rowsum_beta * d.rowsum[row] + t : t;
+        if (ka.partial) ka.rs_partial[(z * splits + split) * d.M + row] = t;
+        else rsum[row] = d.rowsum_beta != 0.f ? d.rowsum_beta * rsum[row] + t : t;
       }
     }
   }
 }
 
 // Sums the split-K slabs in split order and applies the GEMM epilogue.
+// Batched launches (grid.y = batch): batch z reads its own [splits][M][N] slabs and writes C + z sC.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmDesc d, const float* __restrict__ partial, int splits) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.M * d.N) return;
+  partial += (int64_t)blockIdx.y * splits * d.M * d.N;
+  d.C += (int64_t)blockIdx.y * d.sC;
   const int64_t row = i / d.N, col = i % d.N;
   float s = 0.f;
   for (int k = 0; k < splits; ++k) s += partial[(int64_t)k * d.M * d.N + i];
@@ -1294,6 +1303,8 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(GemmDesc d, const f
   if (q >= d.M * n4) return;
   const int64_t row = q / n4, col = (q - row * n4) * 4, i = row * d.N + col;
   const int64_t slab = d.M * d.N;
+  partial += (int64_t)blockIdx.y * splits * slab;
+  d.C += (int64_t)blockIdx.y * d.sC;
   v4f s = *reinterpret_cast<const v4f*>(partial + i);
   for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const v4f*>(partial + (int64_t)k * slab + i);
   v4f v = d.alpha * s;
@@ -1304,10 +1315,13 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(GemmDesc d, const f
   *c = v;
 }
 
+// grid.y = batch: batch z reads rp + z splits M and writes out + z out_stride
 __global__ void rowsum_reduce_kernel(float* __restrict__ out, float beta, const float* __restrict__ rp, int64_t M,
-                                     int splits) {
+                                     int splits, int64_t out_stride = 0) {
   const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
+  rp += (int64_t)blockIdx.y * splits * M;
+  out += (int64_t)blockIdx.y * out_stride;
   float t = 0.f;
   for (int k = 0; k < splits; ++k) t += rp[(int64_t)k * M + m];
   out[m] = beta != 0.f ? beta * out[m] + t : t;
@@ -1371,8 +1385,10 @@ int env_int(const char* name, int dflt) {
 
 // Grid, split-K and scratch for one launch of a BM x BN x BK tile kernel with `per_cu` resident
 // workgroups per CU; fills ka and returns the split count (tile::choose_splits).
+// split_batched: the kernel handles split-K slabs of batched launches ([batch][splits][M][N]; the
+// ping-pong kernels); the others split only batch-1 launches.
 int plan_launch(const GemmDesc& d, int BM, int BN, int BK, int per_cu, KernelArgs& ka, int* splits_out,
-                bool allow_split = true) {
+                bool allow_split = true, bool split_batched = false) {
   const int64_t tm = (d.M + BM - 1) / BM, tn = (d.N + BN - 1) / BN;
   SRK_REQUIRE(tm * tn <= (INT32_MAX >> 5) && d.batch <= 65535, SRK_ERR_INVALID, "gemm: grid too large");
   static const int remap = env_int("SRK_GEMM_REMAP", 1);
@@ -1385,7 +1401,8 @@ int plan_launch(const GemmDesc& d, int BM, int BN, int BK, int per_cu, KernelArg
   ka.group_m = 8;
   ka.remap = remap;
   // Split K when the output grid leaves resident slots idle and K is long (tile::choose_splits).
-  int splits = (d.batch == 1 && allow_split) ? choose_splits(tm * tn, d.K, BK, slots, 16) : 1;
+  const bool can_split = allow_split && (d.batch == 1 || split_batched);
+  int splits = can_split ? choose_splits(tm * tn * d.batch, d.K, BK, slots, 16) : 1;
   static const int splits_env = env_int("SRK_GEMM_SPLITS", 0);   // A/B measurements only
   if (splits_env > 0 && d.batch == 1 && d.K >= (int64_t)splits_env * 4 * BK) splits = splits_env;
   ka.kchunk = splits > 1 ? ((d.K + splits - 1) / splits + BK - 1) / BK * BK : std::max<int64_t>(d.K, 1);
@@ -1393,10 +1410,10 @@ int plan_launch(const GemmDesc& d, int BM, int BN, int BK, int per_cu, KernelArg
   ka.nblk = ka.tiles * splits;
   if (splits > 1) {
     float* scratch = nullptr;
-    const size_t need = (size_t)splits * d.M * d.N + (d.rowsum ? (size_t)splits * d.M : 0);
+    const size_t need = (size_t)d.batch * splits * (d.M * d.N + (d.rowsum ? d.M : 0));
     if (int rc = get_scratch(need, &scratch)) return rc;
     ka.partial = scratch;
-    ka.rs_partial = d.rowsum ? scratch + (size_t)splits * d.M * d.N : nullptr;
+    ka.rs_partial = d.rowsum ? scratch + (size_t)d.batch * splits * d.M * d.N : nullptr;
   }
   *splits_out = splits;
   return SRK_OK;
@@ -1407,17 +1424,17 @@ int finish_splits(const GemmDesc& d, const KernelArgs& ka, int splits, hipStream
   SRK_CHECK_HIP(hipGetLastError());
   if (splits > 1) {
     const int64_t n = d.M * d.N;
-    const bool vec4 = d.N % 4 == 0 && d.ldc % 4 == 0 && (uintptr_t)d.C % 16 == 0 &&
+    const bool vec4 = d.N % 4 == 0 && d.ldc % 4 == 0 && (uintptr_t)d.C % 16 == 0 && d.sC % 4 == 0 &&
                       (d.bias_mode != 1 || (uintptr_t)d.bias % 16 == 0);
     if (vec4)
-      hipLaunchKernelGGL(splitk_reduce4_kernel, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, s, d, ka.partial,
-                         splits);
+      hipLaunchKernelGGL(splitk_reduce4_kernel, dim3((unsigned)((n / 4 + 255) / 256), (unsigned)d.batch), dim3(256), 0,
+                         s, d, ka.partial, splits);
     else
-      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, ka.partial,
-                         splits);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)d.batch), dim3(256), 0, s, d,
+                         ka.partial, splits);
     if (d.rowsum)
-      hipLaunchKernelGGL(rowsum_reduce_kernel, dim3((unsigned)((d.M + 255) / 256)), dim3(256), 0, s, d.rowsum,
-                         d.rowsum_beta, ka.rs_partial, d.M, splits);
+      hipLaunchKernelGGL(rowsum_reduce_kernel, dim3((unsigned)((d.M + 255) / 256), (unsigned)d.batch), dim3(256), 0, s,
+                         d.rowsum, d.rowsum_beta, ka.rs_partial, d.M, splits, d.sRS);
     SRK_CHECK_HIP(hipGetLastError());
   }
   return SRK_OK;
@@ -1527,12 +1544,12 @@ int launch_g16(const GemmDesc& d, hipStream_t s, bool f16) {
   int splits = 1;
   // split K only when the 256 x 256 output grid leaves more than half of the CUs idle: the slabs
   // (M x N fp32 per split, written and re-read) cost more than a partly filled round otherwise
-  const int64_t tiles = ((d.M + 255) / 256) * ((d.N + 255) / 256);
-  if (int rc = plan_launch(d, 256, 256, kG16BK, 1, ka, &splits, tiles * 2 < kCUs)) return rc;
-  ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K);
-  prof.detail("gemm_g16_kernel<%c%c> %lldx%lldx%lld s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', (long long)d.M, (long long)d.N,
-              (long long)d.K, splits);
-  const dim3 grid((unsigned)ka.nblk), block(512);
+  const int64_t tiles = ((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
+  if (int rc = plan_launch(d, 256, 256, kG16BK, 1, ka, &splits, tiles * 2 < kCUs, true)) return rc;
+  ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
+  prof.detail("gemm_g16_kernel<%c%c> %lldx%lldx%lld b%d s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', (long long)d.M,
+              (long long)d.N, (long long)d.K, d.batch, splits);
+  const dim3 grid((unsigned)ka.nblk, (unsigned)d.batch), block(512);
   if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true>), grid, block, 0, s, ka);
   else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false>), grid, block, 0, s, ka);
   return finish_splits(d, ka, splits, s);
@@ -1543,7 +1560,7 @@ int launch_h16(const GemmDesc& d, hipStream_t s, bool f16) {
   static const int cfg_env = env_int("SRK_H16_CFG", 0);
   // the LDS-DMA ping-pong kernel wherever its 256 x 256 tile fills the chip (srk option overrides)
   const int kern = g_opt_gemm16_kernel ? g_opt_gemm16_kernel : (d.M >= 1024 && d.N >= 256 ? 2 : 1);
-  if (kern == 2 || cfg_env == 5) return launch_g16<TA, TB>(d, s, f16);
+  if (kern == 2 || cfg_env == 5 || d.batch > 1) return launch_g16<TA, TB>(d, s, f16);   // only g16 is batched
   // measured (profiles/r01zk_gemm_h16_cfg*.txt): 256 x 256 on x W^T and on the weight gradients
   // (TA != TB: gi 143 vs 148 us, dW_ih 128 vs 137), 256 x 128 on dx (204 tiles of 256 x 256 leave
   // CUs idle: 255 vs 147 us), 128 x 128 below 1024 rows
@@ -1557,12 +1574,12 @@ template <bool TA, bool TB>
 int launch_p32(const GemmDesc& d, hipStream_t s) {
   KernelArgs ka;
   int splits = 1;
-  const int64_t tiles = ((d.M + 255) / 256) * ((d.N + 255) / 256);
-  if (int rc = plan_launch(d, 256, 256, kP32BK, 1, ka, &splits, tiles * 2 < kCUs)) return rc;
-  ProfScope prof("gemm_f32", s, 2.0 * (double)d.M * (double)d.N * (double)d.K);
-  prof.detail("gemm_p32_kernel<%c%c> %lldx%lldx%lld s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', (long long)d.M, (long long)d.N,
-              (long long)d.K, splits);
-  hipLaunchKernelGGL((gemm_p32_kernel<TA, TB>), dim3((unsigned)ka.nblk), dim3(512), 0, s, ka);
+  const int64_t tiles = ((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
+  if (int rc = plan_launch(d, 256, 256, kP32BK, 1, ka, &splits, tiles * 2 < kCUs, true)) return rc;
+  ProfScope prof("gemm_f32", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
+  prof.detail("gemm_p32_kernel<%c%c> %lldx%lldx%lld b%d s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', (long long)d.M,
+              (long long)d.N, (long long)d.K, d.batch, splits);
+  hipLaunchKernelGGL((gemm_p32_kernel<TA, TB>), dim3((unsigned)ka.nblk, (unsigned)d.batch), dim3(512), 0, s, ka);
   return finish_splits(d, ka, splits, s);
 }
 
@@ -1573,10 +1590,14 @@ int dispatch_tile(const GemmDesc& d, hipStream_t s, bool vec) {
   // the LDS-DMA ping-pong kernel where a 256 x 256 grid fills the chip (16-B units, 32-bit buffer
   // offsets, batch 1); srk option gemm32_kernel: 1 register-staged, 2 ping-pong
   const double ext_a = (double)(d.ta ? d.K : d.M) * d.lda * 4, ext_b = (double)(d.tb ? d.N : d.K) * d.ldb * 4;
-  const bool p32_ok = vec && d.batch == 1 && ext_a < 2147483000.0 && ext_b < 2147483000.0;
+  const bool p32_ok = vec && ext_a < 2147483000.0 && ext_b < 2147483000.0;
   // measured (tools/gemm_bench.py, cfg2 shapes): ping-pong 6-7 % faster on dx (NN) and dW_ih (TN),
-  // 8 % slower on the x W^T projection (NT) and on the 12-tile dW_hh grid (split 16)
-  const int kern32 = g_opt_gemm32_kernel ? g_opt_gemm32_kernel : (!TB && d.M >= 2048 && d.N >= 1024 ? 2 : 1);
+  // 8 % slower on the x W^T projection (NT) and on the 12-tile dW_hh grid (split 16); batched
+  // launches (the BiGRU's two dW_hh) and row sums over a batch only exist on the ping-pong kernel
+  const int kern32 = g_opt_gemm32_kernel ? g_opt_gemm32_kernel
+                                         : (!TB && ((d.M >= 2048 && d.N >= 1024) || d.batch > 1) ? 2 : 1);
+  SRK_REQUIRE(!d.rowsum || d.batch == 1 || (p32_ok && kern32 == 2), SRK_ERR_INVALID,
+              "gemm: batched row sums need the fp32 ping-pong kernel (16-B operand rows)");
   if (p32_ok && kern32 == 2) return launch_p32<TA, TB>(d, s);
   // 256 x 128 tiles (one 8-wave workgroup per CU, 110 KB of LDS) halve the L2 -> CU operand
   // traffic per flop of the 128 x 128 tile; used when the grid still fills the chip several times
@@ -1596,8 +1617,11 @@ int gemm_f32(const GemmDesc& d, hipStream_t s) {
   if (d.M == 0 || d.N == 0) return SRK_OK;
   if (d.A16 || d.B16) {   // 16-bit operands in memory
     const int prec = d.prec >= 0 ? d.prec : matmul_prec();
-    SRK_REQUIRE(d.A16 && d.B16 && d.C && prec != kPrecF32 && d.batch == 1 && !d.rowsum, SRK_ERR_INVALID,
-                "gemm: 16-bit operands need both A16 / B16, a 16-bit precision, batch 1 and no row sums");
+    SRK_REQUIRE(d.A16 && d.B16 && d.C && prec != kPrecF32 && !d.rowsum && (d.batch == 1 || d.bias_mode == 0),
+                SRK_ERR_INVALID,
+                "gemm: 16-bit operands need both A16 / B16, a 16-bit precision and no row sums (no bias when batched)");
+    SRK_REQUIRE(d.batch == 1 || (d.sA % 8 == 0 && d.sB % 8 == 0 && d.sC % 4 == 0), SRK_ERR_INVALID,
+                "gemm: batched 16-bit operands need 8-element strides");
     const double ext_a = (double)(d.ta ? d.K : d.M) * d.lda * 2, ext_b = (double)(d.tb ? d.N : d.K) * d.ldb * 2;
     SRK_REQUIRE((uintptr_t)d.A16 % 16 == 0 && (uintptr_t)d.B16 % 16 == 0 && d.lda % 8 == 0 && d.ldb % 8 == 0 &&
                     ((d.ta && d.M % 8 == 0) || (!d.ta && d.K % 8 == 0)) &&
@@ -1613,7 +1637,8 @@ int gemm_f32(const GemmDesc& d, hipStream_t s) {
   }
   SRK_REQUIRE(d.C && (d.K == 0 || (d.A && d.B)), SRK_ERR_INVALID, "gemm: null operand");
   SRK_REQUIRE(d.bias_mode == 0 || d.bias, SRK_ERR_INVALID, "gemm: bias_mode without bias");
-  SRK_REQUIRE(!d.rowsum || d.batch == 1, SRK_ERR_INVALID, "gemm: rowsum needs batch == 1");
+  SRK_REQUIRE(!d.rowsum || d.batch == 1 || d.prec == kPrecF32 || (d.prec < 0 && matmul_prec() == kPrecF32),
+              SRK_ERR_INVALID, "gemm: batched rowsum needs fp32 operands");
   // 16-B loads need 16-B aligned rows, K % 4 == 0 when an operand is k-contiguous (a clamped k vector
   // stays inside the row) and,
   // along M / N (A when ta, B when !tb), a row count that is a multiple of 4 (a clamped vector is
@@ -1701,6 +1726,24 @@ extern "C" int srk_gemm_16(int trans_a, int trans_b, int64_t M, int64_t N, int64
   d.bias = bias; d.bias_mode = bias_mode;
   SRK_REQUIRE(bias_mode >= 0 && bias_mode <= 2, SRK_ERR_INVALID, "gemm: bias_mode must be 0, 1 or 2");
   SRK_REQUIRE(srk::matmul_prec() != srk::kPrecF32, SRK_ERR_INVALID, "gemm_16: set matmul_precision to bf16 / fp16");
+  return srk::gemm_f32(d, srk::as_stream(stream));
+  SRK_API_END
+}
+
+extern "C" int srk_gemm_16_batched(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha,
+                                   const uint16_t* A, int64_t lda, int64_t sA, const uint16_t* B, int64_t ldb,
+                                   int64_t sB, float beta, float* C, int64_t ldc, int64_t sC, int batch,
+                                   void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(batch >= 1, SRK_ERR_INVALID, "gemm_16_batched: batch must be >= 1");
+  srk::GemmDesc d;
+  d.M = M; d.N = N; d.K = K;
+  d.A16 = A; d.lda = lda; d.ta = trans_a != 0;
+  d.B16 = B; d.ldb = ldb; d.tb = trans_b != 0;
+  d.C = C; d.ldc = ldc; d.alpha = alpha; d.beta = beta;
+  d.batch = batch; d.sA = sA; d.sB = sB; d.sC = sC;
+  SRK_REQUIRE(srk::matmul_prec() != srk::kPrecF32, SRK_ERR_INVALID,
+              "gemm_16_batched: set matmul_precision to bf16 / fp16");
   return srk::gemm_f32(d, srk::as_stream(stream));
   SRK_API_END
 }

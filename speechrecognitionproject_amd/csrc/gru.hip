@@ -596,18 +596,25 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
         SRK_CHECK_HIP(hipGetLastError());
       }
     }
-    for (int dir = 0; dir < 2; ++dir) {   // dW_hh[dir] = dgh16[dir]^T h_prev16 (edge rows of dgh16 are zero)
-      const uint16_t* dg = dgh16 + (size_t)dir * BT * 3 * H;
+    {   // dW_hh[dir] = dgh16[dir]^T h_prev16 (edge rows of dgh16 are zero), both directions in ONE
+        // batched launch: dir 0 pairs dgh16 row r + 1 with y16 row r, dir 1 dgh16 row r with y16 row
+        // r + 1 (its reverse half); a 24-tile grid split 10 ways fills the CUs where two 12-tile
+        // launches ran one after the other
       GemmDesc g;
       g.M = 3 * H; g.N = H; g.K = BT - 1;
       g.ta = true; g.lda = 3 * H; g.ldb = 2 * H;
-      g.A16 = dir == 0 ? dg + 3 * H : dg;
-      g.B16 = dir == 0 ? y16 + dir * H : y16 + 2 * H + dir * H;
-      g.C = dw_hh + (size_t)dir * 3 * H * H; g.ldc = H; g.beta = beta;
-      if (g.K > 0) {
+      g.A16 = dgh16 + 3 * H;                 // dir 1: dgh16 + BT 3H
+      g.B16 = y16;                           // dir 1: y16 + 3H (row 1, reverse half)
+      g.C = dw_hh; g.ldc = H; g.beta = beta;
+      g.batch = 2; g.sA = BT * 3 * H - 3 * H; g.sB = 3 * H; g.sC = 3 * H * H;
+      if (g.K > 0 && srk::g_opt_gru_dwhh_batched) {
         if ((rc = srk::gemm_f32(g, s))) return rc;
+      } else if (g.K > 0) {   // one launch per direction (A/B and tests)
+        g.batch = 1;
+        for (int dir = 0; dir < 2; ++dir, g.A16 += g.sA, g.B16 += g.sB, g.C += g.sC)
+          if ((rc = srk::gemm_f32(g, s))) return rc;
       } else if (!accumulate) {
-        SRK_CHECK_HIP(hipMemsetAsync(g.C, 0, sizeof(float) * 3 * H * H, s));
+        SRK_CHECK_HIP(hipMemsetAsync(g.C, 0, sizeof(float) * 2 * 3 * H * H, s));
       }
     }
     if (dx) {   // dx [BT, in] = dgi16 W16
@@ -675,26 +682,35 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
       SRK_CHECK_HIP(hipGetLastError());
     }
   }
-  for (int dir = 0; dir < 2; ++dir) {
+  {
     // dW_hh[dir][3H, H] = sum_(b,t) dgh[b][t]^T h_prev[b][t]; h_prev of row (b,t) is y row (b,t-1)
     // (dir 0) or (b,t+1) (dir 1); the edge rows of dgh are zero so the batch seams contribute 0.
-    // db_hh = row sums of dgh^T (fused) + the edge rows kept aside in dgh_edge.
-    const float* dg = dgh + (size_t)dir * BT * 3 * H;
-    float* dbh = db_hh + dir * 3 * H;
+    // db_hh = row sums of dgh^T (fused) + the edge rows kept aside in dgh_edge.  Both directions run
+    // as ONE batch-2 launch (dir 1 = dir 0's operands + sA / sB; option gru_dwhh_batched).
     GemmDesc g;
     g.M = 3 * H; g.N = H; g.K = BT - 1;
     g.ta = true; g.lda = 3 * H; g.ldb = 2 * H;
-    g.A = dir == 0 ? dg + 3 * H : dg;
-    g.B = dir == 0 ? y + dir * H : y + 2 * H + dir * H;
-    g.C = dw_hh + (size_t)dir * 3 * H * H; g.ldc = H; g.beta = beta;
-    g.rowsum = dbh; g.rowsum_beta = beta;
-    if (g.K > 0) {
+    g.A = dgh + 3 * H;      // dir 1: dgh + BT 3H
+    g.B = y;                // dir 1: y + 3H (row 1, reverse half)
+    g.C = dw_hh; g.ldc = H; g.beta = beta;
+    g.rowsum = db_hh; g.rowsum_beta = beta;
+    g.batch = 2; g.sA = BT * 3 * H - 3 * H; g.sB = 3 * H; g.sC = 3 * H * H; g.sRS = 3 * H;
+    // (the batched row sums exist on the ping-pong kernel only: 16-B rows, 32-bit buffer offsets)
+    const bool batched = srk::g_opt_gru_dwhh_batched && H % 4 == 0 && (double)BT * 3 * H * 4 < 2.1e9 &&
+                         (double)BT * 2 * H * 4 < 2.1e9;
+    if (g.K > 0 && batched) {
       if ((rc = srk::gemm_f32(g, s))) return rc;
+    } else if (g.K > 0) {
+      g.batch = 1;
+      for (int dir = 0; dir < 2; ++dir, g.A += g.sA, g.B += g.sB, g.C += g.sC, g.rowsum += g.sRS)
+        if ((rc = srk::gemm_f32(g, s))) return rc;
     } else if (!accumulate) {
-      SRK_CHECK_HIP(hipMemsetAsync(g.C, 0, sizeof(float) * 3 * H * H, s));
-      SRK_CHECK_HIP(hipMemsetAsync(dbh, 0, sizeof(float) * 3 * H, s));
+      SRK_CHECK_HIP(hipMemsetAsync(dw_hh, 0, sizeof(float) * 2 * 3 * H * H, s));
+      SRK_CHECK_HIP(hipMemsetAsync(db_hh, 0, sizeof(float) * 2 * 3 * H, s));
     }
-    if ((rc = srk::colsum_f32(dgh_edge + (size_t)dir * B * 3 * H, B, 3 * H, 3 * H, dbh, 1.f, s))) return rc;
+    for (int dir = 0; dir < 2; ++dir)
+      if ((rc = srk::colsum_f32(dgh_edge + (size_t)dir * B * 3 * H, B, 3 * H, 3 * H, db_hh + dir * 3 * H, 1.f, s)))
+        return rc;
   }
   if (dx) {  // dx[BT, in] = dgi[BT, 6H] * W_ih_cat[6H, in]
     GemmDesc g;

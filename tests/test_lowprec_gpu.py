@@ -410,6 +410,75 @@ def test_gemm_16bit_kernels_at_tile_edges(prec, kernel, ta, tb, M, N, K):
     assert (Cd.cpu().double() - ref).abs().max().item() <= 2e-6 * (1 + scale)
 
 
+@pytest.mark.parametrize("ta,tb", [(1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("M,N,K,batch", [(1536, 512, 4095, 2), (264, 136, 1032, 3), (1024, 256, 64, 2)])
+def test_gemm_16bit_batched(prec, ta, tb, M, N, K, batch):
+    """srk_gemm_16_batched (the BiGRU backward's batch-2 dW_hh launch; split-K slabs per batch) ==
+    float64 product of the 16-bit values, batch by batch, on strided views of one buffer."""
+    if (not ta or tb) and K % 8:   # a k-contiguous operand needs rows of 8-element multiples
+        K += 8 - K % 8
+    g = torch.Generator().manual_seed(M + 3 * N + 5 * K + batch)
+    dt = TORCH_DT[prec]
+    ra, ca = (K, M) if ta else (M, K)
+    rb, cb = (N, K) if tb else (K, N)
+    sA, sB, sC = ra * ca + 24, rb * cb + 8, M * N + 4     # padded strides (multiples of 8 / 4)
+    A = torch.randn(batch * sA, generator=g).to(dt)
+    B = torch.randn(batch * sB, generator=g).to(dt)
+    C0 = torch.randn(batch * sC, generator=g)
+    Ad, Bd, Cd = A.cuda(), B.cuda(), C0.clone().cuda()
+    call("srk_gemm_16_batched", ta, tb, M, N, K, 1.0, ptr(Ad), ca, sA, ptr(Bd), cb, sB, 1.0, ptr(Cd), N, sC, batch,
+         stream_ptr())
+    torch.cuda.synchronize()
+    out = Cd.cpu().double()
+    for z in range(batch):
+        a = A[z * sA:z * sA + ra * ca].view(ra, ca).double()
+        b = B[z * sB:z * sB + rb * cb].view(rb, cb).double()
+        opA, opB = (a.T if ta else a), (b.T if tb else b)
+        ref = opA @ opB + C0[z * sC:z * sC + M * N].view(M, N).double()
+        scale = (opA.abs() @ opB.abs()).max().item()
+        assert (out[z * sC:z * sC + M * N].view(M, N) - ref).abs().max().item() <= 2e-6 * (1 + scale), z
+        assert torch.equal(out[z * sC + M * N:(z + 1) * sC], C0[z * sC + M * N:(z + 1) * sC].double())  # gaps
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
+def test_bigru_batched_dwhh_matches_per_direction(gpu, precision):
+    """The batch-2 dW_hh launch (option gru_dwhh_batched, default; fp32: the ping-pong kernel with the
+    fused bias-gradient row sums per batch) == one launch per direction up to fp32 split-K summation
+    order; every other gradient is bitwise identical."""
+    from speechrecognitionproject_amd import nn as snn
+    _lib.set_matmul_precision(precision)
+    try:
+        _batched_dwhh_case(snn)
+    finally:
+        _lib.set_matmul_precision("fp32")
+
+
+def _batched_dwhh_case(snn):
+    B, T, IN, H = 256, 20, 39, 512
+    torch.manual_seed(7)
+    mine = snn.BiGRU(IN, H, num_layers=2).cuda()
+    x = torch.randn(B, T, IN, device="cuda")
+    w = torch.randn(B, T, 2 * H, device="cuda")
+    grads = []
+    for batched in (1, 0):
+        _lib.set_option("gru_dwhh_batched", batched)
+        try:
+            for p in mine.parameters():
+                p.grad = None
+            (mine(x)[0] * w).sum().backward()
+            torch.cuda.synchronize()
+        finally:
+            _lib.set_option("gru_dwhh_batched", 1)
+        grads.append({n: p.grad.detach().clone() for n, p in mine.named_parameters()})
+    for n in grads[0]:
+        a, b = grads[0][n], grads[1][n]
+        if "_hh" in n:   # weight_hh (split order) and bias_hh (the fp32 path's fused row sums)
+            assert ((a - b).norm() / b.norm()).item() <= 1e-5, n
+        else:
+            assert torch.equal(a, b), n
+    assert _lib.spin_timeouts() == 0
+
+
 def test_gemm_16bit_rejects_misaligned(prec):
     A = torch.zeros(16, 12, dtype=TORCH_DT[prec], device="cuda")
     C = torch.zeros(16, 16, device="cuda")

@@ -1089,6 +1089,209 @@ __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
   pp_epilogue(ka, acc, reinterpret_cast<float*>(smem), split, m0, n0, grp, wc, wave, lane, z);
 }
 
+// ------------------------------------------------------------------ skinny GEMMs (VALU)
+// GEMMs with one dimension <= 16 — the 12-class output layer of every model (models/model_*.py
+// `fc`: forward x W^T, dx = dY W, dW = dY^T x with db) — are a few MFLOP: on the 128 x 128 matrix-core
+// tiles they are 15-30 us of launch, staging and split-K reduction each (tools/step_kernels.py, r03s3:
+// 59 us of the 1.45 ms cfg2 bf16 step).  These kernels stream the long operand once, coalesced, and
+// keep the <= 16 short-side accumulators in registers: fp32 FMAs on the operands rounded exactly as
+// the matrix cores would (RND 1 bf16, 2 fp16, nearest-even: the products of two 16-bit values are
+// exact in fp32, so only the fp32 summation order differs from the MFMA kernels); row sums of op(A)
+// from the unrounded values, as in the tile kernels.
+template <int RND>
+__device__ __forceinline__ float rnd16(float x) {
+  if constexpr (RND == 1) return (float)(__bf16)x;
+  else if constexpr (RND == 2) return (float)(_Float16)x;
+  else return x;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ void skinny_store(const GemmDesc& d, int64_t m, int64_t n, float acc) {
+  float v = d.alpha * acc;
+  if (d.bias_mode == 1) v += d.bias[n];
+  else if (d.bias_mode == 2) v += d.bias[m];
+  float* c = d.C + m * d.ldc + n;
+  if (d.beta != 0.f) v += d.beta * *c;
+  *c = v;
+}
+
+// N <= 16, A k-contiguous (!ta): a 256-thread block per row m of C; the 4 waves interleave over k
+// (lane + 64 w + 256 i: A's row read once, coalesced), 4 k per lane per iteration with every load
+// issued before the FMAs (K = 1024: one iteration), N accumulators per lane, a wave reduction per
+// column, then the 4 waves' sums added through LDS in wave order (deterministic).
+template <int RND, bool TB>
+__global__ __launch_bounds__(256) void skinny_n_kernel(GemmDesc d) {
+  __shared__ float part[4][17];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t m = blockIdx.x;
+  float acc[16], rs = 0.f;
+#pragma unroll
+  for (int n = 0; n < 16; ++n) acc[n] = 0.f;
+  const float* __restrict__ a = d.A + m * d.lda;
+  for (int64_t k0 = lane + 64 * w; k0 < d.K; k0 += 1024) {
+    float av[4], bv[4][16];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t k = k0 + 256 * u;
+      const bool ok = k < d.K;
+      const int64_t kc = ok ? k : 0;   // clamped: loads stay unconditional
+      av[u] = ok ? a[kc] : 0.f;
+#pragma unroll
+      for (int n = 0; n < 16; ++n) {
+        const int nn = n < d.N ? n : (int)d.N - 1;   // clamped column, never stored
+        bv[u][n] = TB ? d.B[nn * d.ldb + kc] : d.B[kc * d.ldb + nn];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      rs += av[u];
+      const float ar = rnd16<RND>(av[u]);
+#pragma unroll
+      for (int n = 0; n < 16; ++n) acc[n] = fmaf(ar, rnd16<RND>(bv[u][n]), acc[n]);   // av = 0 past K
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < 16; ++n) {   // predicated, no early exit: the accumulators stay in registers
+    const float t = wave_sum(acc[n]);
+    if (lane == n) part[w][n] = t;
+  }
+  const float r = wave_sum(rs);
+  if (lane == 0) part[w][16] = r;
+  __syncthreads();
+  if (w == 0 && lane < d.N) skinny_store(d, m, lane, ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
+  if (w == 0 && lane == 16 && d.rowsum) {
+    const float t = ((part[0][16] + part[1][16]) + part[2][16]) + part[3][16];
+    d.rowsum[m] = d.rowsum_beta != 0.f ? d.rowsum_beta * d.rowsum[m] + t : t;
+  }
+}
+
+// M <= 16, B row-contiguous (!tb), K <= 1024: a 1024-thread block owns 64 columns of C (lane =
+// column).  op(A) (<= 16 x 1024) is first staged into LDS as [k][16]; the 16 waves split K into 16
+// ranges and walk them 16 k at a time — 16 coalesced B loads in flight per lane, op(A)[., k] read as
+// four broadcast ds_read_b128 — and the 16 partial sums per element are added through LDS in wave
+// order (deterministic).  Block 0 also reduces the row sums (of the unrounded op(A)).
+template <int RND, bool TA>
+__global__ __launch_bounds__(1024) void skinny_m_kernel(GemmDesc d) {
+  __shared__ __attribute__((aligned(16))) float As[1024 * 16];
+  __shared__ float red[16][16][64];
+  __shared__ float rsred[16][16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < d.K * 16; i += 1024) {
+    const int k = i >> 4, m = i & 15;
+    As[i] = m < d.M ? (TA ? d.A[(int64_t)k * d.lda + m] : d.A[(int64_t)m * d.lda + k]) : 0.f;
+  }
+  __syncthreads();
+  const int64_t n = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t nc = n < d.N ? n : d.N - 1;   // clamped: every lane takes part in the loads
+  const int kper = (int)((d.K + 15) / 16), kb = w * kper, ke = kb + kper < d.K ? kb + kper : (int)d.K;
+  float acc[16], rs[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) acc[m] = rs[m] = 0.f;
+  for (int k0 = kb; k0 < ke; k0 += 16) {
+    float bv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const bool ok = k0 + u < ke;
+      bv[u] = ok ? d.B[(int64_t)(k0 + u) * d.ldb + nc] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (k0 + u >= ke) break;   // uniform
+      const float b = rnd16<RND>(bv[u]);
+      const v4f* arow = reinterpret_cast<const v4f*>(As + (k0 + u) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const v4f a4 = arow[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          rs[4 * q + e] += a4[e];
+          acc[4 * q + e] = fmaf(rnd16<RND>(a4[e]), b, acc[4 * q + e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    red[w][m][lane] = acc[m];
+    if (lane == 0) rsred[w][m] = rs[m];
+  }
+  __syncthreads();
+  const int m = w;   // wave m finalizes row m of this block's 64 columns
+  if (m < d.M) {
+    float t = 0.f;
+    for (int q = 0; q < 16; ++q) t += red[q][m][lane];
+    if (n < d.N) skinny_store(d, m, n, t);
+    if (d.rowsum && blockIdx.x == 0 && lane == 0) {
+      float r = 0.f;
+      for (int q = 0; q < 16; ++q) r += rsred[q][m];
+      d.rowsum[m] = d.rowsum_beta != 0.f ? d.rowsum_beta * d.rowsum[m] + r : r;
+    }
+  }
+}
+
+// K <= 16, B row-contiguous (!tb): one thread per C element, block = 256 columns of one row m; the
+// k loop is unrolled so every load is in flight at once (op(A)[m, k] is block-uniform).
+template <int RND, bool TA>
+__global__ __launch_bounds__(256) void skinny_k_kernel(GemmDesc d) {
+  const int64_t m = blockIdx.y, n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t nc = n < d.N ? n : d.N - 1;
+  float av[16], bv[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const bool ok = k < d.K;
+    av[k] = ok ? (TA ? d.A[k * d.lda + m] : d.A[m * d.lda + k]) : 0.f;
+    bv[k] = ok ? d.B[k * d.ldb + nc] : 0.f;
+  }
+  float acc = 0.f, rs = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    rs += av[k];
+    acc = fmaf(rnd16<RND>(av[k]), rnd16<RND>(bv[k]), acc);
+  }
+  if (n < d.N) skinny_store(d, m, n, acc);
+  if (d.rowsum && blockIdx.x == 0 && threadIdx.x == 0)
+    d.rowsum[m] = d.rowsum_beta != 0.f ? d.rowsum_beta * d.rowsum[m] + rs : rs;
+}
+
+template <int RND>
+int launch_skinny_rnd(const GemmDesc& d, int kind, hipStream_t s) {
+  ProfScope prof(RND == 0 ? "gemm_f32" : RND == 1 ? "gemm_bf16" : "gemm_f16", s,
+                 2.0 * (double)d.M * (double)d.N * (double)d.K);
+  const char* kn = kind == 0 ? "skinny_n" : kind == 1 ? "skinny_m" : "skinny_k";
+  prof.detail("%s_kernel<%c%c> %lldx%lldx%lld", kn, d.ta ? 'T' : 'N', d.tb ? 'T' : 'N', (long long)d.M,
+              (long long)d.N, (long long)d.K);
+  if (kind == 0) {
+    const dim3 grid((unsigned)d.M);
+    if (d.tb) hipLaunchKernelGGL((skinny_n_kernel<RND, true>), grid, dim3(256), 0, s, d);
+    else hipLaunchKernelGGL((skinny_n_kernel<RND, false>), grid, dim3(256), 0, s, d);
+  } else if (kind == 1) {
+    const dim3 grid((unsigned)((d.N + 63) / 64));
+    if (d.ta) hipLaunchKernelGGL((skinny_m_kernel<RND, true>), grid, dim3(1024), 0, s, d);
+    else hipLaunchKernelGGL((skinny_m_kernel<RND, false>), grid, dim3(1024), 0, s, d);
+  } else {
+    const dim3 grid((unsigned)((d.N + 255) / 256), (unsigned)d.M);
+    if (d.ta) hipLaunchKernelGGL((skinny_k_kernel<RND, true>), grid, dim3(256), 0, s, d);
+    else hipLaunchKernelGGL((skinny_k_kernel<RND, false>), grid, dim3(256), 0, s, d);
+  }
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+}
+
+// Which skinny kernel takes this GEMM (-1: none; the matrix-core tiles run it).  Sizes keep each
+// kernel's per-thread loop short and its streamed operand a few MB at most.
+int skinny_kind(const GemmDesc& d) {
+  if (!g_opt_gemm_skinny || d.batch != 1 || d.A16 || d.B16 || d.K <= 0) return -1;
+  if (d.N <= 16 && !d.ta && d.M <= 65535 * 16 && d.M * d.K <= (int64_t)1 << 24) return 0;
+  if (d.M <= 16 && !d.tb && d.K <= 1024 && d.N * d.K <= (int64_t)1 << 24) return 1;
+  if (d.K <= 16 && !d.tb && d.M <= 65535 && d.M * d.N <= (int64_t)1 << 24) return 2;
+  return -1;
+}
+
 // ------------------------------------------------------------------ fp32: LDS-DMA ping-pong
 // gemm_p32_kernel: the exact-fp32 GEMM (v_mfma_f32_32x32x2_f32) on the structure of gemm_g16_kernel —
 // 256 x 256 tiles, two 4-wave groups running one section apart behind raw barriers, a ring of four
@@ -1637,6 +1840,11 @@ int gemm_f32(const GemmDesc& d, hipStream_t s) {
   }
   SRK_REQUIRE(d.C && (d.K == 0 || (d.A && d.B)), SRK_ERR_INVALID, "gemm: null operand");
   SRK_REQUIRE(d.bias_mode == 0 || d.bias, SRK_ERR_INVALID, "gemm: bias_mode without bias");
+  if (const int kind = skinny_kind(d); kind >= 0) {   // one dimension <= 16: VALU kernels
+    const int prec = d.prec >= 0 ? d.prec : matmul_prec();
+    return prec == kPrecBF16 ? launch_skinny_rnd<1>(d, kind, s)
+           : prec == kPrecF16 ? launch_skinny_rnd<2>(d, kind, s) : launch_skinny_rnd<0>(d, kind, s);
+  }
   SRK_REQUIRE(!d.rowsum || d.batch == 1 || d.prec == kPrecF32 || (d.prec < 0 && matmul_prec() == kPrecF32),
               SRK_ERR_INVALID, "gemm: batched rowsum needs fp32 operands");
   // 16-B loads need 16-B aligned rows, K % 4 == 0 when an operand is k-contiguous (a clamped k vector

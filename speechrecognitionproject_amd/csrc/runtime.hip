@@ -34,6 +34,7 @@ int g_opt_gru_dc = 1;
 unsigned g_opt_gru_dc_offset = 200;
 int g_opt_gru_fast_cell = 1;
 int g_opt_gru_dwhh_batched = 1;
+int g_opt_gemm_skinny = 1;
 std::atomic<int64_t> g_scratch_gen{0};
 
 static thread_local std::string g_last_error;
@@ -385,6 +386,10 @@ int srk_set_option(const char* name, int64_t value) {
   }
   if (n == "gru_lp_wide") {   // 16-bit recurrence over > 256 rows: 64-row workgroups in one launch (1) or 256-row chunks (0)
     srk::g_opt_gru_lp_wide = value != 0;
+    return SRK_OK;
+  }
+  if (n == "gemm_skinny") {   // GEMMs with a dimension <= 16 on the VALU kernels (1) or the matrix-core tiles (0)
+    srk::g_opt_gemm_skinny = value != 0;
     return SRK_OK;
   }
   if (n == "gru_dwhh_batched") {   // 16-bit GRU backward: both directions' dW_hh in one batched GEMM (1) or two (0)

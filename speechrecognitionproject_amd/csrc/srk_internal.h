@@ -93,7 +93,8 @@ extern int g_opt_gemm16_kernel;
 // Kernel of the fp32 GEMM (srk_set_option "gemm32_kernel"): 0 = by shape, 1 = register-staged
 // gemm_f32_kernel, 2 = LDS-DMA ping-pong gemm_p32_kernel.
 extern int g_opt_gemm32_kernel;
-extern int g_opt_gru_dwhh_batched;   // 16-bit GRU backward: one batched dW_hh GEMM for both directions
+extern int g_opt_gru_dwhh_batched;
+extern int g_opt_gemm_skinny;   // GEMMs with a dimension <= 16 on the VALU skinny kernels   // 16-bit GRU backward: one batched dW_hh GEMM for both directions
 // 16-bit conv operand sources (srk_set_option "conv16_sources", default 1): bf16 / fp16 convolutions
 // gather from one pre-rounded 16-bit copy of x / dY / the weights (0 = round at LDS-store time).
 extern int g_opt_conv16_sources;

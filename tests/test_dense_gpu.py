@@ -27,6 +27,54 @@ def test_gemm_f32(gpu, ta, tb, M, N, K):
     assert (out - ref).abs().max() <= 1e-5 * (1 + (A.abs().max() * B.abs().max() * K).item())
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
+@pytest.mark.parametrize("ta,tb,M,N,K", [
+    (0, 1, 256, 12, 1024), (0, 0, 256, 12, 1024), (0, 1, 5, 1, 3), (0, 0, 1000, 16, 4097),   # N <= 16, A k-contiguous
+    (1, 0, 12, 1024, 256), (0, 0, 16, 777, 300), (1, 0, 1, 5, 1),                            # M <= 16, B row-contiguous
+    (0, 0, 256, 1024, 12), (1, 0, 300, 515, 16), (0, 0, 70, 9, 1)])                          # K <= 16
+def test_gemm_skinny(gpu, precision, ta, tb, M, N, K):
+    """GEMMs with a dimension <= 16 (the output layers' fc GEMMs) on the VALU skinny kernels (option
+    gemm_skinny): == float64 product of the (rounded, in bf16 / fp16 mode) operands with alpha, beta,
+    bias, and the fused row sums of the UNROUNDED op(A); == the matrix-core tile path within fp32
+    summation order."""
+    from speechrecognitionproject_amd import _lib
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K + ta)
+    A = torch.randn((K, M) if ta else (M, K), generator=g)
+    B = torch.randn((N, K) if tb else (K, N), generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    dt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[precision]
+    opA, opB = (A.T if ta else A), (B.T if tb else B)
+    ref = 0.5 * (opA.to(dt).double() @ opB.to(dt).double()) + 2.0 * C0.double() + bias.double()
+    tol = 2e-6 * (1 + (opA.abs().double() @ opB.abs().double()).max().item())
+    Ad, Bd = A.cuda(), B.cuda()
+    _lib.set_matmul_precision(precision)
+    outs = []
+    try:
+        for skinny in (1, 0):
+            _lib.set_option("gemm_skinny", skinny)
+            _lib.prof_enable(1)
+            Cd = C0.clone().cuda()
+            call("srk_gemm_f32", ta, tb, M, N, K, 0.5, ptr(Ad), Ad.shape[1], ptr(Bd), Bd.shape[1], 2.0, ptr(Cd), N,
+                 ptr(bias.cuda()), 1, stream_ptr())
+            rs = torch.full((M,), 3.0, device="cuda")
+            Cr = torch.zeros(M, N, device="cuda")
+            call("srk_gemm_rowsum_f32", ta, tb, M, N, K, 1.0, ptr(Ad), Ad.shape[1], ptr(Bd), Bd.shape[1], 0.0,
+                 ptr(Cr), N, ptr(rs), stream_ptr())
+            torch.cuda.synchronize()
+            kinds = [k["kernel"] for k in _lib.prof_kernels()]
+            _lib.prof_enable(0)
+            assert all(("skinny" in k) == bool(skinny) for k in kinds), kinds
+            outs.append((Cd.cpu().double(), rs.cpu().double()))
+    finally:
+        _lib.set_option("gemm_skinny", 1)
+        _lib.set_matmul_precision("fp32")
+    for c, r in outs:
+        assert (c - ref).abs().max().item() <= tol
+        assert (r - opA.double().sum(1)).abs().max().item() <= 1e-4 * (1 + K ** 0.5)   # beta 0: rs overwritten
+    assert (outs[0][0] - outs[1][0]).abs().max().item() <= 2 * tol
+
+
 def _ref_gru(IN, H, L):
     return torch.nn.GRU(IN, H, num_layers=L, bidirectional=True, batch_first=True)
 

@@ -18,8 +18,8 @@ import os
 import re
 import sqlite3
 
-GROUPS = {  # srk_prof name -> substrings of the rocprof kernel symbols it covers
-    "gemm_f32": ("gemm_f32_kernel", "gemm_p32_kernel"), "gemm_bf16": ("gemm_h16_kernel", "gemm_lp_kernel", "gemm_g16_kernel"),
+GROUPS = {  # srk_prof name -> substrings of the rocprof kernel symbols it covers (GEMMs: _gemm_group)
+    "gemm_f32": (), "gemm_bf16": (), "gemm_f16": (), "splitk_reduce": (),
     "gru_fwd_seq": ("gru_fwd_persistent_kernel", "gru_fwd_persistent_dc_kernel"),
     "gru_bwd_seq": ("gru_bwd_persistent_kernel", "gru_bwd_persistent_dc_kernel"),
     "gru_fwd_seq_lp": ("gru_fwd_persistent_lp_kernel", "gru_fwd_persistent_lp2_kernel"),
@@ -39,13 +39,31 @@ def _conv_group(name):
     return ("conv_fwd", "conv_dgrad", "conv_wgrad")[int(m.group(1))] + ("_lp" if m.group(2) != "0" else "")
 
 
+def _gemm_group(name):
+    """The srk_prof GEMM category of a kernel symbol: the operand precision is a template argument
+    (gemm_g16_kernel<TA, TB, F16>, gemm_h16_kernel<.., F16>, gemm_lp_kernel<.., F16, PF>, skinny_*<RND, ..>).
+    The split-K slab / row-sum reductions (run inside the GEMM's timed scope) are reported on their own."""
+    if "splitk_reduce" in name or "rowsum_reduce" in name:
+        return "splitk_reduce"
+    if "gemm_f32_kernel" in name or "gemm_p32_kernel" in name:
+        return "gemm_f32"
+    m = re.search(r"skinny_[nmk]_kernel<(\d)", name)
+    if m:
+        return ("gemm_f32", "gemm_bf16", "gemm_f16")[int(m.group(1))]
+    for k, pos in (("gemm_g16_kernel<", 2), ("gemm_h16_kernel<", 5), ("gemm_lp_kernel<", 6)):
+        if k in name:
+            args = [x.strip() for x in name.split(k, 1)[1].split(">", 1)[0].split(",")]
+            return "gemm_f16" if len(args) > pos and args[pos] in ("true", "1") else "gemm_bf16"
+    return None
+
+
 def collect(d, counter):
     db = sorted(glob.glob(os.path.join(d, "**", "*.db"), recursive=True))[0]
     c = sqlite3.connect(db)
     out = {}
     for name, n, tot in c.execute("select kernel_name, count(*), sum(value) from counters_collection where "
                                   "counter_name = ? group by kernel_name", (counter,)):
-        cg = _conv_group(name)
+        cg = _conv_group(name) or _gemm_group(name)
         for g, subs in GROUPS.items():
             if (g == cg) if cg else any(sub in name for sub in subs):
                 a = out.setdefault(g, [0, 0.0])

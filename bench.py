@@ -46,14 +46,17 @@ come from a separate eager pass of the same step (--prof-steps, default 5), repo
 
 Default run (no --model): the cfg2 headline, then compact records under "configs" for BASELINE.json's
 other configs at their per-GPU batch — cfg3 fbanks_cnn fp32 512, cfg4 resnet_bgru fp32 512, cfg5
-spec_bgru fp16 512 with the noise-mix in the step — each with value / ms_per_step / roofline
-(--no-configs skips them).
+spec_bgru fp16 512 with the noise-mix in the step (static loss scale 1024 with the overflow check and
+skip) — and the metric's literal MFCC+CNN-BiGRU model (mfrn_bgru fp32 256), each with value /
+ms_per_step / roofline (--no-configs skips them); "h2d": the cfg2 step (fp32 and bf16) fed from
+pinned host memory with a double-buffered upload (SURVEY.md §8d's second figure; --no-h2d skips it);
+"feature_roofline_other": K2 (fbank) and K3 (spectrogram) alone on 65,536 clips.
 
 Measurement extras on the same line:
   roofline     — the dominant kernel of the timed steps, timed live with HIP events on its launch
                  stream (srk_prof_*), algorithmic flops / avg launch time vs the MFMA peak of its
                  operand type (fp32 157.3 TF, bf16/fp16 2.5 PF dense);
-  mfcc_roofline— K1 alone on 65,536 clips (HBM-bound): algorithmic bytes / time vs 8 TB/s;
+  feature_roofline — K1 alone on 65,536 clips (HBM-bound): algorithmic bytes / time vs 8 TB/s;
   cpu_baseline — the CPU restatement (oracle/: numpy features per clip + torch-CPU train step) timed
                  on this host's cores (every core this process may use, plus a
                  1-thread figure) on a bounded sample at the config's batch (rank 0, N = 1 only);
@@ -74,12 +77,13 @@ sys.path.insert(0, REPO)
 
 from speechrecognitionproject_amd import _lib, features, parallel   # noqa: E402
 from speechrecognitionproject_amd.nn import CrossEntropyLoss          # noqa: E402
-from speechrecognitionproject_amd.optim import Adam, FlatParams       # noqa: E402
+from speechrecognitionproject_amd.optim import Adam, FlatParams, LossScaler   # noqa: E402
 from speechrecognitionproject_amd.synthetic import synthetic_clips    # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3     # MI355X_MICROARCH.md, dense fp32 matrix (= vector) peak
 PEAK_LP_MFMA_TFLOPS = 2500.0      # MI355X_MICROARCH.md, dense bf16 / fp16 MFMA peak (no sparsity)
-FP16_LOSS_SCALE = 1024.0          # static loss scale of the fp16 mode (unscaled in the Adam kernel)
+FP16_LOSS_SCALE = 1024.0          # static loss scale of the fp16 mode (optim.LossScaler: unscaled in the Adam
+                                  # kernel, a step with inf / NaN gradients skipped and counted)
 PEAK_HBM_GBS = 8000.0             # MI355X HBM3E spec
 MFCC_BYTES_PER_CLIP = 71956       # 64,000 in + 7,956 out
 # FlopCounterMode on the reference modules (cnn_bgru / spec_cnn: on the oracle restatements)
@@ -104,7 +108,7 @@ MATRIX_KERNELS = ("gru_fwd_seq", "gru_bwd_seq", "gru_fwd_step", "gru_bwd_step", 
                   "conv_fwd_lp", "conv_dgrad_lp", "conv_wgrad_lp")
 LP_KERNELS = ("gemm_bf16", "gemm_f16", "gru_fwd_seq_lp", "gru_bwd_seq_lp", "conv_fwd_lp", "conv_dgrad_lp",
               "conv_wgrad_lp")
-OTHER_KERNELS = ("mfcc", "fbank", "spec", "noise_mix", "adam", "batchnorm_fwd", "batchnorm_bwd", "conv1_pool_fwd",
+OTHER_KERNELS = ("mfcc", "fbank", "spec", "noise_mix", "adam", "grad_check", "batchnorm_fwd", "batchnorm_bwd", "conv1_pool_fwd",
                  "conv1_pool_wgrad",
                  "maxpool_fwd", "maxpool_bwd", "conv_to16")
 
@@ -214,9 +218,10 @@ def pmc_traffic(kernel, cmd):
     return None if v is None else v["total"]
 
 
-def feature_roofline(model_name, n_clips=65536):
-    """The model's feature kernel alone on a large batch (HBM-bound): algorithmic bytes / time."""
-    name, per_clip = FEATURE[model_name]
+def feature_roofline(model_name=None, n_clips=65536, kernel=None):
+    """A feature kernel alone on a large batch (HBM-bound): algorithmic bytes / time.  `kernel` (mfcc /
+    fbank / spec) or the feature kernel of `model_name`."""
+    name, per_clip = FEATURE[model_name] if kernel is None else next(v for v in FEATURE.values() if v[0] == kernel)
     fn = {"mfcc": lambda x, out=None: features.mfcc(x, time_major=True, out=out), "fbank": features.fbank,
           "spec": lambda x, out=None: features.spec(x, transposed=True, out=out)}[name]   # the models' layouts
     x, _ = synthetic_clips(1024, seed=123)
@@ -304,10 +309,11 @@ def plumbing(args, rank, world):
               flush=True)
 
 
-EXTRA_CONFIGS = (  # BASELINE.json configs[2..4] at their per-GPU batch (the default run appends them)
-    ("cfg3", "fbanks_cnn", "fp32", 512, 10),
+EXTRA_CONFIGS = (  # BASELINE.json configs[2..4] at their per-GPU batch (the default run appends them), and
+    ("cfg3", "fbanks_cnn", "fp32", 512, 10),     # the metric's literal "MFCC+CNN-BiGRU" model
     ("cfg4", "resnet_bgru", "fp32", 512, 4),
     ("cfg5", "spec_bgru", "fp16", 512, 20),
+    ("mfrn", "mfrn_bgru", "fp32", 256, 10),
 )
 
 
@@ -328,7 +334,7 @@ class Workload:
         parallel.broadcast_flat(self.flat)
         self.reducer = None
         self.crit = CrossEntropyLoss()
-        self.loss_scale = 1.0
+        self.scaler = None
         pool = args.pool
         x, y = synthetic_clips(pool * B, seed=1000 + rank, clip=30000 if model_name == "spec_bgru" else 32767)
         self.lab = torch.from_numpy(y).to(dev).view(pool, B)
@@ -362,7 +368,7 @@ class Workload:
             self.reducer.begin()
         out = self.model(self._inputs(srcs))
         loss = self.crit(out, lab)
-        (loss * self.loss_scale if self.loss_scale != 1.0 else loss).backward()
+        (self.scaler.scale(loss) if self.scaler is not None else loss).backward()
         return loss
 
     def _exchange_and_update(self):
@@ -370,7 +376,7 @@ class Workload:
             self.reducer.finish()        # bucketed all-reduces launched during backward
         else:
             parallel.allreduce_grads(self.flat)
-        self.opt.step()
+        self.opt.step(scaler=self.scaler)
 
     def eager_step(self, i):
         loss = self._fwd_bwd(self._batch(i), self.lab[i % self.args.pool])
@@ -381,7 +387,7 @@ class Workload:
         j = self._slot
         loss = self._fwd_bwd(self._batch(j), self.lab[j])
         if self.world == 1:
-            self.opt.step()
+            self.opt.step(scaler=self.scaler)
         return loss
 
     def run(self, precision, steps, warmup, graph):
@@ -390,8 +396,8 @@ class Workload:
         log("bench: %s %s B=%d, %d warm-up + %d timed steps%s" % (self.name, precision, self.B, warmup, steps,
                                                                    " (HIP graph)" if graph else ""))
         _lib.set_matmul_precision(precision)
-        self.loss_scale = FP16_LOSS_SCALE if precision == "fp16" else 1.0
-        self.opt.grad_scale = 1.0 / (self.world * self.loss_scale)
+        self.scaler = LossScaler(FP16_LOSS_SCALE, dynamic=False, device=self.dev) if precision == "fp16" else None
+        self.opt.grad_scale = 1.0 / self.world
         self.reducer = (parallel.GradReducer(self.flat, bucket_mb=args.bucket_mb)
                         if (self.world > 1 and args.overlap and not graph) else None)
         graphs = []
@@ -460,9 +466,77 @@ class Workload:
         torch.cuda.empty_cache()
         cmd = {"model": self.name, "batch": self.B, "world": self.world, "precision": precision,
                "sync_bn": bool(args.sync_bn)}
+        skipped = self.scaler.overflows() if self.scaler is not None else None
         return {"el": el, "steps": steps, "warmup": warmup, "graph": bool(graph), "final_loss": final_loss,
+                "fp16_skipped_steps": skipped,
                 "kernels": kernels, "roofline": roofline(kernels, singles, cmd), "eager_ms": eager_ms,
                 "prof_steps": args.prof_steps if (graph and prof) else steps}
+
+
+def _workload_h2d(self, precision, steps, warmup):
+    """The graphed step fed from pinned host memory: 2 device batch slots (graphs 0 / 1 read pcm[0] /
+    pcm[1]), host batches uploaded on a copy stream one step ahead.  Returns utt/s over the wall time
+    of `steps` steps (uploads included) and the upload rate; plus the bare upload rate (copies only)."""
+    assert self.name != "spec_bgru" and self.args.pool >= 2
+    from speechrecognitionproject_amd.graphs import GraphedStep
+    _lib.set_matmul_precision(precision)
+    self.scaler = LossScaler(FP16_LOSS_SCALE, dynamic=False, device=self.dev) if precision == "fp16" else None
+    self.opt.grad_scale = 1.0 / self.world
+    n_host = 8
+    x, _ = synthetic_clips(n_host * self.B, seed=4000 + self.rank)
+    host = torch.from_numpy(x).view(n_host, self.B, -1).pin_memory()
+    graphs = []
+    for j in range(2):
+        self._slot = j
+        graphs.append(GraphedStep(self._graph_body, warmup=max(2, warmup) if j == 0 else 0,
+                                  pool=graphs[0].pool() if graphs else None))
+    cs = torch.cuda.Stream()
+    cur = torch.cuda.current_stream()
+    ev_copy = [torch.cuda.Event() for _ in range(2)]
+    ev_done = [torch.cuda.Event() for _ in range(2)]
+    for e in ev_done:
+        e.record(cur)
+
+    def upload(i):
+        j = i % 2
+        cs.wait_event(ev_done[j])              # the step that last read slot j has finished
+        with torch.cuda.stream(cs):
+            self.pcm[j].copy_(host[i % n_host], non_blocking=True)
+            ev_copy[j].record(cs)
+
+    def run(n):
+        upload(0)
+        for i in range(n):
+            j = i % 2
+            cur.wait_event(ev_copy[j])
+            graphs[j].replay()
+            ev_done[j].record(cur)
+            if i + 1 < n:
+                upload(i + 1)
+
+    run(4)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # the upload alone, same buffers and stream
+    t1 = time.perf_counter()
+    for i in range(steps):
+        with torch.cuda.stream(cs):
+            self.pcm[i % 2].copy_(host[i % n_host], non_blocking=True)
+    cs.synchronize()
+    el_copy = time.perf_counter() - t1
+    for g in graphs:
+        g.release()
+    torch.cuda.empty_cache()
+    step_bytes = self.B * 16000 * 4
+    return {"value": round(self.B * steps / el, 2), "unit": "utt/s", "ms_per_step": round(el / steps * 1e3, 3),
+            "upload_bytes_per_step": step_bytes, "needed_gbs": round(step_bytes / (el / steps) / 1e9, 2),
+            "upload_only_gbs": round(step_bytes * steps / el_copy / 1e9, 2), "steps": steps}
+
+
+Workload.run_h2d = _workload_h2d
 
 
 def roofline(kernels, singles, cmd):
@@ -514,6 +588,8 @@ def main():
     ap.add_argument("--no-configs", dest="configs", action="store_false",
                     help="skip the cfg3 / cfg4 / cfg5 records of the default run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-h2d", dest="h2d", action="store_false",
+                    help="skip the default run's \"h2d\" record (the cfg2 step fed from pinned host memory)")
     ap.add_argument("--no-prof", action="store_true")
     ap.add_argument("--no-feature-roofline", "--no-mfcc-roofline", dest="no_feature_roofline", action="store_true")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
@@ -550,6 +626,16 @@ def main():
     lp_rec = None
     if args.lowprec and args.precision == "fp32":
         lp_rec = wl.run("bf16", args.steps, args.warmup, args.graph)
+        _lib.set_matmul_precision(args.precision)
+    h2d_rec = None
+    if default_run and args.h2d:
+        # SURVEY.md §8d's second figure: the same step fed from pinned host PCM (the reference's
+        # DataLoader -> .to(DEVICE) crossing, training.py:77,86), the upload double-buffered
+        h2d_rec = {"what": "cfg2 train step (HIP-graph replays) with each batch uploaded from pinned host memory "
+                           "(float32 PCM, what Dataset yields) on a copy stream, double-buffered: batch i+1 uploads "
+                           "while step i runs; value = clips / wall time including every upload"}
+        for prec in ("fp32", "bf16"):
+            h2d_rec[prec] = wl.run_h2d(prec, args.steps, args.warmup)
         _lib.set_matmul_precision(args.precision)
     del wl
     extras = []
@@ -598,6 +684,8 @@ def main():
                        "eager_ms_per_step": round(lp_rec["eager_ms"], 3) if lp_rec["eager_ms"] else None,
                        "final_loss": round(lp_rec["final_loss"], 5), "roofline": lp_rec["roofline"],
                        "kernels": kern(lp_rec["kernels"])}
+    if main_rec["fp16_skipped_steps"] is not None:
+        res["loss_scale"] = {"kind": "static", "scale": FP16_LOSS_SCALE, "skipped_steps": main_rec["fp16_skipped_steps"]}
     if main_rec["eager_ms"]:
         res["eager_ms_per_step"] = round(main_rec["eager_ms"], 3)
     if extras:
@@ -606,10 +694,17 @@ def main():
                            "value": round(world * r["B"] * r["steps"] / r["el"], 2), "unit": "utt/s",
                            "ms_per_step": round(r["el"] / r["steps"] * 1e3, 3),
                            "eager_ms_per_step": round(r["eager_ms"], 3) if r["eager_ms"] else None,
-                           "final_loss": round(r["final_loss"], 5), "roofline": r["roofline"]} for r in extras]
+                           "final_loss": round(r["final_loss"], 5), "roofline": r["roofline"],
+                           **({"loss_scale": {"kind": "static", "scale": FP16_LOSS_SCALE,
+                                              "skipped_steps": r["fp16_skipped_steps"]}}
+                              if r["fp16_skipped_steps"] is not None else {})} for r in extras]
     if not args.no_feature_roofline and args.model in FEATURE:
         log("bench: feature roofline")
         res["feature_roofline"] = feature_roofline(args.model)
+        if default_run:   # K2 / K3 (the fbank and spectrogram configs' feature kernels) on the same line
+            res["feature_roofline_other"] = [feature_roofline(kernel=k) for k in ("fbank", "spec")]
+    if h2d_rec is not None:
+        res["h2d"] = h2d_rec
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.model, B, args.cpu_seconds)
     print(json.dumps(res), flush=True)

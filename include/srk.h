@@ -302,6 +302,20 @@ int srk_adam_step(float* param, const float* grad, float* exp_avg, float* exp_av
  * corrections on the device (double precision, as srk_adam_step's host side).                    */
 int srk_adam_step_state(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float beta1,
                         float beta2, float eps, int64_t* state, float grad_scale, void* stream);
+/* Loss scaling for 16-bit training (torch.cuda.amp.GradScaler semantics, on the device so a
+ * captured step replays it).  scaler: 8 x 32-bit device words {float scale, float 1/scale, float
+ * growth, float backoff, int found_inf, int good_steps, int growth_interval, int overflows};
+ * growth_interval 0 = static scale.  The caller multiplies the loss by scale (word 0) before
+ * backward.  No reference counterpart: the reference trains fp32 only (training.py:85-91).       */
+int srk_grad_scaler_init(int32_t* scaler, float init_scale, float growth_factor, float backoff_factor,
+                         int growth_interval, void* stream);
+/* srk_adam_step_state on loss-scaled gradients: one pass flags any non-finite gradient element;
+ * if one is found the step is SKIPPED (parameters, moments and the step count unchanged), the
+ * overflow counter (word 7) advances and a dynamic scale backs off; otherwise the gradients are
+ * multiplied by grad_scale / scale inside the update and a dynamic scale grows after
+ * growth_interval clean steps.                                                                    */
+int srk_adam_step_scaled(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float beta1,
+                         float beta2, float eps, int64_t* state, float grad_scale, int32_t* scaler, void* stream);
 /* nn.Dropout(p) training forward: keep[i] = Bernoulli(1-p) from a counter-based hash of
  * (seed, i) (not torch's RNG stream), y = keep ? x / (1-p) : 0.                              */
 int srk_dropout_fwd(const float* x, int64_t n, float p, uint64_t seed, float* y, uint8_t* keep, void* stream);

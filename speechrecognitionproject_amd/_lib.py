@@ -78,6 +78,8 @@ _SIGS = {
     "srk_dropout_fwd": [_P, _I64, _F, ctypes.c_uint64, _P, _P, _P],
     "srk_dropout_fwd_state": [_P, _I64, _F, _P, _P, _P, _P],
     "srk_adam_step_state": [_P, _P, _P, _P, _I64, _F, _F, _F, _P, _F, _P],
+    "srk_grad_scaler_init": [_P, _F, _F, _F, _I, _P],
+    "srk_adam_step_scaled": [_P, _P, _P, _P, _I64, _F, _F, _F, _P, _F, _P, _P],
     "srk_dropout_apply": [_P, _P, _I64, _F, _P, _P],
 }
 _RESTYPE = {"srk_last_error": ctypes.c_char_p, "srk_spin_timeouts": ctypes.c_int64, "srk_scratch_generation": ctypes.c_int64, "srk_gru_workspace_floats": ctypes.c_int64,

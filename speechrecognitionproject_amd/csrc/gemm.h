@@ -32,6 +32,10 @@ struct GemmDesc {
 // Enqueue on `stream`; returns SRK_OK or an srk_status.
 int gemm_f32(const GemmDesc& d, hipStream_t stream);
 
+// Whether gemm_f32 accepts `d` with batch > 1 AND fused row sums (the fp32-operand ping-pong
+// kernel only); callers fall back to one launch per batch entry otherwise.
+bool gemm_f32_batched_rowsum_ok(const GemmDesc& d);
+
 // Column sums: out[n] = beta*out[n] + sum_m X[m, n] (X row-major [M,N], ldx).
 int colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out, float beta, hipStream_t stream);
 

@@ -1815,6 +1815,21 @@ int dispatch_tile(const GemmDesc& d, hipStream_t s, bool vec) {
 
 }  // namespace
 
+bool gemm_f32_batched_rowsum_ok(const GemmDesc& d) {
+  // mirrors gemm_f32 -> dispatch_tile: batched row sums exist only on the fp32-operand ping-pong
+  // kernel (fp32 precision, 16-B operand rows, 32-bit buffer extents, not overridden to kernel 1)
+  const int prec = d.prec >= 0 ? d.prec : matmul_prec();
+  if (prec != kPrecF32 || d.A16 || d.B16 || d.tb || g_opt_gemm32_kernel == 1) return false;
+  const bool kc_operand = !d.ta || d.tb;
+  const bool vec = (d.lda % 4 == 0) && ((uintptr_t)d.A % 16 == 0) && (d.sA % 4 == 0) && (d.ldb % 4 == 0) &&
+                   ((uintptr_t)d.B % 16 == 0) && (d.sB % 4 == 0) && (!kc_operand || d.K % 4 == 0) &&
+                   (!d.ta || d.M % 4 == 0) && (d.tb || d.N % 4 == 0);
+  const double ext_a = (double)(d.ta ? d.K : d.M) * d.lda * 4, ext_b = (double)(d.tb ? d.N : d.K) * d.ldb * 4;
+  // a batched launch spans batch - 1 strides past the first operand
+  const double span_a = ext_a + (double)(d.batch - 1) * d.sA * 4, span_b = ext_b + (double)(d.batch - 1) * d.sB * 4;
+  return vec && span_a < 2147483000.0 && span_b < 2147483000.0;
+}
+
 int gemm_f32(const GemmDesc& d, hipStream_t s) {
   SRK_REQUIRE(d.M >= 0 && d.N >= 0 && d.K >= 0 && d.batch >= 1, SRK_ERR_INVALID, "gemm: bad shape");
   if (d.M == 0 || d.N == 0) return SRK_OK;

@@ -696,8 +696,7 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
     g.rowsum = db_hh; g.rowsum_beta = beta;
     g.batch = 2; g.sA = BT * 3 * H - 3 * H; g.sB = 3 * H; g.sC = 3 * H * H; g.sRS = 3 * H;
     // (the batched row sums exist on the ping-pong kernel only: 16-B rows, 32-bit buffer offsets)
-    const bool batched = srk::g_opt_gru_dwhh_batched && H % 4 == 0 && (double)BT * 3 * H * 4 < 2.1e9 &&
-                         (double)BT * 2 * H * 4 < 2.1e9;
+    const bool batched = srk::g_opt_gru_dwhh_batched && srk::gemm_f32_batched_rowsum_ok(g);
     if (g.K > 0 && batched) {
       if ((rc = srk::gemm_f32(g, s))) return rc;
     } else if (g.K > 0) {

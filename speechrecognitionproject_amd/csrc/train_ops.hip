@@ -3,6 +3,9 @@
 //  * Adam (beta1, beta2, eps; no weight decay, no amsgrad)     — torch.optim.Adam, training.py:74,91
 //    over one flat fp32 parameter buffer (one launch for the whole model)
 //  * inverted dropout with an explicit mask                     — nn.Dropout(), model_fbanks_cnn.py:79,98
+#include <cfloat>
+#include <cmath>
+
 #include "srk_internal.h"
 
 namespace srk {
@@ -113,9 +116,66 @@ __global__ void dropout_fwd_kernel(const float* __restrict__ x, int64_t n, float
   y[i] = k ? x[i] * scale : 0.f;
 }
 
+// Loss-scaler state (include/srk.h srk_grad_scaler_init): 8 words on the device.
+struct ScalerState {
+  float scale, inv_scale, growth, backoff;
+  int found_inf, good_steps, interval, overflows;
+};
+
+__global__ void scaler_init_kernel(ScalerState* __restrict__ s, float scale, float growth, float backoff,
+                                   int interval) {
+  s->scale = scale;
+  s->inv_scale = 1.0f / scale;
+  s->growth = growth;
+  s->backoff = backoff;
+  s->found_inf = 0;
+  s->good_steps = 0;
+  s->interval = interval;
+  s->overflows = 0;
+}
+
+// found_inf |= any non-finite gradient element (16-B loads; one atomic per wave that saw one).
+__global__ __launch_bounds__(256) void finite_check_kernel(const float* __restrict__ g, int64_t n,
+                                                           ScalerState* __restrict__ s) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  bool bad = false;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 3 < n) {
+      const float4 v = *reinterpret_cast<const float4*>(g + i);
+      // |x| <= FLT_MAX is false exactly for +-inf and NaN
+      bad |= !(fabsf(v.x) <= FLT_MAX) || !(fabsf(v.y) <= FLT_MAX) || !(fabsf(v.z) <= FLT_MAX) ||
+             !(fabsf(v.w) <= FLT_MAX);
+    } else {
+      for (int64_t k = i; k < n; ++k) bad |= !(fabsf(g[k]) <= FLT_MAX);
+    }
+  }
+  if (__ballot(bad) != 0 && (threadIdx.x & 63) == 0) atomicOr(&s->found_inf, 1);
+}
+
+// After the (possibly skipped) update: count / back off on an overflow, grow the scale after
+// `interval` clean steps (interval 0 = static scale), clear the flag for the next step.
+__global__ void scaler_update_kernel(ScalerState* __restrict__ s) {
+  if (s->found_inf) {
+    s->overflows += 1;
+    s->good_steps = 0;
+    if (s->interval > 0) {
+      s->scale *= s->backoff;
+      s->inv_scale = 1.0f / s->scale;
+    }
+  } else if (s->interval > 0 && ++s->good_steps >= s->interval) {
+    s->scale *= s->growth;
+    s->inv_scale = 1.0f / s->scale;
+    s->good_steps = 0;
+  }
+  s->found_inf = 0;
+}
+
 // Device-resident optimizer step (graph-replayable): one lane advances the step count and stores the
-// bias corrections the host path would compute (double precision, rounded to float) beside it.
-__global__ void adam_prep_kernel(int64_t* __restrict__ state, float beta1, float beta2) {
+// bias corrections the host path would compute (double precision, rounded to float) beside it.  A
+// step the loss scaler skips (non-finite gradients) does not count, as with torch's GradScaler.
+__global__ void adam_prep_kernel(int64_t* __restrict__ state, float beta1, float beta2,
+                                 const ScalerState* __restrict__ sc) {
+  if (sc && sc->found_inf) return;
   const int64_t step = state[0] + 1;
   state[0] = step;
   float* bc = reinterpret_cast<float*>(state + 1);
@@ -128,7 +188,12 @@ __global__ void adam_prep_kernel(int64_t* __restrict__ state, float beta1, float
 __global__ __launch_bounds__(256) void adam_state_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                          float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                          float b1, float b2, float eps,
-                                                         const int64_t* __restrict__ state, float grad_scale) {
+                                                         const int64_t* __restrict__ state, float grad_scale,
+                                                         const ScalerState* __restrict__ sc) {
+  if (sc) {
+    if (sc->found_inf) return;     // skipped step: parameters and moments stay as they are
+    grad_scale *= sc->inv_scale;
+  }
   const float* f = reinterpret_cast<const float*>(state + 1);   // bc1, sqrt(bc2), lr
   adam_body(p, g, m, v, n, f[2], b1, b2, eps, f[0], f[1], grad_scale);
 }
@@ -205,12 +270,56 @@ int srk_adam_step_state(float* param, const float* grad, float* exp_avg, float* 
   SRK_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0 &&
               (uintptr_t)state % 8 == 0, SRK_ERR_INVALID, "adam_state: buffers must be 16-byte aligned");
   hipStream_t s = srk::as_stream(stream);
-  hipLaunchKernelGGL(srk::adam_prep_kernel, dim3(1), dim3(1), 0, s, state, beta1, beta2);
+  hipLaunchKernelGGL(srk::adam_prep_kernel, dim3(1), dim3(1), 0, s, state, beta1, beta2,
+                     (const srk::ScalerState*)nullptr);
   const int nt = 256;
   const int64_t blocks = std::min<int64_t>((n + nt * 4 - 1) / (nt * 4), 256 * 8);
   srk::ProfScope prof("adam", s, 28.0 * (double)n);   // p,g,m,v read + p,m,v written
   hipLaunchKernelGGL(srk::adam_state_kernel, dim3((unsigned)blocks), dim3(nt), 0, s, param, grad, exp_avg, exp_avg_sq,
-                     n, beta1, beta2, eps, state, grad_scale);
+                     n, beta1, beta2, eps, state, grad_scale, (const srk::ScalerState*)nullptr);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_grad_scaler_init(int32_t* scaler, float init_scale, float growth_factor, float backoff_factor,
+                         int growth_interval, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(scaler && (uintptr_t)scaler % 4 == 0, SRK_ERR_INVALID, "grad_scaler_init: null / misaligned state");
+  SRK_REQUIRE(init_scale > 0.f && std::isfinite(init_scale) && growth_factor >= 1.f && backoff_factor > 0.f &&
+                  backoff_factor <= 1.f && growth_interval >= 0,
+              SRK_ERR_INVALID, "grad_scaler_init: bad scale / growth / backoff / interval");
+  hipLaunchKernelGGL(srk::scaler_init_kernel, dim3(1), dim3(1), 0, srk::as_stream(stream),
+                     reinterpret_cast<srk::ScalerState*>(scaler), init_scale, growth_factor, backoff_factor,
+                     growth_interval);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+  SRK_API_END
+}
+
+int srk_adam_step_scaled(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float beta1,
+                         float beta2, float eps, int64_t* state, float grad_scale, int32_t* scaler, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(n >= 0 && state && scaler, SRK_ERR_INVALID, "adam_scaled: bad n / null state");
+  SRK_REQUIRE(n == 0 || (param && grad && exp_avg && exp_avg_sq), SRK_ERR_INVALID, "adam_scaled: null pointer");
+  SRK_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0 &&
+                  (uintptr_t)state % 8 == 0 && (uintptr_t)scaler % 4 == 0,
+              SRK_ERR_INVALID, "adam_scaled: buffers must be 16-byte aligned");
+  hipStream_t s = srk::as_stream(stream);
+  auto* sc = reinterpret_cast<srk::ScalerState*>(scaler);
+  const int nt = 256;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + nt * 4 - 1) / (nt * 4), 256 * 8));
+  if (n > 0) {
+    srk::ProfScope prof("grad_check", s, 4.0 * (double)n);
+    hipLaunchKernelGGL(srk::finite_check_kernel, dim3((unsigned)blocks), dim3(nt), 0, s, grad, n, sc);
+  }
+  hipLaunchKernelGGL(srk::adam_prep_kernel, dim3(1), dim3(1), 0, s, state, beta1, beta2, (const srk::ScalerState*)sc);
+  if (n > 0) {
+    srk::ProfScope prof("adam", s, 28.0 * (double)n);
+    hipLaunchKernelGGL(srk::adam_state_kernel, dim3((unsigned)blocks), dim3(nt), 0, s, param, grad, exp_avg,
+                       exp_avg_sq, n, beta1, beta2, eps, state, grad_scale, (const srk::ScalerState*)sc);
+  }
+  hipLaunchKernelGGL(srk::scaler_update_kernel, dim3(1), dim3(1), 0, s, sc);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END

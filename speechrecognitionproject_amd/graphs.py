@@ -18,9 +18,21 @@ already have its final size when the capture starts (the warm-up runs the step a
 the per-step kernel timers (srk_prof) stay off during capture and replay; bench.py times kernels in a
 separate eager pass of the same step.
 """
+import gc
+
 import torch
 
 from . import _lib
+
+
+def _detached(out):
+    """The step's output without its autograd graph: a replay only rewrites the tensor's memory, and a
+    live graph would keep this capture's AccumulateGrad nodes (and their stream) into the next one."""
+    if isinstance(out, torch.Tensor):
+        return out.detach()
+    if isinstance(out, (tuple, list)):
+        return type(out)(_detached(o) for o in out)
+    return out
 
 
 class GraphedStep:
@@ -43,13 +55,16 @@ class GraphedStep:
                     self.out = step()
             torch.cuda.current_stream().wait_stream(side)
         # drop the warm-up's output: its autograd graph would keep the side stream's AccumulateGrad
-        # nodes alive into the capture
+        # nodes alive into the capture (and collect any reference cycle still holding one)
         self.out = None
+        gc.collect()
         torch.cuda.synchronize()
         self.generation = _lib.scratch_generation()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, pool=pool):
-            self.out = step()
+            out = step()
+        self.out = _detached(out)
+        del out
         torch.cuda.synchronize()
         if _lib.scratch_generation() != self.generation:
             raise _lib.SrkError("GraphedStep: a library scratch buffer grew during the capture (warm up longer)")

@@ -453,6 +453,22 @@ class MaxPool1d(tnn.Module):
 
 _DROPOUT_STATE = {}   # device index -> int64[2] {base seed, call counter} read by srk_dropout_fwd_state
 _MASK63 = (1 << 63) - 1
+_DROPOUT_REPLAY = [0]
+
+
+class dropout_replay_mode:
+    """Within this block eager dropout calls draw their masks as a replayed HIP graph does: from the
+    device state the last seeded call left, the kernel's counter advancing per call, without
+    re-deriving the seed from torch's generator.  An eager step here is then the arithmetic of a
+    graph replay, mask included (tests/test_graphs_gpu.py compares the two bit for bit)."""
+
+    def __enter__(self):
+        _DROPOUT_REPLAY[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _DROPOUT_REPLAY[0] -= 1
+        return False
 
 
 def _dropout_state(device):
@@ -468,7 +484,7 @@ def _dropout_state(device):
     if st is None:
         st = torch.zeros(2, dtype=torch.int64, device=device)
         _DROPOUT_STATE[idx] = st
-    if not torch.cuda.is_current_stream_capturing():
+    if not torch.cuda.is_current_stream_capturing() and not _DROPOUT_REPLAY[0]:
         gen = torch.cuda.default_generators[idx]
         seed, off = gen.initial_seed(), gen.get_offset()
         gen.set_offset(off + 4)

@@ -65,10 +65,47 @@ class FlatParams:
                 p.grad = self.grad[o:o + p.numel()].view_as(p)
 
 
+class LossScaler:
+    """Loss scaling for fp16 training, torch.cuda.amp.GradScaler semantics with its state on the
+    device (srk_grad_scaler_init / srk_adam_step_scaled), so a captured HIP graph replays it:
+
+        loss = criterion(model(x), y)
+        scaler.scale(loss).backward()         # loss x scale (the scale is read on the device)
+        optimizer.step(scaler=scaler)         # non-finite gradients -> the step is skipped
+
+    ``dynamic=False`` keeps ``init_scale`` fixed (bench.py's static 1024); a skipped step is still
+    counted in ``overflows()``.  ``dynamic=True`` halves the scale on an overflow and doubles it
+    after ``growth_interval`` clean steps (GradScaler's defaults, except the initial scale)."""
+
+    def __init__(self, init_scale=1024.0, dynamic=True, growth_factor=2.0, backoff_factor=0.5,
+                 growth_interval=2000, device=None):
+        require_gpu()
+        device = device or torch.device("cuda", torch.cuda.current_device())
+        self.state = torch.zeros(8, dtype=torch.int32, device=device)
+        self.dynamic = bool(dynamic)
+        call("srk_grad_scaler_init", ptr(self.state), float(init_scale), float(growth_factor),
+             float(backoff_factor), int(growth_interval) if dynamic else 0, stream_ptr())
+
+    def scale(self, loss):
+        return loss * self.state.view(torch.float32)[0]
+
+    def get_scale(self):
+        """The current scale (synchronizes)."""
+        return float(self.state.view(torch.float32)[0].item())
+
+    def overflows(self):
+        """Steps skipped so far because a gradient was inf / NaN (synchronizes)."""
+        return int(self.state[7].item())
+
+
 class Adam(torch.optim.Optimizer):
     """torch.optim.Adam semantics (betas=(0.9, 0.999), eps=1e-8, no weight decay), one fused
     HIP launch per step over a FlatParams buffer.  ``grad_scale`` (e.g. 1/world_size after a
-    summed all-reduce) multiplies the gradient inside the kernel."""
+    summed all-reduce) multiplies the gradient inside the kernel; ``step(scaler=LossScaler)``
+    additionally unscales fp16 loss-scaled gradients and skips a step whose gradients overflowed.
+
+    The step count lives on the device (``state_dev[0]``: a replayed HIP graph advances it without
+    the host; a skipped step does not advance it); ``step_count`` reads it (synchronizes)."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, flat=None):
         params = list(params)
@@ -76,12 +113,15 @@ class Adam(torch.optim.Optimizer):
         self.flat = flat if flat is not None else FlatParams(params)
         self.exp_avg = torch.zeros_like(self.flat.data)
         self.exp_avg_sq = torch.zeros_like(self.flat.data)
-        self.step_count = 0      # host mirror of the device step count
         # {int64 step; float bc1, sqrt(bc2), lr, 0} on the device, so a captured HIP graph replays the
         # step count and follows lr changes (ExponentialLR) made between replays
         self.state_dev = torch.zeros(4, dtype=torch.int64, device=self.flat.data.device)
         self._lr_dev = None
         self.grad_scale = 1.0
+
+    @property
+    def step_count(self):
+        return int(self.state_dev[0].item())
 
     def zero_grad(self, set_to_none=False):
         self.flat.zero_grad()
@@ -96,15 +136,19 @@ class Adam(torch.optim.Optimizer):
             self._lr_dev = lr
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, scaler=None):
         loss = closure() if closure is not None else None
         g = self.param_groups[0]
-        self.step_count += 1
         b1, b2 = g["betas"]
         f = self.flat
         self.sync_lr()
-        call("srk_adam_step_state", ptr(f.data), ptr(f.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq), f.numel,
-             float(b1), float(b2), float(g["eps"]), ptr(self.state_dev), float(self.grad_scale), stream_ptr())
+        if scaler is not None:
+            call("srk_adam_step_scaled", ptr(f.data), ptr(f.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq), f.numel,
+                 float(b1), float(b2), float(g["eps"]), ptr(self.state_dev), float(self.grad_scale),
+                 ptr(scaler.state), stream_ptr())
+        else:
+            call("srk_adam_step_state", ptr(f.data), ptr(f.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq), f.numel,
+                 float(b1), float(b2), float(g["eps"]), ptr(self.state_dev), float(self.grad_scale), stream_ptr())
         # a persistent kernel that timed out produced invalid gradients: fail loudly (a host-pinned
         # word, no device sync; it sees every timeout of the work the GPU has reached so far)
         check_health(sync=False)

@@ -15,8 +15,13 @@ hard-coded paths (:21-24), ``--log-every`` batches loss lines to avoid a host sy
 decode + one on-device augmentation launch per batch, and torchrun environments train
 data-parallel (one process per GPU, RCCL all-reduce).  On one GPU, full-size batches after the
 first two run as replays of a HIP graph of the step (the batch is copied into the graph's static
-input first; a short last batch runs eagerly; ``--no-graph`` disables it) — same arithmetic, bit
-for bit (tests/test_graphs_gpu.py).
+input first; a short last batch runs eagerly; ``--no-graph`` disables it) — the same kernels in the
+same order, so for models without dropout the same arithmetic bit for bit
+(tests/test_graphs_gpu.py, tests/test_training_gpu.py); with dropout a replay draws its mask from
+the device counter on top of the last eager seed, so masks (not the arithmetic) differ from
+``--no-graph``.  ``--precision bf16|fp16`` runs the matrix cores on 16-bit operands (fp32
+accumulation, fp32 parameters); fp16 trains with a loss scale (``--loss-scale``: dynamic by
+default, or a fixed number) and skips any step whose gradients overflowed (optim.LossScaler).
 """
 import argparse
 import importlib
@@ -27,9 +32,10 @@ import torch
 from torch.utils.data import DataLoader
 
 from . import parallel
+from . import _lib
 from ._lib import check_health
 from .nn import CrossEntropyLoss
-from .optim import Adam, FlatParams
+from .optim import Adam, FlatParams, LossScaler
 
 PLUGINS = ("mfcc_bgru", "fbanks_cnn", "spec_bgru", "resnet_bgru", "mfrn_bgru", "cnn_bgru", "spec_cnn")
 
@@ -59,17 +65,34 @@ def parse(argv=None):
     p.add_argument('--loader', choices=('device', 'torch'), default='device',
                    help='WAV datasets: device = native batched decode + K10 on-device augmentation '
                         '(DeviceBatchLoader); torch = per-item Dataset.__getitem__ through DataLoader')
+    p.add_argument('--precision', choices=('fp32', 'bf16', 'fp16'), default='fp32',
+                   help='matrix-core operand precision (fp32 = the reference arithmetic; bf16 / fp16 operands with '
+                        'fp32 accumulation)')
+    p.add_argument('--loss-scale', default='dynamic',
+                   help="fp16: 'dynamic' (start at 1024, halve on overflow, double after 2000 clean steps) or a "
+                        "fixed scale; a step whose gradients are inf / NaN is skipped either way")
+    p.add_argument('--save-model', action='store_true',
+                   help="write model.state_dict() to OUTPUT/models/model_KEY.ckpt after training (the reference's "
+                        "checkpoint path, training.py:104-107)")
     return p.parse_args(argv)
 
 
 def main(argv=None):
     args = parse(argv)
+    try:
+        _train(args)
+    finally:
+        _lib.set_matmul_precision('fp32')     # process-wide: do not leak a 16-bit mode into the caller
+
+
+def _train(args):
     rank, world, local = parallel.init_from_env()
     key = args.filekey or ''
     lr = args.learning_rate if args.learning_rate is not None else 0.0001
     mod = importlib.import_module('speechrecognitionproject_amd.models.model_' + args.model)
     start = time.time()
     device = torch.device('cuda', local)
+    _lib.set_matmul_precision(args.precision)
 
     if args.synthetic:
         from .dataset import SyntheticDataset
@@ -97,6 +120,12 @@ def main(argv=None):
     reducer = parallel.GradReducer(flat) if (world > 1 and args.overlap) else None
     scheduler = torch.optim.lr_scheduler.ExponentialLR(optimizer, 0.87)
     criterion = CrossEntropyLoss()
+    scaler = None
+    if args.precision == 'fp16':
+        if args.loss_scale == 'dynamic':
+            scaler = LossScaler(1024.0, dynamic=True, device=device)
+        else:
+            scaler = LossScaler(float(args.loss_scale), dynamic=False, device=device)
     os.makedirs(args.output_path, exist_ok=True)
     loss_file = os.path.join(args.output_path, 'loss_' + key + '.txt')
 
@@ -112,12 +141,12 @@ def main(argv=None):
             reducer.begin()
         outputs = model(x)
         loss = criterion(outputs, y)
-        loss.backward()
+        (scaler.scale(loss) if scaler is not None else loss).backward()
         if reducer is not None:
             reducer.finish()
         else:
             parallel.allreduce_grads(flat)
-        optimizer.step()
+        optimizer.step(scaler=scaler)
         return loss
 
     def graph_body():
@@ -177,6 +206,9 @@ def main(argv=None):
                 else:
                     if graphed is None:
                         from .graphs import GraphedStep
+                        # the last warm-up loss still holds its step's autograd graph (and with it the
+                        # side stream's AccumulateGrad nodes): drop it before the capture
+                        loss = None
                         graphed = GraphedStep(graph_body, warmup=0)   # warmed up by the side-stream steps
                     static['x'].copy_(x, non_blocking=True)
                     static['y'].copy_(y, non_blocking=True)
@@ -196,6 +228,11 @@ def main(argv=None):
         epoch += 1
         if hasattr(data, 'resample_unknown_class'):
             data.resample_unknown_class()
+    if args.save_model and rank == 0:
+        os.makedirs(os.path.join(args.output_path, 'models'), exist_ok=True)
+        torch.save(model.state_dict(), os.path.join(args.output_path, 'models', 'model_' + key + '.ckpt'))
+    if scaler is not None and rank == 0:
+        print('fp16 steps skipped (inf/NaN gradients): %d, final loss scale %g' % (scaler.overflows(), scaler.get_scale()))
     if rank == 0:
         print('key  ', key)
         print('time  ', time.time() - start)

@@ -31,7 +31,11 @@ def test_gemm_f32(gpu, ta, tb, M, N, K):
 @pytest.mark.parametrize("ta,tb,M,N,K", [
     (0, 1, 256, 12, 1024), (0, 0, 256, 12, 1024), (0, 1, 5, 1, 3), (0, 0, 1000, 16, 4097),   # N <= 16, A k-contiguous
     (1, 0, 12, 1024, 256), (0, 0, 16, 777, 300), (1, 0, 1, 5, 1),                            # M <= 16, B row-contiguous
-    (0, 0, 256, 1024, 12), (1, 0, 300, 515, 16), (0, 0, 70, 9, 1)])                          # K <= 16
+    (0, 0, 256, 1024, 12), (1, 0, 300, 515, 16), (0, 0, 70, 9, 1),                           # K <= 16
+    # every model's 12-class classifier at the configs' batches (forward, dW + db, dx):
+    # fbanks_cnn fc2 (in 256) and the BiGRU heads (in 1024) at B = 512
+    (0, 1, 512, 12, 256), (1, 0, 12, 256, 512), (0, 0, 512, 256, 12),
+    (0, 1, 512, 12, 1024), (1, 0, 12, 1024, 512), (0, 0, 512, 1024, 12)])
 def test_gemm_skinny(gpu, precision, ta, tb, M, N, K):
     """GEMMs with a dimension <= 16 (the output layers' fc GEMMs) on the VALU skinny kernels (option
     gemm_skinny): == float64 product of the (rounded, in bf16 / fp16 mode) operands with alpha, beta,

@@ -484,3 +484,38 @@ def test_gemm_16bit_rejects_misaligned(prec):
     C = torch.zeros(16, 16, device="cuda")
     with pytest.raises(_lib.SrkError):
         call("srk_gemm_16", 0, 1, 16, 16, 12, 1.0, ptr(A), 12, ptr(A), 12, 0.0, ptr(C), 16, None, 0, stream_ptr())
+
+
+@pytest.mark.parametrize("precision,H,opts", [("bf16", 128, {}), ("fp16", 128, {}), ("bf16", 512, {"gru_persistent": 0}),
+                                              ("fp32", 128, {"gemm32_kernel": 1})])
+def test_bigru_backward_when_batched_dwhh_is_unavailable(gpu, precision, H, opts):
+    """the batched dW_hh launch (both directions in one GEMM with fused row sums) exists
+    only on the fp32-operand ping-pong kernel.  The fp32-operand GRU backward that 16-bit mode takes
+    without the persistent kernels (H != 512, gru_persistent=0), and fp32 with the register-staged
+    kernel forced, must fall back to per-direction launches: same gradients as gru_dwhh_batched=0."""
+    from speechrecognitionproject_amd import nn as snn
+    B, T, IN, L = 24, 7, 39, 2
+    torch.manual_seed(5)
+    ref = torch.nn.GRU(IN, H, num_layers=L, bidirectional=True, batch_first=True)
+    x = torch.randn(B, T, IN, device="cuda")
+    w = torch.randn(B, T, 2 * H, device="cuda")
+    grads = []
+    try:
+        _lib.set_matmul_precision(precision)
+        for k, v in opts.items():
+            _lib.set_option(k, v)
+        for batched in (1, 0):
+            _lib.set_option("gru_dwhh_batched", batched)
+            mine = snn.BiGRU(IN, H, num_layers=L).cuda()
+            mine.load_state_dict(ref.state_dict())
+            (mine(x)[0] * w).sum().backward()
+            torch.cuda.synchronize()
+            grads.append({n: p.grad.detach().clone() for n, p in mine.named_parameters()})
+    finally:
+        _lib.set_option("gru_dwhh_batched", 1)
+        _lib.set_option("gru_persistent", 1)
+        _lib.set_option("gemm32_kernel", 0)
+        _lib.set_matmul_precision("fp32")
+    for n in grads[0]:
+        assert torch.isfinite(grads[0][n]).all(), n
+        assert torch.equal(grads[0][n], grads[1][n]), n

@@ -96,3 +96,35 @@ def test_spin_timeout_is_fatal(gpu, tmp_path):
     # and in this (healthy) process the check passes
     from speechrecognitionproject_amd import _lib
     _lib.check_health(sync=True)
+
+
+def test_training_graph_equals_eager(gpu, tmp_path):
+    """training.py's graph path (two eager warm-up batches on a side stream, then a
+    capture and replays) against --no-graph on a dropout-free model, 4 full batches x 2 epochs: the
+    loss files and the final parameters must be identical."""
+    import torch
+    from speechrecognitionproject_amd.training import main
+    res = {}
+    for tag, extra in (("g", []), ("e", ["--no-graph"])):
+        out = tmp_path / tag
+        main(["-key", tag, "-lr", "0.0001", "--model", "mfcc_bgru", "--synthetic", "64", "--batch-size", "16",
+              "--epochs", "2", "--output-path", str(out), "--log-every", "4", "--no-eval", "--save-model"] + extra)
+        res[tag] = (open(out / ("loss_%s.txt" % tag)).read(),
+                    torch.load(out / "models" / ("model_%s.ckpt" % tag), weights_only=True))
+    assert len(res["g"][0].splitlines()) == 8
+    assert res["g"][0] == res["e"][0]
+    for k, v in res["g"][1].items():
+        assert torch.equal(v, res["e"][1][k]), k
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_training_precision_flag(gpu, tmp_path, precision):
+    """--precision (SURVEY.md §5 "Config / flags"): the 16-bit modes through the reference CLI; fp16
+    trains with the dynamic loss scale and reports skipped steps."""
+    from speechrecognitionproject_amd import _lib
+    from speechrecognitionproject_amd.training import main
+    main(["-key", "p", "-lr", "0.0001", "--model", "spec_bgru", "--synthetic", "48", "--batch-size", "16",
+          "--output-path", str(tmp_path), "--log-every", "3", "--precision", precision])
+    losses = [float(l) for l in open(tmp_path / "loss_p.txt")]
+    assert len(losses) == 3 and all(np.isfinite(losses))
+    assert _lib.matmul_precision() == "fp32"          # restored after the run

@@ -20,6 +20,11 @@
   reference-vs-restatement spread (logits_ok) — the HIP spectrogram is a third float32 rounding of
   the same float64 quantity, so its distance to the restatement is of the reference's order, not
   bounded by it — and the model half alone (the oracle model fed the HIP features) to 1e-4.
+* 16-bit train steps at the config shapes (tests/test_trainstep_lowprec_gpu.py): every gradient
+  tensor ||g - g_oracle||_2 / ||g_oracle||_2 <= 2e-2 (LP_GRAD_REL, after unscaling the fp16 loss
+  scale); the fused Adam update vs torch's Adam formula on the same gradient <= 2e-7 absolute
+  (LP_ADAM_ABS; lr = 1e-4); the update's disagreement with the fp32 oracle's own Adam step, weighted
+  by |g_oracle|, <= 2e-2 (LP_UPDATE_WEIGHTED).
 * bf16 / fp16 GRU forward vs a float64 emulation of the same operand rounding: <= 2e-3 absolute on
   y (h in [-1, 1]; a rounding flip of one operand moves a gate pre-activation by ~1e-4).
 """
@@ -36,6 +41,9 @@ SPEC_LIN_REL = 1e-7
 LOGITS_REL = 1e-4
 LOGITS_REL_LOWPREC = 2e-2
 GRU_LOWPREC_EMU_ABS = 2e-3
+LP_GRAD_REL = 2e-2
+LP_ADAM_ABS = 2e-7
+LP_UPDATE_WEIGHTED = 2e-2
 
 
 def fbank_ok(out, ref):

@@ -228,6 +228,20 @@ int srk_conv2d_nhwc_fwd16(const float* x, int64_t N, int64_t H, int64_t W, int64
 int srk_conv2d_nhwc_bwd16(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co,
                           int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw, const float* dy,
                           float* dx, float* dw, float* db, float* ws, const void* x16, void* stream);
+/* Conv2d (stride 1) + bias + MaxPool2d((1, 4)) fused (model_fbanks_cnn.py:74-75,91-92: conv2 then
+ * maxpool2): the implicit GEMM's epilogue pools its own output, so only the pooled activation y
+ * [N][Ho][Wo/4][Co] and the uint8 window argmax [N][Ho][Wo/4][Co] (first maximum, NaN wins: the
+ * maxpool rule) are written.  Needs pool_w = 4 dividing Wo.  x16 / x16_written as fwd16.  The
+ * backward takes the POOLED gradient and the argmax (the dense gradient exists only in library
+ * scratch) and gives what srk_conv2d_nhwc_bwd16 gives for the unpooled gradient.               */
+int srk_conv2d_nhwc_fwd_pool(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w,
+                             const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw,
+                             int64_t pool_w, float* y, uint8_t* argmax, float* ws, void* x16, int* x16_written,
+                             void* stream);
+int srk_conv2d_nhwc_bwd_pool(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co,
+                             int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t pool_w, const float* dy_pooled,
+                             const uint8_t* argmax, float* dx, float* dw, float* db, float* ws, const void* x16,
+                             void* stream);
 /* Max pooling, window = stride = (kh, kw), floor mode, channels-last (nn.MaxPool2d((1,3)),
  * ((1,4)) and nn.MaxPool1d(98), model_fbanks_cnn.py:73,75,78).  Backward routes each gradient to
  * the first maximum of its window, as PyTorch does.                                          */

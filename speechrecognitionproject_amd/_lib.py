@@ -61,6 +61,10 @@ _SIGS = {
                               _P, ctypes.POINTER(_I), _P],
     "srk_conv2d_nhwc_bwd16": [_P, _I64, _I64, _I64, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P,
                               _P, _P, _P, _P],
+    "srk_conv2d_nhwc_fwd_pool": [_P, _I64, _I64, _I64, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P,
+                                 _P, ctypes.POINTER(_I), _P],
+    "srk_conv2d_nhwc_bwd_pool": [_P, _I64, _I64, _I64, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P,
+                                 _P, _P, _P, _P],
     "srk_conv1_pool_workspace_floats": [_I64, _I64, _I64],
     "srk_conv1_pool_fwd": [_P, _I64, _I64, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P],
     "srk_conv1_pool_wgrad": [_P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P],
@@ -196,6 +200,18 @@ class precision_scope:
         if _precision != self.prev:
             set_matmul_precision(self.prev)
         return False
+
+
+_fused_conv_pool = [True]
+
+
+def set_fused_conv_pool(on):
+    """conv + (1, 4) max-pool in one launch (nn.conv_pool) or the separate kernels (A/B, tests)."""
+    _fused_conv_pool[0] = bool(on)
+
+
+def fused_conv_pool():
+    return _fused_conv_pool[0]
 
 
 def spin_timeouts():

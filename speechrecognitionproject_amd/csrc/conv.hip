@@ -54,6 +54,14 @@ struct ConvArgs {
   const unsigned short* b16;
   // divisors of the gathers (host-set): pixel grid (cols, rows), channels, KW, strides (dgrad)
   FastDiv fd_w, fd_h, fd_c, fd_kw, fd_sh, fd_sw;
+  // fwd: max-pool the output over windows of pool_w consecutive output columns in the epilogue
+  // (0 = off): out becomes [M / pool_w][Co], pool_arg the uint8 window argmax
+  int pool_w;
+  uint8_t* pool_arg;
+  // wgrad: column sums of B = dY over this split's pixels (the conv bias gradient), written by the
+  // tiles of the first m row as [split][Co] (null = off)
+  float* colsum_part;
+  float* db;           // host side only: where run_conv_gemm<kWgrad> reduces colsum_part to
 };
 
 // Implicit-GEMM operand gathers.  Each returns the ELEMENT OFFSET of the value (clamped to 0 when
@@ -312,6 +320,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // wgrad bias gradient: every staged B unit of a thread sits at the same 4 columns
+  // n0 + (tid % (BN / 4)) * 4 (NT is a multiple of BN / 4); one m row of tiles sums them
+  const bool csum_on = MODE == kWgrad && !S16 && c.colsum_part != nullptr && tm == 0;
+  v4f csum = {0.f, 0.f, 0.f, 0.f};
 
   auto store_tile = [&](int buf) {
     if constexpr (S16) {
@@ -341,6 +353,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
 #pragma unroll
       for (int i = 0; i < VB; ++i) {
         const v4f v = (bmask >> i) & 1u ? rb[i] : v4f{0.f, 0.f, 0.f, 0.f};
+        if (csum_on) csum += v;   // the unrounded fp32 values, as the GEMMs' fused row sums
         *reinterpret_cast<u32x2_*>(Bs + JB::store_off(tid + i * NT)) =
             __builtin_bit_cast(u32x2_, __builtin_convertvector(v, E4));
       }
@@ -358,6 +371,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
 #pragma unroll
     for (int i = 0; i < VB; ++i) {
       const v4f v = (bmask >> i) & 1u ? rb[i] : v4f{0.f, 0.f, 0.f, 0.f};
+      if (csum_on) csum += v;
       st4(Bs + IB::store_off(tid + i * NT), v);
     }
   };
@@ -408,7 +422,51 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
     __syncthreads();
   }
 
+  if (csum_on) {
+    // the 256 / (BN / 4) threads of each column quad, added through LDS in thread order (fixed)
+    constexpr int Q = BN / 4, G = NT / Q;
+    float* red = smem;   // the k loop ended with a barrier: the stage buffers are free
+    *reinterpret_cast<v4f*>(red + 4 * tid) = csum;
+    __syncthreads();
+    if (tid < Q) {
+      v4f t = *reinterpret_cast<const v4f*>(red + 4 * tid);
+#pragma unroll
+      for (int g = 1; g < G; ++g) t += *reinterpret_cast<const v4f*>(red + 4 * (tid + g * Q));
+      const int64_t n = n0 + 4 * tid;
+      if (n < c.Nn) *reinterpret_cast<v4f*>(c.colsum_part + split * c.Nn + n) = t;
+    }
+  }
+
   const int lh = lane >> 5, lc = lane & 31;
+  if (MODE == kFwd && c.pool_w == 4) {
+    // pooled epilogue (no split-K): the 4 rows (r & 3) = 0..3 of an accumulator group are 4
+    // consecutive output columns of one output row (rows m0 + wm0 + 32 i + 8 (r >> 2) + 4 lh are
+    // multiples of 4 and Wo % 4 == 0) — the window max and its first-maximum argmax in registers
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t col = n0 + wn0 + j * 32 + lc;
+        if (col >= c.Nn) continue;
+        const float bv = c.bias ? c.bias[col] : 0.f;
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {
+          const int64_t row = m0 + wm0 + i * 32 + 8 * rq + 4 * lh;
+          if (row >= c.M) continue;
+          float best = acc[i][j][4 * rq] + bv;
+          int arg = 0;
+#pragma unroll
+          for (int p = 1; p < 4; ++p) {
+            const float v = acc[i][j][4 * rq + p] + bv;
+            if (v > best || (v != v && best == best)) { best = v; arg = p; }
+          }
+          c.out[(row >> 2) * c.Nn + col] = best;
+          c.pool_arg[(row >> 2) * c.Nn + col] = (uint8_t)arg;
+        }
+      }
+    }
+    return;
+  }
   // epilogue.  32x32 accumulator: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -529,6 +587,52 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __r
     }
 }
 
+// db[n] = sum over splits (in order) of the wgrad kernel's column-sum partials
+__global__ void colsum_splits_kernel(const float* __restrict__ part, int splits, int64_t n, float* __restrict__ db) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += part[(int64_t)k * n + i];
+  db[i] = s;
+}
+
+// window (1, kw) max + first-maximum argmax of a dense NHWC activation (the pooled conv's split-K
+// path; the argmax matches the fused epilogue's and maxpool_bwd_kernel's rule)
+__global__ void maxpool_arg_kernel(const float* __restrict__ x, int64_t rows_out, int C, int kw, float* __restrict__ y,
+                                   uint8_t* __restrict__ arg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows_out * C) return;
+  const int64_t r = i / C;
+  const int c = (int)(i - r * C);
+  float m = 0.f;
+  int a = 0;
+  for (int b = 0; b < kw; ++b) {
+    const float v = x[(r * kw + b) * C + c];
+    if (takes(v, m, b == 0)) { m = v; a = b; }
+  }
+  y[i] = m;
+  arg[i] = (uint8_t)a;
+}
+
+// dense gradient of a (1, kw) max-pool from the pooled gradient and the window argmax:
+// dx[(r, b), c] = arg[r, c] == b ? dy[r, c] : 0 (4 channels per thread)
+__global__ void unpool_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ arg, int64_t rows_out, int C,
+                              int kw, float* __restrict__ dx) {
+  const int C4 = C / 4;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows_out * C4) return;
+  const int64_t r = i / C4;
+  const int c = (int)(i - r * C4) * 4;
+  const v4f g = ld4(dy + r * C + c);
+  const unsigned a = *reinterpret_cast<const unsigned*>(arg + r * C + c);
+  for (int b = 0; b < kw; ++b) {
+    v4f o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = ((a >> (8 * e)) & 0xFFu) == (unsigned)b ? g[e] : 0.f;
+    st4(dx + (r * kw + b) * C + c, o);
+  }
+}
+
 __global__ void zero_kernel(float* __restrict__ p, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = 0.f;
@@ -552,6 +656,8 @@ struct ConvScratch {
 };
 ConvScratch g_cs[64];     // split-K slabs
 ConvScratch g_cs16[64];   // 16-bit operand sources
+ConvScratch g_csb[64];    // wgrad bias column-sum partials
+ConvScratch g_csd[64];    // dense activation / gradient of the pooled conv (split-K forward, backward dY)
 std::mutex g_cs_mu;
 
 int conv_scratch(size_t floats, float** out, ConvScratch* pool = g_cs) {
@@ -655,8 +761,20 @@ int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
   c.group_m = 8;
   c.partial = nullptr;
   float* final_out = c.out;
+  float* pooled_out = nullptr;
+  int pool_w = 0;
   if (splits > 1) {
     if (int rc = conv_scratch((size_t)splits * c.M * c.Nn, &c.partial)) return rc;
+    if (MODE == kFwd && c.pool_w) {   // no pooled epilogue across split-K slabs: dense, then pool
+      pooled_out = c.out;
+      if (int rc = conv_scratch((size_t)c.M * c.Nn, &final_out, g_csd)) return rc;
+      pool_w = c.pool_w;
+      c.pool_w = 0;
+    }
+  }
+  c.colsum_part = nullptr;
+  if (MODE == kWgrad && c.db && !c.a16) {
+    if (int rc = conv_scratch((size_t)splits * c.Nn, &c.colsum_part, g_csb)) return rc;
   }
   const int chans = MODE == kDgrad ? c.Co : c.Ci;
   SRK_REQUIRE(c.M < INT32_MAX && c.K < INT32_MAX, SRK_ERR_INVALID, "conv: implicit-GEMM extent >= 2^31");
@@ -683,6 +801,17 @@ int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
     const int64_t n = c.M * c.Nn;
     hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c.partial, splits, n,
                        c.Nn, MODE == kFwd ? c.bias : nullptr, final_out);
+    SRK_CHECK_HIP(hipGetLastError());
+    if (pooled_out) {
+      const int64_t rows = c.M / pool_w;
+      hipLaunchKernelGGL(maxpool_arg_kernel, dim3((unsigned)((rows * c.Nn + 255) / 256)), dim3(256), 0, s, final_out,
+                         rows, (int)c.Nn, pool_w, pooled_out, c.pool_arg);
+      SRK_CHECK_HIP(hipGetLastError());
+    }
+  }
+  if (c.colsum_part) {
+    hipLaunchKernelGGL(colsum_splits_kernel, dim3((unsigned)((c.Nn + 255) / 256)), dim3(256), 0, s, c.colsum_part,
+                       splits, c.Nn, c.db);
     SRK_CHECK_HIP(hipGetLastError());
   }
   return SRK_OK;
@@ -813,13 +942,74 @@ int srk_conv2d_nhwc_bwd16(const float* x, int64_t N, int64_t H, int64_t W, int64
       g.a16 = d16[0];
       g.b16 = d16[1];
     }
+    // the bias gradient = column sums of dY, fused into the weight-gradient kernel (fp32-source
+    // paths: the sums of the unrounded values); the 16-bit-source path keeps the column-sum kernel
+    g.db = srk::g_opt_conv_fused_db ? db : nullptr;
     if ((rc = srk::run_conv_gemm<srk::kWgrad>(g, s, "conv_wgrad"))) return rc;
     hipLaunchKernelGGL(srk::weight_grad_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, ws,
                        (int)Co, (int)Ci, (int)KH, (int)KW, dw);
+    if (db && (!g.db || g.a16) && (rc = srk::colsum_f32(dy, N * Ho * Wo, Co, Co, db, 0.f, s))) return rc;
   }
-  if (db && (rc = srk::colsum_f32(dy, N * Ho * Wo, Co, Co, db, 0.f, s))) return rc;
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
+  SRK_API_END
+}
+
+int srk_conv2d_nhwc_fwd_pool(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w,
+                             const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw,
+                             int64_t pool_w, float* y, uint8_t* argmax, float* ws, void* x16, int* x16_written,
+                             void* stream) {
+  SRK_API_BEGIN
+  if (x16_written) *x16_written = 0;
+  int64_t Ho, Wo;
+  if (int rc = srk::check(N, H, W, Ci, Co, KH, KW, ph, pw, 1, 1, &Ho, &Wo)) return rc;
+  SRK_REQUIRE(x && w && y && argmax && ws, SRK_ERR_INVALID, "conv fwd_pool: null pointer");
+  SRK_REQUIRE(pool_w == 4 && Wo % pool_w == 0, SRK_ERR_INVALID,
+              "conv fwd_pool: the fused pooling needs a (1, 4) window that divides the output width");
+  hipStream_t s = srk::as_stream(stream);
+  const int64_t nw = Co * Ci * KH * KW;
+  hipLaunchKernelGGL(srk::weight_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, (int)Co,
+                     (int)Ci, (int)KH, (int)KW, 0, ws);
+  srk::ConvArgs c{};
+  c.N = (int)N; c.H = (int)H; c.W = (int)W; c.Ci = (int)Ci; c.Ho = (int)Ho; c.Wo = (int)Wo; c.Co = (int)Co;
+  c.KH = (int)KH; c.KW = (int)KW; c.ph = (int)ph; c.pw = (int)pw; c.sh = 1; c.sw = 1;
+  c.x = x; c.wmat = ws; c.out = y; c.bias = bias;
+  c.M = N * Ho * Wo; c.Nn = Co; c.K = KH * KW * Ci;
+  c.pool_w = (int)pool_w;
+  c.pool_arg = argmax;
+  const int prec = srk::matmul_prec();
+  if (srk::s16_ok(prec, Ci, Co, {x, ws, x16})) {
+    const float* src[2] = {x, ws};
+    const int64_t n[2] = {N * H * W * Ci, nw};
+    unsigned short* d16[2] = {static_cast<unsigned short*>(x16), nullptr};
+    if (int rc = srk::to16_all(prec, src, n, 2, d16, s)) return rc;
+    c.a16 = d16[0];
+    c.b16 = d16[1];
+    if (x16 && x16_written) *x16_written = 1;
+  }
+  return srk::run_conv_gemm<srk::kFwd>(c, s, "conv_fwd");
+  SRK_API_END
+}
+
+int srk_conv2d_nhwc_bwd_pool(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co,
+                             int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t pool_w, const float* dy_pooled,
+                             const uint8_t* argmax, float* dx, float* dw, float* db, float* ws, const void* x16,
+                             void* stream) {
+  SRK_API_BEGIN
+  int64_t Ho, Wo;
+  if (int rc = srk::check(N, H, W, Ci, Co, KH, KW, ph, pw, 1, 1, &Ho, &Wo)) return rc;
+  SRK_REQUIRE(dy_pooled && argmax, SRK_ERR_INVALID, "conv bwd_pool: null pointer");
+  SRK_REQUIRE(pool_w == 4 && Wo % pool_w == 0 && Co % 4 == 0 && (uintptr_t)dy_pooled % 16 == 0 &&
+                  (uintptr_t)argmax % 4 == 0,
+              SRK_ERR_INVALID, "conv bwd_pool: (1, 4) window dividing the output width, Co % 4, aligned buffers");
+  hipStream_t s = srk::as_stream(stream);
+  float* dy = nullptr;
+  if (int rc = srk::conv_scratch((size_t)(N * Ho * Wo * Co), &dy, srk::g_csd)) return rc;
+  const int64_t rows = N * Ho * Wo / pool_w;
+  hipLaunchKernelGGL(srk::unpool_kernel, dim3((unsigned)((rows * (Co / 4) + 255) / 256)), dim3(256), 0, s, dy_pooled,
+                     argmax, rows, (int)Co, (int)pool_w, dy);
+  SRK_CHECK_HIP(hipGetLastError());
+  return srk_conv2d_nhwc_bwd16(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, 1, 1, dy, dx, dw, db, ws, x16, stream);
   SRK_API_END
 }
 
@@ -866,7 +1056,7 @@ namespace srk {
 int release_conv_scratch() {
   std::lock_guard<std::mutex> lk(g_cs_mu);
   SRK_CHECK_HIP(hipDeviceSynchronize());
-  for (ConvScratch* pool : {g_cs, g_cs16})
+  for (ConvScratch* pool : {g_cs, g_cs16, g_csb, g_csd})
     for (int d = 0; d < 64; ++d) {
       if (pool[d].p) SRK_CHECK_HIP(hipFree(pool[d].p));
       pool[d].p = nullptr;

@@ -1601,7 +1601,13 @@ int plan_launch(const GemmDesc& d, int BM, int BN, int BK, int per_cu, KernelArg
   ka.tiles_m = (int)tm;
   ka.tiles_n = (int)tn;
   ka.tiles = (int)(tm * tn);
-  ka.group_m = 8;
+  // tile rows per swizzle group: an XCD runs ~32 x per_cu tiles at once out of a contiguous run of
+  // the grouped order (XCD remap), i.e. g rows x (32 per_cu / g) columns of tiles, whose distinct
+  // operand panels (g BM + 32 per_cu BN / g rows of K) its 4 MB L2 must hold; g = sqrt(32 per_cu
+  // BN / BM) minimises them (256 x 128 tiles: 4, was 8 — 8 A panels of 1 MB re-read per round)
+  static const int group_env = env_int("SRK_GROUP_M", 0);   // A/B measurements
+  ka.group_m = group_env > 0 ? group_env
+                             : std::max(1, (int)std::lround(std::sqrt(32.0 * per_cu * BN / (double)BM)));
   ka.remap = remap;
   // Split K when the output grid leaves resident slots idle and K is long (tile::choose_splits).
   const bool can_split = allow_split && (d.batch == 1 || split_batched);

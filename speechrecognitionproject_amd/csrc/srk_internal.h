@@ -98,6 +98,9 @@ extern int g_opt_gemm_skinny;   // GEMMs with a dimension <= 16 on the VALU skin
 // 16-bit conv operand sources (srk_set_option "conv16_sources", default 1): bf16 / fp16 convolutions
 // gather from one pre-rounded 16-bit copy of x / dY / the weights (0 = round at LDS-store time).
 extern int g_opt_conv16_sources;
+// conv bias gradients as column sums fused into the weight-gradient kernel ("conv_fused_db", default
+// 1; 0 = the separate column-sum kernel over dY)
+extern int g_opt_conv_fused_db;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

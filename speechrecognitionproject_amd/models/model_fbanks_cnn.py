@@ -5,13 +5,13 @@
 Same constructor, ``state_dict`` keys/shapes and helpers.  The per-clip CPU ``filter_banks`` loop
 (:84-87) becomes one batched HIP launch (K2); conv1 + maxpool1 run as one fused one-channel kernel
 (srk_conv1_pool_*: the pre-pool activation is never written), conv2-4 as channels-last implicit GEMMs
-on the matrix cores (K6).
+on the matrix cores (K6), conv2's maxpool in its GEMM epilogue (srk_conv2d_nhwc_fwd_pool).
 """
 import torch
 import torch.nn as nn
 
 from .. import features
-from ..nn import Conv2d, Dropout, Linear, MaxPool1d, MaxPool2d, conv1_pool
+from ..nn import Conv2d, Dropout, Linear, MaxPool1d, MaxPool2d, conv1_pool, conv_pool
 from ._common import DEVICE, accuracy, class_accuracy   # noqa: F401
 
 
@@ -38,7 +38,7 @@ class Network(nn.Module):
         with torch.no_grad():
             inx = features.fbank(x)                       # [B, 98, 120]
         h = conv1_pool(inx, self.conv1, self.maxpool1)   # fused conv1 + maxpool1: NHWC [B, 98, 40, 64]
-        h = self.maxpool2(self.conv2(h))                  # [B, 98, 10, 128]
+        h = conv_pool(h, self.conv2, self.maxpool2)      # fused conv2 + maxpool2: [B, 98, 10, 128]
         h = self.conv4(self.conv3(h))                     # [B, 98, 1, 512]
         h = self.maxpool3(h.squeeze(2)).squeeze(1)        # [B, 512]
         h = self.dropout(h)

@@ -405,6 +405,70 @@ def conv1_pool(x, conv, pool):
     return pool(conv(x.unsqueeze(-1)))
 
 
+class _ConvPoolNHWCFn(torch.autograd.Function):
+    """Conv2d (stride 1) + bias + MaxPool2d((1, 4)) with the pooling in the conv's epilogue
+    (srk_conv2d_nhwc_fwd_pool / _bwd_pool): conv2 + maxpool2 of model_fbanks_cnn.py:74-75,91-92.
+    Only the pooled activation and a uint8 argmax are kept; the backward routes the pooled gradient
+    through the argmax inside the library."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, padding, pool_w):
+        x = x.contiguous()
+        w = w.contiguous()
+        _check_cuda(x, w, b)
+        N, H, W, Ci = x.shape
+        Co, _, KH, KW = w.shape
+        ph, pw = padding
+        Ho, Wo = H + 2 * ph - KH + 1, W + 2 * pw - KW + 1
+        y = torch.empty((N, Ho, Wo // pool_w, Co), device=x.device)
+        arg = torch.empty((N, Ho, Wo // pool_w, Co), device=x.device, dtype=torch.uint8)
+        ws = torch.empty(int(_lib.lib().srk_conv2d_workspace_floats(Ci, Co, KH, KW)), device=x.device)
+        x16, written = None, ctypes.c_int(0)
+        if _lib.matmul_precision() != "fp32" and Ci % 8 == 0 and Co % 8 == 0 and ctx.needs_input_grad[1]:
+            x16 = torch.empty(x.numel(), device=x.device, dtype=torch.int16)
+        call("srk_conv2d_nhwc_fwd_pool", ptr(x), N, H, W, Ci, ptr(w), ptr(b) if b is not None else None, Co, KH, KW,
+             ph, pw, pool_w, ptr(y), ptr(arg), ptr(ws), ptr(x16) if x16 is not None else None, ctypes.byref(written),
+             stream_ptr())
+        ctx.x16 = x16 if written.value else None
+        ctx.prec = _lib.matmul_precision()
+        ctx.save_for_backward(x, w, arg)
+        ctx.geom = (padding, pool_w, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, arg = ctx.saved_tensors
+        (ph, pw), pool_w, has_b = ctx.geom
+        N, H, W, Ci = x.shape
+        Co, _, KH, KW = w.shape
+        dy = dy.contiguous()
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty_like(w)
+        db = torch.empty((Co,), device=x.device) if has_b else None
+        ws = torch.empty(int(_lib.lib().srk_conv2d_workspace_floats(Ci, Co, KH, KW)), device=x.device)
+        x16 = ctx.x16 if ctx.prec == _lib.matmul_precision() else None
+        ctx.x16 = None
+        call("srk_conv2d_nhwc_bwd_pool", ptr(x), N, H, W, Ci, ptr(w), Co, KH, KW, ph, pw, pool_w, ptr(dy), ptr(arg),
+             ptr(dx) if dx is not None else None, ptr(dw), ptr(db) if db is not None else None, ptr(ws),
+             ptr(x16) if x16 is not None else None, stream_ptr())
+        return dx, dw, db, None, None
+
+
+def conv_pool(x, conv, pool):
+    """``pool(conv(x))`` for channels-last x: one fused launch (srk_conv2d_nhwc_fwd_pool) when the
+    conv has stride 1 and the pool is (1, 4) with a window count that divides the output width
+    (conv2 + maxpool2 of model_fbanks_cnn); otherwise the separate conv and pool kernels."""
+    kh, kw = pool.kernel_size
+    KH, KW = conv.kernel_size
+    ph, pw = conv.padding
+    Wo = x.shape[2] + 2 * pw - KW + 1
+    if (tuple(conv.stride) == (1, 1) and (kh, kw) == (1, 4) and Wo % 4 == 0 and conv.out_channels % 4 == 0
+            and _lib.fused_conv_pool()):
+        require_gpu()
+        return _ConvPoolNHWCFn.apply(x, conv.weight, conv.bias, conv.padding, 4)
+    return pool(conv(x))
+
+
 class _MaxPoolNHWCFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kh, kw):

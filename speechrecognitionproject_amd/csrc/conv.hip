@@ -62,6 +62,10 @@ struct ConvArgs {
   // tiles of the first m row as [split][Co] (null = off)
   float* colsum_part;
   float* db;           // host side only: where run_conv_gemm<kWgrad> reduces colsum_part to
+  // dgrad / wgrad of a (1, 4)-pooled conv (UNPOOL kernels): dy holds the POOLED gradient
+  // [N*Ho*Wo/4][Co] and dy_arg its window argmax; the gathers rebuild the dense gradient
+  // dY[pixel][co] = dy_arg[pixel/4][co] == pixel % 4 ? dy[pixel/4][co] : 0 at LDS-store time
+  const uint8_t* dy_arg;
 };
 
 // Implicit-GEMM operand gathers.  Each returns the ELEMENT OFFSET of the value (clamped to 0 when
@@ -169,7 +173,8 @@ struct Img16 {
 // S16: 16-bit sources (ConvArgs::a16 / b16, rounded by the same conversion as the LDS-store path,
 // so the MFMA operands are bit-identical): a staged unit is 8 elements = one 16-B load and one
 // 16-B LDS store (needs VEC and VECB with 8-aligned channel counts / N).
-template <int MODE, int BM, int BN, int BK, bool VEC, bool VECB, int LP = 0, bool S16 = false>
+// UNPOOL: dY is the (1, 4)-pooled gradient + argmax (ConvArgs::dy_arg; dgrad / wgrad, fp32 sources)
+template <int MODE, int BM, int BN, int BK, bool VEC, bool VECB, int LP = 0, bool S16 = false, bool UNPOOL = false>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   constexpr int NT = 256;
   constexpr bool AKC = MODE != kWgrad;   // A k-contiguous (channels along k) for fwd / dgrad
@@ -178,6 +183,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   using JA = Img16<AKC, BM, BK>;
   using JB = Img16<false, BN, BK>;
   static_assert(!S16 || (LP != 0 && VEC && VECB), "16-bit sources need the vector gathers");
+  static_assert(!UNPOOL || (MODE != kFwd && !S16 && VEC && VECB), "unpooling gathers: dgrad / wgrad, fp32 sources");
   constexpr int EU = S16 ? 8 : 4;        // elements per staged unit
   constexpr int VA = BM * BK / EU / NT, VB = BN * BK / EU / NT;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -212,6 +218,9 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   }
 
   v4f ra[VA], rb[VB];   // fp32 staged units (unused, and eliminated, when S16)
+  // UNPOOL: the argmax bytes of each staged dY unit and its pixel's window position (2 bits per unit)
+  unsigned parg[UNPOOL ? (MODE == kDgrad ? VA : VB) : 1];
+  unsigned psub = 0;
   u32x4_ ha[S16 ? VA : 1], hb[S16 ? VB : 1];   // S16 staged units (8 x 16 bit)
   unsigned amask = 0, bmask = 0;   // bit = element valid (4 per staged float4; S16: 1 per unit)
   auto load_tile = [&](int64_t k0) {
@@ -255,11 +264,24 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
       const int64_t k = k0 + aq;
       if (VEC) {
         const Tap t = split_tap(k < ke ? k : 0, c.fd_c, c.fd_kw);
+        if constexpr (UNPOOL) psub = 0;
 #pragma unroll
         for (int i = 0; i < VA; ++i) {
           bool ok = k < ke;
           const int64_t off = a_offset<MODE>(c, prow[i], t, ok);
-          ra[i] = ld4(Asrc + off);
+          if constexpr (UNPOOL) {
+            // the dY pixel of this tap (stride 1: ho = h + ph - kh, wo = w + pw - kw), its pooled row
+            // pixel / 4 and window slot pixel % 4
+            const int64_t pix =
+                ok ? ((int64_t)prow[i].n * c.Ho + (prow[i].a + c.ph - t.kh)) * c.Wo + (prow[i].b + c.pw - t.kw) : 0;
+            const int64_t po = (pix >> 2) * c.Co + t.ch;
+            ra[i] = ld4(Asrc + po);
+            parg[i] = *reinterpret_cast<const unsigned*>(c.dy_arg + po);
+            psub |= (unsigned)(pix & 3) << (2 * i);
+          } else {
+            ra[i] = ld4(Asrc + off);
+          }
+          (void)off;
           amask |= (ok ? 0xFu : 0u) << (4 * i);
         }
       } else {
@@ -299,6 +321,21 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
     }
     // B [K][N] row-major, float4 along n: rows clamped (k >= ke zeroed at store), columns clamped
     // (columns >= N only feed output columns that are never stored)
+    if constexpr (UNPOOL && MODE == kWgrad) {
+      psub = 0;
+#pragma unroll
+      for (int i = 0; i < VB; ++i) {
+        const int vi = tid + i * NT;
+        const int64_t k = k0 + vi / (BN / 4), n = n0 + (vi % (BN / 4)) * 4;
+        const int64_t kk = k < ke ? k : ke - 1;   // the dY pixel
+        const int64_t po = (kk >> 2) * c.Nn + (n < c.Nn ? n : c.Nn - 4);
+        rb[i] = ld4(Bsrc + po);
+        parg[i] = *reinterpret_cast<const unsigned*>(c.dy_arg + po);
+        psub |= (unsigned)(kk & 3) << (2 * i);
+        bmask |= (k < ke ? 1u : 0u) << i;
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < VB; ++i) {
       const int vi = tid + i * NT;
@@ -326,6 +363,23 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   v4f csum = {0.f, 0.f, 0.f, 0.f};
 
   auto store_tile = [&](int buf) {
+    if constexpr (UNPOOL) {   // rebuild the dense dY values: keep element e where its window argmax is this pixel
+      if constexpr (MODE == kDgrad) {
+#pragma unroll
+        for (int i = 0; i < VA; ++i) {
+          const unsigned sub = (psub >> (2 * i)) & 3u;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ra[i][e] = ((parg[i] >> (8 * e)) & 0xFFu) == sub ? ra[i][e] : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < VB; ++i) {
+          const unsigned sub = (psub >> (2 * i)) & 3u;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rb[i][e] = ((parg[i] >> (8 * e)) & 0xFFu) == sub ? rb[i][e] : 0.f;
+        }
+      }
+    }
     if constexpr (S16) {
       unsigned short* As = reinterpret_cast<unsigned short*>(smem + buf * STAGE_FLOATS);
       unsigned short* Bs = As + JA::ELEMS;
@@ -719,6 +773,12 @@ int to16_all(int prec, const float* const* src, const int64_t* n, int cnt, unsig
 
 template <int MODE, int BM, int BN, int BK, int LP>
 void launch_conv_p(const ConvArgs& c, dim3 grid, hipStream_t s, bool vec, bool vecb) {
+  if constexpr (MODE != kFwd) {
+    if (c.dy_arg) {   // run_conv_gemm checked vec / vecb and fp32 sources
+      hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, true, true, LP, false, true>), grid, dim3(256), 0, s, c);
+      return;
+    }
+  }
   if constexpr (LP != 0) {
     if (c.a16) {
       hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, true, true, LP, true>), grid, dim3(256), 0, s, c);
@@ -788,10 +848,12 @@ int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
   const bool vec = (chans % 4 == 0) && vecb;
   SRK_REQUIRE(!c.a16 || (prec != kPrecF32 && c.b16 && chans % 8 == 0 && c.Nn % 8 == 0), SRK_ERR_INTERNAL,
               "conv: 16-bit sources need 8-aligned channels");
+  SRK_REQUIRE(!c.dy_arg || (MODE != kFwd && !c.a16 && vec && vecb && c.sh == 1 && c.sw == 1 && c.Wo % 4 == 0),
+              SRK_ERR_INTERNAL, "conv: unpooling gathers need fp32 sources, 4-aligned channels and Wo % 4 == 0");
   ProfScope prof(prec == kPrecF32 ? name : (MODE == kFwd ? "conv_fwd_lp" : MODE == kDgrad ? "conv_dgrad_lp" : "conv_wgrad_lp"),
                  s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
   prof.detail("conv_gemm_kernel<%s,%dx%d%s> %lldx%lldx%lld s%d", MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad",
-              BM, BN, c.a16 ? ",s16" : "", (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
+              BM, BN, c.a16 ? ",s16" : c.dy_arg ? ",unpool" : (MODE == kFwd && c.pool_w) ? ",pool" : "", (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
   const dim3 grid((unsigned)c.nblk);
   if (BM == 64) launch_conv<MODE, 64, 64>(c, grid, s, vec, vecb, prec);
   else if (BN == 64) launch_conv<MODE, 128, 64>(c, grid, s, vec, vecb, prec);
@@ -879,10 +941,14 @@ int srk_conv2d_nhwc_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t
   return srk_conv2d_nhwc_bwd16(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, sh, sw, dy, dx, dw, db, ws, nullptr, stream);
 }
 
-int srk_conv2d_nhwc_bwd16(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co,
-                          int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw, const float* dy,
-                          float* dx, float* dw, float* db, float* ws, const void* x16, void* stream) {
-  SRK_API_BEGIN
+}  // extern "C"
+
+namespace srk {
+// the conv backward; dy_arg != null: dy is the (1, 4)-pooled gradient and the gathers unpool it
+// (the caller guarantees fp32 sources, the fused bias sums and no full-width data gradient)
+int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co, int64_t KH,
+             int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw, const float* dy, const uint8_t* dy_arg,
+             float* dx, float* dw, float* db, float* ws, const void* x16, void* stream) {
   int64_t Ho, Wo;
   if (int rc = srk::check(N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw, &Ho, &Wo)) return rc;
   SRK_REQUIRE(x && w && dy && dw && ws, SRK_ERR_INVALID, "conv bwd: null pointer");
@@ -892,8 +958,11 @@ int srk_conv2d_nhwc_bwd16(const float* x, int64_t N, int64_t H, int64_t W, int64
   c.N = (int)N; c.H = (int)H; c.W = (int)W; c.Ci = (int)Ci; c.Ho = (int)Ho; c.Wo = (int)Wo; c.Co = (int)Co;
   c.KH = (int)KH; c.KW = (int)KW; c.ph = (int)ph; c.pw = (int)pw; c.sh = (int)sh; c.sw = (int)sw;
   c.x = x; c.dy = dy;
+  c.dy_arg = dy_arg;
   int rc;
   const bool full_width = KH == 1 && ph == 0 && sh == 1 && pw == 0 && KW == W && Wo == 1;
+  SRK_REQUIRE(!dy_arg || (!full_width && (!db || srk::g_opt_conv_fused_db)), SRK_ERR_INTERNAL,
+              "conv bwd: pooled dY needs the implicit data gradient and the fused bias sums");
   const bool dgrad_implicit = dx && !full_width;
   if (dgrad_implicit)
     hipLaunchKernelGGL(srk::weight_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, (int)Co,
@@ -901,7 +970,7 @@ int srk_conv2d_nhwc_bwd16(const float* x, int64_t N, int64_t H, int64_t W, int64
   // 16-bit sources: x and dY serve both GEMMs, Wd the data gradient (one scratch allocation)
   unsigned short* d16[3] = {nullptr, nullptr, nullptr};   // x, dY, Wd
   const int prec = srk::matmul_prec();
-  if (srk::s16_ok(prec, Ci, Co, {x, dy, ws, x16})) {
+  if (!dy_arg && srk::s16_ok(prec, Ci, Co, {x, dy, ws, x16})) {
     const float* src[3] = {x, dy, ws};
     const int64_t n[3] = {N * H * W * Ci, N * Ho * Wo * Co, nw};
     const bool ready[3] = {x16 != nullptr, false, false};   // x16: the forward's copy of x
@@ -952,6 +1021,16 @@ int srk_conv2d_nhwc_bwd16(const float* x, int64_t N, int64_t H, int64_t W, int64
   }
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
+}
+}  // namespace srk
+
+extern "C" {
+
+int srk_conv2d_nhwc_bwd16(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co,
+                          int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw, const float* dy,
+                          float* dx, float* dw, float* db, float* ws, const void* x16, void* stream) {
+  SRK_API_BEGIN
+  return srk::conv_bwd(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, sh, sw, dy, nullptr, dx, dw, db, ws, x16, stream);
   SRK_API_END
 }
 
@@ -1003,13 +1082,19 @@ int srk_conv2d_nhwc_bwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
                   (uintptr_t)argmax % 4 == 0,
               SRK_ERR_INVALID, "conv bwd_pool: (1, 4) window dividing the output width, Co % 4, aligned buffers");
   hipStream_t s = srk::as_stream(stream);
-  float* dy = nullptr;
+  // fp32 sources (fp32, or a 16-bit mode whose channel counts rule out the 16-bit copies): the
+  // data- and weight-gradient gathers read the pooled gradient through the argmax themselves
+  const bool full_width = KH == 1 && ph == 0 && pw == 0 && KW == W && Wo == 1;
+  if (srk::g_opt_conv_unpool_gather && !full_width && (!db || srk::g_opt_conv_fused_db) &&
+      !srk::s16_ok(srk::matmul_prec(), Ci, Co, {x, w, x16}))
+    return srk::conv_bwd(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, 1, 1, dy_pooled, argmax, dx, dw, db, ws, x16, stream);
+  float* dy = nullptr;   // else: the dense gradient in library scratch, then the plain backward
   if (int rc = srk::conv_scratch((size_t)(N * Ho * Wo * Co), &dy, srk::g_csd)) return rc;
   const int64_t rows = N * Ho * Wo / pool_w;
   hipLaunchKernelGGL(srk::unpool_kernel, dim3((unsigned)((rows * (Co / 4) + 255) / 256)), dim3(256), 0, s, dy_pooled,
                      argmax, rows, (int)Co, (int)pool_w, dy);
   SRK_CHECK_HIP(hipGetLastError());
-  return srk_conv2d_nhwc_bwd16(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, 1, 1, dy, dx, dw, db, ws, x16, stream);
+  return srk::conv_bwd(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, 1, 1, dy, nullptr, dx, dw, db, ws, x16, stream);
   SRK_API_END
 }
 

@@ -23,6 +23,7 @@ int g_opt_gru_persistent = 1;
 int g_opt_gemm16_kernel = 0;
 int g_opt_conv16_sources = 1;
 int g_opt_conv_fused_db = 1;
+int g_opt_conv_unpool_gather = 1;
 int g_opt_gemm32_kernel = 0;
 static std::atomic<int> g_opt_matmul_prec{kPrecF32};
 int matmul_prec() { return g_opt_matmul_prec.load(std::memory_order_relaxed); }
@@ -352,6 +353,10 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "gemm16_kernel") {   // 0 by shape, 1 register-staged, 2 LDS-DMA ping-pong (16-bit operands)
     SRK_REQUIRE(value >= 0 && value <= 2, SRK_ERR_INVALID, "gemm16_kernel must be 0, 1 or 2");
     srk::g_opt_gemm16_kernel = (int)value;
+    return SRK_OK;
+  }
+  if (n == "conv_unpool_gather") {   // pooled conv backward: gathers unpool (1) or a dense scratch gradient (0)
+    srk::g_opt_conv_unpool_gather = value != 0;
     return SRK_OK;
   }
   if (n == "conv_fused_db") {   // conv bias gradients fused into the weight-gradient kernel (1) or a column sum (0)

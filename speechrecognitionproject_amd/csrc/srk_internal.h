@@ -101,6 +101,9 @@ extern int g_opt_conv16_sources;
 // conv bias gradients as column sums fused into the weight-gradient kernel ("conv_fused_db", default
 // 1; 0 = the separate column-sum kernel over dY)
 extern int g_opt_conv_fused_db;
+// the pooled conv's backward gathers the pooled gradient through the argmax ("conv_unpool_gather",
+// default 1; 0 = unpool into library scratch first)
+extern int g_opt_conv_unpool_gather;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

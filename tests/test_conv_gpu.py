@@ -105,11 +105,13 @@ def test_conv1_pool_fused_vs_torch(gpu, N, H, W, KH, KW, pool):
     (2, 3, 8, 128, 64, 1, 7, 0, 3),        # a few rows, deep k: the split-K forward (dense, then pooled)
     (3, 5, 12, 8, 36, 3, 3, 1, 1),         # 3 x 3 taps, N not a tile multiple
 ])
-def test_conv_pool_fused_equals_separate(gpu, precision, N, H, W, Ci, Co, KH, KW, ph, pw):
+@pytest.mark.parametrize("gather", [1, 0])
+def test_conv_pool_fused_equals_separate(gpu, gather, precision, N, H, W, Ci, Co, KH, KW, ph, pw):
     """conv + bias + MaxPool2d((1, 4)) in one launch (srk_conv2d_nhwc_fwd_pool: pooled epilogue and
     uint8 argmax; the backward unpools through the argmax) == the separate conv and maxpool kernels
     (bitwise: the same accumulators, the same first-maximum rule, the same gradient kernels), and
-    vs torch's CPU fp32 conv + max_pool2d (fp32 mode)."""
+    vs torch's CPU fp32 conv + max_pool2d (fp32 mode).  gather = 1: the backward's gathers read the
+    pooled gradient through the argmax (option conv_unpool_gather); 0: a dense scratch gradient."""
     from speechrecognitionproject_amd import _lib
     g = torch.Generator().manual_seed(N * 7 + Co)
     x = torch.randn(N, H, W, Ci, generator=g)
@@ -122,6 +124,7 @@ def test_conv_pool_fused_equals_separate(gpu, precision, N, H, W, Ci, Co, KH, KW
     outs = []
     try:
         _lib.set_matmul_precision(precision)
+        _lib.set_option("conv_unpool_gather", gather)
         for fused in (True, False):
             _lib.set_fused_conv_pool(fused)
             with torch.no_grad():
@@ -134,6 +137,7 @@ def test_conv_pool_fused_equals_separate(gpu, precision, N, H, W, Ci, Co, KH, KW
             torch.cuda.synchronize()
             outs.append([t.detach().cpu() for t in (y, xm.grad, conv.weight.grad, conv.bias.grad)])
     finally:
+        _lib.set_option("conv_unpool_gather", 1)
         _lib.set_fused_conv_pool(True)
         _lib.set_matmul_precision("fp32")
     for a, c in zip(*outs):

@@ -112,6 +112,10 @@ def lib():
         if v != ABI_VERSION:
             raise SrkError("libsrk.so ABI version %d != expected %d (rebuild)" % (v, ABI_VERSION))
         _lib = L
+        # A/B measurements: SRK_OPTIONS="conv_tile=256,gru_lp2=0" applies srk_set_option at load
+        for item in filter(None, os.environ.get("SRK_OPTIONS", "").split(",")):
+            name, _, val = item.partition("=")
+            call("srk_set_option", name.strip().encode(), int(val))
     return _lib
 
 

@@ -144,9 +144,8 @@ template <> struct ConvLp<2> {
 // the 32x32x16 MFMA fragment of operand rows c0 + (lane & 31), k = kk + 8 (lane >> 5) + 0..7.
 template <bool KC, int ROWS, int BK>
 struct Img16 {
-  static constexpr int P = KC ? BK + 8 : kTrPitch;
+  static constexpr int P = KC ? BK + 8 : (ROWS <= 128 ? kTrPitch : ROWS + 32);   // 32 (mod 128) elements
   static constexpr int ELEMS = KC ? ROWS * P : BK * P;
-  static_assert(KC || ROWS <= kTrPitch, "transposed image pitch");
   __device__ static __forceinline__ int store_off(int vi) {
     return KC ? (vi / (BK / 4)) * P + (vi % (BK / 4)) * 4 : (vi / (ROWS / 4)) * P + (vi % (ROWS / 4)) * 4;
   }
@@ -174,9 +173,14 @@ struct Img16 {
 // so the MFMA operands are bit-identical): a staged unit is 8 elements = one 16-B load and one
 // 16-B LDS store (needs VEC and VECB with 8-aligned channel counts / N).
 // UNPOOL: dY is the (1, 4)-pooled gradient + argmax (ConvArgs::dy_arg; dgrad / wgrad, fp32 sources)
-template <int MODE, int BM, int BN, int BK, bool VEC, bool VECB, int LP = 0, bool S16 = false, bool UNPOOL = false>
-__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
-  constexpr int NT = 256;
+// NW: waves per workgroup — 4 (2 x 2, each (BM/2) x (BN/2)) or 8 (BM = 256: 4 x 2, each 64 x (BN/2);
+// one 8-wave workgroup per CU holds a 256-row tile: half the L2 -> CU operand bytes per flop of two
+// 128-row workgroups)
+template <int MODE, int BM, int BN, int BK, bool VEC, bool VECB, int LP = 0, bool S16 = false, bool UNPOOL = false,
+          int NW = 4>
+__global__ __launch_bounds__(NW * 64) void conv_gemm_kernel(ConvArgs c) {
+  constexpr int NT = NW * 64;
+  constexpr int WM = NW == 8 ? 4 : 2, WN = NW / WM;
   constexpr bool AKC = MODE != kWgrad;   // A k-contiguous (channels along k) for fwd / dgrad
   using IA = Img<AKC, BM, BK>;
   using IB = Img<false, BN, BK>;         // B = row-major [K][N] (Wt / Wd / dY)
@@ -186,8 +190,9 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   static_assert(!UNPOOL || (MODE != kFwd && !S16 && VEC && VECB), "unpooling gathers: dgrad / wgrad, fp32 sources");
   constexpr int EU = S16 ? 8 : 4;        // elements per staged unit
   constexpr int VA = BM * BK / EU / NT, VB = BN * BK / EU / NT;
-  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert(VA >= 1 && VB >= 1 && TM >= 1 && TN >= 1 && VA * 4 <= 32, "bad tile");
+  static_assert(NT % (BN / 4) == 0 && (AKC || NT % (BM / EU) == 0), "a staging thread keeps its columns / taps");
   constexpr int STAGE_FLOATS = LP ? (JA::ELEMS + JB::ELEMS + 1) / 2 : IA::FLOATS + IB::FLOATS;
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE_FLOATS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -196,7 +201,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs c) {
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t kb0 = split * c.kchunk;
   const int64_t ke = (kb0 + c.kchunk < c.K) ? kb0 + c.kchunk : c.K;
-  const int wm0 = (wave >> 1) * (BM / 2), wn0 = (wave & 1) * (BN / 2);
+  const int wm0 = (wave / WN) * (BM / WM), wn0 = (wave % WN) * (BN / WN);
   const float* __restrict__ Asrc = MODE == kDgrad ? c.dy : c.x;
   const float* __restrict__ Bsrc = MODE == kWgrad ? c.dy : c.wmat;
   // pixel / tap splits by the host-set divisors: fd_w, fd_h = the pixel grid of A's rows (fwd / dgrad)
@@ -771,39 +776,58 @@ int to16_all(int prec, const float* const* src, const int64_t* n, int cnt, unsig
   return SRK_OK;
 }
 
-template <int MODE, int BM, int BN, int BK, int LP>
+template <int MODE, int BM, int BN, int BK, int LP, int NW>
 void launch_conv_p(const ConvArgs& c, dim3 grid, hipStream_t s, bool vec, bool vecb) {
+  const dim3 block(NW * 64);
   if constexpr (MODE != kFwd) {
     if (c.dy_arg) {   // run_conv_gemm checked vec / vecb and fp32 sources
-      hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, true, true, LP, false, true>), grid, dim3(256), 0, s, c);
+      hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, true, true, LP, false, true, NW>), grid, block, 0, s, c);
       return;
     }
   }
   if constexpr (LP != 0) {
     if (c.a16) {
-      hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, true, true, LP, true>), grid, dim3(256), 0, s, c);
+      hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, true, true, LP, true, false, NW>), grid, block, 0, s, c);
       return;
     }
   }
-  if (vec && vecb) hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, true, true, LP>), grid, dim3(256), 0, s, c);
-  else if (vecb) hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, false, true, LP>), grid, dim3(256), 0, s, c);
-  else hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, false, false, LP>), grid, dim3(256), 0, s, c);
+  if constexpr (NW == 8) {   // 8-wave tiles are only chosen with vector gathers (run_conv_gemm)
+    hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, true, true, LP, false, false, NW>), grid, block, 0, s, c);
+  } else {
+    if (vec && vecb) hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, true, true, LP>), grid, block, 0, s, c);
+    else if (vecb) hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, false, true, LP>), grid, block, 0, s, c);
+    else hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, BK, false, false, LP>), grid, block, 0, s, c);
+  }
 }
 
-template <int MODE, int BM, int BN>
+template <int MODE, int BM, int BN, int NW = 4>
 void launch_conv(const ConvArgs& c, dim3 grid, hipStream_t s, bool vec, bool vecb, int prec) {
-  if (prec == kPrecBF16) launch_conv_p<MODE, BM, BN, 64, 1>(c, grid, s, vec, vecb);
-  else if (prec == kPrecF16) launch_conv_p<MODE, BM, BN, 64, 2>(c, grid, s, vec, vecb);
-  else launch_conv_p<MODE, BM, BN, 32, 0>(c, grid, s, vec, vecb);
+  if constexpr (NW == 8) {   // the 8-wave 256-row tiles: fp32 operands only (run_conv_gemm)
+    launch_conv_p<MODE, BM, BN, 32, 0, NW>(c, grid, s, vec, vecb);
+  } else {
+    if (prec == kPrecBF16) launch_conv_p<MODE, BM, BN, 64, 1, NW>(c, grid, s, vec, vecb);
+    else if (prec == kPrecF16) launch_conv_p<MODE, BM, BN, 64, 2, NW>(c, grid, s, vec, vecb);
+    else launch_conv_p<MODE, BM, BN, 32, 0, NW>(c, grid, s, vec, vecb);
+  }
 }
 
 template <int MODE>
 int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
   const int prec = matmul_prec();
   const int BK = prec == kPrecF32 ? 32 : 64;   // 16-bit: 64-deep k-tiles (4 MFMA k-steps per barrier)
-  // tile: 128 x 128 unless the GEMM is narrow (N <= 64: 128 x 64) or small (64 x 64)
-  int BM = 128, BN = c.Nn <= 64 ? 64 : 128;
+  // tile: 128 x 128 unless the GEMM is narrow (N <= 64: 128 x 64) or small (64 x 64); srk option
+  // conv_tile = 256: 256 x BN tiles of 8 waves on tall GEMMs with vector gathers
+  int BM = 128, BN = c.Nn <= 64 ? 64 : 128, NW = 4;
   if (((c.M + 127) / 128) * ((c.Nn + BN - 1) / BN) < 64 && c.K < 2048) { BM = 64; BN = 64; }
+  {
+    const int chans_ = MODE == kDgrad ? c.Co : c.Ci;
+    const bool vec_ = chans_ % 4 == 0 && c.Nn % 4 == 0;
+    if (g_opt_conv_tile == 256 && prec == kPrecF32 && BM == 128 && vec_ &&
+        ((c.M + 255) / 256) * ((c.Nn + BN - 1) / BN) >= kCUs) {
+      BM = 256;
+      NW = 8;
+    }
+  }
   const int64_t tm = (c.M + BM - 1) / BM, tn = (c.Nn + BN - 1) / BN;
   SRK_REQUIRE(tm * tn <= (INT32_MAX >> 9), SRK_ERR_INVALID, "conv: grid too large");
   const int lds = prec == kPrecF32 ? 2 * 4 * ((MODE != kWgrad ? BM * (BK + 4) : BK * (BM + 8)) + BK * (BN + 8))
@@ -852,10 +876,12 @@ int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
               SRK_ERR_INTERNAL, "conv: unpooling gathers need fp32 sources, 4-aligned channels and Wo % 4 == 0");
   ProfScope prof(prec == kPrecF32 ? name : (MODE == kFwd ? "conv_fwd_lp" : MODE == kDgrad ? "conv_dgrad_lp" : "conv_wgrad_lp"),
                  s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
-  prof.detail("conv_gemm_kernel<%s,%dx%d%s> %lldx%lldx%lld s%d", MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad",
-              BM, BN, c.a16 ? ",s16" : c.dy_arg ? ",unpool" : (MODE == kFwd && c.pool_w) ? ",pool" : "", (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
+  prof.detail("conv_gemm_kernel<%s,%dx%d%s%s> %lldx%lldx%lld s%d", MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad",
+              BM, BN, NW == 8 ? ",8w" : "", c.a16 ? ",s16" : c.dy_arg ? ",unpool" : (MODE == kFwd && c.pool_w) ? ",pool" : "", (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
   const dim3 grid((unsigned)c.nblk);
   if (BM == 64) launch_conv<MODE, 64, 64>(c, grid, s, vec, vecb, prec);
+  else if (BM == 256 && BN == 64) launch_conv<MODE, 256, 64, 8>(c, grid, s, vec, vecb, prec);
+  else if (BM == 256) launch_conv<MODE, 256, 128, 8>(c, grid, s, vec, vecb, prec);
   else if (BN == 64) launch_conv<MODE, 128, 64>(c, grid, s, vec, vecb, prec);
   else launch_conv<MODE, 128, 128>(c, grid, s, vec, vecb, prec);
   SRK_CHECK_HIP(hipGetLastError());

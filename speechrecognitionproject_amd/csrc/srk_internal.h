@@ -104,6 +104,9 @@ extern int g_opt_conv_fused_db;
 // the pooled conv's backward gathers the pooled gradient through the argmax ("conv_unpool_gather",
 // default 1; 0 = unpool into library scratch first)
 extern int g_opt_conv_unpool_gather;
+// conv tile shape ("conv_tile": 128 = 128-row tiles of 4 waves, 256 = 256-row tiles of 8 waves on
+// tall convolutions)
+extern int g_opt_conv_tile;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

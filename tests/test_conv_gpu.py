@@ -51,6 +51,18 @@ def test_conv2d_nhwc_vs_torch(gpu, shape):
     _check_conv(*shape)
 
 
+@pytest.mark.parametrize("shape", [(64, 98, 40, 64, 128, 1, 7, 0, 3), (40, 98, 40, 64, 64, 1, 7, 0, 3),
+                                   (96, 98, 1, 64, 128, 7, 1, 3, 0)])
+def test_conv2d_tile256_vs_torch(gpu, shape):
+    """srk option conv_tile = 256: the 256-row, 8-wave conv tiles (fp32) on tall convolutions."""
+    from speechrecognitionproject_amd import _lib
+    try:
+        _lib.set_option("conv_tile", 256)
+        _check_conv(*shape)
+    finally:
+        _lib.set_option("conv_tile", 128)
+
+
 @pytest.mark.parametrize("shape", [  # 1-D strided convs of model_resnet_bgru.py:48,19-23 as H=1
     (2, 1, 16000, 1, 64, 1, 80, 0, 38, 1, 16), (2, 1, 1000, 64, 128, 1, 15, 0, 7, 1, 2),
     (2, 1, 1000, 64, 128, 1, 1, 0, 0, 1, 2), (3, 1, 125, 512, 512, 1, 15, 0, 7, 1, 1)])

@@ -378,6 +378,39 @@ __device__ unsigned long long g_mfcc_stamps[512 * kM3Waves * kStampPhases];
 #define MFCC_STAMP(p) do { } while (0)
 #endif
 
+// Pass-B lane layout of the DPP untangle (DPP = true): the partner (frame, 20 - k1) of lane (frame, k1)
+// sits at the DPP row_mirror position (lane ^ 15 within its 16-lane row), so the 16 partner values
+// move by v_mov_b32 dpp row_mirror (VALU) instead of ds_bpermute (LDS pipe, 24-49 cycles a wave).
+// Rows 0-2 = frames 0-2, k1 = 1..8 at p = 0..7 and 12..19 at p = 8..15.  Row 3: (f, 9) at p = f and
+// (f, 11) at 15 - f; (f, 10) at 3 + f with a duplicate at 12 - f (its mirror); (f, 0) at 6 + f (own
+// values, as before); p = 9 idle.  Duplicates and the idle lane write into the slice's unused tail.
+__device__ __forceinline__ void mfcc_passb_lane(int lane, int& fb, int& k1, int& fbw) {
+  const int r = lane >> 4, p = lane & 15;
+  fbw = -1;
+  if (r < 3) {
+    fb = r;
+    k1 = p < 8 ? p + 1 : p + 4;
+  } else if (p < 3) {
+    fb = p; k1 = 9;
+  } else if (p >= 13) {
+    fb = 15 - p; k1 = 11;
+  } else if (p < 6) {
+    fb = p - 3; k1 = 10;
+  } else if (p >= 10) {
+    fb = 12 - p; k1 = 10; fbw = 3;
+  } else if (p < 9) {
+    fb = p - 6; k1 = 0;
+  } else {
+    fb = 2; k1 = 0; fbw = 3;
+  }
+  if (fbw < 0) fbw = fb;
+}
+
+__device__ __forceinline__ float dpp_mirror(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140 /* row_mirror */, 0xF, 0xF, false));
+}
+
+template <bool DPP>
 __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __restrict__ pcm, float* __restrict__ out,
                                                                   int layout, int64_t n_clips, DeviceTables t) {
   __shared__ __attribute__((aligned(16))) v2f tbuf[kM3Waves][3 * 340];
@@ -392,7 +425,15 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
   // the wave index in an SGPR: the chunk loop and its reflect / tail branches stay scalar
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int fa = lane >> 4, j = lane & 15;           // pass A
-  const int fb = lane / 20, k1b = lane - 20 * fb;    // pass B (fb == 3: lanes 60..63 idle)
+  // pass B: lane (frame fb, k1b); bins written to frame fbw's slice (3 = the unused tail)
+  int fb, k1b, fbw;
+  if (DPP) {
+    mfcc_passb_lane(lane, fb, k1b, fbw);
+  } else {
+    fb = lane / 20;                                  // fb == 3: lanes 60..63 idle
+    k1b = lane - 20 * fb;
+    fbw = fb;
+  }
   for (int i = threadIdx.x; i < 320; i += 64 * kM3Waves)
     s_tw[i] = *reinterpret_cast<const v2f*>(t.tw320 + ((i >> 4) * (i & 15)));
   v2f win[20];
@@ -471,11 +512,16 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
     const v2f w160 = s_post[160];
 #pragma unroll
     for (int k2 = 0; k2 < 8; ++k2) {
-      Bx[k2] = bperm(pbyte, b[15 - k2].x);
-      By[k2] = bperm(pbyte, b[15 - k2].y);
+      if (DPP) {
+        Bx[k2] = dpp_mirror(b[15 - k2].x);
+        By[k2] = dpp_mirror(b[15 - k2].y);
+      } else {
+        Bx[k2] = bperm(pbyte, b[15 - k2].x);
+        By[k2] = bperm(pbyte, b[15 - k2].y);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);   // keep the 24 requests ahead of their consumers
-    float* pf = pb + fb * 321;
+    float* pf = pb + fbw * 321;
     auto two_bins = [&](float ax, float ay, float bx, float by, v2f w, int k) {
       const float sx = ax + bx, sy = ay - by, ux = ay + by, uy = bx - ax;
       const float wr = fmaf(w.x, ux, -(w.y * uy)), wi = fmaf(w.y, ux, w.x * uy);
@@ -730,8 +776,12 @@ int srk_mfcc_fwd(const float* pcm, int64_t n_clips, float* out, int layout, void
   if (int rc = srk::get_tables(&t)) return rc;
   srk::ProfScope prof("mfcc", srk::as_stream(stream), 71956.0 * (double)n_clips);     // 64000 + 7956 B/clip
   const int64_t grid = std::min<int64_t>(n_clips, 256 * 2);   // persistent over clips, 2 per CU
-  hipLaunchKernelGGL(srk::mfcc3_kernel, dim3((unsigned)grid), dim3(64 * srk::kM3Waves), 0,
-                     srk::as_stream(stream), pcm, out, layout, n_clips, *t);
+  if (srk::g_opt_mfcc_dpp)
+    hipLaunchKernelGGL(srk::mfcc3_kernel<true>, dim3((unsigned)grid), dim3(64 * srk::kM3Waves), 0,
+                       srk::as_stream(stream), pcm, out, layout, n_clips, *t);
+  else
+    hipLaunchKernelGGL(srk::mfcc3_kernel<false>, dim3((unsigned)grid), dim3(64 * srk::kM3Waves), 0,
+                       srk::as_stream(stream), pcm, out, layout, n_clips, *t);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END

@@ -98,3 +98,21 @@ def test_batch_independence_and_determinism(gpu, fn):
 def test_empty_batch(gpu):
     assert K.fbank(torch.zeros(0, 16000)).shape == (0, 98, 120)
     assert K.mfcc(torch.zeros(0, 16000)).shape == (0, 39, 51)
+
+
+@pytest.mark.parametrize("layout", [True, False])
+def test_mfcc_dpp_untangle_bitwise(gpu, layout):
+    """srk option mfcc_dpp: the untangle's partner values moved by DPP row_mirror over a permuted
+    pass-B lane layout instead of ds_bpermute — the same operands, the same arithmetic: bitwise equal
+    output (both layouts, a batch with every clip kind and more clips than the persistent grid)."""
+    from speechrecognitionproject_amd import _lib
+    x, _ = synthetic_clips(1100, seed=21)
+    xd = torch.from_numpy(x).cuda()
+    outs = []
+    try:
+        for v in (0, 1):
+            _lib.set_option("mfcc_dpp", v)
+            outs.append(K.mfcc(xd, time_major=layout).cpu())
+    finally:
+        _lib.set_option("mfcc_dpp", 0)
+    assert torch.equal(outs[0], outs[1])

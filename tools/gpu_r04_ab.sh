@@ -1,5 +1,7 @@
 #!/bin/bash
-# Round-4 A/B measurements (one gpurun call): GEMM swizzle group size on the cfg2 shapes.
+# Round-4 A/B measurements (one gpurun call):
+#   GEMM swizzle group size on the cfg2 GEMM shapes (SRK_GROUP_M=8: round 3's value, 0: balanced),
+#   conv tile shape on the cfg3 step (SRK_OPTIONS conv_tile=128 / 256).
 set -o pipefail
 OUT=gpurun_out/${1:-r04ab}
 mkdir -p "$OUT"
@@ -9,4 +11,20 @@ for g in 8 0; do
     SRK_GROUP_M=$g timeout -k 10 120 python tools/gemm_bench.py --precision $prec $extra > "$OUT/gemm_${prec}_g$g.txt" 2>&1 || exit 1
   done
 done
+for t in 128 256; do
+  SRK_OPTIONS=conv_tile=$t timeout -k 10 200 python bench.py --model fbanks_cnn --no-lowprec --no-cpu-baseline \
+    --no-feature-roofline --steps 10 > "$OUT/cfg3_tile$t.json" 2> "$OUT/cfg3_tile$t.err" || exit 1
+done
+for v in 0 1 0 1; do
+  SRK_OPTIONS=mfcc_dpp=$v FEAT_ONLY=mfcc timeout -k 10 120 python tools/feat_bench.py >> "$OUT/mfcc_dpp$v.txt" 2>&1 || exit 1
+done
 tail -n 12 "$OUT"/gemm_*.txt
+tail -n 2 "$OUT"/mfcc_dpp*.txt
+python - "$OUT" <<'PY'
+import json, sys
+for t in (128, 256):
+    r = json.loads(open("%s/cfg3_tile%d.json" % (sys.argv[1], t)).read().strip().splitlines()[-1])
+    print("cfg3 conv_tile=%d: %.1f utt/s, %.3f ms/step" % (t, r["value"], r["ms_per_step"]))
+    for k in r["roofline"]["top_kernels"]:
+        print("   ", k)
+PY

@@ -410,7 +410,9 @@ __device__ __forceinline__ float dpp_mirror(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140 /* row_mirror */, 0xF, 0xF, false));
 }
 
-template <bool DPP>
+// VAR bit 0: the DPP untangle exchange; bit 1: the pass-A and untangle twiddles held in registers for
+// the whole kernel (lane constants) instead of 28 LDS reads per chunk
+template <int VAR>
 __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __restrict__ pcm, float* __restrict__ out,
                                                                   int layout, int64_t n_clips, DeviceTables t) {
   __shared__ __attribute__((aligned(16))) v2f tbuf[kM3Waves][3 * 340];
@@ -425,6 +427,7 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
   // the wave index in an SGPR: the chunk loop and its reflect / tail branches stay scalar
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int fa = lane >> 4, j = lane & 15;           // pass A
+  constexpr bool DPP = (VAR & 1) != 0, TWREG = (VAR & 2) != 0;
   // pass B: lane (frame fb, k1b); bins written to frame fbw's slice (3 = the unused tail)
   int fb, k1b, fbw;
   if (DPP) {
@@ -453,6 +456,18 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
 #pragma unroll
   for (int q = 0; q < 18; ++q) asm volatile("" : "+v"(mw[q]));
   __syncthreads();
+  v2f twr[TWREG ? 19 : 1], wpr[TWREG ? 9 : 1];   // TWREG: W320^(j k1), k1 = 1..19; W640^(k1b + 20 k2), k2 < 8, and W640^160
+  if (TWREG) {
+#pragma unroll
+    for (int k1 = 1; k1 < 20; ++k1) twr[k1 - 1] = s_tw[k1 * 16 + j];
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) wpr[k2] = s_post[k1b + 20 * k2];
+    wpr[8] = s_post[160];
+#pragma unroll
+    for (int i = 0; i < 19; ++i) asm volatile("" : "+v"(twr[i]));
+#pragma unroll
+    for (int i = 0; i < 9; ++i) asm volatile("" : "+v"(wpr[i]));
+  }
   v2f* tb = tbuf[wave];
   float* pb = reinterpret_cast<float*>(tb);   // |X|^2 [3][321] over the transpose slice
 #ifdef SRK_MFCC_STAMPS
@@ -475,7 +490,7 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
     // wait out its own LDS round trip (the compiler keeps loads behind stores it cannot disambiguate)
     v2f tw[19];
 #pragma unroll
-    for (int k1 = 1; k1 < 20; ++k1) tw[k1 - 1] = s_tw[k1 * 16 + j];
+    for (int k1 = 1; k1 < 20; ++k1) tw[k1 - 1] = TWREG ? twr[k1 - 1] : s_tw[k1 * 16 + j];
     dft20v(a);
     if (fa < 3) {
 #pragma unroll
@@ -508,8 +523,8 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __
     float Bx[8], By[8];
     v2f wpost[8];   // untangle twiddles, requested with the partner values (not between the stores)
 #pragma unroll
-    for (int k2 = 0; k2 < 8; ++k2) wpost[k2] = s_post[k1b + 20 * k2];
-    const v2f w160 = s_post[160];
+    for (int k2 = 0; k2 < 8; ++k2) wpost[k2] = TWREG ? wpr[k2] : s_post[k1b + 20 * k2];
+    const v2f w160 = TWREG ? wpr[8] : s_post[160];
 #pragma unroll
     for (int k2 = 0; k2 < 8; ++k2) {
       if (DPP) {
@@ -776,12 +791,13 @@ int srk_mfcc_fwd(const float* pcm, int64_t n_clips, float* out, int layout, void
   if (int rc = srk::get_tables(&t)) return rc;
   srk::ProfScope prof("mfcc", srk::as_stream(stream), 71956.0 * (double)n_clips);     // 64000 + 7956 B/clip
   const int64_t grid = std::min<int64_t>(n_clips, 256 * 2);   // persistent over clips, 2 per CU
-  if (srk::g_opt_mfcc_dpp)
-    hipLaunchKernelGGL(srk::mfcc3_kernel<true>, dim3((unsigned)grid), dim3(64 * srk::kM3Waves), 0,
-                       srk::as_stream(stream), pcm, out, layout, n_clips, *t);
-  else
-    hipLaunchKernelGGL(srk::mfcc3_kernel<false>, dim3((unsigned)grid), dim3(64 * srk::kM3Waves), 0,
-                       srk::as_stream(stream), pcm, out, layout, n_clips, *t);
+  const dim3 g((unsigned)grid), b(64 * srk::kM3Waves);
+  switch (srk::g_opt_mfcc_variant) {
+    case 1: hipLaunchKernelGGL(srk::mfcc3_kernel<1>, g, b, 0, srk::as_stream(stream), pcm, out, layout, n_clips, *t); break;
+    case 2: hipLaunchKernelGGL(srk::mfcc3_kernel<2>, g, b, 0, srk::as_stream(stream), pcm, out, layout, n_clips, *t); break;
+    case 3: hipLaunchKernelGGL(srk::mfcc3_kernel<3>, g, b, 0, srk::as_stream(stream), pcm, out, layout, n_clips, *t); break;
+    default: hipLaunchKernelGGL(srk::mfcc3_kernel<0>, g, b, 0, srk::as_stream(stream), pcm, out, layout, n_clips, *t);
+  }
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END

@@ -25,7 +25,7 @@ int g_opt_conv16_sources = 1;
 int g_opt_conv_fused_db = 1;
 int g_opt_conv_unpool_gather = 1;
 int g_opt_conv_tile = 128;
-int g_opt_mfcc_dpp = 0;
+int g_opt_mfcc_variant = 0;
 int g_opt_gemm32_kernel = 0;
 static std::atomic<int> g_opt_matmul_prec{kPrecF32};
 int matmul_prec() { return g_opt_matmul_prec.load(std::memory_order_relaxed); }
@@ -357,8 +357,9 @@ int srk_set_option(const char* name, int64_t value) {
     srk::g_opt_gemm16_kernel = (int)value;
     return SRK_OK;
   }
-  if (n == "mfcc_dpp") {   // K1 untangle exchange: DPP row_mirror (1) or ds_bpermute (0); bitwise the same
-    srk::g_opt_mfcc_dpp = value != 0;
+  if (n == "mfcc_variant") {   // K1: bit 0 DPP untangle exchange, bit 1 twiddles in registers (bitwise the same)
+    SRK_REQUIRE(value >= 0 && value <= 3, SRK_ERR_INVALID, "mfcc_variant must be 0..3");
+    srk::g_opt_mfcc_variant = (int)value;
     return SRK_OK;
   }
   if (n == "conv_tile") {   // 128: 128-row conv tiles (4 waves); 256: 256-row tiles (8 waves) on tall convs

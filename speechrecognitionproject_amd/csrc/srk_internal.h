@@ -107,8 +107,9 @@ extern int g_opt_conv_unpool_gather;
 // conv tile shape ("conv_tile": 128 = 128-row tiles of 4 waves, 256 = 256-row tiles of 8 waves on
 // tall convolutions)
 extern int g_opt_conv_tile;
-// K1 MFCC untangle partner exchange by DPP row_mirror (1) or ds_bpermute (0) ("mfcc_dpp")
-extern int g_opt_mfcc_dpp;
+// K1 MFCC variant ("mfcc_variant", bitwise-identical outputs): bit 0 = the untangle's partner exchange
+// by DPP row_mirror instead of ds_bpermute, bit 1 = twiddles in registers instead of LDS
+extern int g_opt_mfcc_variant;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

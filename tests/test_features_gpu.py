@@ -101,18 +101,20 @@ def test_empty_batch(gpu):
 
 
 @pytest.mark.parametrize("layout", [True, False])
-def test_mfcc_dpp_untangle_bitwise(gpu, layout):
-    """srk option mfcc_dpp: the untangle's partner values moved by DPP row_mirror over a permuted
-    pass-B lane layout instead of ds_bpermute — the same operands, the same arithmetic: bitwise equal
-    output (both layouts, a batch with every clip kind and more clips than the persistent grid)."""
+def test_mfcc_variants_bitwise(gpu, layout):
+    """srk option mfcc_variant: the untangle's partner values moved by DPP row_mirror over a permuted
+    pass-B lane layout instead of ds_bpermute (bit 0), the twiddles held in registers (bit 1) — the
+    same operands, the same arithmetic: bitwise equal output (both layouts, a batch with every clip
+    kind and more clips than the persistent grid)."""
     from speechrecognitionproject_amd import _lib
     x, _ = synthetic_clips(1100, seed=21)
     xd = torch.from_numpy(x).cuda()
     outs = []
     try:
-        for v in (0, 1):
-            _lib.set_option("mfcc_dpp", v)
+        for v in (0, 1, 2, 3):
+            _lib.set_option("mfcc_variant", v)
             outs.append(K.mfcc(xd, time_major=layout).cpu())
     finally:
-        _lib.set_option("mfcc_dpp", 0)
-    assert torch.equal(outs[0], outs[1])
+        _lib.set_option("mfcc_variant", 0)
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)

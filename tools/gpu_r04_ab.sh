@@ -15,11 +15,11 @@ for t in 128 256; do
   SRK_OPTIONS=conv_tile=$t timeout -k 10 200 python bench.py --model fbanks_cnn --no-lowprec --no-cpu-baseline \
     --no-feature-roofline --steps 10 > "$OUT/cfg3_tile$t.json" 2> "$OUT/cfg3_tile$t.err" || exit 1
 done
-for v in 0 1 0 1; do
-  SRK_OPTIONS=mfcc_dpp=$v FEAT_ONLY=mfcc timeout -k 10 120 python tools/feat_bench.py >> "$OUT/mfcc_dpp$v.txt" 2>&1 || exit 1
+for v in 0 1 2 3 0 1 2 3; do
+  SRK_OPTIONS=mfcc_variant=$v FEAT_ONLY=mfcc timeout -k 10 120 python tools/feat_bench.py >> "$OUT/mfcc_var$v.txt" 2>&1 || exit 1
 done
 tail -n 12 "$OUT"/gemm_*.txt
-tail -n 2 "$OUT"/mfcc_dpp*.txt
+tail -n 2 "$OUT"/mfcc_var*.txt
 python - "$OUT" <<'PY'
 import json, sys
 for t in (128, 256):

@@ -35,7 +35,26 @@ struct KernelArgs {
   int64_t kchunk;        // K range per split (a multiple of BK)
   float* partial;        // [splits][M][N] when split
   float* rs_partial;     // [splits][M] when split and rowsum requested
+  // stream-K (gemm_p32_kernel, option gemm_streamk): sk_wgs workgroups split the tiles x sk_ki K-tiles
+  // into equal contiguous runs; a tile covered by several runs is written as partial sums into
+  // sk_slab[order of the run within the tile][M][N] and summed by sk_fixup_kernel
+  int sk_wgs;
+  int sk_ki;
+  float* sk_slab;
 };
+
+// tile index t (one split's grid, grouped order) -> (tile row, tile column); see map_tile
+__device__ __forceinline__ void tile_of(int t, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
+  const int gsz_full = group_m * tiles_n;
+  const int grp = t / gsz_full, first_m = grp * group_m;
+  const int gm = tiles_m - first_m < group_m ? tiles_m - first_m : group_m;
+  const int tin = t - grp * gsz_full;
+  tm = first_m + tin % gm;
+  tn = tin / gm;
+}
+// stream-K: run w covers K-tile iterations [w total / W, (w + 1) total / W); the run holding iteration it
+__device__ __forceinline__ int64_t sk_begin(int64_t w, int64_t total, int64_t W) { return w * total / W; }
+__device__ __forceinline__ int sk_owner(int64_t it, int64_t total, int64_t W) { return (int)(((it + 1) * W - 1) / total); }
 
 // Epilogue shared by the tile kernels.  32x32 accumulator: col = lane & 31,
 // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).  Split-K launches write the raw fp32 slab.
@@ -815,12 +834,12 @@ __global__ __launch_bounds__(NW * 64, (h16_per_cu<TA, TB, BM, BN>())) void gemm_
 // the raw slab; otherwise alpha, bias and beta are applied.
 __device__ __forceinline__ void pp_epilogue(const KernelArgs& ka, const f32x16 (&acc)[4][2], float* lds, int split,
                                             int64_t m0, int64_t n0, int grp, int wc, int wave, int lane,
-                                            int64_t z = 0) {
+                                            int64_t z = 0, float* slab = nullptr) {
   const GemmDesc& d = ka.d;
   float* st = lds + wave * 4096;
-  const bool split_mode = ka.partial != nullptr;
+  const bool split_mode = ka.partial != nullptr || slab != nullptr;   // raw partial sums, [M][N]
   // batched launches: batch z's slabs follow batch z - 1's ([batch][splits][M][N])
-  float* C = split_mode ? ka.partial + (z * (ka.nblk / ka.tiles) + split) * d.M * d.N : d.C + z * d.sC;
+  float* C = slab ? slab : split_mode ? ka.partial + (z * (ka.nblk / ka.tiles) + split) * d.M * d.N : d.C + z * d.sC;
   const int64_t ldc = split_mode ? d.N : d.ldc;
   const bool vec = (ldc % 4 == 0) && ((uintptr_t)C % 16 == 0);
   const int lh = lane >> 5, lc = lane & 31;
@@ -1357,11 +1376,42 @@ __global__ __launch_bounds__(512, 1) void gemm_p32_kernel(KernelArgs ka) {
   };
   const GemmDesc& d = ka.d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = wave >> 2, wc = wave & 3;
-  int split, tm, tn;
-  map_tile(ka.nblk, ka.tiles, ka.tiles_m, ka.tiles_n, ka.group_m, ka.remap != 0, split, tm, tn);
+  // stream-K: this workgroup's run of K-tile iterations, walked tile by tile (segments)
+  const bool sk = ka.sk_wgs > 0;
+  int64_t sk_it = 0, sk_end = 0;
+  const int64_t sk_total = (int64_t)ka.tiles * ka.sk_ki;
+  if (sk) {
+    int lin = blockIdx.x;
+    if (ka.remap) {   // the XCD remap of map_tile: neighbouring runs (tiles) on one XCD
+      const int b = blockIdx.x, xcd = b & 7, q = ka.nblk >> 3, r = ka.nblk & 7;
+      lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    }
+    sk_it = sk_begin(lin, sk_total, ka.sk_wgs);
+    sk_end = sk_begin(lin + 1, sk_total, ka.sk_wgs);
+  }
+  for (bool first_seg = true;; first_seg = false) {
+  int split = 0, tm, tn;
+  int64_t kb0, ke;
+  float* seg_slab = nullptr;
+  if (sk) {
+    if (sk_it >= sk_end) break;
+    const int t = (int)(sk_it / ka.sk_ki);
+    const int64_t t0 = (int64_t)t * ka.sk_ki, kt_end = min((int64_t)ka.sk_ki, sk_end - t0);
+    kb0 = (sk_it - t0) * BK;
+    ke = min(d.K, kt_end * BK);
+    tile_of(t, ka.tiles_m, ka.tiles_n, ka.group_m, tm, tn);
+    const int w0 = sk_owner(t0, sk_total, ka.sk_wgs), w1 = sk_owner(t0 + ka.sk_ki - 1, sk_total, ka.sk_wgs);
+    const int wme = sk_owner(sk_it, sk_total, ka.sk_wgs);
+    if (w1 > w0) seg_slab = ka.sk_slab + (int64_t)(wme - w0) * d.M * d.N;   // a partial tile
+    sk_it = t0 + ka.sk_ki;
+    if (!first_seg) __syncthreads();   // the previous segment's epilogue is done with the LDS ring
+  } else {
+    if (!first_seg) break;
+    map_tile(ka.nblk, ka.tiles, ka.tiles_m, ka.tiles_n, ka.group_m, ka.remap != 0, split, tm, tn);
+    kb0 = split * ka.kchunk;
+    ke = (kb0 + ka.kchunk < d.K) ? kb0 + ka.kchunk : d.K;
+  }
   const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
-  const int64_t kb0 = split * ka.kchunk;
-  const int64_t ke = (kb0 + ka.kchunk < d.K) ? kb0 + ka.kchunk : d.K;
   const int nk = ke > kb0 ? (int)((ke - kb0 + BK - 1) / BK) : 0;
 
   typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
@@ -1465,7 +1515,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p32_kernel(KernelArgs ka) {
   }
   if (grp == 0) bar();
 
-  pp_epilogue(ka, acc, smem, split, m0, n0, grp, wc, wave, lane, z);
+  pp_epilogue(ka, acc, smem, split, m0, n0, grp, wc, wave, lane, z, seg_slab);
   if (do_rs) {   // lanes l and l + 32 hold the two k halves of row (l & 31) of each row block
     const int splits = ka.nblk / ka.tiles;
     float* rsum = d.rowsum + z * d.sRS;
@@ -1477,6 +1527,51 @@ __global__ __launch_bounds__(512, 1) void gemm_p32_kernel(KernelArgs ka) {
         if (ka.partial) ka.rs_partial[(z * splits + split) * d.M + row] = t;
         else rsum[row] = d.rowsum_beta != 0.f ? d.rowsum_beta * rsum[row] + t : t;
       }
+    }
+  }
+  }   // segments
+}
+
+// Stream-K fixup: a tile covered by several runs = the sum of its partial slabs in run order, then
+// alpha / bias / beta (the splitk_reduce epilogue).  One workgroup per tile; whole tiles return.
+__global__ __launch_bounds__(256) void sk_fixup_kernel(KernelArgs ka) {
+  const GemmDesc& d = ka.d;
+  const int t = blockIdx.x;
+  const int64_t total = (int64_t)ka.tiles * ka.sk_ki, t0 = (int64_t)t * ka.sk_ki;
+  const int w0 = sk_owner(t0, total, ka.sk_wgs), w1 = sk_owner(t0 + ka.sk_ki - 1, total, ka.sk_wgs);
+  if (w1 == w0) return;
+  int tm, tn;
+  tile_of(t, ka.tiles_m, ka.tiles_n, ka.group_m, tm, tn);
+  const int nseg = w1 - w0 + 1;
+  const int64_t MN = d.M * d.N;
+  const bool vec = d.N % 4 == 0 && d.ldc % 4 == 0 && (uintptr_t)d.C % 16 == 0 && (uintptr_t)ka.sk_slab % 16 == 0 &&
+                   (d.bias_mode != 1 || (uintptr_t)d.bias % 16 == 0);
+  for (int i = threadIdx.x; i < 256 * 64; i += 256) {   // (row, column quad) of the 256 x 256 tile
+    const int64_t row = (int64_t)tm * 256 + (i >> 6), col = (int64_t)tn * 256 + (i & 63) * 4;
+    if (row >= d.M || col >= d.N) continue;
+    const int64_t o = row * d.N + col;
+    if (vec) {   // col + 3 < N
+      v4f v = *reinterpret_cast<const v4f*>(ka.sk_slab + o);
+      for (int g = 1; g < nseg; ++g) v += *reinterpret_cast<const v4f*>(ka.sk_slab + g * MN + o);
+      v *= d.alpha;
+      if (d.bias_mode == 1) v += *reinterpret_cast<const v4f*>(d.bias + col);
+      else if (d.bias_mode == 2) v += d.bias[row];
+      float* c = d.C + row * d.ldc + col;
+      if (d.beta != 0.f) v += d.beta * *reinterpret_cast<const v4f*>(c);
+      *reinterpret_cast<v4f*>(c) = v;
+      continue;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (col + e >= d.N) break;
+      float v = 0.f;
+      for (int g = 0; g < nseg; ++g) v += ka.sk_slab[g * MN + o + e];
+      v *= d.alpha;
+      if (d.bias_mode == 1) v += d.bias[col + e];
+      else if (d.bias_mode == 2) v += d.bias[row];
+      float* c = d.C + row * d.ldc + col + e;
+      if (d.beta != 0.f) v += d.beta * *c;
+      *c = v;
     }
   }
 }
@@ -1784,11 +1879,22 @@ int launch_p32(const GemmDesc& d, hipStream_t s) {
   KernelArgs ka;
   int splits = 1;
   const int64_t tiles = ((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
-  if (int rc = plan_launch(d, 256, 256, kP32BK, 1, ka, &splits, tiles * 2 < kCUs, true)) return rc;
+  const int64_t ki = (d.K + kP32BK - 1) / kP32BK;
+  // stream-K where one round of 256 x 256 tiles leaves CUs idle but covers at least half of them
+  // (dx of the BiGRU layers: 204 tiles on 256 CUs), K long enough to split
+  const bool streamk = g_opt_gemm_streamk && d.batch == 1 && !d.rowsum && tiles < kCUs && tiles * 2 >= kCUs && ki >= 32;
+  if (int rc = plan_launch(d, 256, 256, kP32BK, 1, ka, &splits, !streamk && tiles * 2 < kCUs, true)) return rc;
+  if (streamk) {
+    ka.sk_wgs = kCUs;
+    ka.sk_ki = (int)ki;
+    ka.nblk = kCUs;
+    if (int rc = get_scratch((size_t)3 * d.M * d.N, &ka.sk_slab)) return rc;   // <= 3 runs per tile (tiles >= W / 2)
+  }
   ProfScope prof("gemm_f32", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
-  prof.detail("gemm_p32_kernel<%c%c> %lldx%lldx%lld b%d s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', (long long)d.M,
-              (long long)d.N, (long long)d.K, d.batch, splits);
+  prof.detail("gemm_p32_kernel<%c%c> %lldx%lldx%lld b%d s%d%s", TA ? 'T' : 'N', TB ? 'T' : 'N', (long long)d.M,
+              (long long)d.N, (long long)d.K, d.batch, splits, streamk ? " streamk" : "");
   hipLaunchKernelGGL((gemm_p32_kernel<TA, TB>), dim3((unsigned)ka.nblk, (unsigned)d.batch), dim3(512), 0, s, ka);
+  if (streamk) hipLaunchKernelGGL(sk_fixup_kernel, dim3((unsigned)ka.tiles), dim3(256), 0, s, ka);
   return finish_splits(d, ka, splits, s);
 }
 

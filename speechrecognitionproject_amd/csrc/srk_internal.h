@@ -110,6 +110,8 @@ extern int g_opt_conv_tile;
 // K1 MFCC variant ("mfcc_variant", bitwise-identical outputs): bit 0 = the untangle's partner exchange
 // by DPP row_mirror instead of ds_bpermute, bit 1 = twiddles in registers instead of LDS
 extern int g_opt_mfcc_variant;
+// stream-K for fp32 ping-pong GEMMs whose 256 x 256 grid covers 1/2 .. 1 round of CUs ("gemm_streamk")
+extern int g_opt_gemm_streamk;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -436,3 +436,36 @@ def test_bigru_lowprec_wide_matches_chunked(gpu, prec, B, T, IN):
     for a, b in [(a0[1], c0[1])] + [(g0[n], h0[n]) for n in g0]:
         err = float((a - b).norm() / b.norm())
         assert err <= 2e-3, err
+
+
+@pytest.mark.parametrize("M,N,K,ta,beta,bias", [(13056, 1024, 3072, 0, 0.0, 0), (8000, 1024, 777, 0, 1.5, 1),
+                                                (7000, 1100, 2048, 1, 0.0, 2)])
+def test_gemm_streamk(gpu, M, N, K, ta, beta, bias):
+    """srk option gemm_streamk: the fp32 ping-pong GEMM over a grid of 1/2 .. 1 round of 256 x 256
+    tiles (the BiGRU layers' dx: 204 tiles on 256 CUs) split into equal runs of K-tiles, partial tiles
+    summed by the fixup kernel — vs float64 and vs the one-run-per-tile launch."""
+    from speechrecognitionproject_amd import _lib
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn((K, M) if ta else (M, K), generator=g)
+    B = torch.randn(K, N, generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    bv = torch.randn(M if bias == 2 else N, generator=g)
+    ref = 0.5 * ((A.T if ta else A).double() @ B.double()) + beta * C0.double()
+    if bias == 1:
+        ref += bv.double()
+    elif bias == 2:
+        ref += bv.double()[:, None]
+    Ad, Bd, bd = A.cuda(), B.cuda(), bv.cuda()
+    outs = []
+    try:
+        for sk in (1, 0):
+            _lib.set_option("gemm_streamk", sk)
+            Cd = C0.clone().cuda()
+            call("srk_gemm_f32", ta, 0, M, N, K, 0.5, ptr(Ad), Ad.shape[1], ptr(Bd), N, beta, ptr(Cd), N,
+                 ptr(bd) if bias else None, bias, stream_ptr())
+            outs.append(Cd.cpu().double())
+    finally:
+        _lib.set_option("gemm_streamk", 0)
+    tol = 1e-5 * (1 + (A.abs().max() * B.abs().max() * K).item())
+    assert (outs[0] - ref).abs().max() <= tol
+    assert (outs[0] - outs[1]).abs().max() <= tol

@@ -11,6 +11,9 @@ for g in 8 0; do
     SRK_GROUP_M=$g timeout -k 10 120 python tools/gemm_bench.py --precision $prec $extra > "$OUT/gemm_${prec}_g$g.txt" 2>&1 || exit 1
   done
 done
+for sk in 0 1; do
+  SRK_OPTIONS=gemm_streamk=$sk timeout -k 10 120 python tools/gemm_bench.py --precision fp32 > "$OUT/gemm_fp32_sk$sk.txt" 2>&1 || exit 1
+done
 for t in 128 256; do
   SRK_OPTIONS=conv_tile=$t timeout -k 10 200 python bench.py --model fbanks_cnn --no-lowprec --no-cpu-baseline \
     --no-feature-roofline --steps 10 > "$OUT/cfg3_tile$t.json" 2> "$OUT/cfg3_tile$t.err" || exit 1

@@ -827,6 +827,53 @@ __global__ __launch_bounds__(NW * 64, (h16_per_cu<TA, TB, BM, BN>())) void gemm_
   store_acc<TM, TN>(ka, acc, split, m0, n0, wm0, wn0, lane, 0);
 }
 
+// map_tile for a virtual block index v (persistent kernels: v = blockIdx.x + r gridDim.x), same order
+__device__ __forceinline__ void map_tile_v(int v, int nblk, int tiles, int tiles_m, int tiles_n, int group_m,
+                                           bool remap, int& split, int& tm, int& tn) {
+  int lin = v;
+  if (remap) {
+    const int xcd = v & 7, q = nblk >> 3, r = nblk & 7;
+    lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (v >> 3);
+  }
+  split = lin / tiles;
+  tile_of(lin - split * tiles, tiles_m, tiles_n, group_m, tm, tn);
+}
+
+// Epilogue of the persistent ping-pong kernel: straight from the 32x32 accumulators (a half-wave
+// writes 32 consecutive floats of one row per instruction), no LDS; split-K slabs are
+// [batch][splits][M][N] as in pp_epilogue.
+__device__ __forceinline__ void direct_epilogue(const KernelArgs& ka, const f32x16 (&acc)[4][2], int split, int64_t m0,
+                                                int64_t n0, int grp, int wc, int lane, int64_t z) {
+  const GemmDesc& d = ka.d;
+  const bool split_mode = ka.partial != nullptr;
+  float* C = split_mode ? ka.partial + (z * (ka.nblk / ka.tiles) + split) * d.M * d.N : d.C + z * d.sC;
+  const int64_t ldc = split_mode ? d.N : d.ldc;
+  const int lh = lane >> 5, lc = lane & 31;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = n0 + wc * 64 + j * 32 + lc;
+      if (col >= d.N) continue;
+      const float bcol = (!split_mode && d.bias_mode == 1) ? d.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + grp * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row >= d.M) continue;
+        float* c = C + row * ldc + col;
+        if (split_mode) {
+          *c = acc[i][j][r];
+          continue;
+        }
+        float v = d.alpha * acc[i][j][r] + bcol;
+        if (d.bias_mode == 2) v += d.bias[row];
+        if (d.beta != 0.f) v += d.beta * *c;
+        *c = v;
+      }
+    }
+  }
+}
+
 // Epilogue of the ping-pong kernels (gemm_g16_kernel, gemm_p32_kernel): each wave stages 64 x 64
 // fp32 of its 128 x 64 accumulator block per pass through LDS (16 KB per wave, 128 KB for the 8
 // waves; the K ring is idle by then), then writes rows as 16-B vectors (4 rows x 256 B per
@@ -963,7 +1010,12 @@ struct G16Half {
 constexpr int kG16Stages = SRK_G16_STAGES;
 static_assert(kG16Stages >= 4 && kG16Stages <= 5, "g16 ring: 4..5 stages of 32 KB (the epilogue needs 128 KB)");
 
-template <bool TA, bool TB, bool F16>
+// PERS: persistent tile loop (option gemm16_persistent) — a grid of one workgroup per CU walks the
+// tiles (virtual block v = blockIdx.x + r gridDim.x through the same XCD-aware map), and the epilogue
+// stores straight from the accumulators (32x32 layout: 128-B row segments per half-wave) instead of
+// staging through the LDS ring, so the next tile's prologue DMA follows the stores at once and the
+// stores drain behind its first K-tiles.
+template <bool TA, bool TB, bool F16, bool PERS = false>
 __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
   using Ops = LpOps<F16>;
   using e8 = typename Ops::e8;
@@ -985,8 +1037,9 @@ __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
   };
   const GemmDesc& d = ka.d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = wave >> 2, wc = wave & 3;
+  for (int vblk = blockIdx.x; vblk < (PERS ? ka.nblk : (int)blockIdx.x + 1); vblk += gridDim.x) {
   int split, tm, tn;
-  map_tile(ka.nblk, ka.tiles, ka.tiles_m, ka.tiles_n, ka.group_m, ka.remap != 0, split, tm, tn);
+  map_tile_v(vblk, ka.nblk, ka.tiles, ka.tiles_m, ka.tiles_n, ka.group_m, ka.remap != 0, split, tm, tn);
   const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
   const int64_t kb0 = split * ka.kchunk;
   const int64_t ke = (kb0 + ka.kchunk < d.K) ? kb0 + ka.kchunk : d.K;
@@ -1105,7 +1158,9 @@ __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
 #if defined(SRK_G16_EXP) && SRK_G16_EXP == 3   // experiment builds only: no C stores (kept live)
   if (d.alpha != 12345.f) return;
 #endif
-  pp_epilogue(ka, acc, reinterpret_cast<float*>(smem), split, m0, n0, grp, wc, wave, lane, z);
+  if (PERS) direct_epilogue(ka, acc, split, m0, n0, grp, wc, lane, z);
+  else pp_epilogue(ka, acc, reinterpret_cast<float*>(smem), split, m0, n0, grp, wc, wave, lane, z);
+  }   // tiles
 }
 
 // ------------------------------------------------------------------ skinny GEMMs (VALU)
@@ -1853,9 +1908,15 @@ int launch_g16(const GemmDesc& d, hipStream_t s, bool f16) {
   ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
   prof.detail("gemm_g16_kernel<%c%c> %lldx%lldx%lld b%d s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', (long long)d.M,
               (long long)d.N, (long long)d.K, d.batch, splits);
-  const dim3 grid((unsigned)ka.nblk, (unsigned)d.batch), block(512);
-  if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true>), grid, block, 0, s, ka);
-  else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false>), grid, block, 0, s, ka);
+  const bool pers = g_opt_gemm16_persistent && ka.nblk > kCUs;   // more than one round of tiles
+  const dim3 grid((unsigned)(pers ? kCUs : ka.nblk), (unsigned)d.batch), block(512);
+  if (pers) {
+    if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true, true>), grid, block, 0, s, ka);
+    else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false, true>), grid, block, 0, s, ka);
+  } else {
+    if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true>), grid, block, 0, s, ka);
+    else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false>), grid, block, 0, s, ka);
+  }
   return finish_splits(d, ka, splits, s);
 }
 

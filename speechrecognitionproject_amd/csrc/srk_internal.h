@@ -112,6 +112,8 @@ extern int g_opt_conv_tile;
 extern int g_opt_mfcc_variant;
 // stream-K for fp32 ping-pong GEMMs whose 256 x 256 grid covers 1/2 .. 1 round of CUs ("gemm_streamk")
 extern int g_opt_gemm_streamk;
+// persistent tile loop with direct-store epilogue for the 16-bit ping-pong GEMM ("gemm16_persistent")
+extern int g_opt_gemm16_persistent;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -519,3 +519,37 @@ def test_bigru_backward_when_batched_dwhh_is_unavailable(gpu, precision, H, opts
     for n in grads[0]:
         assert torch.isfinite(grads[0][n]).all(), n
         assert torch.equal(grads[0][n], grads[1][n]), n
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0)])
+@pytest.mark.parametrize("M,N,K,beta", [(13056, 3072, 1024, 0.0), (4100, 2050, 360, 2.0), (1800, 1000, 8000, 0.0)])
+def test_gemm16_persistent(prec, ta, tb, M, N, K, beta):
+    """srk option gemm16_persistent: the 16-bit ping-pong GEMM as a persistent tile loop (one
+    workgroup per CU walking > 256 tiles; the third shape walks split-K slabs) with the direct-store
+    epilogue == float64 product of the 16-bit values, and == the one-tile-per-workgroup launch up to
+    the epilogue's fp32 rounding."""
+    g = torch.Generator().manual_seed(M + N + K + ta)
+    dt = TORCH_DT[prec]
+    A = torch.randn((K, M) if ta else (M, K), generator=g).to(dt)
+    B = torch.randn((N, K) if tb else (K, N), generator=g).to(dt)
+    C0 = torch.randn(M, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    opA = (A.T if ta else A).double()
+    opB = (B.T if tb else B).double()
+    ref = 0.5 * (opA @ opB) + beta * C0.double() + bias.double()
+    Ad, Bd, bd = A.cuda(), B.cuda(), bias.cuda()
+    outs = []
+    try:
+        _lib.set_option("gemm16_kernel", 2)
+        for pers in (1, 0):
+            _lib.set_option("gemm16_persistent", pers)
+            Cd = C0.clone().cuda()
+            call("srk_gemm_16", ta, tb, M, N, K, 0.5, ptr(Ad), Ad.shape[1], ptr(Bd), Bd.shape[1], beta, ptr(Cd), N,
+                 ptr(bd), 1, stream_ptr())
+            outs.append(Cd.cpu().double())
+    finally:
+        _lib.set_option("gemm16_persistent", 0)
+        _lib.set_option("gemm16_kernel", 0)
+    scale = (opA.abs() @ opB.abs()).max().item()
+    assert (outs[0] - ref).abs().max().item() <= 2e-6 * (1 + scale)
+    assert (outs[0] - outs[1]).abs().max().item() <= 1e-6 * (1 + scale)

@@ -14,6 +14,9 @@ done
 for sk in 0 1; do
   SRK_OPTIONS=gemm_streamk=$sk timeout -k 10 120 python tools/gemm_bench.py --precision fp32 > "$OUT/gemm_fp32_sk$sk.txt" 2>&1 || exit 1
 done
+for pers in 0 1; do
+  SRK_OPTIONS=gemm16_persistent=$pers timeout -k 10 120 python tools/gemm_bench.py --precision bf16 --h16 > "$OUT/gemm_bf16_pers$pers.txt" 2>&1 || exit 1
+done
 for t in 128 256; do
   SRK_OPTIONS=conv_tile=$t timeout -k 10 200 python bench.py --model fbanks_cnn --no-lowprec --no-cpu-baseline \
     --no-feature-roofline --steps 10 > "$OUT/cfg3_tile$t.json" 2> "$OUT/cfg3_tile$t.err" || exit 1

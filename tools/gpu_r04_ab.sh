@@ -11,6 +11,7 @@ for g in 8 0; do
     SRK_GROUP_M=$g timeout -k 10 120 python tools/gemm_bench.py --precision $prec $extra > "$OUT/gemm_${prec}_g$g.txt" 2>&1 || exit 1
   done
 done
+SRK_GROUP_M=0 timeout -k 10 120 python tools/gemm_bench.py --precision fp32 --kernel32 2 > "$OUT/gemm_fp32_k2.txt" 2>&1 || exit 1
 for sk in 0 1; do
   SRK_OPTIONS=gemm_streamk=$sk timeout -k 10 120 python tools/gemm_bench.py --precision fp32 > "$OUT/gemm_fp32_sk$sk.txt" 2>&1 || exit 1
 done

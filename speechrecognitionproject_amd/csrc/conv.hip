@@ -811,8 +811,362 @@ void launch_conv(const ConvArgs& c, dim3 grid, hipStream_t s, bool vec, bool vec
   }
 }
 
+// ------------------------------------------------------------------ fp32 LDS-DMA ring conv (option conv_ring)
+// The implicit GEMMs of stride-1 / channel-aligned convolutions on the structure of gemm_p32_kernel
+// (gemm.hip): 256 x BN tiles (BN = 256 or 128), 8 waves in two groups running one section apart
+// behind raw barriers, a ring of four 16-deep K-tiles filled by inline-asm buffer_load ... lds.  The
+// only conv-specific part is the DMA source address: with the gathered operand's channel count a
+// multiple of 16, a K-tile lies inside one tap (kh, kw), so per K-tile each lane recomputes its unit's
+// source offset from its pixel (decomposed once per tile) and the uniform tap; a unit outside the
+// image, past the problem or past the split's k end is read past num_records, i.e. as zeros.
+//   fwd   A = X[n, a + kh - ph, b + kw - pw, ch..ch+3]       (KC: 4 channels of one pixel per unit)
+//   dgrad A = dY[n, a + ph - kh, b + pw - kw, ch..ch+3]      (KC, stride 1)
+//   wgrad A^T unit = X[pixel k (+ tap), ci..ci+3]           (TR: 4 channels at one pixel per unit)
+//   B = the re-laid-out weights [K][N] (fwd / dgrad) or dY [pixels][Co] (wgrad): plain row-major
+// Epilogue straight from the accumulators (the 96-KB ring of BN = 128 leaves no room to stage),
+// with the (1, 4) pooled variant of conv_gemm_kernel (fwd) and the fused bias column sums (wgrad).
+constexpr int kRBK = 16;
+constexpr unsigned kROOB = 0x80000000u;
+
+template <int MODE, int BN>
+__global__ __launch_bounds__(512, 1) void conv_ring_kernel(ConvArgs c) {
+  constexpr int BK = kRBK, NST = 4;
+  constexpr bool AKC = MODE != kWgrad;
+  constexpr int HALF = 128 * BK;                     // 8 KB of fp32 per 128-row half image
+  constexpr int NBH = BN / 128;                      // B half images
+  constexpr int STAGE = (2 + NBH) * HALF;
+  constexpr int NDMA = 2 + NBH;                      // DMA instructions per wave per K-tile
+  // wave layout in a group of 4: BN 256 -> 1 x 4 (128 x 64 each), BN 128 -> 2 x 2 (64 x 64 each)
+  constexpr int WR = BN == 256 ? 1 : 2, WC = 4 / WR;
+  constexpr int TM = 128 / WR / 32, TN = BN / WC / 32;
+  __shared__ __attribute__((aligned(1024))) float smem[NST * STAGE];
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+  auto bar = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = wave >> 2, w4 = wave & 3;
+  const int wr = w4 / WC, wc = w4 % WC;
+  int split, tm, tn;
+  map_tile(c.nblk, c.tiles, c.tiles_m, c.tiles_n, c.group_m, true, split, tm, tn);
+  const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * BN;
+  const int64_t kb0 = split * c.kchunk;
+  const int64_t ke = (kb0 + c.kchunk < c.K) ? kb0 + c.kchunk : c.K;
+  const int nk = ke > kb0 ? (int)((ke - kb0 + BK - 1) / BK) : 0;
+  const float* Asrc = MODE == kDgrad ? c.dy : c.x;
+  const float* Bsrc = MODE == kWgrad ? c.dy : c.wmat;
+  auto rsrc = [](const float* p) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    return u32x4s{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)a),
+                  (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)), 0x7ffffff0u, 0x00020000u};
+  };
+  const u32x4s rsA = rsrc(Asrc), rsB = rsrc(Bsrc);
+  const int chans = MODE == kDgrad ? c.Co : c.Ci;   // channels of the gathered operand
+
+  // this wave's piece of each A half: the unit (row or m group, k offset) it brings in
+  const int p = wave * 64 + lane;
+  int arow[2], akk[2];
+  Pix apix[2];      // fwd / dgrad: the unit's pixel
+  Tap atap[2];      // wgrad: the unit's (kh, kw, ci)
+  bool aok[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (AKC) {   // p = row * 4 + slot, k = 4 (slot ^ swz(row))
+      arow[h] = p >> 2;
+      akk[h] = ((p & 3) ^ ((arow[h] >> 2) & 3)) * 4;
+      apix[h] = split_pix(m0 + h * 128 + arow[h], c.M, c.fd_w, c.fd_h);
+      aok[h] = apix[h].ok;
+    } else {     // p = k * 32 + unit of 4 rows
+      akk[h] = p >> 5;
+      arow[h] = (p & 31) * 4;
+      const int64_t m = m0 + h * 128 + arow[h];
+      aok[h] = m < c.M;
+      atap[h] = split_tap(aok[h] ? m : 0, c.fd_c, c.fd_kw);
+    }
+  }
+  // B halves: p = k * 32 + unit of 4 columns (plain [K][N])
+  unsigned bvo[NBH];
+  bool bok[NBH];
+  const int bkk = p >> 5;
+#pragma unroll
+  for (int h = 0; h < NBH; ++h) {
+    const int64_t n = n0 + h * 128 + (p & 31) * 4;
+    bok[h] = n < c.Nn;
+    bvo[h] = (unsigned)(((int64_t)bkk * c.Nn + (bok[h] ? n : 0)) * 4);
+  }
+  const unsigned lds0 =
+      (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ptr)smem + (unsigned)wave * 1024u);
+  auto issue = [&](unsigned v, const u32x4s& rs, unsigned ldsa, unsigned soff) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(v), "s"(rs), "s"(ldsa), "s"(soff)
+                 : "memory");
+  };
+  auto dma_a = [&](int t) {
+    const int64_t k0 = kb0 + (int64_t)t * BK;
+    const unsigned ldst = lds0 + (unsigned)((t % NST) * STAGE * 4);
+    // fwd / dgrad: the K-tile's tap and channel base (uniform: chans % 16 == 0, k0 % 16 == 0)
+    const unsigned tap = AKC ? (unsigned)__builtin_amdgcn_readfirstlane(c.fd_c.div((unsigned)k0)) : 0u;
+    const int ch0 = (int)((unsigned)k0 - tap * (unsigned)chans);
+    const int kh = (int)c.fd_kw.div(tap), kw = (int)(tap - (unsigned)kh * c.KW);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      unsigned v = kROOB;
+      if (AKC) {
+        const Pix& q = apix[h];
+        int64_t off;
+        bool ok;
+        if (MODE == kFwd) {
+          const int hi = q.a * c.sh + kh - c.ph, wi = q.b * c.sw + kw - c.pw;
+          ok = hi >= 0 && hi < c.H && wi >= 0 && wi < c.W;
+          off = (((int64_t)q.n * c.H + hi) * c.W + wi) * c.Ci + ch0 + akk[h];
+        } else {
+          const int ho = q.a + c.ph - kh, wo = q.b + c.pw - kw;
+          ok = ho >= 0 && ho < c.Ho && wo >= 0 && wo < c.Wo;
+          off = (((int64_t)q.n * c.Ho + ho) * c.Wo + wo) * c.Co + ch0 + akk[h];
+        }
+        if (aok[h] && ok && k0 + akk[h] < ke) v = (unsigned)(off * 4);
+      } else {
+        const int64_t k = k0 + akk[h];    // the unit's pixel (output grid)
+        const Pix q = split_pix(k < ke ? k : 0, c.K, c.fd_w, c.fd_h);
+        const Tap& t4 = atap[h];
+        const int hi = q.a * c.sh + t4.kh - c.ph, wi = q.b * c.sw + t4.kw - c.pw;
+        const bool ok = aok[h] && k < ke && hi >= 0 && hi < c.H && wi >= 0 && wi < c.W;
+        if (ok) v = (unsigned)(((((int64_t)q.n * c.H + hi) * c.W + wi) * c.Ci + t4.ch) * 4);
+      }
+      issue(v, rsA, ldst + (unsigned)(h * HALF * 4), 0u);
+    }
+  };
+  auto dma_b = [&](int t) {
+    const int64_t k0 = kb0 + (int64_t)t * BK;
+    const unsigned ldst = lds0 + (unsigned)((t % NST) * STAGE * 4);
+    const unsigned soff = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(k0 * c.Nn * 4));
+#pragma unroll
+    for (int h = 0; h < NBH; ++h) {
+      const unsigned v = (bok[h] && k0 + bkk < ke) ? bvo[h] : kROOB;
+      issue(v, rsB, ldst + (unsigned)((2 + h) * HALF * 4), soff);
+    }
+  };
+  auto retire_keep = [](int tiles_in_flight) {   // all but the youngest tiles (NDMA DMAs each)
+    if (tiles_in_flight >= 2) {
+      if (NDMA == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else if (tiles_in_flight == 1) {
+      if (NDMA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // wgrad bias sums: column sums of B from the B fragments of group 0 in the first tile row
+  const bool do_cs = MODE == kWgrad && c.colsum_part != nullptr && tm == 0 && grp == 0 && wr == 0;
+  float cs[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) cs[j] = 0.f;
+
+  for (int t = 0; t < NST - 1; ++t)
+    if (t < nk) {
+      dma_a(t);
+      dma_b(t);
+    }
+  retire_keep(min(nk - 1, NST - 2));
+  bar();
+  if (grp == 1) bar();
+
+  // fragments: A rows grp * 128 + wr * (128 / WR) + i * 32 of half grp; B columns wc * (BN / WC) + j * 32
+  const int ar0 = wr * (128 / WR);
+  const int bh = (wc * (BN / WC)) / 128, bc0 = (wc * (BN / WC)) % 128;
+  auto fragA = [&](const float* img, int r0, int kb) -> v4f {
+    const int row = r0 + (lane & 31), h = lane >> 5;
+    if (AKC) return *reinterpret_cast<const v4f*>(img + row * BK + (((2 * kb + h) ^ ((row >> 2) & 3)) << 2));
+    const float* q = img + (8 * kb + 4 * h) * 128 + row;
+    return v4f{q[0], q[128], q[256], q[384]};
+  };
+  auto fragB = [&](const float* img, int r0, int kb) -> v4f {
+    const float* q = img + (8 * kb + 4 * (lane >> 5)) * 128 + r0 + (lane & 31);
+    return v4f{q[0], q[128], q[256], q[384]};
+  };
+  for (int kt = 0; kt < nk; ++kt) {
+    const float* S = smem + (kt % NST) * STAGE;
+    const float* As = S + grp * HALF;
+    const float* Bs = S + (2 + bh) * HALF;
+    const int tn_ = kt + NST - 1;
+#pragma unroll
+    for (int q = 0; q < BK / 8; ++q) {
+      v4f fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = fragA(As, ar0 + i * 32, q);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = fragB(Bs, bc0 + j * 32, q);
+      if (tn_ < nk) {
+        if (q == 0) dma_a(tn_);
+        else dma_b(tn_);
+      }
+      if (q == BK / 8 - 1) retire_keep(min(nk - 1 - (kt + 1), NST - 2));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bar();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][ss], fb[j][ss], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (do_cs) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) cs[j] += (fb[j][0] + fb[j][1]) + (fb[j][2] + fb[j][3]);
+      }
+      bar();
+    }
+  }
+  if (grp == 0) bar();
+
+  // ---- epilogue from the accumulators (32x32: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5))
+  const int lh = lane >> 5, lc = lane & 31;
+  const int64_t rbase = m0 + grp * 128 + ar0;
+  const int64_t cbase = n0 + bh * 128 + bc0;
+  if (MODE == kFwd && c.pool_w == 4 && !c.partial) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t col = cbase + j * 32 + lc;
+        if (col >= c.Nn) continue;
+        const float bv = c.bias ? c.bias[col] : 0.f;
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {
+          const int64_t row = rbase + i * 32 + 8 * rq + 4 * lh;
+          if (row >= c.M) continue;
+          float best = acc[i][j][4 * rq] + bv;
+          int arg = 0;
+#pragma unroll
+          for (int pp = 1; pp < 4; ++pp) {
+            const float v = acc[i][j][4 * rq + pp] + bv;
+            if (v > best || (v != v && best == best)) { best = v; arg = pp; }
+          }
+          c.out[(row >> 2) * c.Nn + col] = best;
+          c.pool_arg[(row >> 2) * c.Nn + col] = (uint8_t)arg;
+        }
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t col = cbase + j * 32 + lc;
+        if (col >= c.Nn) continue;
+        const float bv = (MODE == kFwd && c.bias && !c.partial) ? c.bias[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t row = rbase + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row >= c.M) continue;
+          if (c.partial) c.partial[((int64_t)split * c.M + row) * c.Nn + col] = acc[i][j][r];
+          else c.out[row * c.Nn + col] = acc[i][j][r] + bv;
+        }
+      }
+  }
+  if (do_cs) {   // lanes l and l + 32 hold the two k halves of column (l & 31)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float t = cs[j] + __shfl_xor(cs[j], 32);
+      const int64_t col = cbase + j * 32 + lc;
+      if (lane < 32 && col < c.Nn) c.colsum_part[(int64_t)split * c.Nn + col] = t;
+    }
+  }
+}
+
+// The ring conv when the shape qualifies (fp32 operands, option conv_ring, channel-aligned, stride 1
+// for the data gradient, 32-bit byte offsets); returns 1 if it did not run.
+template <int MODE>
+int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out, float** partial_out, int* splits_out) {
+  if (!g_opt_conv_ring || matmul_prec() != kPrecF32 || c.a16 || c.dy_arg) return 1;
+  const int chans = MODE == kDgrad ? c.Co : c.Ci;
+  if (MODE != kWgrad && chans % kRBK) return 1;
+  if (MODE == kWgrad && c.Ci % 4) return 1;
+  if (MODE == kDgrad && (c.sh != 1 || c.sw != 1)) return 1;
+  if (c.Nn % 4 || c.Nn < 128 || c.M < 256 || c.M >= INT32_MAX || c.K >= INT32_MAX) return 1;
+  const double xb = 4.0 * c.N * c.H * c.W * c.Ci, yb = 4.0 * c.N * c.Ho * c.Wo * c.Co, wb = 4.0 * c.K * c.Nn;
+  if (xb >= 2.1e9 || yb >= 2.1e9 || wb >= 2.1e9 || (MODE == kWgrad && 4.0 * c.K * c.Nn >= 2.1e9)) return 1;
+  const int BN = c.Nn >= 256 ? 256 : 128;
+  const int64_t tm = (c.M + 255) / 256, tn = (c.Nn + BN - 1) / BN;
+  const int splits0 = choose_splits(tm * tn, c.K, kRBK, kCUs, MODE == kWgrad ? 256 : 16);
+  c.kchunk = splits0 > 1 ? ((c.K + splits0 - 1) / splits0 + kRBK - 1) / kRBK * kRBK : std::max<int64_t>(c.K, 1);
+  const int splits = splits0 > 1 ? (int)((c.K + c.kchunk - 1) / c.kchunk) : 1;
+  c.tiles_m = (int)tm;
+  c.tiles_n = (int)tn;
+  c.tiles = (int)(tm * tn);
+  c.nblk = c.tiles * splits;
+  c.group_m = std::max(1, (int)std::lround(std::sqrt(32.0 * BN / 256.0)));
+  c.partial = nullptr;
+  if (splits > 1) {
+    if (int rc = conv_scratch((size_t)splits * c.M * c.Nn, &c.partial)) return rc;
+  }
+  c.colsum_part = nullptr;
+  if (MODE == kWgrad && c.db) {
+    if (int rc = conv_scratch((size_t)splits * c.Nn, &c.colsum_part, g_csb)) return rc;
+  }
+  c.fd_w = FastDiv((unsigned)(MODE == kDgrad ? c.W : c.Wo));
+  c.fd_h = FastDiv((unsigned)(MODE == kDgrad ? c.H : c.Ho));
+  c.fd_c = FastDiv((unsigned)chans);
+  c.fd_kw = FastDiv((unsigned)c.KW);
+  ProfScope prof(name, s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
+  prof.detail("conv_ring_kernel<%s,256x%d%s> %lldx%lldx%lld s%d", MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad",
+              BN, (MODE == kFwd && c.pool_w) ? ",pool" : "", (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
+  if (BN == 256) hipLaunchKernelGGL((conv_ring_kernel<MODE, 256>), dim3((unsigned)c.nblk), dim3(512), 0, s, c);
+  else hipLaunchKernelGGL((conv_ring_kernel<MODE, 128>), dim3((unsigned)c.nblk), dim3(512), 0, s, c);
+  SRK_CHECK_HIP(hipGetLastError());
+  *partial_out = c.partial;
+  *splits_out = splits;
+  (void)final_out;
+  return 0;
+}
+
 template <int MODE>
 int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
+  {
+    ConvArgs r = c;
+    float* partial = nullptr;
+    int splits = 1;
+    const int rc = try_conv_ring<MODE>(r, s, name, c.out, &partial, &splits);
+    if (rc == 0) {
+      if (splits > 1) {   // slab reduction (+ bias), then the pooled output / bias sums as below
+        const bool pool = MODE == kFwd && c.pool_w;
+        float* dense = c.out;
+        if (pool && (rc == 0)) {
+          if (int e = conv_scratch((size_t)c.M * c.Nn, &dense, g_csd)) return e;
+        }
+        const int64_t n = c.M * c.Nn;
+        hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, partial, splits, n,
+                           c.Nn, MODE == kFwd ? c.bias : nullptr, dense);
+        if (pool) {
+          const int64_t rows = c.M / c.pool_w;
+          hipLaunchKernelGGL(maxpool_arg_kernel, dim3((unsigned)((rows * c.Nn + 255) / 256)), dim3(256), 0, s, dense,
+                             rows, (int)c.Nn, c.pool_w, c.out, c.pool_arg);
+        }
+        SRK_CHECK_HIP(hipGetLastError());
+      }
+      if (r.colsum_part) {
+        hipLaunchKernelGGL(colsum_splits_kernel, dim3((unsigned)((c.Nn + 255) / 256)), dim3(256), 0, s, r.colsum_part,
+                           splits, c.Nn, c.db);
+        SRK_CHECK_HIP(hipGetLastError());
+      }
+      return SRK_OK;
+    }
+    if (rc != 1) return rc;
+  }
   const int prec = matmul_prec();
   const int BK = prec == kPrecF32 ? 32 : 64;   // 16-bit: 64-deep k-tiles (4 MFMA k-steps per barrier)
   // tile: 128 x 128 unless the GEMM is narrow (N <= 64: 128 x 64) or small (64 x 64); srk option

@@ -25,6 +25,7 @@ int g_opt_conv16_sources = 1;
 int g_opt_conv_fused_db = 1;
 int g_opt_conv_unpool_gather = 1;
 int g_opt_conv_tile = 128;
+int g_opt_conv_ring = 0;
 int g_opt_mfcc_variant = 0;
 int g_opt_gemm_streamk = 0;
 int g_opt_gemm16_persistent = 0;
@@ -370,6 +371,10 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "mfcc_variant") {   // K1: bit 0 DPP untangle exchange, bit 1 twiddles in registers (bitwise the same)
     SRK_REQUIRE(value >= 0 && value <= 3, SRK_ERR_INVALID, "mfcc_variant must be 0..3");
     srk::g_opt_mfcc_variant = (int)value;
+    return SRK_OK;
+  }
+  if (n == "conv_ring") {   // fp32 convs on the LDS-DMA ring kernel where the shape qualifies (1) or not (0)
+    srk::g_opt_conv_ring = value != 0;
     return SRK_OK;
   }
   if (n == "conv_tile") {   // 128: 128-row conv tiles (4 waves); 256: 256-row tiles (8 waves) on tall convs

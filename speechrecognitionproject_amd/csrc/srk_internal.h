@@ -107,6 +107,8 @@ extern int g_opt_conv_unpool_gather;
 // conv tile shape ("conv_tile": 128 = 128-row tiles of 4 waves, 256 = 256-row tiles of 8 waves on
 // tall convolutions)
 extern int g_opt_conv_tile;
+// fp32 LDS-DMA ring implicit-GEMM convolutions where the shape qualifies ("conv_ring")
+extern int g_opt_conv_ring;
 // K1 MFCC variant ("mfcc_variant", bitwise-identical outputs): bit 0 = the untangle's partner exchange
 // by DPP row_mirror instead of ds_bpermute, bit 1 = twiddles in registers instead of LDS
 extern int g_opt_mfcc_variant;

@@ -63,6 +63,21 @@ def test_conv2d_tile256_vs_torch(gpu, shape):
         _lib.set_option("conv_tile", 128)
 
 
+@pytest.mark.parametrize("shape", [(2, 98, 40, 64, 128, 1, 7, 0, 3), (3, 98, 1, 256, 512, 7, 1, 3, 0),
+                                   (2, 98, 10, 128, 256, 1, 10, 0, 0), (4, 17, 13, 32, 128, 3, 3, 1, 1),
+                                   (2, 1, 1000, 64, 128, 1, 15, 0, 7, 1, 2), (24, 98, 40, 64, 128, 1, 7, 0, 3)])
+def test_conv2d_ring_vs_torch(gpu, shape):
+    """srk option conv_ring: the fp32 LDS-DMA ring implicit GEMM (gemm_p32_kernel's structure with
+    per-K-tile conv gathers, direct epilogue, fused bias sums) wherever the shape qualifies (channel
+    counts % 16, >= 128 output columns, stride 1 for the data gradient); the rest as before."""
+    from speechrecognitionproject_amd import _lib
+    try:
+        _lib.set_option("conv_ring", 1)
+        _check_conv(*shape)
+    finally:
+        _lib.set_option("conv_ring", 0)
+
+
 @pytest.mark.parametrize("shape", [  # 1-D strided convs of model_resnet_bgru.py:48,19-23 as H=1
     (2, 1, 16000, 1, 64, 1, 80, 0, 38, 1, 16), (2, 1, 1000, 64, 128, 1, 15, 0, 7, 1, 2),
     (2, 1, 1000, 64, 128, 1, 1, 0, 0, 1, 2), (3, 1, 125, 512, 512, 1, 15, 0, 7, 1, 1)])
@@ -117,8 +132,8 @@ def test_conv1_pool_fused_vs_torch(gpu, N, H, W, KH, KW, pool):
     (2, 3, 8, 128, 64, 1, 7, 0, 3),        # a few rows, deep k: the split-K forward (dense, then pooled)
     (3, 5, 12, 8, 36, 3, 3, 1, 1),         # 3 x 3 taps, N not a tile multiple
 ])
-@pytest.mark.parametrize("gather", [1, 0])
-def test_conv_pool_fused_equals_separate(gpu, gather, precision, N, H, W, Ci, Co, KH, KW, ph, pw):
+@pytest.mark.parametrize("gather,ring", [(1, 0), (0, 0), (1, 1)])
+def test_conv_pool_fused_equals_separate(gpu, gather, ring, precision, N, H, W, Ci, Co, KH, KW, ph, pw):
     """conv + bias + MaxPool2d((1, 4)) in one launch (srk_conv2d_nhwc_fwd_pool: pooled epilogue and
     uint8 argmax; the backward unpools through the argmax) == the separate conv and maxpool kernels
     (bitwise: the same accumulators, the same first-maximum rule, the same gradient kernels), and
@@ -137,6 +152,7 @@ def test_conv_pool_fused_equals_separate(gpu, gather, precision, N, H, W, Ci, Co
     try:
         _lib.set_matmul_precision(precision)
         _lib.set_option("conv_unpool_gather", gather)
+        _lib.set_option("conv_ring", ring)
         for fused in (True, False):
             _lib.set_fused_conv_pool(fused)
             with torch.no_grad():
@@ -150,6 +166,7 @@ def test_conv_pool_fused_equals_separate(gpu, gather, precision, N, H, W, Ci, Co
             outs.append([t.detach().cpu() for t in (y, xm.grad, conv.weight.grad, conv.bias.grad)])
     finally:
         _lib.set_option("conv_unpool_gather", 1)
+        _lib.set_option("conv_ring", 0)
         _lib.set_fused_conv_pool(True)
         _lib.set_matmul_precision("fp32")
     for a, c in zip(*outs):

@@ -18,8 +18,9 @@ done
 for pers in 0 1; do
   SRK_OPTIONS=gemm16_persistent=$pers timeout -k 10 120 python tools/gemm_bench.py --precision bf16 --h16 > "$OUT/gemm_bf16_pers$pers.txt" 2>&1 || exit 1
 done
-for t in 128 256; do
-  SRK_OPTIONS=conv_tile=$t timeout -k 10 200 python bench.py --model fbanks_cnn --no-lowprec --no-cpu-baseline \
+for t in 128 256 ring; do
+  opt="conv_tile=$t"; [ $t = ring ] && opt="conv_ring=1"
+  SRK_OPTIONS=$opt timeout -k 10 200 python bench.py --model fbanks_cnn --no-lowprec --no-cpu-baseline \
     --no-feature-roofline --steps 10 > "$OUT/cfg3_tile$t.json" 2> "$OUT/cfg3_tile$t.err" || exit 1
 done
 for v in 0 1 2 3 0 1 2 3; do
@@ -29,9 +30,9 @@ tail -n 12 "$OUT"/gemm_*.txt
 tail -n 2 "$OUT"/mfcc_var*.txt
 python - "$OUT" <<'PY'
 import json, sys
-for t in (128, 256):
-    r = json.loads(open("%s/cfg3_tile%d.json" % (sys.argv[1], t)).read().strip().splitlines()[-1])
-    print("cfg3 conv_tile=%d: %.1f utt/s, %.3f ms/step" % (t, r["value"], r["ms_per_step"]))
+for t in (128, 256, "ring"):
+    r = json.loads(open("%s/cfg3_tile%s.json" % (sys.argv[1], t)).read().strip().splitlines()[-1])
+    print("cfg3 conv %s: %.1f utt/s, %.3f ms/step" % (t, r["value"], r["ms_per_step"]))
     for k in r["roofline"]["top_kernels"]:
         print("   ", k)
 PY

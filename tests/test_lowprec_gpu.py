@@ -292,7 +292,10 @@ CONV_S16 = [  # 8-aligned channel counts: the pre-rounded 16-bit source path (op
 @pytest.mark.parametrize("shape", CONV_S16)
 def test_conv_16bit_sources_bit_identical(prec, shape):
     """bf16 / fp16 convs gathering from the pre-rounded 16-bit copy (conv16_sources = 1) give the
-    SAME bits as rounding the fp32 gathers at LDS-store time (0): same rounding, same MFMA order."""
+    SAME bits as rounding the fp32 gathers at LDS-store time (0): same rounding, same MFMA order.
+    The bias gradient is the exception by design: the fp32-gather path sums it inside the
+    weight-gradient kernel (conv_fused_db), the 16-bit-source path with the column-sum kernel — the
+    same fp32 values in another order (1e-5)."""
     from speechrecognitionproject_amd import nn as snn
     N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw = shape
     g = torch.Generator().manual_seed(N * 31 + Co + KW)
@@ -316,8 +319,10 @@ def test_conv_16bit_sources_bit_identical(prec, shape):
     finally:
         _lib.set_option("conv16_sources", 1)
         _lib.prof_enable(0)
-    for a, c in zip(*outs):
+    for a, c in zip(outs[0][:3], outs[1][:3]):
         assert torch.equal(a, c)
+    db0, db1 = outs[0][3].double(), outs[1][3].double()
+    assert ((db0 - db1).abs().max() / db1.abs().max()).item() <= 1e-5
 
 
 @pytest.mark.parametrize("shape", CONV_S16[:4])

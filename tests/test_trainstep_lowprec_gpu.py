@@ -168,6 +168,7 @@ def test_fp16_overflow_skips_the_step(gpu):
     try:
         _lib.set_matmul_precision("fp16")
         scaler = LossScaler(3e38, dynamic=True)          # the scaled loss overflows to inf
+        opt.sync_lr()                                     # (the step writes lr into state_dev first)
         snap = (flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), opt.state_dev.clone())
         _small_step(net, opt, scaler, x, lab)
         torch.cuda.synchronize()

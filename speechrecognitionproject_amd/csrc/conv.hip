@@ -1092,7 +1092,7 @@ __global__ __launch_bounds__(512, 1) void conv_ring_kernel(ConvArgs c) {
 // for the data gradient, 32-bit byte offsets); returns 1 if it did not run.
 template <int MODE>
 int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out, float** partial_out, int* splits_out) {
-  if (!g_opt_conv_ring || matmul_prec() != kPrecF32 || c.a16 || c.dy_arg) return 1;
+  if (!(g_opt_conv_ring & (1 << MODE)) || matmul_prec() != kPrecF32 || c.a16 || c.dy_arg) return 1;
   const int chans = MODE == kDgrad ? c.Co : c.Ci;
   if (MODE != kWgrad && chans % kRBK) return 1;
   if (MODE == kWgrad && c.Ci % 4) return 1;

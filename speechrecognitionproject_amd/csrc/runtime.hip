@@ -25,9 +25,9 @@ int g_opt_conv16_sources = 1;
 int g_opt_conv_fused_db = 1;
 int g_opt_conv_unpool_gather = 1;
 int g_opt_conv_tile = 128;
-int g_opt_conv_ring = 0;
-int g_opt_mfcc_variant = 0;
-int g_opt_gemm_streamk = 0;
+int g_opt_conv_ring = 6;
+int g_opt_mfcc_variant = 3;
+int g_opt_gemm_streamk = 1;
 int g_opt_gemm16_persistent = 0;
 int g_opt_gemm32_kernel = 0;
 static std::atomic<int> g_opt_matmul_prec{kPrecF32};
@@ -373,8 +373,9 @@ int srk_set_option(const char* name, int64_t value) {
     srk::g_opt_mfcc_variant = (int)value;
     return SRK_OK;
   }
-  if (n == "conv_ring") {   // fp32 convs on the LDS-DMA ring kernel where the shape qualifies (1) or not (0)
-    srk::g_opt_conv_ring = value != 0;
+  if (n == "conv_ring") {   // fp32 convs on the LDS-DMA ring kernel where the shape qualifies: bit 0 fwd, 1 dgrad, 2 wgrad
+    SRK_REQUIRE(value >= 0 && value <= 7, SRK_ERR_INVALID, "conv_ring is a mask of 1 (fwd), 2 (dgrad), 4 (wgrad)");
+    srk::g_opt_conv_ring = (int)value;
     return SRK_OK;
   }
   if (n == "conv_tile") {   // 128: 128-row conv tiles (4 waves); 256: 256-row tiles (8 waves) on tall convs

@@ -107,12 +107,14 @@ extern int g_opt_conv_unpool_gather;
 // conv tile shape ("conv_tile": 128 = 128-row tiles of 4 waves, 256 = 256-row tiles of 8 waves on
 // tall convolutions)
 extern int g_opt_conv_tile;
-// fp32 LDS-DMA ring implicit-GEMM convolutions where the shape qualifies ("conv_ring")
+// fp32 LDS-DMA ring implicit-GEMM convolutions where the shape qualifies ("conv_ring": a mask of
+// 1 = forward, 2 = data gradient, 4 = weight gradient; default 6 — measured, r04ab)
 extern int g_opt_conv_ring;
 // K1 MFCC variant ("mfcc_variant", bitwise-identical outputs): bit 0 = the untangle's partner exchange
-// by DPP row_mirror instead of ds_bpermute, bit 1 = twiddles in registers instead of LDS
+// by DPP row_mirror instead of ds_bpermute, bit 1 = twiddles in registers instead of LDS (default 3)
 extern int g_opt_mfcc_variant;
-// stream-K for fp32 ping-pong GEMMs whose 256 x 256 grid covers 1/2 .. 1 round of CUs ("gemm_streamk")
+// stream-K for fp32 ping-pong GEMMs whose 256 x 256 grid covers 1/2 .. 1 round of CUs ("gemm_streamk",
+// default 1)
 extern int g_opt_gemm_streamk;
 // persistent tile loop with direct-store epilogue for the 16-bit ping-pong GEMM ("gemm16_persistent")
 extern int g_opt_gemm16_persistent;

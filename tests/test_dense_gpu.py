@@ -465,7 +465,7 @@ def test_gemm_streamk(gpu, M, N, K, ta, beta, bias):
                  ptr(bd) if bias else None, bias, stream_ptr())
             outs.append(Cd.cpu().double())
     finally:
-        _lib.set_option("gemm_streamk", 0)
+        _lib.set_option("gemm_streamk", 1)
     tol = 1e-5 * (1 + (A.abs().max() * B.abs().max() * K).item())
     assert (outs[0] - ref).abs().max() <= tol
     assert (outs[0] - outs[1]).abs().max() <= tol

@@ -1088,22 +1088,272 @@ __global__ __launch_bounds__(512, 1) void conv_ring_kernel(ConvArgs c) {
   }
 }
 
+// 16-bit form of the ring conv (bf16 / fp16 matmul precision with the 16-bit operand copies of the
+// S16 path): gemm_g16_kernel's structure — 32-deep K-tiles of 16-bit units (8 elements = 16 B), KC
+// images [128 rows][4 units] read by ds_read_b128, TR images [32 k][16 units] read by
+// ds_read_b64_tr_b16, v_mfma_f32_32x32x16_{bf16,f16} — with the same per-K-tile conv gathers (the
+// gathered operand's channel count a multiple of 32: a K-tile inside one tap).
+constexpr int kR16BK = 32;
+template <bool KC>
+__device__ __forceinline__ int r16_off(int row, int k) {
+  if (KC) return row * kR16BK + ((((k >> 3) ^ ((row >> 2) & 3))) << 3) + (k & 7);
+  return k * 128 + ((((row >> 3) ^ ((k & 3) << 2))) << 3) + (row & 7);
+}
+template <bool KC>
+__device__ __forceinline__ u32x4_ r16_frag(const unsigned short* img, int r0, int kk, int lane) {
+  if (KC) return *reinterpret_cast<const u32x4_*>(img + r16_off<true>(r0 + (lane & 31), kk + 8 * (lane >> 5)));
+  const int q = (lane >> 2) & 3, pp = lane & 3;
+  const int k = kk + 8 * (lane >> 5) + q, row = r0 + 16 * ((lane >> 4) & 1) + 4 * pp;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + r16_off<false>(row, k)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + r16_off<false>(row, k + 4)));
+  const u32x2_ l2 = __builtin_bit_cast(u32x2_, lo), h2 = __builtin_bit_cast(u32x2_, hi);
+  return u32x4_{l2.x, l2.y, h2.x, h2.y};
+}
+
+template <int MODE, int BN, int LP>
+__global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
+  constexpr int BK = kR16BK, NST = 4;
+  constexpr bool AKC = MODE != kWgrad;
+  constexpr int HALF = 128 * BK;                     // 8 KB of 16-bit elements per half image
+  constexpr int NBH = BN / 128;
+  constexpr int STAGE = (2 + NBH) * HALF;
+  constexpr int NDMA = 2 + NBH;
+  constexpr int WR = BN == 256 ? 1 : 2, WC = 4 / WR;
+  constexpr int TM = 128 / WR / 32, TN = BN / WC / 32;
+  __shared__ __attribute__((aligned(1024))) unsigned short smem[NST * STAGE];
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+  auto bar = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = wave >> 2, w4 = wave & 3;
+  const int wr = w4 / WC, wc = w4 % WC;
+  int split, tm, tn;
+  map_tile(c.nblk, c.tiles, c.tiles_m, c.tiles_n, c.group_m, true, split, tm, tn);
+  const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * BN;
+  const int64_t kb0 = split * c.kchunk;
+  const int64_t ke = (kb0 + c.kchunk < c.K) ? kb0 + c.kchunk : c.K;
+  const int nk = ke > kb0 ? (int)((ke - kb0 + BK - 1) / BK) : 0;
+  auto rsrc = [](const unsigned short* p) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    return u32x4s{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)a),
+                  (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)), 0x7ffffff0u, 0x00020000u};
+  };
+  const u32x4s rsA = rsrc(c.a16), rsB = rsrc(c.b16);
+  const int chans = MODE == kDgrad ? c.Co : c.Ci;
+
+  const int p = wave * 64 + lane;
+  int arow[2], akk[2];
+  Pix apix[2];
+  Tap atap[2];
+  bool aok[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (AKC) {   // p = row * 4 + slot: 8 k at 8 (slot ^ swz(row))
+      arow[h] = p >> 2;
+      akk[h] = ((p & 3) ^ ((arow[h] >> 2) & 3)) * 8;
+      apix[h] = split_pix(m0 + h * 128 + arow[h], c.M, c.fd_w, c.fd_h);
+      aok[h] = apix[h].ok;
+    } else {     // p = k * 16 + slot: rows 8 (slot ^ ((k & 3) << 2)) .. +8
+      akk[h] = p >> 4;
+      arow[h] = ((p & 15) ^ ((akk[h] & 3) << 2)) * 8;
+      const int64_t m = m0 + h * 128 + arow[h];
+      aok[h] = m < c.M;
+      atap[h] = split_tap(aok[h] ? m : 0, c.fd_c, c.fd_kw);
+    }
+  }
+  unsigned bvo[NBH];
+  bool bok[NBH];
+  const int bkk = p >> 4;
+#pragma unroll
+  for (int h = 0; h < NBH; ++h) {
+    const int64_t n = n0 + h * 128 + ((p & 15) ^ ((bkk & 3) << 2)) * 8;
+    bok[h] = n < c.Nn;
+    bvo[h] = (unsigned)(((int64_t)bkk * c.Nn + (bok[h] ? n : 0)) * 2);
+  }
+  const unsigned lds0 =
+      (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ptr)smem + (unsigned)wave * 1024u);
+  auto issue = [&](unsigned v, const u32x4s& rs, unsigned ldsa, unsigned soff) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(v), "s"(rs), "s"(ldsa), "s"(soff)
+                 : "memory");
+  };
+  auto dma_a = [&](int t) {
+    const int64_t k0 = kb0 + (int64_t)t * BK;
+    const unsigned ldst = lds0 + (unsigned)((t % NST) * STAGE * 2);
+    const unsigned tap = AKC ? (unsigned)__builtin_amdgcn_readfirstlane(c.fd_c.div((unsigned)k0)) : 0u;
+    const int ch0 = (int)((unsigned)k0 - tap * (unsigned)chans);
+    const int kh = (int)c.fd_kw.div(tap), kw = (int)(tap - (unsigned)kh * c.KW);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      unsigned v = kROOB;
+      if (AKC) {
+        const Pix& q = apix[h];
+        int64_t off;
+        bool ok;
+        if (MODE == kFwd) {
+          const int hi = q.a * c.sh + kh - c.ph, wi = q.b * c.sw + kw - c.pw;
+          ok = hi >= 0 && hi < c.H && wi >= 0 && wi < c.W;
+          off = (((int64_t)q.n * c.H + hi) * c.W + wi) * c.Ci + ch0 + akk[h];
+        } else {
+          const int ho = q.a + c.ph - kh, wo = q.b + c.pw - kw;
+          ok = ho >= 0 && ho < c.Ho && wo >= 0 && wo < c.Wo;
+          off = (((int64_t)q.n * c.Ho + ho) * c.Wo + wo) * c.Co + ch0 + akk[h];
+        }
+        if (aok[h] && ok && k0 + akk[h] < ke) v = (unsigned)(off * 2);
+      } else {
+        const int64_t k = k0 + akk[h];
+        const Pix q = split_pix(k < ke ? k : 0, c.K, c.fd_w, c.fd_h);
+        const Tap& t4 = atap[h];
+        const int hi = q.a * c.sh + t4.kh - c.ph, wi = q.b * c.sw + t4.kw - c.pw;
+        const bool ok = aok[h] && k < ke && hi >= 0 && hi < c.H && wi >= 0 && wi < c.W;
+        if (ok) v = (unsigned)(((((int64_t)q.n * c.H + hi) * c.W + wi) * c.Ci + t4.ch) * 2);
+      }
+      issue(v, rsA, ldst + (unsigned)(h * HALF * 2), 0u);
+    }
+  };
+  auto dma_b = [&](int t) {
+    const int64_t k0 = kb0 + (int64_t)t * BK;
+    const unsigned ldst = lds0 + (unsigned)((t % NST) * STAGE * 2);
+    const unsigned soff = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(k0 * c.Nn * 2));
+#pragma unroll
+    for (int h = 0; h < NBH; ++h) {
+      const unsigned v = (bok[h] && k0 + bkk < ke) ? bvo[h] : kROOB;
+      issue(v, rsB, ldst + (unsigned)((2 + h) * HALF * 2), soff);
+    }
+  };
+  auto retire_keep = [](int tiles_in_flight) {
+    if (tiles_in_flight >= 2) {
+      if (NDMA == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else if (tiles_in_flight == 1) {
+      if (NDMA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  for (int t = 0; t < NST - 1; ++t)
+    if (t < nk) {
+      dma_a(t);
+      dma_b(t);
+    }
+  retire_keep(min(nk - 1, NST - 2));
+  bar();
+  if (grp == 1) bar();
+
+  const int ar0 = wr * (128 / WR);
+  const int bh = (wc * (BN / WC)) / 128, bc0 = (wc * (BN / WC)) % 128;
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned short* S = smem + (kt % NST) * STAGE;
+    const unsigned short* As = S + grp * HALF;
+    const unsigned short* Bs = S + (2 + bh) * HALF;
+    const int tn_ = kt + NST - 1;
+#pragma unroll
+    for (int q = 0; q < BK / 16; ++q) {
+      u32x4_ fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = r16_frag<AKC>(As, ar0 + i * 32, 16 * q, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = r16_frag<false>(Bs, bc0 + j * 32, 16 * q, lane);
+      if (tn_ < nk) {
+        if (q == 0) dma_a(tn_);
+        else dma_b(tn_);
+      }
+      if (q == BK / 16 - 1) retire_keep(min(nk - 1 - (kt + 1), NST - 2));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bar();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = ConvLp<LP>::mma(fa[i], fb[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+    }
+  }
+  if (grp == 0) bar();
+
+  const int lh = lane >> 5, lc = lane & 31;
+  const int64_t rbase = m0 + grp * 128 + ar0;
+  const int64_t cbase = n0 + bh * 128 + bc0;
+  if (MODE == kFwd && c.pool_w == 4 && !c.partial) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t col = cbase + j * 32 + lc;
+        if (col >= c.Nn) continue;
+        const float bv = c.bias ? c.bias[col] : 0.f;
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {
+          const int64_t row = rbase + i * 32 + 8 * rq + 4 * lh;
+          if (row >= c.M) continue;
+          float best = acc[i][j][4 * rq] + bv;
+          int arg = 0;
+#pragma unroll
+          for (int pp = 1; pp < 4; ++pp) {
+            const float v = acc[i][j][4 * rq + pp] + bv;
+            if (v > best || (v != v && best == best)) { best = v; arg = pp; }
+          }
+          c.out[(row >> 2) * c.Nn + col] = best;
+          c.pool_arg[(row >> 2) * c.Nn + col] = (uint8_t)arg;
+        }
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t col = cbase + j * 32 + lc;
+        if (col >= c.Nn) continue;
+        const float bv = (MODE == kFwd && c.bias && !c.partial) ? c.bias[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t row = rbase + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row >= c.M) continue;
+          if (c.partial) c.partial[((int64_t)split * c.M + row) * c.Nn + col] = acc[i][j][r];
+          else c.out[row * c.Nn + col] = acc[i][j][r] + bv;
+        }
+      }
+  }
+}
+
 // The ring conv when the shape qualifies (fp32 operands, option conv_ring, channel-aligned, stride 1
 // for the data gradient, 32-bit byte offsets); returns 1 if it did not run.
 template <int MODE>
 int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out, float** partial_out, int* splits_out) {
-  if (!(g_opt_conv_ring & (1 << MODE)) || matmul_prec() != kPrecF32 || c.a16 || c.dy_arg) return 1;
+  const int prec = matmul_prec();
+  const bool lp = prec != kPrecF32;
+  // fp32 operands (option bits 0..2), or the 16-bit operand copies of the S16 path (bits 4..6)
+  if (!(g_opt_conv_ring & (1 << (MODE + (lp ? 4 : 0)))) || c.dy_arg || (lp != (c.a16 != nullptr))) return 1;
+  const int RBK = lp ? kR16BK : kRBK, unit = lp ? 8 : 4, esz = lp ? 2 : 4;
   const int chans = MODE == kDgrad ? c.Co : c.Ci;
-  if (MODE != kWgrad && chans % kRBK) return 1;
-  if (MODE == kWgrad && c.Ci % 4) return 1;
+  if (MODE != kWgrad && chans % RBK) return 1;
+  if (MODE == kWgrad && c.Ci % unit) return 1;
   if (MODE == kDgrad && (c.sh != 1 || c.sw != 1)) return 1;
-  if (c.Nn % 4 || c.Nn < 128 || c.M < 256 || c.M >= INT32_MAX || c.K >= INT32_MAX) return 1;
-  const double xb = 4.0 * c.N * c.H * c.W * c.Ci, yb = 4.0 * c.N * c.Ho * c.Wo * c.Co, wb = 4.0 * c.K * c.Nn;
-  if (xb >= 2.1e9 || yb >= 2.1e9 || wb >= 2.1e9 || (MODE == kWgrad && 4.0 * c.K * c.Nn >= 2.1e9)) return 1;
+  if (c.Nn % unit || c.Nn < 128 || c.M < 256 || c.M >= INT32_MAX || c.K >= INT32_MAX) return 1;
+  const double xb = (double)esz * c.N * c.H * c.W * c.Ci, yb = (double)esz * c.N * c.Ho * c.Wo * c.Co,
+               wb = (double)esz * c.K * c.Nn;
+  if (xb >= 2.1e9 || yb >= 2.1e9 || wb >= 2.1e9) return 1;
   const int BN = c.Nn >= 256 ? 256 : 128;
   const int64_t tm = (c.M + 255) / 256, tn = (c.Nn + BN - 1) / BN;
-  const int splits0 = choose_splits(tm * tn, c.K, kRBK, kCUs, MODE == kWgrad ? 256 : 16);
-  c.kchunk = splits0 > 1 ? ((c.K + splits0 - 1) / splits0 + kRBK - 1) / kRBK * kRBK : std::max<int64_t>(c.K, 1);
+  const int splits0 = choose_splits(tm * tn, c.K, RBK, kCUs, MODE == kWgrad ? 256 : 16);
+  c.kchunk = splits0 > 1 ? ((c.K + splits0 - 1) / splits0 + RBK - 1) / RBK * RBK : std::max<int64_t>(c.K, 1);
   const int splits = splits0 > 1 ? (int)((c.K + c.kchunk - 1) / c.kchunk) : 1;
   c.tiles_m = (int)tm;
   c.tiles_n = (int)tn;
@@ -1115,18 +1365,29 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
     if (int rc = conv_scratch((size_t)splits * c.M * c.Nn, &c.partial)) return rc;
   }
   c.colsum_part = nullptr;
-  if (MODE == kWgrad && c.db) {
+  if (MODE == kWgrad && c.db && !lp) {   // the 16-bit path keeps the column-sum kernel (fp32 dY)
     if (int rc = conv_scratch((size_t)splits * c.Nn, &c.colsum_part, g_csb)) return rc;
   }
   c.fd_w = FastDiv((unsigned)(MODE == kDgrad ? c.W : c.Wo));
   c.fd_h = FastDiv((unsigned)(MODE == kDgrad ? c.H : c.Ho));
   c.fd_c = FastDiv((unsigned)chans);
   c.fd_kw = FastDiv((unsigned)c.KW);
-  ProfScope prof(name, s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
-  prof.detail("conv_ring_kernel<%s,256x%d%s> %lldx%lldx%lld s%d", MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad",
-              BN, (MODE == kFwd && c.pool_w) ? ",pool" : "", (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
-  if (BN == 256) hipLaunchKernelGGL((conv_ring_kernel<MODE, 256>), dim3((unsigned)c.nblk), dim3(512), 0, s, c);
-  else hipLaunchKernelGGL((conv_ring_kernel<MODE, 128>), dim3((unsigned)c.nblk), dim3(512), 0, s, c);
+  ProfScope prof(lp ? (MODE == kFwd ? "conv_fwd_lp" : MODE == kDgrad ? "conv_dgrad_lp" : "conv_wgrad_lp") : name, s,
+                 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
+  prof.detail("conv_ring%s_kernel<%s,256x%d%s> %lldx%lldx%lld s%d", lp ? "16" : "",
+              MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad", BN, (MODE == kFwd && c.pool_w) ? ",pool" : "",
+              (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
+  const dim3 grid((unsigned)c.nblk), block(512);
+  if (!lp) {
+    if (BN == 256) hipLaunchKernelGGL((conv_ring_kernel<MODE, 256>), grid, block, 0, s, c);
+    else hipLaunchKernelGGL((conv_ring_kernel<MODE, 128>), grid, block, 0, s, c);
+  } else if (prec == kPrecBF16) {
+    if (BN == 256) hipLaunchKernelGGL((conv_ring16_kernel<MODE, 256, 1>), grid, block, 0, s, c);
+    else hipLaunchKernelGGL((conv_ring16_kernel<MODE, 128, 1>), grid, block, 0, s, c);
+  } else {
+    if (BN == 256) hipLaunchKernelGGL((conv_ring16_kernel<MODE, 256, 2>), grid, block, 0, s, c);
+    else hipLaunchKernelGGL((conv_ring16_kernel<MODE, 128, 2>), grid, block, 0, s, c);
+  }
   SRK_CHECK_HIP(hipGetLastError());
   *partial_out = c.partial;
   *splits_out = splits;

@@ -373,8 +373,9 @@ int srk_set_option(const char* name, int64_t value) {
     srk::g_opt_mfcc_variant = (int)value;
     return SRK_OK;
   }
-  if (n == "conv_ring") {   // fp32 convs on the LDS-DMA ring kernel where the shape qualifies: bit 0 fwd, 1 dgrad, 2 wgrad
-    SRK_REQUIRE(value >= 0 && value <= 7, SRK_ERR_INVALID, "conv_ring is a mask of 1 (fwd), 2 (dgrad), 4 (wgrad)");
+  if (n == "conv_ring") {   // ring conv kernels where the shape qualifies: bits 0-2 fp32 fwd / dgrad / wgrad, 4-6 16-bit
+    SRK_REQUIRE(value >= 0 && value <= 0x77, SRK_ERR_INVALID,
+                "conv_ring is a mask of 1 / 2 / 4 (fp32 fwd / dgrad / wgrad) and 16 / 32 / 64 (16-bit)");
     srk::g_opt_conv_ring = (int)value;
     return SRK_OK;
   }

@@ -107,8 +107,9 @@ extern int g_opt_conv_unpool_gather;
 // conv tile shape ("conv_tile": 128 = 128-row tiles of 4 waves, 256 = 256-row tiles of 8 waves on
 // tall convolutions)
 extern int g_opt_conv_tile;
-// fp32 LDS-DMA ring implicit-GEMM convolutions where the shape qualifies ("conv_ring": a mask of
-// 1 = forward, 2 = data gradient, 4 = weight gradient; default 6 — measured, r04ab)
+// LDS-DMA ring implicit-GEMM convolutions where the shape qualifies ("conv_ring": a mask of
+// 1 / 2 / 4 = fp32 forward / data gradient / weight gradient, 16 / 32 / 64 = the same on 16-bit
+// operands; default 6 — measured, r04ab)
 extern int g_opt_conv_ring;
 // K1 MFCC variant ("mfcc_variant", bitwise-identical outputs): bit 0 = the untangle's partner exchange
 // by DPP row_mirror instead of ds_bpermute, bit 1 = twiddles in registers instead of LDS (default 3)

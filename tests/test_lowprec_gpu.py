@@ -558,3 +558,33 @@ def test_gemm16_persistent(prec, ta, tb, M, N, K, beta):
     scale = (opA.abs() @ opB.abs()).max().item()
     assert (outs[0] - ref).abs().max().item() <= 2e-6 * (1 + scale)
     assert (outs[0] - outs[1]).abs().max().item() <= 1e-6 * (1 + scale)
+
+
+@pytest.mark.parametrize("shape", [(2, 98, 40, 64, 128, 1, 7, 0, 3), (3, 98, 1, 256, 512, 7, 1, 3, 0),
+                                   (2, 1, 1000, 64, 128, 1, 15, 0, 7, 1, 2), (4, 17, 13, 32, 256, 3, 3, 1, 1)])
+def test_conv_16bit_ring(prec, shape):
+    """srk option conv_ring bits 4-6: the 16-bit LDS-DMA ring convolutions (gemm_g16_kernel's
+    structure, per-K-tile conv gathers of the 16-bit operand copies) == the register-staged 16-bit
+    conv kernels on the same rounded operands up to the fp32 summation order, forward and backward."""
+    from speechrecognitionproject_amd import nn as snn
+    N, H, W, Ci, Co, KH, KW, ph, pw = shape[:9]
+    sh, sw = (shape[9], shape[10]) if len(shape) > 9 else (1, 1)
+    g = torch.Generator().manual_seed(N * 13 + Co + KW)
+    x = torch.randn(N, H, W, Ci, generator=g).cuda()
+    w = (torch.randn(Co, Ci, KH, KW, generator=g) / (Ci * KH * KW) ** 0.5).cuda()
+    b = torch.randn(Co, generator=g).cuda()
+    Ho, Wo = (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
+    gy = torch.randn(N, Ho, Wo, Co, generator=g).cuda()
+    outs = []
+    try:
+        for mask in (0x70 | 6, 6):
+            _lib.set_option("conv_ring", mask)
+            xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
+            ym = snn._Conv2dNHWCFn.apply(xm, wm, bm, (ph, pw), (sh, sw))
+            (ym * gy).sum().backward()
+            torch.cuda.synchronize()
+            outs.append([t.detach().double() for t in (ym, xm.grad, wm.grad, bm.grad)])
+    finally:
+        _lib.set_option("conv_ring", 6)
+    for a, c in zip(*outs):
+        assert ((a - c).abs().max() / c.abs().max()).item() <= 1e-5

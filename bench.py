@@ -388,7 +388,20 @@ class Workload:
         loss = self._fwd_bwd(self._batch(j), self.lab[j])
         if self.world == 1:
             self.opt.step(scaler=self.scaler)
+        elif self.exchange_in_graph:
+            self._exchange_and_update()   # the bucketed RCCL all-reduces + Adam, captured with the step
         return loss
+
+    def _capture(self, graph, warmup):
+        """One GraphedStep per pre-staged batch slot, sharing one memory pool."""
+        from speechrecognitionproject_amd.graphs import GraphedStep
+        graphs = []
+        mode = "thread_local" if self.exchange_in_graph else "global"
+        for j in range(self.args.pool):
+            self._slot = j
+            graphs.append(GraphedStep(self._graph_body, warmup=max(2, warmup) if j == 0 else 0,
+                                      pool=graphs[0].pool() if graphs else None, capture_error_mode=mode))
+        return graphs
 
     def run(self, precision, steps, warmup, graph):
         """W warm-up + K timed steps at one matrix precision -> record dict (rank 0 uses it)."""
@@ -398,17 +411,38 @@ class Workload:
         _lib.set_matmul_precision(precision)
         self.scaler = LossScaler(FP16_LOSS_SCALE, dynamic=False, device=self.dev) if precision == "fp16" else None
         self.opt.grad_scale = 1.0 / self.world
+        # N > 1 with HIP graphs: by default the bucketed all-reduces are captured inside the step graph
+        # (forked where each bucket's gradients are final, joined before Adam); --allreduce-outside-graph
+        # replays forward + backward and runs one flat all-reduce + Adam eagerly after it
+        self.exchange_in_graph = graph and self.world > 1 and args.overlap and not args.allreduce_outside_graph
         self.reducer = (parallel.GradReducer(self.flat, bucket_mb=args.bucket_mb)
-                        if (self.world > 1 and args.overlap and not graph) else None)
+                        if (self.world > 1 and args.overlap and (self.exchange_in_graph or not graph)) else None)
         graphs = []
         if graph:
             # one graph per pre-staged batch slot, sharing one memory pool: each reads its own resident
             # batch (no per-step input copy); the first capture's warm-up covers the others
-            from speechrecognitionproject_amd.graphs import GraphedStep
-            for j in range(args.pool):
-                self._slot = j
-                graphs.append(GraphedStep(self._graph_body, warmup=max(2, warmup) if j == 0 else 0,
-                                          pool=graphs[0].pool() if graphs else None))
+            failed = 0
+            try:
+                graphs = self._capture(graph, warmup)
+            except Exception as e:   # noqa: BLE001 — every rank must take the same path below
+                if not self.exchange_in_graph:
+                    raise
+                log("bench: capturing the all-reduces in the step graph failed (%s: %s); falling back to the "
+                    "eager all-reduce after each replay" % (type(e).__name__, e))
+                failed = 1
+            if self.exchange_in_graph:
+                flag = torch.tensor([failed], device=self.dev)
+                torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
+                if flag.item():
+                    for g in graphs:
+                        g.release()
+                    torch.cuda.synchronize()
+                    self.exchange_in_graph = False
+                    if self.reducer is not None:
+                        self.reducer.remove()
+                    self.reducer = None
+                    graphs = self._capture(graph, warmup)
+            self.graph_allreduce = "in graph" if self.exchange_in_graph else "eager after replay"
             for g in graphs:
                 loss = g.replay()    # one untimed replay of each: every captured step runs once before timing
         else:
@@ -427,7 +461,7 @@ class Workload:
         for i in range(steps):
             if graphs:
                 loss = graphs[i % args.pool].replay()
-                if self.world > 1:
+                if self.world > 1 and not self.exchange_in_graph:
                     self._exchange_and_update()
             else:
                 loss = self.eager_step(i)
@@ -446,7 +480,10 @@ class Workload:
         eager_ms = None
         if not args.no_prof and graph:
             # kernel timers cannot run inside a graph: an eager pass of the same step, timed per kernel
+            if self.reducer is not None:
+                self.reducer.remove()
             self.reducer = None
+            self.exchange_in_graph = False
             _lib.prof_enable(True)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
@@ -467,7 +504,11 @@ class Workload:
         cmd = {"model": self.name, "batch": self.B, "world": self.world, "precision": precision,
                "sync_bn": bool(args.sync_bn)}
         skipped = self.scaler.overflows() if self.scaler is not None else None
+        if self.reducer is not None:
+            self.reducer.remove()
+            self.reducer = None
         return {"el": el, "steps": steps, "warmup": warmup, "graph": bool(graph), "final_loss": final_loss,
+                "exchange_in_graph": bool(graph and self.world > 1 and getattr(self, "graph_allreduce", "") == "in graph"),
                 "fp16_skipped_steps": skipped,
                 "kernels": kernels, "roofline": roofline(kernels, singles, cmd), "eager_ms": eager_ms,
                 "prof_steps": args.prof_steps if (graph and prof) else steps}
@@ -485,11 +526,15 @@ def _workload_h2d(self, precision, steps, warmup):
     n_host = 8
     x, _ = synthetic_clips(n_host * self.B, seed=4000 + self.rank)
     host = torch.from_numpy(x).view(n_host, self.B, -1).pin_memory()
+    # N > 1: the exchange as the main run settled it (in the graph, or eager after each replay)
+    self.exchange_in_graph = self.world > 1 and getattr(self, "graph_allreduce", "") == "in graph"
+    self.reducer = parallel.GradReducer(self.flat, bucket_mb=self.args.bucket_mb) if self.exchange_in_graph else None
     graphs = []
     for j in range(2):
         self._slot = j
         graphs.append(GraphedStep(self._graph_body, warmup=max(2, warmup) if j == 0 else 0,
-                                  pool=graphs[0].pool() if graphs else None))
+                                  pool=graphs[0].pool() if graphs else None,
+                                  capture_error_mode="thread_local" if self.exchange_in_graph else "global"))
     cs = torch.cuda.Stream()
     cur = torch.cuda.current_stream()
     ev_copy = [torch.cuda.Event() for _ in range(2)]
@@ -510,6 +555,8 @@ def _workload_h2d(self, precision, steps, warmup):
             j = i % 2
             cur.wait_event(ev_copy[j])
             graphs[j].replay()
+            if self.world > 1 and not self.exchange_in_graph:
+                self._exchange_and_update()
             ev_done[j].record(cur)
             if i + 1 < n:
                 upload(i + 1)
@@ -529,6 +576,10 @@ def _workload_h2d(self, precision, steps, warmup):
     el_copy = time.perf_counter() - t1
     for g in graphs:
         g.release()
+    if self.reducer is not None:
+        self.reducer.remove()
+        self.reducer = None
+    self.exchange_in_graph = False
     torch.cuda.empty_cache()
     step_bytes = self.B * 16000 * 4
     return {"value": round(self.B * steps / el, 2), "unit": "utt/s", "ms_per_step": round(el / steps * 1e3, 3),
@@ -596,6 +647,9 @@ def main():
                     help="N > 1, eager: one blocking all-reduce after backward instead of bucketed all-reduces "
                          "overlapped with it (parallel.GradReducer)")
     ap.add_argument("--bucket-mb", type=float, default=8.0, help="gradient bucket size of the overlapped all-reduce")
+    ap.add_argument("--allreduce-outside-graph", action="store_true",
+                    help="N > 1, HIP graphs: replay forward + backward, then one flat all-reduce + Adam eagerly "
+                         "(default: the bucketed all-reduces and Adam are captured in the step graph)")
     ap.add_argument("--sync-bn", action="store_true",
                     help="BatchNorm statistics over the global batch of all ranks (SyncBatchNorm1d; resnet_bgru, "
                          "cnn_bgru, mfrn_bgru)")
@@ -664,10 +718,13 @@ def main():
         "config": {"workload": "%s, CE, backward, Adam (full training.py step), per-GPU batch %d"
                                % (CFG[args.model], B), "model": args.model,
                    "global_batch": world * B, "clip_samples": 16000, "parallelism": "dp%d" % world,
-                   "step_execution": ("HIP graph replay" + (" (forward + backward) + eager RCCL all-reduce + Adam"
-                                                            if world > 1 else " of the whole step")
+                   "step_execution": ("HIP graph replay" + (" of the whole step" if world == 1 or main_rec["exchange_in_graph"]
+                                                            else " (forward + backward) + eager RCCL all-reduce + Adam")
                                       if args.graph else "eager"),
-                   "allreduce": (None if world == 1 else "one flat buffer after backward" if (args.graph or not args.overlap)
+                   "allreduce": (None if world == 1 else
+                                 "bucketed %.0f MB, captured in the step graph, overlapped with backward" % args.bucket_mb
+                                 if main_rec["exchange_in_graph"] else
+                                 "one flat buffer after backward" if (args.graph or not args.overlap)
                                  else "bucketed %.0f MB, overlapped with backward" % args.bucket_mb),
                    "sync_bn": bool(args.sync_bn)},
         "model_tflops": round(value * TRAIN_GFLOP_PER_UTT.get(args.model, 0) / 1e3, 2),

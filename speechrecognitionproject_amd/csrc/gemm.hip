@@ -1015,7 +1015,10 @@ static_assert(kG16Stages >= 4 && kG16Stages <= 5, "g16 ring: 4..5 stages of 32 K
 // stores straight from the accumulators (32x32 layout: 128-B row segments per half-wave) instead of
 // staging through the LDS ring, so the next tile's prologue DMA follows the stores at once and the
 // stores drain behind its first K-tiles.
-template <bool TA, bool TB, bool F16, bool PERS = false>
+// QS: k-steps (16 deep) per section.  1: 8 MFMAs per MFMA section (the round-2 form); 2: one whole
+// 32-deep K-tile per section (16 MFMAs, 12 fragments per load section, half the barriers per k) —
+// option gemm16_qs.
+template <bool TA, bool TB, bool F16, bool PERS = false, int QS = 1>
 __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
   using Ops = LpOps<F16>;
   using e8 = typename Ops::e8;
@@ -1122,32 +1125,44 @@ __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
     const unsigned short* As = S + grp * HALF;
     const unsigned short* Bs = S + (2 + bh) * HALF;
     const int tn_ = kt + NST - 1;   // the K-tile issued during this one (into K-tile kt - 1's stage)
+    static_assert(QS == 1 || QS == 2, "g16: 1 or 2 k-steps per section");
 #pragma unroll
-    for (int q = 0; q < BK / 16; ++q) {
-      // ---- load section: k-step q's fragments (4 A row blocks, 2 B column blocks)
-      u32x4 fa[4], fb[2];
+    for (int q = 0; q < BK / 16; q += QS) {
+      // ---- load section: k-steps q .. q + QS - 1's fragments (4 A row blocks, 2 B column blocks each)
+      u32x4 fa[QS][4], fb[QS][2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = HA::frag(As, i * 32, 16 * q, lane);
+      for (int e = 0; e < QS; ++e) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) fb[j] = HB::frag(Bs, bc0 + j * 32, 16 * q, lane);
+        for (int i = 0; i < 4; ++i) fa[e][i] = HA::frag(As, i * 32, 16 * (q + e), lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[e][j] = HB::frag(Bs, bc0 + j * 32, 16 * (q + e), lane);
+      }
 #if !(defined(SRK_G16_EXP) && SRK_G16_EXP == 1)   // experiment builds only: no DMA after the prologue
       if (tn_ < nk) {
-        if (q == 0) dma_a(tn_);
-        else dma_b(tn_);
+        if (QS == 2) {
+          dma_a(tn_);
+          dma_b(tn_);
+        } else if (q == 0) {
+          dma_a(tn_);
+        } else {
+          dma_b(tn_);
+        }
       }
 #endif
 #if !(defined(SRK_G16_EXP) && SRK_G16_EXP == 2)   // experiment builds only: DMA never waited for in the loop
-      if (q == BK / 16 - 1) retire_keep(min(nk - 1 - (kt + 1), NST - 2));   // K-tile kt + 1 landed (this wave's part)
+      if (q + QS == BK / 16) retire_keep(min(nk - 1 - (kt + 1), NST - 2));   // K-tile kt + 1 landed (this wave's part)
 #endif
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this section's fragments are in registers
       bar();
-      // ---- MFMA section: 8 independent accumulators, one k-step
+      // ---- MFMA section: 8 independent accumulators, QS k-steps
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int e = 0; e < QS; ++e)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = Ops::mma(__builtin_bit_cast(e8, fa[i]), __builtin_bit_cast(e8, fb[j]), acc[i][j]);
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = Ops::mma(__builtin_bit_cast(e8, fa[e][i]), __builtin_bit_cast(e8, fb[e][j]), acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
       bar();
     }
@@ -1913,6 +1928,9 @@ int launch_g16(const GemmDesc& d, hipStream_t s, bool f16) {
   if (pers) {
     if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true, true>), grid, block, 0, s, ka);
     else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false, true>), grid, block, 0, s, ka);
+  } else if (g_opt_gemm16_qs == 2) {
+    if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true, false, 2>), grid, block, 0, s, ka);
+    else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false, false, 2>), grid, block, 0, s, ka);
   } else {
     if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true>), grid, block, 0, s, ka);
     else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false>), grid, block, 0, s, ka);

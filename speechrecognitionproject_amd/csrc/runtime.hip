@@ -29,6 +29,7 @@ int g_opt_conv_ring = 6;
 int g_opt_mfcc_variant = 3;
 int g_opt_gemm_streamk = 1;
 int g_opt_gemm16_persistent = 0;
+int g_opt_gemm16_qs = 1;
 int g_opt_gemm32_kernel = 0;
 static std::atomic<int> g_opt_matmul_prec{kPrecF32};
 int matmul_prec() { return g_opt_matmul_prec.load(std::memory_order_relaxed); }
@@ -358,6 +359,11 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "gemm16_kernel") {   // 0 by shape, 1 register-staged, 2 LDS-DMA ping-pong (16-bit operands)
     SRK_REQUIRE(value >= 0 && value <= 2, SRK_ERR_INVALID, "gemm16_kernel must be 0, 1 or 2");
     srk::g_opt_gemm16_kernel = (int)value;
+    return SRK_OK;
+  }
+  if (n == "gemm16_qs") {   // 16-bit ping-pong GEMM: k-steps per section (1 or 2)
+    SRK_REQUIRE(value == 1 || value == 2, SRK_ERR_INVALID, "gemm16_qs must be 1 or 2");
+    srk::g_opt_gemm16_qs = (int)value;
     return SRK_OK;
   }
   if (n == "gemm16_persistent") {   // 16-bit ping-pong GEMM: persistent tile loop (1) or one tile per workgroup (0)

@@ -119,6 +119,8 @@ extern int g_opt_mfcc_variant;
 extern int g_opt_gemm_streamk;
 // persistent tile loop with direct-store epilogue for the 16-bit ping-pong GEMM ("gemm16_persistent")
 extern int g_opt_gemm16_persistent;
+// k-steps per section of the 16-bit ping-pong GEMM ("gemm16_qs": 1 = 8 MFMAs per section, 2 = 16)
+extern int g_opt_gemm16_qs;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

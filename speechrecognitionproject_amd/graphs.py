@@ -38,10 +38,12 @@ def _detached(out):
 class GraphedStep:
     """``step()`` -> its output tensor(s), captured after ``warmup`` eager calls on a side stream."""
 
-    def __init__(self, step, warmup=2, pool=None):
+    def __init__(self, step, warmup=2, pool=None, capture_error_mode="global"):
         """warmup: eager calls of ``step`` on a side stream before the capture (>= 2 so every scratch
         buffer reaches its size), or 0 when the caller has just run >= 2 steps of the same shapes on a
-        side stream itself (training.py: real steps on real batches, no repeated step)."""
+        side stream itself (training.py: real steps on real batches, no repeated step).
+        capture_error_mode: torch.cuda.graph's; "thread_local" when the step issues RCCL collectives
+        (the process group's watchdog thread keeps making runtime calls during the capture)."""
         if warmup == 1 or warmup < 0:
             raise ValueError("GraphedStep: warmup must be 0 (caller warmed up) or >= 2")
         self.step = step
@@ -61,7 +63,7 @@ class GraphedStep:
         torch.cuda.synchronize()
         self.generation = _lib.scratch_generation()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=pool):
+        with torch.cuda.graph(self.graph, pool=pool, capture_error_mode=capture_error_mode):
             out = step()
         self.out = _detached(out)
         del out

@@ -74,10 +74,18 @@ class GradReducer:
     ``persistent_pending(+1)``; its backward calls ``persistent_done`` right after enqueueing the
     recurrence: until the last such backward is enqueued, ready buckets are held (a collective
     launched afterwards waits for that kernel on the compute stream).  ``finish()`` launches what
-    is left in bucket order (identical on every rank) and makes the compute stream wait for all."""
+    is left in bucket order (identical on every rank) and makes the compute stream wait for all.
 
-    def __init__(self, flat, bucket_mb=8.0, group=None):
+    HIP graphs: the whole step — forward, backward with these bucketed collectives, ``finish()`` and
+    the optimizer — can be captured into one graph (bench.py at N > 1).  The host logic above runs once,
+    during the capture, so each collective is recorded at the point of the stream order where its bucket
+    became final: a graph node on the process group's stream, forked from the compute stream there and
+    joined back before the optimizer.  ``collectives_at_world1`` issues them even in a 1-rank group
+    (the GPU test of that capture on a one-GPU box)."""
+
+    def __init__(self, flat, bucket_mb=8.0, group=None, collectives_at_world1=False):
         self.flat, self.group = flat, group
+        self.min_world = 1 if collectives_at_world1 else 2
         cap = max(1, int(bucket_mb * (1 << 20) / 4))
         groups, cur, size = [], [], 0
         for off, p in sorted(zip(flat.offsets, flat.params), key=lambda t: t[0], reverse=True):
@@ -147,7 +155,7 @@ class GradReducer:
             return
         self.launched[i] = True
         lo, hi, _ = self.buckets[i]
-        if world_size() > 1:
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) >= self.min_world:
             self.works.append(dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
                                               async_op=True))
 

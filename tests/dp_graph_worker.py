@@ -1,0 +1,118 @@
+"""Worker of tests/test_dp_graph_gpu.py (run as a subprocess: it owns a 1-rank RCCL process group).
+
+bench.py at N > 1 captures the whole DP step into a HIP graph: forward, backward with the bucketed
+all-reduces of parallel.GradReducer forked where each bucket's gradients are final, the join, and Adam
+(DESIGN.md §4).  On a one-GPU box the closest check is a 1-rank "nccl" (RCCL) group with the reducer
+told to issue its collectives anyway: the captured step must then replay the eager step bit for bit
+(a 1-rank SUM is the identity), buckets must be forked during the backward (not all at finish()),
+and a captured collective must actually run on replay (a 1-rank all-gather copies a fresh input).
+Prints one JSON line."""
+import json
+import os
+import socket
+import sys
+
+import torch
+import torch.distributed as dist
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def main():
+    name, B, precision = sys.argv[1], int(sys.argv[2]), sys.argv[3]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import importlib
+
+    from oracle import models as OM
+    from speechrecognitionproject_amd import _lib, parallel
+    from speechrecognitionproject_amd import nn as snn
+    from speechrecognitionproject_amd.graphs import GraphedStep
+    from speechrecognitionproject_amd.optim import Adam, FlatParams
+    from speechrecognitionproject_amd.synthetic import synthetic_clips
+
+    ocls = {"mfcc_bgru": OM.MfccBGRU, "spec_bgru": OM.SpecBGRU, "resnet_bgru": OM.ResnetBGRU}[name]
+    _lib.set_matmul_precision(precision)
+    K = 3
+    out = {}
+    states = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        net = importlib.import_module("speechrecognitionproject_amd.models.model_" + name).Network().cuda()
+        net.load_state_dict(OM.seeded_state_dict(ocls(), 0))
+        net.train()
+        flat = FlatParams(net.parameters())
+        opt = Adam(net.parameters(), lr=1e-4, flat=flat)
+        red = parallel.GradReducer(flat, bucket_mb=0.5, collectives_at_world1=True)
+        crit = snn.CrossEntropyLoss()
+        x, y = synthetic_clips(3 * B, seed=23)
+        pcm, lab = torch.from_numpy(x).cuda().view(3, B, -1), torch.from_numpy(y).cuda().view(3, B)
+        sx, sy = pcm[0].clone(), lab[0].clone()
+        launched = []
+
+        def body():
+            opt.zero_grad()
+            red.begin()
+            loss = crit(net(sx), sy)
+            loss.backward()
+            launched.append(len(red.works))          # collectives already forked during backward
+            red.finish()
+            opt.step()
+            return loss
+
+        losses = []
+        if graphed:
+            g = GraphedStep(body, warmup=2, capture_error_mode="thread_local")
+            out["buckets"] = len(red.buckets)
+            out["forked_during_backward"] = launched[-1]
+            for i in range(K):
+                sx.copy_(pcm[(i + 1) % 3])
+                sy.copy_(lab[(i + 1) % 3])
+                losses.append(g.replay().item())
+            g.release()
+        else:
+            for i in range(2 + K):
+                if i >= 2:
+                    sx.copy_(pcm[(i - 1) % 3])
+                    sy.copy_(lab[(i - 1) % 3])
+                loss = body()
+                if i >= 2:
+                    losses.append(loss.item())
+        torch.cuda.synchronize()
+        red.remove()
+        states.append((flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), losses))
+    (p0, m0, v0, l0), (p1, m1, v1, l1) = states
+    out["losses_equal"] = l0 == l1
+    out["params_equal"] = bool(torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1))
+    out["spin_timeouts"] = _lib.spin_timeouts()
+
+    # a captured collective runs on every replay: a 1-rank all-gather copies its input to its output
+    src = torch.arange(1024, device="cuda", dtype=torch.float32)
+    dst = torch.zeros(1024, device="cuda")
+    dist.all_gather_into_tensor(dst, src)           # eager once
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        dist.all_gather_into_tensor(dst, src)
+    ok = []
+    for r in range(3):
+        src.fill_(r + 1.0)
+        dst.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        ok.append(bool(torch.all(dst == r + 1.0).item()))
+    out["captured_collective_replays"] = ok
+    dist.destroy_process_group()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,32 @@
+"""The DP step captured whole into a HIP graph (bench.py at N > 1): forward, backward
+with parallel.GradReducer's bucketed RCCL all-reduces forked where each bucket is final, the join and
+Adam.  Checked on a 1-rank RCCL group in a subprocess (tests/dp_graph_worker.py): graph replays ==
+eager steps bit for bit, more than one bucket forked during the backward (not all at finish()), and a
+captured collective really runs on each replay.  The N > 1 arithmetic of the same reducer is covered
+over gloo on the CPU (tests/test_parallel.py)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("name,B,precision", [("mfcc_bgru", 64, "fp32"), ("mfcc_bgru", 64, "bf16")])
+def test_dp_step_graph_with_captured_allreduce(gpu, name, B, precision):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(HERE, "dp_graph_worker.py"), name, str(B), precision],
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["buckets"] > 2, out
+    assert out["forked_during_backward"] >= 1, out      # overlapped, not all launched at finish()
+    assert out["losses_equal"] and out["params_equal"], out
+    assert out["spin_timeouts"] == 0, out
+    assert out["captured_collective_replays"] == [True, True, True], out

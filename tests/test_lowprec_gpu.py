@@ -560,6 +560,39 @@ def test_gemm16_persistent(prec, ta, tb, M, N, K, beta):
     assert (outs[0] - outs[1]).abs().max().item() <= 1e-6 * (1 + scale)
 
 
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0)])
+@pytest.mark.parametrize("M,N,K,beta", [(5120, 3328, 520, 0.0), (1300, 700, 2056, 2.0), (2560, 2560, 8, 0.0)])
+def test_gemm16_qs(prec, ta, tb, M, N, K, beta):
+    """srk option gemm16_qs = 2: the 16-bit ping-pong GEMM with one whole 32-deep K-tile per section
+    (16 MFMAs, half the barriers) == the 16-deep sections bit for bit (each accumulator adds the same
+    k-steps in the same order) and == float64 of the 16-bit values (k tails: 520, 8; row / column
+    edges: 1300 x 700; split-K: 2056)."""
+    g = torch.Generator().manual_seed(M + 3 * N + K + tb)
+    dt = TORCH_DT[prec]
+    A = torch.randn((K, M) if ta else (M, K), generator=g).to(dt)
+    B = torch.randn((N, K) if tb else (K, N), generator=g).to(dt)
+    C0 = torch.randn(M, N, generator=g)
+    opA = (A.T if ta else A).double()
+    opB = (B.T if tb else B).double()
+    ref = 0.5 * (opA @ opB) + beta * C0.double()
+    Ad, Bd = A.cuda(), B.cuda()
+    outs = []
+    try:
+        _lib.set_option("gemm16_kernel", 2)
+        for qs in (2, 1):
+            _lib.set_option("gemm16_qs", qs)
+            Cd = C0.clone().cuda()
+            call("srk_gemm_16", ta, tb, M, N, K, 0.5, ptr(Ad), Ad.shape[1], ptr(Bd), Bd.shape[1], beta, ptr(Cd), N,
+                 None, 0, stream_ptr())
+            outs.append(Cd.cpu())
+    finally:
+        _lib.set_option("gemm16_qs", 1)
+        _lib.set_option("gemm16_kernel", 0)
+    scale = (opA.abs() @ opB.abs()).max().item()
+    assert (outs[0].double() - ref).abs().max().item() <= 2e-6 * (1 + scale)
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("shape", [(2, 98, 40, 64, 128, 1, 7, 0, 3), (3, 98, 1, 256, 512, 7, 1, 3, 0),
                                    (2, 1, 1000, 64, 128, 1, 15, 0, 7, 1, 2), (4, 17, 13, 32, 256, 3, 3, 1, 1)])
 def test_conv_16bit_ring(prec, shape):

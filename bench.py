@@ -110,7 +110,7 @@ LP_KERNELS = ("gemm_bf16", "gemm_f16", "gru_fwd_seq_lp", "gru_bwd_seq_lp", "conv
               "conv_wgrad_lp")
 OTHER_KERNELS = ("mfcc", "fbank", "spec", "noise_mix", "adam", "grad_check", "batchnorm_fwd", "batchnorm_bwd", "conv1_pool_fwd",
                  "conv1_pool_wgrad",
-                 "maxpool_fwd", "maxpool_bwd", "conv_to16")
+                 "maxpool_fwd", "maxpool_bwd", "conv_to16", "conv_unpool16")
 
 
 def log(*a):
@@ -309,11 +309,13 @@ def plumbing(args, rank, world):
               flush=True)
 
 
-EXTRA_CONFIGS = (  # BASELINE.json configs[2..4] at their per-GPU batch (the default run appends them), and
-    ("cfg3", "fbanks_cnn", "fp32", 512, 10),     # the metric's literal "MFCC+CNN-BiGRU" model
-    ("cfg4", "resnet_bgru", "fp32", 512, 4),
-    ("cfg5", "spec_bgru", "fp16", 512, 20),
+EXTRA_CONFIGS = (  # BASELINE.json configs[2..4] at their per-GPU batch (the default run appends them), the
+    ("cfg3", "fbanks_cnn", "fp32", 512, 10),     # metric's literal "MFCC+CNN-BiGRU" model, and the
+    ("cfg4", "resnet_bgru", "fp32", 512, 4),     # 16-bit re-timings of the conv configs (the matrix cores' 16-bit
+    ("cfg5", "spec_bgru", "fp16", 512, 20),      # conv path on the driver's line)
     ("mfrn", "mfrn_bgru", "fp32", 256, 10),
+    ("cfg3-bf16", "fbanks_cnn", "bf16", 512, 10),
+    ("cfg4-bf16", "resnet_bgru", "bf16", 512, 4),
 )
 
 

@@ -692,6 +692,35 @@ __global__ void unpool_kernel(const float* __restrict__ dy, const uint8_t* __res
   }
 }
 
+// 16-bit modes: the dense data gradient of a pooled conv written straight as the 16-bit operand copy
+// the S16 gathers read (8 channels per thread: one 16-B store per window position), rounded by the
+// same conversion as to16_kernel — so the operands are bitwise those of unpool + to16, without the
+// dense fp32 gradient (N Ho Wo Co x 4 B written and read back twice: conversion and bias sums)
+template <int LP>
+__global__ void unpool16_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ arg, int64_t rows_out, int C,
+                                int kw, unsigned short* __restrict__ dx16) {
+  const int C8 = C / 8;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows_out * C8) return;
+  const int64_t r = i / C8;
+  const int c = (int)(i - r * C8) * 8;
+  const v4f g0 = ld4(dy + r * C + c), g1 = ld4(dy + r * C + c + 4);
+  typedef unsigned u32x2a __attribute__((ext_vector_type(2)));
+  const u32x2a a = *reinterpret_cast<const u32x2a*>(arg + r * C + c);
+  using E4 = typename ConvLp<LP>::e4;
+  for (int b = 0; b < kw; ++b) {
+    v4f o0, o1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o0[e] = ((a.x >> (8 * e)) & 0xFFu) == (unsigned)b ? g0[e] : 0.f;
+      o1[e] = ((a.y >> (8 * e)) & 0xFFu) == (unsigned)b ? g1[e] : 0.f;
+    }
+    const u32x2_ lo = __builtin_bit_cast(u32x2_, __builtin_convertvector(o0, E4));
+    const u32x2_ hi = __builtin_bit_cast(u32x2_, __builtin_convertvector(o1, E4));
+    *reinterpret_cast<u32x4_*>(dx16 + (r * kw + b) * C + c) = u32x4_{lo.x, lo.y, hi.x, hi.y};
+  }
+}
+
 __global__ void zero_kernel(float* __restrict__ p, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = 0.f;
@@ -1341,6 +1370,9 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
   const bool lp = prec != kPrecF32;
   // fp32 operands (option bits 0..2), or the 16-bit operand copies of the S16 path (bits 4..6)
   if (!(g_opt_conv_ring & (1 << (MODE + (lp ? 4 : 0)))) || c.dy_arg || (lp != (c.a16 != nullptr))) return 1;
+  // the 16-bit pooled forward (fbanks_cnn conv2) measured slower on the ring (r04ab3: 2.89 vs 2.68 ms
+  // per 5 cfg3 steps): only with bit 7
+  if (lp && MODE == kFwd && c.pool_w && !(g_opt_conv_ring & 0x80)) return 1;
   const int RBK = lp ? kR16BK : kRBK, unit = lp ? 8 : 4, esz = lp ? 2 : 4;
   const int chans = MODE == kDgrad ? c.Co : c.Ci;
   if (MODE != kWgrad && chans % RBK) return 1;
@@ -1589,10 +1621,11 @@ namespace srk {
 // (the caller guarantees fp32 sources, the fused bias sums and no full-width data gradient)
 int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co, int64_t KH,
              int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw, const float* dy, const uint8_t* dy_arg,
-             float* dx, float* dw, float* db, float* ws, const void* x16, void* stream) {
+             float* dx, float* dw, float* db, float* ws, const void* x16, void* stream,
+             const unsigned short* dy16 = nullptr) {
   int64_t Ho, Wo;
   if (int rc = srk::check(N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw, &Ho, &Wo)) return rc;
-  SRK_REQUIRE(x && w && dy && dw && ws, SRK_ERR_INVALID, "conv bwd: null pointer");
+  SRK_REQUIRE(x && w && (dy || dy16) && dw && ws, SRK_ERR_INVALID, "conv bwd: null pointer");
   hipStream_t s = srk::as_stream(stream);
   const int64_t nw = Co * Ci * KH * KW;
   srk::ConvArgs c{};
@@ -1604,6 +1637,9 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
   const bool full_width = KH == 1 && ph == 0 && sh == 1 && pw == 0 && KW == W && Wo == 1;
   SRK_REQUIRE(!dy_arg || (!full_width && (!db || srk::g_opt_conv_fused_db)), SRK_ERR_INTERNAL,
               "conv bwd: pooled dY needs the implicit data gradient and the fused bias sums");
+  // dy16: the caller's 16-bit dY (no fp32 dY): the implicit 16-bit-source GEMMs only, no bias sums here
+  SRK_REQUIRE(!dy16 || (!dy && !dy_arg && !full_width && !db && srk::s16_ok(srk::matmul_prec(), Ci, Co, {x, ws, x16, dy16})),
+              SRK_ERR_INTERNAL, "conv bwd: a 16-bit dY needs the 16-bit-source implicit GEMMs");
   const bool dgrad_implicit = dx && !full_width;
   if (dgrad_implicit)
     hipLaunchKernelGGL(srk::weight_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, (int)Co,
@@ -1614,8 +1650,9 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
   if (!dy_arg && srk::s16_ok(prec, Ci, Co, {x, dy, ws, x16})) {
     const float* src[3] = {x, dy, ws};
     const int64_t n[3] = {N * H * W * Ci, N * Ho * Wo * Co, nw};
-    const bool ready[3] = {x16 != nullptr, false, false};   // x16: the forward's copy of x
+    const bool ready[3] = {x16 != nullptr, dy16 != nullptr, false};   // x16: the forward's copy of x
     d16[0] = const_cast<unsigned short*>(static_cast<const unsigned short*>(x16));
+    d16[1] = const_cast<unsigned short*>(dy16);
     if ((rc = srk::to16_all(prec, src, n, dgrad_implicit ? 3 : 2, d16, s, ready))) return rc;
   }
   if (dx && full_width) {
@@ -1729,9 +1766,30 @@ int srk_conv2d_nhwc_bwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
   if (srk::g_opt_conv_unpool_gather && !full_width && (!db || srk::g_opt_conv_fused_db) &&
       !srk::s16_ok(srk::matmul_prec(), Ci, Co, {x, w, x16}))
     return srk::conv_bwd(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, 1, 1, dy_pooled, argmax, dx, dw, db, ws, x16, stream);
+  const int64_t rows = N * Ho * Wo / pool_w;
+  const int prec = srk::matmul_prec();
+  if (srk::g_opt_conv_unpool16 && !full_width && Co % 8 == 0 && srk::s16_ok(prec, Ci, Co, {x, w, x16, ws})) {
+    // 16-bit-source modes: the dense dY straight as its 16-bit copy, the bias gradient from the pooled
+    // gradient (each pooled value sits once in the dense dY, the rest are zeros), then the backward
+    float* d = nullptr;
+    if (int rc = srk::conv_scratch((size_t)(N * Ho * Wo * Co + 1) / 2, &d, srk::g_csd)) return rc;
+    unsigned short* dy16 = reinterpret_cast<unsigned short*>(d);
+    {
+      srk::ProfScope prof("conv_unpool16", s, (double)rows * Co * (4.0 + 1.0 + 2.0 * pool_w));
+      const dim3 grid((unsigned)((rows * (Co / 8) + 255) / 256));
+      if (prec == srk::kPrecBF16)
+        hipLaunchKernelGGL(srk::unpool16_kernel<1>, grid, dim3(256), 0, s, dy_pooled, argmax, rows, (int)Co, (int)pool_w, dy16);
+      else
+        hipLaunchKernelGGL(srk::unpool16_kernel<2>, grid, dim3(256), 0, s, dy_pooled, argmax, rows, (int)Co, (int)pool_w, dy16);
+      SRK_CHECK_HIP(hipGetLastError());
+    }
+    if (db)
+      if (int rc = srk::colsum_f32(dy_pooled, rows, Co, Co, db, 0.f, s)) return rc;
+    return srk::conv_bwd(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, 1, 1, nullptr, nullptr, dx, dw, nullptr, ws, x16, stream,
+                         dy16);
+  }
   float* dy = nullptr;   // else: the dense gradient in library scratch, then the plain backward
   if (int rc = srk::conv_scratch((size_t)(N * Ho * Wo * Co), &dy, srk::g_csd)) return rc;
-  const int64_t rows = N * Ho * Wo / pool_w;
   hipLaunchKernelGGL(srk::unpool_kernel, dim3((unsigned)((rows * (Co / 4) + 255) / 256)), dim3(256), 0, s, dy_pooled,
                      argmax, rows, (int)Co, (int)pool_w, dy);
   SRK_CHECK_HIP(hipGetLastError());

@@ -1018,7 +1018,10 @@ static_assert(kG16Stages >= 4 && kG16Stages <= 5, "g16 ring: 4..5 stages of 32 K
 // QS: k-steps (16 deep) per section.  1: 8 MFMAs per MFMA section (the round-2 form); 2: one whole
 // 32-deep K-tile per section (16 MFMAs, 12 fragments per load section, half the barriers per k) —
 // option gemm16_qs.
-template <bool TA, bool TB, bool F16, bool PERS = false, int QS = 1>
+// STATIC_PRIO: no per-section priority flips; the second-dispatched group (waves 4-7, the arbitration
+// loser) runs at s_setprio 1 for the whole loop (MI355X_MICROARCH.md, two waves per SIMD, item 4) —
+// option gemm16_prio.
+template <bool TA, bool TB, bool F16, bool PERS = false, int QS = 1, bool STATIC_PRIO = false>
 __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
   using Ops = LpOps<F16>;
   using e8 = typename Ops::e8;
@@ -1118,6 +1121,7 @@ __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
   retire_keep(min(nk - 1, NST - 2));
   bar();
   if (grp == 1) bar();   // the groups run one section apart
+  if (STATIC_PRIO && grp == 1) __builtin_amdgcn_s_setprio(1);
 
   const int bh = wc >> 1, bc0 = (wc & 1) * 64;   // this wave's B half image and its column base there
   for (int kt = 0; kt < nk; ++kt) {
@@ -1155,7 +1159,7 @@ __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this section's fragments are in registers
       bar();
       // ---- MFMA section: 8 independent accumulators, QS k-steps
-      __builtin_amdgcn_s_setprio(1);
+      if (!STATIC_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int e = 0; e < QS; ++e)
 #pragma unroll
@@ -1163,11 +1167,12 @@ __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             acc[i][j] = Ops::mma(__builtin_bit_cast(e8, fa[e][i]), __builtin_bit_cast(e8, fb[e][j]), acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
+      if (!STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
       bar();
     }
   }
   if (grp == 0) bar();   // equal barrier counts; every wave is past its last LDS read and DMA wait
+  if (STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
 
   // ---- epilogue (the ring is idle now): pp_epilogue
 #if defined(SRK_G16_EXP) && SRK_G16_EXP == 3   // experiment builds only: no C stores (kept live)
@@ -1931,6 +1936,9 @@ int launch_g16(const GemmDesc& d, hipStream_t s, bool f16) {
   } else if (g_opt_gemm16_qs == 2) {
     if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true, false, 2>), grid, block, 0, s, ka);
     else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false, false, 2>), grid, block, 0, s, ka);
+  } else if (g_opt_gemm16_prio) {
+    if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true, false, 1, true>), grid, block, 0, s, ka);
+    else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false, false, 1, true>), grid, block, 0, s, ka);
   } else {
     if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true>), grid, block, 0, s, ka);
     else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false>), grid, block, 0, s, ka);

@@ -25,11 +25,13 @@ int g_opt_conv16_sources = 1;
 int g_opt_conv_fused_db = 1;
 int g_opt_conv_unpool_gather = 1;
 int g_opt_conv_tile = 128;
-int g_opt_conv_ring = 6;
+int g_opt_conv_ring = 0x76;
+int g_opt_conv_unpool16 = 1;
 int g_opt_mfcc_variant = 3;
 int g_opt_gemm_streamk = 1;
 int g_opt_gemm16_persistent = 0;
 int g_opt_gemm16_qs = 1;
+int g_opt_gemm16_prio = 0;
 int g_opt_gemm32_kernel = 0;
 static std::atomic<int> g_opt_matmul_prec{kPrecF32};
 int matmul_prec() { return g_opt_matmul_prec.load(std::memory_order_relaxed); }
@@ -366,6 +368,10 @@ int srk_set_option(const char* name, int64_t value) {
     srk::g_opt_gemm16_qs = (int)value;
     return SRK_OK;
   }
+  if (n == "gemm16_prio") {   // 16-bit ping-pong GEMM: static priority for waves 4-7 (1) or per-section flips (0)
+    srk::g_opt_gemm16_prio = value != 0;
+    return SRK_OK;
+  }
   if (n == "gemm16_persistent") {   // 16-bit ping-pong GEMM: persistent tile loop (1) or one tile per workgroup (0)
     srk::g_opt_gemm16_persistent = value != 0;
     return SRK_OK;
@@ -379,9 +385,15 @@ int srk_set_option(const char* name, int64_t value) {
     srk::g_opt_mfcc_variant = (int)value;
     return SRK_OK;
   }
-  if (n == "conv_ring") {   // ring conv kernels where the shape qualifies: bits 0-2 fp32 fwd / dgrad / wgrad, 4-6 16-bit
-    SRK_REQUIRE(value >= 0 && value <= 0x77, SRK_ERR_INVALID,
-                "conv_ring is a mask of 1 / 2 / 4 (fp32 fwd / dgrad / wgrad) and 16 / 32 / 64 (16-bit)");
+  if (n == "conv_unpool16") {   // 16-bit modes: pooled-conv backward writes dY's 16-bit copy directly (1) or not (0)
+    srk::g_opt_conv_unpool16 = value != 0;
+    return SRK_OK;
+  }
+  if (n == "conv_ring") {   // ring conv kernels where the shape qualifies: bits 0-2 fp32 fwd / dgrad / wgrad, 4-6 16-bit,
+                            // 7 the 16-bit pooled forward too
+    SRK_REQUIRE(value >= 0 && value <= 0xf7, SRK_ERR_INVALID,
+                "conv_ring is a mask of 1 / 2 / 4 (fp32 fwd / dgrad / wgrad), 16 / 32 / 64 (16-bit) and 128 "
+                "(16-bit pooled forward)");
     srk::g_opt_conv_ring = (int)value;
     return SRK_OK;
   }

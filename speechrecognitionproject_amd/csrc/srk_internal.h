@@ -104,12 +104,16 @@ extern int g_opt_conv_fused_db;
 // the pooled conv's backward gathers the pooled gradient through the argmax ("conv_unpool_gather",
 // default 1; 0 = unpool into library scratch first)
 extern int g_opt_conv_unpool_gather;
+// 16-bit-source modes: the pooled conv's backward writes the dense dY straight as its 16-bit copy
+// ("conv_unpool16", default 1; 0 = dense fp32 dY, then the 16-bit conversion and column sums)
+extern int g_opt_conv_unpool16;
 // conv tile shape ("conv_tile": 128 = 128-row tiles of 4 waves, 256 = 256-row tiles of 8 waves on
 // tall convolutions)
 extern int g_opt_conv_tile;
 // LDS-DMA ring implicit-GEMM convolutions where the shape qualifies ("conv_ring": a mask of
 // 1 / 2 / 4 = fp32 forward / data gradient / weight gradient, 16 / 32 / 64 = the same on 16-bit
-// operands; default 6 — measured, r04ab)
+// operands, 128 = also the 16-bit forward with the pooled epilogue; default 0x76 — measured, r04ab /
+// r04ab3: fp32 ring forward and 16-bit pooled ring forward slower)
 extern int g_opt_conv_ring;
 // K1 MFCC variant ("mfcc_variant", bitwise-identical outputs): bit 0 = the untangle's partner exchange
 // by DPP row_mirror instead of ds_bpermute, bit 1 = twiddles in registers instead of LDS (default 3)
@@ -121,6 +125,8 @@ extern int g_opt_gemm_streamk;
 extern int g_opt_gemm16_persistent;
 // k-steps per section of the 16-bit ping-pong GEMM ("gemm16_qs": 1 = 8 MFMAs per section, 2 = 16)
 extern int g_opt_gemm16_qs;
+// 16-bit ping-pong GEMM: static priority for waves 4-7 instead of per-section flips ("gemm16_prio")
+extern int g_opt_gemm16_prio;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

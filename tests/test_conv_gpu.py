@@ -75,7 +75,7 @@ def test_conv2d_ring_vs_torch(gpu, shape):
         _lib.set_option("conv_ring", 7)
         _check_conv(*shape)
     finally:
-        _lib.set_option("conv_ring", 6)
+        _lib.set_option("conv_ring", 0x76)
 
 
 @pytest.mark.parametrize("shape", [  # 1-D strided convs of model_resnet_bgru.py:48,19-23 as H=1
@@ -132,7 +132,7 @@ def test_conv1_pool_fused_vs_torch(gpu, N, H, W, KH, KW, pool):
     (2, 3, 8, 128, 64, 1, 7, 0, 3),        # a few rows, deep k: the split-K forward (dense, then pooled)
     (3, 5, 12, 8, 36, 3, 3, 1, 1),         # 3 x 3 taps, N not a tile multiple
 ])
-@pytest.mark.parametrize("gather,ring", [(1, 0), (0, 0), (0, 6), (0, 7)])
+@pytest.mark.parametrize("gather,ring", [(1, 0), (0, 0), (0, 6), (0, 7), (0, 0x76), (0, 0xf6)])
 def test_conv_pool_fused_equals_separate(gpu, gather, ring, precision, N, H, W, Ci, Co, KH, KW, ph, pw):
     """conv + bias + MaxPool2d((1, 4)) in one launch (srk_conv2d_nhwc_fwd_pool: pooled epilogue and
     uint8 argmax; the backward unpools through the argmax) == the separate conv and maxpool kernels
@@ -166,11 +166,16 @@ def test_conv_pool_fused_equals_separate(gpu, gather, ring, precision, N, H, W, 
             outs.append([t.detach().cpu() for t in (y, xm.grad, conv.weight.grad, conv.bias.grad)])
     finally:
         _lib.set_option("conv_unpool_gather", 1)
-        _lib.set_option("conv_ring", 6)
+        _lib.set_option("conv_ring", 0x76)
         _lib.set_fused_conv_pool(True)
         _lib.set_matmul_precision("fp32")
-    for a, c in zip(*outs):
-        assert torch.equal(a, c)
+    for i, (a, c) in enumerate(zip(*outs)):
+        if i == 3 and precision != "fp32":
+            # 16-bit modes (option conv_unpool16): the fused backward sums the bias gradient over the
+            # pooled rows, the separate one over the dense dY (the same values and zeros, another order)
+            assert rel_err(a.numpy(), c.numpy()) <= 1e-5
+        else:
+            assert torch.equal(a, c)
     if precision == "fp32":
         xr, wr, br = (t.clone().requires_grad_(True) for t in (x.permute(0, 3, 1, 2), w, b))
         yr = F.max_pool2d(F.conv2d(xr, wr, br, padding=(ph, pw)), (1, 4))
@@ -365,3 +370,44 @@ def test_resnet_bgru_mode1_vs_reference_golden(gpu):
             assert np.abs(gv).max() <= 1e-5 and np.abs(g["gval__" + k]).max() <= 1e-5, k
             continue
         assert rel_err(gv, g["gval__" + k]) <= 5e-3, k
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("N,H,W,Ci,Co,KH,KW,ph,pw", [(4, 98, 40, 64, 128, 1, 7, 0, 3), (2, 3, 8, 128, 64, 1, 7, 0, 3)])
+def test_conv_pool_unpool16(gpu, prec, N, H, W, Ci, Co, KH, KW, ph, pw):
+    """16-bit modes: the pooled conv's backward writing the dense dY straight as its 16-bit operand copy
+    (option conv_unpool16 = 1: no dense fp32 dY, bias gradient from the pooled gradient) == the dense
+    fp32 dY + 16-bit conversion path (0): the same rounded operands, so dx / dW bitwise; db to fp32
+    summation order."""
+    from speechrecognitionproject_amd import _lib
+    g = torch.Generator().manual_seed(N * 5 + Co + Ci)
+    x = torch.randn(N, H, W, Ci, generator=g)
+    w = torch.randn(Co, Ci, KH, KW, generator=g) / (Ci * KH * KW) ** 0.5
+    b = torch.randn(Co, generator=g)
+    Wo = W + 2 * pw - KW + 1
+    gy = torch.randn(N, H + 2 * ph - KH + 1, Wo // 4, Co, generator=g).cuda()
+    conv = snn.Conv2d(Ci, Co, (KH, KW), padding=(ph, pw)).cuda()
+    pool = snn.MaxPool2d((1, 4))
+    outs = []
+    try:
+        _lib.set_matmul_precision(prec)
+        for u16 in (1, 0):
+            _lib.set_option("conv_unpool16", u16)
+            with torch.no_grad():
+                conv.weight.copy_(w)
+                conv.bias.copy_(b)
+            conv.weight.grad = conv.bias.grad = None
+            xm = x.cuda().requires_grad_(True)
+            y = snn.conv_pool(xm, conv, pool)
+            (y * gy).sum().backward()
+            torch.cuda.synchronize()
+            outs.append([t.detach().cpu() for t in (y, xm.grad, conv.weight.grad, conv.bias.grad)])
+    finally:
+        _lib.set_option("conv_unpool16", 1)
+        _lib.set_matmul_precision("fp32")
+    for i, (a, c) in enumerate(zip(*outs)):
+        assert torch.isfinite(a).all()
+        if i == 3:
+            assert rel_err(a.numpy(), c.numpy()) <= 1e-5
+        else:
+            assert torch.equal(a, c), i

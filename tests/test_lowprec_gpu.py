@@ -295,7 +295,8 @@ def test_conv_16bit_sources_bit_identical(prec, shape):
     SAME bits as rounding the fp32 gathers at LDS-store time (0): same rounding, same MFMA order.
     The bias gradient is the exception by design: the fp32-gather path sums it inside the
     weight-gradient kernel (conv_fused_db), the 16-bit-source path with the column-sum kernel — the
-    same fp32 values in another order (1e-5)."""
+    same fp32 values in another order (1e-5).  (The 16-bit LDS-DMA ring kernels, conv_ring bits 4-6, read
+    the 16-bit copies only: test_conv_16bit_ring holds them to these kernels.)"""
     from speechrecognitionproject_amd import nn as snn
     N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw = shape
     g = torch.Generator().manual_seed(N * 31 + Co + KW)
@@ -306,6 +307,7 @@ def test_conv_16bit_sources_bit_identical(prec, shape):
     gy = torch.randn(N, Ho, Wo, Co, generator=g).cuda()
     outs = []
     try:
+        _lib.set_option("conv_ring", 6)   # the register-staged 16-bit kernels on both sides (no 16-bit ring)
         for on in (0, 1):
             _lib.set_option("conv16_sources", on)
             xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
@@ -318,6 +320,7 @@ def test_conv_16bit_sources_bit_identical(prec, shape):
             outs.append((ym.detach(), xm.grad, wm.grad, bm.grad))
     finally:
         _lib.set_option("conv16_sources", 1)
+        _lib.set_option("conv_ring", 0x76)
         _lib.prof_enable(0)
     for a, c in zip(outs[0][:3], outs[1][:3]):
         assert torch.equal(a, c)
@@ -561,12 +564,12 @@ def test_gemm16_persistent(prec, ta, tb, M, N, K, beta):
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0)])
-@pytest.mark.parametrize("M,N,K,beta", [(5120, 3328, 520, 0.0), (1300, 700, 2056, 2.0), (2560, 2560, 8, 0.0)])
+@pytest.mark.parametrize("M,N,K,beta", [(5120, 3328, 520, 0.0), (1304, 712, 2056, 2.0), (2560, 2560, 8, 0.0)])
 def test_gemm16_qs(prec, ta, tb, M, N, K, beta):
     """srk option gemm16_qs = 2: the 16-bit ping-pong GEMM with one whole 32-deep K-tile per section
     (16 MFMAs, half the barriers) == the 16-deep sections bit for bit (each accumulator adds the same
     k-steps in the same order) and == float64 of the 16-bit values (k tails: 520, 8; row / column
-    edges: 1300 x 700; split-K: 2056)."""
+    edges: 1304 x 712; split-K: 2056)."""
     g = torch.Generator().manual_seed(M + 3 * N + K + tb)
     dt = TORCH_DT[prec]
     A = torch.randn((K, M) if ta else (M, K), generator=g).to(dt)
@@ -579,18 +582,20 @@ def test_gemm16_qs(prec, ta, tb, M, N, K, beta):
     outs = []
     try:
         _lib.set_option("gemm16_kernel", 2)
-        for qs in (2, 1):
+        for qs, prio in ((2, 0), (1, 1), (1, 0)):   # 32-deep sections; static priority (gemm16_prio); baseline
             _lib.set_option("gemm16_qs", qs)
+            _lib.set_option("gemm16_prio", prio)
             Cd = C0.clone().cuda()
             call("srk_gemm_16", ta, tb, M, N, K, 0.5, ptr(Ad), Ad.shape[1], ptr(Bd), Bd.shape[1], beta, ptr(Cd), N,
                  None, 0, stream_ptr())
             outs.append(Cd.cpu())
     finally:
         _lib.set_option("gemm16_qs", 1)
+        _lib.set_option("gemm16_prio", 0)
         _lib.set_option("gemm16_kernel", 0)
     scale = (opA.abs() @ opB.abs()).max().item()
     assert (outs[0].double() - ref).abs().max().item() <= 2e-6 * (1 + scale)
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[2])
 
 
 @pytest.mark.parametrize("shape", [(2, 98, 40, 64, 128, 1, 7, 0, 3), (3, 98, 1, 256, 512, 7, 1, 3, 0),
@@ -618,6 +623,6 @@ def test_conv_16bit_ring(prec, shape):
             torch.cuda.synchronize()
             outs.append([t.detach().double() for t in (ym, xm.grad, wm.grad, bm.grad)])
     finally:
-        _lib.set_option("conv_ring", 6)
+        _lib.set_option("conv_ring", 0x76)
     for a, c in zip(*outs):
         assert ((a - c).abs().max() / c.abs().max()).item() <= 1e-5

@@ -1370,9 +1370,12 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
   const bool lp = prec != kPrecF32;
   // fp32 operands (option bits 0..2), or the 16-bit operand copies of the S16 path (bits 4..6)
   if (!(g_opt_conv_ring & (1 << (MODE + (lp ? 4 : 0)))) || c.dy_arg || (lp != (c.a16 != nullptr))) return 1;
-  // the 16-bit pooled forward (fbanks_cnn conv2) measured slower on the ring (r04ab3: 2.89 vs 2.68 ms
-  // per 5 cfg3 steps): only with bit 7
-  if (lp && MODE == kFwd && c.pool_w && !(g_opt_conv_ring & 0x80)) return 1;
+  // the pooled forward (fbanks_cnn conv2) measured slower on the ring (r04ab: fp32; r04ab3: 16-bit, 2.89
+  // vs 2.68 ms per 5 cfg3 steps): only with bit 7
+  if (MODE == kFwd && c.pool_w && !(g_opt_conv_ring & 0x80)) return 1;
+  // fp32 forward: faster on the deep-K ResNet layers (r04ab6, cfg4: 64000 x 512 x 7680 and 128000 x 256 x
+  // 3840 -8 %), slower on fbanks_cnn conv4 (50176 x 512 x 1792: +2 %)
+  if (!lp && MODE == kFwd && c.K < 3072 && !(g_opt_conv_ring & 0x80)) return 1;
   const int RBK = lp ? kR16BK : kRBK, unit = lp ? 8 : 4, esz = lp ? 2 : 4;
   const int chans = MODE == kDgrad ? c.Co : c.Ci;
   if (MODE != kWgrad && chans % RBK) return 1;

@@ -62,6 +62,7 @@ struct GruPArgs {
   unsigned spin_limit;   // s_sleep polls before a wait gives up (~2 s by default)
   unsigned dc_offset;    // fp32 two-chain kernels: chain 1 starts this many s_memrealtime ticks (10 ns) late
   int fast_cell;         // fp32 two-chain forward: hardware exp / rcp in the cell (v_exp_f32, v_rcp_f32)
+  int dc_prio;           // fp32 two-chain kernels: 0 = equal priority, 1 / 2 = chain 0 / 1 at s_setprio 1
 };
 
 size_t fwd_lds_bytes(int H);
@@ -81,6 +82,7 @@ extern int g_opt_gru_lp2;                      // 16-bit recurrence on 32 x 32 w
 extern int g_opt_gru_dc;                       // fp32 recurrence: two independent row chains per workgroup (default 1)
 extern unsigned g_opt_gru_dc_offset;            // chain-1 start delay (ticks of 10 ns), default 200 (2 us)
 extern int g_opt_gru_fast_cell;                 // fp32 two-chain forward: hardware exp / rcp cell math (default 1)
+extern int g_opt_gru_dc_prio;                   // fp32 two-chain kernels: static priority of one chain (0, 1, 2)
 // Batch rows per bias-gradient partial of the 16-bit backward kernel (32 or 64; 256-row launch chunks).
 int gru_bias_part_rows(int64_t B);
 // Host-pinned health word (device-mapped pointer in *dev): non-zero once any persistent-kernel

@@ -657,12 +657,16 @@ __device__ __forceinline__ void dc_stamp_chain1(const GruPArgs& a, int step) {
     a.trace[((size_t)blockIdx.x * a.T + step) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
 }
 
-// optional phase offset between the two chains: chain 1 starts a.dc_offset ticks late
+// optional phase offset between the two chains: chain 1 starts a.dc_offset ticks late; optional static
+// priority of one chain (a.dc_prio = 1 + c): the two waves of a SIMD then do not split the matrix pipe
+// evenly when their MFMA phases overlap — the favoured chain runs its phase at full rate and the other
+// fills the gaps, which holds the chains out of phase (MI355X_MICROARCH.md, two waves per SIMD)
 __device__ __forceinline__ void dc_chain_delay(const GruPArgs& a, int c) {
   if (c == 1 && a.dc_offset) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (__builtin_amdgcn_s_memrealtime() - t0 < a.dc_offset) __builtin_amdgcn_s_sleep(2);
   }
+  if (a.dc_prio == 1 + c) __builtin_amdgcn_s_setprio(1);
 }
 
 constexpr int kDcXF = 24;   // floats a lane hands its pair partner: 3 gate accumulators x 4 rows (+ the fused projection's)
@@ -2099,6 +2103,7 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     ac.xcd_local = g_opt_gru_xcd_local;
     ac.dc_offset = g_opt_gru_dc_offset;
     ac.fast_cell = g_opt_gru_fast_cell;
+    ac.dc_prio = g_opt_gru_dc_prio;
     ac.b_begin = c0;
     ac.b_end = std::min(a.B, c0 + rows_per_launch);
     ac.G = (ac.b_end - c0 + rows_g - 1) / rows_g;

@@ -25,7 +25,7 @@ int g_opt_conv16_sources = 1;
 int g_opt_conv_fused_db = 1;
 int g_opt_conv_unpool_gather = 1;
 int g_opt_conv_tile = 128;
-int g_opt_conv_ring = 0x76;
+int g_opt_conv_ring = 0x77;
 int g_opt_conv_unpool16 = 1;
 int g_opt_mfcc_variant = 3;
 int g_opt_gemm_streamk = 1;
@@ -43,6 +43,7 @@ int g_opt_gru_lp_wide = 1;
 int g_opt_gru_dc = 1;
 unsigned g_opt_gru_dc_offset = 200;
 int g_opt_gru_fast_cell = 1;
+int g_opt_gru_dc_prio = 0;
 int g_opt_gru_dwhh_batched = 1;
 int g_opt_gemm_skinny = 1;
 std::atomic<int64_t> g_scratch_gen{0};
@@ -390,10 +391,10 @@ int srk_set_option(const char* name, int64_t value) {
     return SRK_OK;
   }
   if (n == "conv_ring") {   // ring conv kernels where the shape qualifies: bits 0-2 fp32 fwd / dgrad / wgrad, 4-6 16-bit,
-                            // 7 the 16-bit pooled forward too
+                            // 7 the pooled forward too
     SRK_REQUIRE(value >= 0 && value <= 0xf7, SRK_ERR_INVALID,
                 "conv_ring is a mask of 1 / 2 / 4 (fp32 fwd / dgrad / wgrad), 16 / 32 / 64 (16-bit) and 128 "
-                "(16-bit pooled forward)");
+                "(the pooled forward too)");
     srk::g_opt_conv_ring = (int)value;
     return SRK_OK;
   }
@@ -435,6 +436,11 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "gru_dc_offset_ns") {   // fp32 two-chain kernels: delay chain 1's start (phase offset between the chains)
     SRK_REQUIRE(value >= 0 && value <= 1000000, SRK_ERR_INVALID, "gru_dc_offset_ns out of range");
     srk::g_opt_gru_dc_offset = (unsigned)(value / 10);
+    return SRK_OK;
+  }
+  if (n == "gru_dc_prio") {   // fp32 two-chain kernels: 0 equal priority, 1 / 2 chain 0 / 1 at s_setprio 1 (static)
+    SRK_REQUIRE(value >= 0 && value <= 2, SRK_ERR_INVALID, "gru_dc_prio must be 0, 1 or 2");
+    srk::g_opt_gru_dc_prio = (int)value;
     return SRK_OK;
   }
   if (n == "gru_fp32_fast_cell") {   // fp32 two-chain forward: v_exp_f32 / v_rcp_f32 cell nonlinearities

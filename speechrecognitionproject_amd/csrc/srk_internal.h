@@ -112,8 +112,9 @@ extern int g_opt_conv_unpool16;
 extern int g_opt_conv_tile;
 // LDS-DMA ring implicit-GEMM convolutions where the shape qualifies ("conv_ring": a mask of
 // 1 / 2 / 4 = fp32 forward / data gradient / weight gradient, 16 / 32 / 64 = the same on 16-bit
-// operands, 128 = also the 16-bit forward with the pooled epilogue; default 0x76 — measured, r04ab /
-// r04ab3: fp32 ring forward and 16-bit pooled ring forward slower)
+// operands, 128 = the forward with the pooled epilogue and the fp32 forward at K < 3072 too; default
+// 0x77 — measured, r04ab / r04ab3 / r04ab6: the pooled ring forward slower in both precisions, the fp32
+// ring forward faster on the deep-K ResNet layers only)
 extern int g_opt_conv_ring;
 // K1 MFCC variant ("mfcc_variant", bitwise-identical outputs): bit 0 = the untangle's partner exchange
 // by DPP row_mirror instead of ds_bpermute, bit 1 = twiddles in registers instead of LDS (default 3)

@@ -72,10 +72,10 @@ def test_conv2d_ring_vs_torch(gpu, shape):
     counts % 16, >= 128 output columns, stride 1 for the data gradient); the rest as before."""
     from speechrecognitionproject_amd import _lib
     try:
-        _lib.set_option("conv_ring", 7)
+        _lib.set_option("conv_ring", 0x87)   # every qualifying shape, any K
         _check_conv(*shape)
     finally:
-        _lib.set_option("conv_ring", 0x76)
+        _lib.set_option("conv_ring", 0x77)
 
 
 @pytest.mark.parametrize("shape", [  # 1-D strided convs of model_resnet_bgru.py:48,19-23 as H=1
@@ -132,7 +132,7 @@ def test_conv1_pool_fused_vs_torch(gpu, N, H, W, KH, KW, pool):
     (2, 3, 8, 128, 64, 1, 7, 0, 3),        # a few rows, deep k: the split-K forward (dense, then pooled)
     (3, 5, 12, 8, 36, 3, 3, 1, 1),         # 3 x 3 taps, N not a tile multiple
 ])
-@pytest.mark.parametrize("gather,ring", [(1, 0), (0, 0), (0, 6), (0, 7), (0, 0x76), (0, 0xf6)])
+@pytest.mark.parametrize("gather,ring", [(1, 0), (0, 0), (0, 6), (0, 0x87), (0, 0x77), (0, 0xf7)])
 def test_conv_pool_fused_equals_separate(gpu, gather, ring, precision, N, H, W, Ci, Co, KH, KW, ph, pw):
     """conv + bias + MaxPool2d((1, 4)) in one launch (srk_conv2d_nhwc_fwd_pool: pooled epilogue and
     uint8 argmax; the backward unpools through the argmax) == the separate conv and maxpool kernels
@@ -166,7 +166,7 @@ def test_conv_pool_fused_equals_separate(gpu, gather, ring, precision, N, H, W, 
             outs.append([t.detach().cpu() for t in (y, xm.grad, conv.weight.grad, conv.bias.grad)])
     finally:
         _lib.set_option("conv_unpool_gather", 1)
-        _lib.set_option("conv_ring", 0x76)
+        _lib.set_option("conv_ring", 0x77)
         _lib.set_fused_conv_pool(True)
         _lib.set_matmul_precision("fp32")
     for i, (a, c) in enumerate(zip(*outs)):

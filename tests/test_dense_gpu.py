@@ -358,7 +358,8 @@ def test_bigru_fp32_dual_chain_matches_four_wave(gpu, B, T, IN):
     LDS, per-wave flags, a 3-slot hand-off ring; option gru_fp32_dual_chain, default on) against the
     4-wave kernels: the same cell math with the recurrent k sum split in two halves (2e-5 relative), the fused layer-0
     projection (IN <= 64) and the gi-GEMM path, full / partial / chunked (B = 300, 512) grids; and
-    run twice — bitwise the same both times (deterministic order, flags and ring reset per launch)."""
+    run twice — bitwise the same both times (deterministic order, flags and ring reset per launch), and
+    with either chain at static priority (option gru_dc_prio) — bitwise the same again."""
     from speechrecognitionproject_amd import _lib
     H = 512
     torch.manual_seed(5)
@@ -367,8 +368,10 @@ def test_bigru_fp32_dual_chain_matches_four_wave(gpu, B, T, IN):
     w = torch.randn(B, T, 2 * H)
     outs = {}
     try:
-        for mode in (1, 1, 0):
+        # (two-chain, static chain priority): the priority (option gru_dc_prio) changes timing only
+        for mode, prio in ((1, 0), (1, 0), (0, 0), (1, 1), (1, 2)):
             _lib.set_option("gru_fp32_dual_chain", mode)
+            _lib.set_option("gru_dc_prio", prio)
             mine.zero_grad()
             xm = x.cuda().requires_grad_(True)
             ym, _ = mine(xm)
@@ -376,9 +379,11 @@ def test_bigru_fp32_dual_chain_matches_four_wave(gpu, B, T, IN):
             outs.setdefault(mode, []).append([ym.detach().cpu(), xm.grad.cpu()] + [p.grad.cpu() for p in mine.parameters()])
     finally:
         _lib.set_option("gru_fp32_dual_chain", 1)
+        _lib.set_option("gru_dc_prio", 0)
     assert _lib.spin_timeouts() == 0
-    for a, b in zip(outs[1][0], outs[1][1]):
-        assert torch.equal(a, b)
+    for k in (1, 2, 3):
+        for a, b in zip(outs[1][0], outs[1][k]):
+            assert torch.equal(a, b)
     for i, (a, b) in enumerate(zip(outs[1][0], outs[0][0])):
         err = float((a - b).abs().max() / (b.abs().max() + 1e-30))
         assert err <= 2e-5, (i, err)

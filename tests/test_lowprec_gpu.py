@@ -320,7 +320,7 @@ def test_conv_16bit_sources_bit_identical(prec, shape):
             outs.append((ym.detach(), xm.grad, wm.grad, bm.grad))
     finally:
         _lib.set_option("conv16_sources", 1)
-        _lib.set_option("conv_ring", 0x76)
+        _lib.set_option("conv_ring", 0x77)
         _lib.prof_enable(0)
     for a, c in zip(outs[0][:3], outs[1][:3]):
         assert torch.equal(a, c)
@@ -623,6 +623,6 @@ def test_conv_16bit_ring(prec, shape):
             torch.cuda.synchronize()
             outs.append([t.detach().double() for t in (ym, xm.grad, wm.grad, bm.grad)])
     finally:
-        _lib.set_option("conv_ring", 0x76)
+        _lib.set_option("conv_ring", 0x77)
     for a, c in zip(*outs):
         assert ((a - c).abs().max() / c.abs().max()).item() <= 1e-5

@@ -17,10 +17,15 @@ import torch  # noqa: E402
 from speechrecognitionproject_amd import _lib  # noqa: E402
 from speechrecognitionproject_amd import nn as snn  # noqa: E402
 
+DEFAULTS = {"gru_fp32_dual_chain": 1, "gru_dc_offset_ns": 2000, "gru_fp32_fast_cell": 1, "gru_dc_prio": 0}
 VARIANTS = {"dc": {"gru_fp32_dual_chain": 1, "gru_dc_offset_ns": 0, "gru_fp32_fast_cell": 0},
             "dc_off2us": {"gru_dc_offset_ns": 2000}, "dc_off4us": {"gru_dc_offset_ns": 4000},
             "dc_fast": {"gru_dc_offset_ns": 0, "gru_fp32_fast_cell": 1},
-            "4wave": {"gru_fp32_dual_chain": 0, "gru_fp32_fast_cell": 0}}
+            "4wave": {"gru_fp32_dual_chain": 0, "gru_fp32_fast_cell": 0},
+            # round 4: static priority of one chain (defaults otherwise)
+            "default": {}, "prio_c0": {"gru_dc_prio": 1}, "prio_c1": {"gru_dc_prio": 2},
+            "prio_c0_off0": {"gru_dc_prio": 1, "gru_dc_offset_ns": 0},
+            "prio_c1_off0": {"gru_dc_prio": 2, "gru_dc_offset_ns": 0}}
 
 
 def run(B, T, IN, reps, opts):
@@ -54,13 +59,13 @@ def main():
     ap.add_argument("--B", type=int, default=256)
     ap.add_argument("--T", type=int, default=51)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--variants", default=",".join(VARIANTS), help="comma-separated names (each on top of the defaults)")
     a = ap.parse_args()
-    for name, opts in VARIANTS.items():
+    for name in a.variants.split(","):
         for IN in (39, 1024):
-            print(name, "IN=%d" % IN, json.dumps(run(a.B, a.T, IN, a.reps, opts)), flush=True)
-    _lib.set_option("gru_fp32_dual_chain", 1)
-    _lib.set_option("gru_dc_offset_ns", 0)
-    _lib.set_option("gru_fp32_fast_cell", 0)
+            print(name, "IN=%d" % IN, json.dumps(run(a.B, a.T, IN, a.reps, dict(DEFAULTS, **VARIANTS[name]))), flush=True)
+    for k, v in DEFAULTS.items():
+        _lib.set_option(k, v)
 
 
 if __name__ == "__main__":

@@ -16,6 +16,7 @@
 //   fwd:  gi [B*T, 6H] | gates [2][T][B][4H] (r, z, n, W_hn h + b_hn)       — kept for backward
 //   bwd:  dgi [B*T, 6H] | dgh [2][B][T][3H] | dgh_edge [2][B][3H] | dhz [2][B][H]
 #include <algorithm>
+#include <mutex>
 
 #include "gemm.h"
 #include "gru_internal.h"
@@ -389,6 +390,49 @@ __global__ void dbias_reduce_kernel(const float* __restrict__ part, int nparts, 
   db_hh[i] = accumulate ? db_hh[i] + sh : sh;
 }
 
+// dW_hh[dir] (+)= sum over the fused backward's partials [part][2 dir][3H][H], in part order
+// (deterministic); 4 consecutive columns per thread
+// (part p = chunk * 8 + group covers batch rows 256 chunk + 32 group ..; parts past the batch were never
+// written and are skipped)
+__global__ void dwhh_reduce_kernel(const float* __restrict__ part, int nparts, int B, int64_t per_dir,
+                                   float* __restrict__ dw, int accumulate) {
+  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over [2 dir][3H][H] / 4
+  if (i4 * 4 >= 2 * per_dir) return;
+  const int64_t o = i4 * 4, dir = o / per_dir, e = o - dir * per_dir;
+  v4f acc = accumulate ? *reinterpret_cast<const v4f*>(dw + o) : v4f{0.f, 0.f, 0.f, 0.f};
+  for (int p = 0; p < nparts; ++p) {
+    if ((p / 8) * 256 + (p % 8) * 32 >= B) continue;
+    acc += *reinterpret_cast<const v4f*>(part + ((size_t)p * 2 + dir) * per_dir + e);
+  }
+  *reinterpret_cast<v4f*>(dw + o) = acc;
+}
+
+// grow-only scratch of the fused backward's dW_hh partials (graph-safe: bumps g_scratch_gen on growth)
+struct GruScratch {
+  float* p = nullptr;
+  size_t floats = 0;
+};
+GruScratch g_gs[64];
+std::mutex g_gs_mu;
+
+int gru_scratch(size_t floats, float** out) {
+  int dev = 0;
+  SRK_CHECK_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_gs_mu);
+  GruScratch& sc = g_gs[dev & 63];
+  if (sc.floats < floats) {
+    if (sc.p) {
+      SRK_CHECK_HIP(hipDeviceSynchronize());
+      SRK_CHECK_HIP(hipFree(sc.p));
+    }
+    sc.floats = floats + floats / 4;
+    SRK_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&sc.p), sc.floats * sizeof(float)));
+    g_scratch_gen.fetch_add(1);
+  }
+  *out = sc.p;
+  return SRK_OK;
+}
+
 inline int64_t pad4(int64_t v) { return (v + 3) / 4 * 4; }
 inline bool padded_in(int64_t in) { return in % 4 != 0; }
 int pad_cols(const float* src, int64_t rows, int64_t cols, float* dst, hipStream_t s) {
@@ -400,6 +444,18 @@ int pad_cols(const float* src, int64_t rows, int64_t cols, float* dst, hipStream
 }
 
 }  // namespace
+
+int release_gru_scratch() {
+  std::lock_guard<std::mutex> lk(g_gs_mu);
+  SRK_CHECK_HIP(hipDeviceSynchronize());
+  for (GruScratch& sc : g_gs) {
+    if (sc.p) SRK_CHECK_HIP(hipFree(sc.p));
+    sc.p = nullptr;
+    sc.floats = 0;
+  }
+  g_scratch_gen.fetch_add(1);
+  return SRK_OK;
+}
 }  // namespace srk
 
 using srk::GemmDesc;
@@ -576,7 +632,20 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
     p.xbuf = ws + bwd_xbuf_off(B, T, H);
     p.counters = reinterpret_cast<unsigned*>(ws + bwd_counter_off(B, T, H));
     int rc;
+    // the recurrent weight gradient accumulated inside the recurrence kernel (partials per row group)
+    const int dw_parts = srk::gru_dwhh_fused_parts(B, T);
+    if (dw_parts) {
+      if ((rc = srk::gru_scratch((size_t)dw_parts * 2 * 3 * H * H, &p.dw_part))) return rc;
+      p.y16_in = y16;
+    }
     if ((rc = srk::gru_persistent_launch(p, true, s))) return rc;
+    if (dw_parts) {
+      const int64_t per_dir = 3 * H * H, n4 = 2 * per_dir / 4;
+      srk::ProfScope prof("gru_dwhh_reduce", s, 4.0 * (dw_parts + 2) * 2 * per_dir);
+      hipLaunchKernelGGL(srk::dwhh_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, p.dw_part,
+                         dw_parts, (int)B, per_dir, dw_hh, (int)accumulate);
+      SRK_CHECK_HIP(hipGetLastError());
+    }
     const int prows = srk::gru_bias_part_rows(B);
     hipLaunchKernelGGL(srk::dbias_reduce_kernel, dim3((unsigned)((6 * H + 255) / 256)), dim3(256), 0, s, part,
                        (int)(chunks * (256 / prows)), (int)B, (int)H, prows, db_ih, db_hh, accumulate);
@@ -607,7 +676,9 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
       g.B16 = y16;                           // dir 1: y16 + 3H (row 1, reverse half)
       g.C = dw_hh; g.ldc = H; g.beta = beta;
       g.batch = 2; g.sA = BT * 3 * H - 3 * H; g.sB = 3 * H; g.sC = 3 * H * H;
-      if (g.K > 0 && srk::g_opt_gru_dwhh_batched) {
+      if (dw_parts) {
+        // done: the recurrence kernel accumulated it (dwhh_reduce_kernel above)
+      } else if (g.K > 0 && srk::g_opt_gru_dwhh_batched) {
         if ((rc = srk::gemm_f32(g, s))) return rc;
       } else if (g.K > 0) {   // one launch per direction (A/B and tests)
         g.batch = 1;

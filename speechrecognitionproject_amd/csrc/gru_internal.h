@@ -63,6 +63,11 @@ struct GruPArgs {
   unsigned dc_offset;    // fp32 two-chain kernels: chain 1 starts this many s_memrealtime ticks (10 ns) late
   int fast_cell;         // fp32 two-chain forward: hardware exp / rcp in the cell (v_exp_f32, v_rcp_f32)
   int dc_prio;           // fp32 two-chain kernels: 0 = equal priority, 1 / 2 = chain 0 / 1 at s_setprio 1
+  // 16-bit backward with the recurrent weight gradient fused in (gru_dwhh_fused_parts): h_prev in 16 bit
+  // (the forward's y16) and the per-(chunk, row group) partial dW_hh [part][2 dir][3H][H], summed by
+  // dwhh_reduce_kernel
+  const uint16_t* y16_in;
+  float* dw_part;
 };
 
 size_t fwd_lds_bytes(int H);
@@ -85,6 +90,11 @@ extern int g_opt_gru_fast_cell;                 // fp32 two-chain forward: hardw
 extern int g_opt_gru_dc_prio;                   // fp32 two-chain kernels: static priority of one chain (0, 1, 2)
 // Batch rows per bias-gradient partial of the 16-bit backward kernel (32 or 64; 256-row launch chunks).
 int gru_bias_part_rows(int64_t B);
+// Partials of dW_hh the 16-bit backward kernel would write with the fused recurrent weight gradient
+// (option gru_dwhh_fused; 32 x 32 workgroups, 256-row chunks): chunks x 8, or 0 when it does not apply
+// (fp32, the 64-row workgroups of B > 256, the kernel not fitting one workgroup per CU, T < 2).
+int gru_dwhh_fused_parts(int64_t B, int64_t T);
+extern int g_opt_gru_dwhh_fused;               // fused recurrent weight gradient in the 16-bit backward (default 1)
 // Host-pinned health word (device-mapped pointer in *dev): non-zero once any persistent-kernel
 // spin-wait has given up; read without a device synchronization by srk_health_check.
 int health_word(unsigned** host, unsigned** dev);

@@ -1123,6 +1123,8 @@ struct RecOps<true> {
 };
 typedef float v8f __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4_ __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
 
 template <bool F16>
 __device__ __forceinline__ u32x4 pack8(v8f v) {
@@ -1763,9 +1765,120 @@ __global__ __launch_bounds__(128 * RB, 1) void gru_fwd_persistent_lp2_kernel(Gru
 }
 
 // LDS: W^T slice [32][3H + 16] 16-bit (unit jj, gate row c) | dT [16 RB][3][36] | dI [16 RB][36] |
-// exchange [2 RB waves][16][kXP2] | bias partials [2 RB waves][4][16]
-template <int H, bool F16, int RB>
-__global__ __launch_bounds__(128 * RB, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs a) {
+// exchange [2 RB waves][16][kXP2] | bias partials [2 RB waves][4][16] | (DW) dg image [32 rows][96] 16-bit |
+// (DW) h_prev images [4 worker waves][32 rows][128 columns] 16-bit
+//
+// DW (RB = 2, option gru_dwhh_fused): the recurrent weight gradient dW_hh = sum_t dg_t^T h_(t-1) is
+// accumulated by this kernel instead of by a GEMM over the stored dgh16 / y16 afterwards.  The workgroup
+// gets 4 more waves (one more per SIMD) that do only that: after each step's publish barrier, worker
+// wave w multiplies the workgroup's 96 gate rows (3 gates x the slice's 32 units) of dg_t^T [96 x 32 rows]
+// by h_prev [32 rows x columns 128 w .. + 127] on v_mfma_f32_16x16x32 (the 32 batch rows are the k of
+// one MFMA), 6 x 8 accumulator tiles held for the whole sequence — the recurrence waves' matrix pipe is
+// idle through their hand-off waits, and their registers are untouched.  Operands are [row][column]
+// 16-bit LDS images read with ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group, delivered
+// column-major: 8 consecutive rows of one column per lane = the operand fragment): the dg image is
+// written by the cell (rounded exactly as the dgh16 the GEMM read); each worker fetches its own h_prev
+// columns (the forward's y16 rows, zero past the batch) by LDS-DMA one step ahead into a private image,
+// so its loads never sit in front of a recurrence wave's flag poll.  The workers keep the recurrence
+// waves' barrier count (prologue, exchange, cell, publish, bias partials).  At the end each worker
+// writes its partial [96][128] to dw_part[chunk * 8 + group][dir]; dwhh_reduce_kernel sums the
+// partials in part order.
+constexpr int kDgP = 96;   // dg image row pitch (16-bit elements)
+// h_prev image of one worker: [32 rows][8 granules of 32 B]; granule g of row r at g ^ dw_swz(r): the
+// 4 rows of a 16-lane transposed read and the two groups of a 32-lane half (8 rows apart) fall in 8
+// distinct 32-B bank windows
+__device__ __forceinline__ int dw_swz(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
+
+// The DW worker waves (wave 4 + w): see above.  Barrier sequence = the recurrence waves'.
+template <int H, bool F16>
+__device__ __forceinline__ void dw_worker(const GruPArgs& a, const unsigned short* Aimg, unsigned char* Bimg, int dir,
+                                          int group, int j0, int b0, int b_last, int w, int lane) {
+  const int T = a.T;
+  unsigned char* img = Bimg + w * 32 * 256;   // this worker's [32][256 B]
+  typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+  const uint64_t ya = (uint64_t)(uintptr_t)a.y16_in;
+  const u32x4s rsY{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)ya),
+                   (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(ya >> 32)), 0x7ffffff0u, 0x00020000u};
+  const unsigned zero = 0;
+  // h_prev of step s: y16 rows (b, tprev), columns dir H + 128 w .. + 127; DMA instruction i fills rows
+  // 4 i .. 4 i + 3 (1 KB, lane-linear at M0 + 16 lane), so lane l fetches the unit the swizzle puts there
+  auto dma = [&](int s) {
+    const int t = dir == 0 ? T - 1 - s : s, tprev = dir == 0 ? t - 1 : t + 1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = 4 * i + (lane >> 4), g = ((lane & 15) >> 1) ^ dw_swz(row);
+      const int col = 128 * w + 16 * g + 8 * (lane & 1);
+      const unsigned v = b0 + row <= b_last
+                             ? (unsigned)(((((size_t)(b0 + row) * T + tprev) * 2 * H + dir * H) + col) * 2)
+                             : 0x80000000u;
+      const unsigned ldsa = (unsigned)__builtin_amdgcn_readfirstlane(
+          (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)(img + i * 1024));
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(v), "s"(rsY), "s"(ldsa), "s"(zero)
+                   : "memory");
+    }
+  };
+  typedef __attribute__((address_space(3))) s16x4_ lds_s16x4;
+  auto tr4 = [](const void* p) { return __builtin_bit_cast(u32x2_, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p)); };
+  f32x4 acc[6][8];
+#pragma unroll
+  for (int m = 0; m < 6; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g4 = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, r0 = 8 * g4 + q;
+  // raw s_barrier: __syncthreads() would first drain this wave's LDS-DMA (vmcnt(0)) and hold the
+  // recurrence waves' barrier behind the next step's h_prev fetch
+  auto bar = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  bar();   // = the prologue barrier (W slice in LDS)
+  if (T > 1) dma(0);
+  for (int step = 0; step < T; ++step) {
+    if (step > 0) bar();   // = the k-half exchange
+    bar();                 // = the cell barrier: this step's dg image is complete
+    bar();                 // = the publish (lp2_arrive)
+    if (step == T - 1) continue;     // the edge step: h_prev = 0
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this step's h_prev image (its DMA was issued a step ago)
+    u32x4 af[6];
+#pragma unroll
+    for (int mb = 0; mb < 6; ++mb) {
+      const u32x2_ lo = tr4(Aimg + r0 * kDgP + 16 * mb + 4 * p4);
+      const u32x2_ hi = tr4(Aimg + (r0 + 4) * kDgP + 16 * mb + 4 * p4);
+      af[mb] = u32x4{lo.x, lo.y, hi.x, hi.y};
+    }
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) {
+      const unsigned char* bb = img + r0 * 256 + 32 * (nb ^ dw_swz(r0)) + 8 * p4;   // row r0 + 4: the same swizzle
+      const u32x2_ lo = tr4(bb);
+      const u32x2_ hi = tr4(bb + 4 * 256);
+      const u32x4 bf = u32x4{lo.x, lo.y, hi.x, hi.y};
+#pragma unroll
+      for (int mb = 0; mb < 6; ++mb)
+        acc[mb][nb] = RecOps<F16>::mma(__builtin_bit_cast(typename RecOps<F16>::e8, af[mb]),
+                                       __builtin_bit_cast(typename RecOps<F16>::e8, bf), acc[mb][nb]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // image reads done: the next DMA may overwrite
+    if (step + 1 < T - 1) dma(step + 1);
+  }
+  bar();   // = the bias-partials barrier
+  float* dst = a.dw_part + ((size_t)(a.chunk * 8 + group) * 2 + dir) * 3 * H * H;
+#pragma unroll
+  for (int mb = 0; mb < 6; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = (mb >> 1) * H + j0 + 16 * (mb & 1) + 4 * (lane >> 4) + r, col = 128 * w + 16 * nb + (lane & 15);
+        dst[(size_t)row * H + col] = acc[mb][nb][r];
+      }
+}
+
+template <int H, bool F16, int RB, bool DW = false>
+__global__ __launch_bounds__(DW ? 512 : 128 * RB, 1) void gru_bwd_persistent_lp2_kernel(GruPArgs a) {
   using Ops = RecOps<F16>;
   using e8 = typename Ops::e8;
   constexpr int U = kUnits2, S = H / U, WPQ = lp2_bwd_wpq<H>(), DTP = U + 4, NKB = 3 * H / 32, KS = S / 2;
@@ -1776,6 +1889,9 @@ __global__ __launch_bounds__(128 * RB, 1) void gru_bwd_persistent_lp2_kernel(Gru
   float* dI = dT + ROWS * 3 * DTP;             // [ROWS][DTP]: dan (dgi's third gate; dT holds dan * r)
   float* X = dI + ROWS * DTP;                  // [NW][16][kXP2]
   float* red = X + NW * 16 * kXP2;             // [NW][4][16]
+  unsigned short* Aimg = reinterpret_cast<unsigned short*>(red + NW * 4 * 16);   // DW: [32][kDgP]
+  unsigned char* Bimg = reinterpret_cast<unsigned char*>(Aimg + 32 * kDgP);      // DW: [4 workers][32][256 B]
+  static_assert(!DW || (RB == 2 && H == 512), "fused dW_hh: 32-row workgroups, H = 512");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
   const int rb = wave % RB, kh = wave / RB;
   int dir, group, slice;
@@ -1786,6 +1902,12 @@ __global__ __launch_bounds__(128 * RB, 1) void gru_bwd_persistent_lp2_kernel(Gru
   const bool per = a.flags || local;
   const int T = a.T, B = a.B, j0 = slice * U, ju = kh * 16 + lr, j = j0 + ju;
   const int b0 = a.b_begin + group * ROWS, b_last = a.b_end - 1, rbase = b0 + rb * 16;
+  if constexpr (DW) {
+    if (wave >= NW) {   // the dW worker waves
+      dw_worker<H, F16>(a, Aimg, Bimg, dir, group, j0, b0, b_last, wave - NW, lane);
+      return;
+    }
+  }
 
   {  // W_hh[dir][c][j0 .. j0+31] for all 3H rows c, transposed [jj][c] in 8-deep c packs
     const float* W = a.w_hh + (size_t)dir * 3 * H * H;
@@ -1887,6 +2009,14 @@ __global__ __launch_bounds__(128 * RB, 1) void gru_bwd_persistent_lp2_kernel(Gru
       dT[(rl * 3 + 1) * DTP + ju] = daz;
       dT[(rl * 3 + 2) * DTP + ju] = dan * rg;
       dI[rl * DTP + ju] = dan;
+      if constexpr (DW) {   // the dg image of the dW workers, rounded as the dgh16 the dW GEMM reads; rows past
+                            // the batch are zeros (their hand-off input is never written: 0 x garbage = NaN)
+        using E1 = typename std::conditional<F16, _Float16, __bf16>::type;
+        const bool in_batch = b <= b_last;
+        Aimg[rl * kDgP + ju] = in_batch ? __builtin_bit_cast(unsigned short, (E1)dar) : (unsigned short)0;
+        Aimg[rl * kDgP + 32 + ju] = in_batch ? __builtin_bit_cast(unsigned short, (E1)daz) : (unsigned short)0;
+        Aimg[rl * kDgP + 64 + ju] = in_batch ? __builtin_bit_cast(unsigned short, (E1)(dan * rg)) : (unsigned short)0;
+      }
       if (b <= b_last) {
         sb[0] += dar;
         sb[1] += daz;
@@ -1949,10 +2079,11 @@ size_t lds_bytes(int H, bool backward, int prec) {
   return std::max<size_t>(need, 96 * 1024);
 }
 
-size_t lp2_lds_bytes(int H, bool backward, int RB) {
+size_t lp2_lds_bytes(int H, bool backward, int RB, bool dw = false) {
   const size_t rows = 16 * RB, nw = 2 * RB, xp = (RB == 2 ? kFusedIn : 40) + 1;
   const size_t need = backward ? (size_t)kUnits2 * ((3 * H + 16) / 8) * 16 + rows * 3 * (kUnits2 + 4) * 4 +
-                                     rows * (kUnits2 + 4) * 4 + nw * 16 * kXP2 * 4 + nw * 4 * 16 * 4
+                                     rows * (kUnits2 + 4) * 4 + nw * 16 * kXP2 * 4 + nw * 4 * 16 * 4 +
+                                     (dw ? (size_t)32 * kDgP * 2 + (size_t)4 * 32 * 256 : 0)
                                : (size_t)3 * kUnits2 * ((H + 16) / 8) * 16 + rows * (kUnits2 + 4) * 4 +
                                      (size_t)3 * kUnits2 * xp * 4 + nw * 3 * 16 * kXP2 * 4;
   return std::max<size_t>(need, 96 * 1024);   // one workgroup per CU (see lds_bytes)
@@ -1972,6 +2103,29 @@ const void* lp2_kernel_ptr(bool backward, int prec, int RB) {
                     : reinterpret_cast<const void*>(gru_fwd_persistent_lp2_kernel<H, true, 2>);
   return backward ? reinterpret_cast<const void*>(gru_bwd_persistent_lp2_kernel<H, false, 2>)
                   : reinterpret_cast<const void*>(gru_fwd_persistent_lp2_kernel<H, false, 2>);
+}
+
+template <int H>
+const void* lp2_dw_kernel_ptr(int prec) {
+  return prec == kPrecF16 ? reinterpret_cast<const void*>(gru_bwd_persistent_lp2_kernel<H, true, 2, true>)
+                          : reinterpret_cast<const void*>(gru_bwd_persistent_lp2_kernel<H, false, 2, true>);
+}
+
+template <int H>
+int lp2_dw_occupancy_ok(int prec) {
+  static std::mutex mu;
+  static int occ[3] = {-1, -1, -1};
+  std::lock_guard<std::mutex> lk(mu);
+  int& o = occ[prec];
+  if (o < 0) {
+    const void* k = lp2_dw_kernel_ptr<H>(prec);
+    const size_t lds = lp2_lds_bytes(H, true, 2, true);
+    o = 0;
+    if (lds <= 160 * 1024 && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess)
+      SRK_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, 512, lds));
+    (void)hipGetLastError();
+  }
+  return o >= 1 ? 1 : 0;
 }
 
 template <int H>
@@ -2073,6 +2227,13 @@ bool lp2_wide(int64_t B, int prec, bool backward, int in_fused) {
          lp2_occupancy_ok<512>(backward, prec, 4) > 0;
 }
 
+int gru_dwhh_fused_parts(int64_t B, int64_t T) {
+  const int prec = matmul_prec();
+  if (!g_opt_gru_dwhh_fused || prec == kPrecF32 || !g_opt_gru_lp2 || T < 2 || lp2_wide(B, prec, true, 0)) return 0;
+  if (lp2_dw_occupancy_ok<512>(prec) <= 0) return 0;
+  return (int)((B + 255) / 256) * 8;
+}
+
 int gru_bias_part_rows(int64_t B) {
   const int prec = matmul_prec();
   if (lp2_wide(B, prec, true, 0)) return 64;
@@ -2114,7 +2275,7 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     ProfScope prof(backward ? (prec == kPrecF32 ? "gru_bwd_seq" : "gru_bwd_seq_lp")
                             : (prec == kPrecF32 ? "gru_fwd_seq" : "gru_fwd_seq_lp"), s, flops);
     prof.detail("gru_%s_persistent%s_kernel B%d T%d chunk%d", backward ? "bwd" : "fwd",
-                dc ? "_dc" : wide ? "_lp2w" : lp2 ? "_lp2" : (prec == kPrecF32 ? "" : "_lp"),
+                dc ? "_dc" : wide ? "_lp2w" : lp2 ? (backward && ac.dw_part ? "_lp2dw" : "_lp2") : (prec == kPrecF32 ? "" : "_lp"),
                 ac.b_end - c0, a.T, ac.chunk);
     if (dc && backward)
       hipLaunchKernelGGL((gru_bwd_persistent_dc_kernel<512>), grid, dim3(512), dc_bwd_lds_floats(512) * 4, s, ac);
@@ -2122,7 +2283,11 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
       hipLaunchKernelGGL((gru_fwd_persistent_dc_kernel<512, true>), grid, dim3(512), dc_fwd_lds_floats(512) * 4, s, ac);
     else if (dc)
       hipLaunchKernelGGL((gru_fwd_persistent_dc_kernel<512, false>), grid, dim3(512), dc_fwd_lds_floats(512) * 4, s, ac);
-    else if (lp2)
+    else if (lp2 && backward && ac.dw_part) {   // with the fused recurrent weight gradient (gru_dwhh_fused_parts)
+      SRK_REQUIRE(!wide && ac.y16_in, SRK_ERR_INTERNAL, "gru persistent: fused dW_hh needs the 32-row kernel and y16");
+      hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(lp2_dw_kernel_ptr<512>(prec))), grid,
+                         dim3(512), lp2_lds_bytes(512, true, 2, true), s, ac);
+    } else if (lp2)
       hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(lp2_kernel_ptr<512>(backward, prec, wide ? 4 : 2))),
                          grid, dim3(wide ? 512 : 256), lp2_lds_bytes(512, backward, wide ? 4 : 2), s, ac);
     else

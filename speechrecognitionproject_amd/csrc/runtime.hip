@@ -44,6 +44,7 @@ int g_opt_gru_dc = 1;
 unsigned g_opt_gru_dc_offset = 200;
 int g_opt_gru_fast_cell = 1;
 int g_opt_gru_dc_prio = 0;
+int g_opt_gru_dwhh_fused = 1;
 int g_opt_gru_dwhh_batched = 1;
 int g_opt_gemm_skinny = 1;
 std::atomic<int64_t> g_scratch_gen{0};
@@ -348,6 +349,7 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "release_scratch") {   // free the library's grow-only scratch buffers (invalidates captured graphs)
     if (int rc = srk::release_gemm_scratch()) return rc;
     if (int rc = srk::release_conv_scratch()) return rc;
+    if (int rc = srk::release_gru_scratch()) return rc;
     return srk::release_bn_scratch();
   }
   if (n == "gru_persistent") {
@@ -436,6 +438,10 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "gru_dc_offset_ns") {   // fp32 two-chain kernels: delay chain 1's start (phase offset between the chains)
     SRK_REQUIRE(value >= 0 && value <= 1000000, SRK_ERR_INVALID, "gru_dc_offset_ns out of range");
     srk::g_opt_gru_dc_offset = (unsigned)(value / 10);
+    return SRK_OK;
+  }
+  if (n == "gru_dwhh_fused") {   // 16-bit backward: dW_hh accumulated in the recurrence kernel (1) or by a GEMM (0)
+    srk::g_opt_gru_dwhh_fused = value != 0;
     return SRK_OK;
   }
   if (n == "gru_dc_prio") {   // fp32 two-chain kernels: 0 equal priority, 1 / 2 chain 0 / 1 at s_setprio 1 (static)

@@ -89,6 +89,7 @@ extern std::atomic<int64_t> g_scratch_gen;
 int release_gemm_scratch();
 int release_conv_scratch();
 int release_bn_scratch();
+int release_gru_scratch();
 extern int g_opt_gemm16_kernel;
 // Kernel of the fp32 GEMM (srk_set_option "gemm32_kernel"): 0 = by shape, 1 = register-staged
 // gemm_f32_kernel, 2 = LDS-DMA ping-pong gemm_p32_kernel.

@@ -626,3 +626,52 @@ def test_conv_16bit_ring(prec, shape):
         _lib.set_option("conv_ring", 0x77)
     for a, c in zip(*outs):
         assert ((a - c).abs().max() / c.abs().max()).item() <= 1e-5
+
+
+@pytest.mark.parametrize("B,T,IN,wide", [(256, 51, 39, 1), (256, 9, 1024, 1), (200, 6, 39, 1), (300, 5, 1024, 0),
+                                         (64, 2, 24, 1)])
+def test_bigru_dwhh_fused_matches_gemm(prec, B, T, IN, wide):
+    """Option gru_dwhh_fused: the 16-bit backward recurrence kernel accumulates dW_hh itself (4 extra
+    worker waves, dg_t^T h_prev on the matrix cores after each step's publish, per-(chunk, row group)
+    partials summed in order) instead of the batched GEMM over dgh16 / y16.  Same rounded operands, other
+    fp32 summation order: dW_hh within 1e-5 of the GEMM path (relative to its largest element), every
+    other gradient and the output unchanged.  Shapes: the cfg2 layer-0 (fused projection) and layer-1
+    inputs, a partial last row group, two 256-row chunks (64-row workgroups off), T = 2."""
+    from speechrecognitionproject_amd import nn as snn
+    H = 512
+    torch.manual_seed(11)
+    mine = snn.BiGRU(IN, H, num_layers=1).cuda()
+    x = torch.randn(B, T, IN, device="cuda")
+    w = torch.randn(B, T, 2 * H, device="cuda")
+    res = []
+    try:
+        _lib.set_matmul_precision(prec)
+        _lib.set_option("gru_lp_wide", wide)
+        for fused in (1, 0):
+            _lib.set_option("gru_dwhh_fused", fused)
+            mine.zero_grad()
+            xm = x.clone().requires_grad_(True)
+            _lib.prof_enable(True)
+            ym, _ = mine(xm)
+            (ym * w).sum().backward()
+            torch.cuda.synchronize()
+            kinds = [k["kernel"] for k in _lib.prof_kernels()]
+            _lib.prof_enable(False)
+            if fused:   # the fused kernel ran and no dW_hh GEMM did
+                assert any("_lp2dw" in k for k in kinds), kinds
+                assert not any("1536x512" in k for k in kinds), kinds
+            res.append({"y": ym.detach().clone(), "dx": xm.grad.clone(),
+                        **{n: p.grad.detach().clone() for n, p in mine.named_parameters()}})
+    finally:
+        _lib.set_option("gru_dwhh_fused", 1)
+        _lib.set_option("gru_lp_wide", 1)
+        _lib.set_matmul_precision("fp32")
+    assert _lib.spin_timeouts() == 0
+    for n in res[0]:
+        a, b = res[0][n], res[1][n]
+        assert torch.isfinite(a).all(), n
+        if "weight_hh" in n:
+            err = float((a - b).abs().max() / b.abs().max())
+            assert err <= 1e-5, (n, err)
+        else:
+            assert torch.equal(a, b), n

@@ -32,11 +32,16 @@ GROUPS = {  # srk_prof name -> substrings of the rocprof kernel symbols it cover
 
 
 def _conv_group(name):
-    """conv_gemm_kernel<MODE, BM, BN, BK, VEC, VECB, LP, S16>: MODE 0/1/2 = fwd/dgrad/wgrad, LP != 0 = 16-bit."""
+    """conv_gemm_kernel<MODE, BM, BN, BK, VEC, VECB, LP, S16>: MODE 0/1/2 = fwd/dgrad/wgrad, LP != 0 = 16-bit;
+    the LDS-DMA ring kernels conv_ring_kernel<MODE, BN> (fp32) and conv_ring16_kernel<MODE, BN, LP> (16-bit)."""
+    modes = ("conv_fwd", "conv_dgrad", "conv_wgrad")
     m = re.search(r"conv_gemm_kernel<(\d+),[^,]*,[^,]*,[^,]*,[^,]*,[^,]*,\s*(\d+)", name)
-    if not m:
-        return None
-    return ("conv_fwd", "conv_dgrad", "conv_wgrad")[int(m.group(1))] + ("_lp" if m.group(2) != "0" else "")
+    if m:
+        return modes[int(m.group(1))] + ("_lp" if m.group(2) != "0" else "")
+    m = re.search(r"conv_ring(16)?_kernel<(\d+)", name)
+    if m:
+        return modes[int(m.group(2))] + ("_lp" if m.group(1) else "")
+    return None
 
 
 def _gemm_group(name):
@@ -83,6 +88,8 @@ def main():
     ap.add_argument("--precisions", default="fp32", help="comma list: the precisions the command timed")
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--sync-bn", action="store_true")
+    ap.add_argument("--merge", action="store_true",
+                    help="add to an existing -o file of the same model / batch / world / options (another precision)")
     a = ap.parse_args()
     f, w = collect(a.fetch, "FETCH_SIZE"), collect(a.write, "WRITE_SIZE")
     # bench.py reports this traffic only for a command with the same model / batch / world / options
@@ -95,6 +102,14 @@ def main():
         wb = 1024.0 * w[g][1] / w[g][0]
         res["bytes_per_launch"][g] = {"fetch": round(fb), "write": round(wb), "total": round(fb + wb),
                                       "launches": f[g][0]}
+    if a.merge and os.path.exists(a.o):
+        with open(a.o) as fh:
+            old = json.load(fh)
+        oc, nc = old.get("command", {}), res["command"]
+        if all(oc.get(k) == nc[k] for k in ("model", "batch", "world", "sync_bn")):
+            nc["precisions"] = sorted(set(oc.get("precisions", [])) | set(nc["precisions"]))
+            res["source"] = "%s + %s" % (old.get("source", ""), a.source)
+            res["bytes_per_launch"] = dict(old.get("bytes_per_launch", {}), **res["bytes_per_launch"])
     with open(a.o, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))

@@ -61,7 +61,13 @@ int srk_prof_kernels(char* buf, int64_t cap, int64_t* needed);
  * 2 LDS-DMA ping-pong (same results up to fp32 summation order; for A/B measurements and tests);
  * "gemm32_kernel" (default 0 = by shape) = the same choice for the fp32 GEMM;
  * "conv16_sources" (default 1) = bf16 / fp16 convolutions gather from one pre-rounded 16-bit copy
- * of their operands (0 = round at LDS-store time; bit-identical results either way). */
+ * of their operands (0 = round at LDS-store time; bit-identical results either way);
+ * "conv_ring" (default 0x77) = the LDS-DMA ring implicit-GEMM convolutions where the shape
+ * qualifies (bits 0-2 fp32 fwd / dgrad / wgrad, 4-6 the same in 16 bit, 7 also the pooled forward
+ * and the fp32 forward at K < 3072); "conv_unpool16" (default 1) = the 16-bit pooled-conv backward
+ * writes the dense dY straight as its 16-bit operand copy; "gru_dwhh_fused" (default 1) = the 16-bit
+ * BiGRU backward accumulates dW_hh inside the recurrence kernel (0 = a GEMM over dgh16 / y16) —
+ * results equal up to fp32 summation order (A/B measurements and tests). */
 int srk_set_option(const char* name, int64_t value);
 /* Number of bounded spin-waits of the persistent kernels that gave up (synchronizes the
  * device; must stay 0 — a non-zero value means a co-residency assumption failed).  -1 on error. */

@@ -13,9 +13,11 @@ synthetic clips when no Kaggle tree is available, ``--data-path/--output-path`` 
 hard-coded paths (:21-24), ``--log-every`` batches loss lines to avoid a host sync per step,
 ``--loader device`` (default for WAV trees) replaces the per-item DataLoader with native batched
 decode + one on-device augmentation launch per batch, and torchrun environments train
-data-parallel (one process per GPU, RCCL all-reduce).  On one GPU, full-size batches after the
-first two run as replays of a HIP graph of the step (the batch is copied into the graph's static
-input first; a short last batch runs eagerly; ``--no-graph`` disables it) — the same kernels in the
+data-parallel (one process per GPU, RCCL all-reduce).  Full-size batches after the first two run as
+replays of a HIP graph of the step (the batch is copied into the graph's static input first; a short
+last batch runs eagerly; ``--no-graph`` disables it; data-parallel over RCCL the bucketed all-reduces
+are captured in the graph too, DESIGN.md §4, with an eager fallback every rank agrees on if the
+capture fails) — the same kernels in the
 same order, so for models without dropout the same arithmetic bit for bit
 (tests/test_graphs_gpu.py, tests/test_training_gpu.py); with dropout a replay draws its mask from
 the device counter on top of the last eager seed, so masks (not the arithmetic) differ from
@@ -60,8 +62,8 @@ def parse(argv=None):
     p.add_argument('--no-overlap', dest='overlap', action='store_false',
                    help='data-parallel: one all-reduce after backward instead of overlapped buckets')
     p.add_argument('--no-graph', dest='graph', action='store_false',
-                   help='single GPU: run every step eagerly instead of replaying a HIP graph of the step for '
-                        'full-size batches (speechrecognitionproject_amd/graphs.py)')
+                   help='run every step eagerly instead of replaying a HIP graph of the step for full-size '
+                        'batches (speechrecognitionproject_amd/graphs.py; data-parallel: RCCL all-reduces in the graph)')
     p.add_argument('--loader', choices=('device', 'torch'), default='device',
                    help='WAV datasets: device = native batched decode + K10 on-device augmentation '
                         '(DeviceBatchLoader); torch = per-item Dataset.__getitem__ through DataLoader')
@@ -129,10 +131,13 @@ def _train(args):
     os.makedirs(args.output_path, exist_ok=True)
     loss_file = os.path.join(args.output_path, 'loss_' + key + '.txt')
 
-    use_graph = args.graph and world == 1
+    # data-parallel steps are captured whole (collectives included) over RCCL only: gloo cannot be
+    # captured, and the CPU-only gloo runs have no HIP graphs anyway
+    use_graph = args.graph and (world == 1 or torch.distributed.get_backend() == 'nccl')
     graphed = None          # GraphedStep of a full-batch step (captured after two eager full steps)
     static = {}
     full_eager = 0
+    captures = 0
     side = None
 
     def eager_step(x, y):
@@ -209,7 +214,31 @@ def _train(args):
                         # the last warm-up loss still holds its step's autograd graph (and with it the
                         # side stream's AccumulateGrad nodes): drop it before the capture
                         loss = None
-                        graphed = GraphedStep(graph_body, warmup=0)   # warmed up by the side-stream steps
+                        failed = 0
+                        try:   # warmed up by the side-stream steps
+                            graphed = GraphedStep(graph_body, warmup=0,
+                                                  capture_error_mode='thread_local' if world > 1 else 'global')
+                        except Exception as e:   # noqa: BLE001 — a DP capture failure: every rank falls back
+                            if world == 1 or captures:
+                                raise
+                            print('training: capturing the data-parallel step failed (%s: %s); running eagerly'
+                                  % (type(e).__name__, e), flush=True)
+                            failed = 1
+                        if world > 1 and not captures:
+                            # the first capture happens at the same batch on every rank: agree on the
+                            # outcome (a later re-capture is rank-local — rank 0's evaluation can move a
+                            # scratch buffer — and its collectives are captured, not run, so no exchange)
+                            flag = torch.tensor([failed], device=device)
+                            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
+                            if flag.item():
+                                graphed, use_graph = None, False
+                        captures += 1
+                    if graphed is None:   # the DP capture fell back: this batch eagerly
+                        loss = eager_step(x, y)
+                        pending.append(loss.detach())
+                        if len(pending) >= args.log_every:
+                            flush()
+                        continue
                     static['x'].copy_(x, non_blocking=True)
                     static['y'].copy_(y, non_blocking=True)
                     loss = graphed.replay()

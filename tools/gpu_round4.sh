@@ -26,8 +26,10 @@ stats() {   # stats NAME ARGS...: kernel-trace stats of one config's bench comma
   && stats cfg2 && stats cfg3 --model fbanks_cnn --no-lowprec --steps 10 \
   && stats cfg4 --model resnet_bgru --no-lowprec --steps 4 && stats cfg5 --model spec_bgru --precision fp16 --steps 20 \
   && stats mfrn --model mfrn_bgru --no-lowprec --steps 10 \
+  && stats cfg3b --model fbanks_cnn --precision bf16 --no-lowprec --steps 10 \
+  && stats cfg4b --model resnet_bgru --precision bf16 --no-lowprec --steps 4 \
   && echo "stats ok"
 rc=$?
-rm -rf "$OUT"/stats_cfg* "$OUT"/stats_mfrn
+rm -rf "$OUT"/stats_cfg2 "$OUT"/stats_cfg3 "$OUT"/stats_cfg4 "$OUT"/stats_cfg5 "$OUT"/stats_cfg3b "$OUT"/stats_cfg4b "$OUT"/stats_mfrn
 echo "exit $rc"
 exit $rc

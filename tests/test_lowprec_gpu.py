@@ -634,7 +634,7 @@ def test_bigru_dwhh_fused_matches_gemm(prec, B, T, IN, wide):
     """Option gru_dwhh_fused: the 16-bit backward recurrence kernel accumulates dW_hh itself (4 extra
     worker waves, dg_t^T h_prev on the matrix cores after each step's publish, per-(chunk, row group)
     partials summed in order) instead of the batched GEMM over dgh16 / y16.  Same rounded operands, other
-    fp32 summation order: dW_hh within 1e-5 of the GEMM path (relative to its largest element), every
+    fp32 summation order: dW_hh within 1e-5 of the GEMM path norm-wise, every
     other gradient and the output unchanged.  Shapes: the cfg2 layer-0 (fused projection) and layer-1
     inputs, a partial last row group, two 256-row chunks (64-row workgroups off), T = 2."""
     from speechrecognitionproject_amd import nn as snn
@@ -671,7 +671,12 @@ def test_bigru_dwhh_fused_matches_gemm(prec, B, T, IN, wide):
         a, b = res[0][n], res[1][n]
         assert torch.isfinite(a).all(), n
         if "weight_hh" in n:
-            err = float((a - b).abs().max() / b.abs().max())
+            # two fp32 summation orders of up to B (T - 1) = 12.8k products of either sign (GEMM: 32-deep
+            # k-tiles in 10 split-K slabs; fused: 32-row MFMA k-steps accumulated over T, then 8 row-group
+            # partials); element-wise the cancellation amplifies that (measured up to 3.3e-5 of the largest
+            # element, fp16 at B = 200, T = 6), so the bound is norm-wise; a missing or doubled row group /
+            # step would be O(1e-1)
+            err = float((a - b).norm() / b.norm())
             assert err <= 1e-5, (n, err)
         else:
             assert torch.equal(a, b), n

@@ -110,7 +110,7 @@ LP_KERNELS = ("gemm_bf16", "gemm_f16", "gru_fwd_seq_lp", "gru_bwd_seq_lp", "conv
               "conv_wgrad_lp")
 OTHER_KERNELS = ("mfcc", "fbank", "spec", "noise_mix", "adam", "grad_check", "batchnorm_fwd", "batchnorm_bwd", "conv1_pool_fwd",
                  "conv1_pool_wgrad",
-                 "maxpool_fwd", "maxpool_bwd", "conv_to16", "conv_unpool16")
+                 "maxpool_fwd", "maxpool_bwd", "conv_to16", "conv_unpool16", "gru_dwhh_reduce")
 
 
 def log(*a):

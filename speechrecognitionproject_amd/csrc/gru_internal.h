@@ -95,6 +95,7 @@ int gru_bias_part_rows(int64_t B);
 // (fp32, the 64-row workgroups of B > 256, the kernel not fitting one workgroup per CU, T < 2).
 int gru_dwhh_fused_parts(int64_t B, int64_t T);
 extern int g_opt_gru_dwhh_fused;               // fused recurrent weight gradient in the 16-bit backward (default 1)
+extern int g_opt_gru_fwd_worker;               // 16-bit forward: output / input worker waves (default 0 until measured)
 // Host-pinned health word (device-mapped pointer in *dev): non-zero once any persistent-kernel
 // spin-wait has given up; read without a device synchronization by srk_health_check.
 int health_word(unsigned** host, unsigned** dev);

@@ -1534,14 +1534,110 @@ template <int H> constexpr int lp2_fwd_wpq() { return (H + 16) / 8; }
 template <int H> constexpr int lp2_bwd_wpq() { return (3 * H + 16) / 8; }
 constexpr int kXP2 = 20;   // pitch of the k-half exchange tiles (16 columns + 4: conflict-free b32 writes)
 
+// OW (RB = 2, option gru_fwd_worker): the forward with 4 more waves (one more per SIMD) that take every
+// global access off the recurrence waves except the hand-off: vmcnt retires in order, so the y / y16 /
+// gate stores a recurrence wave issued after its publish, and (layer 1) its loads of the next step's gi,
+// held the answer of its next flag poll back behind their own latency.  The recurrence
+// waves now leave h in hT and the gates in an LDS tile; the workers store y, y16 and the gates after the
+// publish barrier, and (no fused projection) fetch gi two steps ahead by LDS-DMA into a double buffer
+// that reuses the fused projection's W_ih region.  Same arithmetic and outputs, bitwise.  The workers
+// keep the recurrence waves' barriers (prologue, exchange, cell, publish).
+template <int H, bool F16>
+__device__ __forceinline__ void fwd_worker(const GruPArgs& a, const float* hT, const float* Gt, float* GI, int dir,
+                                           int group, int j0, int b0, int b_last, int w, int lane) {
+  constexpr int U = kUnits2, HTP = U + 4;
+  const int T = a.T, tid = w * 64 + lane;   // 0 .. 255 over the 4 worker waves
+  const bool fused = a.x_in != nullptr;
+  auto bar = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+  auto rsrc_of = [](const void* p) {
+    const uint64_t ad = (uint64_t)(uintptr_t)p;
+    return u32x4s{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)ad),
+                  (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(ad >> 32)), 0x7ffffff0u, 0x00020000u};
+  };
+  const u32x4s rsG = rsrc_of(a.gi);   // the gi DMA (inline asm: a plain SGPR quad)
+  const __amdgpu_buffer_rsrc_t rsY = rsrc(a.y), rsGt = rsrc(a.gates),
+                               rsY16 = rsrc(a.y16 ? reinterpret_cast<const float*>(a.y16) : a.y);
+  const unsigned zero = 0;
+  // gi of step s (time t): [32 rows][3 gates][32 units] fp32 = 12 KB into buffer s & 1, i.e. [32 rows][24
+  // 16-B units]; DMA instruction k (0 .. 11 over the 4 workers, 1 KB each, lane-linear at M0 + 16 lane)
+  // fills units 64 k .. 64 k + 63 of that linear image
+  auto dma_gi = [&](int s) {
+    const int t = dir == 0 ? s : T - 1 - s;
+    float* buf = GI + (s & 1) * 32 * 96;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int k = 3 * w + i, unit = 64 * k + lane, row = unit / 24, g = (unit % 24) >> 3, q = unit & 7;
+      const unsigned v = b0 + row <= b_last
+                             ? (unsigned)((((size_t)(b0 + row) * T + t) * 6 * H + dir * 3 * H + g * H + j0 + 4 * q) * 4)
+                             : 0x80000000u;
+      const unsigned ldsa = (unsigned)__builtin_amdgcn_readfirstlane(
+          (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)(buf + 64 * k * 4));
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(v), "s"(rsG), "s"(ldsa), "s"(zero)
+                   : "memory");
+    }
+  };
+  // y / y16 / gates of step s from hT and the gate tile: 6 buffer stores per thread, always issued
+  // (rows past the batch go past num_records and are dropped) so the vmcnt count per step is fixed
+  auto store_out = [&](int s) {
+    const int t = dir == 0 ? s : T - 1 - s;
+    {
+      const int row = tid >> 3, u4 = (tid & 7) * 4;
+      const v4f yv = *reinterpret_cast<const v4f*>(hT + row * HTP + u4);
+      const bool ok = b0 + row <= b_last;
+      const size_t e = ((size_t)(b0 + row) * T + t) * 2 * H + dir * H + j0 + u4;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, yv), rsY, ok ? (int)(e * 4) : (int)0x80000000u, 0, 0);
+      typedef __attribute__((ext_vector_type(4))) typename std::conditional<F16, _Float16, __bf16>::type e4;
+      const u32x2_ y2 = __builtin_bit_cast(u32x2_, __builtin_convertvector(yv, e4));
+      __builtin_amdgcn_raw_buffer_store_b64(y2, rsY16, (ok && a.y16) ? (int)(e * 2) : (int)0x80000000u, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // cells (row, unit) = (c / 32, c % 32), c = tid + 256 i: unit-interleaved gates
+      const int c = tid + 256 * i, row = c >> 5, u = c & 31;
+      const v4f gv = *reinterpret_cast<const v4f*>(Gt + (row * 32 + u) * 4);
+      const bool ok = b0 + row <= b_last;
+      const size_t e = ((((size_t)dir * T + t) * a.B + b0 + row) * H + j0 + u) * 4;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, gv), rsGt, ok ? (int)(e * 4) : (int)0x80000000u, 0, 0);
+    }
+  };
+  if (!fused) {   // gi of step 0 before the prologue barrier (the recurrence waves' first cell follows it)
+    dma_gi(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  bar();   // = the prologue barrier
+  if (!fused && T > 1) dma_gi(1);
+  for (int step = 0; step < T; ++step) {
+    if (step > 0) {
+      // gi of this step landed (issued two steps ago): only the previous step's 6 stores and, when it
+      // issued one, its gi DMA (3) may still be in flight
+      if (!fused) {
+        if (step + 1 < T) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      }
+      bar();   // = the k-half exchange
+    }
+    bar();     // = the cell barrier: h and the gates of this step are in LDS
+    bar();     // = the publish (lp2_arrive)
+    store_out(step);
+    if (!fused && step + 2 < T) dma_gi(step + 2);   // into the buffer this step's cell has consumed
+  }
+}
+
 // RB row blocks of 16 per workgroup (2 x RB waves: wave = kh * RB + rb): RB = 2 is the 32 x 32
 // workgroup; RB = 4 (64 rows, 8 waves, the same W slice in LDS) runs a 512-row batch in ONE launch
 // where RB = 2 needs two chunks one after the other.  Per row the arithmetic is the same.
 template <int RB> constexpr int lp2_fused_in() { return RB == 2 ? kFusedIn : 40; }   // RB = 4: LDS fits 40
 // LDS: W slice [96][H + 16] 16-bit (row g * 32 + jj) | hT [16 RB][36] fp32 | W_ih slice [96][KF + 1] fp32 |
 // exchange [2 RB waves][3][16][kXP2] fp32
-template <int H, bool F16, int RB>
-__global__ __launch_bounds__(128 * RB, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs a) {
+template <int H, bool F16, int RB, bool OW = false>
+__global__ __launch_bounds__(OW ? 512 : 128 * RB, 1) void gru_fwd_persistent_lp2_kernel(GruPArgs a) {
   using Ops = RecOps<F16>;
   using e8 = typename Ops::e8;
   constexpr int U = kUnits2, S = H / U, WPQ = lp2_fwd_wpq<H>(), HTP = U + 4, NKB = H / 32, KH = NKB / 2;
@@ -1551,6 +1647,9 @@ __global__ __launch_bounds__(128 * RB, 1) void gru_fwd_persistent_lp2_kernel(Gru
   float* hT = smem + 3 * U * WPQ * 4;
   float* Wx = hT + ROWS * HTP;
   float* X = Wx + 3 * U * XP;
+  float* Gt = X + 2 * RB * 3 * 16 * kXP2;   // OW: the step's gates [32 rows][32 units][4]
+  float* GI = Wx;                           // OW without the fused projection: gi [2][32 rows][3][32]
+  static_assert(!OW || (RB == 2 && 2 * 32 * 96 <= 3 * U * XP), "forward worker: 32-row workgroups");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lq = lane >> 4;
   const int rb = wave % RB, kh = wave / RB;
   int dir, group, slice;
@@ -1561,6 +1660,12 @@ __global__ __launch_bounds__(128 * RB, 1) void gru_fwd_persistent_lp2_kernel(Gru
   const bool per = a.flags || local;
   const int T = a.T, j0 = slice * U, ju = kh * 16 + lr, j = j0 + ju;
   const int b0 = a.b_begin + group * ROWS, b_last = a.b_end - 1, rbase = b0 + rb * 16;
+  if constexpr (OW) {
+    if (wave >= 2 * RB) {   // the output / input worker waves
+      fwd_worker<H, F16>(a, hT, Gt, GI, dir, group, j0, b0, b_last, wave - 2 * RB, lane);
+      return;
+    }
+  }
 
   {  // this slice of W_hh[dir] (3 gates x 32 units), rounded to 16 bits -> LDS; loads issued 8 packs
      // at a time ahead of their stores (the prologue is a chain of L2 round trips otherwise)
@@ -1648,7 +1753,7 @@ __global__ __launch_bounds__(128 * RB, 1) void gru_fwd_persistent_lp2_kernel(Gru
   auto issue_inputs = [&](int step, int t) {
     if (fused) {
       if (step + 1 < T) load_x(a, dir == 0 ? t + 1 : t - 1, min(rbase + lr, b_last), lq, xnext);
-    } else {
+    } else if (!OW) {
       load_gi(t);
     }
   };
@@ -1733,6 +1838,16 @@ __global__ __launch_bounds__(128 * RB, 1) void gru_fwd_persistent_lp2_kernel(Gru
         stamp(a, step, 2);
       }
     }
+    if (OW && !fused) {   // this step's gi, fetched into LDS by the workers (landed before the exchange barrier)
+      const float* gib = GI + (step & 1) * 32 * 96;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = rb * 16 + lq * 4 + r;
+        gr[r] = gib[rl * 96 + ju];
+        gz[r] = gib[rl * 96 + 32 + ju];
+        gn[r] = gib[rl * 96 + 64 + ju];
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int rl = rb * 16 + lq * 4 + r;
@@ -1747,6 +1862,7 @@ __global__ __launch_bounds__(128 * RB, 1) void gru_fwd_persistent_lp2_kernel(Gru
       gsv[r][1] = zg;
       gsv[r][2] = ng;
       gsv[r][3] = ghn;
+      if constexpr (OW) *reinterpret_cast<v4f*>(Gt + (rl * 32 + ju) * 4) = v4f{rg, zg, ng, ghn};
     }
     __syncthreads();
     stamp(a, step, 3);
@@ -1760,7 +1876,7 @@ __global__ __launch_bounds__(128 * RB, 1) void gru_fwd_persistent_lp2_kernel(Gru
     }
     lp2_arrive(a, dir, group, slice, step, per, local);   // the hand-off only: y and the gates go out after it
     stamp(a, step, 4);
-    flush_outputs(step);
+    if constexpr (!OW) flush_outputs(step);   // OW: the worker waves store them
   }
 }
 
@@ -2079,13 +2195,14 @@ size_t lds_bytes(int H, bool backward, int prec) {
   return std::max<size_t>(need, 96 * 1024);
 }
 
-size_t lp2_lds_bytes(int H, bool backward, int RB, bool dw = false) {
+size_t lp2_lds_bytes(int H, bool backward, int RB, bool dw = false, bool ow = false) {
   const size_t rows = 16 * RB, nw = 2 * RB, xp = (RB == 2 ? kFusedIn : 40) + 1;
   const size_t need = backward ? (size_t)kUnits2 * ((3 * H + 16) / 8) * 16 + rows * 3 * (kUnits2 + 4) * 4 +
                                      rows * (kUnits2 + 4) * 4 + nw * 16 * kXP2 * 4 + nw * 4 * 16 * 4 +
                                      (dw ? (size_t)32 * kDgP * 2 + (size_t)4 * 32 * 256 : 0)
                                : (size_t)3 * kUnits2 * ((H + 16) / 8) * 16 + rows * (kUnits2 + 4) * 4 +
-                                     (size_t)3 * kUnits2 * xp * 4 + nw * 3 * 16 * kXP2 * 4;
+                                     (size_t)3 * kUnits2 * xp * 4 + nw * 3 * 16 * kXP2 * 4 +
+                                     (ow ? (size_t)32 * 32 * 4 * 4 : 0);
   return std::max<size_t>(need, 96 * 1024);   // one workgroup per CU (see lds_bytes)
 }
 
@@ -2109,6 +2226,29 @@ template <int H>
 const void* lp2_dw_kernel_ptr(int prec) {
   return prec == kPrecF16 ? reinterpret_cast<const void*>(gru_bwd_persistent_lp2_kernel<H, true, 2, true>)
                           : reinterpret_cast<const void*>(gru_bwd_persistent_lp2_kernel<H, false, 2, true>);
+}
+
+template <int H>
+const void* lp2_ow_kernel_ptr(int prec) {
+  return prec == kPrecF16 ? reinterpret_cast<const void*>(gru_fwd_persistent_lp2_kernel<H, true, 2, true>)
+                          : reinterpret_cast<const void*>(gru_fwd_persistent_lp2_kernel<H, false, 2, true>);
+}
+
+template <int H>
+int lp2_ow_occupancy_ok(int prec) {
+  static std::mutex mu;
+  static int occ[3] = {-1, -1, -1};
+  std::lock_guard<std::mutex> lk(mu);
+  int& o = occ[prec];
+  if (o < 0) {
+    const void* k = lp2_ow_kernel_ptr<H>(prec);
+    const size_t lds = lp2_lds_bytes(H, false, 2, false, true);
+    o = 0;
+    if (lds <= 160 * 1024 && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess)
+      SRK_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, 512, lds));
+    (void)hipGetLastError();
+  }
+  return o >= 1 ? 1 : 0;
 }
 
 template <int H>
@@ -2253,6 +2393,10 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     SRK_REQUIRE(false, SRK_ERR_INVALID, "gru persistent: the 32 x 32 kernels do not fit one workgroup per CU");
   // fp32 forward: the two-chain 8-wave kernel (same grid, W slice and outputs)
   const bool dc = prec == kPrecF32 && g_opt_gru_dc && dc_occupancy_ok<512>() > 0;
+  // 16-bit forward on 32-row workgroups: the output / input worker waves (option gru_fwd_worker; the gate
+  // store offsets are 32-bit buffer offsets)
+  const bool ow = lp2 && !backward && !wide && g_opt_gru_fwd_worker && a.y16 &&
+                  (double)2 * a.T * a.B * 4 * a.H * 4 < 2147483647.0 && lp2_ow_occupancy_ok<512>(prec) > 0;
   for (int c0 = 0; c0 < a.B; c0 += rows_per_launch) {
     GruPArgs ac = a;
     ac.trace = g_opt_gru_trace;
@@ -2275,7 +2419,7 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     ProfScope prof(backward ? (prec == kPrecF32 ? "gru_bwd_seq" : "gru_bwd_seq_lp")
                             : (prec == kPrecF32 ? "gru_fwd_seq" : "gru_fwd_seq_lp"), s, flops);
     prof.detail("gru_%s_persistent%s_kernel B%d T%d chunk%d", backward ? "bwd" : "fwd",
-                dc ? "_dc" : wide ? "_lp2w" : lp2 ? (backward && ac.dw_part ? "_lp2dw" : "_lp2") : (prec == kPrecF32 ? "" : "_lp"),
+                dc ? "_dc" : wide ? "_lp2w" : lp2 ? (backward && ac.dw_part ? "_lp2dw" : ow ? "_lp2ow" : "_lp2") : (prec == kPrecF32 ? "" : "_lp"),
                 ac.b_end - c0, a.T, ac.chunk);
     if (dc && backward)
       hipLaunchKernelGGL((gru_bwd_persistent_dc_kernel<512>), grid, dim3(512), dc_bwd_lds_floats(512) * 4, s, ac);
@@ -2287,6 +2431,9 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
       SRK_REQUIRE(!wide && ac.y16_in, SRK_ERR_INTERNAL, "gru persistent: fused dW_hh needs the 32-row kernel and y16");
       hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(lp2_dw_kernel_ptr<512>(prec))), grid,
                          dim3(512), lp2_lds_bytes(512, true, 2, true), s, ac);
+    } else if (lp2 && !backward && ow) {   // the forward with the output / input worker waves
+      hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(lp2_ow_kernel_ptr<512>(prec))), grid,
+                         dim3(512), lp2_lds_bytes(512, false, 2, false, true), s, ac);
     } else if (lp2)
       hipLaunchKernelGGL(reinterpret_cast<void (*)(GruPArgs)>(const_cast<void*>(lp2_kernel_ptr<512>(backward, prec, wide ? 4 : 2))),
                          grid, dim3(wide ? 512 : 256), lp2_lds_bytes(512, backward, wide ? 4 : 2), s, ac);

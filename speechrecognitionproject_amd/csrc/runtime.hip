@@ -45,6 +45,7 @@ unsigned g_opt_gru_dc_offset = 200;
 int g_opt_gru_fast_cell = 1;
 int g_opt_gru_dc_prio = 0;
 int g_opt_gru_dwhh_fused = 1;
+int g_opt_gru_fwd_worker = 0;
 int g_opt_gru_dwhh_batched = 1;
 int g_opt_gemm_skinny = 1;
 std::atomic<int64_t> g_scratch_gen{0};
@@ -438,6 +439,10 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "gru_dc_offset_ns") {   // fp32 two-chain kernels: delay chain 1's start (phase offset between the chains)
     SRK_REQUIRE(value >= 0 && value <= 1000000, SRK_ERR_INVALID, "gru_dc_offset_ns out of range");
     srk::g_opt_gru_dc_offset = (unsigned)(value / 10);
+    return SRK_OK;
+  }
+  if (n == "gru_fwd_worker") {   // 16-bit forward: y / gate stores and the gi fetch on extra worker waves (1) or not (0)
+    srk::g_opt_gru_fwd_worker = value != 0;
     return SRK_OK;
   }
   if (n == "gru_dwhh_fused") {   // 16-bit backward: dW_hh accumulated in the recurrence kernel (1) or by a GEMM (0)

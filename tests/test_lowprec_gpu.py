@@ -680,3 +680,42 @@ def test_bigru_dwhh_fused_matches_gemm(prec, B, T, IN, wide):
             assert err <= 1e-5, (n, err)
         else:
             assert torch.equal(a, b), n
+
+
+@pytest.mark.parametrize("B,T,IN", [(256, 51, 39), (256, 9, 1024), (200, 6, 1024), (96, 3, 39), (64, 2, 1024), (32, 1, 1024)])
+def test_bigru_fwd_worker_bitwise(prec, B, T, IN):
+    """Option gru_fwd_worker: the 16-bit forward recurrence with 4 worker waves that store y / y16 / the
+    gates from LDS after each publish and (no fused projection) fetch gi two steps ahead by LDS-DMA ==
+    the kernel without them, bit for bit (output and every gradient: the backward reads the gates and
+    y16 the workers wrote).  Shapes: the cfg2 layer-0 (fused projection) and layer-1 inputs, a partial
+    row group, and T = 1..3 (the workers' DMA / wait counts at the sequence edges)."""
+    from speechrecognitionproject_amd import nn as snn
+    H = 512
+    torch.manual_seed(12)
+    mine = snn.BiGRU(IN, H, num_layers=1).cuda()
+    x = torch.randn(B, T, IN, device="cuda")
+    w = torch.randn(B, T, 2 * H, device="cuda")
+    res = []
+    try:
+        _lib.set_matmul_precision(prec)
+        for ow in (1, 0):
+            _lib.set_option("gru_fwd_worker", ow)
+            mine.zero_grad()
+            xm = x.clone().requires_grad_(True)
+            _lib.prof_enable(True)
+            ym, _ = mine(xm)
+            (ym * w).sum().backward()
+            torch.cuda.synchronize()
+            kinds = [k["kernel"] for k in _lib.prof_kernels()]
+            _lib.prof_enable(False)
+            if ow:
+                assert any("_lp2ow" in k for k in kinds), kinds
+            res.append({"y": ym.detach().clone(), "dx": xm.grad.clone(),
+                        **{n: p.grad.detach().clone() for n, p in mine.named_parameters()}})
+    finally:
+        _lib.set_option("gru_fwd_worker", 0)
+        _lib.set_matmul_precision("fp32")
+    assert _lib.spin_timeouts() == 0
+    for n in res[0]:
+        assert torch.isfinite(res[0][n]).all(), n
+        assert torch.equal(res[0][n], res[1][n]), n

@@ -16,8 +16,6 @@ run() {  # run TAG OPTIONS ARGS...
 run cfg2_bf16_dw0_ow0 "gru_dwhh_fused=0,gru_fwd_worker=0" --model mfcc_bgru --precision bf16 --steps 20
 run cfg2_bf16_dw1_ow0 "gru_dwhh_fused=1,gru_fwd_worker=0" --model mfcc_bgru --precision bf16 --steps 20
 run cfg2_bf16_dw1_ow1 "gru_dwhh_fused=1,gru_fwd_worker=1" --model mfcc_bgru --precision bf16 --steps 20
-run mfrn_bf16_dw0_ow0 "gru_dwhh_fused=0,gru_fwd_worker=0" --model mfrn_bgru --precision bf16 --steps 10
-run mfrn_bf16_dw1_ow1 "gru_dwhh_fused=1,gru_fwd_worker=1" --model mfrn_bgru --precision bf16 --steps 10
 python - "$OUT" <<'PY'
 import json, sys, glob, os
 for f in sorted(glob.glob(sys.argv[1] + "/*.json")):
@@ -26,6 +24,3 @@ for f in sorted(glob.glob(sys.argv[1] + "/*.json")):
     for k in r["roofline"]["top_kernels"][:4]:
         print("    ", k)
 PY
-timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_lowprec_gpu.py \
-  tests/test_trainstep_lowprec_gpu.py tests/test_graphs_gpu.py tests/test_dense_gpu.py > "$OUT/pytest_lp.log" 2>&1 || { tail -40 "$OUT/pytest_lp.log"; exit 1; }
-tail -1 "$OUT/pytest_lp.log"

@@ -683,12 +683,15 @@ def test_bigru_dwhh_fused_matches_gemm(prec, B, T, IN, wide):
 
 
 @pytest.mark.parametrize("B,T,IN", [(256, 51, 39), (256, 9, 1024), (200, 6, 1024), (96, 3, 39), (64, 2, 1024), (32, 1, 1024)])
-def test_bigru_fwd_worker_bitwise(prec, B, T, IN):
+def test_bigru_fwd_worker(prec, B, T, IN):
     """Option gru_fwd_worker: the 16-bit forward recurrence with 4 worker waves that store y / y16 / the
-    gates from LDS after each publish and (no fused projection) fetch gi two steps ahead by LDS-DMA ==
-    the kernel without them, bit for bit (output and every gradient: the backward reads the gates and
-    y16 the workers wrote).  Shapes: the cfg2 layer-0 (fused projection) and layer-1 inputs, a partial
-    row group, and T = 1..3 (the workers' DMA / wait counts at the sequence edges)."""
+    gates from LDS after each publish and (no fused projection) fetch gi two steps ahead by LDS-DMA,
+    against the kernel without them.  The same source arithmetic in a separately compiled instantiation
+    (the compiler's multiply-add contraction in the cell may differ, as between the 64- and 32-row
+    kernels, test_bigru_lowprec_wide_matches_chunked): step 0 of each direction bitwise, outputs within
+    5e-4, gradients 2e-3 norm-wise (the backward reads the gates / y16 the workers wrote), each mode
+    bitwise reproducible.  Shapes: the cfg2 layer-0 (fused projection) and layer-1 inputs, a partial row
+    group, and T = 1..3 (the workers' DMA / wait counts at the sequence edges)."""
     from speechrecognitionproject_amd import nn as snn
     H = 512
     torch.manual_seed(12)
@@ -698,7 +701,7 @@ def test_bigru_fwd_worker_bitwise(prec, B, T, IN):
     res = []
     try:
         _lib.set_matmul_precision(prec)
-        for ow in (1, 0):
+        for ow in (1, 1, 0):
             _lib.set_option("gru_fwd_worker", ow)
             mine.zero_grad()
             xm = x.clone().requires_grad_(True)
@@ -708,14 +711,20 @@ def test_bigru_fwd_worker_bitwise(prec, B, T, IN):
             torch.cuda.synchronize()
             kinds = [k["kernel"] for k in _lib.prof_kernels()]
             _lib.prof_enable(False)
-            if ow:
-                assert any("_lp2ow" in k for k in kinds), kinds
+            assert any("_lp2ow" in k for k in kinds) == bool(ow), kinds
             res.append({"y": ym.detach().clone(), "dx": xm.grad.clone(),
                         **{n: p.grad.detach().clone() for n, p in mine.named_parameters()}})
     finally:
         _lib.set_option("gru_fwd_worker", 0)
         _lib.set_matmul_precision("fp32")
     assert _lib.spin_timeouts() == 0
-    for n in res[0]:
-        assert torch.isfinite(res[0][n]).all(), n
-        assert torch.equal(res[0][n], res[1][n]), n
+    a, a2, c = res
+    for n in a:
+        assert torch.isfinite(a[n]).all(), n
+        assert torch.equal(a[n], a2[n]), n
+    assert torch.equal(a["y"][:, 0, :H], c["y"][:, 0, :H]) and torch.equal(a["y"][:, -1, H:], c["y"][:, -1, H:])
+    assert float((a["y"] - c["y"]).abs().max()) <= 5e-4
+    for n in a:
+        if n != "y":
+            err = float((a[n] - c[n]).norm() / c[n].norm())
+            assert err <= 2e-3, (n, err)

@@ -5,7 +5,7 @@ set -o pipefail
 OUT=gpurun_out/${1:-r04ab8}
 mkdir -p "$OUT"
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
-  "tests/test_lowprec_gpu.py::test_bigru_dwhh_fused_matches_gemm" "tests/test_lowprec_gpu.py::test_bigru_fwd_worker_bitwise" \
+  "tests/test_lowprec_gpu.py::test_bigru_dwhh_fused_matches_gemm" "tests/test_lowprec_gpu.py::test_bigru_fwd_worker" \
   > "$OUT/pytest_new.log" 2>&1 || { tail -40 "$OUT/pytest_new.log"; exit 1; }
 tail -3 "$OUT/pytest_new.log"
 run() {  # run TAG OPTIONS ARGS...

@@ -725,6 +725,10 @@ def test_bigru_fwd_worker(prec, B, T, IN):
     assert torch.equal(a["y"][:, 0, :H], c["y"][:, 0, :H]) and torch.equal(a["y"][:, -1, H:], c["y"][:, -1, H:])
     assert float((a["y"] - c["y"]).abs().max()) <= 5e-4
     for n in a:
-        if n != "y":
-            err = float((a[n] - c[n]).norm() / c[n].norm())
-            assert err <= 2e-3, (n, err)
+        if n == "y":
+            continue
+        if float(c[n].norm()) == 0.0:   # T = 1: h_prev = 0, so dW_hh is exactly zero on both paths
+            assert torch.equal(a[n], c[n]), n
+            continue
+        err = float((a[n] - c[n]).norm() / c[n].norm())
+        assert err <= 2e-3, (n, err)

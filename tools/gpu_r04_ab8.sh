@@ -6,12 +6,12 @@ OUT=gpurun_out/${1:-r04ab8}
 mkdir -p "$OUT"
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
   "tests/test_lowprec_gpu.py::test_bigru_dwhh_fused_matches_gemm" "tests/test_lowprec_gpu.py::test_bigru_fwd_worker" \
-  > "$OUT/pytest_new.log" 2>&1 || { tail -40 "$OUT/pytest_new.log"; exit 1; }
+  > "$OUT/pytest_new.log" 2>&1 || { rc=$?; tail -40 "$OUT/pytest_new.log"; exit $rc; }
 tail -3 "$OUT/pytest_new.log"
 run() {  # run TAG OPTIONS ARGS...
   local tag=$1 opt=$2; shift 2
   SRK_OPTIONS=$opt timeout -k 10 300 python bench.py --no-lowprec --no-cpu-baseline --no-feature-roofline "$@" \
-    > "$OUT/$tag.json" 2> "$OUT/$tag.err" || exit 1
+    > "$OUT/$tag.json" 2> "$OUT/$tag.err" || exit $?
 }
 run cfg2_bf16_dw0_ow0 "gru_dwhh_fused=0,gru_fwd_worker=0" --model mfcc_bgru --precision bf16 --steps 20
 run cfg2_bf16_dw1_ow0 "gru_dwhh_fused=1,gru_fwd_worker=0" --model mfcc_bgru --precision bf16 --steps 20

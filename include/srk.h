@@ -66,8 +66,9 @@ int srk_prof_kernels(char* buf, int64_t cap, int64_t* needed);
  * qualifies (bits 0-2 fp32 fwd / dgrad / wgrad, 4-6 the same in 16 bit, 7 also the pooled forward
  * and the fp32 forward at K < 3072); "conv_unpool16" (default 1) = the 16-bit pooled-conv backward
  * writes the dense dY straight as its 16-bit operand copy; "gru_dwhh_fused" (default 1) = the 16-bit
- * BiGRU backward accumulates dW_hh inside the recurrence kernel (0 = a GEMM over dgh16 / y16) —
- * results equal up to fp32 summation order (A/B measurements and tests). */
+ * BiGRU backward accumulates dW_hh inside the recurrence kernel (0 = a GEMM over dgh16 / y16; bits
+ * 1 / 2 of a non-zero value: timing variants, bitwise bit 0's results) — results equal up to fp32
+ * summation order (A/B measurements and tests). */
 int srk_set_option(const char* name, int64_t value);
 /* Number of bounded spin-waits of the persistent kernels that gave up (synchronizes the
  * device; must stay 0 — a non-zero value means a co-residency assumption failed).  -1 on error. */
@@ -227,13 +228,20 @@ int srk_conv2d_nhwc_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t
  * rounds x into x16 (N*H*W*Ci 16-bit elements, 16-B aligned, caller storage) and sets
  * *x16_written = 1 when that path ran, else 0 (x16 untouched); bwd16 gathers from that copy instead
  * of rounding x again (x16 null: as srk_conv2d_nhwc_bwd).  The backward must run at the forward's
- * precision.  Bitwise the results of the plain pair.                                          */
+ * precision.  Bitwise the results of the plain pair.  *x16_written = 2 on entry declares that x16
+ * already holds x's copy at this precision (srk_batchnorm_fwd16's y16): fwd16 then reads it instead
+ * of rounding x.  bwd16_dy16 also takes dY's ready copy dy16 (srk_batchnorm_bwd16's dx16; nullable;
+ * used wherever the 16-bit path would round dy, dy itself still required).                   */
 int srk_conv2d_nhwc_fwd16(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w,
                           const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh,
                           int64_t sw, float* y, float* ws, void* x16, int* x16_written, void* stream);
 int srk_conv2d_nhwc_bwd16(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co,
                           int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw, const float* dy,
                           float* dx, float* dw, float* db, float* ws, const void* x16, void* stream);
+int srk_conv2d_nhwc_bwd16_dy16(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w,
+                               int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw,
+                               const float* dy, const void* dy16, float* dx, float* dw, float* db, float* ws,
+                               const void* x16, void* stream);
 /* Conv2d (stride 1) + bias + MaxPool2d((1, 4)) fused (model_fbanks_cnn.py:74-75,91-92: conv2 then
  * maxpool2): the implicit GEMM's epilogue pools its own output, so only the pooled activation y
  * [N][Ho][Wo/4][Co] and the uint8 window argmax [N][Ho][Wo/4][Co] (first maximum, NaN wins: the
@@ -282,6 +290,20 @@ int srk_batchnorm_fwd(const float* x, int64_t M, int64_t C, const float* gamma, 
 int srk_batchnorm_bwd(const float* x, const float* y, const float* dy, int64_t M, int64_t C, const float* gamma,
                       const float* save_mean, const float* save_invstd, int training, int relu, float* dx,
                       float* dgamma, float* dbeta, float* dresidual, void* stream);
+/* The same pair emitting the 16-bit operand copy of their output for the convolution that consumes it
+ * (model_resnet_bgru.py: every conv reads a BatchNorm output, and every BatchNorm's dx is a conv's dY).
+ * fwd16 writes y16 = y rounded to the bf16 / fp16 matmul precision (M*C 16-bit elements, 16-B aligned,
+ * caller storage) beside y; bwd16 writes dx16 = dx rounded likewise; *_written = 1 when the copy was
+ * written, else 0 (fp32 precision, null or misaligned pointer; dx16 also needs dx).  The rounding is
+ * the convolutions' own (round to nearest even), so srk_conv2d_nhwc_fwd16 (x16_written = 2 on entry)
+ * and srk_conv2d_nhwc_bwd16_dy16 use the copies bitwise as if they had made them.               */
+int srk_batchnorm_fwd16(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta, float eps,
+                        float momentum, int training, float* running_mean, float* running_var, const float* residual,
+                        int relu, float* y, void* y16, int* y16_written, float* save_mean, float* save_invstd,
+                        void* stream);
+int srk_batchnorm_bwd16(const float* x, const float* y, const float* dy, int64_t M, int64_t C, const float* gamma,
+                        const float* save_mean, const float* save_invstd, int training, int relu, float* dx,
+                        void* dx16, int* dx16_written, float* dgamma, float* dbeta, float* dresidual, void* stream);
 /* SyncBatchNorm pieces (torch.nn.SyncBatchNorm semantics: training statistics over the global
  * batch of all data-parallel ranks; model_resnet_bgru.py's BatchNorm1d layers under DP).  Forward:
  * srk_batchnorm_stats (this rank's count, mean, M2 per channel -> stats [3][C]), the caller gathers

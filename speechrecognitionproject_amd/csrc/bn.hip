@@ -53,6 +53,18 @@ inline BnGeom bn_geom(int64_t M, int C) {
 __device__ __forceinline__ v4f ld4(const float* p) { return *reinterpret_cast<const v4f*>(p); }
 __device__ __forceinline__ void st4(float* p, v4f v) { *reinterpret_cast<v4f*>(p) = v; }
 
+// 16-bit copy of an output for the convolution that consumes it next (LP 1 = bf16, 2 = fp16; 0 = none):
+// the conversion of conv.hip's to16_kernel (round to nearest even), so the copy is bitwise the one the
+// convolution would have made from the fp32 tensor
+typedef unsigned u32x2b __attribute__((ext_vector_type(2)));
+typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+typedef _Float16 hf4 __attribute__((ext_vector_type(4)));
+template <int LP>
+__device__ __forceinline__ void st4_16(uint16_t* p, v4f v) {
+  if constexpr (LP == 1) *reinterpret_cast<u32x2b*>(p) = __builtin_bit_cast(u32x2b, __builtin_convertvector(v, bf4));
+  if constexpr (LP == 2) *reinterpret_cast<u32x2b*>(p) = __builtin_bit_cast(u32x2b, __builtin_convertvector(v, hf4));
+}
+
 // Chan et al. pairwise combination of (count, mean, M2) — fixed call order => deterministic.
 __device__ __forceinline__ void chan(float& n, float& mu, float& m2, float nb, float mub, float m2b) {
   if (nb == 0.f) return;
@@ -167,11 +179,11 @@ __device__ __forceinline__ int chan_of(int64_t o, int C) {
   return I32 ? (int)((unsigned)o % (unsigned)C) : (int)(o % C);
 }
 
-template <bool I32>
+template <bool I32, int LP>
 __global__ void bn_apply_kernel(const float* __restrict__ x, int64_t M, int C, const float* __restrict__ mean,
                                 const float* __restrict__ invstd, const float* __restrict__ gamma,
                                 const float* __restrict__ beta, const float* __restrict__ residual, int relu,
-                                float* __restrict__ y) {
+                                float* __restrict__ y, uint16_t* __restrict__ y16) {
   const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i4 * 4 >= M * C) return;
   const int c = chan_of<I32>(i4 * 4, C);
@@ -183,6 +195,7 @@ __global__ void bn_apply_kernel(const float* __restrict__ x, int64_t M, int C, c
     for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
   }
   st4(y + i4 * 4, v);
+  if constexpr (LP != 0) st4_16<LP>(y16 + i4 * 4, v);
 }
 
 __global__ void bn_eval_stats_kernel(const float* __restrict__ rm, const float* __restrict__ rv, int C, float eps,
@@ -270,13 +283,13 @@ __global__ void bn_dgamma_kernel(const float* __restrict__ p0, const float* __re
   dgamma[c] = b;
 }
 
-template <bool I32>
+template <bool I32, int LP>
 __global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ dy,
                              int64_t M, int C, const float* __restrict__ mean, const float* __restrict__ invstd,
                              const float* __restrict__ gamma, const float* __restrict__ dbeta,
                              const float* __restrict__ dgamma, int relu, int train, float m_norm,
                              const float* __restrict__ m_norm_dev, float* __restrict__ dx,
-                             float* __restrict__ dres) {
+                             float* __restrict__ dres, uint16_t* __restrict__ dx16) {
   const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i4 * 4 >= M * C) return;
   const int64_t o = i4 * 4;
@@ -295,9 +308,13 @@ __global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restric
     const float mn = m_norm_dev ? m_norm_dev[0] : m_norm;   // rows the statistics span (all ranks' for SyncBN)
     const float inv_m = 1.0f / mn;
     const v4f db = ld4(dbeta + c), dg = ld4(dgamma + c);
-    st4(dx + o, ga * is * inv_m * (mn * gr - db - xhat * dg));
+    const v4f v = ga * is * inv_m * (mn * gr - db - xhat * dg);
+    st4(dx + o, v);
+    if constexpr (LP != 0) st4_16<LP>(dx16 + o, v);
   } else {
-    st4(dx + o, ga * is * gr);
+    const v4f v = ga * is * gr;
+    st4(dx + o, v);
+    if constexpr (LP != 0) st4_16<LP>(dx16 + o, v);
   }
 }
 
@@ -361,6 +378,45 @@ int bn_scratch(size_t floats, float** out) {
   return SRK_OK;
 }
 
+// the element kernels by index width (32-bit channel arithmetic below 2^32 elements) and 16-bit copy
+template <int LP>
+void launch_apply_lp(int64_t M, int C, hipStream_t s, const float* x, const float* mean, const float* invstd,
+                     const float* gamma, const float* beta, const float* residual, int relu, float* y, uint16_t* y16) {
+  const int64_t n4 = M * C / 4;
+  hipLaunchKernelGGL((M * C < (1LL << 32) ? bn_apply_kernel<true, LP> : bn_apply_kernel<false, LP>),
+                     dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, M, C, mean, invstd, gamma, beta, residual,
+                     relu, y, y16);
+}
+void launch_apply(int LP, int64_t M, int C, hipStream_t s, const float* x, const float* mean, const float* invstd,
+                  const float* gamma, const float* beta, const float* residual, int relu, float* y, uint16_t* y16) {
+  if (LP == 1) launch_apply_lp<1>(M, C, s, x, mean, invstd, gamma, beta, residual, relu, y, y16);
+  else if (LP == 2) launch_apply_lp<2>(M, C, s, x, mean, invstd, gamma, beta, residual, relu, y, y16);
+  else launch_apply_lp<0>(M, C, s, x, mean, invstd, gamma, beta, residual, relu, y, nullptr);
+}
+template <int LP>
+void launch_dx_lp(int64_t M, int C, hipStream_t s, const float* x, const float* y, const float* dy, const float* mean,
+                  const float* invstd, const float* gamma, const float* dbeta, const float* dgamma, int relu, int train,
+                  float m_norm, const float* m_norm_dev, float* dx, float* dres, uint16_t* dx16) {
+  const int64_t n4 = M * C / 4;
+  hipLaunchKernelGGL((M * C < (1LL << 32) ? bn_dx_kernel<true, LP> : bn_dx_kernel<false, LP>),
+                     dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, y, dy, M, C, mean, invstd, gamma, dbeta,
+                     dgamma, relu, train, m_norm, m_norm_dev, dx, dres, dx16);
+}
+void launch_dx(int LP, int64_t M, int C, hipStream_t s, const float* x, const float* y, const float* dy,
+               const float* mean, const float* invstd, const float* gamma, const float* dbeta, const float* dgamma,
+               int relu, int train, float m_norm, const float* m_norm_dev, float* dx, float* dres, uint16_t* dx16) {
+  if (LP == 1) launch_dx_lp<1>(M, C, s, x, y, dy, mean, invstd, gamma, dbeta, dgamma, relu, train, m_norm, m_norm_dev, dx, dres, dx16);
+  else if (LP == 2) launch_dx_lp<2>(M, C, s, x, y, dy, mean, invstd, gamma, dbeta, dgamma, relu, train, m_norm, m_norm_dev, dx, dres, dx16);
+  else launch_dx_lp<0>(M, C, s, x, y, dy, mean, invstd, gamma, dbeta, dgamma, relu, train, m_norm, m_norm_dev, dx, dres, nullptr);
+}
+
+// 16-bit copy requested and possible: the matmul precision's type (1 bf16, 2 fp16), else 0
+int copy16_type(const void* p16) {
+  const int prec = matmul_prec();
+  if (!p16 || prec == kPrecF32 || reinterpret_cast<uintptr_t>(p16) % 16) return 0;
+  return prec == kPrecBF16 ? 1 : 2;
+}
+
 }  // namespace
 }  // namespace srk
 
@@ -369,13 +425,23 @@ extern "C" {
 int srk_batchnorm_fwd(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta, float eps,
                       float momentum, int training, float* running_mean, float* running_var, const float* residual,
                       int relu, float* y, float* save_mean, float* save_invstd, void* stream) {
+  return srk_batchnorm_fwd16(x, M, C, gamma, beta, eps, momentum, training, running_mean, running_var, residual, relu,
+                             y, nullptr, nullptr, save_mean, save_invstd, stream);
+}
+
+int srk_batchnorm_fwd16(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta, float eps,
+                        float momentum, int training, float* running_mean, float* running_var, const float* residual,
+                        int relu, float* y, void* y16, int* y16_written, float* save_mean, float* save_invstd,
+                        void* stream) {
   SRK_API_BEGIN
+  if (y16_written) *y16_written = 0;
   SRK_REQUIRE(M > 0 && C > 0 && C <= (1 << 24), SRK_ERR_INVALID, "batchnorm: bad shape");
   SRK_REQUIRE(C % 4 == 0, SRK_ERR_INVALID, "batchnorm: channels must be a multiple of 4");
   SRK_REQUIRE(x && gamma && beta && y && save_mean && save_invstd && running_mean && running_var, SRK_ERR_INVALID,
               "batchnorm: null pointer");
   hipStream_t s = srk::as_stream(stream);
-  srk::ProfScope prof("batchnorm_fwd", s, (training ? 12.0 : 8.0) * (double)M * C);
+  const int lp = srk::copy16_type(y16);
+  srk::ProfScope prof("batchnorm_fwd", s, ((training ? 12.0 : 8.0) + (lp ? 2.0 : 0.0)) * (double)M * C);
   const srk::BnGeom g = srk::bn_geom(M, (int)C);
   if (training) {
     float* part = nullptr;
@@ -389,10 +455,10 @@ int srk_batchnorm_fwd(const float* x, int64_t M, int64_t C, const float* gamma, 
     hipLaunchKernelGGL(srk::bn_eval_stats_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, running_mean,
                        running_var, (int)C, eps, save_mean, save_invstd);
   }
-  const int64_t n4 = M * C / 4;
-  hipLaunchKernelGGL(M * C < (1LL << 32) ? srk::bn_apply_kernel<true> : srk::bn_apply_kernel<false>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, M, (int)C,
-                     save_mean, save_invstd, gamma, beta, residual, relu, y);
+  srk::launch_apply(lp, M, (int)C, s, x, save_mean, save_invstd, gamma, beta, residual, relu, y,
+                    static_cast<uint16_t*>(y16));
   SRK_CHECK_HIP(hipGetLastError());
+  if (lp && y16_written) *y16_written = 1;
   return SRK_OK;
   SRK_API_END
 }
@@ -400,12 +466,21 @@ int srk_batchnorm_fwd(const float* x, int64_t M, int64_t C, const float* gamma, 
 int srk_batchnorm_bwd(const float* x, const float* y, const float* dy, int64_t M, int64_t C, const float* gamma,
                       const float* save_mean, const float* save_invstd, int training, int relu, float* dx,
                       float* dgamma, float* dbeta, float* dresidual, void* stream) {
+  return srk_batchnorm_bwd16(x, y, dy, M, C, gamma, save_mean, save_invstd, training, relu, dx, nullptr, nullptr,
+                             dgamma, dbeta, dresidual, stream);
+}
+
+int srk_batchnorm_bwd16(const float* x, const float* y, const float* dy, int64_t M, int64_t C, const float* gamma,
+                        const float* save_mean, const float* save_invstd, int training, int relu, float* dx,
+                        void* dx16, int* dx16_written, float* dgamma, float* dbeta, float* dresidual, void* stream) {
   SRK_API_BEGIN
+  if (dx16_written) *dx16_written = 0;
   SRK_REQUIRE(M > 0 && C > 0 && C % 4 == 0, SRK_ERR_INVALID, "batchnorm_bwd: bad shape (C % 4 == 0 required)");
   SRK_REQUIRE(x && y && dy && gamma && save_mean && save_invstd && dgamma && dbeta, SRK_ERR_INVALID,
               "batchnorm_bwd: null pointer");
   hipStream_t s = srk::as_stream(stream);
-  srk::ProfScope prof("batchnorm_bwd", s, 16.0 * (double)M * C);
+  const int lp = dx ? srk::copy16_type(dx16) : 0;
+  srk::ProfScope prof("batchnorm_bwd", s, (16.0 + (lp ? 2.0 : 0.0)) * (double)M * C);
   const srk::BnGeom g = srk::bn_geom(M, (int)C);
   float* part = nullptr;
   if (int rc = srk::bn_scratch((size_t)2 * g.chunks * C, &part)) return rc;
@@ -413,10 +488,10 @@ int srk_batchnorm_bwd(const float* x, const float* y, const float* dy, int64_t M
                      dim3(256), 0, s, x, y, dy, g, save_mean, save_invstd, relu, part, part + (size_t)g.chunks * C);
   hipLaunchKernelGGL(srk::bn_dgamma_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
                      part + (size_t)g.chunks * C, g.chunks, (int)C, dbeta, dgamma);
-  const int64_t n4 = M * C / 4;
-  hipLaunchKernelGGL(M * C < (1LL << 32) ? srk::bn_dx_kernel<true> : srk::bn_dx_kernel<false>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, y, dy, M, (int)C,
-                     save_mean, save_invstd, gamma, dbeta, dgamma, relu, training, (float)M, nullptr, dx, dresidual);
+  srk::launch_dx(lp, M, (int)C, s, x, y, dy, save_mean, save_invstd, gamma, dbeta, dgamma, relu, training, (float)M,
+                 nullptr, dx, dresidual, static_cast<uint16_t*>(dx16));
   SRK_CHECK_HIP(hipGetLastError());
+  if (lp && dx16_written) *dx16_written = 1;
   return SRK_OK;
   SRK_API_END
 }
@@ -464,9 +539,7 @@ int srk_batchnorm_apply(const float* x, int64_t M, int64_t C, const float* save_
   SRK_REQUIRE(x && save_mean && save_invstd && gamma && beta && y, SRK_ERR_INVALID, "batchnorm_apply: null pointer");
   hipStream_t s = srk::as_stream(stream);
   srk::ProfScope prof("batchnorm_fwd", s, 8.0 * (double)M * C);
-  const int64_t n4 = M * C / 4;
-  hipLaunchKernelGGL(M * C < (1LL << 32) ? srk::bn_apply_kernel<true> : srk::bn_apply_kernel<false>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, M, (int)C,
-                     save_mean, save_invstd, gamma, beta, residual, relu, y);
+  srk::launch_apply(0, M, (int)C, s, x, save_mean, save_invstd, gamma, beta, residual, relu, y, nullptr);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END
@@ -501,9 +574,8 @@ int srk_batchnorm_bwd_dx(const float* x, const float* y, const float* dy, int64_
               SRK_ERR_INVALID, "batchnorm_bwd_dx: null pointer");
   hipStream_t s = srk::as_stream(stream);
   srk::ProfScope prof("batchnorm_bwd", s, 16.0 * (double)M * C);
-  const int64_t n4 = M * C / 4;
-  hipLaunchKernelGGL(M * C < (1LL << 32) ? srk::bn_dx_kernel<true> : srk::bn_dx_kernel<false>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, y, dy, M, (int)C,
-                     save_mean, save_invstd, gamma, sums, sums + C, relu, 1, 0.f, total_count, dx, dresidual);
+  srk::launch_dx(0, M, (int)C, s, x, y, dy, save_mean, save_invstd, gamma, sums, sums + C, relu, 1, 0.f, total_count,
+                 dx, dresidual, nullptr);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END

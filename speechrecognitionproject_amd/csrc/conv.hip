@@ -1584,6 +1584,7 @@ int srk_conv2d_nhwc_fwd16(const float* x, int64_t N, int64_t H, int64_t W, int64
                           const float* bias, int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh,
                           int64_t sw, float* y, float* ws, void* x16, int* x16_written, void* stream) {
   SRK_API_BEGIN
+  const bool x16_ready = x16 && x16_written && *x16_written == 2;   // the producer's copy (srk_batchnorm_fwd16)
   if (x16_written) *x16_written = 0;
   int64_t Ho, Wo;
   if (int rc = srk::check(N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw, &Ho, &Wo)) return rc;
@@ -1602,7 +1603,8 @@ int srk_conv2d_nhwc_fwd16(const float* x, int64_t N, int64_t H, int64_t W, int64
     const float* src[2] = {x, ws};
     const int64_t n[2] = {N * H * W * Ci, nw};
     unsigned short* d16[2] = {static_cast<unsigned short*>(x16), nullptr};   // x16: the caller keeps x's copy
-    if (int rc = srk::to16_all(prec, src, n, 2, d16, s)) return rc;
+    const bool ready[2] = {x16_ready, false};
+    if (int rc = srk::to16_all(prec, src, n, 2, d16, s, ready)) return rc;
     c.a16 = d16[0];
     c.b16 = d16[1];
     if (x16 && x16_written) *x16_written = 1;
@@ -1640,8 +1642,9 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
   const bool full_width = KH == 1 && ph == 0 && sh == 1 && pw == 0 && KW == W && Wo == 1;
   SRK_REQUIRE(!dy_arg || (!full_width && (!db || srk::g_opt_conv_fused_db)), SRK_ERR_INTERNAL,
               "conv bwd: pooled dY needs the implicit data gradient and the fused bias sums");
-  // dy16: the caller's 16-bit dY (no fp32 dY): the implicit 16-bit-source GEMMs only, no bias sums here
-  SRK_REQUIRE(!dy16 || (!dy && !dy_arg && !full_width && !db && srk::s16_ok(srk::matmul_prec(), Ci, Co, {x, ws, x16, dy16})),
+  // dy16 without dy: the caller's 16-bit dY only (the pooled backward): the implicit 16-bit-source GEMMs, no
+  // bias sums here; dy16 beside dy: a ready copy, used where the 16-bit path would round dy
+  SRK_REQUIRE(!dy16 || dy || (!dy_arg && !full_width && !db && srk::s16_ok(srk::matmul_prec(), Ci, Co, {x, ws, x16, dy16})),
               SRK_ERR_INTERNAL, "conv bwd: a 16-bit dY needs the 16-bit-source implicit GEMMs");
   const bool dgrad_implicit = dx && !full_width;
   if (dgrad_implicit)
@@ -1650,7 +1653,7 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
   // 16-bit sources: x and dY serve both GEMMs, Wd the data gradient (one scratch allocation)
   unsigned short* d16[3] = {nullptr, nullptr, nullptr};   // x, dY, Wd
   const int prec = srk::matmul_prec();
-  if (!dy_arg && srk::s16_ok(prec, Ci, Co, {x, dy, ws, x16})) {
+  if (!dy_arg && srk::s16_ok(prec, Ci, Co, {x, dy, ws, x16, dy16})) {
     const float* src[3] = {x, dy, ws};
     const int64_t n[3] = {N * H * W * Ci, N * Ho * Wo * Co, nw};
     const bool ready[3] = {x16 != nullptr, dy16 != nullptr, false};   // x16: the forward's copy of x
@@ -1712,6 +1715,17 @@ int srk_conv2d_nhwc_bwd16(const float* x, int64_t N, int64_t H, int64_t W, int64
                           float* dx, float* dw, float* db, float* ws, const void* x16, void* stream) {
   SRK_API_BEGIN
   return srk::conv_bwd(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, sh, sw, dy, nullptr, dx, dw, db, ws, x16, stream);
+  SRK_API_END
+}
+
+int srk_conv2d_nhwc_bwd16_dy16(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w,
+                               int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw,
+                               const float* dy, const void* dy16, float* dx, float* dw, float* db, float* ws,
+                               const void* x16, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(dy, SRK_ERR_INVALID, "conv bwd: null pointer");
+  return srk::conv_bwd(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, sh, sw, dy, nullptr, dx, dw, db, ws, x16, stream,
+                       static_cast<const unsigned short*>(dy16));
   SRK_API_END
 }
 

@@ -68,6 +68,7 @@ struct GruPArgs {
   // dwhh_reduce_kernel
   const uint16_t* y16_in;
   float* dw_part;
+  int dw_mode;           // option gru_dwhh_fused bits: 2 = h_prev fetched after the exchange barrier, 4 = recurrence waves at prio 1
 };
 
 size_t fwd_lds_bytes(int H);

@@ -1951,10 +1951,15 @@ __device__ __forceinline__ void dw_worker(const GruPArgs& a, const unsigned shor
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
+  const bool late = (a.dw_mode & 2) != 0;   // fetch step s's h_prev after step s's exchange barrier (the recurrence
+                                            // waves are past their hand-off loads then), not right after step s-1's MFMAs
   bar();   // = the prologue barrier (W slice in LDS)
   if (T > 1) dma(0);
   for (int step = 0; step < T; ++step) {
-    if (step > 0) bar();   // = the k-half exchange
+    if (step > 0) {
+      bar();   // = the k-half exchange
+      if (late && step < T - 1) dma(step);
+    }
     bar();                 // = the cell barrier: this step's dg image is complete
     bar();                 // = the publish (lp2_arrive)
     if (step == T - 1) continue;     // the edge step: h_prev = 0
@@ -1978,7 +1983,7 @@ __device__ __forceinline__ void dw_worker(const GruPArgs& a, const unsigned shor
                                        __builtin_bit_cast(typename RecOps<F16>::e8, bf), acc[mb][nb]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // image reads done: the next DMA may overwrite
-    if (step + 1 < T - 1) dma(step + 1);
+    if (!late && step + 1 < T - 1) dma(step + 1);
   }
   bar();   // = the bias-partials barrier
   float* dst = a.dw_part + ((size_t)(a.chunk * 8 + group) * 2 + dir) * 3 * H * H;
@@ -2023,6 +2028,7 @@ __global__ __launch_bounds__(DW ? 512 : 128 * RB, 1) void gru_bwd_persistent_lp2
       dw_worker<H, F16>(a, Aimg, Bimg, dir, group, j0, b0, b_last, wave - NW, lane);
       return;
     }
+    if (a.dw_mode & 4) __builtin_amdgcn_s_setprio(1);   // the recurrence waves ahead of the workers at issue
   }
 
   {  // W_hh[dir][c][j0 .. j0+31] for all 3H rows c, transposed [jj][c] in 8-deep c packs
@@ -2409,6 +2415,7 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     ac.dc_offset = g_opt_gru_dc_offset;
     ac.fast_cell = g_opt_gru_fast_cell;
     ac.dc_prio = g_opt_gru_dc_prio;
+    ac.dw_mode = g_opt_gru_dwhh_fused;
     ac.b_begin = c0;
     ac.b_end = std::min(a.B, c0 + rows_per_launch);
     ac.G = (ac.b_end - c0 + rows_g - 1) / rows_g;

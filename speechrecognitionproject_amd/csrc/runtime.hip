@@ -445,8 +445,10 @@ int srk_set_option(const char* name, int64_t value) {
     srk::g_opt_gru_fwd_worker = value != 0;
     return SRK_OK;
   }
-  if (n == "gru_dwhh_fused") {   // 16-bit backward: dW_hh accumulated in the recurrence kernel (1) or by a GEMM (0)
-    srk::g_opt_gru_dwhh_fused = value != 0;
+  if (n == "gru_dwhh_fused") {   // 16-bit backward: dW_hh accumulated in the recurrence kernel (bit 0) or by a GEMM (0);
+                                  // bit 1: h_prev fetched after the next exchange barrier, bit 2: recurrence waves at s_setprio 1
+    SRK_REQUIRE(value >= 0 && value <= 7, SRK_ERR_INVALID, "gru_dwhh_fused must be 0..7");
+    srk::g_opt_gru_dwhh_fused = (value & 1) ? (int)value : 0;
     return SRK_OK;
   }
   if (n == "gru_dc_prio") {   // fp32 two-chain kernels: 0 equal priority, 1 / 2 chain 0 / 1 at s_setprio 1 (static)

@@ -6,6 +6,7 @@ Every forward/backward runs a HIP kernel through the C ABI; there is no CPU or t
 fallback (the GPU and the library are required).
 """
 import ctypes
+import os
 
 import torch
 import torch.nn as tnn
@@ -269,6 +270,49 @@ class CrossEntropyLoss(tnn.Module):
         return _CrossEntropyFn.apply(logits, labels)
 
 
+# ----------------------------------------------------------------------------- 16-bit operand copies
+# At bf16 / fp16 matmul precision the convolutions read 16-bit copies of x and dY.  In resnet_bgru every
+# conv input is a BatchNorm output and every conv dY is a BatchNorm dx (model_resnet_bgru.py:19-39), so
+# BatchNorm writes the copy beside its fp32 output (srk_batchnorm_fwd16 / _bwd16, the same rounding) and
+# the conv takes it instead of re-reading the fp32 tensor to round it.  The hand-over is keyed by the
+# tensor's address and checked against its identity: the entry holds the fp32 tensor itself (so the
+# address cannot be reused while the entry lives), its version counter (any in-place write since
+# invalidates it), element count and precision.  Forward copies are made in training steps only (training
+# mode, autograd on); the producing BatchNorm's backward drops its forward entry, the conv backward pops the
+# dY entry it consumes, and the table is bounded (a step's worth of entries).
+COPIES16 = os.environ.get("SRK_BN_COPY16", "1") != "0"   # A/B switch (tests flip it)
+_copies16 = {}
+_COPIES16_MAX = 64
+
+
+def _copy16_wanted(C):
+    return COPIES16 and _lib.matmul_precision() != "fp32" and C % 8 == 0
+
+
+def _copy16_put(t, t16):
+    _copies16.pop(t.data_ptr(), None)
+    while len(_copies16) >= _COPIES16_MAX:
+        _copies16.pop(next(iter(_copies16)))
+    _copies16[t.data_ptr()] = (t, t._version, t.numel(), _lib.matmul_precision(), t16)
+
+
+def _copy16_get(t, pop=False):
+    """The producer's 16-bit copy of t (a float32 contiguous CUDA tensor) at the current precision, or None."""
+    e = _copies16.get(t.data_ptr())
+    if e is None:
+        return None
+    src, ver, n, prec, t16 = e
+    ok = (t.dtype == torch.float32 and t.is_contiguous() and t.numel() == n and t._version == ver
+          and src.data_ptr() == t.data_ptr() and prec == _lib.matmul_precision())
+    if pop or not ok:
+        _copies16.pop(t.data_ptr(), None)
+    return t16 if ok else None
+
+
+def _copy16_drop(t):
+    _copies16.pop(t.data_ptr(), None)   # t is alive (saved for backward), so the entry at its address is its own
+
+
 # ----------------------------------------------------------------------------- conv / pool (NHWC)
 def _pair(v):
     return (v, v) if isinstance(v, int) else tuple(v)
@@ -292,8 +336,12 @@ class _Conv2dNHWCFn(torch.autograd.Function):
         # 16-bit matmul precision with 8-aligned channels: keep the forward's 16-bit copy of x for the
         # backward's gathers (srk_conv2d_nhwc_fwd16; the library reports whether it wrote it)
         x16, written = None, ctypes.c_int(0)
-        if _lib.matmul_precision() != "fp32" and Ci % 8 == 0 and Co % 8 == 0 and ctx.needs_input_grad[1]:
-            x16 = torch.empty(x.numel(), device=x.device, dtype=torch.int16)
+        if _lib.matmul_precision() != "fp32" and Ci % 8 == 0 and Co % 8 == 0:
+            x16 = _copy16_get(x)   # the producing BatchNorm's copy (written = 2: ready)
+            if x16 is not None:
+                written.value = 2
+            elif ctx.needs_input_grad[1]:
+                x16 = torch.empty(x.numel(), device=x.device, dtype=torch.int16)
         call("srk_conv2d_nhwc_fwd16", ptr(x), N, H, W, Ci, ptr(w), ptr(b) if b is not None else None, Co, KH, KW,
              ph, pw, sh, sw, ptr(y), ptr(ws), ptr(x16) if x16 is not None else None, ctypes.byref(written),
              stream_ptr())
@@ -316,9 +364,10 @@ class _Conv2dNHWCFn(torch.autograd.Function):
         ws = torch.empty(int(_lib.lib().srk_conv2d_workspace_floats(Ci, Co, KH, KW)), device=x.device)
         x16 = ctx.x16 if ctx.prec == _lib.matmul_precision() else None   # a copy in this precision only
         ctx.x16 = None
-        call("srk_conv2d_nhwc_bwd16", ptr(x), N, H, W, Ci, ptr(w), Co, KH, KW, ph, pw, sh, sw, ptr(dy),
-             ptr(dx) if dx is not None else None, ptr(dw), ptr(db) if db is not None else None, ptr(ws),
-             ptr(x16) if x16 is not None else None, stream_ptr())
+        dy16 = _copy16_get(dy, pop=True)   # the producing BatchNorm backward's copy of dY
+        call("srk_conv2d_nhwc_bwd16_dy16", ptr(x), N, H, W, Ci, ptr(w), Co, KH, KW, ph, pw, sh, sw, ptr(dy),
+             ptr(dy16) if dy16 is not None else None, ptr(dx) if dx is not None else None, ptr(dw),
+             ptr(db) if db is not None else None, ptr(ws), ptr(x16) if x16 is not None else None, stream_ptr())
         return dx, dw, db, None, None
 
 
@@ -645,9 +694,14 @@ class _BatchNormFn(torch.autograd.Function):
         mean = torch.empty(C, device=x.device)
         invstd = torch.empty(C, device=x.device)
         res = residual.contiguous() if residual is not None else None
-        call("srk_batchnorm_fwd", ptr(x), M, C, ptr(gamma), ptr(beta), float(eps), float(momentum), int(training),
-             ptr(running_mean), ptr(running_var), ptr(res) if res is not None else None, int(relu), ptr(y), ptr(mean),
-             ptr(invstd), stream_ptr())
+        y16, written = None, ctypes.c_int(0)
+        if training and any(ctx.needs_input_grad[:4]) and _copy16_wanted(C):   # the consuming conv's 16-bit copy of y
+            y16 = torch.empty(y.numel(), device=x.device, dtype=torch.int16)
+        call("srk_batchnorm_fwd16", ptr(x), M, C, ptr(gamma), ptr(beta), float(eps), float(momentum), int(training),
+             ptr(running_mean), ptr(running_var), ptr(res) if res is not None else None, int(relu), ptr(y),
+             ptr(y16) if y16 is not None else None, ctypes.byref(written), ptr(mean), ptr(invstd), stream_ptr())
+        if written.value:
+            _copy16_put(y, y16)
         ctx.save_for_backward(x, y, gamma, mean, invstd)
         ctx.flags = (int(training), int(relu), residual is not None)
         return y
@@ -663,9 +717,15 @@ class _BatchNormFn(torch.autograd.Function):
         dres = torch.empty_like(x) if has_res and ctx.needs_input_grad[3] else None
         dgamma = torch.empty(C, device=x.device)
         dbeta = torch.empty(C, device=x.device)
-        call("srk_batchnorm_bwd", ptr(x), ptr(y), ptr(dy), M, C, ptr(gamma), ptr(mean), ptr(invstd), training, relu,
-             ptr(dx) if dx is not None else None, ptr(dgamma), ptr(dbeta), ptr(dres) if dres is not None else None,
-             stream_ptr())
+        _copy16_drop(y)   # the forward's copy: its consumers' backward has run
+        dx16, written = None, ctypes.c_int(0)
+        if dx is not None and _copy16_wanted(C):   # dx is the producing conv's dY
+            dx16 = torch.empty(dx.numel(), device=x.device, dtype=torch.int16)
+        call("srk_batchnorm_bwd16", ptr(x), ptr(y), ptr(dy), M, C, ptr(gamma), ptr(mean), ptr(invstd), training, relu,
+             ptr(dx) if dx is not None else None, ptr(dx16) if dx16 is not None else None, ctypes.byref(written),
+             ptr(dgamma), ptr(dbeta), ptr(dres) if dres is not None else None, stream_ptr())
+        if written.value:
+            _copy16_put(dx, dx16)
         return dx, dgamma, dbeta, dres, None, None, None, None, None, None
 
 

@@ -1,0 +1,108 @@
+"""BatchNorm-emitted 16-bit conv operands (srk_batchnorm_fwd16 / _bwd16, srk_conv2d_nhwc_fwd16 with a
+ready copy, srk_conv2d_nhwc_bwd16_dy16): the copies are bitwise the rounding the convolutions apply
+themselves, and a resnet_bgru train step with them equals the step without them bit for bit
+(model_resnet_bgru.py:19-39: every conv reads a BatchNorm output, every BatchNorm dx is a conv dY)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from speechrecognitionproject_amd import _lib
+from speechrecognitionproject_amd import nn as snn
+from speechrecognitionproject_amd._lib import call
+from speechrecognitionproject_amd.features import ptr, stream_ptr
+
+pytestmark = pytest.mark.gpu
+
+TORCH16 = {"bf16": torch.bfloat16, "fp16": torch.float16}
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("M,C,relu,res", [(4096, 64, 1, 0), (1000, 128, 1, 1), (333, 512, 0, 0), (17, 8, 1, 1)])
+def test_batchnorm_copies_are_the_conv_rounding(gpu, prec, M, C, relu, res):
+    g = torch.Generator().manual_seed(M + C)
+    x = (torch.randn(M, C, generator=g) * 3 + 0.5).cuda()
+    gamma, beta = (torch.rand(C, generator=g) + 0.5).cuda(), torch.randn(C, generator=g).cuda()
+    r = torch.randn(M, C, generator=g).cuda() if res else None
+    dy = torch.randn(M, C, generator=g).cuda()
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    out = {}
+    try:
+        for p in ("fp32", prec):
+            _lib.set_matmul_precision(p)
+            y, mean, inv = torch.empty_like(x), torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+            y16 = torch.full((M * C,), 7, dtype=torch.int16, device="cuda")
+            wy = ctypes.c_int(-1)
+            call("srk_batchnorm_fwd16", ptr(x), M, C, ptr(gamma), ptr(beta), 1e-5, 0.1, 1, ptr(rm), ptr(rv),
+                 ptr(r) if r is not None else None, relu, ptr(y), ptr(y16), ctypes.byref(wy), ptr(mean), ptr(inv),
+                 stream_ptr())
+            dx, dg, db, dr = (torch.empty_like(x), torch.empty(C, device="cuda"), torch.empty(C, device="cuda"),
+                              torch.empty_like(x) if res else None)
+            dx16 = torch.full((M * C,), 7, dtype=torch.int16, device="cuda")
+            wd = ctypes.c_int(-1)
+            call("srk_batchnorm_bwd16", ptr(x), ptr(y), ptr(dy), M, C, ptr(gamma), ptr(mean), ptr(inv), 1, relu,
+                 ptr(dx), ptr(dx16), ctypes.byref(wd), ptr(dg), ptr(db), ptr(dr) if dr is not None else None,
+                 stream_ptr())
+            torch.cuda.synchronize()
+            out[p] = (y, y16, wy.value, dx, dx16, wd.value, dg, db, dr)
+    finally:
+        _lib.set_matmul_precision("fp32")
+    y, y16, wy, dx, dx16, wd, dg, db, dr = out[prec]
+    assert out["fp32"][2] == 0 and out["fp32"][5] == 0            # fp32 precision: no copies, untouched
+    assert bool((out["fp32"][1] == 7).all()) and bool((out["fp32"][4] == 7).all())
+    assert wy == 1 and wd == 1
+    for a, b in zip(out["fp32"][:1] + out["fp32"][3:4] + out["fp32"][6:], (y, dx, dg, db, dr)):
+        assert (a is None and b is None) or torch.equal(a, b)      # the fp32 outputs do not depend on the copies
+    t = TORCH16[prec]
+    assert torch.equal(y16, y.reshape(-1).to(t).view(torch.int16))
+    assert torch.equal(dx16, dx.reshape(-1).to(t).view(torch.int16))
+
+
+def _resnet_step(net, x, y):
+    net.zero_grad()
+    out = net(x)
+    loss = snn.CrossEntropyLoss()(out, y)
+    loss.backward()
+    torch.cuda.synchronize()
+    return out.detach().clone(), {n: p.grad.detach().clone() for n, p in net.named_parameters() if p.grad is not None}
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_resnet_bgru_step_with_bn_copies_is_bitwise(gpu, prec):
+    from speechrecognitionproject_amd.models import model_resnet_bgru
+    torch.manual_seed(3)
+    net = model_resnet_bgru.Network().cuda().train()
+    g = np.random.default_rng(4)
+    x = torch.from_numpy(g.standard_normal((6, 16000)).astype(np.float32) * 0.1).cuda()
+    y = torch.from_numpy(g.integers(0, 12, 6)).cuda()
+    state = {k: v.clone() for k, v in net.state_dict().items()}
+    res, to16 = {}, {}
+    prev = snn.COPIES16
+    try:
+        _lib.set_matmul_precision(prec)
+        for on in (True, False, True):
+            net.load_state_dict(state)   # the running statistics too
+            snn.COPIES16 = on
+            _lib.prof_enable(True)
+            res.setdefault(on, []).append(_resnet_step(net, x, y))
+            to16[on] = _lib.prof_read("conv_to16")
+            _lib.prof_enable(False)
+            assert len(snn._copies16) == 0, list(snn._copies16)   # every entry consumed or dropped
+    finally:
+        snn.COPIES16 = prev
+        _lib.set_matmul_precision("fp32")
+    (o1, g1), (o3, g3) = res[True]
+    (o0, g0), = res[False]
+    assert torch.isfinite(o1).all()
+    assert torch.equal(o1, o0) and torch.equal(o1, o3)
+    assert g1.keys() == g0.keys()
+    for n in g0:
+        assert torch.equal(g1[n], g0[n]), n
+    # with the BatchNorm copies the convolutions round only their weights (W for the forward, the data
+    # gradient's Wd; 6 B of traffic per element), no activation or gradient (the stem, Ci = 1, has no 16-bit path)
+    wbytes = sum(12.0 * m.weight.numel() for m in net.modules()
+                 if isinstance(m, snn.Conv1d) and m.in_channels % 8 == 0 and m.out_channels % 8 == 0
+                 and m.weight.grad is not None)
+    assert to16[True][2] == wbytes, (to16[True], wbytes)
+    assert to16[False][2] > wbytes, (to16[False], wbytes)

@@ -647,7 +647,7 @@ def test_bigru_dwhh_fused_matches_gemm(prec, B, T, IN, wide):
     try:
         _lib.set_matmul_precision(prec)
         _lib.set_option("gru_lp_wide", wide)
-        for fused in (1, 0):
+        for fused in (1, 0, 3, 5, 7):   # 3 / 5 / 7: the h_prev fetch / priority timing variants, bitwise mode 1
             _lib.set_option("gru_dwhh_fused", fused)
             mine.zero_grad()
             xm = x.clone().requires_grad_(True)
@@ -667,6 +667,9 @@ def test_bigru_dwhh_fused_matches_gemm(prec, B, T, IN, wide):
         _lib.set_option("gru_lp_wide", 1)
         _lib.set_matmul_precision("fp32")
     assert _lib.spin_timeouts() == 0
+    for v in res[2:]:
+        for n in res[0]:
+            assert torch.equal(res[0][n], v[n]), n
     for n in res[0]:
         a, b = res[0][n], res[1][n]
         assert torch.isfinite(a).all(), n

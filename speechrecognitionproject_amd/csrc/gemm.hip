@@ -41,6 +41,7 @@ struct KernelArgs {
   int sk_wgs;
   int sk_ki;
   float* sk_slab;
+  int nt_store;          // option gemm_nt_store: the final C stores of pp_epilogue non-temporal
 };
 
 // tile index t (one split's grid, grouped order) -> (tile row, tile column); see map_tile
@@ -916,7 +917,8 @@ __device__ __forceinline__ void pp_epilogue(const KernelArgs& ka, const f32x16 (
       }
       if (vec && col + 3 < d.N) {
         if (!split_mode && d.beta != 0.f) x += d.beta * *reinterpret_cast<const v4f*>(c);
-        *reinterpret_cast<v4f*>(c) = x;
+        if (ka.nt_store) __builtin_nontemporal_store(x, reinterpret_cast<v4f*>(c));
+        else *reinterpret_cast<v4f*>(c) = x;
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1779,6 +1781,7 @@ int plan_launch(const GemmDesc& d, int BM, int BN, int BK, int per_cu, KernelArg
   ka.group_m = group_env > 0 ? group_env
                              : std::max(1, (int)std::lround(std::sqrt(32.0 * per_cu * BN / (double)BM)));
   ka.remap = remap;
+  ka.nt_store = g_opt_gemm_nt_store;
   // Split K when the output grid leaves resident slots idle and K is long (tile::choose_splits).
   const bool can_split = allow_split && (d.batch == 1 || split_batched);
   int splits = can_split ? choose_splits(tm * tn * d.batch, d.K, BK, slots, 16) : 1;

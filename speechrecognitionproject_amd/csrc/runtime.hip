@@ -32,6 +32,7 @@ int g_opt_gemm_streamk = 1;
 int g_opt_gemm16_persistent = 0;
 int g_opt_gemm16_qs = 1;
 int g_opt_gemm16_prio = 0;
+int g_opt_gemm_nt_store = 0;
 int g_opt_gemm32_kernel = 0;
 static std::atomic<int> g_opt_matmul_prec{kPrecF32};
 int matmul_prec() { return g_opt_matmul_prec.load(std::memory_order_relaxed); }
@@ -374,6 +375,10 @@ int srk_set_option(const char* name, int64_t value) {
   }
   if (n == "gemm16_prio") {   // 16-bit ping-pong GEMM: static priority for waves 4-7 (1) or per-section flips (0)
     srk::g_opt_gemm16_prio = value != 0;
+    return SRK_OK;
+  }
+  if (n == "gemm_nt_store") {   // ping-pong GEMMs: non-temporal C stores in the LDS-staged epilogue (1) or plain (0)
+    srk::g_opt_gemm_nt_store = value != 0;
     return SRK_OK;
   }
   if (n == "gemm16_persistent") {   // 16-bit ping-pong GEMM: persistent tile loop (1) or one tile per workgroup (0)

@@ -129,6 +129,8 @@ extern int g_opt_gemm16_persistent;
 extern int g_opt_gemm16_qs;
 // 16-bit ping-pong GEMM: static priority for waves 4-7 instead of per-section flips ("gemm16_prio")
 extern int g_opt_gemm16_prio;
+// ping-pong GEMMs: non-temporal stores of C in the LDS-staged epilogue ("gemm_nt_store")
+extern int g_opt_gemm_nt_store;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -208,6 +208,20 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
                       const float* w_hh, const float* y, const float* ws_fwd, const float* dy, float* dx,
                       float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, int accumulate, float* ws,
                       void* stream);
+/* The same pair taking x's ready 16-bit copy x16 ([B*T][in] bf16 / fp16 at the current precision,
+ * in % 8 == 0, 16-B aligned; nullable = the plain pair) instead of rounding x: a 2-layer BiGRU's
+ * second layer reads the first layer's own 16-bit h copy, which srk_gru_y16_offset locates in that
+ * layer's forward workspace (in floats; -1 when the layer does not take the 16-bit path).  The
+ * backward must get the forward's x16.  Bitwise the results of the plain pair (the kernels round h
+ * exactly as the conversion of x would).                                                          */
+int64_t srk_gru_y16_offset(int64_t B, int64_t T, int64_t in, int64_t H);
+int srk_gru_layer_fwd_x16(const float* x, const void* x16, int64_t B, int64_t T, int64_t in, int64_t H,
+                          const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, float* y,
+                          float* ws, void* stream);
+int srk_gru_layer_bwd_x16(const float* x, const void* x16, int64_t B, int64_t T, int64_t in, int64_t H,
+                          const float* w_ih, const float* w_hh, const float* y, const float* ws_fwd, const float* dy,
+                          float* dx, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, int accumulate,
+                          float* ws, void* stream);
 
 /* ---------------------------------------------------------------- K6: convolution / pooling
  * nn.Conv2d / nn.Conv1d (zero padding ph/pw, stride sh/sw, no dilation/groups) as implicit GEMM

@@ -52,6 +52,9 @@ _SIGS = {
     "srk_gru_workspace_floats": [_I64, _I64, _I64, _I64, _I],
     "srk_gru_layer_fwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P],
     "srk_gru_layer_bwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
+    "srk_gru_y16_offset": [_I64, _I64, _I64, _I64],
+    "srk_gru_layer_fwd_x16": [_P, _P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P],
+    "srk_gru_layer_bwd_x16": [_P, _P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     "srk_conv2d_workspace_floats": [_I64, _I64, _I64, _I64],
     "srk_conv2d_nhwc_fwd": [_P, _I64, _I64, _I64, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P,
                             _P],
@@ -91,7 +94,7 @@ _SIGS = {
     "srk_adam_step_scaled": [_P, _P, _P, _P, _I64, _F, _F, _F, _P, _F, _P, _P],
     "srk_dropout_apply": [_P, _P, _I64, _F, _P, _P],
 }
-_RESTYPE = {"srk_last_error": ctypes.c_char_p, "srk_spin_timeouts": ctypes.c_int64, "srk_scratch_generation": ctypes.c_int64, "srk_gru_workspace_floats": ctypes.c_int64,
+_RESTYPE = {"srk_last_error": ctypes.c_char_p, "srk_spin_timeouts": ctypes.c_int64, "srk_scratch_generation": ctypes.c_int64, "srk_gru_workspace_floats": ctypes.c_int64, "srk_gru_y16_offset": ctypes.c_int64,
             "srk_conv2d_workspace_floats": ctypes.c_int64, "srk_conv1_pool_workspace_floats": ctypes.c_int64}
 
 

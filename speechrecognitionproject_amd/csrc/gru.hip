@@ -520,6 +520,18 @@ int64_t srk_gru_workspace_floats(int64_t B, int64_t T, int64_t in, int64_t H, in
 
 int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t H, const float* w_ih,
                       const float* w_hh, const float* b_ih, const float* b_hh, float* y, float* ws, void* stream) {
+  return srk_gru_layer_fwd_x16(x, nullptr, B, T, in, H, w_ih, w_hh, b_ih, b_hh, y, ws, stream);
+}
+
+int64_t srk_gru_y16_offset(int64_t B, int64_t T, int64_t in, int64_t H) {
+  if (srk::check_dims(B, T, in, H) || H != 512 || !use_h16(B, T, in, H)) return -1;
+  const int64_t in8 = in8_of(in), BT = B * T;
+  return pad_end(B, T, in, H, 0) + up64(BT * in8 / 2 + 1) + up64(6 * H * in8 / 2 + 1);
+}
+
+int srk_gru_layer_fwd_x16(const float* x, const void* x16_in, int64_t B, int64_t T, int64_t in, int64_t H,
+                          const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, float* y,
+                          float* ws, void* stream) {
   SRK_API_BEGIN
   if (int rc = srk::check_dims(B, T, in, H)) return rc;
   SRK_REQUIRE(x && w_ih && w_hh && b_ih && b_hh && y && ws, SRK_ERR_INVALID, "gru_fwd: null pointer");
@@ -532,7 +544,11 @@ int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
     uint16_t* x16 = reinterpret_cast<uint16_t*>(ws + pad_end(B, T, in, H, 0));
     uint16_t* w16 = x16 + 2 * up64(BT * in8 / 2 + 1);
     y16 = w16 + 2 * up64(6 * H * in8 / 2 + 1);
-    if (int rc = srk::to16(x, BT, in, x16, in8, s)) return rc;
+    // x16_in: the producer's copy of x (the previous layer's y16), used as it is: in == in8 only
+    SRK_REQUIRE(!x16_in || (in8 == in && reinterpret_cast<uintptr_t>(x16_in) % 16 == 0), SRK_ERR_INVALID,
+                "gru_fwd: a ready 16-bit x needs in % 8 == 0 and 16-B alignment");
+    if (x16_in) x16 = const_cast<uint16_t*>(static_cast<const uint16_t*>(x16_in));
+    else if (int rc = srk::to16(x, BT, in, x16, in8, s)) return rc;
     if (int rc = srk::to16(w_ih, 6 * H, in, w16, in8, s)) return rc;
     const bool fuse = in <= srk::kFusedIn;   // the kernel projects the input itself (no gi GEMM)
     if (!fuse) {
@@ -606,6 +622,14 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
                       const float* w_hh, const float* y, const float* ws_fwd, const float* dy, float* dx,
                       float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, int accumulate, float* ws,
                       void* stream) {
+  return srk_gru_layer_bwd_x16(x, nullptr, B, T, in, H, w_ih, w_hh, y, ws_fwd, dy, dx, dw_ih, dw_hh, db_ih, db_hh,
+                               accumulate, ws, stream);
+}
+
+int srk_gru_layer_bwd_x16(const float* x, const void* x16_in, int64_t B, int64_t T, int64_t in, int64_t H,
+                          const float* w_ih, const float* w_hh, const float* y, const float* ws_fwd, const float* dy,
+                          float* dx, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, int accumulate,
+                          float* ws, void* stream) {
   SRK_API_BEGIN
   if (int rc = srk::check_dims(B, T, in, H)) return rc;
   SRK_REQUIRE(x && w_ih && w_hh && y && ws_fwd && dy && dw_ih && dw_hh && db_ih && db_hh && ws, SRK_ERR_INVALID,
@@ -619,6 +643,7 @@ int srk_gru_layer_bwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t 
     const uint16_t* x16 = reinterpret_cast<const uint16_t*>(ws_fwd + pad_end(B, T, in, H, 0));
     const uint16_t* w16 = x16 + 2 * up64(BT * in8 / 2 + 1);
     const uint16_t* y16 = w16 + 2 * up64(6 * H * in8 / 2 + 1);
+    if (x16_in) x16 = static_cast<const uint16_t*>(x16_in);   // the forward's ready copy (srk_gru_layer_fwd_x16)
     uint16_t* dgi16 = reinterpret_cast<uint16_t*>(ws);
     uint16_t* dgh16 = dgi16 + BT * 6 * H;
     float* part = ws + pad_end(B, T, in, H, 1);

@@ -80,8 +80,15 @@ class _GRULayerFn(torch.autograd.Function):
         _check_cuda(x, w_ih, w_hh, b_ih, b_hh)
         y = torch.empty((B, T, 2 * H), device=x.device, dtype=torch.float32)
         ws = torch.empty(int(_lib.lib().srk_gru_workspace_floats(B, T, IN, H, 0)), device=x.device)
-        call("srk_gru_layer_fwd", ptr(x), B, T, IN, H, ptr(w_ih), ptr(w_hh), ptr(b_ih), ptr(b_hh), ptr(y), ptr(ws),
-             stream_ptr())
+        # 16-bit modes: the previous layer's own 16-bit copy of h is this layer's x16 (module note at
+        # _copies16); this layer's copy of its output goes to the next layer
+        x16 = _copy16_get(x) if IN % 8 == 0 else None
+        call("srk_gru_layer_fwd_x16", ptr(x), ptr(x16) if x16 is not None else None, B, T, IN, H, ptr(w_ih),
+             ptr(w_hh), ptr(b_ih), ptr(b_hh), ptr(y), ptr(ws), stream_ptr())
+        ctx.x16 = x16
+        off = int(_lib.lib().srk_gru_y16_offset(B, T, IN, H)) if _copy16_wanted(2 * H) else -1
+        if off >= 0 and any(ctx.needs_input_grad):
+            _copy16_put(y, ws[off:].view(torch.int16)[:y.numel()])
         ctx.save_for_backward(x, w_ih, w_hh, y, ws)
         ctx.dims = (B, T, IN, H)
         ctx.params = (w_ih_f, w_ih_r, w_hh_f, w_hh_r, b_ih_f, b_ih_r, b_hh_f, b_hh_r)
@@ -107,10 +114,12 @@ class _GRULayerFn(torch.autograd.Function):
             db_ih = torch.empty((2, 3 * H), device=x.device)
             db_hh = torch.empty((2, 3 * H), device=x.device)
         ws2 = torch.empty(int(_lib.lib().srk_gru_workspace_floats(B, T, IN, H, 1)), device=x.device)
+        _copy16_drop(y)   # the next layer's backward has run
+        x16, ctx.x16 = ctx.x16, None
         with _lib.precision_scope(ctx.prec):
-            call("srk_gru_layer_bwd", ptr(x), B, T, IN, H, ptr(w_ih), ptr(w_hh), ptr(y), ptr(ws), ptr(dy),
-                 ptr(dx) if dx is not None else None, ptr(dw_ih), ptr(dw_hh), ptr(db_ih), ptr(db_hh), int(acc),
-                 ptr(ws2), stream_ptr())
+            call("srk_gru_layer_bwd_x16", ptr(x), ptr(x16) if x16 is not None else None, B, T, IN, H, ptr(w_ih),
+                 ptr(w_hh), ptr(y), ptr(ws), ptr(dy), ptr(dx) if dx is not None else None, ptr(dw_ih), ptr(dw_hh),
+                 ptr(db_ih), ptr(db_hh), int(acc), ptr(ws2), stream_ptr())
         red = _reducer_of(P[0])
         if red is not None:
             red.persistent_done()

@@ -106,3 +106,39 @@ def test_resnet_bgru_step_with_bn_copies_is_bitwise(gpu, prec):
                  and m.weight.grad is not None)
     assert to16[True][2] == wbytes, (to16[True], wbytes)
     assert to16[False][2] > wbytes, (to16[False], wbytes)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("B,T,IN", [(256, 51, 39), (512, 9, 321), (70, 5, 1024)])
+def test_bigru_layer_handover_is_bitwise(gpu, prec, B, T, IN):
+    """srk_gru_layer_fwd_x16 / _bwd_x16: the second layer of a 2-layer BiGRU reads the first layer's own
+    16-bit copy of h (srk_gru_y16_offset) instead of rounding its fp32 input again; outputs and every
+    gradient equal the plain path bit for bit (cfg2 and cfg5 layer shapes; B = 512: the 64-row kernels)."""
+    H = 512
+    torch.manual_seed(7)
+    mine = snn.BiGRU(IN, H, num_layers=2).cuda()
+    x = torch.randn(B, T, IN, device="cuda")
+    w = torch.randn(B, T, 2 * H, device="cuda")
+    res, seen = [], []
+    prev = snn.COPIES16
+    try:
+        _lib.set_matmul_precision(prec)
+        for on in (True, False):
+            snn.COPIES16 = on
+            mine.zero_grad()
+            xm = x.clone().requires_grad_(True)
+            ym, _ = mine(xm)
+            seen.append(len(snn._copies16))
+            (ym * w).sum().backward()
+            torch.cuda.synchronize()
+            assert len(snn._copies16) == 0, list(snn._copies16)
+            res.append({"y": ym.detach().clone(), "dx": xm.grad.clone(),
+                        **{n: p.grad.detach().clone() for n, p in mine.named_parameters()}})
+    finally:
+        snn.COPIES16 = prev
+        _lib.set_matmul_precision("fp32")
+    assert seen == [2, 0], seen   # both layers' outputs handed over while the step was live
+    assert _lib.spin_timeouts() == 0
+    for n in res[0]:
+        assert torch.isfinite(res[0][n]).all(), n
+        assert torch.equal(res[0][n], res[1][n]), n

@@ -199,7 +199,8 @@ int srk_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, float* out
  * (accumulate = 0) or ADDS TO (accumulate = 1: autograd's .grad accumulation, done in the GEMM
  * epilogues) dw_ih, dw_hh, db_ih, db_hh (same stacked layouts).  The backward must run at the
  * matmul_precision of its forward (with bf16 / fp16 the forward workspace carries the 16-bit
- * operands of the backward's GEMMs).                                                          */
+ * operands of the backward's GEMMs; a layer with the fused input projection, in <= 64, leaves the
+ * 16-bit W_ih slot to the backward, which fills it there only when dx is requested).          */
 int64_t srk_gru_workspace_floats(int64_t B, int64_t T, int64_t in, int64_t H, int backward);
 int srk_gru_layer_fwd(const float* x, int64_t B, int64_t T, int64_t in, int64_t H, const float* w_ih,
                       const float* w_hh, const float* b_ih, const float* b_hh, float* y, float* ws,

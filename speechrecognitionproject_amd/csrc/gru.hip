@@ -373,10 +373,10 @@ int to16(const float* src, int64_t rows, int64_t cols, uint16_t* dst, int64_t co
 // Bias gradients from the 16-bit backward kernel's partials [part][2 dir][4][H] (sums of dar, daz,
 // dan, dan * r), summed over the valid (chunk, group) parts in order: db_ih = (dar, daz, dan),
 // db_hh = (dar, daz, dan * r); `accumulate` adds into the caller's tensors.
-__global__ void dbias_reduce_kernel(const float* __restrict__ part, int nparts, int B, int H, int rows_per_part,
-                                    float* __restrict__ db_ih, float* __restrict__ db_hh, int accumulate) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over [2 dir][3][H]
-  if (i >= 2 * 3 * H) return;
+__device__ __forceinline__ void dbias_reduce_at(int i, const float* __restrict__ part, int nparts, int B, int H,
+                                                int rows_per_part, float* __restrict__ db_ih,
+                                                float* __restrict__ db_hh, int accumulate) {
+  if (i >= 2 * 3 * H) return;   // i over [2 dir][3][H]
   const int dir = i / (3 * H), g = (i / H) % 3, j = i % H;
   const int per_chunk = 256 / rows_per_part;
   float si = 0.f, sh = 0.f;
@@ -389,14 +389,25 @@ __global__ void dbias_reduce_kernel(const float* __restrict__ part, int nparts, 
   db_ih[i] = accumulate ? db_ih[i] + si : si;
   db_hh[i] = accumulate ? db_hh[i] + sh : sh;
 }
+__global__ void dbias_reduce_kernel(const float* __restrict__ part, int nparts, int B, int H, int rows_per_part,
+                                    float* __restrict__ db_ih, float* __restrict__ db_hh, int accumulate) {
+  dbias_reduce_at(blockIdx.x * blockDim.x + threadIdx.x, part, nparts, B, H, rows_per_part, db_ih, db_hh, accumulate);
+}
 
-// dW_hh[dir] (+)= sum over the fused backward's partials [part][2 dir][3H][H], in part order
-// (deterministic); 4 consecutive columns per thread
+// Both reductions of the fused 16-bit backward in one launch.  Blocks [0, dw_blocks): dW_hh[dir] (+)= sum
+// over the partials [part][2 dir][3H][H] in part order (deterministic), 4 consecutive columns per thread
 // (part p = chunk * 8 + group covers batch rows 256 chunk + 32 group ..; parts past the batch were never
-// written and are skipped)
-__global__ void dwhh_reduce_kernel(const float* __restrict__ part, int nparts, int B, int64_t per_dir,
-                                   float* __restrict__ dw, int accumulate) {
-  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over [2 dir][3H][H] / 4
+// written and are skipped).  The rest: the bias gradients, as dbias_reduce_kernel.
+__global__ void dwhh_dbias_reduce_kernel(const float* __restrict__ part, int nparts, int B, int64_t per_dir,
+                                         float* __restrict__ dw, int accumulate, int dw_blocks,
+                                         const float* __restrict__ bpart, int bparts, int H, int rows_per_part,
+                                         float* __restrict__ db_ih, float* __restrict__ db_hh) {
+  if ((int)blockIdx.x >= dw_blocks) {
+    dbias_reduce_at(((int)blockIdx.x - dw_blocks) * blockDim.x + threadIdx.x, bpart, bparts, B, H, rows_per_part,
+                    db_ih, db_hh, accumulate);
+    return;
+  }
+  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i4 * 4 >= 2 * per_dir) return;
   const int64_t o = i4 * 4, dir = o / per_dir, e = o - dir * per_dir;
   v4f acc = accumulate ? *reinterpret_cast<const v4f*>(dw + o) : v4f{0.f, 0.f, 0.f, 0.f};
@@ -549,9 +560,10 @@ int srk_gru_layer_fwd_x16(const float* x, const void* x16_in, int64_t B, int64_t
                 "gru_fwd: a ready 16-bit x needs in % 8 == 0 and 16-B alignment");
     if (x16_in) x16 = const_cast<uint16_t*>(static_cast<const uint16_t*>(x16_in));
     else if (int rc = srk::to16(x, BT, in, x16, in8, s)) return rc;
-    if (int rc = srk::to16(w_ih, 6 * H, in, w16, in8, s)) return rc;
     const bool fuse = in <= srk::kFusedIn;   // the kernel projects the input itself (no gi GEMM)
+    // W16: the gi GEMM's operand; with the fused projection only the backward's dx needs it (rounded there)
     if (!fuse) {
+      if (int rc = srk::to16(w_ih, 6 * H, in, w16, in8, s)) return rc;
       GemmDesc g;   // gi[B*T, 6H] = x16 * W16^T + b_ih
       g.M = BT; g.N = 6 * H; g.K = in8;
       g.A16 = x16; g.lda = in8;
@@ -664,16 +676,18 @@ int srk_gru_layer_bwd_x16(const float* x, const void* x16_in, int64_t B, int64_t
       p.y16_in = y16;
     }
     if ((rc = srk::gru_persistent_launch(p, true, s))) return rc;
-    if (dw_parts) {
-      const int64_t per_dir = 3 * H * H, n4 = 2 * per_dir / 4;
-      srk::ProfScope prof("gru_dwhh_reduce", s, 4.0 * (dw_parts + 2) * 2 * per_dir);
-      hipLaunchKernelGGL(srk::dwhh_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, p.dw_part,
-                         dw_parts, (int)B, per_dir, dw_hh, (int)accumulate);
-      SRK_CHECK_HIP(hipGetLastError());
-    }
     const int prows = srk::gru_bias_part_rows(B);
-    hipLaunchKernelGGL(srk::dbias_reduce_kernel, dim3((unsigned)((6 * H + 255) / 256)), dim3(256), 0, s, part,
-                       (int)(chunks * (256 / prows)), (int)B, (int)H, prows, db_ih, db_hh, accumulate);
+    if (dw_parts) {   // dW_hh and the bias gradients from their partials: one launch
+      const int64_t per_dir = 3 * H * H, n4 = 2 * per_dir / 4;
+      const int dw_blocks = (int)((n4 + 255) / 256);
+      srk::ProfScope prof("gru_dwhh_reduce", s, 4.0 * (dw_parts + 2) * 2 * per_dir);
+      hipLaunchKernelGGL(srk::dwhh_dbias_reduce_kernel, dim3((unsigned)(dw_blocks + (6 * H + 255) / 256)), dim3(256),
+                         0, s, p.dw_part, dw_parts, (int)B, per_dir, dw_hh, (int)accumulate, dw_blocks, part,
+                         (int)(chunks * (256 / prows)), (int)H, prows, db_ih, db_hh);
+    } else {
+      hipLaunchKernelGGL(srk::dbias_reduce_kernel, dim3((unsigned)((6 * H + 255) / 256)), dim3(256), 0, s, part,
+                         (int)(chunks * (256 / prows)), (int)B, (int)H, prows, db_ih, db_hh, accumulate);
+    }
     SRK_CHECK_HIP(hipGetLastError());
     const float beta = accumulate ? 1.f : 0.f;
     {  // dW_ih [6H, in] = dgi16^T x16
@@ -702,7 +716,7 @@ int srk_gru_layer_bwd_x16(const float* x, const void* x16_in, int64_t B, int64_t
       g.C = dw_hh; g.ldc = H; g.beta = beta;
       g.batch = 2; g.sA = BT * 3 * H - 3 * H; g.sB = 3 * H; g.sC = 3 * H * H;
       if (dw_parts) {
-        // done: the recurrence kernel accumulated it (dwhh_reduce_kernel above)
+        // done: the recurrence kernel accumulated it (dwhh_dbias_reduce_kernel above)
       } else if (g.K > 0 && srk::g_opt_gru_dwhh_batched) {
         if ((rc = srk::gemm_f32(g, s))) return rc;
       } else if (g.K > 0) {   // one launch per direction (A/B and tests)
@@ -714,6 +728,9 @@ int srk_gru_layer_bwd_x16(const float* x, const void* x16_in, int64_t B, int64_t
       }
     }
     if (dx) {   // dx [BT, in] = dgi16 W16
+      if (in <= srk::kFusedIn) {   // the fused-projection forward left W16 unwritten: round it here
+        if ((rc = srk::to16(w_ih, 6 * H, in, const_cast<uint16_t*>(w16), in8, s))) return rc;
+      }
       GemmDesc g;
       g.M = BT; g.N = in8; g.K = 6 * H;
       g.A16 = dgi16; g.lda = 6 * H;

@@ -18,9 +18,20 @@ def env_world():
     return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def nccl_env_for_graph_capture():
+    """Process-group settings the HIP-graph-captured collectives need, set before the group exists.
+    ProcessGroupNCCL recycles its work events through a cache: an event last recorded while a step was
+    being captured (a captured all-reduce's end event) can be handed to a later eager collective, and the
+    watchdog thread's query of it then fails on ROCm ("operation not permitted on an event last recorded
+    in a capturing stream", seen once in the 1-rank capture test) and aborts the process.  Fresh events
+    per collective avoid that (TORCH_NCCL_CUDA_EVENT_CACHE=0; an explicit setting is kept)."""
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+
+
 def init_from_env(backend=None):
     """Initialise the default process group if WORLD_SIZE > 1; returns (rank, world, local_rank)."""
     world, rank, local = env_world()
+    nccl_env_for_graph_capture()
     if world > 1 and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"

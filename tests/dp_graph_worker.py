@@ -28,8 +28,10 @@ def main():
     name, B, precision = sys.argv[1], int(sys.argv[2]), sys.argv[3]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from speechrecognitionproject_amd.parallel import nccl_env_for_graph_capture
+    nccl_env_for_graph_capture()   # as bench.py / training.py (parallel.init_from_env)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     import importlib
 
     from oracle import models as OM

@@ -582,9 +582,11 @@ def test_gemm16_qs(prec, ta, tb, M, N, K, beta):
     outs = []
     try:
         _lib.set_option("gemm16_kernel", 2)
-        for qs, prio in ((2, 0), (1, 1), (1, 0)):   # 32-deep sections; static priority (gemm16_prio); baseline
+        # 32-deep sections; static priority (gemm16_prio); non-temporal C stores (gemm_nt_store); baseline
+        for qs, prio, nt in ((2, 0, 0), (1, 1, 0), (1, 0, 1), (1, 0, 0)):
             _lib.set_option("gemm16_qs", qs)
             _lib.set_option("gemm16_prio", prio)
+            _lib.set_option("gemm_nt_store", nt)
             Cd = C0.clone().cuda()
             call("srk_gemm_16", ta, tb, M, N, K, 0.5, ptr(Ad), Ad.shape[1], ptr(Bd), Bd.shape[1], beta, ptr(Cd), N,
                  None, 0, stream_ptr())
@@ -592,10 +594,11 @@ def test_gemm16_qs(prec, ta, tb, M, N, K, beta):
     finally:
         _lib.set_option("gemm16_qs", 1)
         _lib.set_option("gemm16_prio", 0)
+        _lib.set_option("gemm_nt_store", 0)
         _lib.set_option("gemm16_kernel", 0)
     scale = (opA.abs() @ opB.abs()).max().item()
     assert (outs[0].double() - ref).abs().max().item() <= 2e-6 * (1 + scale)
-    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[2])
+    assert all(torch.equal(o, outs[-1]) for o in outs[:-1])
 
 
 @pytest.mark.parametrize("shape", [(2, 98, 40, 64, 128, 1, 7, 0, 3), (3, 98, 1, 256, 512, 7, 1, 3, 0),

@@ -291,7 +291,7 @@ class CrossEntropyLoss(tnn.Module):
 # dY entry it consumes, and the table is bounded (a step's worth of entries).
 COPIES16 = os.environ.get("SRK_BN_COPY16", "1") != "0"   # A/B switch (tests flip it)
 _copies16 = {}
-_COPIES16_MAX = 64
+_COPIES16_MAX = 32   # > the live entries of one resnet_bgru / mfrn_bgru step (about 22)
 
 
 def _copy16_wanted(C):

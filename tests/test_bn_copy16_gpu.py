@@ -79,6 +79,7 @@ def test_resnet_bgru_step_with_bn_copies_is_bitwise(gpu, prec):
     state = {k: v.clone() for k, v in net.state_dict().items()}
     res, to16 = {}, {}
     prev = snn.COPIES16
+    snn._copies16.clear()   # entries of earlier tests' forward-only calls (bounded, never consumed)
     try:
         _lib.set_matmul_precision(prec)
         for on in (True, False, True):
@@ -121,6 +122,7 @@ def test_bigru_layer_handover_is_bitwise(gpu, prec, B, T, IN):
     w = torch.randn(B, T, 2 * H, device="cuda")
     res, seen = [], []
     prev = snn.COPIES16
+    snn._copies16.clear()
     try:
         _lib.set_matmul_precision(prec)
         for on in (True, False):

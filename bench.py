@@ -38,7 +38,8 @@ Step execution: after W warm-up steps the train step is captured into HIP graphs
 (speechrecognitionproject_amd/graphs.py; per-step host values — the Adam step count and the dropout
 seed — live on the device), one per pre-staged batch slot sharing one memory pool, and the K timed
 steps are graph replays.  N > 1: forward + backward are one graph,
-the flat gradient buffer is all-reduced over RCCL between the replay and the Adam launch.
+the flat gradient buffer is all-reduced over RCCL between the replay and the Adam launch
+(--allreduce-in-graph: the bucketed all-reduces and Adam captured in the step graph, opt-in).
 --no-graph times the eager step instead (N > 1: bucketed all-reduces overlapped with backward).
 The per-kernel HIP-event timers cannot run inside a graph: kernel times ("kernels", "roofline")
 come from a separate eager pass of the same step (--prof-steps, default 5), reported with its own
@@ -413,10 +414,12 @@ class Workload:
         _lib.set_matmul_precision(precision)
         self.scaler = LossScaler(FP16_LOSS_SCALE, dynamic=False, device=self.dev) if precision == "fp16" else None
         self.opt.grad_scale = 1.0 / self.world
-        # N > 1 with HIP graphs: by default the bucketed all-reduces are captured inside the step graph
-        # (forked where each bucket's gradients are final, joined before Adam); --allreduce-outside-graph
-        # replays forward + backward and runs one flat all-reduce + Adam eagerly after it
-        self.exchange_in_graph = graph and self.world > 1 and args.overlap and not args.allreduce_outside_graph
+        # N > 1 with HIP graphs: by default forward + backward are replayed and one flat all-reduce + Adam run
+        # eagerly after it; --allreduce-in-graph captures the bucketed all-reduces inside the step graph
+        # (forked where each bucket's gradients are final, joined before Adam) — opt-in: the process group's
+        # watchdog thread aborted the 1-rank capture test now and then
+        self.exchange_in_graph = (graph and self.world > 1 and args.overlap and args.allreduce_in_graph
+                                  and not args.allreduce_outside_graph)
         self.reducer = (parallel.GradReducer(self.flat, bucket_mb=args.bucket_mb)
                         if (self.world > 1 and args.overlap and (self.exchange_in_graph or not graph)) else None)
         graphs = []
@@ -651,7 +654,10 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=8.0, help="gradient bucket size of the overlapped all-reduce")
     ap.add_argument("--allreduce-outside-graph", action="store_true",
                     help="N > 1, HIP graphs: replay forward + backward, then one flat all-reduce + Adam eagerly "
-                         "(default: the bucketed all-reduces and Adam are captured in the step graph)")
+                         "(the default; overrides --allreduce-in-graph)")
+    ap.add_argument("--allreduce-in-graph", action="store_true",
+                    help="N > 1, HIP graphs: capture the bucketed all-reduces and Adam in the step graph "
+                         "(overlapped with the backward; opt-in, DESIGN.md §4)")
     ap.add_argument("--sync-bn", action="store_true",
                     help="BatchNorm statistics over the global batch of all ranks (SyncBatchNorm1d; resnet_bgru, "
                          "cnn_bgru, mfrn_bgru)")

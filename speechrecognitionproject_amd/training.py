@@ -63,7 +63,10 @@ def parse(argv=None):
                    help='data-parallel: one all-reduce after backward instead of overlapped buckets')
     p.add_argument('--no-graph', dest='graph', action='store_false',
                    help='run every step eagerly instead of replaying a HIP graph of the step for full-size '
-                        'batches (speechrecognitionproject_amd/graphs.py; data-parallel: RCCL all-reduces in the graph)')
+                        'batches (speechrecognitionproject_amd/graphs.py; single process)')
+    p.add_argument('--dp-graph', action='store_true',
+                   help='data-parallel over RCCL: replay HIP graphs of the whole step with the all-reduces '
+                        'captured in them (opt-in, DESIGN.md §4)')
     p.add_argument('--loader', choices=('device', 'torch'), default='device',
                    help='WAV datasets: device = native batched decode + K10 on-device augmentation '
                         '(DeviceBatchLoader); torch = per-item Dataset.__getitem__ through DataLoader')
@@ -131,9 +134,10 @@ def _train(args):
     os.makedirs(args.output_path, exist_ok=True)
     loss_file = os.path.join(args.output_path, 'loss_' + key + '.txt')
 
-    # data-parallel steps are captured whole (collectives included) over RCCL only: gloo cannot be
-    # captured, and the CPU-only gloo runs have no HIP graphs anyway
-    use_graph = args.graph and (world == 1 or torch.distributed.get_backend() == 'nccl')
+    # data-parallel steps are captured whole (collectives included) only with --dp-graph, over RCCL (gloo
+    # cannot be captured): the process group's watchdog thread aborted the 1-rank capture test now and
+    # then, so the default DP step runs eagerly
+    use_graph = args.graph and (world == 1 or (args.dp_graph and torch.distributed.get_backend() == 'nccl'))
     graphed = None          # GraphedStep of a full-batch step (captured after two eager full steps)
     static = {}
     full_eager = 0

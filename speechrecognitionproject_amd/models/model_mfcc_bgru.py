@@ -10,7 +10,7 @@ import torch
 import torch.nn as nn
 
 from .. import features
-from ..nn import BiGRU, Linear
+from ..nn import BiGRU, Linear, last_step
 from ._common import DEVICE, accuracy, class_accuracy   # noqa: F401  (plugin API)
 
 
@@ -30,4 +30,4 @@ class Network(nn.Module):
         with torch.no_grad():
             inx = features.mfcc(x, time_major=True)     # [B, 51, 39] = transpose(mfcc, 1, 2)
         inx, _ = self.gru(inx)
-        return self.fc(inx[:, -1, :])
+        return self.fc(last_step(inx))

@@ -13,7 +13,7 @@ import torch
 import torch.nn as nn
 
 from .. import features
-from ..nn import BatchNorm1d, BiGRU, Conv1d, Linear
+from ..nn import BatchNorm1d, BiGRU, Conv1d, Linear, last_step
 from ._common import DEVICE, accuracy, class_accuracy   # noqa: F401  (plugin API)
 from .model_mfcc_bgru import compute_mfcc               # noqa: F401  (same function, :11-19)
 from .model_resnet_bgru import BasicBlock, _kaiming
@@ -64,7 +64,7 @@ class GRU(nn.Module):
 
     def forward(self, x):
         x, _ = self.gru(x)
-        return self.fc2(x[:, -1, :])
+        return self.fc2(last_step(x))
 
 
 class Network(nn.Module):

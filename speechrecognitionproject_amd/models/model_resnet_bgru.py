@@ -18,7 +18,7 @@ BatchNorm under data parallelism uses per-rank batch statistics (DESIGN.md §Mul
 import torch
 import torch.nn as nn
 
-from ..nn import BatchNorm1d, BiGRU, Conv1d, Linear, MaxPool1d, conv1d_nlc
+from ..nn import BatchNorm1d, BiGRU, Conv1d, Linear, MaxPool1d, conv1d_nlc, last_step
 from ._common import DEVICE, accuracy, class_accuracy   # noqa: F401
 
 
@@ -112,7 +112,7 @@ class GRU(nn.Module):
 
     def forward(self, x):
         x, _ = self.gru(x)
-        return self.fc2(x[:, -1, :])
+        return self.fc2(last_step(x))
 
 
 class Network(nn.Module):

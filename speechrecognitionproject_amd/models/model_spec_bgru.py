@@ -5,7 +5,7 @@ import torch
 import torch.nn as nn
 
 from .. import features
-from ..nn import BiGRU, Linear
+from ..nn import BiGRU, Linear, last_step
 from ._common import DEVICE, accuracy, class_accuracy   # noqa: F401
 
 
@@ -24,4 +24,4 @@ class Network(nn.Module):
         with torch.no_grad():
             inx = features.spec(x, transposed=True)     # [B, 49, 321] = transpose(spec, 1, 2)
         inx, _ = self.gru(inx)
-        return self.fc(inx[:, -1, :])
+        return self.fc(last_step(inx))

@@ -167,6 +167,27 @@ class BiGRU(tnn.Module):
         return h, torch.stack(finals)
 
 
+class _LastStepFn(torch.autograd.Function):
+    """``x[:, -1, :]`` of a [B, T, C] sequence — the models' last-step select before their fc layer
+    (model_mfcc_bgru.py:37 and the other BiGRU plugins).  The forward is the same strided view (the Linear
+    GEMM reads it by row stride); the backward writes the [B, T, C] gradient, zeros and the last step, in
+    one pad kernel instead of autograd's zero fill followed by a slice copy (one launch less per step)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.T = x.shape[1]
+        return x[:, -1, :]
+
+    @staticmethod
+    def backward(ctx, g):
+        return tnn.functional.pad(g.unsqueeze(1), (0, 0, ctx.T - 1, 0))
+
+
+def last_step(x):
+    """``x[:, -1, :]`` with a one-kernel backward (``_LastStepFn``)."""
+    return _LastStepFn.apply(x)
+
+
 # ----------------------------------------------------------------------------- Linear
 class _LinearFn(torch.autograd.Function):
     @staticmethod

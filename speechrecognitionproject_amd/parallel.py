@@ -19,12 +19,13 @@ def env_world():
 
 
 def nccl_env_for_graph_capture():
-    """Process-group settings the HIP-graph-captured collectives need, set before the group exists.
-    ProcessGroupNCCL recycles its work events through a cache: an event last recorded while a step was
-    being captured (a captured all-reduce's end event) can be handed to a later eager collective, and the
-    watchdog thread's query of it then fails on ROCm ("operation not permitted on an event last recorded
-    in a capturing stream", seen once in the 1-rank capture test) and aborts the process.  Fresh events
-    per collective avoid that (TORCH_NCCL_CUDA_EVENT_CACHE=0; an explicit setting is kept)."""
+    """Process-group settings for the (opt-in) HIP-graph-captured collectives, set before the group
+    exists.  ProcessGroupNCCL recycles its work events through a cache, so an event last recorded while a
+    step was being captured could be handed to a later eager collective, whose watchdog query would fail
+    on ROCm ("operation not permitted on an event last recorded in a capturing stream") and abort the
+    process.  TORCH_NCCL_CUDA_EVENT_CACHE=0 (an explicit setting is kept) gives every collective fresh
+    events; the abort still recurred in the 1-rank capture test, which is why the captured form is opt-in
+    (DESIGN.md §4)."""
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 

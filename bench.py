@@ -37,9 +37,10 @@ With fp32, the same line also carries "bf16": the identical step re-timed with b
 Step execution: after W warm-up steps the train step is captured into HIP graphs
 (speechrecognitionproject_amd/graphs.py; per-step host values — the Adam step count and the dropout
 seed — live on the device), one per pre-staged batch slot sharing one memory pool, and the K timed
-steps are graph replays.  N > 1: forward + backward are one graph,
-the flat gradient buffer is all-reduced over RCCL between the replay and the Adam launch
-(--allreduce-in-graph: the bucketed all-reduces and Adam captured in the step graph, opt-in).
+steps are graph replays.  N > 1: the whole step is one graph — forward, backward with the bucketed
+RCCL all-reduces forked where each bucket's gradients are final (on a process group used only under
+capture, parallel.capture_group), the join and Adam; --allreduce-outside-graph replays forward +
+backward and all-reduces the flat gradient buffer eagerly between the replay and the Adam launch.
 --no-graph times the eager step instead (N > 1: bucketed all-reduces overlapped with backward).
 The per-kernel HIP-event timers cannot run inside a graph: kernel times ("kernels", "roofline")
 come from a separate eager pass of the same step (--prof-steps, default 5), reported with its own
@@ -414,13 +415,11 @@ class Workload:
         _lib.set_matmul_precision(precision)
         self.scaler = LossScaler(FP16_LOSS_SCALE, dynamic=False, device=self.dev) if precision == "fp16" else None
         self.opt.grad_scale = 1.0 / self.world
-        # N > 1 with HIP graphs: by default forward + backward are replayed and one flat all-reduce + Adam run
-        # eagerly after it; --allreduce-in-graph captures the bucketed all-reduces inside the step graph
-        # (forked where each bucket's gradients are final, joined before Adam) — opt-in: the process group's
-        # watchdog thread aborted the 1-rank capture test now and then
-        self.exchange_in_graph = (graph and self.world > 1 and args.overlap and args.allreduce_in_graph
-                                  and not args.allreduce_outside_graph)
-        self.reducer = (parallel.GradReducer(self.flat, bucket_mb=args.bucket_mb)
+        # N > 1 with HIP graphs: the bucketed all-reduces are captured inside the step graph (forked where each
+        # bucket's gradients are final, joined before Adam) on the capture-only process group;
+        # --allreduce-outside-graph replays forward + backward and runs one flat all-reduce + Adam eagerly
+        self.exchange_in_graph = (graph and self.world > 1 and args.overlap and not args.allreduce_outside_graph)
+        self.reducer = (parallel.GradReducer(self.flat, bucket_mb=args.bucket_mb, capture_group=parallel.capture_group())
                         if (self.world > 1 and args.overlap and (self.exchange_in_graph or not graph)) else None)
         graphs = []
         if graph:
@@ -533,7 +532,8 @@ def _workload_h2d(self, precision, steps, warmup):
     host = torch.from_numpy(x).view(n_host, self.B, -1).pin_memory()
     # N > 1: the exchange as the main run settled it (in the graph, or eager after each replay)
     self.exchange_in_graph = self.world > 1 and getattr(self, "graph_allreduce", "") == "in graph"
-    self.reducer = parallel.GradReducer(self.flat, bucket_mb=self.args.bucket_mb) if self.exchange_in_graph else None
+    self.reducer = (parallel.GradReducer(self.flat, bucket_mb=self.args.bucket_mb, capture_group=parallel.capture_group())
+                    if self.exchange_in_graph else None)
     graphs = []
     for j in range(2):
         self._slot = j
@@ -654,10 +654,10 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=8.0, help="gradient bucket size of the overlapped all-reduce")
     ap.add_argument("--allreduce-outside-graph", action="store_true",
                     help="N > 1, HIP graphs: replay forward + backward, then one flat all-reduce + Adam eagerly "
-                         "(the default; overrides --allreduce-in-graph)")
+                         "(instead of the default: the bucketed all-reduces and Adam captured in the step graph, "
+                         "overlapped with the backward, DESIGN.md §4)")
     ap.add_argument("--allreduce-in-graph", action="store_true",
-                    help="N > 1, HIP graphs: capture the bucketed all-reduces and Adam in the step graph "
-                         "(overlapped with the backward; opt-in, DESIGN.md §4)")
+                    help="accepted for compatibility: the captured exchange is the default")
     ap.add_argument("--sync-bn", action="store_true",
                     help="BatchNorm statistics over the global batch of all ranks (SyncBatchNorm1d; resnet_bgru, "
                          "cnn_bgru, mfrn_bgru)")

@@ -125,6 +125,8 @@ int srk_noise_mix(const int16_t* pcm, const int16_t* bank, int64_t n_files, int6
  *   SRK_AUG_NOISE_SNR add_noise_snr (:163-181): dparam[b] = 10 ** (snr_dB / 10)
  *   SRK_AUG_SILENCE   generate_silence_sample (:148-161): float32(noise * dparam[b]); pcm unused;
  *                     noise_pos[b] < 0 gives the all-zero sample
+ *   SRK_AUG_PITCH     pitch_shifting (:225-235): out = pcm here; srk_pitch_shift (K12) then
+ *                     overwrites the clip with its shifted version (iparam[b] = n_steps)
  * noise = bank[noise_pos[b] .. + 16000) of the flat int16 noise bank (ragged files concatenated);
  * ops without noise ignore noise_pos.  The pad samples the reference draws with
  * np.random.randint(-32, 32, k) come from a counter hash of (seed, b, output position)
@@ -152,10 +154,24 @@ enum { SRK_WAV_ERR_OPEN = -1, SRK_WAV_ERR_FORMAT = -2, SRK_WAV_ERR_UNSUPPORTED =
 int srk_wav_read_batch(const char* const* paths, int64_t n, int16_t* out, int64_t* lengths, int n_threads);
 
 enum { SRK_AUG_NONE = 0, SRK_AUG_SPEED = 1, SRK_AUG_SHIFT = 2, SRK_AUG_NOISE = 3, SRK_AUG_NOISE_SNR = 4,
-       SRK_AUG_SILENCE = 5 };
+       SRK_AUG_SILENCE = 5, SRK_AUG_PITCH = 6 /* srk_augment copies the clip; srk_pitch_shift shifts it */ };
 int srk_augment(const int16_t* pcm, int64_t n_clips, const int16_t* bank, int64_t bank_len, const int32_t* op,
                 const int64_t* iparam, const int64_t* noise_pos, const double* dparam, uint64_t seed, float* out,
                 void* stream);
+
+/* K12: batched pitch_shifting, dataset.py:225-235 — np.int16(librosa.effects.pitch_shift(
+ * sample.astype(float), 16000, n_steps)) for n_steps in {-2, -1, 1, 2} (the reference's level None
+ * leaves the clip as is): librosa 0.6's time_stretch (STFT 2048 / 512, phase vocoder, inverse STFT)
+ * then resampy's kaiser_best resample from 16000 / rate to 16000 Hz, rate = 2^(-n_steps / 12)
+ * (algorithm and dtypes: oracle/pitch.py; parity unpinned — librosa / resampy are absent).
+ * For s < n_shift: out[clip_idx[s]] = the shifted pcm[clip_idx[s]] as int16-valued float32,
+ * level_idx[s] in 0..3 = n_steps -2, -1, 1, 2.  pcm: int16 [n_clips, 16000]; out: float32
+ * [n_clips, 16000] (rows not listed untouched); clip_idx / level_idx: device int32 [n_shift],
+ * validated by the caller.  One launch for the whole batch (one workgroup per shifted clip).
+ * workspace: device scratch of srk_pitch_workspace_bytes(n_shift) bytes, 16-byte aligned.     */
+int64_t srk_pitch_workspace_bytes(int64_t n_shift);
+int srk_pitch_shift(const int16_t* pcm, int64_t n_clips, const int32_t* clip_idx, const int32_t* level_idx,
+                    int64_t n_shift, float* out, void* workspace, int64_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- dense algebra (fp32 MFMA)
  * C[M,N] = alpha * op(A) op(B) + beta * C (+ bias), row-major.  op(A) = A [M,K] (lda) or, with

@@ -18,8 +18,8 @@ Pinning status
   ``sy = floor(fy)``, ``fy -= sy`` (fp32), coefficients ``(1.f - fy, fy)`` in fp32, the two
   source rows ``sy`` and ``sy + 1`` clamped to ``[0, src - 1]`` (the weight is NOT clamped),
   value ``S0 * b0 + S1 * b1`` in float64 without fused multiply-add.
-* ``pitch_shifting`` — needs librosa (absent): not restated; the product path leaves the clip
-  unchanged (DESIGN.md §Out of scope).
+* ``pitch_shifting`` — needs librosa / resampy (absent): restated separately in ``oracle/pitch.py``
+  (parity unpinned, known-answer tests), the checker of K12 ``srk_pitch_shift``.
 
 Fill samples: the reference pads shifted / resampled clips with ``np.random.randint(-32, 32, k)``
 (dataset.py:201,203,216,218).  The device draws them from a counter hash instead

@@ -42,6 +42,8 @@ _SIGS = {
     "srk_spec_fwd": [_P, _I64, _P, _I, _P],
     "srk_noise_mix": [_P, _P, _I64, _I64, _P, _P, _P, _I64, _P, _P],
     "srk_augment": [_P, _I64, _P, _I64, _P, _P, _P, _P, ctypes.c_uint64, _P, _P],
+    "srk_pitch_workspace_bytes": [_I64],
+    "srk_pitch_shift": [_P, _I64, _P, _P, _I64, _P, _P, _I64, _P],
     "srk_wav_read_batch": [ctypes.POINTER(ctypes.c_char_p), _I64, _P, _P, _I],
     "srk_softmax_ensemble": [_P, _I64, _I64, _I64, _P, _P, _P, _P],
     "srk_gemm_f32": [_I, _I, _I64, _I64, _I64, _F, _P, _I64, _P, _I64, _F, _P, _I64, _P, _I, _P],
@@ -95,7 +97,8 @@ _SIGS = {
     "srk_dropout_apply": [_P, _P, _I64, _F, _P, _P],
 }
 _RESTYPE = {"srk_last_error": ctypes.c_char_p, "srk_spin_timeouts": ctypes.c_int64, "srk_scratch_generation": ctypes.c_int64, "srk_gru_workspace_floats": ctypes.c_int64, "srk_gru_y16_offset": ctypes.c_int64,
-            "srk_conv2d_workspace_floats": ctypes.c_int64, "srk_conv1_pool_workspace_floats": ctypes.c_int64}
+            "srk_conv2d_workspace_floats": ctypes.c_int64, "srk_conv1_pool_workspace_floats": ctypes.c_int64,
+            "srk_pitch_workspace_bytes": ctypes.c_int64}
 
 
 class SrkError(RuntimeError):

@@ -11,15 +11,15 @@ Augmentations (training mode, dataset.py:107-116): time shift, uniform noise, SN
 silence synthesis are implemented here exactly.  ``speed_tuning`` re-implements cv2.resize's
 INTER_LINEAR 1-D resampling (OpenCV's generic path: fp32 source coordinate and coefficients, rows
 clamped) in numpy — cv2 is absent from this image, so this path is parity-unpinned.
-``pitch_shifting`` needs librosa.effects.pitch_shift, which is absent: it returns the sample
-unchanged and warns once (DESIGN.md §Out of scope).
+``pitch_shifting`` (librosa.effects.pitch_shift: phase-vocoder time stretch + kaiser_best resample)
+runs on the device, K12 ``srk_pitch_shift`` — librosa is absent, so it is parity-unpinned, restated
+from librosa 0.6 / resampy 0.2 (oracle/pitch.py) and pinned by known answers.
 
 ``DeviceAugment`` is the batched device counterpart of the per-item augmentation of
 ``__getitem__`` (K10, ``srk_augment``): the same draws in the same order per clip on the host
 (a handful of numbers), the arithmetic for the whole batch in one kernel launch.
 """
 import os
-import warnings
 from os import listdir
 from os.path import isfile, join
 from random import randint
@@ -31,8 +31,6 @@ from torch.utils.data import Dataset as _TorchDataset
 
 LABELS = ['yes', 'no', 'up', 'down', 'left', 'right', 'on', 'off', 'stop', 'go', 'unknown', 'silence']
 SEQ_LENGTH = 16000
-
-_pitch_warned = False
 
 
 class Dataset(_TorchDataset):
@@ -159,14 +157,15 @@ class Dataset(_TorchDataset):
         return np.int16(f_sample[int(cut / 2):int(cut / 2) + SEQ_LENGTH])
 
     def pitch_shifting(self, sample):
-        global _pitch_warned
+        """dataset.py:225-235: a level from [-2, -1, 1, 2, None]; None returns the sample, else
+        np.int16(pitch_shift(sample, 16000, n_steps=level)) — one clip through K12 on the device."""
         levels = [-2, -1, 1, 2, None]
-        if levels[randint(0, len(levels) - 1)] is None:
+        level = levels[randint(0, len(levels) - 1)]
+        if level is None:
             return sample
-        if not _pitch_warned:
-            warnings.warn("pitch_shifting needs librosa (absent): sample returned unshifted")
-            _pitch_warned = True
-        return sample
+        from .features import pitch_shift
+        pcm = torch.from_numpy(np.asarray(sample).astype(np.int16).reshape(1, SEQ_LENGTH))
+        return pitch_shift(pcm, [0], [level]).cpu().numpy()[0].astype(np.int16)
 
     def reduce_dataset(self, class_size):
         dist = np.zeros(12, dtype=np.int16)
@@ -293,8 +292,10 @@ class DeviceAugment:
             if not train:
                 continue
             prob = np.random.uniform(0, 1)
-            if prob < 0.2:                                 # pitch_shifting (librosa absent: unchanged)
-                randint(0, 4)
+            if prob < 0.2:                                 # pitch_shifting (None leaves the clip)
+                level = [-2, -1, 1, 2, None][randint(0, 4)]
+                if level is not None:
+                    op[b], ip[b] = K.AUG_PITCH, level
             if 0.2 < prob < 0.4:                           # speed_tuning
                 op[b], ip[b] = K.AUG_SPEED, int(SEQ_LENGTH * np.random.uniform(0.7, 1.3))
             if 0.4 < prob < 0.6:                           # time_stretching

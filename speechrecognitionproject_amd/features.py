@@ -9,7 +9,7 @@ import ctypes
 
 import torch
 
-from ._lib import SrkError, call
+from ._lib import SrkError, call, lib
 
 SEQ_LENGTH = 16000
 
@@ -91,7 +91,8 @@ def noise_mix(pcm_i16, bank_i16, file_idx, offsets, gains, out=None):
     return out
 
 
-AUG_NONE, AUG_SPEED, AUG_SHIFT, AUG_NOISE, AUG_NOISE_SNR, AUG_SILENCE = 0, 1, 2, 3, 4, 5
+AUG_NONE, AUG_SPEED, AUG_SHIFT, AUG_NOISE, AUG_NOISE_SNR, AUG_SILENCE, AUG_PITCH = 0, 1, 2, 3, 4, 5, 6
+PITCH_LEVELS = (-2, -1, 1, 2)      # dataset.py:230 without None (which leaves the clip unchanged)
 
 
 def augment(pcm_i16, bank_i16, op, iparam, noise_pos, dparam, seed, out=None):
@@ -115,8 +116,11 @@ def augment(pcm_i16, bank_i16, op, iparam, noise_pos, dparam, seed, out=None):
         raise SrkError("augment: inconsistent shapes")
     if n == 0:
         return torch.empty((0, SEQ_LENGTH), device=dev, dtype=torch.float32) if out is None else out
-    if op.min() < AUG_NONE or op.max() > AUG_SILENCE:
+    if op.min() < AUG_NONE or op.max() > AUG_PITCH:
         raise SrkError("augment: unknown op")
+    pitch = op == AUG_PITCH
+    if np.any(pitch & ~np.isin(ip, PITCH_LEVELS)):
+        raise SrkError("augment: pitch_shifting n_steps must be one of %s" % (PITCH_LEVELS,))
     blen = bank.numel()
     speed, shift = op == AUG_SPEED, op == AUG_SHIFT
     noisy = (op == AUG_NOISE) | (op == AUG_NOISE_SNR) | ((op == AUG_SILENCE) & (pos >= 0))
@@ -142,4 +146,41 @@ def augment(pcm_i16, bank_i16, op, iparam, noise_pos, dparam, seed, out=None):
     call("srk_augment", ptr(x), n, ptr(bank) if blen else None, blen, ctypes.c_void_p(base + 24 * n),
          ctypes.c_void_p(base), ctypes.c_void_p(base + 8 * n), ctypes.c_void_p(base + 16 * n),
          ctypes.c_uint64(int(seed) & ((1 << 64) - 1)), ptr(out), stream_ptr())
+    if pitch.any():   # K12 overwrites the clips K10 copied
+        idx = np.flatnonzero(pitch)
+        pitch_shift(x, idx, ip[idx], out=out)
+    return out
+
+
+def pitch_shift(pcm_i16, clip_idx, n_steps, out=None):
+    """K12 (srk_pitch_shift): dataset.py:225-235's np.int16(librosa.effects.pitch_shift(sample, 16000,
+    n_steps)) for the clips ``clip_idx`` of an int16 [B, 16000] batch, one launch.  n_steps[s] in
+    (-2, -1, 1, 2) for clip clip_idx[s].  Writes those rows of ``out`` (float32 [B, 16000] on the device,
+    allocated as a copy of the batch when None) and returns it."""
+    import numpy as np
+    require_gpu()
+    dev = torch.device("cuda")
+    x = torch.as_tensor(pcm_i16).to(dev, torch.int16).contiguous()
+    n = x.shape[0]
+    ci = np.asarray(clip_idx, dtype=np.int64).reshape(-1)
+    st = np.asarray(n_steps, dtype=np.int64).reshape(-1)
+    if x.shape != (n, SEQ_LENGTH) or ci.size != st.size:
+        raise SrkError("pitch_shift: inconsistent shapes")
+    if ci.size and (ci.min() < 0 or ci.max() >= n or len(np.unique(ci)) != ci.size):
+        raise SrkError("pitch_shift: clip indices out of range or repeated")
+    if not np.all(np.isin(st, PITCH_LEVELS)):
+        raise SrkError("pitch_shift: n_steps must be one of %s" % (PITCH_LEVELS,))
+    if out is None:
+        out = x.to(torch.float32)
+    if out.shape != (n, SEQ_LENGTH) or out.dtype != torch.float32 or not out.is_contiguous() or out.device.type != "cuda":
+        raise SrkError("pitch_shift: bad output tensor")
+    m = ci.size
+    if m == 0:
+        return out
+    lvl = np.searchsorted(np.asarray(PITCH_LEVELS), st)
+    d = torch.from_numpy(np.concatenate([ci, lvl]).astype(np.int32)).to(dev)
+    nbytes = int(lib().srk_pitch_workspace_bytes(m))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    call("srk_pitch_shift", ptr(x), n, ptr(d), ctypes.c_void_p(d.data_ptr() + 4 * m), m, ptr(out), ptr(ws), nbytes,
+         stream_ptr())
     return out

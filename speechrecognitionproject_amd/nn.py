@@ -71,7 +71,9 @@ class _GRULayerFn(torch.autograd.Function):
     pairs (weight_ih_lN, weight_ih_lN_reverse), ... of the parameters themselves."""
 
     @staticmethod
-    def forward(ctx, x, w_ih_f, w_ih_r, w_hh_f, w_hh_r, b_ih_f, b_ih_r, b_hh_f, b_hh_r):
+    def forward(ctx, x, grad_on, w_ih_f, w_ih_r, w_hh_f, w_hh_r, b_ih_f, b_ih_r, b_hh_f, b_hh_r):
+        # grad_on: torch.is_grad_enabled() at the call (inside forward it is always off, and
+        # needs_input_grad ignores it): an evaluation pass under no_grad must not register copies
         B, T, IN = x.shape
         H = w_hh_f.shape[-1]
         x = x.contiguous()
@@ -87,14 +89,14 @@ class _GRULayerFn(torch.autograd.Function):
              ptr(w_hh), ptr(b_ih), ptr(b_hh), ptr(y), ptr(ws), stream_ptr())
         ctx.x16 = x16
         off = int(_lib.lib().srk_gru_y16_offset(B, T, IN, H)) if _copy16_wanted(2 * H) else -1
-        if off >= 0 and any(ctx.needs_input_grad):
+        if off >= 0 and grad_on and any(ctx.needs_input_grad):
             _copy16_put(y, ws[off:].view(torch.int16)[:y.numel()])
         ctx.save_for_backward(x, w_ih, w_hh, y, ws)
         ctx.dims = (B, T, IN, H)
         ctx.params = (w_ih_f, w_ih_r, w_hh_f, w_hh_r, b_ih_f, b_ih_r, b_hh_f, b_hh_r)
         ctx.prec = _lib.matmul_precision()   # the backward runs at its forward's precision
         red = _reducer_of(w_ih_f)
-        if red is not None and any(ctx.needs_input_grad):
+        if red is not None and grad_on and any(ctx.needs_input_grad):
             red.persistent_pending(1)      # collectives wait until this layer's recurrence is enqueued
         return y
 
@@ -106,7 +108,7 @@ class _GRULayerFn(torch.autograd.Function):
         dy = dy.contiguous()
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         targets = [_grad_pair(P[2 * i], P[2 * i + 1]) for i in range(4)]
-        acc = all(t is not None for t in targets) and all(ctx.needs_input_grad[1:])
+        acc = all(t is not None for t in targets) and all(ctx.needs_input_grad[2:])
         if acc:   # accumulate straight into the parameters' .grad (FlatParams)
             dw_ih, dw_hh, db_ih, db_hh = targets
         else:
@@ -126,8 +128,8 @@ class _GRULayerFn(torch.autograd.Function):
             if acc:
                 red.mark_ready(P)
         if acc:
-            return (dx,) + (None,) * 8
-        return (dx, dw_ih[0], dw_ih[1], dw_hh[0], dw_hh[1], db_ih[0], db_ih[1], db_hh[0], db_hh[1])
+            return (dx, None) + (None,) * 8
+        return (dx, None, dw_ih[0], dw_ih[1], dw_hh[0], dw_hh[1], db_ih[0], db_ih[1], db_hh[0], db_hh[1])
 
 
 class BiGRU(tnn.Module):
@@ -161,7 +163,7 @@ class BiGRU(tnn.Module):
         h = x
         finals = []
         for layer in range(self.num_layers):
-            h = _GRULayerFn.apply(h, *self._pairs(layer))
+            h = _GRULayerFn.apply(h, torch.is_grad_enabled(), *self._pairs(layer))
             H = self.hidden_size
             finals += [h[:, -1, :H], h[:, 0, H:]]
         return h, torch.stack(finals)

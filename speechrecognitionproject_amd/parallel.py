@@ -19,32 +19,65 @@ def env_world():
 
 
 def nccl_env_for_graph_capture():
-    """Process-group settings for the (opt-in) HIP-graph-captured collectives, set before the group
-    exists.  ProcessGroupNCCL recycles its work events through a cache, so an event last recorded while a
-    step was being captured could be handed to a later eager collective, whose watchdog query would fail
-    on ROCm ("operation not permitted on an event last recorded in a capturing stream") and abort the
-    process.  TORCH_NCCL_CUDA_EVENT_CACHE=0 (an explicit setting is kept) gives every collective fresh
-    events; the abort still recurred in the 1-rank capture test, which is why the captured form is opt-in
-    (DESIGN.md §4)."""
+    """Process-group settings for HIP-graph-captured collectives, set before any group exists.
+    ProcessGroupNCCL recycles its work events through a per-device cache shared by all of its groups, so
+    an event last recorded while a step was being captured could be handed to a later eager collective
+    of another group, whose watchdog query would then fail on ROCm; TORCH_NCCL_CUDA_EVENT_CACHE=0 (an
+    explicit setting is kept) gives every collective fresh events.  The cause of the round-4 watchdog
+    abort was a different one (see ``capture_group``)."""
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 
 def init_from_env(backend=None):
-    """Initialise the default process group if WORLD_SIZE > 1; returns (rank, world, local_rank)."""
+    """Initialise the default process group if WORLD_SIZE > 1; returns (rank, world, local_rank).
+    Over RCCL the group is bound to this rank's GPU (``device_id``), which initialises its
+    communicator eagerly and lets ``capture_group`` split a second one off it before any capture."""
     world, rank, local = env_world()
-    nccl_env_for_graph_capture()
     if world > 1 and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {}
         if backend == "nccl":
+            nccl_env_for_graph_capture()
             torch.cuda.set_device(local)
+            kw["device_id"] = torch.device("cuda", local)
         # a long timeout: rank 0 alone runs the reference's per-epoch accuracy passes while the other
         # ranks wait at a barrier (training.py)
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
-                                timeout=datetime.timedelta(seconds=int(os.environ.get("SRK_DIST_TIMEOUT", "7200"))))
+                                timeout=datetime.timedelta(seconds=int(os.environ.get("SRK_DIST_TIMEOUT", "7200"))),
+                                **kw)
     elif torch.cuda.is_available():
         torch.cuda.set_device(local)
     return rank, world, local
+
+
+_CAPTURE_GROUP = None
+
+
+def capture_group():
+    """The process group used ONLY by collectives recorded into HIP graphs (a collective call: every
+    rank calls it, before any capture).
+
+    Why a group of its own (the round-4 watchdog abort): ProcessGroupNCCL hands every
+    EAGER collective's Work to its watchdog thread, which polls the Work's end event (recorded on the
+    group's internal stream) until it sees it complete — on its own interval, so a Work can stay listed
+    well after the device finished it.  A collective issued during a capture makes that same internal
+    stream wait on the capturing stream, i.e. joins it to the capture, and on ROCm ``hipEventQuery`` of
+    an event whose stream is now capturing fails with hipErrorCapturedEvent
+    (tests/test_dp_graph_gpu.py::test_hip_rule_event_on_stream_joined_to_capture).  The watchdog
+    rethrows that and aborts the process — whenever a capture started before it had reaped the warm-up
+    steps' eager all-reduces.  A group that never runs an eager collective has no listed Work whose
+    event could sit on its stream when a capture joins it (captured collectives are not handed to the
+    watchdog), so the race cannot occur.  Over RCCL the group is split off the default group's
+    communicator at creation (the default group is bound to a device, ``init_from_env``), so no
+    communicator setup is left for the first captured collective either."""
+    global _CAPTURE_GROUP
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    world_pg = dist.group.WORLD
+    if _CAPTURE_GROUP is None or _CAPTURE_GROUP[0] is not world_pg:   # (re)initialised default group
+        _CAPTURE_GROUP = (world_pg, dist.new_group(backend=dist.get_backend()))
+    return _CAPTURE_GROUP[1]
 
 
 def world_size():
@@ -88,15 +121,23 @@ class GradReducer:
     launched afterwards waits for that kernel on the compute stream).  ``finish()`` launches what
     is left in bucket order (identical on every rank) and makes the compute stream wait for all.
 
-    HIP graphs: the whole step — forward, backward with these bucketed collectives, ``finish()`` and
-    the optimizer — can be captured into one graph (bench.py at N > 1).  The host logic above runs once,
-    during the capture, so each collective is recorded at the point of the stream order where its bucket
-    became final: a graph node on the process group's stream, forked from the compute stream there and
-    joined back before the optimizer.  ``collectives_at_world1`` issues them even in a 1-rank group
-    (the GPU test of that capture on a one-GPU box)."""
+    Streams: every collective is issued under the stream that was current when ``begin()`` ran (the
+    compute stream of the step), also when ``_launch`` runs from a post-accumulate hook on autograd's
+    device thread, whose current stream is whatever autograd chose for that node.
 
-    def __init__(self, flat, bucket_mb=8.0, group=None, collectives_at_world1=False):
-        self.flat, self.group = flat, group
+    HIP graphs: the whole step — forward, backward with these bucketed collectives, ``finish()`` and
+    the optimizer — is captured into one graph (bench.py and training.py at N > 1 over RCCL).  The host
+    logic above runs once, during the capture, so each collective is recorded at the point of the stream
+    order where its bucket became final: a graph node on the process group's stream, forked from the
+    compute stream there and joined back before the optimizer.  A step that ``begin()`` finds capturing
+    issues its collectives on ``capture_group`` (pass ``parallel.capture_group()``, created eagerly on
+    every rank), eager steps on ``group``: no collective of the capture group is ever run eagerly, which
+    is what keeps the process group's watchdog away from events on a capturing stream (see
+    ``capture_group``).  ``collectives_at_world1`` issues them even in a 1-rank group (the GPU test of
+    that capture on a one-GPU box)."""
+
+    def __init__(self, flat, bucket_mb=8.0, group=None, collectives_at_world1=False, capture_group=None):
+        self.flat, self.group, self.capture_group = flat, group, capture_group
         self.min_world = 1 if collectives_at_world1 else 2
         cap = max(1, int(bucket_mb * (1 << 20) / 4))
         groups, cur, size = [], [], 0
@@ -124,13 +165,20 @@ class GradReducer:
         self.begin()
 
     def begin(self):
-        """Reset per-step state; call before the forward pass of each step."""
+        """Reset per-step state; call before the forward pass of each step (on the step's stream)."""
         self.remaining = [len(ps) for _, _, ps in self.buckets]
         self.launched = [False] * len(self.buckets)
         self.ready = set()
         self.works = []
         self.pending = 0
         self.held = []
+        self.stream, self.capturing = None, False
+        if self.flat.grad.is_cuda:
+            self.stream = torch.cuda.current_stream(self.flat.grad.device)
+            self.capturing = torch.cuda.is_current_stream_capturing()
+        if self.capturing and self.capture_group is None and self._active(self.group):
+            raise RuntimeError("GradReducer: a captured step needs capture_group=parallel.capture_group() "
+                               "(an eager group's collectives cannot be captured safely, DESIGN.md §4)")
 
     def persistent_pending(self, n=1):
         self.pending += n
@@ -162,22 +210,37 @@ class GradReducer:
                 else:
                     self._launch(i)
 
+    def _active(self, group):
+        return (dist.is_available() and dist.is_initialized()
+                and dist.get_world_size(group) >= self.min_world)
+
     def _launch(self, i):
         if self.launched[i]:
             return
         self.launched[i] = True
         lo, hi, _ = self.buckets[i]
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) >= self.min_world:
-            self.works.append(dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
-                                              async_op=True))
+        group = self.capture_group if self.capturing else self.group
+        if not self._active(group):
+            return
+        if self.stream is None:
+            work = dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=group, async_op=True)
+        else:
+            with torch.cuda.stream(self.stream):
+                work = dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=group, async_op=True)
+        self.works.append(work)
 
     def finish(self):
         """Launch every bucket not launched yet (in bucket order) and wait for all of them."""
         self.pending = 0
         for i in range(len(self.buckets)):
             self._launch(i)
-        for w in self.works:
-            w.wait()
+        if self.stream is None:
+            for w in self.works:
+                w.wait()
+        else:
+            with torch.cuda.stream(self.stream):
+                for w in self.works:
+                    w.wait()
         self.works = []
 
     def remove(self):

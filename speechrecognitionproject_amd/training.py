@@ -64,9 +64,10 @@ def parse(argv=None):
     p.add_argument('--no-graph', dest='graph', action='store_false',
                    help='run every step eagerly instead of replaying a HIP graph of the step for full-size '
                         'batches (speechrecognitionproject_amd/graphs.py; single process)')
-    p.add_argument('--dp-graph', action='store_true',
-                   help='data-parallel over RCCL: replay HIP graphs of the whole step with the all-reduces '
-                        'captured in them (opt-in, DESIGN.md §4)')
+    p.add_argument('--no-dp-graph', dest='dp_graph', action='store_false',
+                   help='data-parallel over RCCL: run every step eagerly instead of replaying HIP graphs of the '
+                        'whole step with the bucketed all-reduces captured in them (DESIGN.md §4)')
+    p.add_argument('--dp-graph', dest='dp_graph', action='store_true', help=argparse.SUPPRESS)
     p.add_argument('--loader', choices=('device', 'torch'), default='device',
                    help='WAV datasets: device = native batched decode + K10 on-device augmentation '
                         '(DeviceBatchLoader); torch = per-item Dataset.__getitem__ through DataLoader')
@@ -84,10 +85,11 @@ def parse(argv=None):
 
 def main(argv=None):
     args = parse(argv)
+    saved = _lib.matmul_precision()
     try:
         _train(args)
     finally:
-        _lib.set_matmul_precision('fp32')     # process-wide: do not leak a 16-bit mode into the caller
+        _lib.set_matmul_precision(saved)      # process-wide: give the caller back its own mode
 
 
 def _train(args):
@@ -122,7 +124,11 @@ def _train(args):
     optimizer = Adam(model.parameters(), lr=lr, flat=flat)
     optimizer.grad_scale = 1.0 / world
     parallel.broadcast_flat(flat)
-    reducer = parallel.GradReducer(flat) if (world > 1 and args.overlap) else None
+    # data-parallel steps are captured whole (the bucketed collectives included, on the capture-only
+    # process group) over RCCL; gloo cannot be captured, and --no-dp-graph runs them eagerly
+    use_graph = args.graph and (world == 1 or (args.dp_graph and torch.distributed.get_backend() == 'nccl'))
+    reducer = (parallel.GradReducer(flat, capture_group=parallel.capture_group() if use_graph else None)
+               if (world > 1 and args.overlap) else None)
     scheduler = torch.optim.lr_scheduler.ExponentialLR(optimizer, 0.87)
     criterion = CrossEntropyLoss()
     scaler = None
@@ -134,10 +140,6 @@ def _train(args):
     os.makedirs(args.output_path, exist_ok=True)
     loss_file = os.path.join(args.output_path, 'loss_' + key + '.txt')
 
-    # data-parallel steps are captured whole (collectives included) only with --dp-graph, over RCCL (gloo
-    # cannot be captured): the process group's watchdog thread aborted the 1-rank capture test now and
-    # then, so the default DP step runs eagerly
-    use_graph = args.graph and (world == 1 or (args.dp_graph and torch.distributed.get_backend() == 'nccl'))
     graphed = None          # GraphedStep of a full-batch step (captured after two eager full steps)
     static = {}
     full_eager = 0

@@ -1,8 +1,8 @@
 """Worker of tests/test_dp_graph_gpu.py (run as a subprocess: it owns a 1-rank RCCL process group).
 
-bench.py at N > 1 captures the whole DP step into a HIP graph: forward, backward with the bucketed
-all-reduces of parallel.GradReducer forked where each bucket's gradients are final, the join, and Adam
-(DESIGN.md §4).  On a one-GPU box the closest check is a 1-rank "nccl" (RCCL) group with the reducer
+bench.py and training.py at N > 1 capture the whole DP step into a HIP graph: forward, backward with
+the bucketed all-reduces of parallel.GradReducer forked where each bucket's gradients are final (on the
+capture-only process group, parallel.capture_group), the join, and Adam.  On a one-GPU box the closest check is a 1-rank "nccl" (RCCL) group with the reducer
 told to issue its collectives anyway: the captured step must then replay the eager step bit for bit
 (a 1-rank SUM is the identity), buckets must be forked during the backward (not all at finish()),
 and a captured collective must actually run on replay (a 1-rank all-gather copies a fresh input).
@@ -29,13 +29,15 @@ def main():
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
     torch.cuda.set_device(0)
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from speechrecognitionproject_amd.parallel import nccl_env_for_graph_capture
-    nccl_env_for_graph_capture()   # as bench.py / training.py (parallel.init_from_env)
+    from speechrecognitionproject_amd import parallel
+    # parallel.init_from_env leaves a 1-rank world alone: its RCCL settings by hand (device-bound group)
+    parallel.nccl_env_for_graph_capture()
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    cap_group = parallel.capture_group()
     import importlib
 
     from oracle import models as OM
-    from speechrecognitionproject_amd import _lib, parallel
+    from speechrecognitionproject_amd import _lib
     from speechrecognitionproject_amd import nn as snn
     from speechrecognitionproject_amd.graphs import GraphedStep
     from speechrecognitionproject_amd.optim import Adam, FlatParams
@@ -53,8 +55,18 @@ def main():
         net.train()
         flat = FlatParams(net.parameters())
         opt = Adam(net.parameters(), lr=1e-4, flat=flat)
-        red = parallel.GradReducer(flat, bucket_mb=0.5, collectives_at_world1=True)
+        red = parallel.GradReducer(flat, bucket_mb=0.5, collectives_at_world1=True, capture_group=cap_group)
         crit = snn.CrossEntropyLoss()
+        # which stream the bucket launches see on their own thread (post-accumulate hooks run on
+        # autograd's device thread): GradReducer issues them under the stream begin() saw either way
+        hook_view = []
+        orig_launch = red._launch
+
+        def launch(i, orig=orig_launch):
+            if red.capturing:
+                hook_view.append(bool(torch.cuda.is_current_stream_capturing()))
+            orig(i)
+        red._launch = launch
         x, y = synthetic_clips(3 * B, seed=23)
         pcm, lab = torch.from_numpy(x).cuda().view(3, B, -1), torch.from_numpy(y).cuda().view(3, B)
         sx, sy = pcm[0].clone(), lab[0].clone()
@@ -75,6 +87,7 @@ def main():
             g = GraphedStep(body, warmup=2, capture_error_mode="thread_local")
             out["buckets"] = len(red.buckets)
             out["forked_during_backward"] = launched[-1]
+            out["launch_thread_stream_capturing"] = hook_view
             for i in range(K):
                 sx.copy_(pcm[(i + 1) % 3])
                 sy.copy_(lab[(i + 1) % 3])
@@ -96,14 +109,16 @@ def main():
     out["params_equal"] = bool(torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1))
     out["spin_timeouts"] = _lib.spin_timeouts()
 
-    # a captured collective runs on every replay: a 1-rank all-gather copies its input to its output
+    # a captured collective runs on every replay: a 1-rank all-gather copies its input to its output.
+    # An eager collective of the default group right before the capture (its Work still listed by the
+    # watchdog) is the round-4 abort's precondition; the capture group keeps the two apart.
     src = torch.arange(1024, device="cuda", dtype=torch.float32)
     dst = torch.zeros(1024, device="cuda")
-    dist.all_gather_into_tensor(dst, src)           # eager once
+    dist.all_gather_into_tensor(dst, src)           # eager, default group
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, capture_error_mode="thread_local"):
-        dist.all_gather_into_tensor(dst, src)
+        dist.all_gather_into_tensor(dst, src, group=cap_group)
     ok = []
     for r in range(3):
         src.fill_(r + 1.0)
@@ -112,6 +127,22 @@ def main():
         torch.cuda.synchronize()
         ok.append(bool(torch.all(dst == r + 1.0).item()))
     out["captured_collective_replays"] = ok
+
+    # the abort's precondition, repeated: an eager collective of the default group (its Work listed by
+    # the watchdog for up to its polling interval) immediately followed by a capture with a collective
+    buf = torch.ones(1 << 16, device="cuda")
+    sums = []
+    for r in range(8):
+        dist.all_reduce(buf)                         # eager, default group
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            dist.all_reduce(buf, group=cap_group)
+            buf.add_(1.0)
+        g.replay()
+        torch.cuda.synchronize()
+        sums.append(float(buf[0].item()))
+    out["eager_then_capture"] = sums                 # 1-rank SUM is the identity: 2, 3, ..., 9
     dist.destroy_process_group()
     print(json.dumps(out), flush=True)
 

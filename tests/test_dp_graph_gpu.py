@@ -1,9 +1,11 @@
-"""The DP step captured whole into a HIP graph (bench.py at N > 1): forward, backward
-with parallel.GradReducer's bucketed RCCL all-reduces forked where each bucket is final, the join and
-Adam.  Checked on a 1-rank RCCL group in a subprocess (tests/dp_graph_worker.py): graph replays ==
-eager steps bit for bit, more than one bucket forked during the backward (not all at finish()), and a
-captured collective really runs on each replay.  The N > 1 arithmetic of the same reducer is covered
-over gloo on the CPU (tests/test_parallel.py)."""
+"""The DP step captured whole into a HIP graph (bench.py and training.py at N > 1):
+forward, backward with parallel.GradReducer's bucketed RCCL all-reduces forked where each bucket is
+final (on the capture-only process group, parallel.capture_group), the join and Adam.  Checked on a
+1-rank RCCL group in a subprocess (tests/dp_graph_worker.py): graph replays == eager steps bit for bit,
+more than one bucket forked during the backward (not all at finish()), a captured collective really
+runs on each replay, and eager collectives of the default group right before a capture (the round-4
+watchdog abort's precondition) do not disturb it.  The N > 1 arithmetic of the same reducer is
+covered over gloo on the CPU (tests/test_parallel.py)."""
 import json
 import os
 import subprocess
@@ -16,18 +18,32 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-# The captured-collective path is opt-in (bench.py --allreduce-in-graph, training.py --dp-graph): in 2 of 7
-# runs the worker died in ProcessGroupNCCL's watchdog thread ("operation not permitted on an event last
-# recorded in a capturing stream"), so the default GPU suite leaves it out; SRK_TEST_DP_CAPTURE=1 runs it.
-@pytest.mark.skipif(os.environ.get("SRK_TEST_DP_CAPTURE") != "1",
-                    reason="opt-in captured all-reduce path; its watchdog abort is intermittent (DESIGN.md §4)")
-@pytest.mark.parametrize("name,B,precision", [("mfcc_bgru", 64, "fp32"), ("mfcc_bgru", 64, "bf16")])
-def test_dp_step_graph_with_captured_allreduce(gpu, name, B, precision):
+def _env():
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
+    return env
+
+
+def test_hip_rule_event_on_stream_joined_to_capture(gpu):
+    """The HIP rule behind the round-4 abort, in isolation: an event recorded eagerly (long complete) on
+    a stream that a capture has since joined cannot be queried; the same event can be while a capture
+    that its stream did not join runs, and again after the capture ends."""
+    r = subprocess.run([sys.executable, os.path.join(HERE, "hip_event_rule_worker.py")], env=_env(),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["eager_before"] == {"done": True}, out
+    assert out["capture_not_joined"] == {"done": True}, out
+    assert "capturing stream" in out["S_joined"].get("error", ""), out
+    assert out["after_capture"] == {"done": True}, out
+    assert out["x_after_replay"] == 2.0, out
+
+
+@pytest.mark.parametrize("name,B,precision", [("mfcc_bgru", 64, "fp32"), ("mfcc_bgru", 64, "bf16")])
+def test_dp_step_graph_with_captured_allreduce(gpu, name, B, precision):
     r = subprocess.run([sys.executable, os.path.join(HERE, "dp_graph_worker.py"), name, str(B), precision],
-                       env=env, capture_output=True, text=True, timeout=180)
+                       env=_env(), capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["buckets"] > 2, out
@@ -35,3 +51,4 @@ def test_dp_step_graph_with_captured_allreduce(gpu, name, B, precision):
     assert out["losses_equal"] and out["params_equal"], out
     assert out["spin_timeouts"] == 0, out
     assert out["captured_collective_replays"] == [True, True, True], out
+    assert out["eager_then_capture"] == [float(v) for v in range(2, 10)], out

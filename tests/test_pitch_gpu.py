@@ -1,0 +1,117 @@
+"""K12 srk_pitch_shift (dataset.py:225-235) on the GPU vs the CPU restatement oracle/pitch.py.
+
+Parity is unpinned (librosa / resampy absent; tests/test_pitch.py pins the oracle by known answers).
+Device vs oracle: the same float64 / float32 operations in the same order, except the FFT algorithm
+(radix-2 here, pocketfft in numpy) and the constant tables (glibc vs numpy / scipy transcendentals),
+both at the 1e-16 level — a stored complex64 value or an int16 truncation flips only when a value
+sits that close to a rounding boundary.  Bound (PITCH_EXACT_FRAC, PITCH_MAX_LSB): at least 99.9 % of
+the output samples bit-identical, none more than 2 int16 steps away; plus the known answers on the
+device and the batch / augmentation plumbing."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import pitch as P
+from speechrecognitionproject_amd import features as K
+from speechrecognitionproject_amd.synthetic import synthetic_clips
+
+pytestmark = pytest.mark.gpu
+
+PITCH_EXACT_FRAC = 0.999
+PITCH_MAX_LSB = 2
+SR = 16000
+
+
+def _clips():
+    x, _ = synthetic_clips(10, seed=71)            # the SURVEY §8d mix: noise, loud noise, tones, zeros, half-zero
+    t = np.arange(SR) / SR
+    tones = np.stack([np.int16(9000 * np.sin(2 * np.pi * f * t)) for f in (440.0, 1000.0)])
+    return np.concatenate([x.astype(np.int16), tones])
+
+
+def test_pitch_shift_matches_oracle(gpu):
+    pcm = _clips()
+    n = pcm.shape[0]
+    levels = np.array([(-2, -1, 1, 2)[i % 4] for i in range(n)])
+    out = K.pitch_shift(torch.from_numpy(pcm).cuda(), np.arange(n), levels).cpu().numpy()
+    exact, worst = 0, 0
+    for b in range(n):
+        want = P.pitch_shifting(pcm[b], int(levels[b])).astype(np.float32)
+        d = np.abs(out[b] - want)
+        exact += int((d == 0).sum())
+        worst = max(worst, float(d.max()))
+    frac = exact / (n * SR)
+    assert frac >= PITCH_EXACT_FRAC and worst <= PITCH_MAX_LSB, (frac, worst)
+    assert np.array_equal(out, np.trunc(out))
+
+
+def test_pitch_shift_tone_known_answer(gpu):
+    t = np.arange(SR) / SR
+    x = np.int16(8000 * np.sin(2 * np.pi * 1000.0 * t))
+    pcm = torch.from_numpy(np.stack([x] * 4)).cuda()
+    out = K.pitch_shift(pcm, [0, 1, 2, 3], [-2, -1, 1, 2]).cpu().numpy()
+    for b, n in enumerate((-2, -1, 1, 2)):
+        seg = out[b, 2000:14000].astype(np.float64) * np.hanning(12000)
+        f = np.argmax(np.abs(np.fft.rfft(seg, 48000))) * SR / 48000
+        assert abs(f - 1000.0 * 2 ** (n / 12)) <= 1.5, (n, f)
+
+
+def test_pitch_shift_subset_and_rows_untouched(gpu):
+    pcm = _clips()
+    dev = torch.from_numpy(pcm).cuda()
+    out = dev.to(torch.float32)
+    before = out.clone()
+    K.pitch_shift(dev, [3, 7], [2, -1], out=out)
+    keep = [b for b in range(pcm.shape[0]) if b not in (3, 7)]
+    assert torch.equal(out[keep], before[keep])
+    assert not torch.equal(out[3], before[3]) and not torch.equal(out[7], before[7])
+    with pytest.raises(K.SrkError):
+        K.pitch_shift(dev, [0], [3])
+    with pytest.raises(K.SrkError):
+        K.pitch_shift(dev, [0, 0], [1, 1])
+
+
+def test_augment_pitch_op_is_k10_then_k12(gpu):
+    """augment() with AUG_PITCH rows: those rows == pitch_shift's, every other row == the K10 result."""
+    pcm = _clips()
+    n = pcm.shape[0]
+    bank = np.clip(np.random.default_rng(1).normal(0, 2000, 40000), -6000, 6000).astype(np.int16)
+    op = np.zeros(n, np.int64)
+    ip = np.zeros(n, np.int64)
+    pos = np.full(n, -1, np.int64)
+    dp = np.zeros(n, np.float64)
+    op[[1, 4, 9]] = K.AUG_PITCH
+    ip[[1, 4, 9]] = [1, -2, 2]
+    op[2], ip[2] = K.AUG_SHIFT, 1234
+    op[5], pos[5], dp[5] = K.AUG_NOISE, 100, 0.05
+    out = K.augment(pcm, bank, op, ip, pos, dp, seed=9).cpu()
+    op0 = op.copy()
+    op0[op0 == K.AUG_PITCH] = K.AUG_NONE
+    base = K.augment(pcm, bank, op0, np.where(op == K.AUG_PITCH, 0, ip), pos, dp, seed=9).cpu()
+    ps = K.pitch_shift(torch.from_numpy(pcm).cuda(), [1, 4, 9], [1, -2, 2]).cpu()
+    others = [b for b in range(n) if b not in (1, 4, 9)]
+    assert torch.equal(out[others], base[others])
+    assert torch.equal(out[[1, 4, 9]], ps[[1, 4, 9]])
+
+
+def test_dataset_pitch_shifting_item(gpu):
+    """Dataset.pitch_shifting (the per-item path) draws its level with random.randint like
+    dataset.py:230-231 and shifts the clip on the device (one-clip K12 launch)."""
+    from speechrecognitionproject_amd.dataset import Dataset
+    pcm = _clips()[6]
+    ds = Dataset.__new__(Dataset)
+    seen = set()
+    for seed in range(12):
+        random.seed(seed)
+        level = [-2, -1, 1, 2, None][random.randint(0, 4)]
+        random.seed(seed)
+        y = ds.pitch_shifting(pcm)
+        seen.add(level)
+        if level is None:
+            assert y is pcm
+            continue
+        want = P.pitch_shifting(pcm, level)
+        assert y.dtype == np.int16 and np.abs(y.astype(np.int32) - want).max() <= PITCH_MAX_LSB
+    assert None in seen and len(seen) >= 3

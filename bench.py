@@ -112,7 +112,8 @@ LP_KERNELS = ("gemm_bf16", "gemm_f16", "gru_fwd_seq_lp", "gru_bwd_seq_lp", "conv
               "conv_wgrad_lp")
 OTHER_KERNELS = ("mfcc", "fbank", "spec", "noise_mix", "adam", "grad_check", "batchnorm_fwd", "batchnorm_bwd", "conv1_pool_fwd",
                  "conv1_pool_wgrad",
-                 "maxpool_fwd", "maxpool_bwd", "conv_to16", "conv_unpool16", "gru_dwhh_reduce")
+                 "maxpool_fwd", "maxpool_bwd", "conv_to16", "conv_unpool16", "gru_dwhh_reduce", "conv_colsum",
+                 "conv_to16_colsum", "conv_unpool16_colsum", "pitch_shift")
 
 
 def log(*a):
@@ -519,9 +520,11 @@ class Workload:
 
 
 def _workload_h2d(self, precision, steps, warmup):
-    """The graphed step fed from pinned host memory: 2 device batch slots (graphs 0 / 1 read pcm[0] /
-    pcm[1]), host batches uploaded on a copy stream one step ahead.  Returns utt/s over the wall time
-    of `steps` steps (uploads included) and the upload rate; plus the bare upload rate (copies only)."""
+    """The graphed step fed from pinned host memory: 2 device batch slots (graphs 0 / 1 read slot 0 /
+    slot 1), host batches uploaded on a copy stream one step ahead.  The upload is the clips' int16 PCM
+    (the WAV samples, 32 KB per clip; the feature kernel widens them in its load stage: the same values
+    as the float32 items of Dataset).  Returns utt/s over the wall time of `steps` steps (uploads
+    included) and the upload rate; plus the bare upload rate (copies only)."""
     assert self.name != "spec_bgru" and self.args.pool >= 2
     from speechrecognitionproject_amd.graphs import GraphedStep
     _lib.set_matmul_precision(precision)
@@ -529,7 +532,8 @@ def _workload_h2d(self, precision, steps, warmup):
     self.opt.grad_scale = 1.0 / self.world
     n_host = 8
     x, _ = synthetic_clips(n_host * self.B, seed=4000 + self.rank)
-    host = torch.from_numpy(x).view(n_host, self.B, -1).pin_memory()
+    host = torch.from_numpy(x.astype(np.int16)).view(n_host, self.B, -1).pin_memory()
+    staged, self.pcm = self.pcm, torch.empty((2, self.B, 16000), dtype=torch.int16, device=self.dev)
     # N > 1: the exchange as the main run settled it (in the graph, or eager after each replay)
     self.exchange_in_graph = self.world > 1 and getattr(self, "graph_allreduce", "") == "in graph"
     self.reducer = (parallel.GradReducer(self.flat, bucket_mb=self.args.bucket_mb, capture_group=parallel.capture_group())
@@ -585,8 +589,9 @@ def _workload_h2d(self, precision, steps, warmup):
         self.reducer.remove()
         self.reducer = None
     self.exchange_in_graph = False
+    self.pcm = staged
     torch.cuda.empty_cache()
-    step_bytes = self.B * 16000 * 4
+    step_bytes = self.B * 16000 * 2
     return {"value": round(self.B * steps / el, 2), "unit": "utt/s", "ms_per_step": round(el / steps * 1e3, 3),
             "upload_bytes_per_step": step_bytes, "needed_gbs": round(step_bytes / (el / steps) / 1e9, 2),
             "upload_only_gbs": round(step_bytes * steps / el_copy / 1e9, 2), "steps": steps}
@@ -694,8 +699,9 @@ def main():
         # SURVEY.md §8d's second figure: the same step fed from pinned host PCM (the reference's
         # DataLoader -> .to(DEVICE) crossing, training.py:77,86), the upload double-buffered
         h2d_rec = {"what": "cfg2 train step (HIP-graph replays) with each batch uploaded from pinned host memory "
-                           "(float32 PCM, what Dataset yields) on a copy stream, double-buffered: batch i+1 uploads "
-                           "while step i runs; value = clips / wall time including every upload"}
+                           "(int16 PCM, the WAV samples: K1 widens them to the float32 values Dataset yields) on a "
+                           "copy stream, double-buffered: batch i+1 uploads while step i runs; value = clips / wall "
+                           "time including every upload"}
         for prec in ("fp32", "bf16"):
             h2d_rec[prec] = wl.run_h2d(prec, args.steps, args.warmup)
         _lib.set_matmul_precision(args.precision)

@@ -105,6 +105,13 @@ int srk_mfcc_fwd(const float* pcm, int64_t n_clips, float* out, int layout, void
  * transposed 1: out [n_clips, 49, 321] (time x freq, models/model_spec_cnn.py:14).     */
 int srk_spec_fwd(const float* pcm, int64_t n_clips, float* out, int transposed, void* stream);
 
+/* K1 / K2 / K3 on int16 PCM [n_clips, 16000] (4-byte aligned): the samples the WAV holds, widened to
+ * float32 in the kernels' load stage — the same values as the float32 entry points above (the
+ * reference's float32 PCM is int16-valued, dataset.py:117), at half the bytes to upload and read. */
+int srk_fbank_fwd_i16(const int16_t* pcm, int64_t n_clips, float* out, void* stream);
+int srk_mfcc_fwd_i16(const int16_t* pcm, int64_t n_clips, float* out, int layout, void* stream);
+int srk_spec_fwd_i16(const int16_t* pcm, int64_t n_clips, float* out, int transposed, void* stream);
+
 /* K4: uniform noise mix, dataset.py:183-193 (`add_noise_uniform`) with the random draws made
  * explicit: out[b, i] = (float) int16_trunc( (double)pcm[b, i] + gain[b] * (double)
  *                        bank[file_idx[b] * bank_len + offset[b] + i] ).

@@ -30,7 +30,7 @@ import numpy as np
 
 SEQ_LENGTH = 16000
 
-OP_NONE, OP_SPEED, OP_SHIFT, OP_NOISE, OP_NOISE_SNR, OP_SILENCE = 0, 1, 2, 3, 4, 5
+OP_NONE, OP_SPEED, OP_SHIFT, OP_NOISE, OP_NOISE_SNR, OP_SILENCE, OP_PITCH = 0, 1, 2, 3, 4, 5, 6
 
 _M64 = (1 << 64) - 1
 
@@ -142,6 +142,9 @@ def augment_batch(pcm, bank, op, iparam, noise_pos, dparam, seed):
             y = np.int16(x + np.sqrt((sp / npow) / float(dparam[b])) * seg)
         elif o == OP_SILENCE:
             y = generate_silence_sample(seg, float(dparam[b]))
+        elif o == OP_PITCH:   # iparam = n_steps (oracle/pitch.py, parity unpinned)
+            from oracle import pitch
+            y = pitch.pitch_shifting(x, int(iparam[b]))
         else:
             raise ValueError("bad op %d" % o)
         out[b] = np.asarray(y).astype(np.float32)

@@ -127,43 +127,56 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
   }
 }
 
-// Combine the chunk partials of channel c in chunk order (Chan).  The partials of kPre chunks are
-// loaded before any is combined: the serial combine is the same, but it no longer waits out one
-// load latency per chunk (at 256 chunks that wait was ~90 us per BatchNorm layer).
+// The reduction kernels below load the partials of kPre chunks before any is combined (an in-order sum
+// that no longer waits out one load latency per chunk).
 constexpr int kPre = 32;
-__device__ __forceinline__ void combine_chunks(const float* __restrict__ pmean, const float* __restrict__ pm2,
-                                               const BnGeom& g, int c, float& n, float& mu, float& m2) {
+
+// Combine the chunk partials of channel c (Chan's pairwise formula) as a fixed pairwise tree, one wave
+// per channel: lane l combines chunks 4l .. 4l+3 in order (kMaxChunks = 256 = 4 x 64), then the lanes pair up at distance 1, 2, .. 32 (lane l takes lane
+// l + d when l % 2d == 0).  Deterministic (the tree does not depend on timing) and shallower: 3 + 6
+// dependent Chan steps instead of 256 — the serial chain's dependent divides were ~54 us per BatchNorm
+// layer (r04k cfg4 bf16).  The result sits in lane 0.
+static_assert(kMaxChunks == 4 * 64, "combine_chunks_tree: four chunks per lane");
+__device__ __forceinline__ void combine_chunks_tree(const float* __restrict__ pmean, const float* __restrict__ pm2,
+                                                    const BnGeom& g, int c, float& n, float& mu, float& m2) {
+  const int lane = threadIdx.x & 63;
   n = 0.f;
   mu = 0.f;
   m2 = 0.f;
-  for (int k0 = 0; k0 < g.chunks; k0 += kPre) {
-    float vm[kPre], v2[kPre];
+  float vm[4], v2[4];
 #pragma unroll
-    for (int u = 0; u < kPre; ++u) {
-      const int64_t k = k0 + u < g.chunks ? k0 + u : g.chunks - 1;
-      vm[u] = pmean[k * g.C + c];
-      v2[u] = pm2[k * g.C + c];
-    }
+  for (int u = 0; u < 4; ++u) {
+    const int k = 4 * lane + u < g.chunks ? 4 * lane + u : g.chunks - 1;
+    vm[u] = pmean[(int64_t)k * g.C + c];
+    v2[u] = pm2[(int64_t)k * g.C + c];
+  }
 #pragma unroll
-    for (int u = 0; u < kPre; ++u) {
-      if (k0 + u < g.chunks) {
-        const int64_t r0 = (int64_t)(k0 + u) * g.rows_per_chunk;
-        const float nb = (float)((r0 + g.rows_per_chunk < g.M ? g.rows_per_chunk : g.M - r0));
-        chan(n, mu, m2, nb, vm[u], v2[u]);
-      }
+  for (int u = 0; u < 4; ++u) {
+    const int k = 4 * lane + u;
+    if (k < g.chunks) {
+      const int64_t r0 = (int64_t)k * g.rows_per_chunk;
+      chan(n, mu, m2, (float)(r0 + g.rows_per_chunk < g.M ? g.rows_per_chunk : g.M - r0), vm[u], v2[u]);
     }
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const float nb = __shfl_down(n, d, 64), mb = __shfl_down(mu, d, 64), m2b = __shfl_down(m2, d, 64);
+    if ((lane & (2 * d - 1)) == 0) chan(n, mu, m2, nb, mb, m2b);
   }
 }
 
 // Biased variance for the normalisation, unbiased for the running estimate (nn.BatchNorm1d,
-// momentum update).
-__global__ void bn_finalize_kernel(const float* __restrict__ pmean, const float* __restrict__ pm2, BnGeom g,
-                                   float eps, float momentum, float* __restrict__ mean, float* __restrict__ invstd,
-                                   float* __restrict__ running_mean, float* __restrict__ running_var) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+// momentum update).  Block = 4 waves = 4 channels (combine_chunks_tree).
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ pmean,
+                                                          const float* __restrict__ pm2, BnGeom g, float eps,
+                                                          float momentum, float* __restrict__ mean,
+                                                          float* __restrict__ invstd, float* __restrict__ running_mean,
+                                                          float* __restrict__ running_var) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= g.C) return;
   float n, mu, m2;
-  combine_chunks(pmean, pm2, g, c, n, mu, m2);
+  combine_chunks_tree(pmean, pm2, g, c, n, mu, m2);
+  if ((threadIdx.x & 63) != 0) return;
   const float var = m2 / (float)g.M;
   mean[c] = mu;
   invstd[c] = 1.0f / sqrtf(var + eps);
@@ -321,12 +334,14 @@ __global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restric
 // ---- SyncBatchNorm pieces (torch.nn.SyncBatchNorm over data-parallel ranks).  One rank's (count,
 // mean, M2) per channel from the chunk partials; the ranks' triples are gathered by the caller and
 // combined in rank order (Chan, fixed order: every rank computes identical statistics).
-__global__ void bn_local_stats_kernel(const float* __restrict__ pmean, const float* __restrict__ pm2, BnGeom g,
-                                      float* __restrict__ stats) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void bn_local_stats_kernel(const float* __restrict__ pmean,
+                                                             const float* __restrict__ pm2, BnGeom g,
+                                                             float* __restrict__ stats) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);   // one wave per channel (combine_chunks_tree)
   if (c >= g.C) return;
   float n, mu, m2;
-  combine_chunks(pmean, pm2, g, c, n, mu, m2);
+  combine_chunks_tree(pmean, pm2, g, c, n, mu, m2);
+  if ((threadIdx.x & 63) != 0) return;
   stats[c] = n;
   stats[g.C + c] = mu;
   stats[2 * g.C + c] = m2;
@@ -448,7 +463,7 @@ int srk_batchnorm_fwd16(const float* x, int64_t M, int64_t C, const float* gamma
     if (int rc = srk::bn_scratch((size_t)2 * g.chunks * C, &part)) return rc;
     hipLaunchKernelGGL(srk::bn_stats_kernel, dim3((unsigned)((g.C4 + g.CQ - 1) / g.CQ), (unsigned)g.chunks), dim3(256),
                        0, s, x, g, part, part + (size_t)g.chunks * C);
-    hipLaunchKernelGGL(srk::bn_finalize_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
+    hipLaunchKernelGGL(srk::bn_finalize_kernel, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, s, part,
                        part + (size_t)g.chunks * C, g, eps, momentum, save_mean, save_invstd, running_mean,
                        running_var);
   } else {
@@ -509,7 +524,7 @@ int srk_batchnorm_stats(const float* x, int64_t M, int64_t C, float* stats, void
   if (int rc = srk::bn_scratch((size_t)2 * g.chunks * C, &part)) return rc;
   hipLaunchKernelGGL(srk::bn_stats_kernel, dim3((unsigned)((g.C4 + g.CQ - 1) / g.CQ), (unsigned)g.chunks), dim3(256), 0,
                      s, x, g, part, part + (size_t)g.chunks * C);
-  hipLaunchKernelGGL(srk::bn_local_stats_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
+  hipLaunchKernelGGL(srk::bn_local_stats_kernel, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, s, part,
                      part + (size_t)g.chunks * C, g, stats);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;

@@ -738,6 +738,83 @@ __global__ void to16_kernel(const float* __restrict__ x, int64_t n8, unsigned sh
   *reinterpret_cast<u32x4_*>(y + 8 * i) = u32x4_{lo.x, lo.y, hi.x, hi.y};
 }
 
+// Column sums of a [rows, C] fp32 matrix (C % 8 == 0, 256 % (C / 8) == 0) fused into the one pass that
+// already reads it — the conv bias gradient db = sum over pixels of dY (model_fbanks_cnn.py's conv
+// biases) in 16-bit modes, where the weight-gradient GEMM reads only dY's 16-bit copy.  Thread = (row
+// lane, 8-channel octet): 16-B loads, four rows' loads issued before their adds, each thread adding its
+// rows in row order; the row lanes of an octet are then added through LDS in lane order and one partial
+// row [C] per block goes to `part`; colsum_blocks_kernel adds the blocks in block order (deterministic).
+// KIND 0: the sums only; 1: + the 16-bit operand copy y16 = round(x) (to16_kernel's conversion);
+// 2: x is a (1, kw)-pooled gradient: + its unpooled dense 16-bit copy through the argmax (unpool16_kernel's
+// stores; each pooled value sits once in the dense gradient, so its column sums are the bias gradient).
+template <int LP, int KIND>
+__global__ __launch_bounds__(256) void colsum8_kernel(const float* __restrict__ x, const uint8_t* __restrict__ arg,
+                                                      int64_t rows, int C, int kw, int64_t rows_per_block,
+                                                      unsigned short* __restrict__ y16, float* __restrict__ part) {
+  __shared__ float red[256 * 8];
+  const int C8 = C >> 3, RL = 256 / C8;
+  const int q = threadIdx.x % C8, rl = threadIdx.x / C8;
+  const int c = q * 8;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+  using E4 = typename ConvLp<LP == 0 ? 1 : LP>::e4;
+  typedef unsigned u32x2a __attribute__((ext_vector_type(2)));
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto body = [&](int64_t r, const v4f& g0, const v4f& g1) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc[e] += g0[e];
+      acc[4 + e] += g1[e];
+    }
+    if (KIND == 1) {
+      const u32x2_ lo = __builtin_bit_cast(u32x2_, __builtin_convertvector(g0, E4));
+      const u32x2_ hi = __builtin_bit_cast(u32x2_, __builtin_convertvector(g1, E4));
+      *reinterpret_cast<u32x4_*>(y16 + r * C + c) = u32x4_{lo.x, lo.y, hi.x, hi.y};
+    } else if (KIND == 2) {
+      const u32x2a a = *reinterpret_cast<const u32x2a*>(arg + r * C + c);
+      for (int b = 0; b < kw; ++b) {
+        v4f o0, o1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o0[e] = ((a.x >> (8 * e)) & 0xFFu) == (unsigned)b ? g0[e] : 0.f;
+          o1[e] = ((a.y >> (8 * e)) & 0xFFu) == (unsigned)b ? g1[e] : 0.f;
+        }
+        const u32x2_ lo = __builtin_bit_cast(u32x2_, __builtin_convertvector(o0, E4));
+        const u32x2_ hi = __builtin_bit_cast(u32x2_, __builtin_convertvector(o1, E4));
+        *reinterpret_cast<u32x4_*>(y16 + (r * kw + b) * C + c) = u32x4_{lo.x, lo.y, hi.x, hi.y};
+      }
+    }
+  };
+  int64_t r = r0 + rl;
+  for (; r + 3 * RL < r1; r += 4 * RL) {   // four rows' loads in flight, then their adds in row order
+    v4f g[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      g[u][0] = ld4(x + (r + u * RL) * C + c);
+      g[u][1] = ld4(x + (r + u * RL) * C + c + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) body(r + u * RL, g[u][0], g[u][1]);
+  }
+  for (; r < r1; r += RL) body(r, ld4(x + r * C + c), ld4(x + r * C + c + 4));
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl * C + c + e] = acc[e];
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < C; cc += 256) {
+    float t = 0.f;
+    for (int l = 0; l < RL; ++l) t += red[l * C + cc];
+    part[(int64_t)blockIdx.x * C + cc] = t;
+  }
+}
+
+__global__ void colsum_blocks_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float t = 0.f;
+  for (int b = 0; b < nblk; ++b) t += part[(int64_t)b * C + c];
+  out[c] = t;
+}
+
 struct ConvScratch {
   float* p = nullptr;
   size_t floats = 0;
@@ -801,6 +878,32 @@ int to16_all(int prec, const float* const* src, const int64_t* n, int cnt, unsig
     if (prec == kPrecBF16) hipLaunchKernelGGL(to16_kernel<1>, grid, dim3(256), 0, s, src[i], n8, dst[i]);
     else hipLaunchKernelGGL(to16_kernel<2>, grid, dim3(256), 0, s, src[i], n8, dst[i]);
   }
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+}
+
+bool colsum8_ok(int64_t C) { return g_opt_conv_colsum16 && C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0; }
+
+// out[C] = column sums of x [rows, C] (colsum8_kernel; colsum8_ok(C)), fused with the 16-bit copy (kind 1) or
+// the unpooled 16-bit copy through arg (kind 2) at precision prec
+int colsum8(int kind, int prec, const float* x, const uint8_t* arg, int64_t rows, int C, int kw, unsigned short* y16,
+            float* out, hipStream_t s) {
+  const int RL = 256 / (C / 8);
+  int64_t nblk = std::min<int64_t>((rows + RL - 1) / RL, 2048);
+  int64_t per = (rows + nblk - 1) / nblk;
+  per = (per + RL - 1) / RL * RL;
+  nblk = (rows + per - 1) / per;
+  float* part = nullptr;
+  if (int rc = conv_scratch((size_t)nblk * C, &part, g_csb)) return rc;
+  const double bytes = (double)rows * C * (4.0 + (kind == 1 ? 2.0 : kind == 2 ? 1.0 + 2.0 * kw : 0.0));
+  ProfScope prof(kind == 0 ? "conv_colsum" : kind == 1 ? "conv_to16_colsum" : "conv_unpool16_colsum", s, bytes);
+  const dim3 grid((unsigned)nblk), block(256);
+#define SRK_CS8(LP_, K_) hipLaunchKernelGGL((colsum8_kernel<LP_, K_>), grid, block, 0, s, x, arg, rows, C, kw, per, y16, part)
+  if (kind == 0) SRK_CS8(0, 0);
+  else if (prec == kPrecBF16) { if (kind == 1) SRK_CS8(1, 1); else SRK_CS8(1, 2); }
+  else { if (kind == 1) SRK_CS8(2, 1); else SRK_CS8(2, 2); }
+#undef SRK_CS8
+  hipLaunchKernelGGL(colsum_blocks_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part, (int)nblk, C, out);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
 }
@@ -1145,7 +1248,7 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
   constexpr int BK = kR16BK, NST = 4;
   constexpr bool AKC = MODE != kWgrad;
   constexpr int HALF = 128 * BK;                     // 8 KB of 16-bit elements per half image
-  constexpr int NBH = BN / 128;
+  constexpr int NBH = BN >= 128 ? BN / 128 : 1;   // BN = 64: one 128-wide B image, its upper half masked
   constexpr int STAGE = (2 + NBH) * HALF;
   constexpr int NDMA = 2 + NBH;
   constexpr int WR = BN == 256 ? 1 : 2, WC = 4 / WR;
@@ -1200,7 +1303,7 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
 #pragma unroll
   for (int h = 0; h < NBH; ++h) {
     const int64_t n = n0 + h * 128 + ((p & 15) ^ ((bkk & 3) << 2)) * 8;
-    bok[h] = n < c.Nn;
+    bok[h] = n < c.Nn && n < n0 + BN;
     bvo[h] = (unsigned)(((int64_t)bkk * c.Nn + (bok[h] ? n : 0)) * 2);
   }
   const unsigned lds0 =
@@ -1381,11 +1484,13 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
   if (MODE != kWgrad && chans % RBK) return 1;
   if (MODE == kWgrad && c.Ci % unit) return 1;
   if (MODE == kDgrad && (c.sh != 1 || c.sw != 1)) return 1;
-  if (c.Nn % unit || c.Nn < 128 || c.M < 256 || c.M >= INT32_MAX || c.K >= INT32_MAX) return 1;
+  // 16-bit operands down to N = 64 (a 256 x 64 tile: the narrow data gradients of 64-channel inputs)
+  if (c.Nn % unit || c.Nn < (lp && g_opt_conv_ring64 ? 64 : 128) || c.M < 256 || c.M >= INT32_MAX || c.K >= INT32_MAX)
+    return 1;
   const double xb = (double)esz * c.N * c.H * c.W * c.Ci, yb = (double)esz * c.N * c.Ho * c.Wo * c.Co,
                wb = (double)esz * c.K * c.Nn;
   if (xb >= 2.1e9 || yb >= 2.1e9 || wb >= 2.1e9) return 1;
-  const int BN = c.Nn >= 256 ? 256 : 128;
+  const int BN = c.Nn >= 256 ? 256 : c.Nn >= 128 ? 128 : 64;
   const int64_t tm = (c.M + 255) / 256, tn = (c.Nn + BN - 1) / BN;
   const int splits0 = choose_splits(tm * tn, c.K, RBK, kCUs, MODE == kWgrad ? 256 : 16);
   c.kchunk = splits0 > 1 ? ((c.K + splits0 - 1) / splits0 + RBK - 1) / RBK * RBK : std::max<int64_t>(c.K, 1);
@@ -1418,10 +1523,12 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
     else hipLaunchKernelGGL((conv_ring_kernel<MODE, 128>), grid, block, 0, s, c);
   } else if (prec == kPrecBF16) {
     if (BN == 256) hipLaunchKernelGGL((conv_ring16_kernel<MODE, 256, 1>), grid, block, 0, s, c);
-    else hipLaunchKernelGGL((conv_ring16_kernel<MODE, 128, 1>), grid, block, 0, s, c);
+    else if (BN == 128) hipLaunchKernelGGL((conv_ring16_kernel<MODE, 128, 1>), grid, block, 0, s, c);
+    else hipLaunchKernelGGL((conv_ring16_kernel<MODE, 64, 1>), grid, block, 0, s, c);
   } else {
     if (BN == 256) hipLaunchKernelGGL((conv_ring16_kernel<MODE, 256, 2>), grid, block, 0, s, c);
-    else hipLaunchKernelGGL((conv_ring16_kernel<MODE, 128, 2>), grid, block, 0, s, c);
+    else if (BN == 128) hipLaunchKernelGGL((conv_ring16_kernel<MODE, 128, 2>), grid, block, 0, s, c);
+    else hipLaunchKernelGGL((conv_ring16_kernel<MODE, 64, 2>), grid, block, 0, s, c);
   }
   SRK_CHECK_HIP(hipGetLastError());
   *partial_out = c.partial;
@@ -1653,13 +1760,25 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
   // 16-bit sources: x and dY serve both GEMMs, Wd the data gradient (one scratch allocation)
   unsigned short* d16[3] = {nullptr, nullptr, nullptr};   // x, dY, Wd
   const int prec = srk::matmul_prec();
+  bool db_done = false;
   if (!dy_arg && srk::s16_ok(prec, Ci, Co, {x, dy, ws, x16, dy16})) {
     const float* src[3] = {x, dy, ws};
     const int64_t n[3] = {N * H * W * Ci, N * Ho * Wo * Co, nw};
-    const bool ready[3] = {x16 != nullptr, dy16 != nullptr, false};   // x16: the forward's copy of x
+    // the bias gradient with dY's conversion (or alone when the producer's copy is ready): one read of dY
+    const bool cs = db && dy && srk::colsum8_ok(Co);
+    bool ready[3] = {x16 != nullptr, dy16 != nullptr || cs, false};   // x16: the forward's copy of x
     d16[0] = const_cast<unsigned short*>(static_cast<const unsigned short*>(x16));
     d16[1] = const_cast<unsigned short*>(dy16);
+    if (cs && !dy16) {
+      float* d = nullptr;
+      if ((rc = srk::conv_scratch((size_t)(n[1] + 1) / 2, &d, srk::g_csd))) return rc;
+      d16[1] = reinterpret_cast<unsigned short*>(d);
+    }
     if ((rc = srk::to16_all(prec, src, n, dgrad_implicit ? 3 : 2, d16, s, ready))) return rc;
+    if (cs) {
+      if ((rc = srk::colsum8(dy16 ? 0 : 1, prec, dy, nullptr, N * Ho * Wo, (int)Co, 1, d16[1], db, s))) return rc;
+      db_done = true;
+    }
   }
   if (dx && full_width) {
     // A full-width "valid" conv (model_fbanks_cnn.py:74, conv3 1x10 on width 10): every input
@@ -1701,7 +1820,7 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
     if ((rc = srk::run_conv_gemm<srk::kWgrad>(g, s, "conv_wgrad"))) return rc;
     hipLaunchKernelGGL(srk::weight_grad_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, ws,
                        (int)Co, (int)Ci, (int)KH, (int)KW, dw);
-    if (db && (!g.db || g.a16) && (rc = srk::colsum_f32(dy, N * Ho * Wo, Co, Co, db, 0.f, s))) return rc;
+    if (db && !db_done && (!g.db || g.a16) && (rc = srk::colsum_f32(dy, N * Ho * Wo, Co, Co, db, 0.f, s))) return rc;
   }
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
@@ -1791,7 +1910,9 @@ int srk_conv2d_nhwc_bwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
     float* d = nullptr;
     if (int rc = srk::conv_scratch((size_t)(N * Ho * Wo * Co + 1) / 2, &d, srk::g_csd)) return rc;
     unsigned short* dy16 = reinterpret_cast<unsigned short*>(d);
-    {
+    if (db && srk::colsum8_ok(Co)) {   // the dense 16-bit dY and the bias gradient in one pass over the pooled dY
+      if (int rc = srk::colsum8(2, prec, dy_pooled, argmax, rows, (int)Co, (int)pool_w, dy16, db, s)) return rc;
+    } else {
       srk::ProfScope prof("conv_unpool16", s, (double)rows * Co * (4.0 + 1.0 + 2.0 * pool_w));
       const dim3 grid((unsigned)((rows * (Co / 8) + 255) / 256));
       if (prec == srk::kPrecBF16)
@@ -1799,9 +1920,9 @@ int srk_conv2d_nhwc_bwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
       else
         hipLaunchKernelGGL(srk::unpool16_kernel<2>, grid, dim3(256), 0, s, dy_pooled, argmax, rows, (int)Co, (int)pool_w, dy16);
       SRK_CHECK_HIP(hipGetLastError());
+      if (db)
+        if (int rc = srk::colsum_f32(dy_pooled, rows, Co, Co, db, 0.f, s)) return rc;
     }
-    if (db)
-      if (int rc = srk::colsum_f32(dy_pooled, rows, Co, Co, db, 0.f, s)) return rc;
     return srk::conv_bwd(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, 1, 1, nullptr, nullptr, dx, dw, nullptr, ws, x16, stream,
                          dy16);
   }

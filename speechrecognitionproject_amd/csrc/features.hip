@@ -36,6 +36,16 @@ __device__ __forceinline__ float bperm(int src_byte, float v) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(src_byte, __float_as_int(v)));
 }
 
+// PCM sample loads: float32 (what Dataset yields) or int16 (what the WAV holds — half the upload;
+// the reference's float32 samples are int16-valued, dataset.py:117, so the widened values are equal)
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const int16_t* p) { return (float)*p; }
+__device__ __forceinline__ v2f ld2(const float* p) { return *reinterpret_cast<const v2f*>(p); }
+__device__ __forceinline__ v2f ld2(const int16_t* p) {
+  const short2 v = *reinterpret_cast<const short2*>(p);
+  return v2f{(float)v.x, (float)v.y};
+}
+
 // sum over the 16 lanes of a frame group (lanes 16f .. 16f+15)
 __device__ __forceinline__ double group16_sum(double v) {
 #pragma unroll
@@ -61,7 +71,8 @@ struct FbankTables {
 
 // 4 waves per SIMD (<= 128 VGPRs): the window and the pass-A twiddles are read from LDS tables
 // staged once per workgroup; only the small lane constants stay in registers.
-__global__ __launch_bounds__(256, 4) void fbank_kernel(const float* __restrict__ pcm, float* __restrict__ out,
+template <typename T>
+__global__ __launch_bounds__(256, 4) void fbank_kernel(const T* __restrict__ pcm, float* __restrict__ out,
                                                        int64_t n_clips, FbankTables t) {
   __shared__ v2f sbuf[4][4 * 272];   // per wave: 4 frames x (16 x 17) transpose, reused for spectra / power
   __shared__ __attribute__((aligned(16))) double s_win[400];
@@ -92,7 +103,7 @@ __global__ __launch_bounds__(256, 4) void fbank_kernel(const float* __restrict__
     const int c = (int)(it % kFbChunks);
     const int gf = 4 * c + f;                     // this lane's frame (pass A)
     const bool live = gf < 98;
-    const float* __restrict__ x = pcm + clip * kPcmLen + 160 * (live ? gf : 0);
+    const T* __restrict__ x = pcm + clip * kPcmLen + 160 * (live ? gf : 0);
     // pre-emphasis (fp32, numpy's two roundings) x Hamming (fp64, :33-41), DC / Nyquist sums in fp64
     // every lane loads (dead lanes read in-clip samples) and the products are masked after: with the
     // loads under the condition the compiler serialises their waits
@@ -101,8 +112,8 @@ __global__ __launch_bounds__(256, 4) void fbank_kernel(const float* __restrict__
 #pragma unroll
     for (int i = 0; i < 13; ++i) {
       const int n = j + 16 * i;
-      xv[i] = *reinterpret_cast<const v2f*>(x + 2 * n);
-      xm[i] = x[(n == 0 && !(live && gf > 0)) ? 0 : 2 * n - 1];   // x[-1] only inside the clip
+      xv[i] = ld2(x + 2 * n);
+      xm[i] = ld1(x + ((n == 0 && !(live && gf > 0)) ? 0 : 2 * n - 1));   // x[-1] only inside the clip
     }
     v2f a[16];
     double dc = 0.0, ny = 0.0;
@@ -231,7 +242,8 @@ struct SpecTables {
   float scale;              // 1 / (fs * sum(w^2))
 };
 
-__global__ __launch_bounds__(256, 4) void spec_kernel(const float* __restrict__ pcm, float* __restrict__ out,
+template <typename T>
+__global__ __launch_bounds__(256, 4) void spec_kernel(const T* __restrict__ pcm, float* __restrict__ out,
                                                       int64_t n_clips, int transposed, SpecTables t) {
   __shared__ v2f sbuf[4][3 * 340];
   __shared__ __attribute__((aligned(16))) double s_win[640];
@@ -254,12 +266,12 @@ __global__ __launch_bounds__(256, 4) void spec_kernel(const float* __restrict__ 
     const int c = (int)(it % kSpChunks);
     const int gf = 3 * c + fa;
     const bool live = fa < 3 && gf < 49;
-    const float* __restrict__ x = pcm + clip * kPcmLen + 320 * (live ? gf : 0);
+    const T* __restrict__ x = pcm + clip * kPcmLen + 320 * (live ? gf : 0);
     // every lane loads (a dead lane's x is frame 0 of the clip) and the products are masked after:
     // with the loads under the `live` condition the compiler serialises 40 load / LDS waits
     v2f xv[20];
 #pragma unroll
-    for (int i = 0; i < 20; ++i) xv[i] = *reinterpret_cast<const v2f*>(x + 2 * (j + 16 * i));
+    for (int i = 0; i < 20; ++i) xv[i] = ld2(x + 2 * (j + 16 * i));
     v2f tw[19];   // pass-A twiddles, read ahead of the transpose stores
 #pragma unroll
     for (int k1 = 1; k1 < 20; ++k1) tw[k1 - 1] = s_tw[k1 * 16 + j];
@@ -323,19 +335,20 @@ __global__ __launch_bounds__(256, 4) void spec_kernel(const float* __restrict__ 
 }
 
 // ------------------------------------------------------------------------- K1 MFCC
-__device__ __forceinline__ void mfcc_load_chunk(const float* __restrict__ x, int c, int lane, v2f (&raw)[20]) {
+template <typename T>
+__device__ __forceinline__ void mfcc_load_chunk(const T* __restrict__ x, int c, int lane, v2f (&raw)[20]) {
   const int fa = lane >> 4, j = lane & 15;
   const int gf = 3 * c + (fa < 3 ? fa : 0);
   if (c > 0 && c < 16) {   // wave-uniform: frames 3..47 never touch the reflected padding
 #pragma unroll
-    for (int i = 0; i < 20; ++i) raw[i] = *reinterpret_cast<const v2f*>(x + 320 * gf + 2 * (j + 16 * i) - 320);
+    for (int i = 0; i < 20; ++i) raw[i] = ld2(x + 320 * gf + 2 * (j + 16 * i) - 320);
   } else {
 #pragma unroll
     for (int i = 0; i < 20; ++i) {
       int s0 = 320 * gf + 2 * (j + 16 * i) - 320, s1 = s0 + 1;
       s0 = s0 < 0 ? -s0 : (s0 > kPcmLen - 1 ? 2 * (kPcmLen - 1) - s0 : s0);
       s1 = s1 < 0 ? -s1 : (s1 > kPcmLen - 1 ? 2 * (kPcmLen - 1) - s1 : s1);
-      raw[i] = v2f{x[s0], x[s1]};
+      raw[i] = v2f{ld1(x + s0), ld1(x + s1)};
     }
   }
 }
@@ -412,8 +425,8 @@ __device__ __forceinline__ float dpp_mirror(float v) {
 
 // VAR bit 0: the DPP untangle exchange; bit 1: the pass-A and untangle twiddles held in registers for
 // the whole kernel (lane constants) instead of 28 LDS reads per chunk
-template <int VAR>
-__global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const float* __restrict__ pcm, float* __restrict__ out,
+template <int VAR, typename T>
+__global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const T* __restrict__ pcm, float* __restrict__ out,
                                                                   int layout, int64_t n_clips, DeviceTables t) {
   __shared__ __attribute__((aligned(16))) v2f tbuf[kM3Waves][3 * 340];
   constexpr int DBP = kM3DbP;
@@ -733,73 +746,121 @@ __global__ void noise_mix_kernel(const int16_t* __restrict__ pcm, const int16_t*
 
 using srk::DeviceTables;
 
-extern "C" {
-
 #ifdef SRK_MFCC_STAMPS
-int srk_debug_mfcc_stamps(unsigned long long* host, int64_t n) {
+extern "C" int srk_debug_mfcc_stamps(unsigned long long* host, int64_t n) {
   const int64_t cap = 512 * srk::kM3Waves * srk::kStampPhases;
   if (n > cap) n = cap;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(srk::g_mfcc_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
 }
 #endif
 
-int srk_fbank_fwd(const float* pcm, int64_t n_clips, float* out, void* stream) {
-  SRK_API_BEGIN
+namespace srk {
+namespace {
+
+template <typename T>
+int fbank_fwd(const T* pcm, int64_t n_clips, float* out, void* stream) {
   SRK_REQUIRE(n_clips >= 0 && n_clips <= INT32_MAX, SRK_ERR_INVALID, "srk_fbank_fwd: bad n_clips %lld", (long long)n_clips);
   if (n_clips == 0) return SRK_OK;
   SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_fbank_fwd: null pointer");
-  SRK_REQUIRE((uintptr_t)pcm % 8 == 0, SRK_ERR_INVALID, "srk_fbank_fwd: pcm must be 8-byte aligned");
+  SRK_REQUIRE((uintptr_t)pcm % (2 * sizeof(T)) == 0, SRK_ERR_INVALID, "srk_fbank_fwd: pcm must be %d-byte aligned",
+              (int)(2 * sizeof(T)));
   const DeviceTables* t = nullptr;
-  if (int rc = srk::get_tables(&t)) return rc;
-  srk::FbankTables ft{t->hamming400, t->tw256, t->post512, t->fbp_meta, t->fbp_w};
-  const int64_t items = n_clips * srk::kFbChunks;
+  if (int rc = get_tables(&t)) return rc;
+  FbankTables ft{t->hamming400, t->tw256, t->post512, t->fbp_meta, t->fbp_w};
+  const int64_t items = n_clips * kFbChunks;
   const int64_t blocks = std::min<int64_t>((items + 3) / 4, 2048);   // waves take (clip, 4-frame chunk) items
-  srk::ProfScope prof("fbank", srk::as_stream(stream), 111040.0 * (double)n_clips);   // 64000 in + 47040 out B/clip
-  hipLaunchKernelGGL(srk::fbank_kernel, dim3((unsigned)blocks), dim3(256), 0, srk::as_stream(stream), pcm, out, n_clips,
-                     ft);
+  // algorithmic bytes: the PCM in (64000 B/clip as fp32, 32000 as int16) + 47040 out
+  ProfScope prof("fbank", as_stream(stream), (16000.0 * sizeof(T) + 47040.0) * (double)n_clips);
+  hipLaunchKernelGGL(fbank_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), pcm, out, n_clips, ft);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
+}
+
+template <typename T>
+int spec_fwd(const T* pcm, int64_t n_clips, float* out, int transposed, void* stream) {
+  SRK_REQUIRE(n_clips >= 0 && n_clips <= INT32_MAX, SRK_ERR_INVALID, "srk_spec_fwd: bad n_clips");
+  if (n_clips == 0) return SRK_OK;
+  SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_spec_fwd: null pointer");
+  SRK_REQUIRE((uintptr_t)pcm % (2 * sizeof(T)) == 0, SRK_ERR_INVALID, "srk_spec_fwd: pcm must be %d-byte aligned",
+              (int)(2 * sizeof(T)));
+  const DeviceTables* t = nullptr;
+  if (int rc = get_tables(&t)) return rc;
+  SpecTables st{t->tukey640, t->tw320, t->post640, (float)t->spec_scale};
+  const int64_t items = n_clips * kSpChunks;
+  const int64_t blocks = std::min<int64_t>((items + 3) / 4, 2048);
+  ProfScope prof("spec", as_stream(stream), (16000.0 * sizeof(T) + 62916.0) * (double)n_clips);
+  hipLaunchKernelGGL(spec_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), pcm, out, n_clips,
+                     transposed ? 1 : 0, st);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+}
+
+template <typename T>
+int mfcc_fwd(const T* pcm, int64_t n_clips, float* out, int layout, void* stream) {
+  SRK_REQUIRE(n_clips >= 0 && n_clips <= INT32_MAX, SRK_ERR_INVALID, "srk_mfcc_fwd: bad n_clips");
+  SRK_REQUIRE(layout == 0 || layout == 1, SRK_ERR_INVALID, "srk_mfcc_fwd: layout must be 0 or 1");
+  if (n_clips == 0) return SRK_OK;
+  SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_mfcc_fwd: null pointer");
+  SRK_REQUIRE((uintptr_t)pcm % (2 * sizeof(T)) == 0, SRK_ERR_INVALID, "srk_mfcc_fwd: pcm must be %d-byte aligned",
+              (int)(2 * sizeof(T)));
+  const DeviceTables* t = nullptr;
+  if (int rc = get_tables(&t)) return rc;
+  ProfScope prof("mfcc", as_stream(stream), (16000.0 * sizeof(T) + 7956.0) * (double)n_clips);
+  const int64_t grid = std::min<int64_t>(n_clips, 256 * 2);   // persistent over clips, 2 per CU
+  const dim3 g((unsigned)grid), b(64 * kM3Waves);
+  hipStream_t s = as_stream(stream);
+  if (sizeof(T) == 2) {   // the int16 input: the default variant only
+    hipLaunchKernelGGL((mfcc3_kernel<3, T>), g, b, 0, s, pcm, out, layout, n_clips, *t);
+  } else {
+    switch (g_opt_mfcc_variant) {
+      case 1: hipLaunchKernelGGL((mfcc3_kernel<1, T>), g, b, 0, s, pcm, out, layout, n_clips, *t); break;
+      case 2: hipLaunchKernelGGL((mfcc3_kernel<2, T>), g, b, 0, s, pcm, out, layout, n_clips, *t); break;
+      case 3: hipLaunchKernelGGL((mfcc3_kernel<3, T>), g, b, 0, s, pcm, out, layout, n_clips, *t); break;
+      default: hipLaunchKernelGGL((mfcc3_kernel<0, T>), g, b, 0, s, pcm, out, layout, n_clips, *t);
+    }
+  }
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+}
+
+}  // namespace
+}  // namespace srk
+
+extern "C" {
+
+int srk_fbank_fwd(const float* pcm, int64_t n_clips, float* out, void* stream) {
+  SRK_API_BEGIN
+  return srk::fbank_fwd(pcm, n_clips, out, stream);
+  SRK_API_END
+}
+
+int srk_fbank_fwd_i16(const int16_t* pcm, int64_t n_clips, float* out, void* stream) {
+  SRK_API_BEGIN
+  return srk::fbank_fwd(pcm, n_clips, out, stream);
   SRK_API_END
 }
 
 int srk_spec_fwd(const float* pcm, int64_t n_clips, float* out, int transposed, void* stream) {
   SRK_API_BEGIN
-  SRK_REQUIRE(n_clips >= 0 && n_clips <= INT32_MAX, SRK_ERR_INVALID, "srk_spec_fwd: bad n_clips");
-  if (n_clips == 0) return SRK_OK;
-  SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_spec_fwd: null pointer");
-  SRK_REQUIRE((uintptr_t)pcm % 8 == 0, SRK_ERR_INVALID, "srk_spec_fwd: pcm must be 8-byte aligned");
-  const DeviceTables* t = nullptr;
-  if (int rc = srk::get_tables(&t)) return rc;
-  srk::SpecTables st{t->tukey640, t->tw320, t->post640, (float)t->spec_scale};
-  const int64_t items = n_clips * srk::kSpChunks;
-  const int64_t blocks = std::min<int64_t>((items + 3) / 4, 2048);
-  srk::ProfScope prof("spec", srk::as_stream(stream), 126916.0 * (double)n_clips);    // 64000 + 62916 B/clip
-  hipLaunchKernelGGL(srk::spec_kernel, dim3((unsigned)blocks), dim3(256), 0, srk::as_stream(stream), pcm, out, n_clips,
-                     transposed ? 1 : 0, st);
-  SRK_CHECK_HIP(hipGetLastError());
-  return SRK_OK;
+  return srk::spec_fwd(pcm, n_clips, out, transposed, stream);
+  SRK_API_END
+}
+
+int srk_spec_fwd_i16(const int16_t* pcm, int64_t n_clips, float* out, int transposed, void* stream) {
+  SRK_API_BEGIN
+  return srk::spec_fwd(pcm, n_clips, out, transposed, stream);
   SRK_API_END
 }
 
 int srk_mfcc_fwd(const float* pcm, int64_t n_clips, float* out, int layout, void* stream) {
   SRK_API_BEGIN
-  SRK_REQUIRE(n_clips >= 0 && n_clips <= INT32_MAX, SRK_ERR_INVALID, "srk_mfcc_fwd: bad n_clips");
-  SRK_REQUIRE(layout == 0 || layout == 1, SRK_ERR_INVALID, "srk_mfcc_fwd: layout must be 0 or 1");
-  if (n_clips == 0) return SRK_OK;
-  SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_mfcc_fwd: null pointer");
-  const DeviceTables* t = nullptr;
-  if (int rc = srk::get_tables(&t)) return rc;
-  srk::ProfScope prof("mfcc", srk::as_stream(stream), 71956.0 * (double)n_clips);     // 64000 + 7956 B/clip
-  const int64_t grid = std::min<int64_t>(n_clips, 256 * 2);   // persistent over clips, 2 per CU
-  const dim3 g((unsigned)grid), b(64 * srk::kM3Waves);
-  switch (srk::g_opt_mfcc_variant) {
-    case 1: hipLaunchKernelGGL(srk::mfcc3_kernel<1>, g, b, 0, srk::as_stream(stream), pcm, out, layout, n_clips, *t); break;
-    case 2: hipLaunchKernelGGL(srk::mfcc3_kernel<2>, g, b, 0, srk::as_stream(stream), pcm, out, layout, n_clips, *t); break;
-    case 3: hipLaunchKernelGGL(srk::mfcc3_kernel<3>, g, b, 0, srk::as_stream(stream), pcm, out, layout, n_clips, *t); break;
-    default: hipLaunchKernelGGL(srk::mfcc3_kernel<0>, g, b, 0, srk::as_stream(stream), pcm, out, layout, n_clips, *t);
-  }
-  SRK_CHECK_HIP(hipGetLastError());
-  return SRK_OK;
+  return srk::mfcc_fwd(pcm, n_clips, out, layout, stream);
+  SRK_API_END
+}
+
+int srk_mfcc_fwd_i16(const int16_t* pcm, int64_t n_clips, float* out, int layout, void* stream) {
+  SRK_API_BEGIN
+  return srk::mfcc_fwd(pcm, n_clips, out, layout, stream);
   SRK_API_END
 }
 

@@ -27,6 +27,8 @@ int g_opt_conv_unpool_gather = 1;
 int g_opt_conv_tile = 128;
 int g_opt_conv_ring = 0x77;
 int g_opt_conv_unpool16 = 1;
+int g_opt_conv_colsum16 = 1;
+int g_opt_conv_ring64 = 1;
 int g_opt_mfcc_variant = 3;
 int g_opt_gemm_streamk = 1;
 int g_opt_gemm16_persistent = 0;
@@ -392,6 +394,14 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "mfcc_variant") {   // K1: bit 0 DPP untangle exchange, bit 1 twiddles in registers (bitwise the same)
     SRK_REQUIRE(value >= 0 && value <= 3, SRK_ERR_INVALID, "mfcc_variant must be 0..3");
     srk::g_opt_mfcc_variant = (int)value;
+    return SRK_OK;
+  }
+  if (n == "conv_ring64") {   // 16-bit ring convs down to N = 64 (256 x 64 tiles) (1) or N >= 128 only (0)
+    srk::g_opt_conv_ring64 = value != 0;
+    return SRK_OK;
+  }
+  if (n == "conv_colsum16") {   // 16-bit modes: conv bias gradients fused into dY's 16-bit conversion (1) or not (0)
+    srk::g_opt_conv_colsum16 = value != 0;
     return SRK_OK;
   }
   if (n == "conv_unpool16") {   // 16-bit modes: pooled-conv backward writes dY's 16-bit copy directly (1) or not (0)

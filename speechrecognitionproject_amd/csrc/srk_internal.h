@@ -108,6 +108,11 @@ extern int g_opt_conv_unpool_gather;
 // 16-bit-source modes: the pooled conv's backward writes the dense dY straight as its 16-bit copy
 // ("conv_unpool16", default 1; 0 = dense fp32 dY, then the 16-bit conversion and column sums)
 extern int g_opt_conv_unpool16;
+// 16-bit-source modes: the conv bias gradient (column sums of dY) fused into the pass that rounds dY (or
+// unpools it) to its 16-bit copy ("conv_colsum16", default 1; 0 = a separate column-sum pass over dY)
+extern int g_opt_conv_colsum16;
+// 16-bit ring convs for N = 64 .. 127 as 256 x 64 tiles ("conv_ring64", default 1; 0 = N >= 128 only)
+extern int g_opt_conv_ring64;
 // conv tile shape ("conv_tile": 128 = 128-row tiles of 4 waves, 256 = 256-row tiles of 8 waves on
 // tall convolutions)
 extern int g_opt_conv_tile;

@@ -1,9 +1,10 @@
 """Host wrappers of the feature kernels K1-K4 and the augmentation kernel K10 (include/srk.h).
 Batched, device-resident.
 
-All functions take PCM as float32 [B, 16000] (int16-valued, as dataset.py:117 produces); a CPU
-tensor is copied to the current GPU first (the reference forward receives CPU batches,
-training.py:86).  There is no CPU path: without a GPU and libsrk.so these raise.
+All functions take PCM as float32 [B, 16000] (int16-valued, as dataset.py:117 produces); the
+feature kernels K1-K3 also take int16 PCM (the WAV samples: half the bytes to upload, the same
+values).  A CPU tensor is copied to the current GPU first (the reference forward receives CPU
+batches, training.py:86).  There is no CPU path: without a GPU and libsrk.so these raise.
 """
 import ctypes
 
@@ -27,7 +28,8 @@ def ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-def as_device_pcm(pcm):
+def as_device_pcm(pcm, keep_int16=False):
+    """[B, 16000] PCM on the GPU, contiguous: float32, or int16 kept as is with ``keep_int16``."""
     require_gpu()
     if not torch.is_tensor(pcm):
         pcm = torch.as_tensor(pcm)
@@ -37,32 +39,38 @@ def as_device_pcm(pcm):
         raise SrkError("expected PCM of shape [B, %d], got %s" % (SEQ_LENGTH, tuple(pcm.shape)))
     if pcm.device.type != "cuda":
         pcm = pcm.to("cuda", non_blocking=True)
+    if keep_int16 and pcm.dtype == torch.int16:
+        return pcm.contiguous()
     return pcm.to(torch.float32).contiguous()
+
+
+def _entry(name, x):
+    return name + "_i16" if x.dtype == torch.int16 else name
 
 
 def fbank(pcm, out=None):
     """K2 log-mel filter banks [B, 98, 120] (models/model_fbanks_cnn.py:15-66)."""
-    x = as_device_pcm(pcm)
+    x = as_device_pcm(pcm, keep_int16=True)
     out = torch.empty((x.shape[0], 98, 120), device=x.device, dtype=torch.float32) if out is None else out
-    call("srk_fbank_fwd", ptr(x), x.shape[0], ptr(out), stream_ptr())
+    call(_entry("srk_fbank_fwd", x), ptr(x), x.shape[0], ptr(out), stream_ptr())
     return out
 
 
 def mfcc(pcm, time_major=False, out=None):
     """K1 MFCC+deltas: [B, 39, 51], or [B, 51, 39] if ``time_major`` (model_mfcc_bgru.py:11-19,34)."""
-    x = as_device_pcm(pcm)
+    x = as_device_pcm(pcm, keep_int16=True)
     shape = (x.shape[0], 51, 39) if time_major else (x.shape[0], 39, 51)
     out = torch.empty(shape, device=x.device, dtype=torch.float32) if out is None else out
-    call("srk_mfcc_fwd", ptr(x), x.shape[0], ptr(out), 1 if time_major else 0, stream_ptr())
+    call(_entry("srk_mfcc_fwd", x), ptr(x), x.shape[0], ptr(out), 1 if time_major else 0, stream_ptr())
     return out
 
 
 def spec(pcm, transposed=False, out=None):
     """K3 log spectrogram: [B, 321, 49], or [B, 49, 321] if ``transposed`` (model_spec_*.py)."""
-    x = as_device_pcm(pcm)
+    x = as_device_pcm(pcm, keep_int16=True)
     shape = (x.shape[0], 49, 321) if transposed else (x.shape[0], 321, 49)
     out = torch.empty(shape, device=x.device, dtype=torch.float32) if out is None else out
-    call("srk_spec_fwd", ptr(x), x.shape[0], ptr(out), 1 if transposed else 0, stream_ptr())
+    call(_entry("srk_spec_fwd", x), ptr(x), x.shape[0], ptr(out), 1 if transposed else 0, stream_ptr())
     return out
 
 

@@ -118,3 +118,15 @@ def test_mfcc_variants_bitwise(gpu, layout):
         _lib.set_option("mfcc_variant", 3)
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
+
+
+@pytest.mark.parametrize("kind", ["mfcc", "mfcc_tm", "fbank", "spec", "spec_t"])
+def test_int16_pcm_entry_points_equal_float32(gpu, kind):
+    """srk_{mfcc,fbank,spec}_fwd_i16: int16 PCM widened in the load stage gives bit for bit the result of
+    the float32 entry on the same (int16-valued) samples — edge clips, reflect-padded chunks included."""
+    x, _ = synthetic_clips(67, seed=81)
+    x16 = torch.from_numpy(x.astype(np.int16)).cuda()
+    x32 = x16.to(torch.float32)
+    f = {"mfcc": lambda p: K.mfcc(p), "mfcc_tm": lambda p: K.mfcc(p, time_major=True), "fbank": K.fbank,
+         "spec": lambda p: K.spec(p), "spec_t": lambda p: K.spec(p, transposed=True)}[kind]
+    assert torch.equal(f(x16), f(x32))

@@ -4,9 +4,9 @@ Parity is unpinned (librosa / resampy absent; tests/test_pitch.py pins the oracl
 Device vs oracle: the same float64 / float32 operations in the same order, except the FFT algorithm
 (radix-2 here, pocketfft in numpy) and the constant tables (glibc vs numpy / scipy transcendentals),
 both at the 1e-16 level — a stored complex64 value or an int16 truncation flips only when a value
-sits that close to a rounding boundary.  Bound (PITCH_EXACT_FRAC, PITCH_MAX_LSB): at least 99.9 % of
-the output samples bit-identical, none more than 2 int16 steps away; plus the known answers on the
-device and the batch / augmentation plumbing."""
+sits that close to a rounding boundary.  Bound (tests/tolerances.py PITCH_EXACT_FRAC, PITCH_MAX_LSB):
+at least 99.9 % of the output samples bit-identical, none more than 2 int16 steps away; plus the known
+answers on the device and the batch / augmentation plumbing."""
 import random
 
 import numpy as np
@@ -14,13 +14,12 @@ import pytest
 import torch
 
 from oracle import pitch as P
+from tolerances import PITCH_EXACT_FRAC, PITCH_MAX_LSB
 from speechrecognitionproject_amd import features as K
 from speechrecognitionproject_amd.synthetic import synthetic_clips
 
 pytestmark = pytest.mark.gpu
 
-PITCH_EXACT_FRAC = 0.999
-PITCH_MAX_LSB = 2
 SR = 16000
 
 

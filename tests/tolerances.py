@@ -25,6 +25,9 @@
   scale); the fused Adam update vs torch's Adam formula on the same gradient <= 2e-7 absolute
   (LP_ADAM_ABS; lr = 1e-4); the update's disagreement with the fp32 oracle's own Adam step, weighted
   by |g_oracle|, <= 2e-2 (LP_UPDATE_WEIGHTED).
+* pitch_shifting (K12, parity unpinned): device vs oracle/pitch.py int16 outputs, >= 99.9 % of the
+  samples bit-identical and none more than 2 int16 steps apart (PITCH_EXACT_FRAC, PITCH_MAX_LSB):
+  the same operations in the same order except the FFT algorithm and the constant tables' libm.
 * bf16 / fp16 GRU forward vs a float64 emulation of the same operand rounding: <= 2e-3 absolute on
   y (h in [-1, 1]; a rounding flip of one operand moves a gate pre-activation by ~1e-4).
 """
@@ -44,6 +47,8 @@ GRU_LOWPREC_EMU_ABS = 2e-3
 LP_GRAD_REL = 2e-2
 LP_ADAM_ABS = 2e-7
 LP_UPDATE_WEIGHTED = 2e-2
+PITCH_EXACT_FRAC = 0.999
+PITCH_MAX_LSB = 2
 
 
 def fbank_ok(out, ref):

@@ -131,6 +131,31 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
 // that no longer waits out one load latency per chunk).
 constexpr int kPre = 32;
 
+// Combine the chunk partials of channel c in chunk order (Chan), one lane (srk option bn_tree = 0).
+__device__ __forceinline__ void combine_chunks(const float* __restrict__ pmean, const float* __restrict__ pm2,
+                                               const BnGeom& g, int c, float& n, float& mu, float& m2) {
+  n = 0.f;
+  mu = 0.f;
+  m2 = 0.f;
+  for (int k0 = 0; k0 < g.chunks; k0 += kPre) {
+    float vm[kPre], v2[kPre];
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+      const int64_t k = k0 + u < g.chunks ? k0 + u : g.chunks - 1;
+      vm[u] = pmean[k * g.C + c];
+      v2[u] = pm2[k * g.C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+      if (k0 + u < g.chunks) {
+        const int64_t r0 = (int64_t)(k0 + u) * g.rows_per_chunk;
+        const float nb = (float)((r0 + g.rows_per_chunk < g.M ? g.rows_per_chunk : g.M - r0));
+        chan(n, mu, m2, nb, vm[u], v2[u]);
+      }
+    }
+  }
+}
+
 // Combine the chunk partials of channel c (Chan's pairwise formula) as a fixed pairwise tree, one wave
 // per channel: lane l combines chunks 4l .. 4l+3 in order (kMaxChunks = 256 = 4 x 64), then the lanes pair up at distance 1, 2, .. 32 (lane l takes lane
 // l + d when l % 2d == 0).  Deterministic (the tree does not depend on timing) and shallower: 3 + 6
@@ -167,16 +192,21 @@ __device__ __forceinline__ void combine_chunks_tree(const float* __restrict__ pm
 
 // Biased variance for the normalisation, unbiased for the running estimate (nn.BatchNorm1d,
 // momentum update).  Block = 4 waves = 4 channels (combine_chunks_tree).
+template <bool TREE>
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ pmean,
                                                           const float* __restrict__ pm2, BnGeom g, float eps,
                                                           float momentum, float* __restrict__ mean,
                                                           float* __restrict__ invstd, float* __restrict__ running_mean,
                                                           float* __restrict__ running_var) {
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int c = TREE ? blockIdx.x * 4 + (threadIdx.x >> 6) : blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.C) return;
   float n, mu, m2;
-  combine_chunks_tree(pmean, pm2, g, c, n, mu, m2);
-  if ((threadIdx.x & 63) != 0) return;
+  if (TREE) {
+    combine_chunks_tree(pmean, pm2, g, c, n, mu, m2);
+    if ((threadIdx.x & 63) != 0) return;
+  } else {
+    combine_chunks(pmean, pm2, g, c, n, mu, m2);
+  }
   const float var = m2 / (float)g.M;
   mean[c] = mu;
   invstd[c] = 1.0f / sqrtf(var + eps);
@@ -463,9 +493,14 @@ int srk_batchnorm_fwd16(const float* x, int64_t M, int64_t C, const float* gamma
     if (int rc = srk::bn_scratch((size_t)2 * g.chunks * C, &part)) return rc;
     hipLaunchKernelGGL(srk::bn_stats_kernel, dim3((unsigned)((g.C4 + g.CQ - 1) / g.CQ), (unsigned)g.chunks), dim3(256),
                        0, s, x, g, part, part + (size_t)g.chunks * C);
-    hipLaunchKernelGGL(srk::bn_finalize_kernel, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, s, part,
-                       part + (size_t)g.chunks * C, g, eps, momentum, save_mean, save_invstd, running_mean,
-                       running_var);
+    if (srk::g_opt_bn_tree)
+      hipLaunchKernelGGL(srk::bn_finalize_kernel<true>, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, s, part,
+                         part + (size_t)g.chunks * C, g, eps, momentum, save_mean, save_invstd, running_mean,
+                         running_var);
+    else
+      hipLaunchKernelGGL(srk::bn_finalize_kernel<false>, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
+                         part + (size_t)g.chunks * C, g, eps, momentum, save_mean, save_invstd, running_mean,
+                         running_var);
   } else {
     hipLaunchKernelGGL(srk::bn_eval_stats_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, running_mean,
                        running_var, (int)C, eps, save_mean, save_invstd);

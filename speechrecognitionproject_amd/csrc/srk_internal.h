@@ -113,6 +113,9 @@ extern int g_opt_conv_unpool16;
 extern int g_opt_conv_colsum16;
 // 16-bit ring convs for N = 64 .. 127 as 256 x 64 tiles ("conv_ring64", default 1; 0 = N >= 128 only)
 extern int g_opt_conv_ring64;
+// BatchNorm training statistics: the 256 chunk partials combined as a fixed pairwise tree, one wave per
+// channel ("bn_tree", default 1; 0 = one lane per channel in chunk order)
+extern int g_opt_bn_tree;
 // conv tile shape ("conv_tile": 128 = 128-row tiles of 4 waves, 256 = 256-row tiles of 8 waves on
 // tall convolutions)
 extern int g_opt_conv_tile;

@@ -41,23 +41,29 @@ def main():
     # control: a capture on C that S never joins
     g0 = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g0, stream=C, capture_error_mode="relaxed"):
-        x.mul_(1.0)
+        x.add_(0.5)
         res["capture_not_joined"] = query_in_thread(e)
 
     # S joins the capture through an event recorded in it, then is joined back before it ends
     g1 = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g1, stream=C, capture_error_mode="relaxed"):
-        f = torch.cuda.Event()
-        f.record(C)
-        S.wait_event(f)
-        res["S_joined"] = query_in_thread(e)
-        with torch.cuda.stream(S):
-            x.add_(1.0)
-        C.wait_stream(S)
-    res["after_capture"] = query_in_thread(e)
-    g1.replay()
+    try:
+        with torch.cuda.graph(g1, stream=C, capture_error_mode="relaxed"):
+            f = torch.cuda.Event()
+            f.record(C)
+            S.wait_event(f)
+            res["S_joined"] = query_in_thread(e)
+            try:
+                with torch.cuda.stream(S):
+                    x.add_(1.0)
+                res["capture_after_query"] = "ok"
+            except RuntimeError as err:
+                res["capture_after_query"] = str(err).splitlines()[0]
+            C.wait_stream(S)
+        res["capture_end"] = "ok"
+    except RuntimeError as err:
+        res["capture_end"] = str(err).splitlines()[0]
     torch.cuda.synchronize()
-    res["x_after_replay"] = float(x[0].item())   # 1 (eager) + 1 (replay of g1); g0 multiplies by 1
+    res["after_capture"] = query_in_thread(e)
     print(json.dumps(res), flush=True)
 
 

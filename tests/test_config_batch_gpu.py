@@ -145,7 +145,23 @@ def cfg4_f64(cfg4_case):
     return _resnet_oracle_f64(sd, x, y)
 
 
-def test_resnet_bgru_train_step_at_cfg4_batch(gpu, cfg4_case, cfg4_f64):
+@pytest.fixture(scope="module")
+def cfg4_noise(cfg4_case, cfg4_f64):
+    """Per gradient tensor, how far the reference's own fp32 arithmetic lands from float64 under two
+    batch orders (the step on the clips as given and reversed: the same mathematics — mean loss, batch
+    statistics — summed in another order): max of the two max-abs relative errors."""
+    x, y, sd, ref = cfg4_case[:4]
+    rev, _, _ = _resnet_oracle(sd, np.ascontiguousarray(x[::-1]), np.ascontiguousarray(y[::-1]))
+    p64 = dict(cfg4_f64.named_parameters())
+    out = {}
+    for r in (ref, rev):
+        for n, p in r.named_parameters():
+            if p64[n].grad is not None:
+                out[n] = max(out.get(n, 0.0), rel_err(p.grad.double().numpy(), p64[n].grad.numpy()))
+    return out
+
+
+def test_resnet_bgru_train_step_at_cfg4_batch(gpu, cfg4_case, cfg4_f64, cfg4_noise):
     """cfg4 rank shard (B = 512, fp32): logits, loss, every gradient and every BatchNorm running
     statistic vs the oracle's training-mode step on the same clips."""
     from speechrecognitionproject_amd.models import model_resnet_bgru
@@ -157,11 +173,20 @@ def test_resnet_bgru_train_step_at_cfg4_batch(gpu, cfg4_case, cfg4_f64):
     assert _lib.spin_timeouts() == 0
     assert rel_err(out, want) <= LOGITS_REL, rel_err(out, want)
     assert abs(loss - want_loss) <= 1e-4 * max(1.0, abs(want_loss))
-    # gradients vs float64, bounded by the fp32 oracle's own worst tensor error (module docstring)
+    # gradients vs float64, each tensor within twice the reference fp32 arithmetic's own error on it
+    # (module docstring; cfg4_noise)
     ref64 = cfg4_f64
-    p64, p32 = dict(ref64.named_parameters()), dict(ref.named_parameters())
-    spread = max(rel_err(p32[n].grad.double().numpy(), p64[n].grad.numpy()) for n in p64 if p64[n].grad is not None)
-    _check_grads(net, ref64, bound=max(GRAD_REL, 1.25 * spread))
+    p64 = dict(ref64.named_parameters())
+    worst = {}
+    for n, p in net.named_parameters():
+        if p64[n].grad is None:
+            assert p.grad is None, n
+            continue
+        e = rel_err(p.grad.cpu().double().numpy(), p64[n].grad.numpy())
+        worst[n] = (round(e, 5), round(cfg4_noise[n], 5))
+    print(sorted(worst.items(), key=lambda kv: -kv[1][0])[:8])
+    bad = {n: v for n, v in worst.items() if not v[0] <= max(GRAD_REL, 2.0 * v[1])}
+    assert not bad, bad
     refb = dict(ref.named_buffers())
     nbn = ntrack = 0
     for n, b in net.named_buffers():

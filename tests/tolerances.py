@@ -25,9 +25,17 @@
   scale); the fused Adam update vs torch's Adam formula on the same gradient <= 2e-7 absolute
   (LP_ADAM_ABS; lr = 1e-4); the update's disagreement with the fp32 oracle's own Adam step, weighted
   by |g_oracle|, <= 2e-2 (LP_UPDATE_WEIGHTED).
-* pitch_shifting (K12, parity unpinned): device vs oracle/pitch.py int16 outputs, >= 99.9 % of the
-  samples bit-identical and none more than 2 int16 steps apart (PITCH_EXACT_FRAC, PITCH_MAX_LSB):
-  the same operations in the same order except the FFT algorithm and the constant tables' libm.
+* pitch_shifting (K12, parity unpinned): device vs oracle/pitch.py int16 outputs per clip, RMS
+  difference <= 1e-3 of the clip's RMS and every sample within 64 int16 steps, modulo the int16 wrap
+  (PITCH_REL_RMS, PITCH_MAX_LSB, pitch_close).  Not bitwise, measured (tools/pitch_diag.py): the STFT's
+  first column is the reflect-padded frame centred on sample 0, an even signal, so its spectrum is real
+  and the imaginary parts are FFT roundoff whose SIGN decides each phase between 0 and +-pi — any two
+  FFT implementations (numpy's pocketfft and the device's radix-2) disagree on ~2 % of them; the phase
+  vocoder starts its float32 phase accumulator there, so a 2 pi offset changes the float32 rounding of
+  phases that reach ~5e4 rad (ulp 0.004 rad).  Measured: 1.6-2.8e-4 RMS, <= 20 steps on loud clips.
+  Degenerate inputs are excluded: a tone with a whole number of periods per frame (1000 Hz at 16 kHz)
+  leaves most bins exactly zero, so their phases — accumulated over the clip and loud again in the last,
+  reflect-padded frame — are FFT roundoff in ANY implementation (measured: 8 % RMS device vs oracle).
 * bf16 / fp16 GRU forward vs a float64 emulation of the same operand rounding: <= 2e-3 absolute on
   y (h in [-1, 1]; a rounding flip of one operand moves a gate pre-activation by ~1e-4).
 """
@@ -47,8 +55,17 @@ GRU_LOWPREC_EMU_ABS = 2e-3
 LP_GRAD_REL = 2e-2
 LP_ADAM_ABS = 2e-7
 LP_UPDATE_WEIGHTED = 2e-2
-PITCH_EXACT_FRAC = 0.999
-PITCH_MAX_LSB = 2
+PITCH_REL_RMS = 1e-3
+PITCH_MAX_LSB = 64
+
+
+def pitch_close(out, ref):
+    """K12 output vs oracle/pitch.py for one clip (int16-valued float arrays): (ok, (rel_rms, max_lsb)),
+    differences taken modulo the int16 wrap (a value at the +-32768 edge wraps on one side only)."""
+    d = np.abs(np.asarray(out, np.float64) - np.asarray(ref, np.float64))
+    d = np.minimum(d, 65536.0 - d)
+    rms = np.sqrt(np.mean(d ** 2)) / max(np.sqrt(np.mean(np.asarray(ref, np.float64) ** 2)), 1.0)
+    return (rms <= PITCH_REL_RMS and d.max() <= PITCH_MAX_LSB), (rms, d.max())
 
 
 def fbank_ok(out, ref):

@@ -27,3 +27,8 @@ for c in r.get("configs", []): line += " | %s %s %s" % (c["config"], c["dtype"],
 print(line)
 PY
 done
+if [ -n "$HANDOFF" ]; then
+  timeout -k 10 120 tools/_exp/handoff_micro > "$OUT/handoff_micro.txt" 2>&1; rc=$?
+  cat "$OUT/handoff_micro.txt"
+  exit $rc
+fi

@@ -378,6 +378,13 @@ typedef float f32x4_ __attribute__((ext_vector_type(4)));
 
 // Diagnostic build only (tools/build_variant.sh ... -DSRK_MFCC_STAMPS): per-wave s_memtime phase
 // totals, read back by srk_debug_mfcc_stamps (tools/mfcc_stamps.py).  Never in the product build.
+// Diagnostic builds only (tools/build_variant.sh ... -DSRK_MFCC_STOP=n, tools/feat_budget.sh): the chunk
+// step ends after phase n (0 = the sample loads only, 1 = + window / pass A / transpose, 2 = + pass B,
+// 3 = + untangle, 4 = everything), so per-phase instruction counts are differences of SQ_INSTS_* per clip.
+#ifndef SRK_MFCC_STOP
+#define SRK_MFCC_STOP 4
+#endif
+
 #ifdef SRK_MFCC_STAMPS
 constexpr int kStampPhases = 10;
 __device__ unsigned long long g_mfcc_stamps[512 * kM3Waves * kStampPhases];
@@ -496,6 +503,15 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const T* __rest
   // so those loads overlap pass B, the untangle and the mel reduction.
   auto step = [&](v2f (&raw)[20], int64_t clip, int k, float& vmax) {
     const int c = chunk_of(k);
+    if (SRK_MFCC_STOP == 0) {
+      const bool more = k + 1 < nsteps;
+      int64_t nclip = more ? clip : clip + gridDim.x;
+      nclip = nclip < n_clips ? nclip : clip;
+#pragma unroll
+      for (int i = 0; i < 20; ++i) asm volatile("" :: "v"(raw[i].x), "v"(raw[i].y));
+      mfcc_load_chunk(pcm + nclip * kPcmLen, chunk_of(more ? k + 1 : 0), lane, raw);
+      return;
+    }
     v2f a[20];
 #pragma unroll
     for (int i = 0; i < 20; ++i) a[i] = raw[i] * win[i];
@@ -516,6 +532,7 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const T* __rest
       nclip = nclip < n_clips ? nclip : clip;
       mfcc_load_chunk(pcm + nclip * kPcmLen, chunk_of(more ? k + 1 : 0), lane, raw);
     }
+    if (SRK_MFCC_STOP == 1) return;
     wave_lds_fence();
     // lanes 60..63 (fb = 3) duplicate frame 2's reads and park their results in the unused tail
     // of the slice (3 * 321 + 303 < 2 * 1020 floats): no divergent branches in this phase
@@ -524,6 +541,11 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const T* __rest
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) b[jj] = tb[fbr * 340 + k1b * 17 + jj];
     dft16v(b);
+    if (SRK_MFCC_STOP == 2) {
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) asm volatile("" :: "v"(b[jj].x), "v"(b[jj].y));
+      return;
+    }
     wave_lds_fence();
     MFCC_STAMP(1);
     // untangle the packed real FFT: with A = Z[k], B = Z[320 - k], W = W640^k,
@@ -564,6 +586,7 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const T* __rest
       two_bins(b[k2].x, b[k2].y, bx, by, wpost[k2], k1b + 20 * k2);
     }
     if (k1b == 0) two_bins(b[8].x, b[8].y, b[8].x, b[8].y, w160, 160);
+    if (SRK_MFCC_STOP == 3) return;
     wave_lds_fence();
     MFCC_STAMP(2);
     // Slaney mel (the lane's narrow and wide filter) -> power_to_db(ref = 1, amin = 1e-10).  The 18

@@ -30,6 +30,7 @@ int g_opt_conv_unpool16 = 1;
 int g_opt_conv_colsum16 = 1;
 int g_opt_conv_ring64 = 1;
 int g_opt_bn_tree = 1;
+int g_opt_gru_poll_pipe = 0;
 int g_opt_mfcc_variant = 3;
 int g_opt_gemm_streamk = 1;
 int g_opt_gemm16_persistent = 0;
@@ -395,6 +396,10 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "mfcc_variant") {   // K1: bit 0 DPP untangle exchange, bit 1 twiddles in registers (bitwise the same)
     SRK_REQUIRE(value >= 0 && value <= 3, SRK_ERR_INVALID, "mfcc_variant must be 0..3");
     srk::g_opt_mfcc_variant = (int)value;
+    return SRK_OK;
+  }
+  if (n == "gru_poll_pipe") {   // 16-bit persistent GRU: four flag polls in flight (1) or one at a time (0)
+    srk::g_opt_gru_poll_pipe = value != 0;
     return SRK_OK;
   }
   if (n == "bn_tree") {   // BatchNorm statistics: chunk partials combined as a pairwise tree (1) or in order (0)

@@ -15,6 +15,8 @@
 //   8  4 waves per workgroup: wave 0 polls, a workgroup barrier releases the others, every wave loads
 //      its 1 KB and stores its own, barrier, one lane publishes (the recurrence kernels' step shape)
 //  16  partner on another XCD (blocks 0 and 1) instead of the same XCD (blocks 0 and 8)
+//  32  pipelined polls: four flag loads in flight (issued ~64 clk apart), each checked as it returns
+//      (vmcnt retires in order), instead of one load -> wait -> check -> sleep at a time
 // Every spin is bounded (a hop that waits > ~1 s gives up and the run reports it), and every
 // workgroup of the grid reaches the end.
 #include <hip/hip_runtime.h>
@@ -37,7 +39,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rs(const void* p) {
 template <int V>
 __global__ __launch_bounds__(256) void pingpong(unsigned* flags, float* payload, unsigned long long* out, int iters,
                                                 unsigned* failed) {
-  constexpr bool WT = V & 1, NOSLEEP = V & 2, NOPAY = V & 4, FOURW = V & 8, CROSS = V & 16;
+  constexpr bool WT = V & 1, NOSLEEP = V & 2, NOPAY = V & 4, FOURW = V & 8, CROSS = V & 16, PIPE = V & 32;
   const int partner = CROSS ? 1 : 8;
   const int role = blockIdx.x == 0 ? 0 : blockIdx.x == partner ? 1 : -1;
   if (role < 0) return;
@@ -56,7 +58,31 @@ __global__ __launch_bounds__(256) void pingpong(unsigned* flags, float* payload,
     // wait: role 0 waits for the partner's step i (none at i = 0), role 1 for step i + 1
     const unsigned need = role == 0 ? (unsigned)i : (unsigned)(i + 1);
     if (need > 0) {
-      if (wave == 0) {
+      if (wave == 0 && PIPE) {
+        unsigned spins = 0;
+        unsigned q0 = __hip_atomic_load(other_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_sleep(1);
+        unsigned q1 = __hip_atomic_load(other_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_sleep(1);
+        unsigned q2 = __hip_atomic_load(other_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_sleep(1);
+        unsigned q3 = __hip_atomic_load(other_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (true) {
+          if (q0 >= need) break;
+          q0 = __hip_atomic_load(other_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (q1 >= need) break;
+          q1 = __hip_atomic_load(other_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (q2 >= need) break;
+          q2 = __hip_atomic_load(other_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (q3 >= need) break;
+          q3 = __hip_atomic_load(other_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (++spins >= kSpin / 4) {
+            if (lane == 0) bad = 1;
+            break;
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (wave == 0) {
         unsigned spins = 0;
         while (true) {
           const unsigned v = __hip_atomic_load(other_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -137,6 +163,9 @@ int main() {
       {17, "write-through payload+flag, other XCD, sleep"},
       {19, "write-through payload+flag, other XCD, no sleep"},
       {25, "4 waves + barriers, write-through, other XCD, sleep"},
+      {32, "pipelined polls, plain payload+flag (XCD-local)"},
+      {40, "pipelined polls, 4 waves + barriers, plain (XCD-local)"},
+      {49, "pipelined polls, write-through, other XCD"},
   };
   for (auto& e : vs) {
     unsigned xcc[2] = {99, 99};
@@ -152,6 +181,9 @@ int main() {
       case 17: ns = run<17>(flags, pay, out, failed, iters, xcc); break;
       case 19: ns = run<19>(flags, pay, out, failed, iters, xcc); break;
       case 25: ns = run<25>(flags, pay, out, failed, iters, xcc); break;
+      case 32: ns = run<32>(flags, pay, out, failed, iters, xcc); break;
+      case 40: ns = run<40>(flags, pay, out, failed, iters, xcc); break;
+      case 49: ns = run<49>(flags, pay, out, failed, iters, xcc); break;
     }
     std::printf("variant %2d  %-55s  %8.1f ns/hop  (xcc %u / %u)\n", e.v, e.what, ns, xcc[0], xcc[1]);
   }

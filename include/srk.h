@@ -280,6 +280,12 @@ int srk_conv2d_nhwc_bwd16_dy16(const float* x, int64_t N, int64_t H, int64_t W, 
                                int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw,
                                const float* dy, const void* dy16, float* dx, float* dw, float* db, float* ws,
                                const void* x16, void* stream);
+/* The same with dw_accumulate = 1: dw is the parameter's existing .grad and the weight gradient is ADDED
+ * to it (autograd's accumulation of a returned gradient, fused into the layout kernel that writes it). */
+int srk_conv2d_nhwc_bwd16_acc(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w,
+                              int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw,
+                              const float* dy, const void* dy16, float* dx, float* dw, float* db, float* ws,
+                              const void* x16, int dw_accumulate, void* stream);
 /* Conv2d (stride 1) + bias + MaxPool2d((1, 4)) fused (model_fbanks_cnn.py:74-75,91-92: conv2 then
  * maxpool2): the implicit GEMM's epilogue pools its own output, so only the pooled activation y
  * [N][Ho][Wo/4][Co] and the uint8 window argmax [N][Ho][Wo/4][Co] (first maximum, NaN wins: the
@@ -342,6 +348,12 @@ int srk_batchnorm_fwd16(const float* x, int64_t M, int64_t C, const float* gamma
 int srk_batchnorm_bwd16(const float* x, const float* y, const float* dy, int64_t M, int64_t C, const float* gamma,
                         const float* save_mean, const float* save_invstd, int training, int relu, float* dx,
                         void* dx16, int* dx16_written, float* dgamma, float* dbeta, float* dresidual, void* stream);
+/* The same, and dgamma_acc / dbeta_acc (nullable: the parameters' existing .grad) += dgamma / dbeta
+ * (autograd's accumulation fused into the kernel that forms the sums; dgamma / dbeta stay outputs). */
+int srk_batchnorm_bwd16_acc(const float* x, const float* y, const float* dy, int64_t M, int64_t C,
+                            const float* gamma, const float* save_mean, const float* save_invstd, int training,
+                            int relu, float* dx, void* dx16, int* dx16_written, float* dgamma, float* dbeta,
+                            float* dresidual, float* dgamma_acc, float* dbeta_acc, void* stream);
 /* SyncBatchNorm pieces (torch.nn.SyncBatchNorm semantics: training statistics over the global
  * batch of all data-parallel ranks; model_resnet_bgru.py's BatchNorm1d layers under DP).  Forward:
  * srk_batchnorm_stats (this rank's count, mean, M2 per channel -> stats [3][C]), the caller gathers

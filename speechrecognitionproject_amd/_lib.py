@@ -71,6 +71,8 @@ _SIGS = {
                               _P, _P, _P, _P],
     "srk_conv2d_nhwc_bwd16_dy16": [_P, _I64, _I64, _I64, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P,
                                    _P, _P, _P, _P, _P, _P],
+    "srk_conv2d_nhwc_bwd16_acc": [_P, _I64, _I64, _I64, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P,
+                                  _P, _P, _P, _P, _P, _I, _P],
     "srk_conv2d_nhwc_fwd_pool": [_P, _I64, _I64, _I64, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P,
                                  _P, ctypes.POINTER(_I), _P],
     "srk_conv2d_nhwc_bwd_pool": [_P, _I64, _I64, _I64, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P,
@@ -85,6 +87,8 @@ _SIGS = {
     "srk_batchnorm_fwd16": [_P, _I64, _I64, _P, _P, _F, _F, _I, _P, _P, _P, _I, _P, _P, ctypes.POINTER(_I), _P, _P,
                             _P],
     "srk_batchnorm_bwd16": [_P, _P, _P, _I64, _I64, _P, _P, _P, _I, _I, _P, _P, ctypes.POINTER(_I), _P, _P, _P, _P],
+    "srk_batchnorm_bwd16_acc": [_P, _P, _P, _I64, _I64, _P, _P, _P, _I, _I, _P, _P, ctypes.POINTER(_I), _P, _P, _P,
+                                _P, _P, _P],
     "srk_batchnorm_stats": [_P, _I64, _I64, _P, _P],
     "srk_batchnorm_combine": [_P, _I, _I64, _F, _F, _P, _P, _P, _P, _P, _P],
     "srk_batchnorm_apply": [_P, _I64, _I64, _P, _P, _P, _P, _P, _I, _P, _P],

@@ -301,8 +301,11 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const float* __rest
   }
 }
 
+// acc_dbeta / acc_dgamma (nullable): the parameters' .grad buffers, which the same sums are added into
+// (autograd's accumulation fused here instead of one add kernel per parameter)
 __global__ void bn_dgamma_kernel(const float* __restrict__ p0, const float* __restrict__ p1, int chunks, int C,
-                                 float* __restrict__ dbeta, float* __restrict__ dgamma) {
+                                 float* __restrict__ dbeta, float* __restrict__ dgamma, float* __restrict__ acc_dbeta,
+                                 float* __restrict__ acc_dgamma) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float a = 0.f, b = 0.f;
@@ -324,6 +327,8 @@ __global__ void bn_dgamma_kernel(const float* __restrict__ p0, const float* __re
   }
   dbeta[c] = a;
   dgamma[c] = b;
+  if (acc_dbeta) acc_dbeta[c] += a;
+  if (acc_dgamma) acc_dgamma[c] += b;
 }
 
 template <bool I32, int LP>
@@ -523,6 +528,14 @@ int srk_batchnorm_bwd(const float* x, const float* y, const float* dy, int64_t M
 int srk_batchnorm_bwd16(const float* x, const float* y, const float* dy, int64_t M, int64_t C, const float* gamma,
                         const float* save_mean, const float* save_invstd, int training, int relu, float* dx,
                         void* dx16, int* dx16_written, float* dgamma, float* dbeta, float* dresidual, void* stream) {
+  return srk_batchnorm_bwd16_acc(x, y, dy, M, C, gamma, save_mean, save_invstd, training, relu, dx, dx16, dx16_written,
+                                 dgamma, dbeta, dresidual, nullptr, nullptr, stream);
+}
+
+int srk_batchnorm_bwd16_acc(const float* x, const float* y, const float* dy, int64_t M, int64_t C, const float* gamma,
+                            const float* save_mean, const float* save_invstd, int training, int relu, float* dx,
+                            void* dx16, int* dx16_written, float* dgamma, float* dbeta, float* dresidual,
+                            float* dgamma_acc, float* dbeta_acc, void* stream) {
   SRK_API_BEGIN
   if (dx16_written) *dx16_written = 0;
   SRK_REQUIRE(M > 0 && C > 0 && C % 4 == 0, SRK_ERR_INVALID, "batchnorm_bwd: bad shape (C % 4 == 0 required)");
@@ -537,7 +550,7 @@ int srk_batchnorm_bwd16(const float* x, const float* y, const float* dy, int64_t
   hipLaunchKernelGGL(srk::bn_bwd_partial_kernel, dim3((unsigned)((g.C4 + g.CQ - 1) / g.CQ), (unsigned)g.chunks),
                      dim3(256), 0, s, x, y, dy, g, save_mean, save_invstd, relu, part, part + (size_t)g.chunks * C);
   hipLaunchKernelGGL(srk::bn_dgamma_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
-                     part + (size_t)g.chunks * C, g.chunks, (int)C, dbeta, dgamma);
+                     part + (size_t)g.chunks * C, g.chunks, (int)C, dbeta, dgamma, dbeta_acc, dgamma_acc);
   srk::launch_dx(lp, M, (int)C, s, x, y, dy, save_mean, save_invstd, gamma, dbeta, dgamma, relu, training, (float)M,
                  nullptr, dx, dresidual, static_cast<uint16_t*>(dx16));
   SRK_CHECK_HIP(hipGetLastError());
@@ -608,7 +621,7 @@ int srk_batchnorm_bwd_reduce(const float* x, const float* y, const float* dy, in
   hipLaunchKernelGGL(srk::bn_bwd_partial_kernel, dim3((unsigned)((g.C4 + g.CQ - 1) / g.CQ), (unsigned)g.chunks),
                      dim3(256), 0, s, x, y, dy, g, save_mean, save_invstd, relu, part, part + (size_t)g.chunks * C);
   hipLaunchKernelGGL(srk::bn_dgamma_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
-                     part + (size_t)g.chunks * C, g.chunks, (int)C, sums, sums + C);
+                     part + (size_t)g.chunks * C, g.chunks, (int)C, sums, sums + C, nullptr, nullptr);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END

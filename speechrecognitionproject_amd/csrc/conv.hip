@@ -570,8 +570,9 @@ __global__ void weight_layout_kernel(const float* __restrict__ w, int Co, int Ci
 }
 
 // dWt [(kh,kw,ci)][co] -> [Co][Ci][KH][KW]
+// accumulate: dw += (the parameter's .grad, autograd's accumulation fused here) instead of dw =
 __global__ void weight_grad_layout_kernel(const float* __restrict__ dwt, int Co, int Ci, int KH, int KW,
-                                          float* __restrict__ dw) {
+                                          float* __restrict__ dw, int accumulate) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = (int64_t)Co * Ci * KH * KW;
   if (i >= n) return;
@@ -580,7 +581,8 @@ __global__ void weight_grad_layout_kernel(const float* __restrict__ dwt, int Co,
   const int kh = (int)(t % KH);
   t /= KH;
   const int ci = (int)(t % Ci), co = (int)(t / Ci);
-  dw[i] = dwt[(((int64_t)kh * KW + kw) * Ci + ci) * Co + co];
+  const float v = dwt[(((int64_t)kh * KW + kw) * Ci + ci) * Co + co];
+  dw[i] = accumulate ? dw[i] + v : v;
 }
 
 // ------------------------------------------------------------------ max pooling (NHWC)
@@ -1734,7 +1736,7 @@ namespace srk {
 int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w, int64_t Co, int64_t KH,
              int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw, const float* dy, const uint8_t* dy_arg,
              float* dx, float* dw, float* db, float* ws, const void* x16, void* stream,
-             const unsigned short* dy16 = nullptr) {
+             const unsigned short* dy16 = nullptr, int dw_accumulate = 0) {
   int64_t Ho, Wo;
   if (int rc = srk::check(N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw, &Ho, &Wo)) return rc;
   SRK_REQUIRE(x && w && (dy || dy16) && dw && ws, SRK_ERR_INVALID, "conv bwd: null pointer");
@@ -1819,7 +1821,7 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
     g.db = srk::g_opt_conv_fused_db ? db : nullptr;
     if ((rc = srk::run_conv_gemm<srk::kWgrad>(g, s, "conv_wgrad"))) return rc;
     hipLaunchKernelGGL(srk::weight_grad_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, ws,
-                       (int)Co, (int)Ci, (int)KH, (int)KW, dw);
+                       (int)Co, (int)Ci, (int)KH, (int)KW, dw, dw_accumulate);
     if (db && !db_done && (!g.db || g.a16) && (rc = srk::colsum_f32(dy, N * Ho * Wo, Co, Co, db, 0.f, s))) return rc;
   }
   SRK_CHECK_HIP(hipGetLastError());
@@ -1841,10 +1843,18 @@ int srk_conv2d_nhwc_bwd16_dy16(const float* x, int64_t N, int64_t H, int64_t W, 
                                int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw,
                                const float* dy, const void* dy16, float* dx, float* dw, float* db, float* ws,
                                const void* x16, void* stream) {
+  return srk_conv2d_nhwc_bwd16_acc(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, sh, sw, dy, dy16, dx, dw, db, ws, x16, 0,
+                                   stream);
+}
+
+int srk_conv2d_nhwc_bwd16_acc(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const float* w,
+                              int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t sh, int64_t sw,
+                              const float* dy, const void* dy16, float* dx, float* dw, float* db, float* ws,
+                              const void* x16, int dw_accumulate, void* stream) {
   SRK_API_BEGIN
   SRK_REQUIRE(dy, SRK_ERR_INVALID, "conv bwd: null pointer");
   return srk::conv_bwd(x, N, H, W, Ci, w, Co, KH, KW, ph, pw, sh, sw, dy, nullptr, dx, dw, db, ws, x16, stream,
-                       static_cast<const unsigned short*>(dy16));
+                       static_cast<const unsigned short*>(dy16), dw_accumulate ? 1 : 0);
   SRK_API_END
 }
 

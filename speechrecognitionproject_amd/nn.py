@@ -353,8 +353,13 @@ def _pair(v):
 class _Conv2dNHWCFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, padding, stride):
+        # w: the Conv2d weight [Co, Ci, KH, KW], or a Conv1d weight [Co, Ci, K] taken as [Co, Ci, 1, K] (the
+        # parameter itself either way, so the backward can accumulate into its .grad)
         x = x.contiguous()
+        w_param = w
         w = w.contiguous()
+        if w.dim() == 3:
+            w = w.unsqueeze(2)
         _check_cuda(x, w, b)
         N, H, W, Ci = x.shape
         Co, Ci2, KH, KW = w.shape
@@ -380,6 +385,7 @@ class _Conv2dNHWCFn(torch.autograd.Function):
         ctx.x16 = x16 if written.value else None
         ctx.prec = _lib.matmul_precision()
         ctx.save_for_backward(x, w)
+        ctx.w_param = w_param
         ctx.geom = (padding, stride, b is not None)
         return y
 
@@ -391,15 +397,25 @@ class _Conv2dNHWCFn(torch.autograd.Function):
         Co, _, KH, KW = w.shape
         dy = dy.contiguous()
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
-        dw = torch.empty_like(w)
+        # the weight gradient ADDED to a FlatParams-owned .grad in the layout kernel (no autograd add kernel)
+        gw = _flat_grad(ctx.w_param) if ctx.needs_input_grad[1] else None
+        dw = gw if gw is not None else torch.empty_like(w)
         db = torch.empty((Co,), device=x.device) if has_b else None
         ws = torch.empty(int(_lib.lib().srk_conv2d_workspace_floats(Ci, Co, KH, KW)), device=x.device)
         x16 = ctx.x16 if ctx.prec == _lib.matmul_precision() else None   # a copy in this precision only
         ctx.x16 = None
         dy16 = _copy16_get(dy, pop=True)   # the producing BatchNorm backward's copy of dY
-        call("srk_conv2d_nhwc_bwd16_dy16", ptr(x), N, H, W, Ci, ptr(w), Co, KH, KW, ph, pw, sh, sw, ptr(dy),
+        call("srk_conv2d_nhwc_bwd16_acc", ptr(x), N, H, W, Ci, ptr(w), Co, KH, KW, ph, pw, sh, sw, ptr(dy),
              ptr(dy16) if dy16 is not None else None, ptr(dx) if dx is not None else None, ptr(dw),
-             ptr(db) if db is not None else None, ptr(ws), ptr(x16) if x16 is not None else None, stream_ptr())
+             ptr(db) if db is not None else None, ptr(ws), ptr(x16) if x16 is not None else None,
+             1 if gw is not None else 0, stream_ptr())
+        if gw is not None:
+            red = _reducer_of(ctx.w_param)
+            if red is not None:
+                red.mark_ready([ctx.w_param])
+            dw = None
+        else:
+            dw = dw.view(ctx.w_param.shape)
         return dx, dw, db, None, None
 
 
@@ -439,7 +455,7 @@ def conv1d_nlc(x, weight, bias=None, stride=1, padding=0):
     """K6 1-D convolution of channels-last [N, L, Ci] input with an nn.Conv1d weight [Co, Ci, K]."""
     require_gpu()
     N, L, C = x.shape
-    y = _Conv2dNHWCFn.apply(x.reshape(N, 1, L, C), weight.unsqueeze(2), bias, (0, padding), (1, stride))
+    y = _Conv2dNHWCFn.apply(x.reshape(N, 1, L, C), weight, bias, (0, padding), (1, stride))
     return y.reshape(N, y.shape[2], weight.shape[0])
 
 
@@ -735,6 +751,7 @@ class _BatchNormFn(torch.autograd.Function):
         if written.value:
             _copy16_put(y, y16)
         ctx.save_for_backward(x, y, gamma, mean, invstd)
+        ctx.params = (gamma, beta)
         ctx.flags = (int(training), int(relu), residual is not None)
         return y
 
@@ -753,11 +770,22 @@ class _BatchNormFn(torch.autograd.Function):
         dx16, written = None, ctypes.c_int(0)
         if dx is not None and _copy16_wanted(C):   # dx is the producing conv's dY
             dx16 = torch.empty(dx.numel(), device=x.device, dtype=torch.int16)
-        call("srk_batchnorm_bwd16", ptr(x), ptr(y), ptr(dy), M, C, ptr(gamma), ptr(mean), ptr(invstd), training, relu,
-             ptr(dx) if dx is not None else None, ptr(dx16) if dx16 is not None else None, ctypes.byref(written),
-             ptr(dgamma), ptr(dbeta), ptr(dres) if dres is not None else None, stream_ptr())
+        # dgamma / dbeta also ADDED to FlatParams-owned .grad buffers in the kernel that forms them
+        gp, bp = ctx.params
+        gg = _flat_grad(gp) if ctx.needs_input_grad[1] else None
+        gb = _flat_grad(bp) if ctx.needs_input_grad[2] else None
+        acc = gg is not None and gb is not None
+        call("srk_batchnorm_bwd16_acc", ptr(x), ptr(y), ptr(dy), M, C, ptr(gamma), ptr(mean), ptr(invstd), training,
+             relu, ptr(dx) if dx is not None else None, ptr(dx16) if dx16 is not None else None, ctypes.byref(written),
+             ptr(dgamma), ptr(dbeta), ptr(dres) if dres is not None else None, ptr(gg) if acc else None,
+             ptr(gb) if acc else None, stream_ptr())
         if written.value:
             _copy16_put(dx, dx16)
+        if acc:
+            red = _reducer_of(gp)
+            if red is not None:
+                red.mark_ready([gp, bp])
+            return dx, None, None, dres, None, None, None, None, None, None
         return dx, dgamma, dbeta, dres, None, None, None, None, None, None
 
 

@@ -674,6 +674,32 @@ constexpr int kDcXF = 24;   // floats a lane hands its pair partner: 3 gate accu
 __device__ __forceinline__ void dc_wait(const GruPArgs& a, const unsigned* f, int step) {
   const int lane = threadIdx.x & 63;
   unsigned spins = 0;
+  if (a.poll_pipe) {   // four polls in flight (option gru_poll_pipe; lp2_wait)
+    auto poll = [&] {
+      return lane < 32 ? __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xffffffffu;
+    };
+    unsigned q0 = poll();
+    __builtin_amdgcn_s_sleep(1);
+    unsigned q1 = poll();
+    __builtin_amdgcn_s_sleep(1);
+    unsigned q2 = poll();
+    __builtin_amdgcn_s_sleep(1);
+    unsigned q3 = poll();
+    while (true) {
+      if (__all(q0 >= (unsigned)step)) return;
+      q0 = poll();
+      if (__all(q1 >= (unsigned)step)) return;
+      q1 = poll();
+      if (__all(q2 >= (unsigned)step)) return;
+      q2 = poll();
+      if (__all(q3 >= (unsigned)step)) return;
+      q3 = poll();
+      if ((spins += 4) >= a.spin_limit) {
+        if (lane == 0) spin_gave_up(a);
+        return;
+      }
+    }
+  }
   while (true) {
     const unsigned v = lane < 32 ? __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xffffffffu;
     if (__all(v >= (unsigned)step)) break;

@@ -116,7 +116,8 @@ extern int g_opt_conv_ring64;
 // BatchNorm training statistics: the 256 chunk partials combined as a fixed pairwise tree, one wave per
 // channel ("bn_tree", default 1; 0 = one lane per channel in chunk order)
 extern int g_opt_bn_tree;
-// 16-bit persistent GRU: the per-producer flag wait keeps four polls in flight ("gru_poll_pipe", default 0)
+// persistent GRU (16-bit kernels, fp32 two-chain kernels): the per-producer flag wait keeps four polls in flight
+// ("gru_poll_pipe", default 0)
 extern int g_opt_gru_poll_pipe;
 // conv tile shape ("conv_tile": 128 = 128-row tiles of 4 waves, 256 = 256-row tiles of 8 waves on
 // tall convolutions)

@@ -79,6 +79,7 @@ _SIGS = {
                                  _P, _P, _P, _P],
     "srk_conv1_pool_workspace_floats": [_I64, _I64, _I64],
     "srk_conv1_pool_fwd": [_P, _I64, _I64, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P],
+    "srk_conv1_pool_fwd16": [_P, _I64, _I64, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P],
     "srk_conv1_pool_wgrad": [_P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P],
     "srk_maxpool_nhwc_fwd": [_P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P],
     "srk_maxpool_nhwc_bwd": [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P],

@@ -1863,6 +1863,7 @@ int srk_conv2d_nhwc_fwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
                              int64_t pool_w, float* y, uint8_t* argmax, float* ws, void* x16, int* x16_written,
                              void* stream) {
   SRK_API_BEGIN
+  const bool x16_ready = x16 && x16_written && *x16_written == 2;   // the producer's copy (srk_conv1_pool_fwd16)
   if (x16_written) *x16_written = 0;
   int64_t Ho, Wo;
   if (int rc = srk::check(N, H, W, Ci, Co, KH, KW, ph, pw, 1, 1, &Ho, &Wo)) return rc;
@@ -1885,7 +1886,8 @@ int srk_conv2d_nhwc_fwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
     const float* src[2] = {x, ws};
     const int64_t n[2] = {N * H * W * Ci, nw};
     unsigned short* d16[2] = {static_cast<unsigned short*>(x16), nullptr};
-    if (int rc = srk::to16_all(prec, src, n, 2, d16, s)) return rc;
+    const bool ready[2] = {x16_ready, false};
+    if (int rc = srk::to16_all(prec, src, n, 2, d16, s, ready)) return rc;
     c.a16 = d16[0];
     c.b16 = d16[1];
     if (x16 && x16_written) *x16_written = 1;

@@ -39,7 +39,12 @@ struct C1Args {
   uint8_t* arg;        // [N][H][W/PW][64] window argmax
   const float* dy;     // bwd: pooled gradient [N][H][W/PW][64]
   float* partial;      // bwd: [blocks][64 * (KH*KW + 1)]
+  unsigned short* y16; // fwd (16-bit matmul modes, optional): the pooled activation's 16-bit operand copy
 };
+
+typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2c __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ bool takes(float v, float m, bool first) { return first || v > m || (v != v && m == m); }
 
@@ -55,7 +60,9 @@ __device__ __forceinline__ void load_patch(const C1Args& a, int n, int h0, float
   }
 }
 
-template <int KH, int KW, int PW>
+// LP: 0 fp32 output only; 1 / 2 also the bf16 / fp16 copy of it (RNE, the conversion srk's to16 makes), which
+// conv2's 16-bit implicit GEMMs read instead of converting the 514 MB fp32 activation again
+template <int KH, int KW, int PW, int LP>
 __global__ __launch_bounds__(256) void conv1_pool_fwd_kernel(C1Args a) {
   constexpr int T = KH * KW;
   extern __shared__ float patch[];
@@ -100,6 +107,8 @@ __global__ __launch_bounds__(256) void conv1_pool_fwd_kernel(C1Args a) {
     const size_t o = (((size_t)n * a.H + h0 + r) * Wq + wq) * kCo + c4 * 4;
     *reinterpret_cast<v4f*>(a.y + o) = best;
     *reinterpret_cast<unsigned*>(a.arg + o) = idx;
+    if (LP == 1) *reinterpret_cast<u32x2c*>(a.y16 + o) = __builtin_bit_cast(u32x2c, __builtin_convertvector(best, bf4));
+    if (LP == 2) *reinterpret_cast<u32x2c*>(a.y16 + o) = __builtin_bit_cast(u32x2c, __builtin_convertvector(best, h4));
   }
 }
 
@@ -229,23 +238,42 @@ int64_t srk_conv1_pool_workspace_floats(int64_t Co, int64_t KH, int64_t KW) {
 int srk_conv1_pool_fwd(const float* x, int64_t N, int64_t H, int64_t W, const float* w, const float* bias, int64_t Co,
                        int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t pool, float* y, uint8_t* argmax,
                        void* stream) {
+  return srk_conv1_pool_fwd16(x, N, H, W, w, bias, Co, KH, KW, ph, pw, pool, y, argmax, nullptr, nullptr, stream);
+}
+
+int srk_conv1_pool_fwd16(const float* x, int64_t N, int64_t H, int64_t W, const float* w, const float* bias,
+                         int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t pool, float* y,
+                         uint8_t* argmax, void* y16, int* y16_written, void* stream) {
   SRK_API_BEGIN
+  if (y16_written) *y16_written = 0;
   if (int rc = srk::check_c1(N, H, W, Co, KH, KW, ph, pw, pool)) return rc;
   SRK_REQUIRE(x && w && bias && y && argmax, SRK_ERR_INVALID, "conv1_pool_fwd: null pointer");
-  SRK_REQUIRE((uintptr_t)y % 16 == 0 && (uintptr_t)argmax % 4 == 0, SRK_ERR_INVALID, "conv1_pool_fwd: misaligned output");
+  SRK_REQUIRE((uintptr_t)y % 16 == 0 && (uintptr_t)argmax % 4 == 0 && (uintptr_t)y16 % 8 == 0, SRK_ERR_INVALID,
+              "conv1_pool_fwd: misaligned output");
+  const int prec = srk::matmul_prec();
+  const int lp = y16 && prec != srk::kPrecF32 ? (prec == srk::kPrecBF16 ? 1 : 2) : 0;
   srk::C1Args a{};
   a.N = (int)N; a.H = (int)H; a.W = (int)W; a.ph = (int)ph; a.pw = (int)pw;
   a.x = x; a.w = w; a.bias = bias; a.y = y; a.arg = argmax;
+  a.y16 = static_cast<unsigned short*>(y16);
   hipStream_t s = srk::as_stream(stream);
   const int hp = (int)((H + srk::kRows - 1) / srk::kRows);
   const size_t lds = (size_t)(srk::kRows + KH - 1) * (W + KW) * 4;
-  // algorithmic: the input image once + pooled output + argmax
-  srk::ProfScope prof("conv1_pool_fwd", s, 4.0 * N * H * W + 5.0 * N * H * (W / pool) * Co);
-  if (KH == 7)
-    hipLaunchKernelGGL((srk::conv1_pool_fwd_kernel<7, 3, 3>), dim3((unsigned)(N * hp)), dim3(256), lds, s, a);
-  else
-    hipLaunchKernelGGL((srk::conv1_pool_fwd_kernel<3, 7, 5>), dim3((unsigned)(N * hp)), dim3(256), lds, s, a);
+  // algorithmic: the input image once + pooled output + argmax (+ the 16-bit copy)
+  srk::ProfScope prof("conv1_pool_fwd", s, 4.0 * N * H * W + (lp ? 7.0 : 5.0) * N * H * (W / pool) * Co);
+  const dim3 g((unsigned)(N * hp));
+#define SRK_C1F(KH_, KW_, PW_)                                                                              \
+  if (lp == 1) hipLaunchKernelGGL((srk::conv1_pool_fwd_kernel<KH_, KW_, PW_, 1>), g, dim3(256), lds, s, a); \
+  else if (lp == 2) hipLaunchKernelGGL((srk::conv1_pool_fwd_kernel<KH_, KW_, PW_, 2>), g, dim3(256), lds, s, a); \
+  else hipLaunchKernelGGL((srk::conv1_pool_fwd_kernel<KH_, KW_, PW_, 0>), g, dim3(256), lds, s, a);
+  if (KH == 7) {
+    SRK_C1F(7, 3, 3)
+  } else {
+    SRK_C1F(3, 7, 5)
+  }
+#undef SRK_C1F
   SRK_CHECK_HIP(hipGetLastError());
+  if (lp && y16_written) *y16_written = 1;
   return SRK_OK;
   SRK_API_END
 }

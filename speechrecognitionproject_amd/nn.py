@@ -471,8 +471,16 @@ class _Conv1PoolFn(torch.autograd.Function):
         Co, _, KH, KW = w.shape
         y = torch.empty((N, H, W // pool, Co), device=x.device)
         arg = torch.empty((N, H, W // pool, Co), device=x.device, dtype=torch.uint8)
-        call("srk_conv1_pool_fwd", ptr(x), N, H, W, ptr(w.contiguous()), ptr(b), Co, KH, KW, padding[0], padding[1],
-             pool, ptr(y), ptr(arg), stream_ptr())
+        # training steps in a 16-bit mode: the kernel also writes y's 16-bit operand copy, which conv2's
+        # fused conv + pool takes as ready (no second pass over the fp32 activation)
+        y16 = None
+        if _copy16_wanted(Co) and torch.is_grad_enabled() and ctx.needs_input_grad[1]:
+            y16 = torch.empty(y.numel(), device=x.device, dtype=torch.int16)
+        written = ctypes.c_int(0)
+        call("srk_conv1_pool_fwd16", ptr(x), N, H, W, ptr(w.contiguous()), ptr(b), Co, KH, KW, padding[0], padding[1],
+             pool, ptr(y), ptr(arg), ptr(y16) if y16 is not None else None, ctypes.byref(written), stream_ptr())
+        if written.value:
+            _copy16_put(y, y16)
         ctx.save_for_backward(x, arg)
         ctx.geom = (Co, KH, KW, padding, pool)
         return y
@@ -521,8 +529,12 @@ class _ConvPoolNHWCFn(torch.autograd.Function):
         arg = torch.empty((N, Ho, Wo // pool_w, Co), device=x.device, dtype=torch.uint8)
         ws = torch.empty(int(_lib.lib().srk_conv2d_workspace_floats(Ci, Co, KH, KW)), device=x.device)
         x16, written = None, ctypes.c_int(0)
-        if _lib.matmul_precision() != "fp32" and Ci % 8 == 0 and Co % 8 == 0 and ctx.needs_input_grad[1]:
-            x16 = torch.empty(x.numel(), device=x.device, dtype=torch.int16)
+        if _lib.matmul_precision() != "fp32" and Ci % 8 == 0 and Co % 8 == 0:
+            x16 = _copy16_get(x, pop=True)   # the producing srk_conv1_pool_fwd16's copy (written = 2: ready)
+            if x16 is not None:
+                written.value = 2
+            elif ctx.needs_input_grad[1]:
+                x16 = torch.empty(x.numel(), device=x.device, dtype=torch.int16)
         call("srk_conv2d_nhwc_fwd_pool", ptr(x), N, H, W, Ci, ptr(w), ptr(b) if b is not None else None, Co, KH, KW,
              ph, pw, pool_w, ptr(y), ptr(arg), ptr(ws), ptr(x16) if x16 is not None else None, ctypes.byref(written),
              stream_ptr())

@@ -1,5 +1,11 @@
 """Conv micro-benchmark: fwd / dgrad / wgrad of the model_fbanks_cnn layers (B = 512) and the
-model_resnet_bgru stage convs (B = 512), timed with srk_prof events (algorithmic flops / time)."""
+model_resnet_bgru stage convs (B = 512), timed with srk_prof events (algorithmic flops / time).
+
+    python tools/conv_bench.py [--prec bf16] [--only fb_conv2,rn_l1] [--var "" --var "conv_ring64=0" ...]
+
+Each --var is a comma-separated srk option list applied with srk_set_option before the shape runs; options
+stay set afterwards, so give every variant the full list it compares (e.g. "conv_ring64=1" / "conv_ring64=0"); fb_conv2 runs as the fused conv + (1, 4) max pool model_fbanks_cnn uses."""
+import argparse
 import json
 import os
 import sys
@@ -19,21 +25,62 @@ SHAPES = {  # name: N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw
     "rn_l2": (512, 1, 500, 128, 128, 1, 15, 0, 7, 1, 1),
     "rn_l4": (512, 1, 125, 512, 512, 1, 15, 0, 7, 1, 1),
 }
-res = {}
-for name, (N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw) in SHAPES.items():
+CATS = ("conv_fwd", "conv_dgrad", "conv_wgrad", "conv_fwd_lp", "conv_dgrad_lp", "conv_wgrad_lp", "conv_to16",
+        "conv_colsum")
+
+
+def parse_opts(s):
+    out = []
+    for kv in filter(None, (t.strip() for t in s.split(","))):
+        k, v = kv.split("=")
+        out.append((k, int(v)))
+    return out
+
+
+def run_shape(name, prec, opts):
+    N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw = SHAPES[name]
     x = torch.randn(N, H, W, Ci, device="cuda", requires_grad=Ci > 1)
     w = (torch.randn(Co, Ci, KH, KW, device="cuda") * 0.05).requires_grad_(True)
     b = torch.zeros(Co, device="cuda", requires_grad=True)
-    for it in range(3):
-        if it == 2:
-            _lib.prof_enable(True)
-        y = snn._Conv2dNHWCFn.apply(x, w, b, (ph, pw), (sh, sw))
-        y.backward(torch.ones_like(y))
-    r = {}
-    for k in ("conv_fwd", "conv_dgrad", "conv_wgrad"):
-        c, ms, fl = _lib.prof_read(k)
-        if c:
-            r[k] = {"us": round(ms / c * 1e3, 1), "TF": round(fl / (ms * 1e-3) / 1e12, 1)}
-    _lib.prof_enable(False)
-    res[name] = r
-    print(name, json.dumps(r), flush=True)
+    pooled = name == "fb_conv2"
+    _lib.set_matmul_precision(prec)
+    for k, v in opts:
+        _lib.set_option(k, v)
+    try:
+        r = {}
+        for it in range(4):
+            if it == 3:
+                _lib.prof_enable(True)
+            if pooled:
+                y = snn._ConvPoolNHWCFn.apply(x, w, b, (ph, pw), 4)
+            else:
+                y = snn._Conv2dNHWCFn.apply(x, w, b, (ph, pw), (sh, sw))
+            y.backward(torch.ones_like(y))
+        torch.cuda.synchronize()
+        for k in CATS:
+            c, ms, work = _lib.prof_read(k)
+            if c:
+                unit = "GB/s" if k in ("conv_to16", "conv_colsum") else "TF"
+                r[k] = {"us": round(ms * 1e3, 1), unit: round(work / (ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12), 1)}
+        r["kernels"] = [{"kernel": e["kernel"], "us": round(e["ms_total"] * 1e3, 1)} for e in _lib.prof_kernels()]
+        _lib.prof_enable(False)
+        return r
+    finally:
+        _lib.set_matmul_precision("fp32")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--prec", default="fp32")
+    ap.add_argument("--only", default="")
+    ap.add_argument("--var", action="append", default=None)
+    a = ap.parse_args()
+    names = [n for n in SHAPES if not a.only or n in a.only.split(",")]
+    for var in a.var or [""]:
+        for name in names:
+            r = run_shape(name, a.prec, parse_opts(var))
+            print(json.dumps({"shape": name, "prec": a.prec, "opts": var, **r}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -360,6 +360,17 @@ int srk_batchnorm_bwd16_acc(const float* x, const float* y, const float* dy, int
                             const float* gamma, const float* save_mean, const float* save_invstd, int training,
                             int relu, float* dx, void* dx16, int* dx16_written, float* dgamma, float* dbeta,
                             float* dresidual, float* dgamma_acc, float* dbeta_acc, void* stream);
+/* The ReLU as bits: with relu set, fwd16_mask also writes relu_mask (M*C/4 bytes; byte i holds bit e = y[4i+e] > 0,
+ * nullable), and bwd16_mask takes that mask in place of y (y may then be null) — the backward's two reads of the
+ * ReLU pattern are 1/16 of y's bytes.  Otherwise as fwd16 / bwd16_acc, whose results they equal bit for bit. */
+int srk_batchnorm_fwd16_mask(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta, float eps,
+                             float momentum, int training, float* running_mean, float* running_var,
+                             const float* residual, int relu, float* y, void* y16, int* y16_written,
+                             uint8_t* relu_mask, float* save_mean, float* save_invstd, void* stream);
+int srk_batchnorm_bwd16_mask(const float* x, const float* y, const uint8_t* relu_mask, const float* dy, int64_t M,
+                             int64_t C, const float* gamma, const float* save_mean, const float* save_invstd,
+                             int training, int relu, float* dx, void* dx16, int* dx16_written, float* dgamma,
+                             float* dbeta, float* dresidual, float* dgamma_acc, float* dbeta_acc, void* stream);
 /* SyncBatchNorm pieces (torch.nn.SyncBatchNorm semantics: training statistics over the global
  * batch of all data-parallel ranks; model_resnet_bgru.py's BatchNorm1d layers under DP).  Forward:
  * srk_batchnorm_stats (this rank's count, mean, M2 per channel -> stats [3][C]), the caller gathers

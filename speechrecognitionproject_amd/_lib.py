@@ -90,6 +90,10 @@ _SIGS = {
     "srk_batchnorm_bwd16": [_P, _P, _P, _I64, _I64, _P, _P, _P, _I, _I, _P, _P, ctypes.POINTER(_I), _P, _P, _P, _P],
     "srk_batchnorm_bwd16_acc": [_P, _P, _P, _I64, _I64, _P, _P, _P, _I, _I, _P, _P, ctypes.POINTER(_I), _P, _P, _P,
                                 _P, _P, _P],
+    "srk_batchnorm_fwd16_mask": [_P, _I64, _I64, _P, _P, _F, _F, _I, _P, _P, _P, _I, _P, _P, ctypes.POINTER(_I), _P,
+                                 _P, _P, _P],
+    "srk_batchnorm_bwd16_mask": [_P, _P, _P, _P, _I64, _I64, _P, _P, _P, _I, _I, _P, _P, ctypes.POINTER(_I), _P, _P,
+                                 _P, _P, _P, _P],
     "srk_batchnorm_stats": [_P, _I64, _I64, _P, _P],
     "srk_batchnorm_combine": [_P, _I, _I64, _F, _F, _P, _P, _P, _P, _P, _P],
     "srk_batchnorm_apply": [_P, _I64, _I64, _P, _P, _P, _P, _P, _I, _P, _P],

@@ -226,7 +226,7 @@ template <bool I32, int LP>
 __global__ void bn_apply_kernel(const float* __restrict__ x, int64_t M, int C, const float* __restrict__ mean,
                                 const float* __restrict__ invstd, const float* __restrict__ gamma,
                                 const float* __restrict__ beta, const float* __restrict__ residual, int relu,
-                                float* __restrict__ y, uint16_t* __restrict__ y16) {
+                                float* __restrict__ y, uint16_t* __restrict__ y16, uint8_t* __restrict__ mask) {
   const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i4 * 4 >= M * C) return;
   const int c = chan_of<I32>(i4 * 4, C);
@@ -234,8 +234,13 @@ __global__ void bn_apply_kernel(const float* __restrict__ x, int64_t M, int C, c
   v4f v = (ld4(x + i4 * 4) - mu) * is * ga + be;
   if (residual) v += ld4(residual + i4 * 4);
   if (relu) {
+    unsigned bits = 0;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+    for (int e = 0; e < 4; ++e) {
+      bits |= (v[e] > 0.f ? 1u : 0u) << e;   // y > 0 exactly (NaN -> 0, as the ReLU below)
+      v[e] = v[e] > 0.f ? v[e] : 0.f;
+    }
+    if (mask) mask[i4] = (uint8_t)bits;
   }
   st4(y + i4 * 4, v);
   if constexpr (LP != 0) st4_16<LP>(y16 + i4 * 4, v);
@@ -251,6 +256,7 @@ __global__ void bn_eval_stats_kernel(const float* __restrict__ rm, const float* 
 
 // Backward partials: per chunk and channel, sum g and sum g * xhat, g = dy * act'(y).
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                             const uint8_t* __restrict__ mask,
                                                              const float* __restrict__ dy, BnGeom g,
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ invstd, int relu,
@@ -265,19 +271,24 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const float* __rest
     const v4f mu = ld4(mean + c4 * 4), is = ld4(invstd + c4 * 4);
     for (int64_t r = r0 + rp; r < r1; r += kUnroll * g.RP) {
       v4f vd[kUnroll], vy[kUnroll], vx[kUnroll];
+      unsigned mb[kUnroll];
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int64_t ru = r + u * g.RP;
         const int64_t o = (ru < r1 ? ru : r) * g.C + c4 * 4;
         vd[u] = ld4(dy + o);
-        if (relu) vy[u] = ld4(y + o);
+        if (relu && mask) mb[u] = mask[o >> 2];
+        else if (relu) vy[u] = ld4(y + o);
         vx[u] = ld4(x + o);
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         if (r + u * g.RP < r1) {
           v4f gr = vd[u];
-          if (relu) {
+          if (relu && mask) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) gr[e] = (mb[u] >> e) & 1u ? gr[e] : 0.f;
+          } else if (relu) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) gr[e] = vy[u][e] <= 0.f ? 0.f : gr[e];
           }
@@ -332,7 +343,8 @@ __global__ void bn_dgamma_kernel(const float* __restrict__ p0, const float* __re
 }
 
 template <bool I32, int LP>
-__global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ dy,
+__global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restrict__ y, const uint8_t* __restrict__ mask,
+                             const float* __restrict__ dy,
                              int64_t M, int C, const float* __restrict__ mean, const float* __restrict__ invstd,
                              const float* __restrict__ gamma, const float* __restrict__ dbeta,
                              const float* __restrict__ dgamma, int relu, int train, float m_norm,
@@ -343,7 +355,11 @@ __global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restric
   const int64_t o = i4 * 4;
   const int c = chan_of<I32>(o, C);
   v4f gr = ld4(dy + o);
-  if (relu) {
+  if (relu && mask) {   // the forward's ReLU bits (srk_batchnorm_fwd16_mask): 1/16 of y's bytes
+    const unsigned mb = mask[i4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gr[e] = (mb >> e) & 1u ? gr[e] : 0.f;
+  } else if (relu) {
     const v4f yv = ld4(y + o);
 #pragma unroll
     for (int e = 0; e < 4; ++e) gr[e] = yv[e] <= 0.f ? 0.f : gr[e];
@@ -431,33 +447,36 @@ int bn_scratch(size_t floats, float** out) {
 // the element kernels by index width (32-bit channel arithmetic below 2^32 elements) and 16-bit copy
 template <int LP>
 void launch_apply_lp(int64_t M, int C, hipStream_t s, const float* x, const float* mean, const float* invstd,
-                     const float* gamma, const float* beta, const float* residual, int relu, float* y, uint16_t* y16) {
+                     const float* gamma, const float* beta, const float* residual, int relu, float* y, uint16_t* y16,
+                     uint8_t* mask) {
   const int64_t n4 = M * C / 4;
   hipLaunchKernelGGL((M * C < (1LL << 32) ? bn_apply_kernel<true, LP> : bn_apply_kernel<false, LP>),
                      dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, M, C, mean, invstd, gamma, beta, residual,
-                     relu, y, y16);
+                     relu, y, y16, mask);
 }
 void launch_apply(int LP, int64_t M, int C, hipStream_t s, const float* x, const float* mean, const float* invstd,
-                  const float* gamma, const float* beta, const float* residual, int relu, float* y, uint16_t* y16) {
-  if (LP == 1) launch_apply_lp<1>(M, C, s, x, mean, invstd, gamma, beta, residual, relu, y, y16);
-  else if (LP == 2) launch_apply_lp<2>(M, C, s, x, mean, invstd, gamma, beta, residual, relu, y, y16);
-  else launch_apply_lp<0>(M, C, s, x, mean, invstd, gamma, beta, residual, relu, y, nullptr);
+                  const float* gamma, const float* beta, const float* residual, int relu, float* y, uint16_t* y16,
+                  uint8_t* mask = nullptr) {
+  if (LP == 1) launch_apply_lp<1>(M, C, s, x, mean, invstd, gamma, beta, residual, relu, y, y16, mask);
+  else if (LP == 2) launch_apply_lp<2>(M, C, s, x, mean, invstd, gamma, beta, residual, relu, y, y16, mask);
+  else launch_apply_lp<0>(M, C, s, x, mean, invstd, gamma, beta, residual, relu, y, nullptr, mask);
 }
 template <int LP>
-void launch_dx_lp(int64_t M, int C, hipStream_t s, const float* x, const float* y, const float* dy, const float* mean,
-                  const float* invstd, const float* gamma, const float* dbeta, const float* dgamma, int relu, int train,
-                  float m_norm, const float* m_norm_dev, float* dx, float* dres, uint16_t* dx16) {
+void launch_dx_lp(int64_t M, int C, hipStream_t s, const float* x, const float* y, const uint8_t* mask, const float* dy,
+                  const float* mean, const float* invstd, const float* gamma, const float* dbeta, const float* dgamma,
+                  int relu, int train, float m_norm, const float* m_norm_dev, float* dx, float* dres, uint16_t* dx16) {
   const int64_t n4 = M * C / 4;
   hipLaunchKernelGGL((M * C < (1LL << 32) ? bn_dx_kernel<true, LP> : bn_dx_kernel<false, LP>),
-                     dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, y, dy, M, C, mean, invstd, gamma, dbeta,
-                     dgamma, relu, train, m_norm, m_norm_dev, dx, dres, dx16);
+                     dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, y, mask, dy, M, C, mean, invstd, gamma,
+                     dbeta, dgamma, relu, train, m_norm, m_norm_dev, dx, dres, dx16);
 }
-void launch_dx(int LP, int64_t M, int C, hipStream_t s, const float* x, const float* y, const float* dy,
-               const float* mean, const float* invstd, const float* gamma, const float* dbeta, const float* dgamma,
-               int relu, int train, float m_norm, const float* m_norm_dev, float* dx, float* dres, uint16_t* dx16) {
-  if (LP == 1) launch_dx_lp<1>(M, C, s, x, y, dy, mean, invstd, gamma, dbeta, dgamma, relu, train, m_norm, m_norm_dev, dx, dres, dx16);
-  else if (LP == 2) launch_dx_lp<2>(M, C, s, x, y, dy, mean, invstd, gamma, dbeta, dgamma, relu, train, m_norm, m_norm_dev, dx, dres, dx16);
-  else launch_dx_lp<0>(M, C, s, x, y, dy, mean, invstd, gamma, dbeta, dgamma, relu, train, m_norm, m_norm_dev, dx, dres, nullptr);
+void launch_dx(int LP, int64_t M, int C, hipStream_t s, const float* x, const float* y, const uint8_t* mask,
+               const float* dy, const float* mean, const float* invstd, const float* gamma, const float* dbeta,
+               const float* dgamma, int relu, int train, float m_norm, const float* m_norm_dev, float* dx, float* dres,
+               uint16_t* dx16) {
+  if (LP == 1) launch_dx_lp<1>(M, C, s, x, y, mask, dy, mean, invstd, gamma, dbeta, dgamma, relu, train, m_norm, m_norm_dev, dx, dres, dx16);
+  else if (LP == 2) launch_dx_lp<2>(M, C, s, x, y, mask, dy, mean, invstd, gamma, dbeta, dgamma, relu, train, m_norm, m_norm_dev, dx, dres, dx16);
+  else launch_dx_lp<0>(M, C, s, x, y, mask, dy, mean, invstd, gamma, dbeta, dgamma, relu, train, m_norm, m_norm_dev, dx, dres, nullptr);
 }
 
 // 16-bit copy requested and possible: the matmul precision's type (1 bf16, 2 fp16), else 0
@@ -483,6 +502,14 @@ int srk_batchnorm_fwd16(const float* x, int64_t M, int64_t C, const float* gamma
                         float momentum, int training, float* running_mean, float* running_var, const float* residual,
                         int relu, float* y, void* y16, int* y16_written, float* save_mean, float* save_invstd,
                         void* stream) {
+  return srk_batchnorm_fwd16_mask(x, M, C, gamma, beta, eps, momentum, training, running_mean, running_var, residual,
+                                  relu, y, y16, y16_written, nullptr, save_mean, save_invstd, stream);
+}
+
+int srk_batchnorm_fwd16_mask(const float* x, int64_t M, int64_t C, const float* gamma, const float* beta, float eps,
+                             float momentum, int training, float* running_mean, float* running_var,
+                             const float* residual, int relu, float* y, void* y16, int* y16_written,
+                             uint8_t* relu_mask, float* save_mean, float* save_invstd, void* stream) {
   SRK_API_BEGIN
   if (y16_written) *y16_written = 0;
   SRK_REQUIRE(M > 0 && C > 0 && C <= (1 << 24), SRK_ERR_INVALID, "batchnorm: bad shape");
@@ -491,7 +518,9 @@ int srk_batchnorm_fwd16(const float* x, int64_t M, int64_t C, const float* gamma
               "batchnorm: null pointer");
   hipStream_t s = srk::as_stream(stream);
   const int lp = srk::copy16_type(y16);
-  srk::ProfScope prof("batchnorm_fwd", s, ((training ? 12.0 : 8.0) + (lp ? 2.0 : 0.0)) * (double)M * C);
+  const bool mk = relu && relu_mask;
+  srk::ProfScope prof("batchnorm_fwd", s,
+                      ((training ? 12.0 : 8.0) + (lp ? 2.0 : 0.0) + (mk ? 0.25 : 0.0)) * (double)M * C);
   const srk::BnGeom g = srk::bn_geom(M, (int)C);
   if (training) {
     float* part = nullptr;
@@ -511,7 +540,7 @@ int srk_batchnorm_fwd16(const float* x, int64_t M, int64_t C, const float* gamma
                        running_var, (int)C, eps, save_mean, save_invstd);
   }
   srk::launch_apply(lp, M, (int)C, s, x, save_mean, save_invstd, gamma, beta, residual, relu, y,
-                    static_cast<uint16_t*>(y16));
+                    static_cast<uint16_t*>(y16), mk ? relu_mask : nullptr);
   SRK_CHECK_HIP(hipGetLastError());
   if (lp && y16_written) *y16_written = 1;
   return SRK_OK;
@@ -536,23 +565,33 @@ int srk_batchnorm_bwd16_acc(const float* x, const float* y, const float* dy, int
                             const float* save_mean, const float* save_invstd, int training, int relu, float* dx,
                             void* dx16, int* dx16_written, float* dgamma, float* dbeta, float* dresidual,
                             float* dgamma_acc, float* dbeta_acc, void* stream) {
+  return srk_batchnorm_bwd16_mask(x, y, nullptr, dy, M, C, gamma, save_mean, save_invstd, training, relu, dx, dx16,
+                                  dx16_written, dgamma, dbeta, dresidual, dgamma_acc, dbeta_acc, stream);
+}
+
+int srk_batchnorm_bwd16_mask(const float* x, const float* y, const uint8_t* relu_mask, const float* dy, int64_t M,
+                             int64_t C, const float* gamma, const float* save_mean, const float* save_invstd,
+                             int training, int relu, float* dx, void* dx16, int* dx16_written, float* dgamma,
+                             float* dbeta, float* dresidual, float* dgamma_acc, float* dbeta_acc, void* stream) {
   SRK_API_BEGIN
   if (dx16_written) *dx16_written = 0;
   SRK_REQUIRE(M > 0 && C > 0 && C % 4 == 0, SRK_ERR_INVALID, "batchnorm_bwd: bad shape (C % 4 == 0 required)");
-  SRK_REQUIRE(x && y && dy && gamma && save_mean && save_invstd && dgamma && dbeta, SRK_ERR_INVALID,
-              "batchnorm_bwd: null pointer");
+  SRK_REQUIRE(x && (y || (relu && relu_mask)) && dy && gamma && save_mean && save_invstd && dgamma && dbeta,
+              SRK_ERR_INVALID, "batchnorm_bwd: null pointer");
   hipStream_t s = srk::as_stream(stream);
   const int lp = dx ? srk::copy16_type(dx16) : 0;
-  srk::ProfScope prof("batchnorm_bwd", s, (16.0 + (lp ? 2.0 : 0.0)) * (double)M * C);
+  const uint8_t* mk = relu ? relu_mask : nullptr;
+  // algorithmic bytes: x, dy and y (or its mask bits) read twice, dx written (+ its 16-bit copy)
+  srk::ProfScope prof("batchnorm_bwd", s, ((mk ? 12.5 : 16.0) + (lp ? 2.0 : 0.0)) * (double)M * C);
   const srk::BnGeom g = srk::bn_geom(M, (int)C);
   float* part = nullptr;
   if (int rc = srk::bn_scratch((size_t)2 * g.chunks * C, &part)) return rc;
   hipLaunchKernelGGL(srk::bn_bwd_partial_kernel, dim3((unsigned)((g.C4 + g.CQ - 1) / g.CQ), (unsigned)g.chunks),
-                     dim3(256), 0, s, x, y, dy, g, save_mean, save_invstd, relu, part, part + (size_t)g.chunks * C);
+                     dim3(256), 0, s, x, y, mk, dy, g, save_mean, save_invstd, relu, part, part + (size_t)g.chunks * C);
   hipLaunchKernelGGL(srk::bn_dgamma_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
                      part + (size_t)g.chunks * C, g.chunks, (int)C, dbeta, dgamma, dbeta_acc, dgamma_acc);
-  srk::launch_dx(lp, M, (int)C, s, x, y, dy, save_mean, save_invstd, gamma, dbeta, dgamma, relu, training, (float)M,
-                 nullptr, dx, dresidual, static_cast<uint16_t*>(dx16));
+  srk::launch_dx(lp, M, (int)C, s, x, y, mk, dy, save_mean, save_invstd, gamma, dbeta, dgamma, relu, training,
+                 (float)M, nullptr, dx, dresidual, static_cast<uint16_t*>(dx16));
   SRK_CHECK_HIP(hipGetLastError());
   if (lp && dx16_written) *dx16_written = 1;
   return SRK_OK;
@@ -619,7 +658,8 @@ int srk_batchnorm_bwd_reduce(const float* x, const float* y, const float* dy, in
   float* part = nullptr;
   if (int rc = srk::bn_scratch((size_t)2 * g.chunks * C, &part)) return rc;
   hipLaunchKernelGGL(srk::bn_bwd_partial_kernel, dim3((unsigned)((g.C4 + g.CQ - 1) / g.CQ), (unsigned)g.chunks),
-                     dim3(256), 0, s, x, y, dy, g, save_mean, save_invstd, relu, part, part + (size_t)g.chunks * C);
+                     dim3(256), 0, s, x, y, nullptr, dy, g, save_mean, save_invstd, relu, part,
+                     part + (size_t)g.chunks * C);
   hipLaunchKernelGGL(srk::bn_dgamma_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
                      part + (size_t)g.chunks * C, g.chunks, (int)C, sums, sums + C, nullptr, nullptr);
   SRK_CHECK_HIP(hipGetLastError());
@@ -637,8 +677,8 @@ int srk_batchnorm_bwd_dx(const float* x, const float* y, const float* dy, int64_
               SRK_ERR_INVALID, "batchnorm_bwd_dx: null pointer");
   hipStream_t s = srk::as_stream(stream);
   srk::ProfScope prof("batchnorm_bwd", s, 16.0 * (double)M * C);
-  srk::launch_dx(0, M, (int)C, s, x, y, dy, save_mean, save_invstd, gamma, sums, sums + C, relu, 1, 0.f, total_count,
-                 dx, dresidual, nullptr);
+  srk::launch_dx(0, M, (int)C, s, x, y, nullptr, dy, save_mean, save_invstd, gamma, sums, sums + C, relu, 1, 0.f,
+                 total_count, dx, dresidual, nullptr);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
   SRK_API_END

@@ -1245,7 +1245,10 @@ __device__ __forceinline__ u32x4_ r16_frag(const unsigned short* img, int r0, in
   return u32x4_{l2.x, l2.y, h2.x, h2.y};
 }
 
-template <int MODE, int BN, int LP>
+// QS: k-steps (16 deep) per MFMA section, as gemm_g16_kernel's: 1 = a barrier pair per k-step (BN / 32
+// MFMAs per wave between barriers: 2 at BN = 64), 2 = the whole 32-deep K-tile per section (twice the
+// MFMAs per barrier pair, both DMAs issued in the one load section) — option conv_ring_qs
+template <int MODE, int BN, int LP, int QS = 1>
 __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
   constexpr int BK = kR16BK, NST = 4;
   constexpr bool AKC = MODE != kWgrad;
@@ -1397,25 +1400,37 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
     const unsigned short* As = S + grp * HALF;
     const unsigned short* Bs = S + (2 + bh) * HALF;
     const int tn_ = kt + NST - 1;
+    static_assert(QS == 1 || QS == 2, "ring16: 1 or 2 k-steps per section");
 #pragma unroll
-    for (int q = 0; q < BK / 16; ++q) {
-      u32x4_ fa[TM], fb[TN];
+    for (int q = 0; q < BK / 16; q += QS) {
+      u32x4_ fa[QS][TM], fb[QS][TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa[i] = r16_frag<AKC>(As, ar0 + i * 32, 16 * q, lane);
+      for (int e = 0; e < QS; ++e) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = r16_frag<false>(Bs, bc0 + j * 32, 16 * q, lane);
-      if (tn_ < nk) {
-        if (q == 0) dma_a(tn_);
-        else dma_b(tn_);
+        for (int i = 0; i < TM; ++i) fa[e][i] = r16_frag<AKC>(As, ar0 + i * 32, 16 * (q + e), lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[e][j] = r16_frag<false>(Bs, bc0 + j * 32, 16 * (q + e), lane);
       }
-      if (q == BK / 16 - 1) retire_keep(min(nk - 1 - (kt + 1), NST - 2));
+      if (tn_ < nk) {
+        if (QS == 2) {
+          dma_a(tn_);
+          dma_b(tn_);
+        } else if (q == 0) {
+          dma_a(tn_);
+        } else {
+          dma_b(tn_);
+        }
+      }
+      if (q + QS == BK / 16) retire_keep(min(nk - 1 - (kt + 1), NST - 2));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       bar();
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int e = 0; e < QS; ++e)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = ConvLp<LP>::mma(fa[i], fb[j], acc[i][j]);
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = ConvLp<LP>::mma(fa[e][i], fb[e][j], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
       bar();
     }
@@ -1516,21 +1531,27 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
   c.fd_kw = FastDiv((unsigned)c.KW);
   ProfScope prof(lp ? (MODE == kFwd ? "conv_fwd_lp" : MODE == kDgrad ? "conv_dgrad_lp" : "conv_wgrad_lp") : name, s,
                  2.0 * (double)c.M * (double)c.Nn * (double)c.K);
-  prof.detail("conv_ring%s_kernel<%s,256x%d%s> %lldx%lldx%lld s%d", lp ? "16" : "",
+  prof.detail("conv_ring%s_kernel<%s,256x%d%s%s> %lldx%lldx%lld s%d", lp ? "16" : "",
               MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad", BN, (MODE == kFwd && c.pool_w) ? ",pool" : "",
+              lp && ((g_opt_conv_ring_qs >> (BN == 64 ? 0 : BN == 128 ? 1 : 2)) & 1) ? ",qs2" : "",
               (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
   const dim3 grid((unsigned)c.nblk), block(512);
   if (!lp) {
     if (BN == 256) hipLaunchKernelGGL((conv_ring_kernel<MODE, 256>), grid, block, 0, s, c);
     else hipLaunchKernelGGL((conv_ring_kernel<MODE, 128>), grid, block, 0, s, c);
-  } else if (prec == kPrecBF16) {
-    if (BN == 256) hipLaunchKernelGGL((conv_ring16_kernel<MODE, 256, 1>), grid, block, 0, s, c);
-    else if (BN == 128) hipLaunchKernelGGL((conv_ring16_kernel<MODE, 128, 1>), grid, block, 0, s, c);
-    else hipLaunchKernelGGL((conv_ring16_kernel<MODE, 64, 1>), grid, block, 0, s, c);
   } else {
-    if (BN == 256) hipLaunchKernelGGL((conv_ring16_kernel<MODE, 256, 2>), grid, block, 0, s, c);
-    else if (BN == 128) hipLaunchKernelGGL((conv_ring16_kernel<MODE, 128, 2>), grid, block, 0, s, c);
-    else hipLaunchKernelGGL((conv_ring16_kernel<MODE, 64, 2>), grid, block, 0, s, c);
+    // the 16-bit ring: BN x precision x k-steps per section (QS 2 where the option asks for it at this width:
+    // bit 0 BN 64, bit 1 BN 128, bit 2 BN 256)
+    const bool qs2 = (g_opt_conv_ring_qs >> (BN == 64 ? 0 : BN == 128 ? 1 : 2)) & 1;
+#define SRK_R16(BN_, LP_)                                                                        \
+  if (qs2) hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 2>), grid, block, 0, s, c);   \
+  else hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 1>), grid, block, 0, s, c);
+    if (prec == kPrecBF16) {
+      if (BN == 256) { SRK_R16(256, 1) } else if (BN == 128) { SRK_R16(128, 1) } else { SRK_R16(64, 1) }
+    } else {
+      if (BN == 256) { SRK_R16(256, 2) } else if (BN == 128) { SRK_R16(128, 2) } else { SRK_R16(64, 2) }
+    }
+#undef SRK_R16
   }
   SRK_CHECK_HIP(hipGetLastError());
   *partial_out = c.partial;

@@ -113,6 +113,9 @@ extern int g_opt_conv_unpool16;
 extern int g_opt_conv_colsum16;
 // 16-bit ring convs for N = 64 .. 127 as 256 x 64 tiles ("conv_ring64", default 1; 0 = N >= 128 only)
 extern int g_opt_conv_ring64;
+// 16-bit ring convs: whole 32-deep K-tiles per MFMA section (QS 2) by tile width, a mask ("conv_ring_qs": bit 0
+// BN 64, bit 1 BN 128, bit 2 BN 256; default 0 = one 16-deep k-step per section everywhere)
+extern int g_opt_conv_ring_qs;
 // BatchNorm training statistics: the 256 chunk partials combined as a fixed pairwise tree, one wave per
 // channel ("bn_tree", default 1; 0 = one lane per channel in chunk order)
 extern int g_opt_bn_tree;

@@ -313,6 +313,7 @@ class CrossEntropyLoss(tnn.Module):
 # mode, autograd on); the producing BatchNorm's backward drops its forward entry, the conv backward pops the
 # dY entry it consumes, and the table is bounded (a step's worth of entries).
 COPIES16 = os.environ.get("SRK_BN_COPY16", "1") != "0"   # A/B switch (tests flip it)
+RELU_MASK = os.environ.get("SRK_BN_RELU_MASK", "1") != "0"   # BatchNorm ReLU bits for the backward (A/B switch)
 _copies16 = {}
 _COPIES16_MAX = 32   # > the live entries of one resnet_bgru / mfrn_bgru step (about 22)
 
@@ -757,11 +758,17 @@ class _BatchNormFn(torch.autograd.Function):
         y16, written = None, ctypes.c_int(0)
         if training and any(ctx.needs_input_grad[:4]) and _copy16_wanted(C):   # the consuming conv's 16-bit copy of y
             y16 = torch.empty(y.numel(), device=x.device, dtype=torch.int16)
-        call("srk_batchnorm_fwd16", ptr(x), M, C, ptr(gamma), ptr(beta), float(eps), float(momentum), int(training),
-             ptr(running_mean), ptr(running_var), ptr(res) if res is not None else None, int(relu), ptr(y),
-             ptr(y16) if y16 is not None else None, ctypes.byref(written), ptr(mean), ptr(invstd), stream_ptr())
+        # the ReLU pattern as bits for the backward (1/16 of y's bytes, read twice there)
+        mask = None
+        if relu and RELU_MASK and any(ctx.needs_input_grad[:4]):
+            mask = torch.empty(M * C // 4, device=x.device, dtype=torch.uint8)
+        call("srk_batchnorm_fwd16_mask", ptr(x), M, C, ptr(gamma), ptr(beta), float(eps), float(momentum),
+             int(training), ptr(running_mean), ptr(running_var), ptr(res) if res is not None else None, int(relu),
+             ptr(y), ptr(y16) if y16 is not None else None, ctypes.byref(written),
+             ptr(mask) if mask is not None else None, ptr(mean), ptr(invstd), stream_ptr())
         if written.value:
             _copy16_put(y, y16)
+        ctx.mask = mask
         ctx.save_for_backward(x, y, gamma, mean, invstd)
         ctx.params = (gamma, beta)
         ctx.flags = (int(training), int(relu), residual is not None)
@@ -787,10 +794,11 @@ class _BatchNormFn(torch.autograd.Function):
         gg = _flat_grad(gp) if ctx.needs_input_grad[1] else None
         gb = _flat_grad(bp) if ctx.needs_input_grad[2] else None
         acc = gg is not None and gb is not None
-        call("srk_batchnorm_bwd16_acc", ptr(x), ptr(y), ptr(dy), M, C, ptr(gamma), ptr(mean), ptr(invstd), training,
-             relu, ptr(dx) if dx is not None else None, ptr(dx16) if dx16 is not None else None, ctypes.byref(written),
-             ptr(dgamma), ptr(dbeta), ptr(dres) if dres is not None else None, ptr(gg) if acc else None,
-             ptr(gb) if acc else None, stream_ptr())
+        mask, ctx.mask = ctx.mask, None
+        call("srk_batchnorm_bwd16_mask", ptr(x), ptr(y), ptr(mask) if mask is not None else None, ptr(dy), M, C,
+             ptr(gamma), ptr(mean), ptr(invstd), training, relu, ptr(dx) if dx is not None else None,
+             ptr(dx16) if dx16 is not None else None, ctypes.byref(written), ptr(dgamma), ptr(dbeta),
+             ptr(dres) if dres is not None else None, ptr(gg) if acc else None, ptr(gb) if acc else None, stream_ptr())
         if written.value:
             _copy16_put(dx, dx16)
         if acc:

@@ -182,3 +182,71 @@ def test_fbanks_cnn_step_with_conv1_copy_is_bitwise(gpu, prec):
         assert torch.equal(g1[n], g3[n]), n
     act = 5 * 98 * 40 * 64   # conv1's pooled output: 4 B read + 2 B written less per element
     assert to16[False][2] - to16[True][2] == 6.0 * act, (to16[True], to16[False])
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("M,C,res", [(4096, 64, 0), (1000, 128, 1), (17, 8, 1)])
+def test_batchnorm_relu_mask(gpu, prec, M, C, res):
+    """srk_batchnorm_fwd16_mask / bwd16_mask: the ReLU bits are exactly y > 0 (byte i, bit e: element 4i + e),
+    and the backward reading them (y passed as null) equals the y-reading backward bit for bit."""
+    g = torch.Generator().manual_seed(M + 3 * C)
+    x = (torch.randn(M, C, generator=g) * 2 + 0.3).cuda()
+    gamma, beta = (torch.rand(C, generator=g) + 0.5).cuda(), torch.randn(C, generator=g).cuda()
+    r = torch.randn(M, C, generator=g).cuda() if res else None
+    dy = torch.randn(M, C, generator=g).cuda()
+    out = []
+    try:
+        _lib.set_matmul_precision(prec)
+        for use_mask in (True, False):
+            rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+            y, mean, inv = torch.empty_like(x), torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+            mask = torch.full((M * C // 4,), 0xEE, dtype=torch.uint8, device="cuda") if use_mask else None
+            wy = ctypes.c_int(-1)
+            call("srk_batchnorm_fwd16_mask", ptr(x), M, C, ptr(gamma), ptr(beta), 1e-5, 0.1, 1, ptr(rm), ptr(rv),
+                 ptr(r) if r is not None else None, 1, ptr(y), None, ctypes.byref(wy),
+                 ptr(mask) if mask is not None else None, ptr(mean), ptr(inv), stream_ptr())
+            dx, dg, db = torch.empty_like(x), torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+            dr = torch.empty_like(x) if res else None
+            wd = ctypes.c_int(-1)
+            call("srk_batchnorm_bwd16_mask", ptr(x), None if use_mask else ptr(y), ptr(mask) if use_mask else None,
+                 ptr(dy), M, C, ptr(gamma), ptr(mean), ptr(inv), 1, 1, ptr(dx), None, ctypes.byref(wd), ptr(dg),
+                 ptr(db), ptr(dr) if dr is not None else None, None, None, stream_ptr())
+            torch.cuda.synchronize()
+            out.append((y, mask, dx, dg, db, dr))
+    finally:
+        _lib.set_matmul_precision("fp32")
+    (y, mask, dx, dg, db, dr), (y0, _, dx0, dg0, db0, dr0) = out
+    bits = (y > 0).reshape(-1, 4).to(torch.int32)
+    want = (bits * torch.tensor([1, 2, 4, 8], device="cuda", dtype=torch.int32)).sum(1).to(torch.uint8)
+    assert torch.equal(mask, want)
+    assert torch.equal(y, y0) and torch.equal(dx, dx0) and torch.equal(dg, dg0) and torch.equal(db, db0)
+    assert dr is None or torch.equal(dr, dr0)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_resnet_bgru_step_with_relu_mask_is_bitwise(gpu, prec):
+    """nn.BatchNorm1d's backward reading the forward's ReLU bits (RELU_MASK) instead of y: the train step
+    equals the y-reading step bit for bit (model_resnet_bgru.py: every BatchNorm but the heads' has a ReLU)."""
+    from speechrecognitionproject_amd.models import model_resnet_bgru
+    torch.manual_seed(13)
+    net = model_resnet_bgru.Network().cuda().train()
+    g = np.random.default_rng(14)
+    x = torch.from_numpy(g.standard_normal((4, 16000)).astype(np.float32) * 0.1).cuda()
+    y = torch.from_numpy(g.integers(0, 12, 4)).cuda()
+    state = {k: v.clone() for k, v in net.state_dict().items()}
+    res = {}
+    prev = snn.RELU_MASK
+    snn._copies16.clear()
+    try:
+        _lib.set_matmul_precision(prec)
+        for on in (True, False):
+            net.load_state_dict(state)
+            snn.RELU_MASK = on
+            res[on] = _resnet_step(net, x, y)
+    finally:
+        snn.RELU_MASK = prev
+        _lib.set_matmul_precision("fp32")
+    (o1, g1), (o0, g0) = res[True], res[False]
+    assert torch.isfinite(o1).all() and torch.equal(o1, o0)
+    for n in g0:
+        assert torch.equal(g1[n], g0[n]), n

@@ -618,8 +618,11 @@ def test_conv_16bit_ring(prec, shape):
     gy = torch.randn(N, Ho, Wo, Co, generator=g).cuda()
     outs = []
     try:
-        for mask in (0x70 | 6, 6):
+        # ring (one k-step per MFMA section), ring with whole K-tiles per section (conv_ring_qs, every width),
+        # register-staged
+        for mask, qs in ((0x70 | 6, 0), (0x70 | 6, 7), (6, 0)):
             _lib.set_option("conv_ring", mask)
+            _lib.set_option("conv_ring_qs", qs)
             xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
             ym = snn._Conv2dNHWCFn.apply(xm, wm, bm, (ph, pw), (sh, sw))
             (ym * gy).sum().backward()
@@ -627,7 +630,10 @@ def test_conv_16bit_ring(prec, shape):
             outs.append([t.detach().double() for t in (ym, xm.grad, wm.grad, bm.grad)])
     finally:
         _lib.set_option("conv_ring", 0x77)
-    for a, c in zip(*outs):
+        _lib.set_option("conv_ring_qs", 0)
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)   # the same MFMA order per accumulator
+    for a, c in zip(outs[0], outs[2]):
         assert ((a - c).abs().max() / c.abs().max()).item() <= 1e-5
 
 

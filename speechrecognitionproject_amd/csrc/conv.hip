@@ -550,6 +550,7 @@ __global__ void splitk_sum_kernel(const float* __restrict__ partial, int splits,
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float s = 0.f;
+#pragma unroll 8   // loads ahead of the in-order adds: the weight-gradient slabs are few threads x many splits
   for (int k = 0; k < splits; ++k) s += partial[(int64_t)k * n + i];
   out[i] = bias ? s + bias[i % ncol] : s;
 }
@@ -653,6 +654,7 @@ __global__ void colsum_splits_kernel(const float* __restrict__ part, int splits,
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float s = 0.f;
+#pragma unroll 8   // loads ahead of the in-order adds (not one dependent load latency per split)
   for (int k = 0; k < splits; ++k) s += part[(int64_t)k * n + i];
   db[i] = s;
 }
@@ -809,12 +811,37 @@ __global__ __launch_bounds__(256) void colsum8_kernel(const float* __restrict__ 
   }
 }
 
-__global__ void colsum_blocks_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// out[c] = sum over the nblk partial rows, in a fixed order: workgroup = 64 columns (lane = column) x 16
+// waves, wave w adds its contiguous run of blocks with 8 loads in flight, then the 16 wave sums are added in
+// wave order.  (One lane walking ~2,000 blocks one dependent load at a time took 400-700 us: r05c, cfg3 bf16.)
+constexpr int kCsWaves = 16;
+__global__ __launch_bounds__(64 * kCsWaves) void colsum_blocks_kernel(const float* __restrict__ part, int nblk, int C,
+                                                                      float* __restrict__ out) {
+  __shared__ float red[kCsWaves][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int run = (nblk + kCsWaves - 1) / kCsWaves;
+  const int b0 = wave * run, b1 = min(nblk, b0 + run);
   float t = 0.f;
-  for (int b = 0; b < nblk; ++b) t += part[(int64_t)b * C + c];
-  out[c] = t;
+  if (c < C) {
+    int b = b0;
+    for (; b + 8 <= b1; b += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(b + u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t += v[u];
+    }
+    for (; b < b1; ++b) t += part[(int64_t)b * C + c];
+  }
+  red[wave][lane] = t;
+  __syncthreads();
+  if (wave == 0 && c < C) {
+    float a = red[0][lane];
+#pragma unroll
+    for (int w = 1; w < kCsWaves; ++w) a += red[w][lane];
+    out[c] = a;
+  }
 }
 
 struct ConvScratch {
@@ -905,7 +932,8 @@ int colsum8(int kind, int prec, const float* x, const uint8_t* arg, int64_t rows
   else if (prec == kPrecBF16) { if (kind == 1) SRK_CS8(1, 1); else SRK_CS8(1, 2); }
   else { if (kind == 1) SRK_CS8(2, 1); else SRK_CS8(2, 2); }
 #undef SRK_CS8
-  hipLaunchKernelGGL(colsum_blocks_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part, (int)nblk, C, out);
+  hipLaunchKernelGGL(colsum_blocks_kernel, dim3((unsigned)((C + 63) / 64)), dim3(64 * kCsWaves), 0, s, part, (int)nblk,
+                     C, out);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
 }
@@ -1248,9 +1276,16 @@ __device__ __forceinline__ u32x4_ r16_frag(const unsigned short* img, int r0, in
 // QS: k-steps (16 deep) per MFMA section, as gemm_g16_kernel's: 1 = a barrier pair per k-step (BN / 32
 // MFMAs per wave between barriers: 2 at BN = 64), 2 = the whole 32-deep K-tile per section (twice the
 // MFMAs per barrier pair, both DMAs issued in the one load section) — option conv_ring_qs
-template <int MODE, int BN, int LP, int QS = 1>
+// NST: ring stages (4; up to 160 KB of LDS: 5 at BN = 256, 6 at BN <= 128 — option conv_ring_deep): the
+// K-tiles in flight (NST - 1) bound the gather throughput at the L2 / HBM latency, not the bandwidth.
+template <int VM>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(VM >= 0 && VM < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
+}
+template <int MODE, int BN, int LP, int QS = 1, int NST = 4>
 __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
-  constexpr int BK = kR16BK, NST = 4;
+  constexpr int BK = kR16BK;
   constexpr bool AKC = MODE != kWgrad;
   constexpr int HALF = 128 * BK;                     // 8 KB of 16-bit elements per half image
   constexpr int NBH = BN >= 128 ? BN / 128 : 1;   // BN = 64: one 128-wide B image, its upper half masked
@@ -1364,16 +1399,13 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
       issue(v, rsB, ldst + (unsigned)((2 + h) * HALF * 2), soff);
     }
   };
-  auto retire_keep = [](int tiles_in_flight) {
-    if (tiles_in_flight >= 2) {
-      if (NDMA == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else if (tiles_in_flight == 1) {
-      if (NDMA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+  static_assert(NST >= 4 && NST * STAGE * 2 <= 160 * 1024, "ring16: 4+ stages within 160 KB of LDS");
+  auto retire_keep = [](int tiles_in_flight) {   // at most NST - 2 K-tiles (NDMA instructions each) left in flight
+    if (NST >= 6 && tiles_in_flight >= 4) wait_vm<4 * NDMA>();
+    else if (NST >= 5 && tiles_in_flight >= 3) wait_vm<3 * NDMA>();
+    else if (tiles_in_flight >= 2) wait_vm<2 * NDMA>();
+    else if (tiles_in_flight == 1) wait_vm<NDMA>();
+    else wait_vm<0>();
   };
 
   f32x16 acc[TM][TN];
@@ -1533,7 +1565,9 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
                  2.0 * (double)c.M * (double)c.Nn * (double)c.K);
   prof.detail("conv_ring%s_kernel<%s,256x%d%s%s> %lldx%lldx%lld s%d", lp ? "16" : "",
               MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad", BN, (MODE == kFwd && c.pool_w) ? ",pool" : "",
-              lp && ((g_opt_conv_ring_qs >> (BN == 64 ? 0 : BN == 128 ? 1 : 2)) & 1) ? ",qs2" : "",
+              lp && BN >= 128 && ((g_opt_conv_ring_qs >> (BN == 128 ? 1 : 2)) & 1)
+                  ? (((g_opt_conv_ring_deep >> (BN == 128 ? 1 : 2)) & 1) ? ",qs2,deep" : ",qs2")
+                  : "",
               (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
   const dim3 grid((unsigned)c.nblk), block(512);
   if (!lp) {
@@ -1542,14 +1576,18 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
   } else {
     // the 16-bit ring: BN x precision x k-steps per section (QS 2 where the option asks for it at this width:
     // bit 0 BN 64, bit 1 BN 128, bit 2 BN 256)
-    const bool qs2 = (g_opt_conv_ring_qs >> (BN == 64 ? 0 : BN == 128 ? 1 : 2)) & 1;
-#define SRK_R16(BN_, LP_)                                                                        \
-  if (qs2) hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 2>), grid, block, 0, s, c);   \
+    const int wbit = BN == 64 ? 0 : BN == 128 ? 1 : 2;
+    const bool qs2 = (g_opt_conv_ring_qs >> wbit) & 1, deep = qs2 && BN >= 128 && ((g_opt_conv_ring_deep >> wbit) & 1);
+#define SRK_R16(BN_, LP_)                                                                                        \
+  if (deep) hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 2, BN_ == 256 ? 5 : 6>), grid, block, 0, s, c); \
+  else if (qs2) hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 2>), grid, block, 0, s, c);              \
   else hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 1>), grid, block, 0, s, c);
     if (prec == kPrecBF16) {
-      if (BN == 256) { SRK_R16(256, 1) } else if (BN == 128) { SRK_R16(128, 1) } else { SRK_R16(64, 1) }
+      if (BN == 256) { SRK_R16(256, 1) } else if (BN == 128) { SRK_R16(128, 1) }
+      else hipLaunchKernelGGL((conv_ring16_kernel<MODE, 64, 1>), grid, block, 0, s, c);
     } else {
-      if (BN == 256) { SRK_R16(256, 2) } else if (BN == 128) { SRK_R16(128, 2) } else { SRK_R16(64, 2) }
+      if (BN == 256) { SRK_R16(256, 2) } else if (BN == 128) { SRK_R16(128, 2) }
+      else hipLaunchKernelGGL((conv_ring16_kernel<MODE, 64, 2>), grid, block, 0, s, c);
     }
 #undef SRK_R16
   }

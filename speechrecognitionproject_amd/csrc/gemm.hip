@@ -1662,6 +1662,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmDesc d, const fl
   d.C += (int64_t)blockIdx.y * d.sC;
   const int64_t row = i / d.N, col = i % d.N;
   float s = 0.f;
+#pragma unroll 8   // loads ahead of the in-order adds
   for (int k = 0; k < splits; ++k) s += partial[(int64_t)k * d.M * d.N + i];
   float v = d.alpha * s;
   if (d.bias_mode == 1) v += d.bias[col];
@@ -1698,6 +1699,7 @@ __global__ void rowsum_reduce_kernel(float* __restrict__ out, float beta, const 
   rp += (int64_t)blockIdx.y * splits * M;
   out += (int64_t)blockIdx.y * out_stride;
   float t = 0.f;
+#pragma unroll 8   // loads ahead of the in-order adds (not one dependent load latency per split)
   for (int k = 0; k < splits; ++k) t += rp[(int64_t)k * M + m];
   out[m] = beta != 0.f ? beta * out[m] + t : t;
 }

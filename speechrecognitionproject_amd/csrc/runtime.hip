@@ -28,8 +28,9 @@ int g_opt_conv_tile = 128;
 int g_opt_conv_ring = 0x77;
 int g_opt_conv_unpool16 = 1;
 int g_opt_conv_colsum16 = 1;
-int g_opt_conv_ring64 = 1;
-int g_opt_conv_ring_qs = 0;
+int g_opt_conv_ring64 = 0;
+int g_opt_conv_ring_qs = 6;
+int g_opt_conv_ring_deep = 0;
 int g_opt_bn_tree = 1;
 int g_opt_gru_poll_pipe = 0;
 int g_opt_mfcc_variant = 3;
@@ -414,6 +415,11 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "conv_ring_qs") {   // 16-bit ring convs: whole K-tiles per MFMA section, mask by width (64, 128, 256)
     SRK_REQUIRE(value >= 0 && value <= 7, SRK_ERR_INVALID, "conv_ring_qs is a 3-bit mask");
     srk::g_opt_conv_ring_qs = (int)value;
+    return SRK_OK;
+  }
+  if (n == "conv_ring_deep") {   // 16-bit ring convs (QS 2): 5 / 6 ring stages, mask by width (128, 256)
+    SRK_REQUIRE(value >= 0 && value <= 7, SRK_ERR_INVALID, "conv_ring_deep is a 3-bit mask");
+    srk::g_opt_conv_ring_deep = (int)value;
     return SRK_OK;
   }
   if (n == "conv_colsum16") {   // 16-bit modes: conv bias gradients fused into dY's 16-bit conversion (1) or not (0)

@@ -111,11 +111,15 @@ extern int g_opt_conv_unpool16;
 // 16-bit-source modes: the conv bias gradient (column sums of dY) fused into the pass that rounds dY (or
 // unpools it) to its 16-bit copy ("conv_colsum16", default 1; 0 = a separate column-sum pass over dY)
 extern int g_opt_conv_colsum16;
-// 16-bit ring convs for N = 64 .. 127 as 256 x 64 tiles ("conv_ring64", default 1; 0 = N >= 128 only)
+// 16-bit ring convs for N = 64 .. 127 as 256 x 64 tiles ("conv_ring64", default 0 = N >= 128 only: slower than
+// the register-staged 128 x 64 kernels on fbanks_cnn conv2 / resnet layer1, r05b)
 extern int g_opt_conv_ring64;
-// 16-bit ring convs: whole 32-deep K-tiles per MFMA section (QS 2) by tile width, a mask ("conv_ring_qs": bit 0
-// BN 64, bit 1 BN 128, bit 2 BN 256; default 0 = one 16-deep k-step per section everywhere)
+// 16-bit ring convs: whole 32-deep K-tiles per MFMA section (QS 2) by tile width, a mask ("conv_ring_qs": bit 1
+// BN 128, bit 2 BN 256; default 6; bit 0 (BN 64) is ignored: that tile keeps one k-step per section)
 extern int g_opt_conv_ring_qs;
+// 16-bit ring convs with QS 2: the deepest ring the LDS holds (5 stages at BN 256, 6 at BN 128) by width, a mask
+// ("conv_ring_deep": bit 1 BN 128, bit 2 BN 256; default 0 = 4 stages)
+extern int g_opt_conv_ring_deep;
 // BatchNorm training statistics: the 256 chunk partials combined as a fixed pairwise tree, one wave per
 // channel ("bn_tree", default 1; 0 = one lane per channel in chunk order)
 extern int g_opt_bn_tree;

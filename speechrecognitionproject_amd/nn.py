@@ -475,7 +475,7 @@ class _Conv1PoolFn(torch.autograd.Function):
         # training steps in a 16-bit mode: the kernel also writes y's 16-bit operand copy, which conv2's
         # fused conv + pool takes as ready (no second pass over the fp32 activation)
         y16 = None
-        if _copy16_wanted(Co) and torch.is_grad_enabled() and ctx.needs_input_grad[1]:
+        if _copy16_wanted(Co) and ctx.needs_input_grad[1]:   # (forward runs under no_grad: needs_input_grad tells)
             y16 = torch.empty(y.numel(), device=x.device, dtype=torch.int16)
         written = ctypes.c_int(0)
         call("srk_conv1_pool_fwd16", ptr(x), N, H, W, ptr(w.contiguous()), ptr(b), Co, KH, KW, padding[0], padding[1],

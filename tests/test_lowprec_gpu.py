@@ -620,9 +620,12 @@ def test_conv_16bit_ring(prec, shape):
     try:
         # ring (one k-step per MFMA section), ring with whole K-tiles per section (conv_ring_qs, every width),
         # register-staged
-        for mask, qs in ((0x70 | 6, 0), (0x70 | 6, 7), (6, 0)):
+        # (and the deepest rings, conv_ring_deep), the 256 x 64 tiles on (conv_ring64)
+        _lib.set_option("conv_ring64", 1)
+        for mask, qs, deep in ((0x70 | 6, 0, 0), (0x70 | 6, 7, 0), (0x70 | 6, 7, 7), (6, 0, 0)):
             _lib.set_option("conv_ring", mask)
             _lib.set_option("conv_ring_qs", qs)
+            _lib.set_option("conv_ring_deep", deep)
             xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
             ym = snn._Conv2dNHWCFn.apply(xm, wm, bm, (ph, pw), (sh, sw))
             (ym * gy).sum().backward()
@@ -630,10 +633,13 @@ def test_conv_16bit_ring(prec, shape):
             outs.append([t.detach().double() for t in (ym, xm.grad, wm.grad, bm.grad)])
     finally:
         _lib.set_option("conv_ring", 0x77)
-        _lib.set_option("conv_ring_qs", 0)
-    for a, c in zip(outs[0], outs[1]):
-        assert torch.equal(a, c)   # the same MFMA order per accumulator
-    for a, c in zip(outs[0], outs[2]):
+        _lib.set_option("conv_ring_qs", 6)
+        _lib.set_option("conv_ring_deep", 0)
+        _lib.set_option("conv_ring64", 0)
+    for o in outs[1:3]:
+        for a, c in zip(outs[0], o):
+            assert torch.equal(a, c)   # the same MFMA order per accumulator
+    for a, c in zip(outs[0], outs[3]):
         assert ((a - c).abs().max() / c.abs().max()).item() <= 1e-5
 
 

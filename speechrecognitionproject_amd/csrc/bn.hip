@@ -66,12 +66,18 @@ __device__ __forceinline__ void st4_16(uint16_t* p, v4f v) {
 }
 
 // Chan et al. pairwise combination of (count, mean, M2) — fixed call order => deterministic.
+// The update is spelled out with fmaf (mu = fma(d, nb / nt, mu), m2 += fma(d d, n nb / nt, m2b)), so every
+// form that uses it rounds identically whatever the compiler's contraction / vectorisation choices.
+__device__ __forceinline__ void chan_step(float n, float& mu, float& m2, float nb, float nt, float mub, float m2b) {
+  const float d = mub - mu, r = nb / nt, q = n * nb / nt;
+  mu = fmaf(d, r, mu);
+  m2 = m2 + fmaf(d * d, q, m2b);
+}
 __device__ __forceinline__ void chan(float& n, float& mu, float& m2, float nb, float mub, float m2b) {
   if (nb == 0.f) return;
   if (n == 0.f) { n = nb; mu = mub; m2 = m2b; return; }
-  const float nt = n + nb, d = mub - mu;
-  mu += d * (nb / nt);
-  m2 += m2b + d * d * (n * nb / nt);
+  const float nt = n + nb;
+  chan_step(n, mu, m2, nb, nt, mub, m2b);
   n = nt;
 }
 
@@ -156,6 +162,38 @@ __device__ __forceinline__ void combine_chunks(const float* __restrict__ pmean, 
   }
 }
 
+// combine_chunks's arithmetic, bit for bit, without its dependent divides: every chunk has >= 1 row, so
+// past chunk 0 (taken as is: chan's n == 0 case) the counts n, nb and the ratios nb / nt, n nb / nt are
+// data-independent — computed off the (mu, m2) chain, which keeps only chan_step's subtract / fma / fma / add
+// per chunk (chan_step itself, so the same roundings).  The in-order form that bn_finalize runs by
+// default (bn_tree = 0): ~54 us per BatchNorm layer with the divides in the chain (r04k cfg4 bf16).
+__device__ __forceinline__ void combine_chunks_fast(const float* __restrict__ pmean, const float* __restrict__ pm2,
+                                                    const BnGeom& g, int c, float& n, float& mu, float& m2) {
+  const float rpc = (float)g.rows_per_chunk;
+  const float last = (float)(g.M - (int64_t)(g.chunks - 1) * g.rows_per_chunk);
+  n = g.chunks == 1 ? last : rpc;
+  mu = pmean[c];
+  m2 = pm2[c];
+  for (int k0 = 1; k0 < g.chunks; k0 += kPre) {
+    float vm[kPre], v2[kPre];
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+      const int64_t k = k0 + u < g.chunks ? k0 + u : g.chunks - 1;
+      vm[u] = pmean[k * g.C + c];
+      v2[u] = pm2[k * g.C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+      if (k0 + u < g.chunks) {
+        const float nb = k0 + u == g.chunks - 1 ? last : rpc;
+        const float nt = n + nb;
+        chan_step(n, mu, m2, nb, nt, vm[u], v2[u]);
+        n = nt;
+      }
+    }
+  }
+}
+
 // Combine the chunk partials of channel c (Chan's pairwise formula) as a fixed pairwise tree, one wave
 // per channel: lane l combines chunks 4l .. 4l+3 in order (kMaxChunks = 256 = 4 x 64), then the lanes pair up at distance 1, 2, .. 32 (lane l takes lane
 // l + d when l % 2d == 0).  Deterministic (the tree does not depend on timing) and shallower: 3 + 6
@@ -192,20 +230,24 @@ __device__ __forceinline__ void combine_chunks_tree(const float* __restrict__ pm
 
 // Biased variance for the normalisation, unbiased for the running estimate (nn.BatchNorm1d,
 // momentum update).  Block = 4 waves = 4 channels (combine_chunks_tree).
-template <bool TREE>
+// TREE: 0 = in order (combine_chunks_fast), 1 = pairwise tree, 2 = in order with the divides in the chain
+// (combine_chunks: the bitwise reference of form 0)
+template <int TREE>
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ pmean,
                                                           const float* __restrict__ pm2, BnGeom g, float eps,
                                                           float momentum, float* __restrict__ mean,
                                                           float* __restrict__ invstd, float* __restrict__ running_mean,
                                                           float* __restrict__ running_var) {
-  const int c = TREE ? blockIdx.x * 4 + (threadIdx.x >> 6) : blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = TREE == 1 ? blockIdx.x * 4 + (threadIdx.x >> 6) : blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= g.C) return;
   float n, mu, m2;
-  if (TREE) {
+  if (TREE == 1) {
     combine_chunks_tree(pmean, pm2, g, c, n, mu, m2);
     if ((threadIdx.x & 63) != 0) return;
-  } else {
+  } else if (TREE == 2) {
     combine_chunks(pmean, pm2, g, c, n, mu, m2);
+  } else {
+    combine_chunks_fast(pmean, pm2, g, c, n, mu, m2);
   }
   const float var = m2 / (float)g.M;
   mean[c] = mu;
@@ -527,12 +569,17 @@ int srk_batchnorm_fwd16_mask(const float* x, int64_t M, int64_t C, const float* 
     if (int rc = srk::bn_scratch((size_t)2 * g.chunks * C, &part)) return rc;
     hipLaunchKernelGGL(srk::bn_stats_kernel, dim3((unsigned)((g.C4 + g.CQ - 1) / g.CQ), (unsigned)g.chunks), dim3(256),
                        0, s, x, g, part, part + (size_t)g.chunks * C);
-    if (srk::g_opt_bn_tree)
-      hipLaunchKernelGGL(srk::bn_finalize_kernel<true>, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, s, part,
+    // one wave per channel (tree) or one lane per channel in 64-lane blocks (in order: C / 64 waves over the chip)
+    if (srk::g_opt_bn_tree == 1)
+      hipLaunchKernelGGL(srk::bn_finalize_kernel<1>, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, s, part,
+                         part + (size_t)g.chunks * C, g, eps, momentum, save_mean, save_invstd, running_mean,
+                         running_var);
+    else if (srk::g_opt_bn_tree == 2)
+      hipLaunchKernelGGL(srk::bn_finalize_kernel<2>, dim3((unsigned)((C + 63) / 64)), dim3(64), 0, s, part,
                          part + (size_t)g.chunks * C, g, eps, momentum, save_mean, save_invstd, running_mean,
                          running_var);
     else
-      hipLaunchKernelGGL(srk::bn_finalize_kernel<false>, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part,
+      hipLaunchKernelGGL(srk::bn_finalize_kernel<0>, dim3((unsigned)((C + 63) / 64)), dim3(64), 0, s, part,
                          part + (size_t)g.chunks * C, g, eps, momentum, save_mean, save_invstd, running_mean,
                          running_var);
   } else {

@@ -852,6 +852,7 @@ ConvScratch g_cs[64];     // split-K slabs
 ConvScratch g_cs16[64];   // 16-bit operand sources
 ConvScratch g_csb[64];    // wgrad bias column-sum partials
 ConvScratch g_csd[64];    // dense activation / gradient of the pooled conv (split-K forward, backward dY)
+ConvScratch g_csy[64];    // conv_bwd: dY's 16-bit copy made with the bias sums (dY itself may sit in g_csd)
 std::mutex g_cs_mu;
 
 int conv_scratch(size_t floats, float** out, ConvScratch* pool = g_cs) {
@@ -1832,7 +1833,7 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
     d16[1] = const_cast<unsigned short*>(dy16);
     if (cs && !dy16) {
       float* d = nullptr;
-      if ((rc = srk::conv_scratch((size_t)(n[1] + 1) / 2, &d, srk::g_csd))) return rc;
+      if ((rc = srk::conv_scratch((size_t)(n[1] + 1) / 2, &d, srk::g_csy))) return rc;
       d16[1] = reinterpret_cast<unsigned short*>(d);
     }
     if ((rc = srk::to16_all(prec, src, n, dgrad_implicit ? 3 : 2, d16, s, ready))) return rc;
@@ -2049,7 +2050,7 @@ namespace srk {
 int release_conv_scratch() {
   std::lock_guard<std::mutex> lk(g_cs_mu);
   SRK_CHECK_HIP(hipDeviceSynchronize());
-  for (ConvScratch* pool : {g_cs, g_cs16, g_csb, g_csd})
+  for (ConvScratch* pool : {g_cs, g_cs16, g_csb, g_csd, g_csy})
     for (int d = 0; d < 64; ++d) {
       if (pool[d].p) SRK_CHECK_HIP(hipFree(pool[d].p));
       pool[d].p = nullptr;

@@ -31,7 +31,8 @@ int g_opt_conv_colsum16 = 1;
 int g_opt_conv_ring64 = 0;
 int g_opt_conv_ring_qs = 6;
 int g_opt_conv_ring_deep = 0;
-int g_opt_bn_tree = 1;
+int g_opt_conv1_mfma = 1;
+int g_opt_bn_tree = 0;
 int g_opt_gru_poll_pipe = 0;
 int g_opt_mfcc_variant = 3;
 int g_opt_gemm_streamk = 1;
@@ -405,7 +406,8 @@ int srk_set_option(const char* name, int64_t value) {
     return SRK_OK;
   }
   if (n == "bn_tree") {   // BatchNorm statistics: chunk partials combined as a pairwise tree (1) or in order (0)
-    srk::g_opt_bn_tree = value != 0;
+    SRK_REQUIRE(value >= 0 && value <= 2, SRK_ERR_INVALID, "bn_tree must be 0, 1 or 2");
+    srk::g_opt_bn_tree = (int)value;
     return SRK_OK;
   }
   if (n == "conv_ring64") {   // 16-bit ring convs down to N = 64 (256 x 64 tiles) (1) or N >= 128 only (0)
@@ -415,6 +417,10 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "conv_ring_qs") {   // 16-bit ring convs: whole K-tiles per MFMA section, mask by width (64, 128, 256)
     SRK_REQUIRE(value >= 0 && value <= 7, SRK_ERR_INVALID, "conv_ring_qs is a 3-bit mask");
     srk::g_opt_conv_ring_qs = (int)value;
+    return SRK_OK;
+  }
+  if (n == "conv1_mfma") {   // conv1 + maxpool1 forward on the fp32 matrix cores (1) or the VALU (0)
+    srk::g_opt_conv1_mfma = value != 0;
     return SRK_OK;
   }
   if (n == "conv_ring_deep") {   // 16-bit ring convs (QS 2): 5 / 6 ring stages, mask by width (128, 256)

@@ -120,8 +120,14 @@ extern int g_opt_conv_ring_qs;
 // 16-bit ring convs with QS 2: the deepest ring the LDS holds (5 stages at BN 256, 6 at BN 128) by width, a mask
 // ("conv_ring_deep": bit 1 BN 128, bit 2 BN 256; default 0 = 4 stages)
 extern int g_opt_conv_ring_deep;
-// BatchNorm training statistics: the 256 chunk partials combined as a fixed pairwise tree, one wave per
-// channel ("bn_tree", default 1; 0 = one lane per channel in chunk order)
+// fused conv1 + maxpool1 forward on the fp32 matrix cores (v_mfma_f32_32x32x2_f32, bitwise the VALU kernel's fma
+// chain) ("conv1_mfma", default 1; 0 = the VALU kernel)
+extern int g_opt_conv1_mfma;
+// BatchNorm training statistics: the <= 256 chunk partials combined in chunk order, the count ratios off the
+// dependent chain ("bn_tree" 0, default); 1 = a fixed pairwise tree, one wave per channel (more accurate, but
+// other bits than the reference's in-order arithmetic: ReLU decisions on values within roundoff of 0 move —
+// tests/test_conv_gpu.py golden resnet_bgru at B = 2); 2 = in order with the divides in the chain (form 0's
+// bitwise reference)
 extern int g_opt_bn_tree;
 // persistent GRU (16-bit kernels, fp32 two-chain kernels): the per-producer flag wait keeps four polls in flight
 // ("gru_poll_pipe", default 0)

@@ -17,8 +17,8 @@ weight gradient of a conv feeding it sums x * dy over 512 x 250 rows where dy ha
 mean removed and x (post-ReLU) has a large mean — a cancellation, so ANY fp32 summation order puts
 some element of some tensor off by percent of the tensor's largest element, and WHICH tensor moves
 with the order (measured, tools/cfg4_grad_diag.py, r05c: the reference's own fp32 CPU arithmetic
-1.6 % on layer3.1.conv1; the HIP path 1.6 % on layer3.1.conv2 with the in-order BatchNorm finalize,
-3.7 % on layer4.0.conv1 with the pairwise-tree finalize — which is itself the more accurate one for
+1.6 % on layer3.1.conv1; the HIP path 1.6 % on layer3.1.conv2 with the in-order BatchNorm finalize
+(the default), 3.7 % on layer4.0.conv1 with the pairwise-tree option — itself the more accurate one for
 the statistics, tools/bn_diag.py).  So the oracle also runs in float64 and every HIP gradient tensor
 is held AGAINST FLOAT64 to (a) norm-wise error <= 5e-3 (the HIP path's worst tensor: 3.4e-3; the
 reference fp32 arithmetic's: 1.9e-3) — the accuracy claim — and (b) worst element <= 2.5 x the

@@ -8,7 +8,10 @@ import torch.nn.functional as F
 from conftest import golden
 from oracle import models as OM
 from tolerances import LOGITS_REL, rel_err
+from speechrecognitionproject_amd import _lib
 from speechrecognitionproject_amd import nn as snn
+from speechrecognitionproject_amd._lib import call
+from speechrecognitionproject_amd.features import ptr, stream_ptr
 from speechrecognitionproject_amd.models import model_fbanks_cnn
 from speechrecognitionproject_amd.optim import Adam
 
@@ -123,6 +126,47 @@ def test_conv1_pool_fused_vs_torch(gpu, N, H, W, KH, KW, pool):
     assert rel_err(ym.detach().permute(0, 3, 1, 2).cpu().numpy(), yr.detach().numpy()) <= 1e-5
     assert rel_err(wm.grad.cpu().numpy(), wr.grad.numpy()) <= 1e-4
     assert rel_err(bm.grad.cpu().numpy(), br.grad.numpy()) <= 1e-5
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
+@pytest.mark.parametrize("N,H,W,KH,KW,pool", [
+    (3, 98, 120, 7, 3, 3), (2, 7, 9, 7, 3, 3), (1, 37, 31, 7, 3, 3), (3, 49, 321, 3, 7, 5), (2, 17, 13, 3, 7, 5)])
+def test_conv1_pool_mfma_equals_valu(gpu, prec, N, H, W, KH, KW, pool):
+    """Option conv1_mfma: the fused conv1 + maxpool forward on the fp32 matrix cores (v_mfma_f32_32x32x2_f32,
+    a k-ordered fmaf chain from the bias) equals the VALU kernel bit for bit — pooled values, argmax bytes and
+    the 16-bit copy (srk_conv1_pool_fwd16); partial 32-output groups and block row tails included."""
+    import ctypes
+    g = torch.Generator().manual_seed(N * 11 + W + KH)
+    x = (torch.randn(N, H, W, generator=g) * 30.0).cuda()
+    w = (torch.randn(64, 1, KH, KW, generator=g) * 0.2).cuda()
+    b = torch.randn(64, generator=g).cuda()
+    x[0, 0, :4] = float("nan")   # NaN windows: the maxpool rule (NaN wins, first maximum)
+    Wq = W // pool
+    out = []
+    try:
+        _lib.set_matmul_precision(prec)
+        for mf in (1, 0):
+            _lib.set_option("conv1_mfma", mf)
+            y = torch.full((N, H, Wq, 64), 7.0, device="cuda")
+            arg = torch.full((N, H, Wq, 64), 9, dtype=torch.uint8, device="cuda")
+            y16 = torch.full((N * H * Wq * 64,), 3, dtype=torch.int16, device="cuda")
+            wr = ctypes.c_int(-1)
+            call("srk_conv1_pool_fwd16", ptr(x), N, H, W, ptr(w), ptr(b), 64, KH, KW, KH // 2, KW // 2, pool, ptr(y),
+                 ptr(arg), ptr(y16), ctypes.byref(wr), stream_ptr())
+            torch.cuda.synchronize()
+            out.append((y, arg, y16, wr.value))
+    finally:
+        _lib.set_option("conv1_mfma", 1)
+        _lib.set_matmul_precision("fp32")
+    (y1, a1, c1, w1), (y0, a0, c0, w0) = out
+    assert w1 == w0 == (0 if prec == "fp32" else 1)
+    nan = torch.isnan(y1)
+    assert bool(nan.any()) and torch.equal(nan, torch.isnan(y0))   # NaN payloads may differ: compare the rest
+    assert torch.equal(y1.view(torch.int32)[~nan], y0.view(torch.int32)[~nan])
+    assert torch.equal(a1, a0)
+    if w1:
+        assert torch.equal(c1[~nan.reshape(-1)], c0[~nan.reshape(-1)])
+    assert bool((a1 < pool).all())
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])

@@ -11,11 +11,12 @@ from speechrecognitionproject_amd.nn import BatchNorm1d   # noqa: E402
 
 torch.manual_seed(0)
 for (M, C, mu, sd) in ((512 * 1000, 64, 0.5, 1.0), (512 * 125, 512, 3.0, 0.7), (512 * 125, 512, 0.0, 1e-2),
-                       (512 * 250, 256, 10.0, 1.0)):
+                       (512 * 250, 256, 10.0, 1.0), (2 * 1000, 64, 0.5, 1.0), (2 * 63, 512, 1.0, 1.0),
+                       (2 * 125, 256, 1.0, 1.0), (2 * 250, 128, 1.0, 1.0)):
     x = (torch.randn(M, C, dtype=torch.float64) * sd + mu + torch.randn(C, dtype=torch.float64) * sd)
     x32 = x.float()
     bn = BatchNorm1d(C).cuda().train()
-    y = bn(x32.cuda().view(512, -1, C)).double().cpu().view(M, C)
+    y = bn(x32.cuda().view(-1, C)).double().cpu().view(M, C)
     x64 = x32.double()
     m = x64.mean(0)
     v = x64.var(0, unbiased=False)

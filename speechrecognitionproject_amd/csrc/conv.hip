@@ -66,6 +66,11 @@ struct ConvArgs {
   // [N*Ho*Wo/4][Co] and dy_arg its window argmax; the gathers rebuild the dense gradient
   // dY[pixel][co] = dy_arg[pixel/4][co] == pixel % 4 ? dy[pixel/4][co] : 0 at LDS-store time
   const uint8_t* dy_arg;
+  // 16-bit sources, fwd / dgrad (host-set, run_conv_gemm): the gathered operand's channel count is a multiple
+  // of the K-tile (one tap per K-tile, uniform over the workgroup), dgrad stride 1, and both 16-bit operands
+  // under 2^30 elements — the gathers then use per-row base offsets fixed for the whole k loop, 32-bit buffer
+  // loads whose out-of-range offset returns zeros (no masks, no selects at LDS-store time)
+  int fast16;
 };
 
 // Implicit-GEMM operand gathers.  Each returns the ELEMENT OFFSET of the value (clamped to 0 when
@@ -222,6 +227,27 @@ __global__ __launch_bounds__(NW * 64) void conv_gemm_kernel(ConvArgs c) {
     for (int e = 0; e < 4; ++e) mtap[e] = split_tap(m0 + aq + e < c.M ? m0 + aq + e : 0, c.fd_c, c.fd_kw);
   }
 
+  // fast16 gathers (ConvArgs::fast16): per A row, the element offset of tap (0, 0) channel 0 relative to the
+  // row's pixel and the row's first valid tap row / column as (lo, hi) windows the uniform tap is checked against
+  int rbase[AKC && S16 ? VA : 1], rh[AKC && S16 ? VA : 1], rw[AKC && S16 ? VA : 1];
+  if constexpr (AKC && S16) {
+    if (c.fast16) {
+#pragma unroll
+      for (int i = 0; i < VA; ++i) {
+        const Pix& q = prow[i];
+        if (MODE == kFwd) {   // hi = a sh - ph + kh, wi = b sw - pw + kw
+          rh[i] = q.ok ? q.a * c.sh - c.ph : -(1 << 20);
+          rw[i] = q.b * c.sw - c.pw;
+          rbase[i] = ((q.n * c.H + rh[i]) * c.W + rw[i]) * c.Ci;
+        } else {              // stride 1: ho = a + ph - kh, wo = b + pw - kw
+          rh[i] = q.ok ? q.a + c.ph : -(1 << 20);
+          rw[i] = q.b + c.pw;
+          rbase[i] = ((q.n * c.Ho + rh[i]) * c.Wo + rw[i]) * c.Co;
+        }
+      }
+    }
+  }
+
   v4f ra[VA], rb[VB];   // fp32 staged units (unused, and eliminated, when S16)
   // UNPOOL: the argmax bytes of each staged dY unit and its pixel's window position (2 bits per unit)
   unsigned parg[UNPOOL ? (MODE == kDgrad ? VA : VB) : 1];
@@ -232,6 +258,47 @@ __global__ __launch_bounds__(NW * 64) void conv_gemm_kernel(ConvArgs c) {
     amask = 0;
     bmask = 0;
     if constexpr (S16) {
+      if constexpr (AKC) {
+        if (c.fast16) {   // one tap per K-tile (uniform), buffer loads: out of range -> 16 zero bytes
+          const auto rsA16 = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(c.a16), (short)0, 0x7ffffff0,
+                                                               0x00020000);
+          const auto rsB16 = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(c.b16), (short)0, 0x7ffffff0,
+                                                               0x00020000);
+          const int chans = MODE == kDgrad ? c.Co : c.Ci;
+          const int tap = __builtin_amdgcn_readfirstlane((int)((unsigned)k0 / (unsigned)chans));
+          const int ch = (int)k0 - tap * chans + aq;
+          const int kh = __builtin_amdgcn_readfirstlane(tap / c.KW), kw = tap - kh * c.KW;
+          const bool kin = k0 + aq < ke;
+#pragma unroll
+          for (int i = 0; i < VA; ++i) {
+            bool ok;
+            int off;
+            if (MODE == kFwd) {
+              const int hi = rh[i] + kh, wi = rw[i] + kw;
+              ok = kin && (unsigned)hi < (unsigned)c.H && (unsigned)wi < (unsigned)c.W;
+              off = rbase[i] + (kh * c.W + kw) * c.Ci + ch;
+            } else {
+              const int ho = rh[i] - kh, wo = rw[i] - kw;
+              ok = kin && (unsigned)ho < (unsigned)c.Ho && (unsigned)wo < (unsigned)c.Wo;
+              off = rbase[i] - (kh * c.Wo + kw) * c.Co + ch;
+            }
+            ha[i] = __builtin_bit_cast(u32x4_, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rsA16, ok ? (int)((unsigned)off * 2u) : (int)0x80000000u, 0, 0));
+          }
+#pragma unroll
+          for (int i = 0; i < VB; ++i) {
+            const int vi = tid + i * NT;
+            const int k = (int)k0 + vi / (BN / EU), n = (int)n0 + (vi % (BN / EU)) * EU;
+            const bool ok = k < ke && n < c.Nn;
+            hb[i] = __builtin_bit_cast(u32x4_, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rsB16, ok ? (int)((unsigned)(k * (int)c.Nn + n) * 2u) : (int)0x80000000u,
+                                                   0, 0));
+          }
+          amask = (1u << VA) - 1u;
+          bmask = (1u << VB) - 1u;
+          return;
+        }
+      }
       // every unit shares one pixel and one tap (channel counts % 8 == 0) and never straddles ke
       // (K and the split chunks are multiples of 8)
       if (AKC) {
@@ -389,6 +456,13 @@ __global__ __launch_bounds__(NW * 64) void conv_gemm_kernel(ConvArgs c) {
       unsigned short* As = reinterpret_cast<unsigned short*>(smem + buf * STAGE_FLOATS);
       unsigned short* Bs = As + JA::ELEMS;
       const u32x4_ z = {0u, 0u, 0u, 0u};
+      if (AKC && c.fast16) {   // zeros came from the loads
+#pragma unroll
+        for (int i = 0; i < VA; ++i) *reinterpret_cast<u32x4_*>(As + JA::store_off8(tid + i * NT)) = ha[i];
+#pragma unroll
+        for (int i = 0; i < VB; ++i) *reinterpret_cast<u32x4_*>(Bs + JB::store_off8(tid + i * NT)) = hb[i];
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < VA; ++i)
         *reinterpret_cast<u32x4_*>(As + JA::store_off8(tid + i * NT)) = (amask >> i) & 1u ? ha[i] : z;
@@ -1277,14 +1351,19 @@ __device__ __forceinline__ u32x4_ r16_frag(const unsigned short* img, int r0, in
 // QS: k-steps (16 deep) per MFMA section, as gemm_g16_kernel's: 1 = a barrier pair per k-step (BN / 32
 // MFMAs per wave between barriers: 2 at BN = 64), 2 = the whole 32-deep K-tile per section (twice the
 // MFMAs per barrier pair, both DMAs issued in the one load section) — option conv_ring_qs
-// NST: ring stages (4; up to 160 KB of LDS: 5 at BN = 256, 6 at BN <= 128 — option conv_ring_deep): the
-// K-tiles in flight (NST - 1) bound the gather throughput at the L2 / HBM latency, not the bandwidth.
+// NST: ring stages (4; up to 160 KB of LDS: 5 at BN = 256, 6 at BN <= 128).  Deeper rings measured slower on the
+// cfg3 / cfg4 shapes (r05c: rn_l4 wgrad 486 -> 587 us at 5 stages), so only NST = 4 is instantiated.
 template <int VM>
 __device__ __forceinline__ void wait_vm() {
   static_assert(VM >= 0 && VM < 64, "vmcnt is 6 bits");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
 }
-template <int MODE, int BN, int LP, int QS = 1, int NST = 4>
+// PERS: persistent tile loop (option conv_ring_pers) — a grid of one workgroup per CU walks the tiles (virtual
+// block v = blockIdx.x + r gridDim.x through the same XCD-aware map), and the ring runs on across tiles: the
+// last K-steps of a tile issue the NEXT tile's first NST - 1 K-tiles, so its prologue latency hides behind this
+// tile's MFMAs and epilogue (short-K convs — fbanks_cnn conv2: K = 448, 14 K-tiles — spent about half of each
+// tile in that prologue at one workgroup per CU).  Needs every tile's K range >= NST - 1 K-tiles (host check).
+template <int MODE, int BN, int LP, int QS = 1, int NST = 4, bool PERS = false>
 __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
   constexpr int BK = kR16BK;
   constexpr bool AKC = MODE != kWgrad;
@@ -1304,12 +1383,6 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
   };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = wave >> 2, w4 = wave & 3;
   const int wr = w4 / WC, wc = w4 % WC;
-  int split, tm, tn;
-  map_tile(c.nblk, c.tiles, c.tiles_m, c.tiles_n, c.group_m, true, split, tm, tn);
-  const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * BN;
-  const int64_t kb0 = split * c.kchunk;
-  const int64_t ke = (kb0 + c.kchunk < c.K) ? kb0 + c.kchunk : c.K;
-  const int nk = ke > kb0 ? (int)((ke - kb0 + BK - 1) / BK) : 0;
   auto rsrc = [](const unsigned short* p) {
     const uint64_t a = (uint64_t)(uintptr_t)p;
     return u32x4s{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)a),
@@ -1318,35 +1391,56 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
   const u32x4s rsA = rsrc(c.a16), rsB = rsrc(c.b16);
   const int chans = MODE == kDgrad ? c.Co : c.Ci;
 
+  // this lane's DMA slots (fixed): A rows / k of the two half images, B k and columns
   const int p = wave * 64 + lane;
   int arow[2], akk[2];
-  Pix apix[2];
-  Tap atap[2];
-  bool aok[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (AKC) {   // p = row * 4 + slot: 8 k at 8 (slot ^ swz(row))
       arow[h] = p >> 2;
       akk[h] = ((p & 3) ^ ((arow[h] >> 2) & 3)) * 8;
-      apix[h] = split_pix(m0 + h * 128 + arow[h], c.M, c.fd_w, c.fd_h);
-      aok[h] = apix[h].ok;
     } else {     // p = k * 16 + slot: rows 8 (slot ^ ((k & 3) << 2)) .. +8
       akk[h] = p >> 4;
       arow[h] = ((p & 15) ^ ((akk[h] & 3) << 2)) * 8;
-      const int64_t m = m0 + h * 128 + arow[h];
-      aok[h] = m < c.M;
-      atap[h] = split_tap(aok[h] ? m : 0, c.fd_c, c.fd_kw);
     }
   }
-  unsigned bvo[NBH];
-  bool bok[NBH];
   const int bkk = p >> 4;
+  // one tile's coordinates: its origin, K range and this lane's gather coordinates there
+  struct TileC {
+    int64_t m0, n0, kb0, ke;
+    int nk, split;
+    Pix apix[2];
+    Tap atap[2];
+    bool aok[2];
+    unsigned bvo[NBH];
+    bool bok[NBH];
+  };
+  auto coords = [&](int v, TileC& T) {
+    int tm, tn;
+    map_tile_at(v, c.nblk, c.tiles, c.tiles_m, c.tiles_n, c.group_m, true, T.split, tm, tn);
+    T.m0 = (int64_t)tm * 256;
+    T.n0 = (int64_t)tn * BN;
+    T.kb0 = T.split * c.kchunk;
+    T.ke = (T.kb0 + c.kchunk < c.K) ? T.kb0 + c.kchunk : c.K;
+    T.nk = T.ke > T.kb0 ? (int)((T.ke - T.kb0 + BK - 1) / BK) : 0;
 #pragma unroll
-  for (int h = 0; h < NBH; ++h) {
-    const int64_t n = n0 + h * 128 + ((p & 15) ^ ((bkk & 3) << 2)) * 8;
-    bok[h] = n < c.Nn && n < n0 + BN;
-    bvo[h] = (unsigned)(((int64_t)bkk * c.Nn + (bok[h] ? n : 0)) * 2);
-  }
+    for (int h = 0; h < 2; ++h) {
+      if (AKC) {
+        T.apix[h] = split_pix(T.m0 + h * 128 + arow[h], c.M, c.fd_w, c.fd_h);
+        T.aok[h] = T.apix[h].ok;
+      } else {
+        const int64_t m = T.m0 + h * 128 + arow[h];
+        T.aok[h] = m < c.M;
+        T.atap[h] = split_tap(T.aok[h] ? m : 0, c.fd_c, c.fd_kw);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < NBH; ++h) {
+      const int64_t n = T.n0 + h * 128 + ((p & 15) ^ ((bkk & 3) << 2)) * 8;
+      T.bok[h] = n < c.Nn && n < T.n0 + BN;
+      T.bvo[h] = (unsigned)(((int64_t)bkk * c.Nn + (T.bok[h] ? n : 0)) * 2);
+    }
+  };
   const unsigned lds0 =
       (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ptr)smem + (unsigned)wave * 1024u);
   auto issue = [&](unsigned v, const u32x4s& rs, unsigned ldsa, unsigned soff) {
@@ -1356,9 +1450,10 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
                  : "v"(v), "s"(rs), "s"(ldsa), "s"(soff)
                  : "memory");
   };
-  auto dma_a = [&](int t) {
-    const int64_t k0 = kb0 + (int64_t)t * BK;
-    const unsigned ldst = lds0 + (unsigned)((t % NST) * STAGE * 2);
+  // K-tile t of tile T into ring stage g % NST (g: the ring's running K-tile count)
+  auto dma_a = [&](const TileC& T, int t, int g) {
+    const int64_t k0 = T.kb0 + (int64_t)t * BK;
+    const unsigned ldst = lds0 + (unsigned)((g % NST) * STAGE * 2);
     const unsigned tap = AKC ? (unsigned)__builtin_amdgcn_readfirstlane(c.fd_c.div((unsigned)k0)) : 0u;
     const int ch0 = (int)((unsigned)k0 - tap * (unsigned)chans);
     const int kh = (int)c.fd_kw.div(tap), kw = (int)(tap - (unsigned)kh * c.KW);
@@ -1366,7 +1461,7 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
     for (int h = 0; h < 2; ++h) {
       unsigned v = kROOB;
       if (AKC) {
-        const Pix& q = apix[h];
+        const Pix& q = T.apix[h];
         int64_t off;
         bool ok;
         if (MODE == kFwd) {
@@ -1378,25 +1473,25 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
           ok = ho >= 0 && ho < c.Ho && wo >= 0 && wo < c.Wo;
           off = (((int64_t)q.n * c.Ho + ho) * c.Wo + wo) * c.Co + ch0 + akk[h];
         }
-        if (aok[h] && ok && k0 + akk[h] < ke) v = (unsigned)(off * 2);
+        if (T.aok[h] && ok && k0 + akk[h] < T.ke) v = (unsigned)(off * 2);
       } else {
         const int64_t k = k0 + akk[h];
-        const Pix q = split_pix(k < ke ? k : 0, c.K, c.fd_w, c.fd_h);
-        const Tap& t4 = atap[h];
+        const Pix q = split_pix(k < T.ke ? k : 0, c.K, c.fd_w, c.fd_h);
+        const Tap& t4 = T.atap[h];
         const int hi = q.a * c.sh + t4.kh - c.ph, wi = q.b * c.sw + t4.kw - c.pw;
-        const bool ok = aok[h] && k < ke && hi >= 0 && hi < c.H && wi >= 0 && wi < c.W;
+        const bool ok = T.aok[h] && k < T.ke && hi >= 0 && hi < c.H && wi >= 0 && wi < c.W;
         if (ok) v = (unsigned)(((((int64_t)q.n * c.H + hi) * c.W + wi) * c.Ci + t4.ch) * 2);
       }
       issue(v, rsA, ldst + (unsigned)(h * HALF * 2), 0u);
     }
   };
-  auto dma_b = [&](int t) {
-    const int64_t k0 = kb0 + (int64_t)t * BK;
-    const unsigned ldst = lds0 + (unsigned)((t % NST) * STAGE * 2);
+  auto dma_b = [&](const TileC& T, int t, int g) {
+    const int64_t k0 = T.kb0 + (int64_t)t * BK;
+    const unsigned ldst = lds0 + (unsigned)((g % NST) * STAGE * 2);
     const unsigned soff = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(k0 * c.Nn * 2));
 #pragma unroll
     for (int h = 0; h < NBH; ++h) {
-      const unsigned v = (bok[h] && k0 + bkk < ke) ? bvo[h] : kROOB;
+      const unsigned v = (T.bok[h] && k0 + bkk < T.ke) ? T.bvo[h] : kROOB;
       issue(v, rsB, ldst + (unsigned)((2 + h) * HALF * 2), soff);
     }
   };
@@ -1409,110 +1504,128 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
     else wait_vm<0>();
   };
 
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
+  int vt = blockIdx.x;
+  TileC cur, nxt;
+  coords(vt, cur);
   for (int t = 0; t < NST - 1; ++t)
-    if (t < nk) {
-      dma_a(t);
-      dma_b(t);
+    if (t < cur.nk) {
+      dma_a(cur, t, t);
+      dma_b(cur, t, t);
     }
-  retire_keep(min(nk - 1, NST - 2));
+  retire_keep(min(cur.nk - 1, NST - 2));
   bar();
   if (grp == 1) bar();
 
   const int ar0 = wr * (128 / WR);
   const int bh = (wc * (BN / WC)) / 128, bc0 = (wc * (BN / WC)) % 128;
-  for (int kt = 0; kt < nk; ++kt) {
-    const unsigned short* S = smem + (kt % NST) * STAGE;
-    const unsigned short* As = S + grp * HALF;
-    const unsigned short* Bs = S + (2 + bh) * HALF;
-    const int tn_ = kt + NST - 1;
-    static_assert(QS == 1 || QS == 2, "ring16: 1 or 2 k-steps per section");
+  const int lh = lane >> 5, lc = lane & 31;
+  int g0 = 0;   // the ring's K-tile count at this tile's first K-tile
+  while (true) {
+    const int vn = vt + (int)gridDim.x;
+    const bool has_next = PERS && vn < c.nblk;
+    if (has_next) coords(vn, nxt);
+    f32x16 acc[TM][TN];
 #pragma unroll
-    for (int q = 0; q < BK / 16; q += QS) {
-      u32x4_ fa[QS][TM], fb[QS][TN];
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int e = 0; e < QS; ++e) {
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[e][i] = r16_frag<AKC>(As, ar0 + i * 32, 16 * (q + e), lane);
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nk = cur.nk;
+    for (int kt = 0; kt < nk; ++kt) {
+      const unsigned short* S = smem + ((g0 + kt) % NST) * STAGE;
+      const unsigned short* As = S + grp * HALF;
+      const unsigned short* Bs = S + (2 + bh) * HALF;
+      const int tn_ = kt + NST - 1;   // the K-tile issued now (this tile's, or the next tile's first ones)
+      static_assert(QS == 1 || QS == 2, "ring16: 1 or 2 k-steps per section");
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fb[e][j] = r16_frag<false>(Bs, bc0 + j * 32, 16 * (q + e), lane);
-      }
-      if (tn_ < nk) {
-        if (QS == 2) {
-          dma_a(tn_);
-          dma_b(tn_);
-        } else if (q == 0) {
-          dma_a(tn_);
-        } else {
-          dma_b(tn_);
+      for (int q = 0; q < BK / 16; q += QS) {
+        u32x4_ fa[QS][TM], fb[QS][TN];
+#pragma unroll
+        for (int e = 0; e < QS; ++e) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) fa[e][i] = r16_frag<AKC>(As, ar0 + i * 32, 16 * (q + e), lane);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) fb[e][j] = r16_frag<false>(Bs, bc0 + j * 32, 16 * (q + e), lane);
         }
+        if (tn_ < nk || has_next) {
+          const TileC& T = tn_ < nk ? cur : nxt;
+          const int tt = tn_ < nk ? tn_ : tn_ - nk;
+          if (QS == 2) {
+            dma_a(T, tt, g0 + tn_);
+            dma_b(T, tt, g0 + tn_);
+          } else if (q == 0) {
+            dma_a(T, tt, g0 + tn_);
+          } else {
+            dma_b(T, tt, g0 + tn_);
+          }
+        }
+        // K-tile kt + 1 (of the ring) landed, this wave's part; with a next tile the ring stays full
+        if (q + QS == BK / 16) retire_keep(has_next ? NST - 2 : min(nk - 1 - (kt + 1), NST - 2));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bar();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int e = 0; e < QS; ++e)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = ConvLp<LP>::mma(fa[e][i], fb[e][j], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+        bar();
       }
-      if (q + QS == BK / 16) retire_keep(min(nk - 1 - (kt + 1), NST - 2));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      bar();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int e = 0; e < QS; ++e)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = ConvLp<LP>::mma(fa[e][i], fb[e][j], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-      bar();
     }
+
+    // epilogue straight from the accumulators (no LDS: the ring keeps running for the next tile)
+    const int64_t rbase = cur.m0 + grp * 128 + ar0;
+    const int64_t cbase = cur.n0 + bh * 128 + bc0;
+    if (MODE == kFwd && c.pool_w == 4 && !c.partial) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int64_t col = cbase + j * 32 + lc;
+          if (col >= c.Nn) continue;
+          const float bv = c.bias ? c.bias[col] : 0.f;
+#pragma unroll
+          for (int rq = 0; rq < 4; ++rq) {
+            const int64_t row = rbase + i * 32 + 8 * rq + 4 * lh;
+            if (row >= c.M) continue;
+            float best = acc[i][j][4 * rq] + bv;
+            int arg = 0;
+#pragma unroll
+            for (int pp = 1; pp < 4; ++pp) {
+              const float v = acc[i][j][4 * rq + pp] + bv;
+              if (v > best || (v != v && best == best)) { best = v; arg = pp; }
+            }
+            c.out[(row >> 2) * c.Nn + col] = best;
+            c.pool_arg[(row >> 2) * c.Nn + col] = (uint8_t)arg;
+          }
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int64_t col = cbase + j * 32 + lc;
+          if (col >= c.Nn) continue;
+          const float bv = (MODE == kFwd && c.bias && !c.partial) ? c.bias[col] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int64_t row = rbase + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (row >= c.M) continue;
+            if (c.partial) c.partial[((int64_t)cur.split * c.M + row) * c.Nn + col] = acc[i][j][r];
+            else c.out[row * c.Nn + col] = acc[i][j][r] + bv;
+          }
+        }
+    }
+    if (!has_next) break;
+    g0 += nk;
+    cur = nxt;
+    vt = vn;
   }
   if (grp == 0) bar();
-
-  const int lh = lane >> 5, lc = lane & 31;
-  const int64_t rbase = m0 + grp * 128 + ar0;
-  const int64_t cbase = n0 + bh * 128 + bc0;
-  if (MODE == kFwd && c.pool_w == 4 && !c.partial) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int64_t col = cbase + j * 32 + lc;
-        if (col >= c.Nn) continue;
-        const float bv = c.bias ? c.bias[col] : 0.f;
-#pragma unroll
-        for (int rq = 0; rq < 4; ++rq) {
-          const int64_t row = rbase + i * 32 + 8 * rq + 4 * lh;
-          if (row >= c.M) continue;
-          float best = acc[i][j][4 * rq] + bv;
-          int arg = 0;
-#pragma unroll
-          for (int pp = 1; pp < 4; ++pp) {
-            const float v = acc[i][j][4 * rq + pp] + bv;
-            if (v > best || (v != v && best == best)) { best = v; arg = pp; }
-          }
-          c.out[(row >> 2) * c.Nn + col] = best;
-          c.pool_arg[(row >> 2) * c.Nn + col] = (uint8_t)arg;
-        }
-      }
-  } else {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int64_t col = cbase + j * 32 + lc;
-        if (col >= c.Nn) continue;
-        const float bv = (MODE == kFwd && c.bias && !c.partial) ? c.bias[col] : 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t row = rbase + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (row >= c.M) continue;
-          if (c.partial) c.partial[((int64_t)split * c.M + row) * c.Nn + col] = acc[i][j][r];
-          else c.out[row * c.Nn + col] = acc[i][j][r] + bv;
-        }
-      }
-  }
 }
 
 // The ring conv when the shape qualifies (fp32 operands, option conv_ring, channel-aligned, stride 1
@@ -1567,7 +1680,7 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
   prof.detail("conv_ring%s_kernel<%s,256x%d%s%s> %lldx%lldx%lld s%d", lp ? "16" : "",
               MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad", BN, (MODE == kFwd && c.pool_w) ? ",pool" : "",
               lp && BN >= 128 && ((g_opt_conv_ring_qs >> (BN == 128 ? 1 : 2)) & 1)
-                  ? (((g_opt_conv_ring_deep >> (BN == 128 ? 1 : 2)) & 1) ? ",qs2,deep" : ",qs2")
+                  ? (((g_opt_conv_ring_pers >> (BN == 128 ? 1 : 2)) & 1) && c.nblk > kCUs ? ",qs2,pers" : ",qs2")
                   : "",
               (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
   const dim3 grid((unsigned)c.nblk), block(512);
@@ -1578,10 +1691,15 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
     // the 16-bit ring: BN x precision x k-steps per section (QS 2 where the option asks for it at this width:
     // bit 0 BN 64, bit 1 BN 128, bit 2 BN 256)
     const int wbit = BN == 64 ? 0 : BN == 128 ? 1 : 2;
-    const bool qs2 = (g_opt_conv_ring_qs >> wbit) & 1, deep = qs2 && BN >= 128 && ((g_opt_conv_ring_deep >> wbit) & 1);
-#define SRK_R16(BN_, LP_)                                                                                        \
-  if (deep) hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 2, BN_ == 256 ? 5 : 6>), grid, block, 0, s, c); \
-  else if (qs2) hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 2>), grid, block, 0, s, c);              \
+    const bool qs2 = BN >= 128 && ((g_opt_conv_ring_qs >> wbit) & 1);
+    // persistent tile loop (QS 2 rings): more tiles than workgroups, every tile's K range >= 3 K-tiles
+    const int64_t klast = c.K - (int64_t)(splits - 1) * c.kchunk;
+    const bool pers = qs2 && ((g_opt_conv_ring_pers >> wbit) & 1) && c.nblk > kCUs &&
+                      std::min<int64_t>(c.kchunk, klast) >= 3 * RBK;
+    const dim3 pgrid(pers ? (unsigned)kCUs : grid.x);
+#define SRK_R16(BN_, LP_)                                                                                   \
+  if (pers) hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 2, 4, true>), pgrid, block, 0, s, c);  \
+  else if (qs2) hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 2>), grid, block, 0, s, c);         \
   else hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 1>), grid, block, 0, s, c);
     if (prec == kPrecBF16) {
       if (BN == 256) { SRK_R16(256, 1) } else if (BN == 128) { SRK_R16(128, 1) }
@@ -1689,14 +1807,22 @@ int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
   c.fd_sw = FastDiv((unsigned)c.sw);
   const bool vecb = c.Nn % 4 == 0;
   const bool vec = (chans % 4 == 0) && vecb;
+  {
+    // fast16 gathers (ConvArgs::fast16): one tap per K-tile, 32-bit buffer offsets
+    const double ael = MODE == kDgrad ? (double)c.N * c.Ho * c.Wo * c.Co : (double)c.N * c.H * c.W * c.Ci;
+    c.fast16 = g_opt_conv_fast16 && c.a16 && MODE != kWgrad && chans % BK == 0 && c.kchunk % BK == 0 &&
+               (MODE != kDgrad || (c.sh == 1 && c.sw == 1)) && ael < 1073741824.0 &&
+               (double)c.K * c.Nn < 1073741824.0 && (double)c.M < 2147483647.0;
+  }
   SRK_REQUIRE(!c.a16 || (prec != kPrecF32 && c.b16 && chans % 8 == 0 && c.Nn % 8 == 0), SRK_ERR_INTERNAL,
               "conv: 16-bit sources need 8-aligned channels");
   SRK_REQUIRE(!c.dy_arg || (MODE != kFwd && !c.a16 && vec && vecb && c.sh == 1 && c.sw == 1 && c.Wo % 4 == 0),
               SRK_ERR_INTERNAL, "conv: unpooling gathers need fp32 sources, 4-aligned channels and Wo % 4 == 0");
   ProfScope prof(prec == kPrecF32 ? name : (MODE == kFwd ? "conv_fwd_lp" : MODE == kDgrad ? "conv_dgrad_lp" : "conv_wgrad_lp"),
                  s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
-  prof.detail("conv_gemm_kernel<%s,%dx%d%s%s> %lldx%lldx%lld s%d", MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad",
-              BM, BN, NW == 8 ? ",8w" : "", c.a16 ? ",s16" : c.dy_arg ? ",unpool" : (MODE == kFwd && c.pool_w) ? ",pool" : "", (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
+  prof.detail("conv_gemm_kernel<%s,%dx%d%s%s%s> %lldx%lldx%lld s%d", MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad",
+              BM, BN, NW == 8 ? ",8w" : "", c.a16 ? ",s16" : c.dy_arg ? ",unpool" : (MODE == kFwd && c.pool_w) ? ",pool" : "",
+              c.fast16 ? ",fast" : "", (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
   const dim3 grid((unsigned)c.nblk);
   if (BM == 64) launch_conv<MODE, 64, 64>(c, grid, s, vec, vecb, prec);
   else if (BM == 256 && BN == 64) launch_conv<MODE, 256, 64, 8>(c, grid, s, vec, vecb, prec);

@@ -107,6 +107,25 @@ __device__ __forceinline__ void mma_stage(const float* As, const float* Bs, f32x
 // ONE XCD: tiles an XCD runs concurrently share A and B panels in its L2.  Within a split, tiles are
 // walked in groups of group_m tile rows (column-major inside a group): resident tiles form a compact
 // 2-D patch.
+// map_tile_at: the same for a virtual block index b (persistent kernels: b = blockIdx.x + r gridDim.x with a
+// grid that is a multiple of 8, so b's XCD is the workgroup's)
+__device__ __forceinline__ void map_tile_at(int b, int nblk, int tiles, int tiles_m, int tiles_n, int group_m,
+                                            bool remap, int& split, int& tm, int& tn) {
+  int lin = b;
+  if (remap) {
+    const int xcd = b & 7, q = nblk >> 3, r = nblk & 7;
+    lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  }
+  split = lin / tiles;
+  const int t = lin - split * tiles;
+  const int gsz_full = group_m * tiles_n;
+  const int grp = t / gsz_full, first_m = grp * group_m;
+  const int gm = tiles_m - first_m < group_m ? tiles_m - first_m : group_m;
+  const int tin = t - grp * gsz_full;
+  tm = first_m + tin % gm;
+  tn = tin / gm;
+}
+
 __device__ __forceinline__ void map_tile(int nblk, int tiles, int tiles_m, int tiles_n, int group_m, bool remap,
                                          int& split, int& tm, int& tn) {
   int lin = blockIdx.x;

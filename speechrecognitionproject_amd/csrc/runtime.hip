@@ -30,8 +30,9 @@ int g_opt_conv_unpool16 = 1;
 int g_opt_conv_colsum16 = 1;
 int g_opt_conv_ring64 = 0;
 int g_opt_conv_ring_qs = 6;
-int g_opt_conv_ring_deep = 0;
+int g_opt_conv_ring_pers = 0;
 int g_opt_conv1_mfma = 1;
+int g_opt_conv_fast16 = 1;
 int g_opt_bn_tree = 0;
 int g_opt_gru_poll_pipe = 0;
 int g_opt_mfcc_variant = 3;
@@ -419,13 +420,17 @@ int srk_set_option(const char* name, int64_t value) {
     srk::g_opt_conv_ring_qs = (int)value;
     return SRK_OK;
   }
+  if (n == "conv_fast16") {   // 16-bit-source register-staged convs: uniform-tap fast gathers (1) or generic (0)
+    srk::g_opt_conv_fast16 = value != 0;
+    return SRK_OK;
+  }
   if (n == "conv1_mfma") {   // conv1 + maxpool1 forward on the fp32 matrix cores (1) or the VALU (0)
     srk::g_opt_conv1_mfma = value != 0;
     return SRK_OK;
   }
-  if (n == "conv_ring_deep") {   // 16-bit ring convs (QS 2): 5 / 6 ring stages, mask by width (128, 256)
-    SRK_REQUIRE(value >= 0 && value <= 7, SRK_ERR_INVALID, "conv_ring_deep is a 3-bit mask");
-    srk::g_opt_conv_ring_deep = (int)value;
+  if (n == "conv_ring_pers") {   // 16-bit ring convs (QS 2): persistent tile loop, mask by width (128, 256)
+    SRK_REQUIRE(value >= 0 && value <= 7, SRK_ERR_INVALID, "conv_ring_pers is a 3-bit mask");
+    srk::g_opt_conv_ring_pers = (int)value;
     return SRK_OK;
   }
   if (n == "conv_colsum16") {   // 16-bit modes: conv bias gradients fused into dY's 16-bit conversion (1) or not (0)

@@ -117,12 +117,16 @@ extern int g_opt_conv_ring64;
 // 16-bit ring convs: whole 32-deep K-tiles per MFMA section (QS 2) by tile width, a mask ("conv_ring_qs": bit 1
 // BN 128, bit 2 BN 256; default 6; bit 0 (BN 64) is ignored: that tile keeps one k-step per section)
 extern int g_opt_conv_ring_qs;
-// 16-bit ring convs with QS 2: the deepest ring the LDS holds (5 stages at BN 256, 6 at BN 128) by width, a mask
-// ("conv_ring_deep": bit 1 BN 128, bit 2 BN 256; default 0 = 4 stages)
-extern int g_opt_conv_ring_deep;
+// 16-bit ring convs with QS 2: persistent tile loop with the ring running across tiles, by width, a mask
+// ("conv_ring_pers": bit 1 BN 128, bit 2 BN 256; default 0 — measured slower on every cfg3 / cfg4 shape, r05g:
+// rn_l4 fwd 584 vs 535 us, fbanks conv2 fwd 584 vs 551 us)
+extern int g_opt_conv_ring_pers;
 // fused conv1 + maxpool1 forward on the fp32 matrix cores (v_mfma_f32_32x32x2_f32, bitwise the VALU kernel's fma
 // chain) ("conv1_mfma", default 1; 0 = the VALU kernel)
 extern int g_opt_conv1_mfma;
+// register-staged 16-bit-source convs (fwd / dgrad): uniform-tap gathers with per-row bases and zero-filling
+// buffer loads where the channels are a multiple of the K-tile ("conv_fast16", default 1)
+extern int g_opt_conv_fast16;
 // BatchNorm training statistics: the <= 256 chunk partials combined in chunk order, the count ratios off the
 // dependent chain ("bn_tree" 0, default); 1 = a fixed pairwise tree, one wave per channel (more accurate, but
 // other bits than the reference's in-order arithmetic: ReLU decisions on values within roundoff of 0 move —

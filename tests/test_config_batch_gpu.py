@@ -26,9 +26,14 @@ reference fp32 arithmetic's worst tensor (max-abs relative) — a sanity bound o
 
 The bf16 records of the driver's line (cfg3-bf16, cfg4-bf16) are pinned here at the same shapes: one
 full 16-bit train step each (forward, backward, the fused Adam) against the fp32 oracle — logits and
-loss <= 2e-2, every gradient tensor norm-wise <= 2e-2 (cfg4: against float64, widened to 1.25 x the
-fp32 oracle's own error on the BatchNorm-cancellation tensors), the Adam update (tests/lowprec_checks.py).
+loss <= 2e-2, every gradient tensor norm-wise <= 2e-2 (cfg4: against float64, widened to 1.5 x the
+error of the oracle step with bf16-rounded conv operands — bf16 rounding alone puts resnet_bgru's conv /
+BatchNorm gradients 4-34 % from float64, tools/bf16_emul_resnet.py), the Adam update
+(tests/lowprec_checks.py).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -268,10 +273,11 @@ def test_resnet_bgru_bf16_train_step_at_cfg4_batch(gpu, cfg4_case, cfg4_f64):
     """cfg4-bf16 (the driver line's record): the rank-shard step (B = 512, training-mode BatchNorm) with
     bf16 operands on every conv, GEMM and the 16-bit recurrence — the ring convs, the BatchNorm-emitted
     16-bit copies, the BiGRU layer hand-over.  Logits and loss <= 2e-2 of the fp32 oracle.  Gradients:
-    norm-wise against FLOAT64, each tensor within max(2e-2, 1.25 x the fp32 oracle's own norm-wise error
-    on that tensor) — the BatchNorm-cancellation weight gradients (module docstring) are not resolved
-    better than that by the reference's fp32 arithmetic either.  BatchNorm running statistics <= 2e-2,
-    and the Adam update (tests/lowprec_checks.py)."""
+    norm-wise against FLOAT64, each tensor within max(2e-2, 1.25 x the fp32 oracle's own error, 1.5 x the
+    error of the oracle step with bf16-rounded conv operands) — bf16 rounding alone puts this model's
+    conv / BatchNorm gradients 4-34 % from float64 (the emulated oracle and the HIP step agree on that to
+    a factor 0.74-1.24 per tensor, r05f).  BatchNorm running statistics <= 2e-2, and the Adam update
+    (tests/lowprec_checks.py)."""
     from speechrecognitionproject_amd.models import model_resnet_bgru
     x, y, sd, ref, want, want_loss = cfg4_case
     net = model_resnet_bgru.Network().cuda()
@@ -282,13 +288,26 @@ def test_resnet_bgru_bf16_train_step_at_cfg4_batch(gpu, cfg4_case, cfg4_f64):
     assert abs(loss - want_loss) <= LOGITS_REL_LOWPREC * max(1.0, abs(want_loss))
     p32 = {n: p.grad.detach() for n, p in ref.named_parameters() if p.grad is not None}
     p64 = {n: p.grad.detach() for n, p in cfg4_f64.named_parameters() if p.grad is not None}
+    # FlatParams hands every parameter a .grad view: those the forward does not use (the mode-1 backend) stay 0
+    for n in set(grads) - set(p64):
+        assert grads[n].abs().max().item() == 0.0, n
+    grads = {n: g for n, g in grads.items() if n in p64}
     assert set(grads) == set(p64), set(grads) ^ set(p64)
+    # bf16 operand rounding itself moves this model's conv / BatchNorm gradients 4-34 % norm-wise (the
+    # training-BatchNorm backward chain amplifies it): the oracle step with bf16-rounded Conv1d operands and fp32
+    # accumulation lands that far from float64 too (tests/golden/cfg4_bf16_emul_nw.json, tools/bf16_emul_resnet.py,
+    # same clips and weights).  Each tensor: within 1.5 x that emulated error, or 2e-2, or 1.25 x the fp32 oracle's.
+    fix = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "cfg4_bf16_emul_nw.json")))
+    emul, emul_adam = fix["bf16conv_nw"], fix["bf16conv_adam_dis"]
     spread = {n: normwise(p32[n], p64[n]) or 0.0 for n in p64}
-    check_grads(grads, p64, bound=lambda n: max(LP_GRAD_REL, 1.25 * spread[n]))
+    check_grads(grads, p64, bound=lambda n: max(LP_GRAD_REL, 1.25 * spread[n], 1.5 * emul.get(n, 0.0)))
     refb = dict(ref.named_buffers())
     for n, b in net.named_buffers():
         if n.endswith("running_mean") or n.endswith("running_var"):
             assert rel_err(b.cpu().numpy(), refb[n].numpy()) <= LOGITS_REL_LOWPREC, n
     p0_ref = {n: sd[n].clone() for n in p0}
+    # the update's disagreement with the fp32 oracle's Adam step: as bounded elsewhere, or 1.5 x the emulated
+    # bf16 oracle's own (the same bf16-rounding origin as the gradient bound above)
     check_adam([(n, p) for n, p in net.named_parameters() if n in grads], p0,
-               grads, p0_ref, {n: p32[n] for n in grads}, LR)
+               grads, p0_ref, {n: p32[n] for n in grads}, LR,
+               update_bound=lambda n: max(LP_UPDATE_WEIGHTED, 1.5 * emul_adam.get(n, 0.0)))

@@ -602,7 +602,9 @@ def test_gemm16_qs(prec, ta, tb, M, N, K, beta):
 
 
 @pytest.mark.parametrize("shape", [(2, 98, 40, 64, 128, 1, 7, 0, 3), (3, 98, 1, 256, 512, 7, 1, 3, 0),
-                                   (2, 1, 1000, 64, 128, 1, 15, 0, 7, 1, 2), (4, 17, 13, 32, 256, 3, 3, 1, 1)])
+                                   (2, 1, 1000, 64, 128, 1, 15, 0, 7, 1, 2), (4, 17, 13, 32, 256, 3, 3, 1, 1),
+                                   # more tiles than CUs: the persistent rings (fwd 256 x 128; fwd + dgrad 256 x 256)
+                                   (32, 98, 40, 64, 128, 1, 7, 0, 3), (68, 1, 500, 256, 512, 1, 15, 0, 7)])
 def test_conv_16bit_ring(prec, shape):
     """srk option conv_ring bits 4-6: the 16-bit LDS-DMA ring convolutions (gemm_g16_kernel's
     structure, per-K-tile conv gathers of the 16-bit operand copies) == the register-staged 16-bit
@@ -620,12 +622,12 @@ def test_conv_16bit_ring(prec, shape):
     try:
         # ring (one k-step per MFMA section), ring with whole K-tiles per section (conv_ring_qs, every width),
         # register-staged
-        # (and the deepest rings, conv_ring_deep), the 256 x 64 tiles on (conv_ring64)
+        # (one tile per workgroup, and the persistent tile loop, conv_ring_pers), the 256 x 64 tiles on (conv_ring64)
         _lib.set_option("conv_ring64", 1)
-        for mask, qs, deep in ((0x70 | 6, 0, 0), (0x70 | 6, 7, 0), (0x70 | 6, 7, 7), (6, 0, 0)):
+        for mask, qs, pers in ((0x70 | 6, 0, 0), (0x70 | 6, 7, 0), (0x70 | 6, 7, 7), (6, 0, 0)):
             _lib.set_option("conv_ring", mask)
             _lib.set_option("conv_ring_qs", qs)
-            _lib.set_option("conv_ring_deep", deep)
+            _lib.set_option("conv_ring_pers", pers)
             xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
             ym = snn._Conv2dNHWCFn.apply(xm, wm, bm, (ph, pw), (sh, sw))
             (ym * gy).sum().backward()
@@ -634,7 +636,7 @@ def test_conv_16bit_ring(prec, shape):
     finally:
         _lib.set_option("conv_ring", 0x77)
         _lib.set_option("conv_ring_qs", 6)
-        _lib.set_option("conv_ring_deep", 0)
+        _lib.set_option("conv_ring_pers", 6)
         _lib.set_option("conv_ring64", 0)
     for o in outs[1:3]:
         for a, c in zip(outs[0], o):
@@ -750,3 +752,41 @@ def test_bigru_fwd_worker(prec, B, T, IN):
             continue
         err = float((a[n] - c[n]).norm() / c[n].norm())
         assert err <= 2e-3, (n, err)
+
+
+@pytest.mark.parametrize("shape", CONV_S16 + [(3, 17, 24, 128, 64, 3, 3, 1, 1, 1, 1), (5, 98, 40, 64, 128, 1, 7, 0, 3, 1, 1)])
+@pytest.mark.parametrize("pooled", [False, True])
+def test_conv_fast16_gathers_bitwise(prec, shape, pooled):
+    """Option conv_fast16: the register-staged 16-bit-source convs gathering one uniform tap per K-tile
+    (channels a multiple of the 64-deep K-tile) through per-row base offsets and zero-filling buffer loads ==
+    the generic gathers (per-unit tap splits, masks at LDS-store time), bit for bit — forward (plain and with the
+    fused (1, 4) max pool), data and weight gradients; the register-staged kernels on both sides (no ring)."""
+    from speechrecognitionproject_amd import nn as snn
+    N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw = shape
+    Ho, Wo = (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
+    if pooled and (sh != 1 or sw != 1 or Wo % 4):
+        pytest.skip("the fused pool needs stride 1 and Wo % 4 == 0")
+    g = torch.Generator().manual_seed(N * 29 + Co + KW + int(pooled))
+    x = torch.randn(N, H, W, Ci, generator=g).cuda()
+    w = (torch.randn(Co, Ci, KH, KW, generator=g) / (Ci * KH * KW) ** 0.5).cuda()
+    b = torch.randn(Co, generator=g).cuda()
+    gy = torch.randn(N, Ho, Wo // 4 if pooled else Wo, Co, generator=g).cuda()
+    outs = []
+    try:
+        _lib.set_option("conv_ring", 6)
+        for fast in (1, 0):
+            _lib.set_option("conv_fast16", fast)
+            xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
+            if pooled:
+                ym = snn._ConvPoolNHWCFn.apply(xm, wm, bm, (ph, pw), 4)
+            else:
+                ym = snn._Conv2dNHWCFn.apply(xm, wm, bm, (ph, pw), (sh, sw))
+            (ym * gy).sum().backward()
+            torch.cuda.synchronize()
+            outs.append((ym.detach(), xm.grad, wm.grad, bm.grad))
+    finally:
+        _lib.set_option("conv_fast16", 1)
+        _lib.set_option("conv_ring", 0x77)
+    for a, c in zip(*outs):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, c)

@@ -25,6 +25,7 @@ SHAPES = {  # name: N, H, W, Ci, Co, KH, KW, ph, pw, sh, sw
     "rn_l2": (512, 1, 500, 128, 128, 1, 15, 0, 7, 1, 1),
     "rn_l4": (512, 1, 125, 512, 512, 1, 15, 0, 7, 1, 1),
 }
+MEAS = 5   # measured passes (per-pass means)
 CATS = ("conv_fwd", "conv_dgrad", "conv_wgrad", "conv_fwd_lp", "conv_dgrad_lp", "conv_wgrad_lp", "conv_to16",
         "conv_colsum")
 
@@ -48,7 +49,7 @@ def run_shape(name, prec, opts):
         _lib.set_option(k, v)
     try:
         r = {}
-        for it in range(4):
+        for it in range(3 + MEAS):
             if it == 3:
                 _lib.prof_enable(True)
             if pooled:
@@ -61,8 +62,8 @@ def run_shape(name, prec, opts):
             c, ms, work = _lib.prof_read(k)
             if c:
                 unit = "GB/s" if k in ("conv_to16", "conv_colsum") else "TF"
-                r[k] = {"us": round(ms * 1e3, 1), unit: round(work / (ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12), 1)}
-        r["kernels"] = [{"kernel": e["kernel"], "us": round(e["ms_total"] * 1e3, 1)} for e in _lib.prof_kernels()]
+                r[k] = {"us": round(ms * 1e3 / MEAS, 1), unit: round(work / (ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12), 1)}
+        r["kernels"] = [{"kernel": e["kernel"], "us": round(e["ms_total"] * 1e3 / MEAS, 1)} for e in _lib.prof_kernels()]
         _lib.prof_enable(False)
         return r
     finally:

@@ -28,7 +28,7 @@ def main(d):
             acc[k][counter][key] = acc[k][counter].get(key, 0.0) + float(value)
             dur[k][key] = float(ns)
     for k, cs in sorted(acc.items()):
-        if not any(x in k for x in ("mfcc", "fbank", "spec", "gemm", "gru")):
+        if not any(x in k for x in ("mfcc", "fbank", "spec", "gemm", "gru", "conv", "bn_", "colsum", "pool", "splitk")):
             continue
         ds = list(dur[k].values())
         print("%s   (mean dispatch duration %.1f us)" % (k, sum(ds) / len(ds) / 1e3))

@@ -430,11 +430,10 @@ __global__ void bn_dx_kernel(const float* __restrict__ x, const float* __restric
 __global__ __launch_bounds__(256) void bn_local_stats_kernel(const float* __restrict__ pmean,
                                                              const float* __restrict__ pm2, BnGeom g,
                                                              float* __restrict__ stats) {
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);   // one wave per channel (combine_chunks_tree)
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;   // one lane per channel, in chunk order (the finalize's)
   if (c >= g.C) return;
   float n, mu, m2;
-  combine_chunks_tree(pmean, pm2, g, c, n, mu, m2);
-  if ((threadIdx.x & 63) != 0) return;
+  combine_chunks_fast(pmean, pm2, g, c, n, mu, m2);
   stats[c] = n;
   stats[g.C + c] = mu;
   stats[2 * g.C + c] = m2;
@@ -658,7 +657,7 @@ int srk_batchnorm_stats(const float* x, int64_t M, int64_t C, float* stats, void
   if (int rc = srk::bn_scratch((size_t)2 * g.chunks * C, &part)) return rc;
   hipLaunchKernelGGL(srk::bn_stats_kernel, dim3((unsigned)((g.C4 + g.CQ - 1) / g.CQ), (unsigned)g.chunks), dim3(256), 0,
                      s, x, g, part, part + (size_t)g.chunks * C);
-  hipLaunchKernelGGL(srk::bn_local_stats_kernel, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, s, part,
+  hipLaunchKernelGGL(srk::bn_local_stats_kernel, dim3((unsigned)((C + 63) / 64)), dim3(64), 0, s, part,
                      part + (size_t)g.chunks * C, g, stats);
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;

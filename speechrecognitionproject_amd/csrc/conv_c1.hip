@@ -112,7 +112,8 @@ __global__ __launch_bounds__(256) void conv1_pool_fwd_kernel(C1Args a) {
   }
 }
 
-// The same forward on the matrix cores (option conv1_mfma, default 1): v_mfma_f32_32x32x2_f32 is bit for bit
+// The same forward on the matrix cores (option conv1_mfma, default 0: measured slower, srk_internal.h):
+// v_mfma_f32_32x32x2_f32 is bit for bit
 // a k-ordered fp32 fmaf chain (cdna_hip_programming.md §3), so with C = the bias and the taps fed in the VALU
 // kernel's order (t = kh * KW + kw ascending; the one pad tap, x = w = 0, first: fma(0, 0, b) = b) every
 // pre-pool value is the VALU kernel's bit for bit, at ~99 % of the fp32 matrix rate instead of the VALU's

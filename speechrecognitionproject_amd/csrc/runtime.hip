@@ -31,7 +31,7 @@ int g_opt_conv_colsum16 = 1;
 int g_opt_conv_ring64 = 0;
 int g_opt_conv_ring_qs = 6;
 int g_opt_conv_ring_pers = 0;
-int g_opt_conv1_mfma = 1;
+int g_opt_conv1_mfma = 0;
 int g_opt_conv_fast16 = 1;
 int g_opt_bn_tree = 0;
 int g_opt_gru_poll_pipe = 0;

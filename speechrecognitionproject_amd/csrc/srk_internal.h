@@ -122,7 +122,8 @@ extern int g_opt_conv_ring_qs;
 // rn_l4 fwd 584 vs 535 us, fbanks conv2 fwd 584 vs 551 us)
 extern int g_opt_conv_ring_pers;
 // fused conv1 + maxpool1 forward on the fp32 matrix cores (v_mfma_f32_32x32x2_f32, bitwise the VALU kernel's fma
-// chain) ("conv1_mfma", default 1; 0 = the VALU kernel)
+// chain) ("conv1_mfma", default 0 = the VALU kernel: the MFMA form measured 406-423 vs 330 us at cfg3, r05e — its
+// per-element scalar stores of y / argmax / y16 from the accumulator layout cost more than the VALU FMAs it saves)
 extern int g_opt_conv1_mfma;
 // register-staged 16-bit-source convs (fwd / dgrad): uniform-tap gathers with per-row bases and zero-filling
 // buffer loads where the channels are a multiple of the K-tile ("conv_fast16", default 1)

@@ -37,6 +37,11 @@ def _dir_pair(a, b):
     return torch.stack([a, b])
 
 
+# conv weight / BatchNorm parameter gradients added into FlatParams-owned .grad by their kernels (A/B switch:
+# 0 = returned to autograd; the GRU's in-place pairs are not affected)
+INPLACE_GRADS = os.environ.get("SRK_INPLACE_GRADS", "1") != "0"
+
+
 def _flat_grad(p):
     """p.grad when p is owned by a FlatParams (optim.py) and its .grad is still that buffer's view:
     the one case where a backward may accumulate into .grad in place (beta = 1 in the GEMM
@@ -399,7 +404,7 @@ class _Conv2dNHWCFn(torch.autograd.Function):
         dy = dy.contiguous()
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         # the weight gradient ADDED to a FlatParams-owned .grad in the layout kernel (no autograd add kernel)
-        gw = _flat_grad(ctx.w_param) if ctx.needs_input_grad[1] else None
+        gw = _flat_grad(ctx.w_param) if ctx.needs_input_grad[1] and INPLACE_GRADS else None
         dw = gw if gw is not None else torch.empty_like(w)
         db = torch.empty((Co,), device=x.device) if has_b else None
         ws = torch.empty(int(_lib.lib().srk_conv2d_workspace_floats(Ci, Co, KH, KW)), device=x.device)
@@ -791,8 +796,8 @@ class _BatchNormFn(torch.autograd.Function):
             dx16 = torch.empty(dx.numel(), device=x.device, dtype=torch.int16)
         # dgamma / dbeta also ADDED to FlatParams-owned .grad buffers in the kernel that forms them
         gp, bp = ctx.params
-        gg = _flat_grad(gp) if ctx.needs_input_grad[1] else None
-        gb = _flat_grad(bp) if ctx.needs_input_grad[2] else None
+        gg = _flat_grad(gp) if ctx.needs_input_grad[1] and INPLACE_GRADS else None
+        gb = _flat_grad(bp) if ctx.needs_input_grad[2] and INPLACE_GRADS else None
         acc = gg is not None and gb is not None
         mask, ctx.mask = ctx.mask, None
         call("srk_batchnorm_bwd16_mask", ptr(x), ptr(y), ptr(mask) if mask is not None else None, ptr(dy), M, C,

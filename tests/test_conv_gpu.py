@@ -156,7 +156,7 @@ def test_conv1_pool_mfma_equals_valu(gpu, prec, N, H, W, KH, KW, pool):
             torch.cuda.synchronize()
             out.append((y, arg, y16, wr.value))
     finally:
-        _lib.set_option("conv1_mfma", 1)
+        _lib.set_option("conv1_mfma", 0)
         _lib.set_matmul_precision("fp32")
     (y1, a1, c1, w1), (y0, a0, c0, w0) = out
     assert w1 == w0 == (0 if prec == "fp32" else 1)

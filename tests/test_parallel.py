@@ -442,8 +442,12 @@ def test_dp_syncbn_overlap_matches_global_batch(gpu, mode):
         # 139 elements of layer4.0.downsample in mode 1); a wrong sign or scale would exceed it
         assert dg.max().item() <= 0.2 * gmax + 3.0 * fl.abs().max().item() + 1e-9, (n, dg.max().item(), gmax)
         d = (res[0][0][sl] - p1[sl]).abs()
-        sure = g1.abs() > 2.0 * dg.max() + 1e-12    # no sign flip possible: Adam's first step is lr * sign(g)
-        assert d[sure].max().item() <= 2e-6 if sure.any() else True, n
+        # no sign flip possible, and |g| >> Adam's eps (1e-8), where its first step is lr * sign(g): at |g| ~ 1e-7 a
+        # 2e-8 gradient difference alone moves lr g / (|g| + eps) by 2e-6 (r05h: layer3.1.conv2, g 8.9e-8 vs 7.2e-8)
+        sure = g1.abs() > torch.clamp(2.0 * dg.max(), min=1e-6)
+        if sure.any():
+            k = int(torch.argmax(torch.where(sure, d, torch.zeros_like(d))))
+            assert d[sure].max().item() <= 2e-6, (n, d[k].item(), g1[k].item(), g2[k].item(), dg.max().item())
         assert d.max().item() <= 2e-4 + 1e-6, n
         assert (p1[sl] - p0[sl]).abs().max().item() <= 1e-4 * 1.001 + 1e-7, n   # Adam's first step
     mine = {n: b.cpu() for n, b in net.named_buffers()}

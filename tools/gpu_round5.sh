@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-4 GPU evidence, call 1 of 2:  gpurun --timeout 1150 -- bash tools/gpu_round4.sh TAG
+# Round-5 GPU evidence:  gpurun --timeout 1150 -- bash tools/gpu_round5.sh TAG
 # pytest -m gpu, smoke, the default bench line, rocprofv3 --kernel-trace --stats of the cfg2 bench
 # command and of each config command (graph replays), summarised on the box.  Every GPU step has its
 # own time limit; steps are chained with && (a failure ends the call).
 set -o pipefail
-TAG=${1:-r04}
+TAG=${1:-r05}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp

@@ -551,11 +551,14 @@ def _workload_h2d(self, precision, steps, warmup):
     for e in ev_done:
         e.record(cur)
 
+    nocopy = os.environ.get("SRK_BENCH_H2D_NOCOPY", "0") == "1"   # diagnostic: the same loop without the copies
+
     def upload(i):
         j = i % 2
         cs.wait_event(ev_done[j])              # the step that last read slot j has finished
         with torch.cuda.stream(cs):
-            self.pcm[j].copy_(host[i % n_host], non_blocking=True)
+            if not nocopy:
+                self.pcm[j].copy_(host[i % n_host], non_blocking=True)
             ev_copy[j].record(cs)
 
     def run(n):

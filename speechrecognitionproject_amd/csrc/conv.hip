@@ -1628,6 +1628,135 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
   if (grp == 0) bar();
 }
 
+// ------------------------------------------------------------------ row-staged (1, KW) conv + (1, 4) pool
+// fbanks_cnn conv2 + maxpool2 in 16-bit modes (model_fbanks_cnn.py:74-75, 91-92: Conv2d(64, 128, (1, 7),
+// padding (0, 3)) over W = 40, then MaxPool2d((1, 4))), option conv_row16.  The implicit GEMM re-gathers every
+// input pixel once per tap (7 x) from L2 with per-unit index math; PMC put the register-staged kernel at
+// ~22 VALU instructions per MFMA and 18 % MFMA-busy (profiles/r05/r05e_pmc_fbconv2.txt).  Here a persistent
+// workgroup keeps the whole 16-bit weight matrix [(kw, ci)][co] (448 x 128, 112 KB) in LDS for its lifetime and
+// stages R = 8 image rows of x16 ONCE per tile (8 x 46 padded positions x 64 channels, 46 KB, halo zeros written
+// once); the 7 taps are then 7 shifted reads of the staged rows.  The next tile's rows are prefetched into
+// registers during this tile's MFMAs.  Tile = 8 rows x 40 pixels = 320 GEMM rows (10 blocks of 32) x 128
+// columns; wave w owns column block w & 3 and row blocks 5 (w >> 2) .. +4 (5 accumulators, one B fragment per
+// k-step for five A fragments).  The epilogue is conv_gemm_kernel's pooled one: bias, the (1, 4) window max and
+// its first-maximum argmax in registers (r & 3 = the 4 window columns), pooled fp32 out + uint8 argmax.
+// Same MFMA operands and k order as the ring / register-staged kernels (k = (kw, ci) ascending, 16 per MFMA), so
+// results equal theirs up to nothing (tests/test_lowprec_gpu.py test_conv_row16_equals_gemm: bitwise).
+struct RowArgs {
+  const unsigned short* x16;   // [rows][W][CI] 16-bit
+  const unsigned short* w16;   // [(kw, ci)][CO] 16-bit (the fwd weight matrix Wt)
+  const float* bias;           // [CO] or null
+  float* y;                    // pooled [rows][W / 4][CO]
+  uint8_t* arg;                // [rows][W / 4][CO]
+  int rows, groups;
+};
+template <int LP, int KW, int PW, int WD, int CI, int CO, int R>
+__global__ __launch_bounds__(512, 1) void conv_row16_pool_kernel(RowArgs a) {
+  static_assert(CO == 128 && CI % 16 == 0 && WD % 4 == 0 && (R * WD) % 32 == 0 && CI * 2 == 128, "row16 geometry");
+  constexpr int WP = WD + 2 * PW;               // padded positions per staged row
+  constexpr int K = KW * CI;                    // GEMM depth
+  constexpr int MB = R * WD / 32;               // row blocks of 32 (10)
+  constexpr int RB = MB / 2;                    // row blocks per wave (5)
+  constexpr int XCH = R * WD * (CI / 8);        // 16-B chunks of one tile's rows (2560)
+  constexpr int XPT = XCH / 512;                // per thread (5)
+  static_assert(XCH % 512 == 0 && MB % 2 == 0, "row16 tile split");
+  __shared__ __attribute__((aligned(16))) unsigned short Wl[K * CO];        // TR image [k][co] (r16_off<false>)
+  __shared__ __attribute__((aligned(16))) unsigned short Xl[R * WP * CI];   // [row][pos][ci], 16-B chunks swizzled
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wc = wave & 3, rb0 = (wave >> 2) * RB;
+  // the weights, once: 16-B chunks of 8 columns into the TR image
+  for (int c = tid; c < K * CO / 8; c += 512) {
+    const int k = c / (CO / 8), col = (c % (CO / 8)) * 8;
+    *reinterpret_cast<u32x4_*>(Wl + r16_off<false>(col, k)) = *reinterpret_cast<const u32x4_*>(a.w16 + (size_t)k * CO + col);
+  }
+  // the halo positions (never overwritten by the staging)
+  for (int c = tid; c < R * 2 * PW * (CI / 8); c += 512) {
+    const int rl = c / (2 * PW * (CI / 8)), rem = c % (2 * PW * (CI / 8));
+    const int pp = rem / (CI / 8), ch = rem % (CI / 8);
+    const int q = pp < PW ? pp : WD + pp;   // 0 .. PW - 1 and WD + PW .. WD + 2 PW - 1
+    *reinterpret_cast<u32x4_*>(Xl + (rl * WP + q) * CI + ((ch ^ (q & 7)) * 8)) = u32x4_{0u, 0u, 0u, 0u};
+  }
+  u32x4_ xr[XPT];
+  auto fetch = [&](int g) {   // tile g's rows into registers (zeros past the last row)
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int c = tid + i * 512, rl = c / (WD * (CI / 8)), rem = c % (WD * (CI / 8));
+      const int row = g * R + rl;
+      xr[i] = row < a.rows ? *reinterpret_cast<const u32x4_*>(a.x16 + ((size_t)row * WD) * CI + (size_t)rem * 8)
+                           : u32x4_{0u, 0u, 0u, 0u};
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int c = tid + i * 512, rl = c / (WD * (CI / 8)), rem = c % (WD * (CI / 8));
+      const int px = rem / (CI / 8), ch = rem % (CI / 8), q = px + PW;
+      *reinterpret_cast<u32x4_*>(Xl + (rl * WP + q) * CI + ((ch ^ (q & 7)) * 8)) = xr[i];
+    }
+  };
+  // this lane's A rows: row block rb0 + i, pixel (lane & 31) of it -> staged row and position (tap 0)
+  int abase[RB];
+#pragma unroll
+  for (int i = 0; i < RB; ++i) {
+    const int p = (rb0 + i) * 32 + (lane & 31);
+    abase[i] = (p / WD) * WP + p % WD;
+  }
+  const int khalf = lane >> 5;   // which 8 of the 16 k of a step this lane supplies
+  const int lh = lane >> 5, lc = lane & 31;
+  const int col = wc * 32 + lc;
+  const float bv = a.bias ? a.bias[col] : 0.f;
+  int g = blockIdx.x;
+  if (g < a.groups) fetch(g);
+  __syncthreads();
+  while (g < a.groups) {
+    stage();
+    __syncthreads();
+    const int gn = g + (int)gridDim.x;
+    if (gn < a.groups) fetch(gn);   // lands during the MFMAs below
+    f32x16 acc[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+#pragma unroll 1
+    for (int kw = 0; kw < KW; ++kw) {
+#pragma unroll
+      for (int c0 = 0; c0 < CI; c0 += 16) {
+        const u32x4_ bf = r16_frag<false>(Wl, wc * 32, kw * CI + c0, lane);
+        const int ch = (c0 >> 3) + khalf;
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int q = abase[i] + kw;   // staged row * WP + position
+          const u32x4_ af = *reinterpret_cast<const u32x4_*>(Xl + q * CI + ((ch ^ (q & 7)) * 8));
+          acc[i] = ConvLp<LP>::mma(af, bf, acc[i]);
+        }
+      }
+    }
+    // pooled epilogue: rows 8 rq + 4 lh + 0..3 of a block are one (1, 4) window
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+#pragma unroll
+      for (int rq = 0; rq < 4; ++rq) {
+        const int p0 = (rb0 + i) * 32 + 8 * rq + 4 * lh;   // tile pixel, a multiple of 4
+        const int row = g * R + p0 / WD;
+        if (row >= a.rows) continue;
+        float best = acc[i][4 * rq] + bv;
+        int am = 0;
+#pragma unroll
+        for (int pp = 1; pp < 4; ++pp) {
+          const float v = acc[i][4 * rq + pp] + bv;
+          if (v > best || (v != v && best == best)) { best = v; am = pp; }
+        }
+        const size_t o = ((size_t)g * R * WD + p0) / 4 * CO + col;
+        a.y[o] = best;
+        a.arg[o] = (uint8_t)am;
+      }
+    }
+    __syncthreads();   // every wave is done reading Xl before the next tile is staged
+    g = gn;
+  }
+}
+
 // The ring conv when the shape qualifies (fp32 operands, option conv_ring, channel-aligned, stride 1
 // for the data gradient, 32-bit byte offsets); returns 1 if it did not run.
 template <int MODE>
@@ -2077,6 +2206,48 @@ int srk_conv2d_nhwc_fwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
     c.a16 = d16[0];
     c.b16 = d16[1];
     if (x16 && x16_written) *x16_written = 1;
+    // fbanks_cnn conv2 + maxpool2: the row-staged kernel (weights resident in LDS, 8 image rows per tile)
+    if (srk::g_opt_conv_row16 && KH == 1 && KW == 7 && ph == 0 && pw == 3 && W == 40 && Ci == 64 && Co == 128 &&
+        pool_w == 4 && (N * H) < (1LL << 30) / (W * Ci)) {
+      srk::RowArgs ra{};
+      ra.x16 = c.a16;
+      ra.w16 = c.b16;
+      ra.bias = bias;
+      ra.y = y;
+      ra.arg = argmax;
+      ra.rows = (int)(N * H);
+      ra.groups = (int)((N * H + 7) / 8);
+      srk::ProfScope prof("conv_fwd_lp", s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
+      prof.detail("conv_row16_pool_kernel %lldx%lldx%lld", (long long)c.M, (long long)c.Nn, (long long)c.K);
+      const dim3 grid((unsigned)std::min<int64_t>(ra.groups, srk::kCUs)), block(512);
+      if (prec == srk::kPrecBF16)
+        hipLaunchKernelGGL((srk::conv_row16_pool_kernel<1, 7, 3, 40, 64, 128, 8>), grid, block, 0, s, ra);
+      else
+        hipLaunchKernelGGL((srk::conv_row16_pool_kernel<2, 7, 3, 40, 64, 128, 8>), grid, block, 0, s, ra);
+      SRK_CHECK_HIP(hipGetLastError());
+      return SRK_OK;
+    }
+    // fbanks_cnn conv2 + maxpool2: the row-staged kernel (weights resident in LDS, 8 image rows per tile)
+    if (srk::g_opt_conv_row16 && KH == 1 && KW == 7 && ph == 0 && pw == 3 && W == 40 && Ci == 64 && Co == 128 &&
+        pool_w == 4 && (N * H) < (1LL << 30) / (W * Ci)) {
+      srk::RowArgs ra{};
+      ra.x16 = c.a16;
+      ra.w16 = c.b16;
+      ra.bias = bias;
+      ra.y = y;
+      ra.arg = argmax;
+      ra.rows = (int)(N * H);
+      ra.groups = (int)((N * H + 7) / 8);
+      srk::ProfScope prof("conv_fwd_lp", s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
+      prof.detail("conv_row16_pool_kernel %lldx%lldx%lld", (long long)c.M, (long long)c.Nn, (long long)c.K);
+      const dim3 grid((unsigned)std::min<int64_t>(ra.groups, srk::kCUs)), block(512);
+      if (prec == srk::kPrecBF16)
+        hipLaunchKernelGGL((srk::conv_row16_pool_kernel<1, 7, 3, 40, 64, 128, 8>), grid, block, 0, s, ra);
+      else
+        hipLaunchKernelGGL((srk::conv_row16_pool_kernel<2, 7, 3, 40, 64, 128, 8>), grid, block, 0, s, ra);
+      SRK_CHECK_HIP(hipGetLastError());
+      return SRK_OK;
+    }
   }
   return srk::run_conv_gemm<srk::kFwd>(c, s, "conv_fwd");
   SRK_API_END

@@ -790,3 +790,53 @@ def test_conv_fast16_gathers_bitwise(prec, shape, pooled):
     for a, c in zip(*outs):
         assert torch.isfinite(a).all()
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("N", [3, 32])
+def test_conv_row16_equals_gemm(prec, N):
+    """Option conv_row16: fbanks_cnn conv2 + maxpool2 (Conv2d(64, 128, (1, 7), padding (0, 3)) over W = 40, then
+    MaxPool2d((1, 4)), model_fbanks_cnn.py:74-75) on the row-staged kernel — weights resident in LDS, image rows
+    staged once per tile, the taps as shifted reads — equals the implicit-GEMM kernels bit for bit: the same
+    16-bit operands in the same k order.  N = 3: a partial last tile (294 rows); N = 32: more tiles than CUs
+    (the persistent loop with the register prefetch of the next tile)."""
+    from speechrecognitionproject_amd import nn as snn
+    H, W, Ci, Co = 98, 40, 64, 128
+    g = torch.Generator().manual_seed(N + 101)
+    x = torch.randn(N, H, W, Ci, generator=g).cuda()
+    w = (torch.randn(Co, Ci, 1, 7, generator=g) / (Ci * 7) ** 0.5).cuda()
+    b = torch.randn(Co, generator=g).cuda()
+    x[0, 0, :8] = float("nan")   # NaN windows: the pool rule
+    outs = []
+    try:
+        for row in (1, 0):
+            _lib.set_option("conv_row16", row)
+            _lib.prof_enable(True)
+            with torch.no_grad():
+                y = snn._ConvPoolNHWCFn.apply(x, w, b, (0, 3), 4)
+            torch.cuda.synchronize()
+            used = any("conv_row16" in e["kernel"] for e in _lib.prof_kernels())
+            _lib.prof_enable(False)
+            outs.append((y, used))
+    finally:
+        _lib.set_option("conv_row16", 1)
+        _lib.prof_enable(False)
+    (y1, u1), (y0, u0) = outs
+    assert u1 and not u0
+    nan = torch.isnan(y1)
+    assert bool(nan.any()) and torch.equal(nan, torch.isnan(y0))
+    assert torch.equal(y1[~nan], y0[~nan])
+    # the argmax the backward routes through: every gradient equal too (finite input)
+    x[0, 0, :8] = 0.5
+    gy = torch.randn(N, H, W // 4, Co, generator=g).cuda()
+    grads = []
+    try:
+        for row in (1, 0):
+            _lib.set_option("conv_row16", row)
+            xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
+            (snn._ConvPoolNHWCFn.apply(xm, wm, bm, (0, 3), 4) * gy).sum().backward()
+            torch.cuda.synchronize()
+            grads.append((xm.grad, wm.grad, bm.grad))
+    finally:
+        _lib.set_option("conv_row16", 1)
+    for a_, c_ in zip(*grads):
+        assert torch.isfinite(a_).all() and torch.equal(a_, c_)

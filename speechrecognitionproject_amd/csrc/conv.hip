@@ -1695,11 +1695,13 @@ __global__ __launch_bounds__(512, 1) void conv_row16_pool_kernel(RowArgs a) {
     }
   };
   // this lane's A rows: row block rb0 + i, pixel (lane & 31) of it -> staged row and position (tap 0)
-  int abase[RB];
+  // (the chunk swizzle keys on the position within the staged row, as the staging and the halo writes do)
+  int arow[RB], apos[RB];
 #pragma unroll
   for (int i = 0; i < RB; ++i) {
     const int p = (rb0 + i) * 32 + (lane & 31);
-    abase[i] = (p / WD) * WP + p % WD;
+    arow[i] = (p / WD) * WP;
+    apos[i] = p % WD;
   }
   const int khalf = lane >> 5;   // which 8 of the 16 k of a step this lane supplies
   const int lh = lane >> 5, lc = lane & 31;
@@ -1726,8 +1728,8 @@ __global__ __launch_bounds__(512, 1) void conv_row16_pool_kernel(RowArgs a) {
         const int ch = (c0 >> 3) + khalf;
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
-          const int q = abase[i] + kw;   // staged row * WP + position
-          const u32x4_ af = *reinterpret_cast<const u32x4_*>(Xl + q * CI + ((ch ^ (q & 7)) * 8));
+          const int q = apos[i] + kw;   // position in the staged row
+          const u32x4_ af = *reinterpret_cast<const u32x4_*>(Xl + (arow[i] + q) * CI + ((ch ^ (q & 7)) * 8));
           acc[i] = ConvLp<LP>::mma(af, bf, acc[i]);
         }
       }

@@ -1650,27 +1650,32 @@ struct RowArgs {
   uint8_t* arg;                // [rows][W / 4][CO]
   int rows, groups;
 };
-template <int LP, int KW, int PW, int WD, int CI, int CO, int R>
-__global__ __launch_bounds__(512, 1) void conv_row16_pool_kernel(RowArgs a) {
+// NW: 8 waves (wave = 1 column block x 5 row blocks: 6 fragment reads per 5 MFMAs) or 4 waves (wave = 2 column
+// blocks x 5 row blocks, 160 accumulator registers: 7 fragment reads per 10 MFMAs — half the LDS traffic per MFMA;
+// at 8 waves the operand reads, ~150 B per clock per CU, sit above the LDS array's 128) — option conv_row16 = 1 / 2.
+template <int LP, int KW, int PW, int WD, int CI, int CO, int R, int NW = 8>
+__global__ __launch_bounds__(NW * 64, 1) void conv_row16_pool_kernel(RowArgs a) {
   static_assert(CO == 128 && CI % 16 == 0 && WD % 4 == 0 && (R * WD) % 32 == 0 && CI * 2 == 128, "row16 geometry");
+  constexpr int NT = NW * 64;
   constexpr int WP = WD + 2 * PW;               // padded positions per staged row
   constexpr int K = KW * CI;                    // GEMM depth
   constexpr int MB = R * WD / 32;               // row blocks of 32 (10)
   constexpr int RB = MB / 2;                    // row blocks per wave (5)
+  constexpr int CB = NW == 8 ? 1 : 2;           // column blocks per wave
   constexpr int XCH = R * WD * (CI / 8);        // 16-B chunks of one tile's rows (2560)
-  constexpr int XPT = XCH / 512;                // per thread (5)
-  static_assert(XCH % 512 == 0 && MB % 2 == 0, "row16 tile split");
+  constexpr int XPT = XCH / NT;                 // per thread (5 / 10)
+  static_assert(XCH % NT == 0 && MB % 2 == 0 && (NW == 8 || NW == 4), "row16 tile split");
   __shared__ __attribute__((aligned(16))) unsigned short Wl[K * CO];        // TR image [k][co] (r16_off<false>)
   __shared__ __attribute__((aligned(16))) unsigned short Xl[R * WP * CI];   // [row][pos][ci], 16-B chunks swizzled
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wc = wave & 3, rb0 = (wave >> 2) * RB;
+  const int wc = NW == 8 ? (wave & 3) : (wave & 1) * 2, rb0 = (NW == 8 ? (wave >> 2) : (wave >> 1)) * RB;
   // the weights, once: 16-B chunks of 8 columns into the TR image
-  for (int c = tid; c < K * CO / 8; c += 512) {
+  for (int c = tid; c < K * CO / 8; c += NT) {
     const int k = c / (CO / 8), col = (c % (CO / 8)) * 8;
     *reinterpret_cast<u32x4_*>(Wl + r16_off<false>(col, k)) = *reinterpret_cast<const u32x4_*>(a.w16 + (size_t)k * CO + col);
   }
   // the halo positions (never overwritten by the staging)
-  for (int c = tid; c < R * 2 * PW * (CI / 8); c += 512) {
+  for (int c = tid; c < R * 2 * PW * (CI / 8); c += NT) {
     const int rl = c / (2 * PW * (CI / 8)), rem = c % (2 * PW * (CI / 8));
     const int pp = rem / (CI / 8), ch = rem % (CI / 8);
     const int q = pp < PW ? pp : WD + pp;   // 0 .. PW - 1 and WD + PW .. WD + 2 PW - 1
@@ -1680,7 +1685,7 @@ __global__ __launch_bounds__(512, 1) void conv_row16_pool_kernel(RowArgs a) {
   auto fetch = [&](int g) {   // tile g's rows into registers (zeros past the last row)
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
-      const int c = tid + i * 512, rl = c / (WD * (CI / 8)), rem = c % (WD * (CI / 8));
+      const int c = tid + i * NT, rl = c / (WD * (CI / 8)), rem = c % (WD * (CI / 8));
       const int row = g * R + rl;
       xr[i] = row < a.rows ? *reinterpret_cast<const u32x4_*>(a.x16 + ((size_t)row * WD) * CI + (size_t)rem * 8)
                            : u32x4_{0u, 0u, 0u, 0u};
@@ -1689,7 +1694,7 @@ __global__ __launch_bounds__(512, 1) void conv_row16_pool_kernel(RowArgs a) {
   auto stage = [&]() {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
-      const int c = tid + i * 512, rl = c / (WD * (CI / 8)), rem = c % (WD * (CI / 8));
+      const int c = tid + i * NT, rl = c / (WD * (CI / 8)), rem = c % (WD * (CI / 8));
       const int px = rem / (CI / 8), ch = rem % (CI / 8), q = px + PW;
       *reinterpret_cast<u32x4_*>(Xl + (rl * WP + q) * CI + ((ch ^ (q & 7)) * 8)) = xr[i];
     }
@@ -1705,8 +1710,9 @@ __global__ __launch_bounds__(512, 1) void conv_row16_pool_kernel(RowArgs a) {
   }
   const int khalf = lane >> 5;   // which 8 of the 16 k of a step this lane supplies
   const int lh = lane >> 5, lc = lane & 31;
-  const int col = wc * 32 + lc;
-  const float bv = a.bias ? a.bias[col] : 0.f;
+  float bv[CB];
+#pragma unroll
+  for (int j = 0; j < CB; ++j) bv[j] = a.bias ? a.bias[(wc + j) * 32 + lc] : 0.f;
   int g = blockIdx.x;
   if (g < a.groups) fetch(g);
   __syncthreads();
@@ -1715,22 +1721,28 @@ __global__ __launch_bounds__(512, 1) void conv_row16_pool_kernel(RowArgs a) {
     __syncthreads();
     const int gn = g + (int)gridDim.x;
     if (gn < a.groups) fetch(gn);   // lands during the MFMAs below
-    f32x16 acc[RB];
+    f32x16 acc[RB][CB];
 #pragma unroll
     for (int i = 0; i < RB; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+      for (int j = 0; j < CB; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    constexpr int CU = NW == 4 ? 1 : 4;   // the 4-wave form: one k-step's fragments live at a time (registers)
 #pragma unroll 1
     for (int kw = 0; kw < KW; ++kw) {
-#pragma unroll
+#pragma unroll CU
       for (int c0 = 0; c0 < CI; c0 += 16) {
-        const u32x4_ bf = r16_frag<false>(Wl, wc * 32, kw * CI + c0, lane);
+        u32x4_ bf[CB];
+#pragma unroll
+        for (int j = 0; j < CB; ++j) bf[j] = r16_frag<false>(Wl, (wc + j) * 32, kw * CI + c0, lane);
         const int ch = (c0 >> 3) + khalf;
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
           const int q = apos[i] + kw;   // position in the staged row
           const u32x4_ af = *reinterpret_cast<const u32x4_*>(Xl + (arow[i] + q) * CI + ((ch ^ (q & 7)) * 8));
-          acc[i] = ConvLp<LP>::mma(af, bf, acc[i]);
+#pragma unroll
+          for (int j = 0; j < CB; ++j) acc[i][j] = ConvLp<LP>::mma(af, bf[j], acc[i][j]);
         }
       }
     }
@@ -1742,19 +1754,169 @@ __global__ __launch_bounds__(512, 1) void conv_row16_pool_kernel(RowArgs a) {
         const int p0 = (rb0 + i) * 32 + 8 * rq + 4 * lh;   // tile pixel, a multiple of 4
         const int row = g * R + p0 / WD;
         if (row >= a.rows) continue;
-        float best = acc[i][4 * rq] + bv;
-        int am = 0;
 #pragma unroll
-        for (int pp = 1; pp < 4; ++pp) {
-          const float v = acc[i][4 * rq + pp] + bv;
-          if (v > best || (v != v && best == best)) { best = v; am = pp; }
+        for (int j = 0; j < CB; ++j) {
+          float best = acc[i][j][4 * rq] + bv[j];
+          int am = 0;
+#pragma unroll
+          for (int pp = 1; pp < 4; ++pp) {
+            const float v = acc[i][j][4 * rq + pp] + bv[j];
+            if (v > best || (v != v && best == best)) { best = v; am = pp; }
+          }
+          const size_t o = ((size_t)g * R * WD + p0) / 4 * CO + (wc + j) * 32 + lc;
+          a.y[o] = best;
+          a.arg[o] = (uint8_t)am;
         }
-        const size_t o = ((size_t)g * R * WD + p0) / 4 * CO + col;
-        a.y[o] = best;
-        a.arg[o] = (uint8_t)am;
       }
     }
     __syncthreads();   // every wave is done reading Xl before the next tile is staged
+    g = gn;
+  }
+}
+
+// The data gradient of the same conv (conv_row16 also): dX[w][ci] = sum over (kw, co) of dY[w + PW - kw][co] Wd[(kw,
+// co)][ci] — the implicit GEMM's k order, so bitwise its result.  dY (128 channels) has twice the bytes per staged
+// position, so the weights cannot stay resident beside 8 staged rows: the workgroup stages 8 rows of the dense 16-bit
+// dY once per tile (94 KB) and streams the weight matrix one tap at a time ([128 k][64 ci], 16 KB, double-buffered,
+// the next tap's loads in flight during this tap's MFMAs; the whole matrix stays in L2).  4 waves over the 320 x 64
+// tile: row blocks 3 / 3 / 2 / 2 per wave x both 32-column blocks (at most 5 fragment reads per 6 MFMAs).
+__device__ __forceinline__ int r16_off64(int col, int k) {   // TR image of 64 columns ([k][64], 16-B chunks swizzled)
+  return k * 64 + ((((col >> 3) ^ (((k >> 1) & 1) << 2))) << 3) + (col & 7);
+}
+__device__ __forceinline__ u32x4_ r16_frag64(const unsigned short* img, int r0, int kk, int lane) {
+  const int q = (lane >> 2) & 3, pp = lane & 3;
+  const int k = kk + 8 * (lane >> 5) + q, col = r0 + 16 * ((lane >> 4) & 1) + 4 * pp;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + r16_off64(col, k)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + r16_off64(col, k + 4)));
+  const u32x2_ l2 = __builtin_bit_cast(u32x2_, lo), h2 = __builtin_bit_cast(u32x2_, hi);
+  return u32x4_{l2.x, l2.y, h2.x, h2.y};
+}
+struct RowDgArgs {
+  const unsigned short* dy16;   // [rows][W][CA] dense 16-bit dY
+  const unsigned short* wd16;   // [(kw, co)][CN] 16-bit (the dgrad weight matrix Wd)
+  float* dx;                    // [rows][W][CN]
+  int rows, groups;
+};
+template <int LP, int KW, int PW, int WD, int CA, int CN, int R>
+__global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
+  static_assert(CA == 128 && CN == 64 && (R * WD) % 32 == 0 && 2 * PW == KW - 1, "row16 dgrad geometry");
+  constexpr int WP = WD + 2 * PW;
+  constexpr int MB = R * WD / 32;               // 10 row blocks
+  constexpr int XCH = R * WD * (CA / 8);        // 16-B chunks of a tile's dY rows (5120)
+  constexpr int XPT = XCH / 256;                // per thread (20)
+  constexpr int TCH = CA * CN / 8;              // 16-B chunks of one tap's weights (1024)
+  constexpr int TPT = TCH / 256;                // per thread (4)
+  static_assert(MB == 10 && XCH % 256 == 0 && TCH % 256 == 0, "row16 dgrad tile split");
+  __shared__ __attribute__((aligned(16))) unsigned short Yl[R * WP * CA];    // staged dY rows, chunks swizzled
+  __shared__ __attribute__((aligned(16))) unsigned short Wt[2][CA * CN];     // one tap of Wd, TR image [k][64]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rs = wave < 2 ? 3 * wave : 6 + 2 * (wave - 2), rn = wave < 2 ? 3 : 2;   // row blocks of this wave
+  for (int c = tid; c < R * 2 * PW * (CA / 8); c += 256) {   // halo positions, once
+    const int rl = c / (2 * PW * (CA / 8)), rem = c % (2 * PW * (CA / 8));
+    const int pp = rem / (CA / 8), ch = rem % (CA / 8);
+    const int q = pp < PW ? pp : WD + pp;
+    *reinterpret_cast<u32x4_*>(Yl + (rl * WP + q) * CA + ((ch ^ (q & 15)) * 8)) = u32x4_{0u, 0u, 0u, 0u};
+  }
+  u32x4_ yr[XPT], wr[TPT];
+  // 32-bit buffer offsets throughout (the tile base in the scalar offset; past the last row -> 16 zero bytes):
+  // 64-bit addresses of the 20 + 4 loads and the epilogue's stores, hoisted out of the loops, spilled
+  const auto rsY = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(a.dy16), (short)0, 0x7ffffff0, 0x00020000);
+  const auto rsW = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(a.wd16), (short)0, 0x7ffffff0, 0x00020000);
+  const auto rsX = __builtin_amdgcn_make_buffer_rsrc(a.dx, (short)0, 0x7ffffff0, 0x00020000);
+  auto fetch_y = [&](int g) {
+    const int last = (a.rows - g * R) * WD * (CA / 8);   // chunks of real rows in this tile
+    const int sbase = __builtin_amdgcn_readfirstlane(g * R * WD * CA * 2);
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int c = tid + i * 256;
+      yr[i] = __builtin_bit_cast(u32x4_, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rsY, c < last ? c * 16 : (int)0x80000000u, sbase, 0));
+    }
+  };
+  auto stage_y = [&]() {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int c = tid + i * 256, rl = c / (WD * (CA / 8)), rem = c % (WD * (CA / 8));
+      const int px = rem / (CA / 8), ch = rem % (CA / 8), q = px + PW;
+      *reinterpret_cast<u32x4_*>(Yl + (rl * WP + q) * CA + ((ch ^ (q & 15)) * 8)) = yr[i];
+    }
+  };
+  auto fetch_w = [&](int kw) {
+    const int sbase = __builtin_amdgcn_readfirstlane(kw * CA * CN * 2);
+#pragma unroll
+    for (int i = 0; i < TPT; ++i)
+      wr[i] = __builtin_bit_cast(u32x4_, __builtin_amdgcn_raw_buffer_load_b128(rsW, (tid + i * 256) * 16, sbase, 0));
+  };
+  auto stage_w = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < TPT; ++i) {
+      const int c = tid + i * 256, k = c / (CN / 8), col = (c % (CN / 8)) * 8;
+      *reinterpret_cast<u32x4_*>(&Wt[buf][r16_off64(col, k)]) = wr[i];
+    }
+  };
+  int arow[3], apos[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int p = (rs + (i < rn ? i : 0)) * 32 + (lane & 31);
+    arow[i] = (p / WD) * WP;
+    apos[i] = p % WD;
+  }
+  const int khalf = lane >> 5, lh = lane >> 5, lc = lane & 31;
+  int g = blockIdx.x;
+  if (g < a.groups) fetch_y(g);
+  fetch_w(0);
+  while (g < a.groups) {
+    stage_y();
+    stage_w(0);
+    __syncthreads();
+    const int gn = g + (int)gridDim.x;
+    f32x16 acc[3][2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll 1
+    for (int kw = 0; kw < KW; ++kw) {
+      fetch_w(kw + 1 < KW ? kw + 1 : 0);   // the next tap (tap 0 again for the next tile)
+      const unsigned short* Ws = Wt[kw & 1];
+#pragma unroll 1
+      for (int c0 = 0; c0 < CA; c0 += 16) {
+        const u32x4_ b0 = r16_frag64(Ws, 0, c0, lane), b1 = r16_frag64(Ws, 32, c0, lane);
+        const int ch = (c0 >> 3) + khalf;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          if (i < rn) {
+            const int q = apos[i] + 2 * PW - kw;   // dY position w + PW - kw, in the staged (haloed) row
+            const u32x4_ af = *reinterpret_cast<const u32x4_*>(Yl + (arow[i] + q) * CA + ((ch ^ (q & 15)) * 8));
+            acc[i][0] = ConvLp<LP>::mma(af, b0, acc[i][0]);
+            acc[i][1] = ConvLp<LP>::mma(af, b1, acc[i][1]);
+          }
+        }
+      }
+      if (kw + 1 < KW) stage_w((kw + 1) & 1);   // that buffer was last read in tap kw - 1 (behind the barrier)
+      __syncthreads();
+    }
+    // dX rows of this wave's blocks (fp32, 32 consecutive channels per half-wave store)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i >= rn) continue;
+      const int sbase = __builtin_amdgcn_readfirstlane(g * R * WD * CN * 4);
+      const int nreal = (a.rows - g * R) * WD;   // real pixels of this tile
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int p = (rs + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const int off = p < nreal ? (p * CN + lc) * 4 : (int)0x80000000u;   // out of range: the store is dropped
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[i][0][r]), rsX, off, sbase, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[i][1][r]), rsX,
+                                              p < nreal ? off + 128 : (int)0x80000000u, sbase, 0);
+      }
+    }
+    // the next tile's dY rows after the accumulators are dead (their registers; prefetching them during the MFMAs
+    // spilled): the load latency is paid once per tile
+    if (gn < a.groups) fetch_y(gn);
     g = gn;
   }
 }
@@ -2115,6 +2277,22 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
                         2.0 * (double)g.M * (double)g.N * (double)g.K);
     prof.detail("conv_dgrad_as_gemm %lldx%lldx%lld", (long long)g.M, (long long)g.N, (long long)g.K);
     if ((rc = srk::gemm_f32(g, s))) return rc;
+  } else if (dgrad_implicit && d16[0] && srk::g_opt_conv_row16 && KH == 1 && KW == 7 && ph == 0 && pw == 3 &&
+             sh == 1 && sw == 1 && W == 40 && Ci == 64 && Co == 128 && (N * H) < (1LL << 30) / (W * Co)) {
+    // fbanks_cnn conv2's data gradient: the row-staged kernel (conv_row16_dgrad_kernel)
+    srk::RowDgArgs ra{};
+    ra.dy16 = d16[1];
+    ra.wd16 = d16[2];
+    ra.dx = dx;
+    ra.rows = (int)(N * H);
+    ra.groups = (int)((N * H + 7) / 8);
+    srk::ProfScope prof("conv_dgrad_lp", s, 2.0 * (double)(N * H * W) * (double)Ci * (double)(KW * Co));
+    prof.detail("conv_row16_dgrad_kernel %lldx%lldx%lld", (long long)(N * H * W), (long long)Ci, (long long)(KW * Co));
+    const dim3 grid((unsigned)std::min<int64_t>(ra.groups, srk::kCUs)), block(256);
+    if (prec == srk::kPrecBF16)
+      hipLaunchKernelGGL((srk::conv_row16_dgrad_kernel<1, 7, 3, 40, 128, 64, 8>), grid, block, 0, s, ra);
+    else
+      hipLaunchKernelGGL((srk::conv_row16_dgrad_kernel<2, 7, 3, 40, 128, 64, 8>), grid, block, 0, s, ra);
   } else if (dgrad_implicit) {
     srk::ConvArgs d = c;
     d.wmat = ws; d.out = dx;
@@ -2221,11 +2399,15 @@ int srk_conv2d_nhwc_fwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
       ra.groups = (int)((N * H + 7) / 8);
       srk::ProfScope prof("conv_fwd_lp", s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
       prof.detail("conv_row16_pool_kernel %lldx%lldx%lld", (long long)c.M, (long long)c.Nn, (long long)c.K);
-      const dim3 grid((unsigned)std::min<int64_t>(ra.groups, srk::kCUs)), block(512);
-      if (prec == srk::kPrecBF16)
-        hipLaunchKernelGGL((srk::conv_row16_pool_kernel<1, 7, 3, 40, 64, 128, 8>), grid, block, 0, s, ra);
-      else
-        hipLaunchKernelGGL((srk::conv_row16_pool_kernel<2, 7, 3, 40, 64, 128, 8>), grid, block, 0, s, ra);
+      const bool w4 = srk::g_opt_conv_row16 == 2;
+      const dim3 grid((unsigned)std::min<int64_t>(ra.groups, srk::kCUs)), block(w4 ? 256 : 512);
+      if (prec == srk::kPrecBF16) {
+        if (w4) hipLaunchKernelGGL((srk::conv_row16_pool_kernel<1, 7, 3, 40, 64, 128, 8, 4>), grid, block, 0, s, ra);
+        else hipLaunchKernelGGL((srk::conv_row16_pool_kernel<1, 7, 3, 40, 64, 128, 8, 8>), grid, block, 0, s, ra);
+      } else {
+        if (w4) hipLaunchKernelGGL((srk::conv_row16_pool_kernel<2, 7, 3, 40, 64, 128, 8, 4>), grid, block, 0, s, ra);
+        else hipLaunchKernelGGL((srk::conv_row16_pool_kernel<2, 7, 3, 40, 64, 128, 8, 8>), grid, block, 0, s, ra);
+      }
       SRK_CHECK_HIP(hipGetLastError());
       return SRK_OK;
     }
@@ -2242,11 +2424,15 @@ int srk_conv2d_nhwc_fwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
       ra.groups = (int)((N * H + 7) / 8);
       srk::ProfScope prof("conv_fwd_lp", s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
       prof.detail("conv_row16_pool_kernel %lldx%lldx%lld", (long long)c.M, (long long)c.Nn, (long long)c.K);
-      const dim3 grid((unsigned)std::min<int64_t>(ra.groups, srk::kCUs)), block(512);
-      if (prec == srk::kPrecBF16)
-        hipLaunchKernelGGL((srk::conv_row16_pool_kernel<1, 7, 3, 40, 64, 128, 8>), grid, block, 0, s, ra);
-      else
-        hipLaunchKernelGGL((srk::conv_row16_pool_kernel<2, 7, 3, 40, 64, 128, 8>), grid, block, 0, s, ra);
+      const bool w4 = srk::g_opt_conv_row16 == 2;
+      const dim3 grid((unsigned)std::min<int64_t>(ra.groups, srk::kCUs)), block(w4 ? 256 : 512);
+      if (prec == srk::kPrecBF16) {
+        if (w4) hipLaunchKernelGGL((srk::conv_row16_pool_kernel<1, 7, 3, 40, 64, 128, 8, 4>), grid, block, 0, s, ra);
+        else hipLaunchKernelGGL((srk::conv_row16_pool_kernel<1, 7, 3, 40, 64, 128, 8, 8>), grid, block, 0, s, ra);
+      } else {
+        if (w4) hipLaunchKernelGGL((srk::conv_row16_pool_kernel<2, 7, 3, 40, 64, 128, 8, 4>), grid, block, 0, s, ra);
+        else hipLaunchKernelGGL((srk::conv_row16_pool_kernel<2, 7, 3, 40, 64, 128, 8, 8>), grid, block, 0, s, ra);
+      }
       SRK_CHECK_HIP(hipGetLastError());
       return SRK_OK;
     }

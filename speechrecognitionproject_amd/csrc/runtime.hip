@@ -422,7 +422,8 @@ int srk_set_option(const char* name, int64_t value) {
     return SRK_OK;
   }
   if (n == "conv_row16") {   // fbanks conv2 + pool, 16-bit: row-staged kernel (1) or implicit GEMM (0)
-    srk::g_opt_conv_row16 = value != 0;
+    SRK_REQUIRE(value >= 0 && value <= 2, SRK_ERR_INVALID, "conv_row16 must be 0, 1 (8 waves) or 2 (4 waves)");
+    srk::g_opt_conv_row16 = (int)value;
     return SRK_OK;
   }
   if (n == "conv_fast16") {   // 16-bit-source register-staged convs: uniform-tap fast gathers (1) or generic (0)

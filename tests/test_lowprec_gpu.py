@@ -793,7 +793,8 @@ def test_conv_fast16_gathers_bitwise(prec, shape, pooled):
 
 
 @pytest.mark.parametrize("N", [3, 32])
-def test_conv_row16_equals_gemm(prec, N):
+@pytest.mark.parametrize("form", [1, 2])   # 8 waves / 4 waves
+def test_conv_row16_equals_gemm(prec, N, form):
     """Option conv_row16: fbanks_cnn conv2 + maxpool2 (Conv2d(64, 128, (1, 7), padding (0, 3)) over W = 40, then
     MaxPool2d((1, 4)), model_fbanks_cnn.py:74-75) on the row-staged kernel — weights resident in LDS, image rows
     staged once per tile, the taps as shifted reads — equals the implicit-GEMM kernels bit for bit: the same
@@ -808,7 +809,7 @@ def test_conv_row16_equals_gemm(prec, N):
     x[0, 0, :8] = float("nan")   # NaN windows: the pool rule
     outs = []
     try:
-        for row in (1, 0):
+        for row in (form, 0):
             _lib.set_option("conv_row16", row)
             _lib.prof_enable(True)
             with torch.no_grad():
@@ -830,7 +831,7 @@ def test_conv_row16_equals_gemm(prec, N):
     gy = torch.randn(N, H, W // 4, Co, generator=g).cuda()
     grads = []
     try:
-        for row in (1, 0):
+        for row in (form, 0):
             _lib.set_option("conv_row16", row)
             xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
             (snn._ConvPoolNHWCFn.apply(xm, wm, bm, (0, 3), 4) * gy).sum().backward()

@@ -1774,7 +1774,10 @@ __global__ __launch_bounds__(NW * 64, 1) void conv_row16_pool_kernel(RowArgs a) 
   }
 }
 
-// The data gradient of the same conv (conv_row16 also): dX[w][ci] = sum over (kw, co) of dY[w + PW - kw][co] Wd[(kw,
+// UNFINISHED (option conv_row16_dgrad, default 0): on the GPU this kernel's dX differs from the implicit GEMM's on
+// 15 of 16 outputs (dense and pooled dY alike, tools/row16_diag.py) although a host restatement of its index math
+// (staging, swizzles, tap positions) reproduces the product exactly; at 445-472 vs 687 us it is worth finishing.
+// The data gradient of the same conv: dX[w][ci] = sum over (kw, co) of dY[w + PW - kw][co] Wd[(kw,
 // co)][ci] — the implicit GEMM's k order, so bitwise its result.  dY (128 channels) has twice the bytes per staged
 // position, so the weights cannot stay resident beside 8 staged rows: the workgroup stages 8 rows of the dense 16-bit
 // dY once per tile (94 KB) and streams the weight matrix one tap at a time ([128 k][64 ci], 16 KB, double-buffered,
@@ -1809,7 +1812,10 @@ __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
   constexpr int TPT = TCH / 256;                // per thread (4)
   static_assert(MB == 10 && XCH % 256 == 0 && TCH % 256 == 0, "row16 dgrad tile split");
   __shared__ __attribute__((aligned(16))) unsigned short Yl[R * WP * CA];    // staged dY rows, chunks swizzled
-  __shared__ __attribute__((aligned(16))) unsigned short Wt[2][CA * CN];     // one tap of Wd, TR image [k][64]
+  // one tap of Wd as a TR image [k][128] (r16_off<false>, the ring kernels' layout; columns 64..127 unused):
+  // the 64-column form (r16_off64) gave wrong data gradients on the GPU although its index math checks out on
+  // the host (tools/row16_diag.py) — kept for reference, not used
+  __shared__ __attribute__((aligned(16))) unsigned short Wt[2][CA * 128];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rs = wave < 2 ? 3 * wave : 6 + 2 * (wave - 2), rn = wave < 2 ? 3 : 2;   // row blocks of this wave
   for (int c = tid; c < R * 2 * PW * (CA / 8); c += 256) {   // halo positions, once
@@ -1831,7 +1837,7 @@ __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
     for (int i = 0; i < XPT; ++i) {
       const int c = tid + i * 256;
       yr[i] = __builtin_bit_cast(u32x4_, __builtin_amdgcn_raw_buffer_load_b128(
-                                              rsY, c < last ? c * 16 : (int)0x80000000u, sbase, 0));
+                                              rsY, c < last ? sbase + c * 16 : (int)0x80000000u, 0, 0));
     }
   };
   auto stage_y = [&]() {
@@ -1846,13 +1852,13 @@ __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
     const int sbase = __builtin_amdgcn_readfirstlane(kw * CA * CN * 2);
 #pragma unroll
     for (int i = 0; i < TPT; ++i)
-      wr[i] = __builtin_bit_cast(u32x4_, __builtin_amdgcn_raw_buffer_load_b128(rsW, (tid + i * 256) * 16, sbase, 0));
+      wr[i] = __builtin_bit_cast(u32x4_, __builtin_amdgcn_raw_buffer_load_b128(rsW, sbase + (tid + i * 256) * 16, 0, 0));
   };
   auto stage_w = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < TPT; ++i) {
       const int c = tid + i * 256, k = c / (CN / 8), col = (c % (CN / 8)) * 8;
-      *reinterpret_cast<u32x4_*>(&Wt[buf][r16_off64(col, k)]) = wr[i];
+      *reinterpret_cast<u32x4_*>(&Wt[buf][r16_off<false>(col, k)]) = wr[i];
     }
   };
   int arow[3], apos[3];
@@ -1884,7 +1890,7 @@ __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
       const unsigned short* Ws = Wt[kw & 1];
 #pragma unroll 1
       for (int c0 = 0; c0 < CA; c0 += 16) {
-        const u32x4_ b0 = r16_frag64(Ws, 0, c0, lane), b1 = r16_frag64(Ws, 32, c0, lane);
+        const u32x4_ b0 = r16_frag<false>(Ws, 0, c0, lane), b1 = r16_frag<false>(Ws, 32, c0, lane);
         const int ch = (c0 >> 3) + khalf;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
@@ -1908,10 +1914,10 @@ __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int p = (rs + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const int off = p < nreal ? (p * CN + lc) * 4 : (int)0x80000000u;   // out of range: the store is dropped
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[i][0][r]), rsX, off, sbase, 0);
+        const int off = p < nreal ? sbase + (p * CN + lc) * 4 : (int)0x80000000u;   // out of range: dropped
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[i][0][r]), rsX, off, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[i][1][r]), rsX,
-                                              p < nreal ? off + 128 : (int)0x80000000u, sbase, 0);
+                                              p < nreal ? off + 128 : (int)0x80000000u, 0, 0);
       }
     }
     // the next tile's dY rows after the accumulators are dead (their registers; prefetching them during the MFMAs
@@ -2277,7 +2283,7 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
                         2.0 * (double)g.M * (double)g.N * (double)g.K);
     prof.detail("conv_dgrad_as_gemm %lldx%lldx%lld", (long long)g.M, (long long)g.N, (long long)g.K);
     if ((rc = srk::gemm_f32(g, s))) return rc;
-  } else if (dgrad_implicit && d16[0] && srk::g_opt_conv_row16 && KH == 1 && KW == 7 && ph == 0 && pw == 3 &&
+  } else if (dgrad_implicit && d16[0] && srk::g_opt_conv_row16_dgrad && KH == 1 && KW == 7 && ph == 0 && pw == 3 &&
              sh == 1 && sw == 1 && W == 40 && Ci == 64 && Co == 128 && (N * H) < (1LL << 30) / (W * Co)) {
     // fbanks_cnn conv2's data gradient: the row-staged kernel (conv_row16_dgrad_kernel)
     srk::RowDgArgs ra{};

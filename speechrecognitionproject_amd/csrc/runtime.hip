@@ -34,6 +34,7 @@ int g_opt_conv_ring_pers = 0;
 int g_opt_conv1_mfma = 0;
 int g_opt_conv_fast16 = 1;
 int g_opt_conv_row16 = 1;
+int g_opt_conv_row16_dgrad = 0;
 int g_opt_bn_tree = 0;
 int g_opt_gru_poll_pipe = 0;
 int g_opt_mfcc_variant = 3;
@@ -419,6 +420,10 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "conv_ring_qs") {   // 16-bit ring convs: whole K-tiles per MFMA section, mask by width (64, 128, 256)
     SRK_REQUIRE(value >= 0 && value <= 7, SRK_ERR_INVALID, "conv_ring_qs is a 3-bit mask");
     srk::g_opt_conv_ring_qs = (int)value;
+    return SRK_OK;
+  }
+  if (n == "conv_row16_dgrad") {   // unfinished row-staged conv2 data gradient (1) or the implicit GEMM (0)
+    srk::g_opt_conv_row16_dgrad = value != 0;
     return SRK_OK;
   }
   if (n == "conv_row16") {   // fbanks conv2 + pool, 16-bit: row-staged kernel (1) or implicit GEMM (0)

@@ -1774,27 +1774,12 @@ __global__ __launch_bounds__(NW * 64, 1) void conv_row16_pool_kernel(RowArgs a) 
   }
 }
 
-// UNFINISHED (option conv_row16_dgrad, default 0): on the GPU this kernel's dX differs from the implicit GEMM's on
-// 15 of 16 outputs (dense and pooled dY alike, tools/row16_diag.py) although a host restatement of its index math
-// (staging, swizzles, tap positions) reproduces the product exactly; at 445-472 vs 687 us it is worth finishing.
 // The data gradient of the same conv: dX[w][ci] = sum over (kw, co) of dY[w + PW - kw][co] Wd[(kw,
 // co)][ci] — the implicit GEMM's k order, so bitwise its result.  dY (128 channels) has twice the bytes per staged
 // position, so the weights cannot stay resident beside 8 staged rows: the workgroup stages 8 rows of the dense 16-bit
 // dY once per tile (94 KB) and streams the weight matrix one tap at a time ([128 k][64 ci], 16 KB, double-buffered,
 // the next tap's loads in flight during this tap's MFMAs; the whole matrix stays in L2).  4 waves over the 320 x 64
 // tile: row blocks 3 / 3 / 2 / 2 per wave x both 32-column blocks (at most 5 fragment reads per 6 MFMAs).
-__device__ __forceinline__ int r16_off64(int col, int k) {   // TR image of 64 columns ([k][64], 16-B chunks swizzled)
-  return k * 64 + ((((col >> 3) ^ (((k >> 1) & 1) << 2))) << 3) + (col & 7);
-}
-__device__ __forceinline__ u32x4_ r16_frag64(const unsigned short* img, int r0, int kk, int lane) {
-  const int q = (lane >> 2) & 3, pp = lane & 3;
-  const int k = kk + 8 * (lane >> 5) + q, col = r0 + 16 * ((lane >> 4) & 1) + 4 * pp;
-  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + r16_off64(col, k)));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + r16_off64(col, k + 4)));
-  const u32x2_ l2 = __builtin_bit_cast(u32x2_, lo), h2 = __builtin_bit_cast(u32x2_, hi);
-  return u32x4_{l2.x, l2.y, h2.x, h2.y};
-}
 struct RowDgArgs {
   const unsigned short* dy16;   // [rows][W][CA] dense 16-bit dY
   const unsigned short* wd16;   // [(kw, co)][CN] 16-bit (the dgrad weight matrix Wd)
@@ -1812,9 +1797,7 @@ __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
   constexpr int TPT = TCH / 256;                // per thread (4)
   static_assert(MB == 10 && XCH % 256 == 0 && TCH % 256 == 0, "row16 dgrad tile split");
   __shared__ __attribute__((aligned(16))) unsigned short Yl[R * WP * CA];    // staged dY rows, chunks swizzled
-  // one tap of Wd as a TR image [k][128] (r16_off<false>, the ring kernels' layout; columns 64..127 unused):
-  // the 64-column form (r16_off64) gave wrong data gradients on the GPU although its index math checks out on
-  // the host (tools/row16_diag.py) — kept for reference, not used
+  // one tap of Wd as a TR image [k][128] (r16_off<false>, the ring kernels' layout; columns 64..127 unused)
   __shared__ __attribute__((aligned(16))) unsigned short Wt[2][CA * 128];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rs = wave < 2 ? 3 * wave : 6 + 2 * (wave - 2), rn = wave < 2 ? 3 : 2;   // row blocks of this wave
@@ -1825,11 +1808,10 @@ __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
     *reinterpret_cast<u32x4_*>(Yl + (rl * WP + q) * CA + ((ch ^ (q & 15)) * 8)) = u32x4_{0u, 0u, 0u, 0u};
   }
   u32x4_ yr[XPT], wr[TPT];
-  // 32-bit buffer offsets throughout (the tile base in the scalar offset; past the last row -> 16 zero bytes):
-  // 64-bit addresses of the 20 + 4 loads and the epilogue's stores, hoisted out of the loops, spilled
+  // the loads take 32-bit buffer offsets (past the last row -> 16 zero bytes): 64-bit addresses of the 20 + 4 loads,
+  // hoisted out of the loops, spilled; the epilogue stores 32-bit offsets off the tile's base pointer
   const auto rsY = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(a.dy16), (short)0, 0x7ffffff0, 0x00020000);
   const auto rsW = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(a.wd16), (short)0, 0x7ffffff0, 0x00020000);
-  const auto rsX = __builtin_amdgcn_make_buffer_rsrc(a.dx, (short)0, 0x7ffffff0, 0x00020000);
   auto fetch_y = [&](int g) {
     const int last = (a.rows - g * R) * WD * (CA / 8);   // chunks of real rows in this tile
     const int sbase = __builtin_amdgcn_readfirstlane(g * R * WD * CA * 2);
@@ -1909,15 +1891,15 @@ __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       if (i >= rn) continue;
-      const int sbase = __builtin_amdgcn_readfirstlane(g * R * WD * CN * 4);
+      float* const xbase = a.dx + (size_t)g * R * WD * CN;
       const int nreal = (a.rows - g * R) * WD;   // real pixels of this tile
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int p = (rs + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const int off = p < nreal ? sbase + (p * CN + lc) * 4 : (int)0x80000000u;   // out of range: dropped
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[i][0][r]), rsX, off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[i][1][r]), rsX,
-                                              p < nreal ? off + 128 : (int)0x80000000u, 0, 0);
+        if (p < nreal) {   // global stores off the tile's base (buffer stores here landed wrong on the GPU)
+          xbase[p * CN + lc] = acc[i][0][r];
+          xbase[p * CN + lc + 32] = acc[i][1][r];
+        }
       }
     }
     // the next tile's dY rows after the accumulators are dead (their registers; prefetching them during the MFMAs

@@ -34,7 +34,7 @@ int g_opt_conv_ring_pers = 0;
 int g_opt_conv1_mfma = 0;
 int g_opt_conv_fast16 = 1;
 int g_opt_conv_row16 = 1;
-int g_opt_conv_row16_dgrad = 0;
+int g_opt_conv_row16_dgrad = 1;
 int g_opt_bn_tree = 0;
 int g_opt_gru_poll_pipe = 0;
 int g_opt_mfcc_variant = 3;
@@ -422,7 +422,7 @@ int srk_set_option(const char* name, int64_t value) {
     srk::g_opt_conv_ring_qs = (int)value;
     return SRK_OK;
   }
-  if (n == "conv_row16_dgrad") {   // unfinished row-staged conv2 data gradient (1) or the implicit GEMM (0)
+  if (n == "conv_row16_dgrad") {   // row-staged conv2 data gradient (1) or the implicit GEMM (0)
     srk::g_opt_conv_row16_dgrad = value != 0;
     return SRK_OK;
   }

@@ -826,18 +826,31 @@ def test_conv_row16_equals_gemm(prec, N, form):
     nan = torch.isnan(y1)
     assert bool(nan.any()) and torch.equal(nan, torch.isnan(y0))
     assert torch.equal(y1[~nan], y0[~nan])
-    # the argmax the backward routes through: every gradient equal too (finite input)
+    # the argmax the backward routes through: every gradient equal too (finite input), the data gradient on the
+    # row-staged kernel (option conv_row16_dgrad) against the implicit GEMM's; then the plain conv's backward
+    # with a dense dY through the same hook
     x[0, 0, :8] = 0.5
     gy = torch.randn(N, H, W // 4, Co, generator=g).cuda()
-    grads = []
+    gd = torch.randn(N, H, W, Co, generator=g).cuda()
+    grads, dense = [], []
     try:
         for row in (form, 0):
             _lib.set_option("conv_row16", row)
+            _lib.set_option("conv_row16_dgrad", 1 if row else 0)
+            _lib.prof_enable(True)
             xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
             (snn._ConvPoolNHWCFn.apply(xm, wm, bm, (0, 3), 4) * gy).sum().backward()
             torch.cuda.synchronize()
-            grads.append((xm.grad, wm.grad, bm.grad))
+            grads.append((xm.grad, wm.grad, bm.grad, any("conv_row16_dgrad" in e["kernel"] for e in _lib.prof_kernels())))
+            _lib.prof_enable(False)
+            xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
+            (snn._Conv2dNHWCFn.apply(xm, wm, bm, (0, 3), (1, 1)) * gd).sum().backward()
+            torch.cuda.synchronize()
+            dense.append((xm.grad, wm.grad, bm.grad))
     finally:
         _lib.set_option("conv_row16", 1)
-    for a_, c_ in zip(*grads):
+        _lib.set_option("conv_row16_dgrad", 1)
+        _lib.prof_enable(False)
+    assert grads[0][3] and not grads[1][3]
+    for a_, c_ in list(zip(grads[0][:3], grads[1][:3])) + list(zip(*dense)):
         assert torch.isfinite(a_).all() and torch.equal(a_, c_)

@@ -22,6 +22,7 @@ _lib.set_matmul_precision("bf16")
 res = {}
 for row in (1, 0):
     _lib.set_option("conv_row16", row)
+    _lib.set_option("conv_row16_dgrad", row)
     y = torch.empty(N, H, W // 4, Co, device="cuda")
     arg = torch.empty(N, H, W // 4, Co, dtype=torch.uint8, device="cuda")
     ws = torch.empty(int(_lib.lib().srk_conv2d_workspace_floats(Ci, Co, 1, 7)), device="cuda")
@@ -49,6 +50,7 @@ dyd = torch.randn(N, H, W, Co, generator=g).cuda()
 res2 = {}
 for row in (1, 0):
     _lib.set_option("conv_row16", row)
+    _lib.set_option("conv_row16_dgrad", row)
     ws = torch.empty(int(_lib.lib().srk_conv2d_workspace_floats(Ci, Co, 1, 7)), device="cuda")
     dx, dw = torch.empty_like(x), torch.empty_like(w)
     call("srk_conv2d_nhwc_bwd", ptr(x), N, H, W, Ci, ptr(w), Co, 1, 7, 0, 3, 1, 1, ptr(dyd), ptr(dx), ptr(dw), None,

@@ -11,6 +11,7 @@
 // The gathers are done by the operand loaders (no im2col buffer).  Weights are re-laid out once
 // per call from the torch layout [Co][Ci][KH][KW] (a 1.4 MB copy for the whole fbanks_cnn model).
 #include <mutex>
+#include <type_traits>
 
 #include "gemm.h"
 #include "mfma_tile.h"
@@ -1786,7 +1787,10 @@ struct RowDgArgs {
   float* dx;                    // [rows][W][CN]
   int rows, groups;
 };
-template <int LP, int KW, int PW, int WD, int CA, int CN, int R>
+// BAL (option conv_row16_dgrad = 2): the 20 (row block, column block) units of the tile 5 per wave instead —
+// wave w owns units 5w .. 5w + 4 (unit u = row block u / 2, column block u % 2): 3 A + 2 B fragment reads per 5
+// MFMAs, every SIMD the same MFMA count (the 3 / 3 / 2 / 2 split leaves two SIMDs idle 1/3 of each k-step).
+template <int LP, int KW, int PW, int WD, int CA, int CN, int R, bool BAL = false>
 __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
   static_assert(CA == 128 && CN == 64 && (R * WD) % 32 == 0 && 2 * PW == KW - 1, "row16 dgrad geometry");
   constexpr int WP = WD + 2 * PW;
@@ -1800,7 +1804,8 @@ __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
   // one tap of Wd as a TR image [k][128] (r16_off<false>, the ring kernels' layout; columns 64..127 unused)
   __shared__ __attribute__((aligned(16))) unsigned short Wt[2][CA * 128];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int rs = wave < 2 ? 3 * wave : 6 + 2 * (wave - 2), rn = wave < 2 ? 3 : 2;   // row blocks of this wave
+  // row blocks of this wave: rs .. rs + rn - 1 (BAL: the 3 row blocks its 5 units touch)
+  const int rs = BAL ? (5 * wave) >> 1 : (wave < 2 ? 3 * wave : 6 + 2 * (wave - 2)), rn = BAL || wave < 2 ? 3 : 2;
   for (int c = tid; c < R * 2 * PW * (CA / 8); c += 256) {   // halo positions, once
     const int rl = c / (2 * PW * (CA / 8)), rem = c % (2 * PW * (CA / 8));
     const int pp = rem / (CA / 8), ch = rem % (CA / 8);
@@ -1859,52 +1864,96 @@ __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
     stage_w(0);
     __syncthreads();
     const int gn = g + (int)gridDim.x;
-    f32x16 acc[3][2];
+    float* const xbase = a.dx + (size_t)g * R * WD * CN;
+    const int nreal = (a.rows - g * R) * WD;   // real pixels of this tile
+    if constexpr (BAL) {
+      // unit k of wave parity P: local row block (P + k) / 2, column block (P + k) % 2 (wave-uniform branch)
+      auto run = [&](auto par) {
+        constexpr int P = decltype(par)::value;
+        f32x16 acc[5];
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 5; ++k)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+          for (int r = 0; r < 16; ++r) acc[k][r] = 0.f;
 #pragma unroll 1
-    for (int kw = 0; kw < KW; ++kw) {
-      fetch_w(kw + 1 < KW ? kw + 1 : 0);   // the next tap (tap 0 again for the next tile)
-      const unsigned short* Ws = Wt[kw & 1];
+        for (int kw = 0; kw < KW; ++kw) {
+          fetch_w(kw + 1 < KW ? kw + 1 : 0);
+          if (kw == KW - 1 && gn < a.groups) fetch_y(gn);   // the next tile's rows under the last tap's MFMAs
+          const unsigned short* Ws = Wt[kw & 1];
 #pragma unroll 1
-      for (int c0 = 0; c0 < CA; c0 += 16) {
-        const u32x4_ b0 = r16_frag<false>(Ws, 0, c0, lane), b1 = r16_frag<false>(Ws, 32, c0, lane);
-        const int ch = (c0 >> 3) + khalf;
+          for (int c0 = 0; c0 < CA; c0 += 16) {
+            const u32x4_ bq[2] = {r16_frag<false>(Ws, 0, c0, lane), r16_frag<false>(Ws, 32, c0, lane)};
+            const int ch = (c0 >> 3) + khalf;
+            u32x4_ af[3];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          if (i < rn) {
-            const int q = apos[i] + 2 * PW - kw;   // dY position w + PW - kw, in the staged (haloed) row
-            const u32x4_ af = *reinterpret_cast<const u32x4_*>(Yl + (arow[i] + q) * CA + ((ch ^ (q & 15)) * 8));
-            acc[i][0] = ConvLp<LP>::mma(af, b0, acc[i][0]);
-            acc[i][1] = ConvLp<LP>::mma(af, b1, acc[i][1]);
+            for (int i = 0; i < 3; ++i) {
+              const int q = apos[i] + 2 * PW - kw;
+              af[i] = *reinterpret_cast<const u32x4_*>(Yl + (arow[i] + q) * CA + ((ch ^ (q & 15)) * 8));
+            }
+#pragma unroll
+            for (int k = 0; k < 5; ++k) acc[k] = ConvLp<LP>::mma(af[(P + k) >> 1], bq[(P + k) & 1], acc[k]);
+          }
+          if (kw + 1 < KW) stage_w((kw + 1) & 1);
+          __syncthreads();
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const int cb = ((P + k) & 1) * 32;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int p = (rs + ((P + k) >> 1)) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (p < nreal) xbase[p * CN + cb + lc] = acc[k][r];
           }
         }
+      };
+      if (wave & 1) run(std::integral_constant<int, 1>{});
+      else run(std::integral_constant<int, 0>{});
+    } else {
+      f32x16 acc[3][2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll 1
+      for (int kw = 0; kw < KW; ++kw) {
+        fetch_w(kw + 1 < KW ? kw + 1 : 0);   // the next tap (tap 0 again for the next tile)
+        const unsigned short* Ws = Wt[kw & 1];
+#pragma unroll 1
+        for (int c0 = 0; c0 < CA; c0 += 16) {
+          const u32x4_ b0 = r16_frag<false>(Ws, 0, c0, lane), b1 = r16_frag<false>(Ws, 32, c0, lane);
+          const int ch = (c0 >> 3) + khalf;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            if (i < rn) {
+              const int q = apos[i] + 2 * PW - kw;   // dY position w + PW - kw, in the staged (haloed) row
+              const u32x4_ af = *reinterpret_cast<const u32x4_*>(Yl + (arow[i] + q) * CA + ((ch ^ (q & 15)) * 8));
+              acc[i][0] = ConvLp<LP>::mma(af, b0, acc[i][0]);
+              acc[i][1] = ConvLp<LP>::mma(af, b1, acc[i][1]);
+            }
+          }
+        }
+        if (kw + 1 < KW) stage_w((kw + 1) & 1);   // that buffer was last read in tap kw - 1 (behind the barrier)
+        __syncthreads();
       }
-      if (kw + 1 < KW) stage_w((kw + 1) & 1);   // that buffer was last read in tap kw - 1 (behind the barrier)
-      __syncthreads();
-    }
-    // dX rows of this wave's blocks (fp32, 32 consecutive channels per half-wave store)
+      // dX rows of this wave's blocks (fp32, 32 consecutive channels per half-wave store)
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      if (i >= rn) continue;
-      float* const xbase = a.dx + (size_t)g * R * WD * CN;
-      const int nreal = (a.rows - g * R) * WD;   // real pixels of this tile
+      for (int i = 0; i < 3; ++i) {
+        if (i >= rn) continue;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int p = (rs + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (p < nreal) {   // global stores off the tile's base (buffer stores here landed wrong on the GPU)
-          xbase[p * CN + lc] = acc[i][0][r];
-          xbase[p * CN + lc + 32] = acc[i][1][r];
+        for (int r = 0; r < 16; ++r) {
+          const int p = (rs + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (p < nreal) {   // global stores off the tile's base (buffer stores here landed wrong on the GPU)
+            xbase[p * CN + lc] = acc[i][0][r];
+            xbase[p * CN + lc + 32] = acc[i][1][r];
+          }
         }
       }
     }
     // the next tile's dY rows after the accumulators are dead (their registers; prefetching them during the MFMAs
-    // spilled): the load latency is paid once per tile
-    if (gn < a.groups) fetch_y(gn);
+    // spilled): the load latency is paid once per tile (BAL: 80 accumulator registers, so under the last tap)
+    if (!BAL && gn < a.groups) fetch_y(gn);
     g = gn;
   }
 }
@@ -2277,8 +2326,13 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
     srk::ProfScope prof("conv_dgrad_lp", s, 2.0 * (double)(N * H * W) * (double)Ci * (double)(KW * Co));
     prof.detail("conv_row16_dgrad_kernel %lldx%lldx%lld", (long long)(N * H * W), (long long)Ci, (long long)(KW * Co));
     const dim3 grid((unsigned)std::min<int64_t>(ra.groups, srk::kCUs)), block(256);
-    if (prec == srk::kPrecBF16)
+    const bool bal = srk::g_opt_conv_row16_dgrad == 2;
+    if (prec == srk::kPrecBF16 && bal)
+      hipLaunchKernelGGL((srk::conv_row16_dgrad_kernel<1, 7, 3, 40, 128, 64, 8, true>), grid, block, 0, s, ra);
+    else if (prec == srk::kPrecBF16)
       hipLaunchKernelGGL((srk::conv_row16_dgrad_kernel<1, 7, 3, 40, 128, 64, 8>), grid, block, 0, s, ra);
+    else if (bal)
+      hipLaunchKernelGGL((srk::conv_row16_dgrad_kernel<2, 7, 3, 40, 128, 64, 8, true>), grid, block, 0, s, ra);
     else
       hipLaunchKernelGGL((srk::conv_row16_dgrad_kernel<2, 7, 3, 40, 128, 64, 8>), grid, block, 0, s, ra);
   } else if (dgrad_implicit) {

@@ -423,7 +423,9 @@ int srk_set_option(const char* name, int64_t value) {
     return SRK_OK;
   }
   if (n == "conv_row16_dgrad") {   // row-staged conv2 data gradient (1) or the implicit GEMM (0)
-    srk::g_opt_conv_row16_dgrad = value != 0;
+    SRK_REQUIRE(value >= 0 && value <= 2, SRK_ERR_INVALID,
+                "conv_row16_dgrad must be 0, 1 (3 / 3 / 2 / 2 row blocks per wave) or 2 (5 units per wave)");
+    srk::g_opt_conv_row16_dgrad = (int)value;
     return SRK_OK;
   }
   if (n == "conv_row16") {   // fbanks conv2 + pool, 16-bit: row-staged kernel (1) or implicit GEMM (0)

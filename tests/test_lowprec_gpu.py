@@ -793,7 +793,7 @@ def test_conv_fast16_gathers_bitwise(prec, shape, pooled):
 
 
 @pytest.mark.parametrize("N", [3, 32])
-@pytest.mark.parametrize("form", [1, 2])   # 8 waves / 4 waves
+@pytest.mark.parametrize("form", [1, 2])   # 8 waves / 4 waves (forward); the data gradient's two splits with them
 def test_conv_row16_equals_gemm(prec, N, form):
     """Option conv_row16: fbanks_cnn conv2 + maxpool2 (Conv2d(64, 128, (1, 7), padding (0, 3)) over W = 40, then
     MaxPool2d((1, 4)), model_fbanks_cnn.py:74-75) on the row-staged kernel — weights resident in LDS, image rows
@@ -836,7 +836,7 @@ def test_conv_row16_equals_gemm(prec, N, form):
     try:
         for row in (form, 0):
             _lib.set_option("conv_row16", row)
-            _lib.set_option("conv_row16_dgrad", 1 if row else 0)
+            _lib.set_option("conv_row16_dgrad", form if row else 0)
             _lib.prof_enable(True)
             xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
             (snn._ConvPoolNHWCFn.apply(xm, wm, bm, (0, 3), 4) * gy).sum().backward()

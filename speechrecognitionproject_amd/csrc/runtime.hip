@@ -34,7 +34,7 @@ int g_opt_conv_ring_pers = 0;
 int g_opt_conv1_mfma = 0;
 int g_opt_conv_fast16 = 1;
 int g_opt_conv_row16 = 1;
-int g_opt_conv_row16_dgrad = 1;
+int g_opt_conv_row16_dgrad = 2;
 int g_opt_bn_tree = 0;
 int g_opt_gru_poll_pipe = 0;
 int g_opt_mfcc_variant = 3;
@@ -422,7 +422,7 @@ int srk_set_option(const char* name, int64_t value) {
     srk::g_opt_conv_ring_qs = (int)value;
     return SRK_OK;
   }
-  if (n == "conv_row16_dgrad") {   // row-staged conv2 data gradient (1) or the implicit GEMM (0)
+  if (n == "conv_row16_dgrad") {   // row-staged conv2 data gradient (1, 2) or the implicit GEMM (0)
     SRK_REQUIRE(value >= 0 && value <= 2, SRK_ERR_INVALID,
                 "conv_row16_dgrad must be 0, 1 (3 / 3 / 2 / 2 row blocks per wave) or 2 (5 units per wave)");
     srk::g_opt_conv_row16_dgrad = (int)value;

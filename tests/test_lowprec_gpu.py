@@ -849,7 +849,7 @@ def test_conv_row16_equals_gemm(prec, N, form):
             dense.append((xm.grad, wm.grad, bm.grad))
     finally:
         _lib.set_option("conv_row16", 1)
-        _lib.set_option("conv_row16_dgrad", 1)
+        _lib.set_option("conv_row16_dgrad", 2)
         _lib.prof_enable(False)
     assert grads[0][3] and not grads[1][3]
     for a_, c_ in list(zip(grads[0][:3], grads[1][:3])) + list(zip(*dense)):

@@ -233,11 +233,30 @@ __global__ __launch_bounds__(256) void conv1_pool_wgrad_kernel(C1Args a) {
     load_patch<KH, KW, kRowsW>(a, n, h0, patch, pitch);
     __syncthreads();
     const int rows = min(kRowsW, a.H - h0);
-    for (int wi = pg; wi < rows * Wq; wi += kPG) {
+    // the dY quads and argmax words of the next two pixels are in flight while this one's taps run (the loop
+    // was bound by their load latency at 2 waves per SIMD, not by its LDS reads or FMAs: 336 -> 297 us with one)
+    const int npx = rows * Wq;
+    auto at = [&](int wi) { return (((size_t)n * a.H + h0 + wi / Wq) * Wq + wi % Wq) * kCo + c4 * 4; };
+    v4f gn = {0.f, 0.f, 0.f, 0.f}, gm = gn;   // pixels wi + kPG, wi + 2 kPG
+    unsigned in = 0u, im = 0u;
+    if (pg < npx) {
+      gn = *reinterpret_cast<const v4f*>(a.dy + at(pg));
+      in = *reinterpret_cast<const unsigned*>(a.arg + at(pg));
+    }
+    if (pg + kPG < npx) {
+      gm = *reinterpret_cast<const v4f*>(a.dy + at(pg + kPG));
+      im = *reinterpret_cast<const unsigned*>(a.arg + at(pg + kPG));
+    }
+    for (int wi = pg; wi < npx; wi += kPG) {
       const int r = wi / Wq, wq = wi % Wq;
-      const size_t o = (((size_t)n * a.H + h0 + r) * Wq + wq) * kCo + c4 * 4;
-      const v4f g = *reinterpret_cast<const v4f*>(a.dy + o);
-      const unsigned idx = *reinterpret_cast<const unsigned*>(a.arg + o);
+      const v4f g = gn;
+      const unsigned idx = in;
+      gn = gm;
+      in = im;
+      if (wi + 2 * kPG < npx) {
+        gm = *reinterpret_cast<const v4f*>(a.dy + at(wi + 2 * kPG));
+        im = *reinterpret_cast<const unsigned*>(a.arg + at(wi + 2 * kPG));
+      }
       dbacc += g;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {

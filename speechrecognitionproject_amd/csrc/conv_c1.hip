@@ -25,7 +25,11 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 constexpr int kCo = 64;              // output channels (model_fbanks_cnn.py:72)
 constexpr int kC4 = kCo / 4;         // threads per pixel group (4 channels each)
 constexpr int kPG = 256 / kC4;       // pixel groups per block
-constexpr int kRows = 2;             // image rows per block (forward)
+#ifndef SRK_C1_ROWS   // (experiment builds: -DSRK_C1_ROWS=n)
+#define SRK_C1_ROWS 8
+#endif
+constexpr int kRows = SRK_C1_ROWS;   // image rows per block (forward): 2 -> 8 = 340 -> 276 us at cfg3 (r05r), the
+                                     // per-block weight loads and the halo amortised over 4x the outputs
 constexpr int kRowsW = 8;            // image rows per grid-stride step of the weight gradient: the
                                      // (KH - 1)-row halo and the two barriers amortised over 4x the rows
 constexpr int kWgradBlocks = 1024;   // persistent blocks of the backward (partials: 5.8 MB)

@@ -32,6 +32,9 @@ constexpr int kRows = SRK_C1_ROWS;   // image rows per block (forward): 2 -> 8 =
                                      // per-block weight loads and the halo amortised over 4x the outputs
 constexpr int kRowsW = 8;            // image rows per grid-stride step of the weight gradient: the
                                      // (KH - 1)-row halo and the two barriers amortised over 4x the rows
+#ifndef SRK_C1W_PF   // weight gradient: next slab's patch prefetched into registers (1) or loaded per slab (0)
+#define SRK_C1W_PF 0
+#endif
 constexpr int kWgradBlocks = 1024;   // persistent blocks of the backward (partials: 5.8 MB)
 
 struct C1Args {
@@ -231,11 +234,37 @@ __global__ __launch_bounds__(256) void conv1_pool_wgrad_kernel(C1Args a) {
 #pragma unroll
   for (int t = 0; t < T; ++t) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
   v4f dbacc = {0.f, 0.f, 0.f, 0.f};
+  // the next slab's input patch is fetched into registers under this slab's taps (8 per thread: up to 2,048
+  // patch values; larger patches take the synchronous load)
+  constexpr int PR = kRowsW + KH - 1;
+  const int PC = a.W + KW - 1;
+  const bool pf = SRK_C1W_PF && PR * PC <= 256 * 8;
+  float pr[8];
+  auto fetch_patch = [&](int b) {
+    const int n = b / hp, h0 = (b % hp) * kRowsW;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = threadIdx.x + j * 256;
+      const int r = i / PC, cidx = i % PC;
+      const int h = h0 - a.ph + r, w = cidx - a.pw;
+      pr[j] = (i < PR * PC && h >= 0 && h < a.H && w >= 0 && w < a.W) ? a.x[((size_t)n * a.H + h) * a.W + w] : 0.f;
+    }
+  };
+  if (pf && (int)blockIdx.x < a.N * hp) fetch_patch(blockIdx.x);
   for (int blk = blockIdx.x; blk < a.N * hp; blk += gridDim.x) {
     const int n = blk / hp, h0 = (blk % hp) * kRowsW;
     __syncthreads();   // previous patch fully consumed
-    load_patch<KH, KW, kRowsW>(a, n, h0, patch, pitch);
+    if (pf) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = threadIdx.x + j * 256;
+        if (i < PR * PC) patch[(i / PC) * pitch + i % PC] = pr[j];
+      }
+    } else {
+      load_patch<KH, KW, kRowsW>(a, n, h0, patch, pitch);
+    }
     __syncthreads();
+    if (pf && blk + (int)gridDim.x < a.N * hp) fetch_patch(blk + gridDim.x);
     const int rows = min(kRowsW, a.H - h0);
     // the dY quads and argmax words of the next two pixels are in flight while this one's taps run (the loop
     // was bound by their load latency at 2 waves per SIMD, not by its LDS reads or FMAs: 336 -> 297 us with one)

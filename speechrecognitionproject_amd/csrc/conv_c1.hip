@@ -32,8 +32,8 @@ constexpr int kRows = SRK_C1_ROWS;   // image rows per block (forward): 2 -> 8 =
                                      // per-block weight loads and the halo amortised over 4x the outputs
 constexpr int kRowsW = 8;            // image rows per grid-stride step of the weight gradient: the
                                      // (KH - 1)-row halo and the two barriers amortised over 4x the rows
-#ifndef SRK_C1W_PF   // weight gradient: next slab's patch prefetched into registers (1) or loaded per slab (0)
-#define SRK_C1W_PF 0
+#ifndef SRK_C1W_PF   // weight gradient: next slab's patch prefetched into registers (1: 295 -> 274 us, r05t) or per slab (0)
+#define SRK_C1W_PF 1
 #endif
 constexpr int kWgradBlocks = 1024;   // persistent blocks of the backward (partials: 5.8 MB)
 

@@ -420,7 +420,11 @@ class Workload:
         # bucket's gradients are final, joined before Adam) on the capture-only process group;
         # --allreduce-outside-graph replays forward + backward and runs one flat all-reduce + Adam eagerly
         self.exchange_in_graph = (graph and self.world > 1 and args.overlap and not args.allreduce_outside_graph)
-        self.reducer = (parallel.GradReducer(self.flat, bucket_mb=args.bucket_mb, capture_group=parallel.capture_group())
+        if graph and self.world > 1:
+            parallel.capture_group()   # before any capture: SyncBN's captured exchanges use it in every form
+        self.reducer = (parallel.GradReducer(
+            self.flat, bucket_mb=args.bucket_mb,
+            capture_group=parallel.capture_group() if self.exchange_in_graph else None)
                         if (self.world > 1 and args.overlap and (self.exchange_in_graph or not graph)) else None)
         graphs = []
         if graph:

@@ -1349,8 +1349,8 @@ __device__ __forceinline__ u32x4_ r16_frag(const unsigned short* img, int r0, in
   return u32x4_{l2.x, l2.y, h2.x, h2.y};
 }
 
-// QS: k-steps (16 deep) per MFMA section, as gemm_g16_kernel's: 1 = a barrier pair per k-step (BN / 32
-// MFMAs per wave between barriers: 2 at BN = 64), 2 = the whole 32-deep K-tile per section (twice the
+// QS: k-steps (16 deep) per MFMA section: 1 = a barrier pair per k-step (BN / 32 MFMAs per wave
+// between barriers), 2 = the whole 32-deep K-tile per section (twice the
 // MFMAs per barrier pair, both DMAs issued in the one load section) — option conv_ring_qs
 // NST: ring stages (4; up to 160 KB of LDS: 5 at BN = 256, 6 at BN <= 128).  Deeper rings measured slower on the
 // cfg3 / cfg4 shapes (r05c: rn_l4 wgrad 486 -> 587 us at 5 stages), so only NST = 4 is instantiated.
@@ -1359,17 +1359,15 @@ __device__ __forceinline__ void wait_vm() {
   static_assert(VM >= 0 && VM < 64, "vmcnt is 6 bits");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
 }
-// PERS: persistent tile loop (option conv_ring_pers) — a grid of one workgroup per CU walks the tiles (virtual
-// block v = blockIdx.x + r gridDim.x through the same XCD-aware map), and the ring runs on across tiles: the
-// last K-steps of a tile issue the NEXT tile's first NST - 1 K-tiles, so its prologue latency hides behind this
-// tile's MFMAs and epilogue (short-K convs — fbanks_cnn conv2: K = 448, 14 K-tiles — spent about half of each
-// tile in that prologue at one workgroup per CU).  Needs every tile's K range >= NST - 1 K-tiles (host check).
-template <int MODE, int BN, int LP, int QS = 1, int NST = 4, bool PERS = false>
+// Measured and dropped in round 5 (git history keeps them): a persistent tile loop running the ring across
+// tiles, and 256 x 64 tiles for N = 64.
+template <int MODE, int BN, int LP, int QS = 1, int NST = 4>
 __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
   constexpr int BK = kR16BK;
   constexpr bool AKC = MODE != kWgrad;
   constexpr int HALF = 128 * BK;                     // 8 KB of 16-bit elements per half image
-  constexpr int NBH = BN >= 128 ? BN / 128 : 1;   // BN = 64: one 128-wide B image, its upper half masked
+  static_assert(BN == 128 || BN == 256, "ring16: 128- or 256-wide tiles");
+  constexpr int NBH = BN / 128;
   constexpr int STAGE = (2 + NBH) * HALF;
   constexpr int NDMA = 2 + NBH;
   constexpr int WR = BN == 256 ? 1 : 2, WC = 4 / WR;
@@ -1505,9 +1503,8 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
     else wait_vm<0>();
   };
 
-  int vt = blockIdx.x;
-  TileC cur, nxt;
-  coords(vt, cur);
+  TileC cur;
+  coords(blockIdx.x, cur);
   for (int t = 0; t < NST - 1; ++t)
     if (t < cur.nk) {
       dma_a(cur, t, t);
@@ -1520,11 +1517,8 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
   const int ar0 = wr * (128 / WR);
   const int bh = (wc * (BN / WC)) / 128, bc0 = (wc * (BN / WC)) % 128;
   const int lh = lane >> 5, lc = lane & 31;
-  int g0 = 0;   // the ring's K-tile count at this tile's first K-tile
-  while (true) {
-    const int vn = vt + (int)gridDim.x;
-    const bool has_next = PERS && vn < c.nblk;
-    if (has_next) coords(vn, nxt);
+  const int g0 = 0;   // the ring's K-tile count at this tile's first K-tile
+  {
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -1538,7 +1532,7 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
       const unsigned short* S = smem + ((g0 + kt) % NST) * STAGE;
       const unsigned short* As = S + grp * HALF;
       const unsigned short* Bs = S + (2 + bh) * HALF;
-      const int tn_ = kt + NST - 1;   // the K-tile issued now (this tile's, or the next tile's first ones)
+      const int tn_ = kt + NST - 1;   // the K-tile issued now
       static_assert(QS == 1 || QS == 2, "ring16: 1 or 2 k-steps per section");
 #pragma unroll
       for (int q = 0; q < BK / 16; q += QS) {
@@ -1550,9 +1544,9 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
 #pragma unroll
           for (int j = 0; j < TN; ++j) fb[e][j] = r16_frag<false>(Bs, bc0 + j * 32, 16 * (q + e), lane);
         }
-        if (tn_ < nk || has_next) {
-          const TileC& T = tn_ < nk ? cur : nxt;
-          const int tt = tn_ < nk ? tn_ : tn_ - nk;
+        if (tn_ < nk) {
+          const TileC& T = cur;
+          const int tt = tn_;
           if (QS == 2) {
             dma_a(T, tt, g0 + tn_);
             dma_b(T, tt, g0 + tn_);
@@ -1562,8 +1556,8 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
             dma_b(T, tt, g0 + tn_);
           }
         }
-        // K-tile kt + 1 (of the ring) landed, this wave's part; with a next tile the ring stays full
-        if (q + QS == BK / 16) retire_keep(has_next ? NST - 2 : min(nk - 1 - (kt + 1), NST - 2));
+        // K-tile kt + 1 (of the ring) landed, this wave's part
+        if (q + QS == BK / 16) retire_keep(min(nk - 1 - (kt + 1), NST - 2));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         bar();
         __builtin_amdgcn_s_setprio(1);
@@ -1578,7 +1572,7 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
       }
     }
 
-    // epilogue straight from the accumulators (no LDS: the ring keeps running for the next tile)
+    // epilogue straight from the accumulators
     const int64_t rbase = cur.m0 + grp * 128 + ar0;
     const int64_t cbase = cur.n0 + bh * 128 + bc0;
     if (MODE == kFwd && c.pool_w == 4 && !c.partial) {
@@ -1621,10 +1615,6 @@ __global__ __launch_bounds__(512, 1) void conv_ring16_kernel(ConvArgs c) {
           }
         }
     }
-    if (!has_next) break;
-    g0 += nk;
-    cur = nxt;
-    vt = vn;
   }
   if (grp == 0) bar();
 }
@@ -1977,13 +1967,12 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
   if (MODE != kWgrad && chans % RBK) return 1;
   if (MODE == kWgrad && c.Ci % unit) return 1;
   if (MODE == kDgrad && (c.sh != 1 || c.sw != 1)) return 1;
-  // 16-bit operands down to N = 64 (a 256 x 64 tile: the narrow data gradients of 64-channel inputs)
-  if (c.Nn % unit || c.Nn < (lp && g_opt_conv_ring64 ? 64 : 128) || c.M < 256 || c.M >= INT32_MAX || c.K >= INT32_MAX)
+  if (c.Nn % unit || c.Nn < 128 || c.M < 256 || c.M >= INT32_MAX || c.K >= INT32_MAX)
     return 1;
   const double xb = (double)esz * c.N * c.H * c.W * c.Ci, yb = (double)esz * c.N * c.Ho * c.Wo * c.Co,
                wb = (double)esz * c.K * c.Nn;
   if (xb >= 2.1e9 || yb >= 2.1e9 || wb >= 2.1e9) return 1;
-  const int BN = c.Nn >= 256 ? 256 : c.Nn >= 128 ? 128 : 64;
+  const int BN = c.Nn >= 256 ? 256 : 128;
   const int64_t tm = (c.M + 255) / 256, tn = (c.Nn + BN - 1) / BN;
   const int splits0 = choose_splits(tm * tn, c.K, RBK, kCUs, MODE == kWgrad ? 256 : 16);
   c.kchunk = splits0 > 1 ? ((c.K + splits0 - 1) / splits0 + RBK - 1) / RBK * RBK : std::max<int64_t>(c.K, 1);
@@ -2009,9 +1998,7 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
                  2.0 * (double)c.M * (double)c.Nn * (double)c.K);
   prof.detail("conv_ring%s_kernel<%s,256x%d%s%s> %lldx%lldx%lld s%d", lp ? "16" : "",
               MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad", BN, (MODE == kFwd && c.pool_w) ? ",pool" : "",
-              lp && BN >= 128 && ((g_opt_conv_ring_qs >> (BN == 128 ? 1 : 2)) & 1)
-                  ? (((g_opt_conv_ring_pers >> (BN == 128 ? 1 : 2)) & 1) && c.nblk > kCUs ? ",qs2,pers" : ",qs2")
-                  : "",
+              lp && ((g_opt_conv_ring_qs >> (BN == 128 ? 1 : 2)) & 1) ? ",qs2" : "",
               (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
   const dim3 grid((unsigned)c.nblk), block(512);
   if (!lp) {
@@ -2019,24 +2006,15 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
     else hipLaunchKernelGGL((conv_ring_kernel<MODE, 128>), grid, block, 0, s, c);
   } else {
     // the 16-bit ring: BN x precision x k-steps per section (QS 2 where the option asks for it at this width:
-    // bit 0 BN 64, bit 1 BN 128, bit 2 BN 256)
-    const int wbit = BN == 64 ? 0 : BN == 128 ? 1 : 2;
-    const bool qs2 = BN >= 128 && ((g_opt_conv_ring_qs >> wbit) & 1);
-    // persistent tile loop (QS 2 rings): more tiles than workgroups, every tile's K range >= 3 K-tiles
-    const int64_t klast = c.K - (int64_t)(splits - 1) * c.kchunk;
-    const bool pers = qs2 && ((g_opt_conv_ring_pers >> wbit) & 1) && c.nblk > kCUs &&
-                      std::min<int64_t>(c.kchunk, klast) >= 3 * RBK;
-    const dim3 pgrid(pers ? (unsigned)kCUs : grid.x);
+    // bit 1 BN 128, bit 2 BN 256)
+    const bool qs2 = (g_opt_conv_ring_qs >> (BN == 128 ? 1 : 2)) & 1;
 #define SRK_R16(BN_, LP_)                                                                                   \
-  if (pers) hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 2, 4, true>), pgrid, block, 0, s, c);  \
-  else if (qs2) hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 2>), grid, block, 0, s, c);         \
+  if (qs2) hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 2>), grid, block, 0, s, c);              \
   else hipLaunchKernelGGL((conv_ring16_kernel<MODE, BN_, LP_, 1>), grid, block, 0, s, c);
     if (prec == kPrecBF16) {
-      if (BN == 256) { SRK_R16(256, 1) } else if (BN == 128) { SRK_R16(128, 1) }
-      else hipLaunchKernelGGL((conv_ring16_kernel<MODE, 64, 1>), grid, block, 0, s, c);
+      if (BN == 256) { SRK_R16(256, 1) } else { SRK_R16(128, 1) }
     } else {
-      if (BN == 256) { SRK_R16(256, 2) } else if (BN == 128) { SRK_R16(128, 2) }
-      else hipLaunchKernelGGL((conv_ring16_kernel<MODE, 64, 2>), grid, block, 0, s, c);
+      if (BN == 256) { SRK_R16(256, 2) } else { SRK_R16(128, 2) }
     }
 #undef SRK_R16
   }
@@ -2428,31 +2406,6 @@ int srk_conv2d_nhwc_fwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
     c.a16 = d16[0];
     c.b16 = d16[1];
     if (x16 && x16_written) *x16_written = 1;
-    // fbanks_cnn conv2 + maxpool2: the row-staged kernel (weights resident in LDS, 8 image rows per tile)
-    if (srk::g_opt_conv_row16 && KH == 1 && KW == 7 && ph == 0 && pw == 3 && W == 40 && Ci == 64 && Co == 128 &&
-        pool_w == 4 && (N * H) < (1LL << 30) / (W * Ci)) {
-      srk::RowArgs ra{};
-      ra.x16 = c.a16;
-      ra.w16 = c.b16;
-      ra.bias = bias;
-      ra.y = y;
-      ra.arg = argmax;
-      ra.rows = (int)(N * H);
-      ra.groups = (int)((N * H + 7) / 8);
-      srk::ProfScope prof("conv_fwd_lp", s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
-      prof.detail("conv_row16_pool_kernel %lldx%lldx%lld", (long long)c.M, (long long)c.Nn, (long long)c.K);
-      const bool w4 = srk::g_opt_conv_row16 == 2;
-      const dim3 grid((unsigned)std::min<int64_t>(ra.groups, srk::kCUs)), block(w4 ? 256 : 512);
-      if (prec == srk::kPrecBF16) {
-        if (w4) hipLaunchKernelGGL((srk::conv_row16_pool_kernel<1, 7, 3, 40, 64, 128, 8, 4>), grid, block, 0, s, ra);
-        else hipLaunchKernelGGL((srk::conv_row16_pool_kernel<1, 7, 3, 40, 64, 128, 8, 8>), grid, block, 0, s, ra);
-      } else {
-        if (w4) hipLaunchKernelGGL((srk::conv_row16_pool_kernel<2, 7, 3, 40, 64, 128, 8, 4>), grid, block, 0, s, ra);
-        else hipLaunchKernelGGL((srk::conv_row16_pool_kernel<2, 7, 3, 40, 64, 128, 8, 8>), grid, block, 0, s, ra);
-      }
-      SRK_CHECK_HIP(hipGetLastError());
-      return SRK_OK;
-    }
     // fbanks_cnn conv2 + maxpool2: the row-staged kernel (weights resident in LDS, 8 image rows per tile)
     if (srk::g_opt_conv_row16 && KH == 1 && KW == 7 && ph == 0 && pw == 3 && W == 40 && Ci == 64 && Co == 128 &&
         pool_w == 4 && (N * H) < (1LL << 30) / (W * Ci)) {

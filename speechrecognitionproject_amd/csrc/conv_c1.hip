@@ -119,107 +119,8 @@ __global__ __launch_bounds__(256) void conv1_pool_fwd_kernel(C1Args a) {
   }
 }
 
-// The same forward on the matrix cores (option conv1_mfma, default 0: measured slower, srk_internal.h):
-// v_mfma_f32_32x32x2_f32 is bit for bit
-// a k-ordered fp32 fmaf chain (cdna_hip_programming.md §3), so with C = the bias and the taps fed in the VALU
-// kernel's order (t = kh * KW + kw ascending; the one pad tap, x = w = 0, first: fma(0, 0, b) = b) every
-// pre-pool value is the VALU kernel's bit for bit, at ~99 % of the fp32 matrix rate instead of the VALU's
-// issue-bound ~55 %.  Wave = groups of 32 pooled outputs (the MFMA rows) x 64 channels (two 32-column
-// blocks): per pool position p one 11-step MFMA chain per column block, then the running max / first-argmax
-// over p in registers (the accumulator layouts coincide).  Block = 4 waves over kRowsM image rows.
-typedef float f32x16c __attribute__((ext_vector_type(16)));
-constexpr int kRowsM = 16;
-template <int KH, int KW, int PW, int LP>
-__global__ __launch_bounds__(256) void conv1_pool_fwd_mfma_kernel(C1Args a) {
-  constexpr int T = KH * KW, KS = (T + 2) / 2;   // k-steps of 2 taps, the pad tap first
-  static_assert(T == 21, "conv1 geometries with 21 taps");
-  extern __shared__ float patch[];
-  const int pitch = a.W + KW - 1 + 1;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 31, kk = lane >> 5;
-  const int hp = (a.H + kRowsM - 1) / kRowsM;
-  const int n = blockIdx.x / hp, h0 = (blockIdx.x % hp) * kRowsM;
-  load_patch<KH, KW, kRowsM>(a, n, h0, patch, pitch);
-  // B operands: w[co][t] for co = nb * 32 + li, t = 2 s - 1 + kk (s = 0, kk = 0: the pad tap)
-  float wb[2][KS];
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-    for (int s2 = 0; s2 < KS; ++s2) {
-      const int t = 2 * s2 - 1 + kk;
-      wb[nb][s2] = t >= 0 ? a.w[(nb * 32 + li) * T + t] : 0.f;
-    }
-  // this lane's tap offsets in the patch (row * pitch + col) per k-step; -1: the pad tap
-  int toff[KS];
-#pragma unroll
-  for (int s2 = 0; s2 < KS; ++s2) {
-    const int t = 2 * s2 - 1 + kk;
-    toff[s2] = t >= 0 ? (t / KW) * pitch + (t % KW) : -1;
-  }
-  const float b0 = a.bias[li], b1 = a.bias[32 + li];
-  __syncthreads();
-  const int Wq = a.W / PW;
-  const int rows = min(kRowsM, a.H - h0);
-  const int outs = rows * Wq, groups = (outs + 31) / 32;
-  for (int g = wave; g < groups; g += 4) {
-    // A row li: pooled output o = g * 32 + li (masked past the block's outputs)
-    const int o = g * 32 + li;
-    const bool ok = o < outs;
-    const int r = ok ? o / Wq : 0, wq = ok ? o % Wq : 0;
-    const float* prow = patch + r * pitch + wq * PW;
-    auto chain = [&](int p, f32x16c& c0, f32x16c& c1) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        c0[e] = b0;
-        c1[e] = b1;
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < KS; ++s2) {
-        const float av = (ok && toff[s2] >= 0) ? prow[p + toff[s2]] : 0.f;
-        c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wb[0][s2], c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wb[1][s2], c1, 0, 0, 0);
-      }
-    };
-    f32x16c best0, best1;
-    chain(0, best0, best1);
-    unsigned ix0[4] = {0u, 0u, 0u, 0u}, ix1[4] = {0u, 0u, 0u, 0u};   // argmax bytes: [e >> 2], byte e & 3
-#pragma unroll 1
-    for (int p = 1; p < PW; ++p) {
-      f32x16c a0, a1;
-      chain(p, a0, a1);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {   // the maxpool rule: first maximum, NaN wins
-        const bool t0 = a0[e] > best0[e] || (a0[e] != a0[e] && best0[e] == best0[e]);
-        const bool t1 = a1[e] > best1[e] || (a1[e] != a1[e] && best1[e] == best1[e]);
-        best0[e] = t0 ? a0[e] : best0[e];
-        best1[e] = t1 ? a1[e] : best1[e];
-        const unsigned sh = 8 * (e & 3), m = ~(0xFFu << sh), pv = (unsigned)p << sh;
-        ix0[e >> 2] = t0 ? ((ix0[e >> 2] & m) | pv) : ix0[e >> 2];
-        ix1[e >> 2] = t1 ? ((ix1[e >> 2] & m) | pv) : ix1[e >> 2];
-      }
-    }
-    // D row of register e: 8 (e >> 2) + 4 kk + (e & 3); column li (+ 32)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int orow = g * 32 + 8 * (e >> 2) + 4 * kk + (e & 3);
-      if (orow >= outs) continue;
-      const int rr = orow / Wq, qq = orow - rr * Wq;
-      const size_t oo = (((size_t)n * a.H + h0 + rr) * Wq + qq) * kCo + li;
-      const float v0 = best0[e], v1 = best1[e];
-      a.y[oo] = v0;
-      a.y[oo + 32] = v1;
-      a.arg[oo] = (uint8_t)(ix0[e >> 2] >> (8 * (e & 3)));
-      a.arg[oo + 32] = (uint8_t)(ix1[e >> 2] >> (8 * (e & 3)));
-      if (LP == 1) {
-        a.y16[oo] = __builtin_bit_cast(unsigned short, (__bf16)v0);
-        a.y16[oo + 32] = __builtin_bit_cast(unsigned short, (__bf16)v1);
-      }
-      if (LP == 2) {
-        a.y16[oo] = __builtin_bit_cast(unsigned short, (_Float16)v0);
-        a.y16[oo + 32] = __builtin_bit_cast(unsigned short, (_Float16)v1);
-      }
-    }
-  }
-}
+// Measured and dropped in round 5 (git history keeps it): the same forward on the fp32 matrix cores
+// (bitwise this kernel, but its per-element stores from the accumulator layout cost 406-423 vs 330 us).
 
 template <int KH, int KW, int PW>
 __global__ __launch_bounds__(256) void conv1_pool_wgrad_kernel(C1Args a) {
@@ -411,21 +312,14 @@ int srk_conv1_pool_fwd16(const float* x, int64_t N, int64_t H, int64_t W, const 
   a.x = x; a.w = w; a.bias = bias; a.y = y; a.arg = argmax;
   a.y16 = static_cast<unsigned short*>(y16);
   hipStream_t s = srk::as_stream(stream);
-  const bool mf = srk::g_opt_conv1_mfma != 0;
-  const int rows_blk = mf ? srk::kRowsM : srk::kRows;
-  const int hp = (int)((H + rows_blk - 1) / rows_blk);
-  const size_t lds = (size_t)(rows_blk + KH - 1) * (W + KW) * 4;
+  const int hp = (int)((H + srk::kRows - 1) / srk::kRows);
+  const size_t lds = (size_t)(srk::kRows + KH - 1) * (W + KW) * 4;
   // algorithmic: the input image once + pooled output + argmax (+ the 16-bit copy)
   srk::ProfScope prof("conv1_pool_fwd", s, 4.0 * N * H * W + (lp ? 7.0 : 5.0) * N * H * (W / pool) * Co);
-  prof.detail("conv1_pool_fwd_%s<%lldx%lld,pool%lld>", mf ? "mfma" : "valu", (long long)KH, (long long)KW,
-              (long long)pool);
+  prof.detail("conv1_pool_fwd_valu<%lldx%lld,pool%lld>", (long long)KH, (long long)KW, (long long)pool);
   const dim3 g((unsigned)(N * hp));
 #define SRK_C1F(KH_, KW_, PW_)                                                                                  \
-  if (mf) {                                                                                                     \
-    if (lp == 1) hipLaunchKernelGGL((srk::conv1_pool_fwd_mfma_kernel<KH_, KW_, PW_, 1>), g, dim3(256), lds, s, a); \
-    else if (lp == 2) hipLaunchKernelGGL((srk::conv1_pool_fwd_mfma_kernel<KH_, KW_, PW_, 2>), g, dim3(256), lds, s, a); \
-    else hipLaunchKernelGGL((srk::conv1_pool_fwd_mfma_kernel<KH_, KW_, PW_, 0>), g, dim3(256), lds, s, a);     \
-  } else if (lp == 1) hipLaunchKernelGGL((srk::conv1_pool_fwd_kernel<KH_, KW_, PW_, 1>), g, dim3(256), lds, s, a); \
+  if (lp == 1) hipLaunchKernelGGL((srk::conv1_pool_fwd_kernel<KH_, KW_, PW_, 1>), g, dim3(256), lds, s, a); \
   else if (lp == 2) hipLaunchKernelGGL((srk::conv1_pool_fwd_kernel<KH_, KW_, PW_, 2>), g, dim3(256), lds, s, a);  \
   else hipLaunchKernelGGL((srk::conv1_pool_fwd_kernel<KH_, KW_, PW_, 0>), g, dim3(256), lds, s, a);
   if (KH == 7) {

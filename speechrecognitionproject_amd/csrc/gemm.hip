@@ -41,7 +41,6 @@ struct KernelArgs {
   int sk_wgs;
   int sk_ki;
   float* sk_slab;
-  int nt_store;          // option gemm_nt_store: the final C stores of pp_epilogue non-temporal
 };
 
 // tile index t (one split's grid, grouped order) -> (tile row, tile column); see map_tile
@@ -840,41 +839,6 @@ __device__ __forceinline__ void map_tile_v(int v, int nblk, int tiles, int tiles
   tile_of(lin - split * tiles, tiles_m, tiles_n, group_m, tm, tn);
 }
 
-// Epilogue of the persistent ping-pong kernel: straight from the 32x32 accumulators (a half-wave
-// writes 32 consecutive floats of one row per instruction), no LDS; split-K slabs are
-// [batch][splits][M][N] as in pp_epilogue.
-__device__ __forceinline__ void direct_epilogue(const KernelArgs& ka, const f32x16 (&acc)[4][2], int split, int64_t m0,
-                                                int64_t n0, int grp, int wc, int lane, int64_t z) {
-  const GemmDesc& d = ka.d;
-  const bool split_mode = ka.partial != nullptr;
-  float* C = split_mode ? ka.partial + (z * (ka.nblk / ka.tiles) + split) * d.M * d.N : d.C + z * d.sC;
-  const int64_t ldc = split_mode ? d.N : d.ldc;
-  const int lh = lane >> 5, lc = lane & 31;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t col = n0 + wc * 64 + j * 32 + lc;
-      if (col >= d.N) continue;
-      const float bcol = (!split_mode && d.bias_mode == 1) ? d.bias[col] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + grp * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row >= d.M) continue;
-        float* c = C + row * ldc + col;
-        if (split_mode) {
-          *c = acc[i][j][r];
-          continue;
-        }
-        float v = d.alpha * acc[i][j][r] + bcol;
-        if (d.bias_mode == 2) v += d.bias[row];
-        if (d.beta != 0.f) v += d.beta * *c;
-        *c = v;
-      }
-    }
-  }
-}
-
 // Epilogue of the ping-pong kernels (gemm_g16_kernel, gemm_p32_kernel): each wave stages 64 x 64
 // fp32 of its 128 x 64 accumulator block per pass through LDS (16 KB per wave, 128 KB for the 8
 // waves; the K ring is idle by then), then writes rows as 16-B vectors (4 rows x 256 B per
@@ -917,8 +881,7 @@ __device__ __forceinline__ void pp_epilogue(const KernelArgs& ka, const f32x16 (
       }
       if (vec && col + 3 < d.N) {
         if (!split_mode && d.beta != 0.f) x += d.beta * *reinterpret_cast<const v4f*>(c);
-        if (ka.nt_store) __builtin_nontemporal_store(x, reinterpret_cast<v4f*>(c));
-        else *reinterpret_cast<v4f*>(c) = x;
+        *reinterpret_cast<v4f*>(c) = x;
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1012,18 +975,10 @@ struct G16Half {
 constexpr int kG16Stages = SRK_G16_STAGES;
 static_assert(kG16Stages >= 4 && kG16Stages <= 5, "g16 ring: 4..5 stages of 32 KB (the epilogue needs 128 KB)");
 
-// PERS: persistent tile loop (option gemm16_persistent) — a grid of one workgroup per CU walks the
-// tiles (virtual block v = blockIdx.x + r gridDim.x through the same XCD-aware map), and the epilogue
-// stores straight from the accumulators (32x32 layout: 128-B row segments per half-wave) instead of
-// staging through the LDS ring, so the next tile's prologue DMA follows the stores at once and the
-// stores drain behind its first K-tiles.
-// QS: k-steps (16 deep) per section.  1: 8 MFMAs per MFMA section (the round-2 form); 2: one whole
-// 32-deep K-tile per section (16 MFMAs, 12 fragments per load section, half the barriers per k) —
-// option gemm16_qs.
-// STATIC_PRIO: no per-section priority flips; the second-dispatched group (waves 4-7, the arbitration
-// loser) runs at s_setprio 1 for the whole loop (MI355X_MICROARCH.md, two waves per SIMD, item 4) —
-// option gemm16_prio.
-template <bool TA, bool TB, bool F16, bool PERS = false, int QS = 1, bool STATIC_PRIO = false>
+// Measured and dropped (rounds 4-5, git history keeps them): a persistent tile loop with a direct
+// epilogue, 32-deep sections (16 MFMAs between barriers), static priority for the second group,
+// non-temporal C stores.
+template <bool TA, bool TB, bool F16>
 __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
   using Ops = LpOps<F16>;
   using e8 = typename Ops::e8;
@@ -1045,7 +1000,7 @@ __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
   };
   const GemmDesc& d = ka.d;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = wave >> 2, wc = wave & 3;
-  for (int vblk = blockIdx.x; vblk < (PERS ? ka.nblk : (int)blockIdx.x + 1); vblk += gridDim.x) {
+  const int vblk = blockIdx.x;
   int split, tm, tn;
   map_tile_v(vblk, ka.nblk, ka.tiles, ka.tiles_m, ka.tiles_n, ka.group_m, ka.remap != 0, split, tm, tn);
   const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
@@ -1123,7 +1078,6 @@ __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
   retire_keep(min(nk - 1, NST - 2));
   bar();
   if (grp == 1) bar();   // the groups run one section apart
-  if (STATIC_PRIO && grp == 1) __builtin_amdgcn_s_setprio(1);
 
   const int bh = wc >> 1, bc0 = (wc & 1) * 64;   // this wave's B half image and its column base there
   for (int kt = 0; kt < nk; ++kt) {
@@ -1131,58 +1085,43 @@ __global__ __launch_bounds__(512, 1) void gemm_g16_kernel(KernelArgs ka) {
     const unsigned short* As = S + grp * HALF;
     const unsigned short* Bs = S + (2 + bh) * HALF;
     const int tn_ = kt + NST - 1;   // the K-tile issued during this one (into K-tile kt - 1's stage)
-    static_assert(QS == 1 || QS == 2, "g16: 1 or 2 k-steps per section");
 #pragma unroll
-    for (int q = 0; q < BK / 16; q += QS) {
-      // ---- load section: k-steps q .. q + QS - 1's fragments (4 A row blocks, 2 B column blocks each)
-      u32x4 fa[QS][4], fb[QS][2];
+    for (int q = 0; q < BK / 16; ++q) {
+      // ---- load section: k-step q's fragments (4 A row blocks, 2 B column blocks)
+      u32x4 fa[4], fb[2];
 #pragma unroll
-      for (int e = 0; e < QS; ++e) {
+      for (int i = 0; i < 4; ++i) fa[i] = HA::frag(As, i * 32, 16 * q, lane);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[e][i] = HA::frag(As, i * 32, 16 * (q + e), lane);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) fb[e][j] = HB::frag(Bs, bc0 + j * 32, 16 * (q + e), lane);
-      }
+      for (int j = 0; j < 2; ++j) fb[j] = HB::frag(Bs, bc0 + j * 32, 16 * q, lane);
 #if !(defined(SRK_G16_EXP) && SRK_G16_EXP == 1)   // experiment builds only: no DMA after the prologue
       if (tn_ < nk) {
-        if (QS == 2) {
-          dma_a(tn_);
-          dma_b(tn_);
-        } else if (q == 0) {
-          dma_a(tn_);
-        } else {
-          dma_b(tn_);
-        }
+        if (q == 0) dma_a(tn_);
+        else dma_b(tn_);
       }
 #endif
 #if !(defined(SRK_G16_EXP) && SRK_G16_EXP == 2)   // experiment builds only: DMA never waited for in the loop
-      if (q + QS == BK / 16) retire_keep(min(nk - 1 - (kt + 1), NST - 2));   // K-tile kt + 1 landed (this wave's part)
+      if (q + 1 == BK / 16) retire_keep(min(nk - 1 - (kt + 1), NST - 2));   // K-tile kt + 1 landed (this wave's part)
 #endif
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this section's fragments are in registers
       bar();
-      // ---- MFMA section: 8 independent accumulators, QS k-steps
-      if (!STATIC_PRIO) __builtin_amdgcn_s_setprio(1);
+      // ---- MFMA section: 8 independent accumulators
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int e = 0; e < QS; ++e)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = Ops::mma(__builtin_bit_cast(e8, fa[e][i]), __builtin_bit_cast(e8, fb[e][j]), acc[i][j]);
-      if (!STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = Ops::mma(__builtin_bit_cast(e8, fa[i]), __builtin_bit_cast(e8, fb[j]), acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
       bar();
     }
   }
   if (grp == 0) bar();   // equal barrier counts; every wave is past its last LDS read and DMA wait
-  if (STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
 
   // ---- epilogue (the ring is idle now): pp_epilogue
 #if defined(SRK_G16_EXP) && SRK_G16_EXP == 3   // experiment builds only: no C stores (kept live)
   if (d.alpha != 12345.f) return;
 #endif
-  if (PERS) direct_epilogue(ka, acc, split, m0, n0, grp, wc, lane, z);
-  else pp_epilogue(ka, acc, reinterpret_cast<float*>(smem), split, m0, n0, grp, wc, wave, lane, z);
-  }   // tiles
+  pp_epilogue(ka, acc, reinterpret_cast<float*>(smem), split, m0, n0, grp, wc, wave, lane, z);
 }
 
 // ------------------------------------------------------------------ skinny GEMMs (VALU)
@@ -1783,7 +1722,6 @@ int plan_launch(const GemmDesc& d, int BM, int BN, int BK, int per_cu, KernelArg
   ka.group_m = group_env > 0 ? group_env
                              : std::max(1, (int)std::lround(std::sqrt(32.0 * per_cu * BN / (double)BM)));
   ka.remap = remap;
-  ka.nt_store = g_opt_gemm_nt_store;
   // Split K when the output grid leaves resident slots idle and K is long (tile::choose_splits).
   const bool can_split = allow_split && (d.batch == 1 || split_batched);
   int splits = can_split ? choose_splits(tm * tn * d.batch, d.K, BK, slots, 16) : 1;
@@ -1933,21 +1871,9 @@ int launch_g16(const GemmDesc& d, hipStream_t s, bool f16) {
   ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
   prof.detail("gemm_g16_kernel<%c%c> %lldx%lldx%lld b%d s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', (long long)d.M,
               (long long)d.N, (long long)d.K, d.batch, splits);
-  const bool pers = g_opt_gemm16_persistent && ka.nblk > kCUs;   // more than one round of tiles
-  const dim3 grid((unsigned)(pers ? kCUs : ka.nblk), (unsigned)d.batch), block(512);
-  if (pers) {
-    if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true, true>), grid, block, 0, s, ka);
-    else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false, true>), grid, block, 0, s, ka);
-  } else if (g_opt_gemm16_qs == 2) {
-    if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true, false, 2>), grid, block, 0, s, ka);
-    else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false, false, 2>), grid, block, 0, s, ka);
-  } else if (g_opt_gemm16_prio) {
-    if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true, false, 1, true>), grid, block, 0, s, ka);
-    else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false, false, 1, true>), grid, block, 0, s, ka);
-  } else {
-    if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true>), grid, block, 0, s, ka);
-    else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false>), grid, block, 0, s, ka);
-  }
+  const dim3 grid((unsigned)ka.nblk, (unsigned)d.batch), block(512);
+  if (f16) hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, true>), grid, block, 0, s, ka);
+  else hipLaunchKernelGGL((gemm_g16_kernel<TA, TB, false>), grid, block, 0, s, ka);
   return finish_splits(d, ka, splits, s);
 }
 

@@ -69,7 +69,6 @@ struct GruPArgs {
   const uint16_t* y16_in;
   float* dw_part;
   int dw_mode;           // option gru_dwhh_fused bits: 2 = h_prev fetched after the exchange barrier, 4 = recurrence waves at prio 1
-  int poll_pipe;         // option gru_poll_pipe: four flag polls in flight (lp2_wait, dc_wait)
 };
 
 size_t fwd_lds_bytes(int H);

@@ -674,32 +674,6 @@ constexpr int kDcXF = 24;   // floats a lane hands its pair partner: 3 gate accu
 __device__ __forceinline__ void dc_wait(const GruPArgs& a, const unsigned* f, int step) {
   const int lane = threadIdx.x & 63;
   unsigned spins = 0;
-  if (a.poll_pipe) {   // four polls in flight (option gru_poll_pipe; lp2_wait)
-    auto poll = [&] {
-      return lane < 32 ? __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xffffffffu;
-    };
-    unsigned q0 = poll();
-    __builtin_amdgcn_s_sleep(1);
-    unsigned q1 = poll();
-    __builtin_amdgcn_s_sleep(1);
-    unsigned q2 = poll();
-    __builtin_amdgcn_s_sleep(1);
-    unsigned q3 = poll();
-    while (true) {
-      if (__all(q0 >= (unsigned)step)) return;
-      q0 = poll();
-      if (__all(q1 >= (unsigned)step)) return;
-      q1 = poll();
-      if (__all(q2 >= (unsigned)step)) return;
-      q2 = poll();
-      if (__all(q3 >= (unsigned)step)) return;
-      q3 = poll();
-      if ((spins += 4) >= a.spin_limit) {
-        if (lane == 0) spin_gave_up(a);
-        return;
-      }
-    }
-  }
   while (true) {
     const unsigned v = lane < 32 ? __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xffffffffu;
     if (__all(v >= (unsigned)step)) break;
@@ -1515,37 +1489,7 @@ __device__ __forceinline__ void lp2_wait(const GruPArgs& a, int dir, int group, 
                                          bool per) {
   const int lane = threadIdx.x & 63;
   unsigned spins = 0;
-  if (per && a.poll_pipe) {   // per-producer flags, four polls in flight (option gru_poll_pipe)
-    // vmcnt retires in order: each check waits only for the oldest of the four loads, so a flag is seen
-    // one load latency (+ a quarter of one) after it lands instead of up to two latencies; the polls still
-    // in flight at the exit retire before the hand-off loads issued after them, which wait a full latency
-    // of their own anyway
-    unsigned* fl = a.counters + pw_flag_lp2(dir, a.G, group, first);
-    auto poll = [&] {
-      return lane < count ? __hip_atomic_load(fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xffffffffu;
-    };
-    unsigned q0 = poll();
-    __builtin_amdgcn_s_sleep(1);
-    unsigned q1 = poll();
-    __builtin_amdgcn_s_sleep(1);
-    unsigned q2 = poll();
-    __builtin_amdgcn_s_sleep(1);
-    unsigned q3 = poll();
-    while (true) {
-      if (__all(q0 >= (unsigned)step)) break;
-      q0 = poll();
-      if (__all(q1 >= (unsigned)step)) break;
-      q1 = poll();
-      if (__all(q2 >= (unsigned)step)) break;
-      q2 = poll();
-      if (__all(q3 >= (unsigned)step)) break;
-      q3 = poll();
-      if ((spins += 4) >= a.spin_limit) {
-        if (lane == 0) spin_gave_up(a);
-        break;
-      }
-    }
-  } else if (per) {   // per-producer flags, this wave's producers only
+  if (per) {   // per-producer flags, this wave's producers only
     unsigned* fl = a.counters + pw_flag_lp2(dir, a.G, group, first);
     while (true) {
       const unsigned v = lane < count ? __hip_atomic_load(fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -2472,7 +2416,6 @@ int gru_persistent_launch(GruPArgs a, bool backward, hipStream_t s) {
     ac.fast_cell = g_opt_gru_fast_cell;
     ac.dc_prio = g_opt_gru_dc_prio;
     ac.dw_mode = g_opt_gru_dwhh_fused;
-    ac.poll_pipe = g_opt_gru_poll_pipe;
     ac.b_begin = c0;
     ac.b_end = std::min(a.B, c0 + rows_per_launch);
     ac.G = (ac.b_end - c0 + rows_g - 1) / rows_g;

@@ -28,21 +28,13 @@ int g_opt_conv_tile = 128;
 int g_opt_conv_ring = 0x77;
 int g_opt_conv_unpool16 = 1;
 int g_opt_conv_colsum16 = 1;
-int g_opt_conv_ring64 = 0;
 int g_opt_conv_ring_qs = 6;
-int g_opt_conv_ring_pers = 0;
-int g_opt_conv1_mfma = 0;
 int g_opt_conv_fast16 = 1;
 int g_opt_conv_row16 = 1;
 int g_opt_conv_row16_dgrad = 2;
 int g_opt_bn_tree = 0;
-int g_opt_gru_poll_pipe = 0;
 int g_opt_mfcc_variant = 3;
 int g_opt_gemm_streamk = 1;
-int g_opt_gemm16_persistent = 0;
-int g_opt_gemm16_qs = 1;
-int g_opt_gemm16_prio = 0;
-int g_opt_gemm_nt_store = 0;
 int g_opt_gemm32_kernel = 0;
 static std::atomic<int> g_opt_matmul_prec{kPrecF32};
 int matmul_prec() { return g_opt_matmul_prec.load(std::memory_order_relaxed); }
@@ -378,23 +370,6 @@ int srk_set_option(const char* name, int64_t value) {
     srk::g_opt_gemm16_kernel = (int)value;
     return SRK_OK;
   }
-  if (n == "gemm16_qs") {   // 16-bit ping-pong GEMM: k-steps per section (1 or 2)
-    SRK_REQUIRE(value == 1 || value == 2, SRK_ERR_INVALID, "gemm16_qs must be 1 or 2");
-    srk::g_opt_gemm16_qs = (int)value;
-    return SRK_OK;
-  }
-  if (n == "gemm16_prio") {   // 16-bit ping-pong GEMM: static priority for waves 4-7 (1) or per-section flips (0)
-    srk::g_opt_gemm16_prio = value != 0;
-    return SRK_OK;
-  }
-  if (n == "gemm_nt_store") {   // ping-pong GEMMs: non-temporal C stores in the LDS-staged epilogue (1) or plain (0)
-    srk::g_opt_gemm_nt_store = value != 0;
-    return SRK_OK;
-  }
-  if (n == "gemm16_persistent") {   // 16-bit ping-pong GEMM: persistent tile loop (1) or one tile per workgroup (0)
-    srk::g_opt_gemm16_persistent = value != 0;
-    return SRK_OK;
-  }
   if (n == "gemm_streamk") {   // fp32 ping-pong GEMM: stream-K over a partial round of tiles (1) or not (0)
     srk::g_opt_gemm_streamk = value != 0;
     return SRK_OK;
@@ -404,17 +379,9 @@ int srk_set_option(const char* name, int64_t value) {
     srk::g_opt_mfcc_variant = (int)value;
     return SRK_OK;
   }
-  if (n == "gru_poll_pipe") {   // 16-bit persistent GRU: four flag polls in flight (1) or one at a time (0)
-    srk::g_opt_gru_poll_pipe = value != 0;
-    return SRK_OK;
-  }
   if (n == "bn_tree") {   // BatchNorm statistics: chunk partials combined as a pairwise tree (1) or in order (0)
     SRK_REQUIRE(value >= 0 && value <= 2, SRK_ERR_INVALID, "bn_tree must be 0, 1 or 2");
     srk::g_opt_bn_tree = (int)value;
-    return SRK_OK;
-  }
-  if (n == "conv_ring64") {   // 16-bit ring convs down to N = 64 (256 x 64 tiles) (1) or N >= 128 only (0)
-    srk::g_opt_conv_ring64 = value != 0;
     return SRK_OK;
   }
   if (n == "conv_ring_qs") {   // 16-bit ring convs: whole K-tiles per MFMA section, mask by width (64, 128, 256)
@@ -435,15 +402,6 @@ int srk_set_option(const char* name, int64_t value) {
   }
   if (n == "conv_fast16") {   // 16-bit-source register-staged convs: uniform-tap fast gathers (1) or generic (0)
     srk::g_opt_conv_fast16 = value != 0;
-    return SRK_OK;
-  }
-  if (n == "conv1_mfma") {   // conv1 + maxpool1 forward on the fp32 matrix cores (1) or the VALU (0)
-    srk::g_opt_conv1_mfma = value != 0;
-    return SRK_OK;
-  }
-  if (n == "conv_ring_pers") {   // 16-bit ring convs (QS 2): persistent tile loop, mask by width (128, 256)
-    SRK_REQUIRE(value >= 0 && value <= 7, SRK_ERR_INVALID, "conv_ring_pers is a 3-bit mask");
-    srk::g_opt_conv_ring_pers = (int)value;
     return SRK_OK;
   }
   if (n == "conv_colsum16") {   // 16-bit modes: conv bias gradients fused into dY's 16-bit conversion (1) or not (0)

@@ -111,20 +111,9 @@ extern int g_opt_conv_unpool16;
 // 16-bit-source modes: the conv bias gradient (column sums of dY) fused into the pass that rounds dY (or
 // unpools it) to its 16-bit copy ("conv_colsum16", default 1; 0 = a separate column-sum pass over dY)
 extern int g_opt_conv_colsum16;
-// 16-bit ring convs for N = 64 .. 127 as 256 x 64 tiles ("conv_ring64", default 0 = N >= 128 only: slower than
-// the register-staged 128 x 64 kernels on fbanks_cnn conv2 / resnet layer1, r05b)
-extern int g_opt_conv_ring64;
 // 16-bit ring convs: whole 32-deep K-tiles per MFMA section (QS 2) by tile width, a mask ("conv_ring_qs": bit 1
-// BN 128, bit 2 BN 256; default 6; bit 0 (BN 64) is ignored: that tile keeps one k-step per section)
+// BN 128, bit 2 BN 256; default 6)
 extern int g_opt_conv_ring_qs;
-// 16-bit ring convs with QS 2: persistent tile loop with the ring running across tiles, by width, a mask
-// ("conv_ring_pers": bit 1 BN 128, bit 2 BN 256; default 0 — measured slower on every cfg3 / cfg4 shape, r05g:
-// rn_l4 fwd 584 vs 535 us, fbanks conv2 fwd 584 vs 551 us)
-extern int g_opt_conv_ring_pers;
-// fused conv1 + maxpool1 forward on the fp32 matrix cores (v_mfma_f32_32x32x2_f32, bitwise the VALU kernel's fma
-// chain) ("conv1_mfma", default 0 = the VALU kernel: the MFMA form measured 406-423 vs 330 us at cfg3, r05e — its
-// per-element scalar stores of y / argmax / y16 from the accumulator layout cost more than the VALU FMAs it saves)
-extern int g_opt_conv1_mfma;
 // register-staged 16-bit-source convs (fwd / dgrad): uniform-tap gathers with per-row bases and zero-filling
 // buffer loads where the channels are a multiple of the K-tile ("conv_fast16", default 1)
 extern int g_opt_conv_fast16;
@@ -140,9 +129,6 @@ extern int g_opt_conv_row16_dgrad;
 // tests/test_conv_gpu.py golden resnet_bgru at B = 2); 2 = in order with the divides in the chain (form 0's
 // bitwise reference)
 extern int g_opt_bn_tree;
-// persistent GRU (16-bit kernels, fp32 two-chain kernels): the per-producer flag wait keeps four polls in flight
-// ("gru_poll_pipe", default 0)
-extern int g_opt_gru_poll_pipe;
 // conv tile shape ("conv_tile": 128 = 128-row tiles of 4 waves, 256 = 256-row tiles of 8 waves on
 // tall convolutions)
 extern int g_opt_conv_tile;
@@ -158,14 +144,6 @@ extern int g_opt_mfcc_variant;
 // stream-K for fp32 ping-pong GEMMs whose 256 x 256 grid covers 1/2 .. 1 round of CUs ("gemm_streamk",
 // default 1)
 extern int g_opt_gemm_streamk;
-// persistent tile loop with direct-store epilogue for the 16-bit ping-pong GEMM ("gemm16_persistent")
-extern int g_opt_gemm16_persistent;
-// k-steps per section of the 16-bit ping-pong GEMM ("gemm16_qs": 1 = 8 MFMAs per section, 2 = 16)
-extern int g_opt_gemm16_qs;
-// 16-bit ping-pong GEMM: static priority for waves 4-7 instead of per-section flips ("gemm16_prio")
-extern int g_opt_gemm16_prio;
-// ping-pong GEMMs: non-temporal stores of C in the LDS-staged epilogue ("gemm_nt_store")
-extern int g_opt_gemm_nt_store;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -29,6 +29,11 @@ import torch
 from scipy.io.wavfile import read
 from torch.utils.data import Dataset as _TorchDataset
 
+class DeviceInWorkerError(RuntimeError):
+    """The per-item ``pitch_shifting`` runs K12 on the GPU; a forked DataLoader worker cannot
+    initialise the GPU.  Raised through ``__getitem__``'s catch-all (it is not a data error)."""
+
+
 LABELS = ['yes', 'no', 'up', 'down', 'left', 'right', 'on', 'off', 'stop', 'go', 'unknown', 'silence']
 SEQ_LENGTH = 16000
 
@@ -91,6 +96,8 @@ class Dataset(_TorchDataset):
                     new_sample = self.add_noise_uniform(new_sample, 0.1)
             new_sample = new_sample.astype(np.float32)
             return {'audio': new_sample, 'label': label_idx if self.mode != "submission" else item_name}
+        except DeviceInWorkerError:
+            raise
         except Exception:                           # dataset.py:124-128 swallows every error
             print("bugged item:", item_name)
             print("label", label_idx, item_name.split('/')[0])
@@ -158,11 +165,17 @@ class Dataset(_TorchDataset):
 
     def pitch_shifting(self, sample):
         """dataset.py:225-235: a level from [-2, -1, 1, 2, None]; None returns the sample, else
-        np.int16(pitch_shift(sample, 16000, n_steps=level)) — one clip through K12 on the device."""
+        np.int16(pitch_shift(sample, 16000, n_steps=level)) — one clip through K12 on the device.
+        It needs the GPU in this process: a DataLoader with ``num_workers > 0`` must use the spawn start
+        method, or use the batched ``DeviceAugment`` (``training.py --loader device``) instead."""
         levels = [-2, -1, 1, 2, None]
         level = levels[randint(0, len(levels) - 1)]
         if level is None:
             return sample
+        if torch.utils.data.get_worker_info() is not None and torch.cuda._is_in_bad_fork():
+            raise DeviceInWorkerError(
+                "Dataset.pitch_shifting runs on the GPU and cannot run in a forked DataLoader worker: use "
+                "num_workers=0, multiprocessing_context='spawn', or DeviceAugment (training.py --loader device)")
         from .features import pitch_shift
         pcm = torch.from_numpy(np.asarray(sample).astype(np.int16).reshape(1, SEQ_LENGTH))
         return pitch_shift(pcm, [0], [level]).cpu().numpy()[0].astype(np.int16)

@@ -884,6 +884,10 @@ class _SyncBatchNormFn(torch.autograd.Function):
         C = x.shape[-1]
         M = x.numel() // C
         _check_cuda(x, gamma, beta, residual)
+        from . import parallel
+        # under a HIP-graph capture the statistics exchange runs on the capture-only group, never on the
+        # default group the eager warm-up steps used; the backward reuses the forward's choice
+        group = parallel.group_for_now(group)
         world, rank = dist.get_world_size(group), dist.get_rank(group)
         # all-gather as an all-reduce of rank-owned slots (x + 0 is exact; works on every backend)
         allst = torch.zeros((world, 3 * C), device=x.device)
@@ -930,6 +934,9 @@ class SyncBatchNorm1d(BatchNorm1d):
     Same parameters / buffers / state_dict keys as BatchNorm1d; eval mode and a world of 1 take the
     plain BatchNorm1d path.  Build one with ``convert_sync_batchnorm(model)``."""
 
+    # a 1-rank group normally takes the plain path; the GPU test of the captured exchange sets this
+    collectives_at_world1 = False
+
     def __init__(self, num_features, eps=1e-5, momentum=0.1, process_group=None):
         super().__init__(num_features, eps, momentum)
         self.process_group = process_group
@@ -939,7 +946,7 @@ class SyncBatchNorm1d(BatchNorm1d):
         # comes through here too, so its statistics span the ranks as well
         import torch.distributed as dist
         if not (self.training and dist.is_available() and dist.is_initialized()
-                and dist.get_world_size(self.process_group) > 1):
+                and dist.get_world_size(self.process_group) > (0 if self.collectives_at_world1 else 1)):
             return super()._normalize(x, gamma, beta, residual, running_mean, running_var, relu)
         return _SyncBatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, self.momentum, self.eps,
                                       relu, self.process_group)

@@ -80,6 +80,22 @@ def capture_group():
     return _CAPTURE_GROUP[1]
 
 
+def group_for_now(group=None):
+    """The process group a collective issued at this point must run on: ``group`` eagerly, the
+    capture-only group while the current stream is capturing a HIP graph (see ``capture_group``; it
+    must already exist — creating a communicator under capture is not possible).  A capture of a
+    collective on a non-default ``group`` has no capture-only counterpart and is refused."""
+    if not (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+        return group
+    if group is not None and group is not dist.group.WORLD:
+        raise RuntimeError("a collective on a non-default process group cannot be captured safely "
+                           "(DESIGN.md §4); run the step eagerly")
+    if _CAPTURE_GROUP is None or _CAPTURE_GROUP[0] is not dist.group.WORLD:
+        raise RuntimeError("a captured collective needs parallel.capture_group() created (on every rank) "
+                           "before the capture starts (DESIGN.md §4)")
+    return _CAPTURE_GROUP[1]
+
+
 def world_size():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
@@ -95,11 +111,14 @@ def broadcast_flat(flat):
         dist.broadcast(flat.data, src=0)
 
 
-def allreduce_grads(flat):
+def allreduce_grads(flat, at_world1=False):
     """Sum the flat gradient buffer over ranks (one collective per step).  The optimizer applies
-    1/world through its grad_scale, so no separate scaling pass runs."""
-    if world_size() > 1:
-        dist.all_reduce(flat.grad, op=dist.ReduceOp.SUM)
+    1/world through its grad_scale, so no separate scaling pass runs.  Inside a HIP-graph capture
+    it runs on the capture-only group (``group_for_now``), never on the default group that the
+    warm-up steps used eagerly.  ``at_world1`` issues it in a 1-rank group too (the GPU test of that
+    capture on a one-GPU box)."""
+    if world_size() > (0 if at_world1 else 1):
+        dist.all_reduce(flat.grad, op=dist.ReduceOp.SUM, group=group_for_now())
 
 
 class GradReducer:

@@ -127,8 +127,10 @@ def _train(args):
     # data-parallel steps are captured whole (the bucketed collectives included, on the capture-only
     # process group) over RCCL; gloo cannot be captured, and --no-dp-graph runs them eagerly
     use_graph = args.graph and (world == 1 or (args.dp_graph and torch.distributed.get_backend() == 'nccl'))
-    reducer = (parallel.GradReducer(flat, capture_group=parallel.capture_group() if use_graph else None)
-               if (world > 1 and args.overlap) else None)
+    # the capture-only group exists before any capture, for the bucketed reducer, the single flat
+    # all-reduce of --no-overlap and SyncBatchNorm's statistics alike (parallel.group_for_now)
+    cap_group = parallel.capture_group() if (use_graph and world > 1) else None
+    reducer = parallel.GradReducer(flat, capture_group=cap_group) if (world > 1 and args.overlap) else None
     scheduler = torch.optim.lr_scheduler.ExponentialLR(optimizer, 0.87)
     criterion = CrossEntropyLoss()
     scaler = None

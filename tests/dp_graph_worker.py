@@ -6,6 +6,9 @@ capture-only process group, parallel.capture_group), the join, and Adam (DESIGN.
 told to issue its collectives anyway: the captured step must then replay the eager step bit for bit
 (a 1-rank SUM is the identity), buckets must be forked during the backward (not all at finish()),
 and a captured collective must actually run on replay (a 1-rank all-gather copies a fresh input).
+Mode "flat_syncbn" (ADVICE r05): no reducer — the single flat all-reduce of ``--no-overlap`` — and
+SyncBatchNorm1d's statistics / backward sums, all captured right after eager warm-up steps on the
+default group; parallel.group_for_now must put the captured ones on the capture-only group.
 Prints one JSON line."""
 import json
 import os
@@ -26,6 +29,7 @@ def _free_port():
 
 def main():
     name, B, precision = sys.argv[1], int(sys.argv[2]), sys.argv[3]
+    mode = sys.argv[4] if len(sys.argv) > 4 else "overlap"
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
     torch.cuda.set_device(0)
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -53,20 +57,34 @@ def main():
         net = importlib.import_module("speechrecognitionproject_amd.models.model_" + name).Network().cuda()
         net.load_state_dict(OM.seeded_state_dict(ocls(), 0))
         net.train()
+        if mode == "flat_syncbn":
+            net = snn.convert_sync_batchnorm(net)
+            snn.SyncBatchNorm1d.collectives_at_world1 = True
         flat = FlatParams(net.parameters())
         opt = Adam(net.parameters(), lr=1e-4, flat=flat)
-        red = parallel.GradReducer(flat, bucket_mb=0.5, collectives_at_world1=True, capture_group=cap_group)
+        red = (parallel.GradReducer(flat, bucket_mb=0.5, collectives_at_world1=True, capture_group=cap_group)
+               if mode == "overlap" else None)
+        groups_used = []
+        real_group_for_now = parallel.group_for_now
+
+        def group_for_now(group=None, real=real_group_for_now):
+            g = real(group)
+            if torch.cuda.is_current_stream_capturing():
+                groups_used.append(g is cap_group)
+            return g
+        parallel.group_for_now = group_for_now
         crit = snn.CrossEntropyLoss()
         # which stream the bucket launches see on their own thread (post-accumulate hooks run on
         # autograd's device thread): GradReducer issues them under the stream begin() saw either way
         hook_view = []
-        orig_launch = red._launch
+        if red is not None:
+            orig_launch = red._launch
 
-        def launch(i, orig=orig_launch):
-            if red.capturing:
-                hook_view.append(bool(torch.cuda.is_current_stream_capturing()))
-            orig(i)
-        red._launch = launch
+            def launch(i, orig=orig_launch):
+                if red.capturing:
+                    hook_view.append(bool(torch.cuda.is_current_stream_capturing()))
+                orig(i)
+            red._launch = launch
         x, y = synthetic_clips(3 * B, seed=23)
         pcm, lab = torch.from_numpy(x).cuda().view(3, B, -1), torch.from_numpy(y).cuda().view(3, B)
         sx, sy = pcm[0].clone(), lab[0].clone()
@@ -74,20 +92,26 @@ def main():
 
         def body():
             opt.zero_grad()
-            red.begin()
+            if red is not None:
+                red.begin()
             loss = crit(net(sx), sy)
             loss.backward()
-            launched.append(len(red.works))          # collectives already forked during backward
-            red.finish()
+            if red is not None:
+                launched.append(len(red.works))          # collectives already forked during backward
+                red.finish()
+            else:
+                parallel.allreduce_grads(flat, at_world1=True)
             opt.step()
             return loss
 
         losses = []
         if graphed:
             g = GraphedStep(body, warmup=2, capture_error_mode="thread_local")
-            out["buckets"] = len(red.buckets)
-            out["forked_during_backward"] = launched[-1]
-            out["launch_thread_stream_capturing"] = hook_view
+            if red is not None:
+                out["buckets"] = len(red.buckets)
+                out["forked_during_backward"] = launched[-1]
+                out["launch_thread_stream_capturing"] = hook_view
+            out["captured_on_capture_group"] = groups_used
             for i in range(K):
                 sx.copy_(pcm[(i + 1) % 3])
                 sy.copy_(lab[(i + 1) % 3])
@@ -102,7 +126,10 @@ def main():
                 if i >= 2:
                     losses.append(loss.item())
         torch.cuda.synchronize()
-        red.remove()
+        parallel.group_for_now = real_group_for_now
+        snn.SyncBatchNorm1d.collectives_at_world1 = False
+        if red is not None:
+            red.remove()
         states.append((flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), losses))
     (p0, m0, v0, l0), (p1, m1, v1, l1) = states
     out["losses_equal"] = l0 == l1

@@ -55,3 +55,17 @@ def test_dp_step_graph_with_captured_allreduce(gpu, name, B, precision):
     assert out["spin_timeouts"] == 0, out
     assert out["captured_collective_replays"] == [True, True, True], out
     assert out["eager_then_capture"] == [float(v) for v in range(2, 10)], out
+
+
+def test_dp_step_graph_flat_allreduce_and_syncbn(gpu):
+    """the single flat all-reduce of --no-overlap and SyncBatchNorm1d's exchanges, captured
+    right after eager warm-up steps on the default group, run on the capture-only group
+    (parallel.group_for_now) and the replays equal the eager steps bit for bit."""
+    r = subprocess.run([sys.executable, os.path.join(HERE, "dp_graph_worker.py"), "resnet_bgru", "16", "fp32",
+                        "flat_syncbn"], env=_env(), capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    # 1 flat all-reduce + SyncBN statistics for every BatchNorm layer, all on the capture group
+    assert len(out["captured_on_capture_group"]) > 10 and all(out["captured_on_capture_group"]), out
+    assert out["losses_equal"] and out["params_equal"], out
+    assert out["spin_timeouts"] == 0, out

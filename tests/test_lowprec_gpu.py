@@ -530,46 +530,12 @@ def test_bigru_backward_when_batched_dwhh_is_unavailable(gpu, precision, H, opts
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0)])
-@pytest.mark.parametrize("M,N,K,beta", [(5120, 3328, 512, 0.0), (8200, 2056, 360, 2.0), (2560, 2560, 2048, 0.0)])
-def test_gemm16_persistent(prec, ta, tb, M, N, K, beta):
-    """srk option gemm16_persistent: the 16-bit ping-pong GEMM as a persistent tile loop (one
-    workgroup per CU walking > 256 tiles; the third shape walks split-K slabs) with the direct-store
-    epilogue == float64 product of the 16-bit values, and == the one-tile-per-workgroup launch up to
-    the epilogue's fp32 rounding."""
-    g = torch.Generator().manual_seed(M + N + K + ta)
-    dt = TORCH_DT[prec]
-    A = torch.randn((K, M) if ta else (M, K), generator=g).to(dt)
-    B = torch.randn((N, K) if tb else (K, N), generator=g).to(dt)
-    C0 = torch.randn(M, N, generator=g)
-    bias = torch.randn(N, generator=g)
-    opA = (A.T if ta else A).double()
-    opB = (B.T if tb else B).double()
-    ref = 0.5 * (opA @ opB) + beta * C0.double() + bias.double()
-    Ad, Bd, bd = A.cuda(), B.cuda(), bias.cuda()
-    outs = []
-    try:
-        _lib.set_option("gemm16_kernel", 2)
-        for pers in (1, 0):
-            _lib.set_option("gemm16_persistent", pers)
-            Cd = C0.clone().cuda()
-            call("srk_gemm_16", ta, tb, M, N, K, 0.5, ptr(Ad), Ad.shape[1], ptr(Bd), Bd.shape[1], beta, ptr(Cd), N,
-                 ptr(bd), 1, stream_ptr())
-            outs.append(Cd.cpu().double())
-    finally:
-        _lib.set_option("gemm16_persistent", 0)
-        _lib.set_option("gemm16_kernel", 0)
-    scale = (opA.abs() @ opB.abs()).max().item()
-    assert (outs[0] - ref).abs().max().item() <= 2e-6 * (1 + scale)
-    assert (outs[0] - outs[1]).abs().max().item() <= 1e-6 * (1 + scale)
-
-
-@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0)])
-@pytest.mark.parametrize("M,N,K,beta", [(5120, 3328, 520, 0.0), (1304, 712, 2056, 2.0), (2560, 2560, 8, 0.0)])
-def test_gemm16_qs(prec, ta, tb, M, N, K, beta):
-    """srk option gemm16_qs = 2: the 16-bit ping-pong GEMM with one whole 32-deep K-tile per section
-    (16 MFMAs, half the barriers) == the 16-deep sections bit for bit (each accumulator adds the same
-    k-steps in the same order) and == float64 of the 16-bit values (k tails: 520, 8; row / column
-    edges: 1304 x 712; split-K: 2056)."""
+@pytest.mark.parametrize("M,N,K,beta", [(5120, 3328, 520, 0.0), (1304, 712, 2056, 2.0), (2560, 2560, 8, 0.0),
+                                        (5120, 3328, 512, 1.0)])
+def test_gemm16_pingpong(prec, ta, tb, M, N, K, beta):
+    """The 16-bit ping-pong GEMM (gemm16_kernel = 2) == float64 of the 16-bit values (k tails: 520, 8;
+    row / column edges: 1304 x 712; split-K: 2056; more than one round of tiles: 5120 x 3328) and == the
+    register-staged 16-bit kernel up to the fp32 summation order."""
     g = torch.Generator().manual_seed(M + 3 * N + K + tb)
     dt = TORCH_DT[prec]
     A = torch.randn((K, M) if ta else (M, K), generator=g).to(dt)
@@ -581,29 +547,22 @@ def test_gemm16_qs(prec, ta, tb, M, N, K, beta):
     Ad, Bd = A.cuda(), B.cuda()
     outs = []
     try:
-        _lib.set_option("gemm16_kernel", 2)
-        # 32-deep sections; static priority (gemm16_prio); non-temporal C stores (gemm_nt_store); baseline
-        for qs, prio, nt in ((2, 0, 0), (1, 1, 0), (1, 0, 1), (1, 0, 0)):
-            _lib.set_option("gemm16_qs", qs)
-            _lib.set_option("gemm16_prio", prio)
-            _lib.set_option("gemm_nt_store", nt)
+        for kern in (2, 1):
+            _lib.set_option("gemm16_kernel", kern)
             Cd = C0.clone().cuda()
             call("srk_gemm_16", ta, tb, M, N, K, 0.5, ptr(Ad), Ad.shape[1], ptr(Bd), Bd.shape[1], beta, ptr(Cd), N,
                  None, 0, stream_ptr())
-            outs.append(Cd.cpu())
+            outs.append(Cd.cpu().double())
     finally:
-        _lib.set_option("gemm16_qs", 1)
-        _lib.set_option("gemm16_prio", 0)
-        _lib.set_option("gemm_nt_store", 0)
         _lib.set_option("gemm16_kernel", 0)
     scale = (opA.abs() @ opB.abs()).max().item()
-    assert (outs[0].double() - ref).abs().max().item() <= 2e-6 * (1 + scale)
-    assert all(torch.equal(o, outs[-1]) for o in outs[:-1])
+    assert (outs[0] - ref).abs().max().item() <= 2e-6 * (1 + scale)
+    assert (outs[0] - outs[1]).abs().max().item() <= 2e-6 * (1 + scale)
 
 
 @pytest.mark.parametrize("shape", [(2, 98, 40, 64, 128, 1, 7, 0, 3), (3, 98, 1, 256, 512, 7, 1, 3, 0),
                                    (2, 1, 1000, 64, 128, 1, 15, 0, 7, 1, 2), (4, 17, 13, 32, 256, 3, 3, 1, 1),
-                                   # more tiles than CUs: the persistent rings (fwd 256 x 128; fwd + dgrad 256 x 256)
+                                   # more tiles than CUs (fwd 256 x 128; fwd + dgrad 256 x 256)
                                    (32, 98, 40, 64, 128, 1, 7, 0, 3), (68, 1, 500, 256, 512, 1, 15, 0, 7)])
 def test_conv_16bit_ring(prec, shape):
     """srk option conv_ring bits 4-6: the 16-bit LDS-DMA ring convolutions (gemm_g16_kernel's
@@ -622,12 +581,9 @@ def test_conv_16bit_ring(prec, shape):
     try:
         # ring (one k-step per MFMA section), ring with whole K-tiles per section (conv_ring_qs, every width),
         # register-staged
-        # (one tile per workgroup, and the persistent tile loop, conv_ring_pers), the 256 x 64 tiles on (conv_ring64)
-        _lib.set_option("conv_ring64", 1)
-        for mask, qs, pers in ((0x70 | 6, 0, 0), (0x70 | 6, 7, 0), (0x70 | 6, 7, 7), (6, 0, 0)):
+        for mask, qs in ((0x70 | 6, 0), (0x70 | 6, 7), (6, 0)):
             _lib.set_option("conv_ring", mask)
             _lib.set_option("conv_ring_qs", qs)
-            _lib.set_option("conv_ring_pers", pers)
             xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
             ym = snn._Conv2dNHWCFn.apply(xm, wm, bm, (ph, pw), (sh, sw))
             (ym * gy).sum().backward()
@@ -636,12 +592,9 @@ def test_conv_16bit_ring(prec, shape):
     finally:
         _lib.set_option("conv_ring", 0x77)
         _lib.set_option("conv_ring_qs", 6)
-        _lib.set_option("conv_ring_pers", 6)
-        _lib.set_option("conv_ring64", 0)
-    for o in outs[1:3]:
-        for a, c in zip(outs[0], o):
-            assert torch.equal(a, c)   # the same MFMA order per accumulator
-    for a, c in zip(outs[0], outs[3]):
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)   # the same MFMA order per accumulator
+    for a, c in zip(outs[0], outs[2]):
         assert ((a - c).abs().max() / c.abs().max()).item() <= 1e-5
 
 

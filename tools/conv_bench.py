@@ -1,10 +1,10 @@
 """Conv micro-benchmark: fwd / dgrad / wgrad of the model_fbanks_cnn layers (B = 512) and the
 model_resnet_bgru stage convs (B = 512), timed with srk_prof events (algorithmic flops / time).
 
-    python tools/conv_bench.py [--prec bf16] [--only fb_conv2,rn_l1] [--var "" --var "conv_ring64=0" ...]
+    python tools/conv_bench.py [--prec bf16] [--only fb_conv2,rn_l1] [--var "" --var "conv_ring_qs=0" ...]
 
 Each --var is a comma-separated srk option list applied with srk_set_option before the shape runs; options
-stay set afterwards, so give every variant the full list it compares (e.g. "conv_ring64=1" / "conv_ring64=0"); fb_conv2 runs as the fused conv + (1, 4) max pool model_fbanks_cnn uses."""
+stay set afterwards, so give every variant the full list it compares (e.g. "conv_ring_qs=6" / "conv_ring_qs=0"); fb_conv2 runs as the fused conv + (1, 4) max pool model_fbanks_cnn uses."""
 import argparse
 import json
 import os

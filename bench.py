@@ -105,6 +105,7 @@ CFG = {"mfcc_bgru": "cfg2 mfcc_bgru: on-device MFCC[39x51] + 2-layer BiGRU(512) 
 # feature kernel of each model and its algorithmic bytes per clip
 FEATURE = {"mfcc_bgru": ("mfcc", 71956), "fbanks_cnn": ("fbank", 111040), "spec_bgru": ("spec", 126916),
            "mfrn_bgru": ("mfcc", 71956), "spec_cnn": ("spec", 126916)}
+FEATURE_BYTES = {k: b for k, b in FEATURE.values()}
 MATRIX_KERNELS = ("gru_fwd_seq", "gru_bwd_seq", "gru_fwd_step", "gru_bwd_step", "gemm_f32",
                   "conv_fwd", "conv_dgrad", "conv_wgrad", "gemm_bf16", "gemm_f16", "gru_fwd_seq_lp", "gru_bwd_seq_lp",
                   "conv_fwd_lp", "conv_dgrad_lp", "conv_wgrad_lp")
@@ -204,21 +205,30 @@ def cpu_baseline(model_name, batch, seconds):
 
 
 def pmc_traffic(kernel, cmd):
-    """HBM bytes per launch of the kernel category `kernel` from the committed PMC summary of THIS
-    command (tools/pmc_traffic.py over separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes,
-    gfx950-corrected): profiles/pmc_traffic_<model>.json, used only when the command it records
-    (model, per-GPU batch, world size, precisions, options) matches `cmd`; otherwise None."""
+    """(HBM bytes per launch, source) of the kernel category `kernel` from the committed PMC summary of
+    THIS command and THIS build (tools/pmc_traffic.py over separate rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes, gfx950-corrected): profiles/pmc_traffic_<model>.json, used only when the command it records
+    (model, per-GPU batch, world size, precisions, options) matches `cmd` AND its source stamp equals the
+    loaded library's srk_source_stamp() — counters of other kernel sources describe other code; else
+    (None, reason)."""
     p = os.path.join(REPO, "profiles", "pmc_traffic_%s.json" % cmd["model"])
     try:
         with open(p) as f:
             doc = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, "no PMC file"
     rec = doc.get("command") or {}
     same = (rec.get("model") == cmd["model"] and rec.get("batch") == cmd["batch"] and rec.get("world") == cmd["world"]
             and cmd["precision"] in rec.get("precisions", ()) and bool(rec.get("sync_bn")) == cmd["sync_bn"])
-    v = doc.get("bytes_per_launch", {}).get(kernel) if same else None
-    return None if v is None else v["total"]
+    if not same:
+        return None, "PMC file of another command"
+    stamp = doc.get("source_stamp")
+    if stamp != _lib.source_stamp():
+        return None, "PMC file of another build (stamp %s, library %s)" % (stamp, _lib.source_stamp())
+    v = doc.get("bytes_per_launch", {}).get(kernel)
+    if v is None:
+        return None, "kernel not in PMC file"
+    return v["total"], "profiles/pmc_traffic_%s.json (%s, stamp %s)" % (cmd["model"], doc.get("source", ""), stamp)
 
 
 def feature_roofline(model_name=None, n_clips=65536, kernel=None):
@@ -259,11 +269,15 @@ def feature_pmc(name, n_clips):
     ent = rec.get("kernels", {}).get(name)
     if rec.get("clips_per_launch") != n_clips or not ent or "traffic_per_launch" not in ent:
         return {}
+    if rec.get("source_stamp") != _lib.source_stamp():     # counters of another build: not this kernel
+        return {"pmc_source": "none: profiles/pmc_feature.json is of another build (stamp %s, library %s)"
+                              % (rec.get("source_stamp"), _lib.source_stamp())}
     pc = ent.get("per_clip", {})
     return {"traffic": ent["traffic_per_launch"], "traffic_per_clip": ent["traffic_per_clip"],
             "sq_insts_valu_per_clip": pc.get("SQ_INSTS_VALU"), "sq_wait_inst_any_per_clip": pc.get("SQ_WAIT_INST_ANY"),
-            "sq_wave_cycles_per_clip": pc.get("SQ_WAVE_CYCLES"),
-            "pmc_source": "profiles/pmc_feature.json (%s)" % rec.get("source", "")}
+            "sq_wave_cycles_per_clip": pc.get("SQ_WAVE_CYCLES"), "sq_insts_lds_per_clip": pc.get("SQ_INSTS_LDS"),
+            "traffic_ratio": round(ent["traffic_per_clip"] / FEATURE_BYTES[name], 3),
+            "pmc_source": "profiles/pmc_feature.json (%s, stamp %s)" % (rec.get("source", ""), rec.get("source_stamp"))}
 
 
 def _relaunch(args):
@@ -618,9 +632,14 @@ def roofline(kernels, singles, cmd):
     k = mm[dom]
     tf = k["work"] / (k["ms_total"] * 1e-3) / 1e12
     peak = PEAK_LP_MFMA_TFLOPS if dom in LP_KERNELS else PEAK_FP32_MFMA_TFLOPS
+    traffic, src = pmc_traffic(dom, cmd)
+    # algorithmic HBM bytes of the category's launches (ProfScope::bytes: operands once + the output)
+    alg = sum(r.get("bytes", 0.0) for r in singles if r["name"] == dom) / k["launches"]
     res = {"bound": "mfma", "kernel": dom, "achieved": round(tf, 2), "peak": peak,
            "unit": "TFLOP/s", "frac": round(tf / peak, 4),
-           "traffic": pmc_traffic(dom, cmd), "traffic_unit": "bytes/launch",
+           "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": src,
+           "algorithmic_bytes_per_launch": round(alg) if alg else None,
+           "traffic_ratio": round(traffic / alg, 3) if traffic and alg else None,
            "avg_launch_ms": round(k["ms_total"] / k["launches"], 5),
            "flops_per_launch": k["work"] / k["launches"]}
     mat = [r for r in singles if r["name"] in MATRIX_KERNELS and r["work"] > 0]

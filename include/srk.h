@@ -36,6 +36,10 @@ enum srk_status {
 
 /* ---------------------------------------------------------------- library / device */
 int srk_version(void);                 /* ABI version, bumped on any signature change */
+/* First 16 hex digits of the sha256 over the library's sources (csrc/*.hip, *.h, *.cpp and this
+ * header, in name order) as built: profiling records (profiles/pmc_*.json) carry the stamp of the
+ * library they measured, and bench.py attaches them only to a run of the same build.              */
+const char* srk_source_stamp(void);
 const char* srk_last_error(void);      /* thread-local, never NULL */
 int srk_init(int device);              /* build + upload constant tables on `device` */
 /* Opt-in kernel timing: while enabled, instrumented launches record a HIP event pair on their
@@ -49,8 +53,10 @@ int64_t srk_scratch_generation(void);
 int srk_prof_enable(int on);
 int srk_prof_read(const char* name, int64_t* count, double* total_ms, double* total_work);
 /* Every record since srk_prof_enable grouped by (name, launch detail: kernel template + shape), one
- * "name\tdetail\tcount\ttotal_ms\ttotal_work\n" line each, NUL-terminated into buf (truncated at
- * cap bytes); *needed = the full size.  bench.py names the largest single kernel with it. */
+ * "name\tdetail\tcount\ttotal_ms\ttotal_work\ttotal_bytes\n" line each, NUL-terminated into buf
+ * (truncated at cap bytes); *needed = the full size.  total_bytes = the launches' ALGORITHMIC HBM
+ * bytes where the launch site states them (matrix kernels: operands once + the output; 0 elsewhere).
+ * bench.py names the largest single kernel with it and prices PMC traffic against the bytes. */
 int srk_prof_kernels(char* buf, int64_t cap, int64_t* needed);
 /* Runtime options: "gru_persistent" (default 1) = run each GRU layer's recurrence as ONE
  * persistent launch with W_hh resident in LDS (0 = one launch per time step);

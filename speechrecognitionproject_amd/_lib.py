@@ -30,6 +30,7 @@ _SIGS = {
     "srk_prof_read": [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
                       ctypes.POINTER(ctypes.c_double)],
     "srk_prof_kernels": [ctypes.c_char_p, _I64, ctypes.POINTER(ctypes.c_int64)],
+    "srk_source_stamp": [],
     "srk_set_option": [ctypes.c_char_p, _I64],
     "srk_spin_timeouts": [],
     "srk_scratch_generation": [],
@@ -110,7 +111,7 @@ _SIGS = {
 }
 _RESTYPE = {"srk_last_error": ctypes.c_char_p, "srk_spin_timeouts": ctypes.c_int64, "srk_scratch_generation": ctypes.c_int64, "srk_gru_workspace_floats": ctypes.c_int64, "srk_gru_y16_offset": ctypes.c_int64,
             "srk_conv2d_workspace_floats": ctypes.c_int64, "srk_conv1_pool_workspace_floats": ctypes.c_int64,
-            "srk_pitch_workspace_bytes": ctypes.c_int64}
+            "srk_pitch_workspace_bytes": ctypes.c_int64, "srk_source_stamp": ctypes.c_char_p}
 
 
 class SrkError(RuntimeError):
@@ -142,6 +143,11 @@ def lib():
     return _lib
 
 
+def source_stamp():
+    """srk_source_stamp(): the source hash the loaded libsrk.so was built from (build.py)."""
+    return lib().srk_source_stamp().decode()
+
+
 def call(name, *args):
     """Invoke an srk_* entry point and raise SrkError with srk_last_error() on failure."""
     rc = getattr(lib(), name)(*args)
@@ -166,16 +172,17 @@ def prof_read(name):
 
 def prof_kernels():
     """Every recorded launch grouped by (category name, kernel template + shape):
-    [{"name", "kernel", "launches", "ms_total", "work"}]."""
+    [{"name", "kernel", "launches", "ms_total", "work", "bytes"}] (bytes: algorithmic HBM bytes, 0 where
+    the launch site does not state them)."""
     need = ctypes.c_int64(0)
     call("srk_prof_kernels", None, 0, ctypes.byref(need))
     buf = ctypes.create_string_buffer(int(need.value) + 256)
     call("srk_prof_kernels", buf, len(buf), ctypes.byref(need))
     out = []
     for line in buf.value.decode().splitlines():
-        name, detail, n, ms, work = line.split("\t")
+        name, detail, n, ms, work, nbytes = line.split("\t")
         out.append({"name": name, "kernel": detail or name, "launches": int(n), "ms_total": float(ms),
-                    "work": float(work)})
+                    "work": float(work), "bytes": float(nbytes)})
     return out
 
 

@@ -1950,6 +1950,19 @@ __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
 
 // The ring conv when the shape qualifies (fp32 operands, option conv_ring, channel-aligned, stride 1
 // for the data gradient, 32-bit byte offsets); returns 1 if it did not run.
+// Algorithmic HBM bytes of one implicit-GEMM conv launch (ProfScope::bytes): the two operand tensors read once
+// at their element size in HBM (esz: 2 for 16-bit sources, 4 otherwise) and the output written once in fp32
+// (a pooled forward: the pooled values + their uint8 argmax).  fwd: x, W -> y; dgrad: dY, W -> dX; wgrad:
+// x, dY -> dW.  A pooled backward's gathers read the pooled dY + argmax instead of the dense dY.
+inline double conv_bytes(const ConvArgs& c, int mode, int esz) {
+  const double x = (double)c.N * c.H * c.W * c.Ci, y = (double)c.N * c.Ho * c.Wo * c.Co,
+               w = (double)c.KH * c.KW * c.Ci * c.Co;
+  const double dy = c.dy_arg ? y / 4.0 * (esz + 1.0) : y * esz;
+  if (mode == kFwd) return (x + w) * esz + (c.pool_w ? y / c.pool_w * 5.0 : y * 4.0);
+  if (mode == kDgrad) return dy + w * esz + x * 4.0;
+  return x * esz + dy + w * 4.0;
+}
+
 template <int MODE>
 int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out, float** partial_out, int* splits_out) {
   const int prec = matmul_prec();
@@ -1996,6 +2009,7 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
   c.fd_kw = FastDiv((unsigned)c.KW);
   ProfScope prof(lp ? (MODE == kFwd ? "conv_fwd_lp" : MODE == kDgrad ? "conv_dgrad_lp" : "conv_wgrad_lp") : name, s,
                  2.0 * (double)c.M * (double)c.Nn * (double)c.K);
+  prof.bytes(conv_bytes(c, MODE, lp ? 2 : 4));
   prof.detail("conv_ring%s_kernel<%s,256x%d%s%s> %lldx%lldx%lld s%d", lp ? "16" : "",
               MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad", BN, (MODE == kFwd && c.pool_w) ? ",pool" : "",
               lp && ((g_opt_conv_ring_qs >> (BN == 128 ? 1 : 2)) & 1) ? ",qs2" : "",
@@ -2128,6 +2142,7 @@ int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
               SRK_ERR_INTERNAL, "conv: unpooling gathers need fp32 sources, 4-aligned channels and Wo % 4 == 0");
   ProfScope prof(prec == kPrecF32 ? name : (MODE == kFwd ? "conv_fwd_lp" : MODE == kDgrad ? "conv_dgrad_lp" : "conv_wgrad_lp"),
                  s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
+  prof.bytes(conv_bytes(c, MODE, c.a16 ? 2 : 4));
   prof.detail("conv_gemm_kernel<%s,%dx%d%s%s%s> %lldx%lldx%lld s%d", MODE == kFwd ? "fwd" : MODE == kDgrad ? "dgrad" : "wgrad",
               BM, BN, NW == 8 ? ",8w" : "", c.a16 ? ",s16" : c.dy_arg ? ",unpool" : (MODE == kFwd && c.pool_w) ? ",pool" : "",
               c.fast16 ? ",fast" : "", (long long)c.M, (long long)c.Nn, (long long)c.K, splits);
@@ -2291,6 +2306,7 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
     srk::ProfScope prof(srk::matmul_prec() == srk::kPrecF32 ? "conv_dgrad" : "conv_dgrad_lp", s,
                         2.0 * (double)g.M * (double)g.N * (double)g.K);
     prof.detail("conv_dgrad_as_gemm %lldx%lldx%lld", (long long)g.M, (long long)g.N, (long long)g.K);
+    prof.bytes(4.0 * ((double)g.M * g.K + (double)g.K * g.N + (double)g.M * g.N));
     if ((rc = srk::gemm_f32(g, s))) return rc;
   } else if (dgrad_implicit && d16[0] && srk::g_opt_conv_row16_dgrad && KH == 1 && KW == 7 && ph == 0 && pw == 3 &&
              sh == 1 && sw == 1 && W == 40 && Ci == 64 && Co == 128 && (N * H) < (1LL << 30) / (W * Co)) {
@@ -2303,6 +2319,7 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
     ra.groups = (int)((N * H + 7) / 8);
     srk::ProfScope prof("conv_dgrad_lp", s, 2.0 * (double)(N * H * W) * (double)Ci * (double)(KW * Co));
     prof.detail("conv_row16_dgrad_kernel %lldx%lldx%lld", (long long)(N * H * W), (long long)Ci, (long long)(KW * Co));
+    prof.bytes(2.0 * (double)(N * H * W) * Co + 2.0 * (double)(KW * Co) * Ci + 4.0 * (double)(N * H * W) * Ci);
     const dim3 grid((unsigned)std::min<int64_t>(ra.groups, srk::kCUs)), block(256);
     const bool bal = srk::g_opt_conv_row16_dgrad == 2;
     if (prec == srk::kPrecBF16 && bal)
@@ -2419,6 +2436,7 @@ int srk_conv2d_nhwc_fwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
       ra.groups = (int)((N * H + 7) / 8);
       srk::ProfScope prof("conv_fwd_lp", s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
       prof.detail("conv_row16_pool_kernel %lldx%lldx%lld", (long long)c.M, (long long)c.Nn, (long long)c.K);
+      prof.bytes(srk::conv_bytes(c, srk::kFwd, 2));
       const bool w4 = srk::g_opt_conv_row16 == 2;
       const dim3 grid((unsigned)std::min<int64_t>(ra.groups, srk::kCUs)), block(w4 ? 256 : 512);
       if (prec == srk::kPrecBF16) {

@@ -1293,10 +1293,18 @@ __global__ __launch_bounds__(256) void skinny_k_kernel(GemmDesc d) {
     d.rowsum[m] = d.rowsum_beta != 0.f ? d.rowsum_beta * d.rowsum[m] + rs : rs;
 }
 
+// Algorithmic HBM bytes of one GEMM launch (ProfScope::bytes): op(A) and op(B) read once at their element
+// size in HBM, C written once (and read once when beta != 0), per batch entry.
+inline double gemm_bytes(const GemmDesc& d, int esz) {
+  const double c = (double)d.M * (double)d.N * 4.0 * (d.beta != 0.f ? 2.0 : 1.0);
+  return ((double)d.M * (double)d.K * esz + (double)d.K * (double)d.N * esz + c) * (double)d.batch;
+}
+
 template <int RND>
 int launch_skinny_rnd(const GemmDesc& d, int kind, hipStream_t s) {
   ProfScope prof(RND == 0 ? "gemm_f32" : RND == 1 ? "gemm_bf16" : "gemm_f16", s,
                  2.0 * (double)d.M * (double)d.N * (double)d.K);
+  prof.bytes(gemm_bytes(d, 4));
   const char* kn = kind == 0 ? "skinny_n" : kind == 1 ? "skinny_m" : "skinny_k";
   prof.detail("%s_kernel<%c%c> %lldx%lldx%lld", kn, d.ta ? 'T' : 'N', d.tb ? 'T' : 'N', (long long)d.M,
               (long long)d.N, (long long)d.K);
@@ -1771,6 +1779,7 @@ int launch(const GemmDesc& d, hipStream_t s, bool vec) {
   int splits = 1;
   if (int rc = plan_launch(d, BM, BN, BK, per_cu, ka, &splits)) return rc;
   ProfScope prof("gemm_f32", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
+  prof.bytes(gemm_bytes(d, 4));
   // 8 waves (4 per SIMD at 2 workgroups / CU) cover the k-tile staging + barrier phases better
   // (measured: weight-gradient GEMMs +4..17 %); the x W^T projection shape keeps 4.
   static const int waves_env = env_int("SRK_GEMM_WAVES", 0);
@@ -1810,6 +1819,7 @@ int launch_lp_cfg(const GemmDesc& d, hipStream_t s, bool vec, bool f16) {
   int splits = 1;
   if (int rc = plan_launch(d, BM, BN, kLpBK, per_cu, ka, &splits)) return rc;
   ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
+  prof.bytes(gemm_bytes(d, 4));   // fp32 operands in HBM, rounded on chip
   prof.detail("gemm_lp_kernel<%c%c,%dx%d> %lldx%lldx%lld s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', BM, BN, (long long)d.M,
               (long long)d.N, (long long)d.K, splits);
   const dim3 grid((unsigned)ka.nblk, 1, (unsigned)d.batch), block(NW * 64);
@@ -1852,6 +1862,7 @@ int launch_h16_cfg(const GemmDesc& d, hipStream_t s, bool f16) {
   int splits = 1;
   if (int rc = plan_launch(d, BM, BN, kLpBK, per_cu, ka, &splits)) return rc;
   ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K);
+  prof.bytes(gemm_bytes(d, 2));
   prof.detail("gemm_h16_kernel<%c%c,%dx%d> %lldx%lldx%lld s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', BM, BN, (long long)d.M,
               (long long)d.N, (long long)d.K, splits);
   const dim3 grid((unsigned)ka.nblk), block(NW * 64);
@@ -1869,6 +1880,7 @@ int launch_g16(const GemmDesc& d, hipStream_t s, bool f16) {
   const int64_t tiles = ((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
   if (int rc = plan_launch(d, 256, 256, kG16BK, 1, ka, &splits, tiles * 2 < kCUs, true)) return rc;
   ProfScope prof(f16 ? "gemm_f16" : "gemm_bf16", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
+  prof.bytes(gemm_bytes(d, 2));
   prof.detail("gemm_g16_kernel<%c%c> %lldx%lldx%lld b%d s%d", TA ? 'T' : 'N', TB ? 'T' : 'N', (long long)d.M,
               (long long)d.N, (long long)d.K, d.batch, splits);
   const dim3 grid((unsigned)ka.nblk, (unsigned)d.batch), block(512);
@@ -1909,6 +1921,7 @@ int launch_p32(const GemmDesc& d, hipStream_t s) {
     if (int rc = get_scratch((size_t)3 * d.M * d.N, &ka.sk_slab)) return rc;   // <= 3 runs per tile (tiles >= W / 2)
   }
   ProfScope prof("gemm_f32", s, 2.0 * (double)d.M * (double)d.N * (double)d.K * d.batch);
+  prof.bytes(gemm_bytes(d, 4));
   prof.detail("gemm_p32_kernel<%c%c> %lldx%lldx%lld b%d s%d%s", TA ? 'T' : 'N', TB ? 'T' : 'N', (long long)d.M,
               (long long)d.N, (long long)d.K, d.batch, splits, streamk ? " streamk" : "");
   hipLaunchKernelGGL((gemm_p32_kernel<TA, TB>), dim3((unsigned)ka.nblk, (unsigned)d.batch), dim3(512), 0, s, ka);

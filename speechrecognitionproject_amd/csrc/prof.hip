@@ -19,7 +19,7 @@ namespace {
 struct Rec {
   std::string name, detail;
   hipEvent_t a, b;
-  double work;
+  double work, bytes;
 };
 
 std::atomic<bool> g_on{false};
@@ -62,7 +62,7 @@ ProfScope::~ProfScope() {
   hipEvent_t b = take_event();
   if (!b) return;
   (void)hipEventRecord(b, s_);
-  g_recs.push_back(Rec{name_, detail_, static_cast<hipEvent_t>(a_), b, work_});
+  g_recs.push_back(Rec{name_, detail_, static_cast<hipEvent_t>(a_), b, work_, bytes_});
 }
 
 void ProfScope::detail(const char* fmt, ...) {
@@ -115,7 +115,7 @@ int srk_prof_kernels(char* buf, int64_t cap, int64_t* needed) {
   SRK_API_BEGIN
   SRK_REQUIRE(needed && (buf || cap == 0), SRK_ERR_INVALID, "prof_kernels: null pointer");
   std::lock_guard<std::mutex> lk(srk::g_mu);
-  struct Agg { int64_t n = 0; double ms = 0.0, work = 0.0; };
+  struct Agg { int64_t n = 0; double ms = 0.0, work = 0.0, bytes = 0.0; };
   std::map<std::pair<std::string, std::string>, Agg> agg;
   for (auto& r : srk::g_recs) {
     SRK_CHECK_HIP(hipEventSynchronize(r.b));
@@ -125,12 +125,13 @@ int srk_prof_kernels(char* buf, int64_t cap, int64_t* needed) {
     g.n += 1;
     g.ms += ms;
     g.work += r.work;
+    g.bytes += r.bytes;
   }
   std::string out;
-  char line[320];
+  char line[360];
   for (auto& kv : agg) {
-    snprintf(line, sizeof(line), "%s\t%s\t%lld\t%.6f\t%.6e\n", kv.first.first.c_str(), kv.first.second.c_str(),
-             (long long)kv.second.n, kv.second.ms, kv.second.work);
+    snprintf(line, sizeof(line), "%s\t%s\t%lld\t%.6f\t%.6e\t%.6e\n", kv.first.first.c_str(),
+             kv.first.second.c_str(), (long long)kv.second.n, kv.second.ms, kv.second.work, kv.second.bytes);
     out += line;
   }
   *needed = (int64_t)out.size() + 1;

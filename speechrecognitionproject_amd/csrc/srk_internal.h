@@ -158,12 +158,16 @@ class ProfScope {
   // The launch's kernel and shape ("gemm_f32_kernel<NT,256x128> 13056x3072x1024"), printf-style;
   // srk_prof_kernels groups records by (name, detail).  No-op (no formatting) when profiling is off.
   void detail(const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+  // The launch's ALGORITHMIC HBM bytes (matrix kernels, whose `work` is flops): each operand tensor read
+  // once + the output written once — what PMC traffic is priced against.
+  void bytes(double b) { bytes_ = b; }
 
  private:
   const char* name_;
   hipStream_t s_;
   void* a_;
   double work_;
+  double bytes_ = 0.0;
   char detail_[96];
 };
 

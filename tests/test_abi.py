@@ -25,6 +25,14 @@ def test_version_and_error_channel():
     assert rc == -1
 
 
+def test_source_stamp_matches_tree():
+    """The shipped libsrk.so was built from these sources: its srk_source_stamp() (build.py's sha256 over
+    csrc/* and include/*.h) equals the stamp of the tree.  PMC records carry the same stamp, and bench.py
+    attaches their counters only to a library with it (profiles/pmc_*.json)."""
+    from speechrecognitionproject_amd import build
+    assert _lib.source_stamp() == build.source_stamp()
+
+
 def test_training_cli_flags():
     """training.py's reference CLI (-key / -lr, training.py:29-32) plus the 16-bit / checkpoint flags
     (SURVEY.md §5 "Config / flags": --precision {fp32,bf16,fp16}); parsed on the CPU."""

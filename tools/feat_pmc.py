@@ -20,6 +20,17 @@ import json
 import os
 import sqlite3
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def lib_stamp():
+    """srk_source_stamp() of the in-tree libsrk.so (the build the counters were collected on); bench.py
+    attaches counter data only to a run of the library with the same stamp."""
+    import ctypes
+    L = ctypes.CDLL(os.path.join(REPO, "speechrecognitionproject_amd", "libsrk.so"))
+    L.srk_source_stamp.restype = ctypes.c_char_p
+    return L.srk_source_stamp().decode()
+
 KERNELS = {"mfcc": ("mfcc3_kernel", "mfcc4_kernel", "mfcc2_kernel"), "fbank": ("fbank_kernel",),
            "spec": ("spec_kernel",)}
 PCM_BYTES_PER_CLIP = 64000
@@ -49,7 +60,8 @@ def main():
     ap.add_argument("--clips", type=int, required=True)
     ap.add_argument("--source", default="")
     a = ap.parse_args()
-    res = {"source": a.source, "command": "python3 tools/mfcc_only.py <feature> %d" % a.clips,
+    res = {"source": a.source, "source_stamp": lib_stamp(),
+           "command": "python3 tools/mfcc_only.py <feature> %d" % a.clips,
            "clips_per_launch": a.clips, "kernels": {}}
     for feature in KERNELS:
         m, ns, nd = per_dispatch(a.dir, feature)

@@ -18,6 +18,17 @@ import os
 import re
 import sqlite3
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def lib_stamp():
+    """srk_source_stamp() of the in-tree libsrk.so (the build the counters were collected on); bench.py
+    attaches counter data only to a run of the library with the same stamp."""
+    import ctypes
+    L = ctypes.CDLL(os.path.join(REPO, "speechrecognitionproject_amd", "libsrk.so"))
+    L.srk_source_stamp.restype = ctypes.c_char_p
+    return L.srk_source_stamp().decode()
+
 GROUPS = {  # srk_prof name -> substrings of the rocprof kernel symbols it covers (GEMMs: _gemm_group)
     "gemm_f32": (), "gemm_bf16": (), "gemm_f16": (), "splitk_reduce": (),
     "gru_fwd_seq": ("gru_fwd_persistent_kernel", "gru_fwd_persistent_dc_kernel"),
@@ -93,7 +104,8 @@ def main():
     a = ap.parse_args()
     f, w = collect(a.fetch, "FETCH_SIZE"), collect(a.write, "WRITE_SIZE")
     # bench.py reports this traffic only for a command with the same model / batch / world / options
-    res = {"source": a.source, "correction": "FETCH_SIZE KiB x 2 x 1024 + WRITE_SIZE KiB x 1024 (gfx950)",
+    res = {"source": a.source, "source_stamp": lib_stamp(),
+           "correction": "FETCH_SIZE KiB x 2 x 1024 + WRITE_SIZE KiB x 1024 (gfx950)",
            "command": {"model": a.model, "batch": a.batch, "world": a.world, "precisions": a.precisions.split(","),
                        "sync_bn": bool(a.sync_bn)},
            "bytes_per_launch": {}}
@@ -106,7 +118,8 @@ def main():
         with open(a.o) as fh:
             old = json.load(fh)
         oc, nc = old.get("command", {}), res["command"]
-        if all(oc.get(k) == nc[k] for k in ("model", "batch", "world", "sync_bn")):
+        if (all(oc.get(k) == nc[k] for k in ("model", "batch", "world", "sync_bn"))
+                and old.get("source_stamp") == res["source_stamp"]):
             nc["precisions"] = sorted(set(oc.get("precisions", [])) | set(nc["precisions"]))
             res["source"] = "%s + %s" % (old.get("source", ""), a.source)
             res["bytes_per_launch"] = dict(old.get("bytes_per_launch", {}), **res["bytes_per_launch"])

@@ -127,6 +127,14 @@ int srk_noise_mix(const int16_t* pcm, const int16_t* bank, int64_t n_files, int6
                   const int64_t* file_idx, const int64_t* offset, const double* gain,
                   int64_t n_clips, float* out, void* stream);
 
+/* K4 fused into K3's load stage (model_spec_bgru on noise-augmented clips, dataset.py:183-193 then
+ * models/model_spec_bgru.py:11-17): out = srk_spec_fwd of srk_noise_mix(pcm, bank, ...) — the same
+ * values bit for bit — without the mixed fp32 PCM going through HBM (int16 clip + int16 noise window
+ * in, the spectrogram out).  Arguments as srk_noise_mix (bank 4-byte aligned) and srk_spec_fwd. */
+int srk_spec_noise_fwd(const int16_t* pcm, const int16_t* bank, int64_t n_files, int64_t bank_len,
+                       const int64_t* file_idx, const int64_t* offset, const double* gain, int64_t n_clips,
+                       float* out, int transposed, void* stream);
+
 /* K10: batched training-mode augmentation, dataset.py:103-118 and its helpers :148-223, with the
  * random draws made explicit (one op per clip; the Python `Dataset.__getitem__` draws them per
  * item, srk_augment applies a whole batch in one launch).  op[b]:

@@ -45,6 +45,7 @@ _SIGS = {
     "srk_mfcc_fwd_i16": [_P, _I64, _P, _I, _P],
     "srk_spec_fwd_i16": [_P, _I64, _P, _I, _P],
     "srk_noise_mix": [_P, _P, _I64, _I64, _P, _P, _P, _I64, _P, _P],
+    "srk_spec_noise_fwd": [_P, _P, _I64, _I64, _P, _P, _P, _I64, _P, _I, _P],
     "srk_augment": [_P, _I64, _P, _I64, _P, _P, _P, _P, ctypes.c_uint64, _P, _P],
     "srk_pitch_workspace_bytes": [_I64],
     "srk_pitch_shift": [_P, _I64, _P, _P, _I64, _P, _P, _I64, _P],

@@ -228,6 +228,26 @@ __global__ __launch_bounds__(256, 4) void fbank_kernel(const T* __restrict__ pcm
   }
 }
 
+// ------------------------------------------------------------------------- K4 noise mix (shared)
+// numpy: sample + (gain * noise) in float64 (two roundings, never fused), then np.int16()
+// truncates toward zero.
+__device__ __forceinline__ float mix_one(short s, double g, short n) {
+#pragma clang fp contract(off)
+  const double v = (double)s + g * (double)n;
+  return (float)(int16_t)(int)v;
+}
+
+// K4 fused into K3's sample loads (srk_spec_noise_fwd, model_spec_bgru + dataset.py:183-193): the kernel
+// reads the int16 clip and its noise window and mixes each sample as it loads it, so the mixed fp32 PCM
+// never goes through HBM (128,000 B/clip for the separate K4 + 64,000 re-read by K3 -> 64,000 in).
+struct NoiseArgs {
+  const int16_t* bank;       // [n_files][bank_len]
+  int64_t n_files, bank_len;
+  const int64_t* file_idx;   // [n_clips]
+  const int64_t* offs;       // [n_clips]
+  const double* gains;       // [n_clips]
+};
+
 // ------------------------------------------------------------------------- K3 spectrogram
 // models/model_spec_bgru.py:11-17: scipy.signal.spectrogram(fs=16000, nperseg=640, noverlap=320)
 // = 49 frames of 640 samples (no padding), periodic Tukey(0.25), PSD density scaling, one-sided
@@ -242,9 +262,10 @@ struct SpecTables {
   float scale;              // 1 / (fs * sum(w^2))
 };
 
-template <typename T>
+template <typename T, bool MIX = false>
 __global__ __launch_bounds__(256, 4) void spec_kernel(const T* __restrict__ pcm, float* __restrict__ out,
-                                                      int64_t n_clips, int transposed, SpecTables t) {
+                                                      int64_t n_clips, int transposed, SpecTables t,
+                                                      NoiseArgs nm = NoiseArgs{}) {
   __shared__ v2f sbuf[4][3 * 340];
   __shared__ __attribute__((aligned(16))) double s_win[640];
   __shared__ v2f s_tw[20 * 16];      // W320^(j k1) at [k1][j]
@@ -270,8 +291,32 @@ __global__ __launch_bounds__(256, 4) void spec_kernel(const T* __restrict__ pcm,
     // every lane loads (a dead lane's x is frame 0 of the clip) and the products are masked after:
     // with the loads under the `live` condition the compiler serialises 40 load / LDS waits
     v2f xv[20];
+    if constexpr (MIX) {
+      // the clip's noise window (file, offset clamped into the bank as in noise_mix_kernel) mixed in at load
+      const int64_t fi = min(max(nm.file_idx[clip], (int64_t)0), nm.n_files - 1);
+      const int64_t off = min(max(nm.offs[clip], (int64_t)0), nm.bank_len - kPcmLen);
+      const double g = nm.gains[clip];
+      const int64_t base = fi * nm.bank_len + off;
+      const int16_t* __restrict__ nz = nm.bank + base + 320 * (live ? gf : 0);
+      if ((base & 1) == 0) {   // wave-uniform: sample pairs of the noise window are 4-B aligned
 #pragma unroll
-    for (int i = 0; i < 20; ++i) xv[i] = ld2(x + 2 * (j + 16 * i));
+        for (int i = 0; i < 20; ++i) {
+          const short2 sv = *reinterpret_cast<const short2*>(x + 2 * (j + 16 * i));
+          const short2 nv = *reinterpret_cast<const short2*>(nz + 2 * (j + 16 * i));
+          xv[i] = v2f{mix_one(sv.x, g, nv.x), mix_one(sv.y, g, nv.y)};
+        }
+      } else {                 // odd window start: 2-B noise loads (every access naturally aligned)
+#pragma unroll
+        for (int i = 0; i < 20; ++i) {
+          const short2 sv = *reinterpret_cast<const short2*>(x + 2 * (j + 16 * i));
+          const short n0 = nz[2 * (j + 16 * i)], n1 = nz[2 * (j + 16 * i) + 1];
+          xv[i] = v2f{mix_one(sv.x, g, n0), mix_one(sv.y, g, n1)};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 20; ++i) xv[i] = ld2(x + 2 * (j + 16 * i));
+    }
     v2f tw[19];   // pass-A twiddles, read ahead of the transpose stores
 #pragma unroll
     for (int k1 = 1; k1 < 20; ++k1) tw[k1 - 1] = s_tw[k1 * 16 + j];
@@ -729,14 +774,6 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const T* __rest
 }
 
 // ------------------------------------------------------------------------- K4 noise mix
-// numpy: sample + (gain * noise) in float64 (two roundings, never fused), then np.int16()
-// truncates toward zero.
-__device__ __forceinline__ float mix_one(short s, double g, short n) {
-#pragma clang fp contract(off)
-  const double v = (double)s + g * (double)n;
-  return (float)(int16_t)(int)v;
-}
-
 __global__ void noise_mix_kernel(const int16_t* __restrict__ pcm, const int16_t* __restrict__ bank,
                                  int64_t n_files, int64_t bank_len, const int64_t* __restrict__ file_idx,
                                  const int64_t* __restrict__ offs, const double* __restrict__ gains,
@@ -800,7 +837,7 @@ int fbank_fwd(const T* pcm, int64_t n_clips, float* out, void* stream) {
 }
 
 template <typename T>
-int spec_fwd(const T* pcm, int64_t n_clips, float* out, int transposed, void* stream) {
+int spec_fwd(const T* pcm, int64_t n_clips, float* out, int transposed, void* stream, const NoiseArgs* nm = nullptr) {
   SRK_REQUIRE(n_clips >= 0 && n_clips <= INT32_MAX, SRK_ERR_INVALID, "srk_spec_fwd: bad n_clips");
   if (n_clips == 0) return SRK_OK;
   SRK_REQUIRE(pcm && out, SRK_ERR_INVALID, "srk_spec_fwd: null pointer");
@@ -811,9 +848,17 @@ int spec_fwd(const T* pcm, int64_t n_clips, float* out, int transposed, void* st
   SpecTables st{t->tukey640, t->tw320, t->post640, (float)t->spec_scale};
   const int64_t items = n_clips * kSpChunks;
   const int64_t blocks = std::min<int64_t>((items + 3) / 4, 2048);
-  ProfScope prof("spec", as_stream(stream), (16000.0 * sizeof(T) + 62916.0) * (double)n_clips);
-  hipLaunchKernelGGL(spec_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), pcm, out, n_clips,
-                     transposed ? 1 : 0, st);
+  hipStream_t s = as_stream(stream);
+  if (nm) {   // K4 + K3: int16 clip + int16 noise window in, the spectrogram out (126,916 B/clip)
+    ProfScope prof("spec", s, (32000.0 + 32000.0 + 62916.0) * (double)n_clips);
+    prof.detail("spec_kernel<int16,noise_mix>");
+    hipLaunchKernelGGL((spec_kernel<int16_t, true>), dim3((unsigned)blocks), dim3(256), 0, s,
+                       reinterpret_cast<const int16_t*>(pcm), out, n_clips, transposed ? 1 : 0, st, *nm);
+  } else {
+    ProfScope prof("spec", s, (16000.0 * sizeof(T) + 62916.0) * (double)n_clips);
+    hipLaunchKernelGGL(spec_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, s, pcm, out, n_clips,
+                       transposed ? 1 : 0, st, NoiseArgs{});
+  }
   SRK_CHECK_HIP(hipGetLastError());
   return SRK_OK;
 }
@@ -872,6 +917,21 @@ int srk_spec_fwd(const float* pcm, int64_t n_clips, float* out, int transposed, 
 int srk_spec_fwd_i16(const int16_t* pcm, int64_t n_clips, float* out, int transposed, void* stream) {
   SRK_API_BEGIN
   return srk::spec_fwd(pcm, n_clips, out, transposed, stream);
+  SRK_API_END
+}
+
+int srk_spec_noise_fwd(const int16_t* pcm, const int16_t* bank, int64_t n_files, int64_t bank_len,
+                       const int64_t* file_idx, const int64_t* offset, const double* gain, int64_t n_clips, float* out,
+                       int transposed, void* stream) {
+  SRK_API_BEGIN
+  SRK_REQUIRE(n_clips >= 0, SRK_ERR_INVALID, "srk_spec_noise_fwd: bad n_clips");
+  if (n_clips == 0) return SRK_OK;
+  SRK_REQUIRE(bank && file_idx && offset && gain, SRK_ERR_INVALID, "srk_spec_noise_fwd: null pointer");
+  SRK_REQUIRE(n_files > 0 && bank_len >= 16000, SRK_ERR_INVALID,
+              "srk_spec_noise_fwd: bank must hold >= 1 file of >= 16000 samples");
+  SRK_REQUIRE((uintptr_t)bank % 4 == 0, SRK_ERR_INVALID, "srk_spec_noise_fwd: bank must be 4-byte aligned");
+  const srk::NoiseArgs nm{bank, n_files, bank_len, file_idx, offset, gain};
+  return srk::spec_fwd(pcm, n_clips, out, transposed, stream, &nm);
   SRK_API_END
 }
 

@@ -242,13 +242,18 @@ class DeviceNoiseMix:
         self.upper_bound = upper_bound
         self.rng = np.random.default_rng(seed)
 
-    def __call__(self, pcm_i16):
-        from .features import noise_mix
+    def draw(self, pcm_i16):
+        """The batch with its draws, not yet mixed (features.NoisyClips): a spectrogram plugin mixes it
+        inside K3's sample loads, any other consumer through K4."""
+        from .features import NoisyClips
         n = pcm_i16.shape[0]
         files = self.rng.integers(0, self.bank.shape[0], n)
         offs = self.rng.integers(0, self.bank.shape[1] - SEQ_LENGTH + 1, n)
         gains = self.rng.uniform(0, self.upper_bound, n)
-        return noise_mix(pcm_i16, self.bank, files, offs, gains)
+        return NoisyClips(pcm_i16, self.bank, files, offs, gains)
+
+    def __call__(self, pcm_i16):
+        return self.draw(pcm_i16).mixed()
 
 
 class DeviceAugment:

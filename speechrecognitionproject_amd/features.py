@@ -28,9 +28,52 @@ def ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+class NoisyClips:
+    """A batch of int16 clips with their K4 noise draws (dataset.py:183-193 ``add_noise_uniform``:
+    out = int16(pcm + gain * bank[file, offset : offset + 16000])), not yet mixed.  The spectrogram
+    plugins take it as their input and ``spec`` mixes inside K3's sample loads (srk_spec_noise_fwd:
+    the mixed fp32 PCM never goes through HBM); every other consumer gets the mixed PCM from K4
+    (``mixed()``).  Build one with ``DeviceNoiseMix.draw`` or directly from device tensors."""
+
+    def __init__(self, pcm_i16, bank_i16, file_idx, offsets, gains):
+        require_gpu()
+        dev = torch.device("cuda")
+        self.pcm = torch.as_tensor(pcm_i16).to(dev, torch.int16).contiguous()
+        bank = torch.as_tensor(bank_i16).to(dev, torch.int16).contiguous()
+        self.bank = bank.unsqueeze(0) if bank.dim() == 1 else bank
+        self.file_idx = torch.as_tensor(file_idx).to(dev, torch.int64).contiguous()
+        self.offsets = torch.as_tensor(offsets).to(dev, torch.int64).contiguous()
+        self.gains = torch.as_tensor(gains).to(dev, torch.float64).contiguous()
+        n = self.pcm.shape[0]
+        if (self.pcm.shape != (n, SEQ_LENGTH) or self.file_idx.numel() != n or self.offsets.numel() != n
+                or self.gains.numel() != n):
+            raise SrkError("NoisyClips: inconsistent shapes")
+        _check_draws(self.bank, self.file_idx, self.offsets)
+
+    @property
+    def shape(self):
+        return self.pcm.shape
+
+    def mixed(self, out=None):
+        """K4: the mixed float32 PCM [B, 16000]."""
+        return noise_mix(self.pcm, self.bank, self.file_idx, self.offsets, self.gains, out=out)
+
+
+def _check_draws(bank, fi, of):
+    # host-side bounds check of the draws (skipped inside a HIP-graph capture, where reading them back
+    # is not possible; the kernels clamp them into the bank either way)
+    if fi.numel() and not torch.cuda.is_current_stream_capturing() and (
+            int(of.min()) < 0 or int(of.max()) > bank.shape[1] - SEQ_LENGTH or int(fi.min()) < 0
+            or int(fi.max()) >= bank.shape[0]):
+        raise SrkError("noise mix: file index / offset out of range")
+
+
 def as_device_pcm(pcm, keep_int16=False):
-    """[B, 16000] PCM on the GPU, contiguous: float32, or int16 kept as is with ``keep_int16``."""
+    """[B, 16000] PCM on the GPU, contiguous: float32, or int16 kept as is with ``keep_int16``
+    (a ``NoisyClips`` batch is mixed first, K4)."""
     require_gpu()
+    if isinstance(pcm, NoisyClips):
+        return pcm.mixed()
     if not torch.is_tensor(pcm):
         pcm = torch.as_tensor(pcm)
     if pcm.dim() == 1:
@@ -66,7 +109,15 @@ def mfcc(pcm, time_major=False, out=None):
 
 
 def spec(pcm, transposed=False, out=None):
-    """K3 log spectrogram: [B, 321, 49], or [B, 49, 321] if ``transposed`` (model_spec_*.py)."""
+    """K3 log spectrogram: [B, 321, 49], or [B, 49, 321] if ``transposed`` (model_spec_*.py).  A
+    ``NoisyClips`` batch is mixed inside K3's sample loads (srk_spec_noise_fwd, K4 fused)."""
+    if isinstance(pcm, NoisyClips):
+        n = pcm.pcm.shape[0]
+        shape = (n, 49, 321) if transposed else (n, 321, 49)
+        out = torch.empty(shape, device=pcm.pcm.device, dtype=torch.float32) if out is None else out
+        call("srk_spec_noise_fwd", ptr(pcm.pcm), ptr(pcm.bank), pcm.bank.shape[0], pcm.bank.shape[1],
+             ptr(pcm.file_idx), ptr(pcm.offsets), ptr(pcm.gains), n, ptr(out), 1 if transposed else 0, stream_ptr())
+        return out
     x = as_device_pcm(pcm, keep_int16=True)
     shape = (x.shape[0], 49, 321) if transposed else (x.shape[0], 321, 49)
     out = torch.empty(shape, device=x.device, dtype=torch.float32) if out is None else out
@@ -88,11 +139,7 @@ def noise_mix(pcm_i16, bank_i16, file_idx, offsets, gains, out=None):
     n = x.shape[0]
     if x.shape != (n, SEQ_LENGTH) or fi.numel() != n or of.numel() != n or g.numel() != n:
         raise SrkError("noise_mix: inconsistent shapes")
-    # host-side bounds check of the draws (skipped inside a HIP-graph capture, where reading them back
-    # is not possible; the kernel clamps them into the bank either way)
-    if n and not torch.cuda.is_current_stream_capturing() and (int(of.min()) < 0 or int(of.max()) > bank.shape[1] - SEQ_LENGTH or int(fi.min()) < 0
-              or int(fi.max()) >= bank.shape[0]):
-        raise SrkError("noise_mix: file index / offset out of range")
+    _check_draws(bank, fi, of)
     out = torch.empty((n, SEQ_LENGTH), device=dev, dtype=torch.float32) if out is None else out
     call("srk_noise_mix", ptr(x), ptr(bank), bank.shape[0], bank.shape[1], ptr(fi), ptr(of), ptr(g), n, ptr(out),
          stream_ptr())

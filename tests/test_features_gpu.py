@@ -79,6 +79,38 @@ def test_noise_mix_bit_exact_vs_oracle_large(gpu):
     assert np.array_equal(out, ref.astype(np.float32))
 
 
+@pytest.mark.parametrize("transposed", [True, False])
+@pytest.mark.parametrize("bank_len", [960000, 16001])
+def test_spec_noise_fused_equals_mix_then_spec(gpu, transposed, bank_len):
+    """K4 fused into K3's loads (srk_spec_noise_fwd): bit for bit the spectrogram of K4's mixed PCM —
+    even and odd window starts (an odd bank_len makes file starts alternate parity), offsets 0 and
+    bank_len - 16000 (the window's last sample is the bank's last), every file."""
+    n = 96
+    x, _ = synthetic_clips(n, seed=5, clip=30000)
+    x16 = torch.from_numpy(x.astype(np.int16)).cuda()
+    rng = np.random.default_rng(bank_len)
+    bank = np.clip(np.rint(rng.normal(0, 2000, (3, bank_len))), -6000, 6000).astype(np.int16)
+    f = rng.integers(0, 3, n)
+    o = rng.integers(0, bank_len - 16000 + 1, n)
+    o[:4] = [0, 1, bank_len - 16000, bank_len - 16001]
+    f[:4] = [0, 2, 2, 1]
+    gns = rng.uniform(0, 0.1, n)
+    clips = K.NoisyClips(x16, bank, f, o, gns)
+    fused = K.spec(clips, transposed=transposed)
+    ref = K.spec(clips.mixed(), transposed=transposed)
+    assert torch.equal(fused, ref)
+    assert torch.isfinite(fused).all()
+
+
+def test_spec_noise_fused_vs_reference_golden_mix(gpu):
+    """The fused K4 + K3 on the reference-generated noise-mix fixture: equal to K3 of the fixture's
+    mixed samples (which K4 reproduces bit for bit, test_noise_mix_bit_exact_vs_reference_golden)."""
+    g = golden("noise_mix_golden.npz")
+    clips = K.NoisyClips(g["pcm"].astype(np.int16), g["bank"], g["file_idx"], g["start"], g["gain"])
+    ref = K.spec(torch.from_numpy(g["out"].astype(np.float32)))
+    assert torch.equal(K.spec(clips), ref)
+
+
 @pytest.mark.parametrize("fn", ["fbank", "mfcc", "spec"])
 def test_batch_independence_and_determinism(gpu, fn):
     # size-independent properties at a large batch: each clip's features do not depend on the

@@ -1,7 +1,7 @@
 """The 16-bit train steps bench.py times, at BASELINE.json's own shapes, against the fp32 CPU oracle
 (SURVEY.md §8(a) A5 / A9, §8(d) configs[1] and configs[4]; VERDICT r03 "next" #1):
 
-* cfg5 — int16 PCM + resident noise bank -> K4 noise mix (dataset.py:183-193) -> spectrogram
+* cfg5 — int16 PCM + resident noise bank -> K4 noise mix (dataset.py:183-193) fused into the spectrogram
   [49 x 321] -> model_spec_bgru (model_spec_bgru.py:19-35), B = 512, fp16 matrix-core operands, the
   static loss scale of bench.py (1024) through optim.LossScaler, CE, backward, Adam;
 * cfg2 — MFCC [51 x 39] -> model_mfcc_bgru (model_mfcc_bgru.py:21-37), B = 256, bf16 operands.
@@ -94,12 +94,12 @@ def test_lowprec_train_step_at_config_shape(gpu, oracle_case, precision):
         scaler = LossScaler(LOSS_SCALE, dynamic=False) if precision == "fp16" else None
         scale = LOSS_SCALE if scaler is not None else 1.0
         opt.zero_grad()
-        if name == "spec_bgru":     # cfg5: the K4 mix inside the step, as bench.py runs it
+        if name == "spec_bgru":     # cfg5: the K4 mix inside the step (fused into K3's loads), as bench.py runs it
             files, offs, gains = inp["draws"]
-            x = K.noise_mix(torch.from_numpy(inp["pcm16"]).cuda(), torch.from_numpy(inp["bank"]).cuda(),
-                            torch.from_numpy(files).cuda(), torch.from_numpy(offs).cuda(),
-                            torch.from_numpy(gains).cuda())
-            assert np.array_equal(x.cpu().numpy(), inp["mixed"])
+            x = K.NoisyClips(torch.from_numpy(inp["pcm16"]).cuda(), torch.from_numpy(inp["bank"]).cuda(),
+                             torch.from_numpy(files).cuda(), torch.from_numpy(offs).cuda(),
+                             torch.from_numpy(gains).cuda())
+            assert np.array_equal(x.mixed().cpu().numpy(), inp["mixed"])
         else:
             x = torch.from_numpy(inp["mixed"]).cuda()
         out = net(x)

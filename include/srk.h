@@ -36,7 +36,7 @@ enum srk_status {
 
 /* ---------------------------------------------------------------- library / device */
 int srk_version(void);                 /* ABI version, bumped on any signature change */
-/* First 16 hex digits of the sha256 over the library's sources (csrc/*.hip, *.h, *.cpp and this
+/* First 16 hex digits of the sha256 over the library's sources (the csrc .hip / .h / .cpp files and this
  * header, in name order) as built: profiling records (profiles/pmc_*.json) carry the stamp of the
  * library they measured, and bench.py attaches them only to a run of the same build.              */
 const char* srk_source_stamp(void);
@@ -449,6 +449,18 @@ int srk_dropout_fwd_state(const float* x, int64_t n, float p, uint64_t* state, f
                           void* stream);
 /* y = keep ? x * scale : 0 (dropout with an explicit keep-mask; also its backward).          */
 int srk_dropout_apply(const float* x, const uint8_t* keep, int64_t n, float scale, float* y, void* stream);
+
+/* ---------------------------------------------------------------- diagnostics (tests only)
+ * Directed checks of two instruction patterns (csrc/diag.hip; tests/test_diag_gpu.py):
+ * srk_diag_acc_store: the row-staged data gradient's epilogue (raw buffer stores of 32x32 MFMA
+ *   accumulators, its descriptor, offsets and drop value) into dx [rows][40][64] fp32 (rows % 8 == 0):
+ *   tile g's first 32 pixels get 1 + 64 p + c + 2048 g; variant 0 = the product form, 1 = the round-5
+ *   source form (a bit cast of a vector-component lvalue, miscompiled to component 0).
+ * srk_diag_tr16_read: ds_read_b64_tr_b16 B fragments of a [32 k][cols] 16-bit matrix m staged as the
+ *   64-column (cols = 64) or the 128-column TR image: out[(fragment * 64 + lane) * 4 + d], fragments
+ *   (r0 = 0, 32, ...) x (kk = 0, 16). */
+int srk_diag_acc_store(float* dx, int64_t rows, int variant, void* stream);
+int srk_diag_tr16_read(const uint16_t* m, int64_t cols, uint32_t* out, void* stream);
 
 #ifdef __cplusplus
 }

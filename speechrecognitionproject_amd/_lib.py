@@ -31,6 +31,8 @@ _SIGS = {
                       ctypes.POINTER(ctypes.c_double)],
     "srk_prof_kernels": [ctypes.c_char_p, _I64, ctypes.POINTER(ctypes.c_int64)],
     "srk_source_stamp": [],
+    "srk_diag_acc_store": [_P, _I64, _I, _P],
+    "srk_diag_tr16_read": [_P, _I64, _P, _P],
     "srk_set_option": [ctypes.c_char_p, _I64],
     "srk_spin_timeouts": [],
     "srk_scratch_generation": [],

@@ -2216,6 +2216,13 @@ int srk_conv2d_nhwc_fwd16(const float* x, int64_t N, int64_t H, int64_t W, int64
   c.KH = (int)KH; c.KW = (int)KW; c.ph = (int)ph; c.pw = (int)pw; c.sh = (int)sh; c.sw = (int)sw;
   c.x = x; c.wmat = ws; c.out = y; c.bias = bias;
   c.M = N * Ho * Wo; c.Nn = Co; c.K = KH * KW * Ci;
+  if (srk::g_opt_conv_fwd_fp32 && srk::matmul_prec() != srk::kPrecF32) {
+    // the faithful 16-bit mode: this forward on fp32 operands; a producer's 16-bit copy of x stays the
+    // backward's (its weight gradient runs 16-bit)
+    if (x16_ready && x16_written) *x16_written = 1;
+    srk::PrecScope fp32(srk::kPrecF32);
+    return srk::run_conv_gemm<srk::kFwd>(c, s, "conv_fwd");
+  }
   const int prec = srk::matmul_prec();
   if (srk::s16_ok(prec, Ci, Co, {x, ws, x16})) {
     const float* src[2] = {x, ws};
@@ -2397,6 +2404,12 @@ int srk_conv2d_nhwc_fwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
   SRK_API_BEGIN
   const bool x16_ready = x16 && x16_written && *x16_written == 2;   // the producer's copy (srk_conv1_pool_fwd16)
   if (x16_written) *x16_written = 0;
+  // the faithful 16-bit mode ("conv_fwd_fp32"): this forward on fp32 operands, a producer's copy kept for the
+  // backward
+  const bool fwd32 = srk::g_opt_conv_fwd_fp32 && srk::matmul_prec() != srk::kPrecF32;
+  if (fwd32 && x16_ready) *x16_written = 1;
+  srk::PrecScope fp32(fwd32 ? srk::kPrecF32 : -1);
+  if (fwd32) x16 = nullptr;
   int64_t Ho, Wo;
   if (int rc = srk::check(N, H, W, Ci, Co, KH, KW, ph, pw, 1, 1, &Ho, &Wo)) return rc;
   SRK_REQUIRE(x && w && y && argmax && ws, SRK_ERR_INVALID, "conv fwd_pool: null pointer");

@@ -37,7 +37,9 @@ int g_opt_mfcc_variant = 3;
 int g_opt_gemm_streamk = 1;
 int g_opt_gemm32_kernel = 0;
 static std::atomic<int> g_opt_matmul_prec{kPrecF32};
-int matmul_prec() { return g_opt_matmul_prec.load(std::memory_order_relaxed); }
+thread_local int t_prec_override = -1;
+int matmul_prec() { return t_prec_override >= 0 ? t_prec_override : g_opt_matmul_prec.load(std::memory_order_relaxed); }
+int g_opt_conv_fwd_fp32 = 0;
 unsigned long long* g_opt_gru_trace = nullptr;
 unsigned g_opt_gru_spin_limit = 0;
 int g_opt_gru_xcd_local = 1;
@@ -358,6 +360,10 @@ int srk_set_option(const char* name, int64_t value) {
   }
   if (n == "gru_persistent") {
     srk::g_opt_gru_persistent = value != 0;
+    return SRK_OK;
+  }
+  if (n == "conv_fwd_fp32") {   // 16-bit modes: conv forward passes on fp32 operands (1), or 16-bit (0)
+    srk::g_opt_conv_fwd_fp32 = value != 0;
     return SRK_OK;
   }
   if (n == "matmul_precision") {   // 0 fp32, 1 bf16, 2 fp16 matrix-core operands (fp32 accumulate)

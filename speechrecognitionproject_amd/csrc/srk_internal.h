@@ -79,6 +79,21 @@ int get_tables(const DeviceTables** out);
 // nearest-even when staged into LDS) with fp32 accumulation and fp32 inputs / outputs.
 enum MatmulPrec { kPrecF32 = 0, kPrecBF16 = 1, kPrecF16 = 2 };
 int matmul_prec();
+// Scoped override of matmul_prec() on this host thread (p < 0: no override): the conv forward passes under
+// "conv_fwd_fp32" run their whole dispatch at fp32.
+extern thread_local int t_prec_override;
+struct PrecScope {
+  int saved;
+  explicit PrecScope(int p) : saved(t_prec_override) {
+    if (p >= 0) t_prec_override = p;
+  }
+  ~PrecScope() { t_prec_override = saved; }
+};
+// 16-bit modes: every convolution FORWARD pass on fp32 operands, the data / weight gradients on 16-bit ones
+// ("conv_fwd_fp32", default 0).  resnet_bgru's training-mode BatchNorm chain amplifies the forward's operand
+// rounding into 4-39 % norm-wise gradient errors, while 16-bit gradients alone stay <= 0.9 %
+// (tools/bf16_policy_resnet.py): the faithful 16-bit training mode of the BatchNorm models.
+extern int g_opt_conv_fwd_fp32;
 
 // Kernel of the 16-bit-operand GEMM (srk_set_option "gemm16_kernel", A/B measurements and tests):
 // 0 = by shape, 1 = register-staged gemm_h16_kernel, 2 = LDS-DMA ping-pong gemm_g16_kernel.

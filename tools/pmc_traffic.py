@@ -99,6 +99,7 @@ def main():
     ap.add_argument("--precisions", default="fp32", help="comma list: the precisions the command timed")
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--sync-bn", action="store_true")
+    ap.add_argument("--conv-fwd-fp32", action="store_true")
     ap.add_argument("--merge", action="store_true",
                     help="add to an existing -o file of the same model / batch / world / options (another precision)")
     a = ap.parse_args()
@@ -107,7 +108,7 @@ def main():
     res = {"source": a.source, "source_stamp": lib_stamp(),
            "correction": "FETCH_SIZE KiB x 2 x 1024 + WRITE_SIZE KiB x 1024 (gfx950)",
            "command": {"model": a.model, "batch": a.batch, "world": a.world, "precisions": a.precisions.split(","),
-                       "sync_bn": bool(a.sync_bn)},
+                       "sync_bn": bool(a.sync_bn), "conv_fwd_fp32": bool(a.conv_fwd_fp32)},
            "bytes_per_launch": {}}
     for g in sorted(set(f) & set(w)):
         fb = 2.0 * 1024.0 * f[g][1] / f[g][0]
@@ -118,7 +119,7 @@ def main():
         with open(a.o) as fh:
             old = json.load(fh)
         oc, nc = old.get("command", {}), res["command"]
-        if (all(oc.get(k) == nc[k] for k in ("model", "batch", "world", "sync_bn"))
+        if (all(oc.get(k) == nc[k] for k in ("model", "batch", "world", "sync_bn", "conv_fwd_fp32"))
                 and old.get("source_stamp") == res["source_stamp"]):
             nc["precisions"] = sorted(set(oc.get("precisions", [])) | set(nc["precisions"]))
             res["source"] = "%s + %s" % (old.get("source", ""), a.source)

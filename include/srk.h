@@ -329,7 +329,8 @@ int srk_conv1_pool_fwd(const float* x, int64_t N, int64_t H, int64_t W, const fl
                        uint8_t* argmax, void* stream);
 /* As srk_conv1_pool_fwd, and in the 16-bit matmul modes also the pooled activation's bf16 / fp16 operand copy
  * (y16: N*H*(W/pool)*Co 16-bit elements, 8-byte aligned, or null), the one srk_conv2d_nhwc_fwd_pool accepts as
- * ready (x16_written = 2) instead of converting y again; *y16_written = 1 when it was written. */
+ * ready (x16_written = 2) instead of converting y again; *y16_written = 1 when it was written.  *y16_written = 3
+ * on entry: the caller consumes only the copy, and y is left unwritten when the copy is written. */
 int srk_conv1_pool_fwd16(const float* x, int64_t N, int64_t H, int64_t W, const float* w, const float* bias,
                          int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t pool, float* y,
                          uint8_t* argmax, void* y16, int* y16_written, void* stream);

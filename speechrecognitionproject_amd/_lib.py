@@ -143,6 +143,7 @@ def lib():
         for item in filter(None, os.environ.get("SRK_OPTIONS", "").split(",")):
             name, _, val = item.partition("=")
             call("srk_set_option", name.strip().encode(), int(val))
+            _options[name.strip()] = int(val)
     return _lib
 
 
@@ -194,9 +195,19 @@ def scratch_generation():
     return int(lib().srk_scratch_generation())
 
 
+_options = {}
+
+
 def set_option(name, value):
     """srk_set_option (include/srk.h): e.g. set_option("gru_persistent", 0)."""
     call("srk_set_option", name.encode(), int(value))
+    _options[name] = int(value)
+
+
+def option(name, default=0):
+    """The last value this process gave option `name` (set_option / SRK_OPTIONS), else `default`."""
+    lib()
+    return _options.get(name, default)
 
 
 PRECISIONS = {"fp32": 0, "bf16": 1, "fp16": 2}

@@ -630,6 +630,48 @@ __global__ void splitk_sum_kernel(const float* __restrict__ partial, int splits,
   out[i] = bias ? s + bias[i % ncol] : s;
 }
 
+// The same reduction for many splits (the weight gradients' deep split-K: up to 256 slabs of a few hundred
+// thousand outputs, where one thread per output walking every split is latency-bound — cfg3 bf16: 218 us per
+// step over 5 launches, r05u): a block = 8 waves x 64 lanes over 256 outputs (a float4 per lane), wave w adds
+// the splits [w S / 8, (w + 1) S / 8) in order, then the 8 wave partials are added in wave order through LDS.
+// Deterministic; n % 4 == 0 and 16-B aligned slabs (the host checks).
+__global__ __launch_bounds__(512) void splitk_sum8_kernel(const float* __restrict__ partial, int splits, int64_t n,
+                                                          int64_t ncol, const float* __restrict__ bias,
+                                                          float* __restrict__ out) {
+  __shared__ v4f red[8][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i4 = ((int64_t)blockIdx.x * 64 + lane) * 4;
+  const int per = (splits + 7) / 8, k0 = min(splits, w * per), k1 = min(splits, k0 + per);
+  v4f s = {0.f, 0.f, 0.f, 0.f};
+  if (i4 < n) {
+#pragma unroll 8
+    for (int k = k0; k < k1; ++k) s += *reinterpret_cast<const v4f*>(partial + (int64_t)k * n + i4);
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && i4 < n) {
+    v4f t = red[0][lane];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) t += red[q][lane];
+    if (bias) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[e] += bias[(i4 + e) % ncol];
+    }
+    *reinterpret_cast<v4f*>(out + i4) = t;
+  }
+}
+
+// splitk_sum_kernel or, for >= 16 splits of a 4-aligned slab, splitk_sum8_kernel
+void launch_splitk_sum(const float* partial, int splits, int64_t n, int64_t ncol, const float* bias, float* out,
+                       hipStream_t s) {
+  if (splits >= 16 && n % 4 == 0 && (uintptr_t)partial % 16 == 0 && (uintptr_t)out % 16 == 0)
+    hipLaunchKernelGGL(splitk_sum8_kernel, dim3((unsigned)((n / 4 + 63) / 64)), dim3(512), 0, s, partial, splits, n,
+                       ncol, bias, out);
+  else
+    hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, partial, splits, n,
+                       ncol, bias, out);
+}
+
 // [Co][Ci][KH][KW] -> fwd Wt [(kh,kw,ci)][co]  or  dgrad Wd [(kh,kw,co)][ci]
 __global__ void weight_layout_kernel(const float* __restrict__ w, int Co, int Ci, int KH, int KW, int to_dgrad,
                                      float* __restrict__ out) {
@@ -2054,8 +2096,7 @@ int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
           if (int e = conv_scratch((size_t)c.M * c.Nn, &dense, g_csd)) return e;
         }
         const int64_t n = c.M * c.Nn;
-        hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, partial, splits, n,
-                           c.Nn, MODE == kFwd ? c.bias : nullptr, dense);
+        launch_splitk_sum(partial, splits, n, c.Nn, MODE == kFwd ? c.bias : nullptr, dense, s);
         if (pool) {
           const int64_t rows = c.M / c.pool_w;
           hipLaunchKernelGGL(maxpool_arg_kernel, dim3((unsigned)((rows * c.Nn + 255) / 256)), dim3(256), 0, s, dense,
@@ -2155,8 +2196,7 @@ int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
   SRK_CHECK_HIP(hipGetLastError());
   if (splits > 1) {
     const int64_t n = c.M * c.Nn;
-    hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c.partial, splits, n,
-                       c.Nn, MODE == kFwd ? c.bias : nullptr, final_out);
+    launch_splitk_sum(c.partial, splits, n, c.Nn, MODE == kFwd ? c.bias : nullptr, final_out, s);
     SRK_CHECK_HIP(hipGetLastError());
     if (pooled_out) {
       const int64_t rows = c.M / pool_w;

@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void conv1_pool_fwd_kernel(C1Args a) {
         }
     }
     const size_t o = (((size_t)n * a.H + h0 + r) * Wq + wq) * kCo + c4 * 4;
-    *reinterpret_cast<v4f*>(a.y + o) = best;
+    if (a.y) *reinterpret_cast<v4f*>(a.y + o) = best;   // null: only the 16-bit copy is consumed
     *reinterpret_cast<unsigned*>(a.arg + o) = idx;
     if (LP == 1) *reinterpret_cast<u32x2c*>(a.y16 + o) = __builtin_bit_cast(u32x2c, __builtin_convertvector(best, bf4));
     if (LP == 2) *reinterpret_cast<u32x2c*>(a.y16 + o) = __builtin_bit_cast(u32x2c, __builtin_convertvector(best, h4));
@@ -300,6 +300,10 @@ int srk_conv1_pool_fwd16(const float* x, int64_t N, int64_t H, int64_t W, const 
                          int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t pool, float* y,
                          uint8_t* argmax, void* y16, int* y16_written, void* stream) {
   SRK_API_BEGIN
+  // *y16_written == 3 on entry: the caller consumes only the 16-bit copy (fbanks_cnn's fused conv2 + pool in a
+  // 16-bit training step), so the fp32 pooled activation is not stored — 5 instead of 7 B per output of the
+  // 0.92 GB this launch writes at cfg3; ignored unless the copy is written
+  const bool only16 = y16_written && *y16_written == 3;
   if (y16_written) *y16_written = 0;
   if (int rc = srk::check_c1(N, H, W, Co, KH, KW, ph, pw, pool)) return rc;
   SRK_REQUIRE(x && w && bias && y && argmax, SRK_ERR_INVALID, "conv1_pool_fwd: null pointer");
@@ -311,11 +315,14 @@ int srk_conv1_pool_fwd16(const float* x, int64_t N, int64_t H, int64_t W, const 
   a.N = (int)N; a.H = (int)H; a.W = (int)W; a.ph = (int)ph; a.pw = (int)pw;
   a.x = x; a.w = w; a.bias = bias; a.y = y; a.arg = argmax;
   a.y16 = static_cast<unsigned short*>(y16);
+  const bool skip_y = only16 && lp;
+  if (skip_y) a.y = nullptr;
   hipStream_t s = srk::as_stream(stream);
   const int hp = (int)((H + srk::kRows - 1) / srk::kRows);
   const size_t lds = (size_t)(srk::kRows + KH - 1) * (W + KW) * 4;
   // algorithmic: the input image once + pooled output + argmax (+ the 16-bit copy)
-  srk::ProfScope prof("conv1_pool_fwd", s, 4.0 * N * H * W + (lp ? 7.0 : 5.0) * N * H * (W / pool) * Co);
+  srk::ProfScope prof("conv1_pool_fwd", s,
+                      4.0 * N * H * W + ((lp ? 7.0 : 5.0) - (skip_y ? 4.0 : 0.0)) * N * H * (W / pool) * Co);
   prof.detail("conv1_pool_fwd_valu<%lldx%lld,pool%lld>", (long long)KH, (long long)KW, (long long)pool);
   const dim3 g((unsigned)(N * hp));
 #define SRK_C1F(KH_, KW_, PW_)                                                                                  \

@@ -37,7 +37,8 @@ class Network(nn.Module):
     def forward(self, x):
         with torch.no_grad():
             inx = features.fbank(x)                       # [B, 98, 120]
-        h = conv1_pool(inx, self.conv1, self.maxpool1)   # fused conv1 + maxpool1: NHWC [B, 98, 40, 64]
+        # fused conv1 + maxpool1: NHWC [B, 98, 40, 64] (its fp32 copy skipped when conv2 reads the 16-bit one)
+        h = conv1_pool(inx, self.conv1, self.maxpool1, next_conv_pool16=True)
         h = conv_pool(h, self.conv2, self.maxpool2)      # fused conv2 + maxpool2: [B, 98, 10, 128]
         h = self.conv4(self.conv3(h))                     # [B, 98, 1, 512]
         h = self.maxpool3(h.squeeze(2)).squeeze(1)        # [B, 512]

@@ -470,7 +470,7 @@ class _Conv1PoolFn(torch.autograd.Function):
     _wgrad): one input channel, the pooled NHWC output; the input (features) gets no gradient."""
 
     @staticmethod
-    def forward(ctx, x, w, b, padding, pool):
+    def forward(ctx, x, w, b, padding, pool, y16_only=False):
         x = x.contiguous()
         _check_cuda(x, w, b)
         N, H, W = x.shape
@@ -482,7 +482,9 @@ class _Conv1PoolFn(torch.autograd.Function):
         y16 = None
         if _copy16_wanted(Co) and ctx.needs_input_grad[1]:   # (forward runs under no_grad: needs_input_grad tells)
             y16 = torch.empty(y.numel(), device=x.device, dtype=torch.int16)
-        written = ctypes.c_int(0)
+        # y16_only: the caller's consumer reads only the copy (fbanks_cnn's fused conv2 + pool on 16-bit operands),
+        # so the library may leave the fp32 y unwritten (it does only when it writes the copy)
+        written = ctypes.c_int(3 if (y16_only and y16 is not None) else 0)
         call("srk_conv1_pool_fwd16", ptr(x), N, H, W, ptr(w.contiguous()), ptr(b), Co, KH, KW, padding[0], padding[1],
              pool, ptr(y), ptr(arg), ptr(y16) if y16 is not None else None, ctypes.byref(written), stream_ptr())
         if written.value:
@@ -501,18 +503,21 @@ class _Conv1PoolFn(torch.autograd.Function):
         ws = torch.empty(int(_lib.lib().srk_conv1_pool_workspace_floats(Co, KH, KW)), device=x.device)
         call("srk_conv1_pool_wgrad", ptr(x), N, H, W, Co, KH, KW, padding[0], padding[1], pool, ptr(dy.contiguous()),
              ptr(arg), ptr(dw), ptr(db), ptr(ws), stream_ptr())
-        return None, dw, db, None, None
+        return None, dw, db, None, None, None
 
 
-def conv1_pool(x, conv, pool):
+def conv1_pool(x, conv, pool, next_conv_pool16=False):
     """Fused ``pool(conv(x))`` for a one-channel NHW input when the geometry is the one
     srk_conv1_pool supports (conv1 + maxpool1 of model_fbanks_cnn / model_spec_cnn) and ``x`` needs
-    no gradient; otherwise the separate conv and pool kernels.  Returns NHWC."""
+    no gradient; otherwise the separate conv and pool kernels.  Returns NHWC.
+    next_conv_pool16: the result goes straight into ``conv_pool`` (fbanks_cnn conv2): in a 16-bit training
+    step with 16-bit conv forwards that reads only the 16-bit copy, so the fp32 activation is not stored."""
     geom = (tuple(conv.kernel_size), tuple(conv.padding), tuple(pool.kernel_size))
     if (conv.in_channels == 1 and conv.out_channels == 64 and tuple(conv.stride) == (1, 1) and conv.bias is not None
             and geom in (((7, 3), (3, 1), (1, 3)), ((3, 7), (1, 3), (1, 5))) and not x.requires_grad):
         require_gpu()
-        return _Conv1PoolFn.apply(x, conv.weight, conv.bias, conv.padding, pool.kernel_size[1])
+        y16_only = bool(next_conv_pool16 and _lib.fused_conv_pool() and not _lib.option("conv_fwd_fp32"))
+        return _Conv1PoolFn.apply(x, conv.weight, conv.bias, conv.padding, pool.kernel_size[1], y16_only)
     return pool(conv(x.unsqueeze(-1)))
 
 

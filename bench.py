@@ -595,7 +595,7 @@ def _workload_h2d(self, precision, steps, warmup):
                 self.pcm[j].copy_(host[i % n_host], non_blocking=True)
             ev_copy[j].record(cs)
 
-    def run(n):
+    def run(n, mark=None):
         upload(0)
         for i in range(n):
             j = i % 2
@@ -604,15 +604,24 @@ def _workload_h2d(self, precision, steps, warmup):
             if self.world > 1 and not self.exchange_in_graph:
                 self._exchange_and_update()
             ev_done[j].record(cur)
+            if mark is not None and i == mark[0]:
+                mark[1].record(cur)
             if i + 1 < n:
                 upload(i + 1)
 
     run(4)
     torch.cuda.synchronize()
+    # steady state: `skip` steps into an unbroken loop (the first batch's upload, which nothing can hide, and the
+    # clock ramp after the synchronize behind), then `steps` steps timed by events on the compute stream; the
+    # wall time of the whole loop (start-up included) is reported beside it
+    skip = 4
+    ev_a, ev_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    run(steps)
+    run(skip + steps, mark=(skip - 1, ev_a))
+    ev_b.record(cur)
     torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+    el_all = time.perf_counter() - t0
+    el = ev_a.elapsed_time(ev_b) * 1e-3
     # the upload alone, same buffers and stream
     t1 = time.perf_counter()
     for i in range(steps):
@@ -630,6 +639,9 @@ def _workload_h2d(self, precision, steps, warmup):
     torch.cuda.empty_cache()
     step_bytes = self.B * 16000 * 2
     return {"value": round(self.B * steps / el, 2), "unit": "utt/s", "ms_per_step": round(el / steps * 1e3, 3),
+            "timing": "steady state: %d steps after %d untimed ones of the same unbroken loop, HIP events on the "
+                      "compute stream (every upload overlapped with the previous step)" % (steps, skip),
+            "value_incl_startup": round(self.B * (skip + steps) / el_all, 2),
             "upload_bytes_per_step": step_bytes, "needed_gbs": round(step_bytes / (el / steps) / 1e9, 2),
             "upload_only_gbs": round(step_bytes * steps / el_copy / 1e9, 2), "steps": steps}
 

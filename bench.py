@@ -90,10 +90,13 @@ PEAK_HBM_GBS = 8000.0             # MI355X HBM3E spec
 MFCC_BYTES_PER_CLIP = 71956       # 64,000 in + 7,956 out
 # FlopCounterMode on the reference modules (cnn_bgru / spec_cnn: on the oracle restatements)
 TRAIN_GFLOP_PER_UTT = {"mfcc_bgru": 1.9434, "fbanks_cnn": 2.1449, "resnet_bgru": 25.8191,
-                       "spec_bgru": 2.0367, "mfrn_bgru": 10.5777, "cnn_bgru": 27.1020, "spec_cnn": 1.4726}
+                       "spec_bgru": 2.0367, "mfrn_bgru": 10.5777, "cnn_bgru": 27.1020, "spec_cnn": 1.4726,
+                       "mfcc_bgru_40x98": 1.9434 * 98 / 51}   # (the 51-step figure scaled to 98 steps)
 DEFAULT_BATCH = {"mfcc_bgru": 256, "fbanks_cnn": 512, "resnet_bgru": 512, "spec_bgru": 512, "mfrn_bgru": 256,
-                 "cnn_bgru": 512, "spec_cnn": 512}
+                 "cnn_bgru": 512, "spec_cnn": 512, "mfcc_bgru_40x98": 256}
 CFG = {"mfcc_bgru": "cfg2 mfcc_bgru: on-device MFCC[39x51] + 2-layer BiGRU(512) + FC",
+       "mfcc_bgru_40x98": "cfg2 literal, PERF-ONLY NON-REFERENCE variant: on-device MFCC[40x98] (DCT of the K2 "
+                          "fbank) + 2-layer BiGRU(40 -> 512) over 98 steps + FC (SURVEY.md §0.1)",
        "fbanks_cnn": "cfg3 fbanks_cnn: on-device log-mel fbank[98x120] + 4 Conv2d + pools + dropout + 2 FC",
        "resnet_bgru": "cfg4 resnet_bgru: raw-wave ResNet-1D (BN, ReLU) + Linear + 2-layer BiGRU(512) + FC",
        "spec_bgru": "cfg5 spec_bgru: on-device noise-mix (K4) fused into the log spectrogram[49x321] (K3) + 2-layer BiGRU(512) + FC",
@@ -125,6 +128,9 @@ def build_model(name):
     import importlib
     if name not in DEFAULT_BATCH:
         raise SystemExit("unknown --model %s" % name)
+    if name == "mfcc_bgru_40x98":   # the perf-only "MFCC (40x98)" variant of the cfg2 model
+        from speechrecognitionproject_amd.models import model_mfcc_bgru
+        return model_mfcc_bgru.Network(features="mfcc40x98")
     return importlib.import_module("speechrecognitionproject_amd.models.model_%s" % name).Network()
 
 
@@ -337,6 +343,8 @@ EXTRA_CONFIGS = (  # BASELINE.json configs[2..4] at their per-GPU batch (the def
     # the faithful 16-bit mode of the BatchNorm model: conv forwards on fp32 operands (srk option conv_fwd_fp32;
     # cfg4-bf16's gradients are 4-39 % norm-wise from float64, these <= 2e-2: tools/bf16_policy_resnet.py)
     ("cfg4-bf16-faithful", "resnet_bgru", "bf16", 512, 4),
+    # BASELINE.json configs[1] read literally, "MFCC (40x98) ... bf16": a perf-only, non-reference variant
+    ("cfg2-mfcc40x98-bf16", "mfcc_bgru_40x98", "bf16", 256, 20),
 )
 # what each 16-bit record's gradients are worth against float64 (tests/test_config_batch_gpu.py)
 GRADIENTS = {"cfg3-bf16": "every gradient tensor <= 2e-2 norm-wise of the fp32 oracle",

@@ -19,6 +19,8 @@ Pinning status
   tests (silence → c0 = -100*sqrt(128); DCT orthonormality; tone band placement).
 * ``add_noise_uniform`` — pinned: ``tests/golden/noise_mix_golden.npz`` from the reference's
   ``dataset.py:183-193`` with seeded draws.
+* ``mfcc40x98``      — NOT a reference function: the perf-only "MFCC (40x98)" variant BASELINE.json
+  names = scipy's orthonormal DCT-II of the pinned ``filter_banks``, first 40.
 """
 import numpy as np
 
@@ -240,6 +242,14 @@ def compute_mfcc(sample, index=None):
     d = np.gradient(m, axis=1)                                           # :14
     dd = np.gradient(d, axis=1)                                          # :16
     return np.concatenate((m, d, dd)).astype(np.float32)                # :15-18
+
+
+def mfcc40x98(sample, index=None):
+    """float32[16000] -> float32[98, 40]: the perf-only variant (features.mfcc40x98) — scipy.fft.dct type 2,
+    norm 'ortho', over the 120 mel bands of filter_banks (dB), coefficients 0..39, in float64."""
+    import scipy.fft
+    fb = filter_banks(sample, index).astype(np.float64)
+    return scipy.fft.dct(fb, type=2, norm="ortho", axis=1)[:, :40].astype(np.float32)
 
 
 # ----------------------------------------------------------------------------------------

@@ -10,6 +10,7 @@ import ctypes
 
 import torch
 
+from . import _lib
 from ._lib import SrkError, call, lib
 
 SEQ_LENGTH = 16000
@@ -105,6 +106,37 @@ def mfcc(pcm, time_major=False, out=None):
     shape = (x.shape[0], 51, 39) if time_major else (x.shape[0], 39, 51)
     out = torch.empty(shape, device=x.device, dtype=torch.float32) if out is None else out
     call(_entry("srk_mfcc_fwd", x), ptr(x), x.shape[0], ptr(out), 1 if time_major else 0, stream_ptr())
+    return out
+
+
+_DCT40 = {}
+
+
+def _dct40(device):
+    """Orthonormal DCT-II rows k = 0..39 over the 120 mel bands: [40, 120] fp32 on `device`."""
+    import math
+    key = str(device)
+    if key not in _DCT40:
+        n = torch.arange(120, dtype=torch.float64)
+        rows = [math.sqrt((1.0 if k == 0 else 2.0) / 120.0) * torch.cos(math.pi * k * (2 * n + 1) / 240.0)
+                for k in range(40)]
+        _DCT40[key] = torch.stack(rows).to(device=device, dtype=torch.float32).contiguous()
+    return _DCT40[key]
+
+
+def mfcc40x98(pcm, out=None):
+    """PERF-ONLY, NON-REFERENCE variant (BASELINE.json configs[1] names "MFCC (40x98)",
+    which the reference does not compute — its MFCC is 39 x 51, model_mfcc_bgru.py:13-16): 40 MFCCs over
+    98 frames, [B, 98, 40] time-major = the orthonormal DCT-II (first 40 coefficients) of K2's log-mel
+    fbank (400-sample frames, hop 160, 120 mel bands in dB, model_fbanks_cnn.py:15-66), the DCT as one
+    fp32 GEMM (srk_gemm_f32) over the B x 98 frames."""
+    fb = fbank(pcm)
+    n = fb.shape[0] * 98
+    out = torch.empty((fb.shape[0], 98, 40), device=fb.device, dtype=torch.float32) if out is None else out
+    d = _dct40(fb.device)
+    with _lib.precision_scope("fp32"):
+        call("srk_gemm_f32", 0, 1, n, 40, 120, 1.0, ptr(fb), 120, ptr(d), 120, 0.0, ptr(out), 40, None, 0,
+             stream_ptr())
     return out
 
 

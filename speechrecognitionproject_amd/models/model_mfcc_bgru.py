@@ -21,13 +21,24 @@ def compute_mfcc(sample):
 
 
 class Network(nn.Module):
-    def __init__(self, num_features=512, num_layers=2):
+    """features="mfcc39x51" is the reference model.  features="mfcc40x98" is a PERF-ONLY, NON-REFERENCE
+    variant for BASELINE.json configs[1]'s literal "MFCC (40x98)" (features.mfcc40x98: 40 MFCCs over 98
+    frames, GRU input 40, 98 steps) — its state_dict differs in the first GRU layer."""
+
+    def __init__(self, num_features=512, num_layers=2, features="mfcc39x51"):
         super().__init__()
-        self.gru = BiGRU(39, num_features, num_layers=num_layers, bidirectional=True, batch_first=True)
+        if features not in ("mfcc39x51", "mfcc40x98"):
+            raise ValueError("features must be 'mfcc39x51' (the reference) or 'mfcc40x98' (perf-only)")
+        self.features = features
+        n_in = 39 if features == "mfcc39x51" else 40
+        self.gru = BiGRU(n_in, num_features, num_layers=num_layers, bidirectional=True, batch_first=True)
         self.fc = Linear(num_features * 2, 12)
 
     def forward(self, x):
         with torch.no_grad():
-            inx = features.mfcc(x, time_major=True)     # [B, 51, 39] = transpose(mfcc, 1, 2)
+            if self.features == "mfcc39x51":
+                inx = features.mfcc(x, time_major=True)     # [B, 51, 39] = transpose(mfcc, 1, 2)
+            else:
+                inx = features.mfcc40x98(x)                 # [B, 98, 40] (perf-only variant)
         inx, _ = self.gru(inx)
         return self.fc(last_step(inx))

@@ -1807,6 +1807,154 @@ __global__ __launch_bounds__(NW * 64, 1) void conv_row16_pool_kernel(RowArgs a) 
   }
 }
 
+// The same conv + (1, 4) pool on fp32 operands (cfg3 at the reference's precision; option conv_row32): the fp32
+// weight matrix (448 x 128 x 4 B = 224 KB) does not fit in LDS beside the staged rows, so the workgroup stages 8
+// image rows of x ONCE per tile ([8][46 padded positions][64 ci] fp32, 92 KB, 16-B chunks XOR-swizzled by position)
+// and streams Wt one tap at a time ([64 ci][128 co], 32 KB, double-buffered, the next tap's loads in flight during
+// this tap's MFMAs; the whole matrix stays in L2).  8 waves over the 320 x 128 tile: wave = column block w & 3 x
+// row blocks 5 (w >> 2) .. +4, v_mfma_f32_32x32x2_f32 with the k-permuted 8-deep blocks of the tile core
+// (mfma_tile.h: sub-step s of block b pairs k = 8 b + s and 8 b + 4 + s, A by one ds_read_b128, B by 4 ds_read_b32
+// whose halves the column swizzle puts on disjoint banks).  k = (kw, ci) ascending in 8-deep blocks — the
+// implicit GEMM's sequence per accumulator, and the same pooled epilogue: bitwise its result
+// (tests/test_conv_gpu.py test_conv_row32_equals_gemm).
+struct Row32Args {
+  const float* x;      // [rows][WD][CI] fp32
+  const float* wt;     // [(kw, ci)][CO] fp32 (the fwd weight matrix Wt)
+  const float* bias;   // [CO] or null
+  float* y;            // pooled [rows][WD / 4][CO]
+  uint8_t* arg;        // [rows][WD / 4][CO]
+  int rows, groups;
+};
+template <int KW, int PW, int WD, int CI, int CO, int R>
+__global__ __launch_bounds__(512, 1) void conv_row32_pool_kernel(Row32Args a) {
+  static_assert(CO == 128 && CI == 64 && WD % 4 == 0 && (R * WD) % 32 == 0, "row32 geometry");
+  constexpr int NT = 512;
+  constexpr int WP = WD + 2 * PW;               // padded positions per staged row
+  constexpr int MB = R * WD / 32;               // row blocks of 32 (10)
+  constexpr int RB = MB / 2;                    // row blocks per wave (5)
+  constexpr int XCH = R * WD * (CI / 4);        // 16-B chunks of one tile's rows (5120)
+  constexpr int XPT = XCH / NT;                 // per thread (10)
+  constexpr int TCH = CI * CO / 4;              // 16-B chunks of one tap's weights (2048)
+  constexpr int TPT = TCH / NT;                 // per thread (4)
+  static_assert(XCH % NT == 0 && TCH % NT == 0 && MB % 2 == 0, "row32 tile split");
+  __shared__ __attribute__((aligned(16))) float Xl[R * WP * CI];   // [row][pos][ci], chunk ch at ch ^ (pos & 15)
+  __shared__ __attribute__((aligned(16))) float Wl[2][CI * CO];    // one tap [k][co], co ^ (((k >> 2) & 1) << 5)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wc = wave & 3, rb0 = (wave >> 2) * RB;
+  for (int c = tid; c < R * 2 * PW * (CI / 4); c += NT) {   // the halo positions, once
+    const int rl = c / (2 * PW * (CI / 4)), rem = c % (2 * PW * (CI / 4));
+    const int pp = rem / (CI / 4), ch = rem % (CI / 4);
+    const int q = pp < PW ? pp : WD + pp;
+    *reinterpret_cast<v4f*>(Xl + (rl * WP + q) * CI + ((ch ^ (q & 15)) * 4)) = v4f{0.f, 0.f, 0.f, 0.f};
+  }
+  v4f xr[XPT], wr[TPT];
+  const auto rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x), (short)0, 0x7ffffff0, 0x00020000);
+  const auto rsW = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.wt), (short)0, 0x7ffffff0, 0x00020000);
+  auto fetch_x = [&](int g) {   // tile g's rows into registers (past the last row: 16 zero bytes)
+    const int last = (a.rows - g * R) * WD * (CI / 4);
+    const int sbase = __builtin_amdgcn_readfirstlane(g * R * WD * CI * 4);
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int c = tid + i * NT;
+      xr[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rsX, c < last ? sbase + c * 16 : (int)0x80000000u,
+                                                                             0, 0));
+    }
+  };
+  auto stage_x = [&]() {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int c = tid + i * NT, rl = c / (WD * (CI / 4)), rem = c % (WD * (CI / 4));
+      const int px = rem / (CI / 4), ch = rem % (CI / 4), q = px + PW;
+      *reinterpret_cast<v4f*>(Xl + (rl * WP + q) * CI + ((ch ^ (q & 15)) * 4)) = xr[i];
+    }
+  };
+  auto fetch_w = [&](int kw) {
+    const int sbase = __builtin_amdgcn_readfirstlane(kw * CI * CO * 4);
+#pragma unroll
+    for (int i = 0; i < TPT; ++i)
+      wr[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rsW, sbase + (tid + i * NT) * 16, 0, 0));
+  };
+  auto stage_w = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < TPT; ++i) {
+      const int c = tid + i * NT, k = c / (CO / 4), col = (c % (CO / 4)) * 4;
+      *reinterpret_cast<v4f*>(&Wl[buf][k * CO + (col ^ (((k >> 2) & 1) << 5))]) = wr[i];
+    }
+  };
+  int arow[RB], apos[RB];
+#pragma unroll
+  for (int i = 0; i < RB; ++i) {
+    const int p = (rb0 + i) * 32 + (lane & 31);
+    arow[i] = (p / WD) * WP;
+    apos[i] = p % WD;
+  }
+  const int lh = lane >> 5, lc = lane & 31;
+  const int bcol = (wc * 32 + lc) ^ (lh << 5);   // this lane's B column in the swizzled tap image (k >> 2 & 1 = lh)
+  const float bv = a.bias ? a.bias[wc * 32 + lc] : 0.f;
+  int g = blockIdx.x;
+  if (g < a.groups) fetch_x(g);
+  fetch_w(0);
+  while (g < a.groups) {
+    stage_x();
+    stage_w(0);
+    __syncthreads();
+    const int gn = g + (int)gridDim.x;
+    f32x16 acc[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+#pragma unroll 1
+    for (int kw = 0; kw < KW; ++kw) {
+      fetch_w(kw + 1 < KW ? kw + 1 : 0);   // the next tap (tap 0 again for the next tile)
+      const float* Ws = Wl[kw & 1];
+      // one 8-deep block's fragments at a time (a double-buffered prefetch spilled at 2 waves per SIMD: the
+      // other wave of the SIMD covers the LDS latency)
+#pragma unroll 1
+      for (int kb = 0; kb < CI / 8; ++kb) {
+        const float* q0 = Ws + (kb * 8 + 4 * lh) * CO + bcol;
+        const v4f fb = v4f{q0[0], q0[CO], q0[2 * CO], q0[3 * CO]};
+        const int ch = 2 * kb + lh;
+        v4f fa[RB];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int q = apos[i] + kw;   // position in the staged row
+          fa[i] = *reinterpret_cast<const v4f*>(Xl + (arow[i] + q) * CI + ((ch ^ (q & 15)) * 4));
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+          for (int i = 0; i < RB; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s2], fb[s2], acc[i], 0, 0, 0);
+      }
+      if (kw + 1 < KW) stage_w((kw + 1) & 1);   // that buffer was last read in tap kw - 1 (behind the barrier)
+      __syncthreads();
+    }
+    // pooled epilogue (the implicit GEMM's): rows 8 rq + 4 lh + 0..3 of a block are one (1, 4) window
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+#pragma unroll
+      for (int rq = 0; rq < 4; ++rq) {
+        const int p0 = (rb0 + i) * 32 + 8 * rq + 4 * lh;   // tile pixel, a multiple of 4
+        const int row = g * R + p0 / WD;
+        if (row >= a.rows) continue;
+        float best = acc[i][4 * rq] + bv;
+        int am = 0;
+#pragma unroll
+        for (int pp = 1; pp < 4; ++pp) {
+          const float v = acc[i][4 * rq + pp] + bv;
+          if (v > best || (v != v && best == best)) { best = v; am = pp; }
+        }
+        const size_t o = ((size_t)g * R * WD + p0) / 4 * CO + wc * 32 + lc;
+        a.y[o] = best;
+        a.arg[o] = (uint8_t)am;
+      }
+    }
+    if (gn < a.groups) fetch_x(gn);
+    __syncthreads();   // every wave is done reading Xl before the next tile is staged
+    g = gn;
+  }
+}
+
 // The data gradient of the same conv: dX[w][ci] = sum over (kw, co) of dY[w + PW - kw][co] Wd[(kw,
 // co)][ci] — the implicit GEMM's k order, so bitwise its result.  dY (128 channels) has twice the bytes per staged
 // position, so the weights cannot stay resident beside 8 staged rows: the workgroup stages 8 rows of the dense 16-bit
@@ -2502,6 +2650,25 @@ int srk_conv2d_nhwc_fwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
       SRK_CHECK_HIP(hipGetLastError());
       return SRK_OK;
     }
+  }
+  // fbanks_cnn conv2 + maxpool2 on fp32 operands: the row-staged kernel (weights streamed per tap)
+  if (!c.a16 && srk::matmul_prec() == srk::kPrecF32 && srk::g_opt_conv_row32 && KH == 1 && KW == 7 && ph == 0 &&
+      pw == 3 && W == 40 && Ci == 64 && Co == 128 && pool_w == 4 && (N * H) < (1LL << 31) / (W * Ci * 4)) {
+    srk::Row32Args ra{};
+    ra.x = x;
+    ra.wt = ws;
+    ra.bias = bias;
+    ra.y = y;
+    ra.arg = argmax;
+    ra.rows = (int)(N * H);
+    ra.groups = (int)((N * H + 7) / 8);
+    srk::ProfScope prof("conv_fwd", s, 2.0 * (double)c.M * (double)c.Nn * (double)c.K);
+    prof.detail("conv_row32_pool_kernel %lldx%lldx%lld", (long long)c.M, (long long)c.Nn, (long long)c.K);
+    prof.bytes(srk::conv_bytes(c, srk::kFwd, 4));
+    hipLaunchKernelGGL((srk::conv_row32_pool_kernel<7, 3, 40, 64, 128, 8>),
+                       dim3((unsigned)std::min<int64_t>(ra.groups, srk::kCUs)), dim3(512), 0, s, ra);
+    SRK_CHECK_HIP(hipGetLastError());
+    return SRK_OK;
   }
   return srk::run_conv_gemm<srk::kFwd>(c, s, "conv_fwd");
   SRK_API_END

@@ -31,6 +31,7 @@ int g_opt_conv_colsum16 = 1;
 int g_opt_conv_ring_qs = 6;
 int g_opt_conv_fast16 = 1;
 int g_opt_conv_row16 = 1;
+int g_opt_conv_row32 = 1;
 int g_opt_conv_row16_dgrad = 2;
 int g_opt_bn_tree = 0;
 int g_opt_mfcc_variant = 3;
@@ -404,6 +405,10 @@ int srk_set_option(const char* name, int64_t value) {
   if (n == "conv_row16") {   // fbanks conv2 + pool, 16-bit: row-staged kernel (1) or implicit GEMM (0)
     SRK_REQUIRE(value >= 0 && value <= 2, SRK_ERR_INVALID, "conv_row16 must be 0, 1 (8 waves) or 2 (4 waves)");
     srk::g_opt_conv_row16 = (int)value;
+    return SRK_OK;
+  }
+  if (n == "conv_row32") {   // fbanks conv2 on fp32 operands: row-staged kernels (1) or the implicit GEMM (0)
+    srk::g_opt_conv_row32 = value != 0;
     return SRK_OK;
   }
   if (n == "conv_fast16") {   // 16-bit-source register-staged convs: uniform-tap fast gathers (1) or generic (0)

@@ -135,6 +135,9 @@ extern int g_opt_conv_fast16;
 // fbanks_cnn conv2 + maxpool2 in 16-bit modes on the row-staged kernel (weights resident in LDS, image rows staged
 // once per tile) ("conv_row16", default 1; 0 = the implicit-GEMM kernels)
 extern int g_opt_conv_row16;
+// fbanks_cnn conv2 (+ maxpool2) on fp32 operands on the row-staged kernels (x rows staged once per tile, the weights
+// streamed one tap at a time) ("conv_row32", default 1; 0 = the implicit-GEMM kernels)
+extern int g_opt_conv_row32;
 // the row-staged data gradient of the same conv ("conv_row16_dgrad", default 2 = 5 units per wave; 1 = 3 / 3 / 2 / 2
 // row blocks per wave, 418 vs 475-485 us, r05p; 0 = the implicit GEMM)
 extern int g_opt_conv_row16_dgrad;

@@ -1955,6 +1955,168 @@ __global__ __launch_bounds__(512, 1) void conv_row32_pool_kernel(Row32Args a) {
   }
 }
 
+// The fp32 data gradient of the same conv (option conv_row32): dX[w][ci] = sum over (kw, co) of dY[w + PW - kw][co]
+// Wd[(kw, co)][ci].  8 staged rows of dY in fp32 are 184 KB, so the workgroup stages them one 64-channel HALF at a
+// time ([8][46][64] fp32, 92 KB, 16-B chunks XOR-swizzled by position) and streams Wd one (tap, half) slice at a
+// time ([64 co][64 ci], 16 KB, double-buffered); the next half's (or the next tile's) dY rows load into registers
+// during the current half's MFMAs.  POOLED: dY arrives as fbanks_cnn's pooled gradient + its uint8 window argmax
+// (the pooled conv's backward) and is rebuilt at staging time, dY[px][co] = arg[px / 4][co] == px % 4 ?
+// dP[px / 4][co] : 0 — the implicit GEMM's UNPOOL gather — so a quarter of the dense bytes is read.  4 waves (one
+// per SIMD, 512 registers): wave = column block w & 1 x row blocks 5 (w >> 1) .. +4 on v_mfma_f32_32x32x2_f32 in
+// the tile core's k-permuted 8-deep blocks, the next block's fragments read ahead of this block's MFMAs.  k order
+// (half, kw, co) — another fp32 summation order than the implicit GEMM's (kw, co) (tests: within 1e-5).
+struct Row32DgArgs {
+  const float* dy;      // dense [rows][WD][CA], or POOLED [rows][WD / 4][CA]
+  const uint8_t* arg;   // POOLED: [rows][WD / 4][CA] window argmax
+  const float* wd;      // [(kw, co)][CN] fp32 (the dgrad weight matrix Wd)
+  float* dx;            // [rows][WD][CN]
+  int rows, groups;
+};
+template <int KW, int PW, int WD, int CA, int CN, int R, bool POOLED>
+__global__ __launch_bounds__(256, 1) void conv_row32_dgrad_kernel(Row32DgArgs a) {
+  static_assert(CA == 128 && CN == 64 && WD % 4 == 0 && (R * WD) % 32 == 0 && 2 * PW == KW - 1, "row32 dgrad geometry");
+  constexpr int NT = 256, CH = 64;                       // threads; channels of dY per staged half
+  constexpr int WP = WD + 2 * PW;
+  constexpr int MB = R * WD / 32;                        // row blocks (10)
+  constexpr int RB = MB / 2;                             // row blocks per wave (5)
+  constexpr int YCH = POOLED ? R * (WD / 4) * (CH / 4) : R * WD * (CH / 4);   // loaded 16-B chunks per half tile
+  constexpr int YPT = YCH / NT;                          // per thread (5 pooled / 20 dense)
+  constexpr int TCH = CH * CN / 4;                       // 16-B chunks of one (tap, half) slice (1024)
+  constexpr int TPT = TCH / NT;                          // per thread (4)
+  static_assert(YCH % NT == 0 && TCH % NT == 0 && MB == 10, "row32 dgrad tile split");
+  __shared__ __attribute__((aligned(16))) float Yl[R * WP * CH];   // [row][pos][co of the half], ch ^ (pos & 15)
+  __shared__ __attribute__((aligned(16))) float Wl[2][CH * CN];    // one slice [co][ci], ci ^ (((co >> 2) & 1) << 5)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cb = wave & 1, rb0 = (wave >> 1) * RB;
+  for (int c = tid; c < R * 2 * PW * (CH / 4); c += NT) {   // halo positions, once
+    const int rl = c / (2 * PW * (CH / 4)), rem = c % (2 * PW * (CH / 4));
+    const int pp = rem / (CH / 4), ch = rem % (CH / 4);
+    const int q = pp < PW ? pp : WD + pp;
+    *reinterpret_cast<v4f*>(Yl + (rl * WP + q) * CH + ((ch ^ (q & 15)) * 4)) = v4f{0.f, 0.f, 0.f, 0.f};
+  }
+  v4f yr[YPT], wr[TPT];
+  unsigned ar[POOLED ? YPT : 1];
+  const auto rsY = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.dy), (short)0, 0x7ffffff0, 0x00020000);
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(POOLED ? a.arg : nullptr), (short)0,
+                                                     0x7ffffff0, 0x00020000);
+  const auto rsW = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.wd), (short)0, 0x7ffffff0, 0x00020000);
+  constexpr int PXL = POOLED ? WD / 4 : WD;   // loaded positions per row
+  auto fetch_y = [&](int g, int h) {   // half h of tile g's dY rows (past the last row: zeros)
+    const int last = (a.rows - g * R) * PXL * (CH / 4);
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) {
+      const int c = tid + i * NT, rl = c / (PXL * (CH / 4)), rem = c % (PXL * (CH / 4));
+      const int px = rem / (CH / 4), ch = rem % (CH / 4);
+      const int e = ((g * R + rl) * PXL + px) * CA + h * CH + ch * 4;   // element index (< 2^31 / 4: host check)
+      const bool ok = c < last;
+      yr[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rsY, ok ? e * 4 : (int)0x80000000u, 0, 0));
+      if constexpr (POOLED) ar[i] = __builtin_amdgcn_raw_buffer_load_b32(rsA, ok ? e : (int)0x80000000u, 0, 0);
+    }
+  };
+  auto stage_y = [&]() {
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) {
+      const int c = tid + i * NT, rl = c / (PXL * (CH / 4)), rem = c % (PXL * (CH / 4));
+      const int px = rem / (CH / 4), ch = rem % (CH / 4);
+      if constexpr (POOLED) {   // the pooled value goes to the window position its argmax names, zeros elsewhere
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+          const int q = 4 * px + pp + PW;
+          v4f v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = ((ar[i] >> (8 * e)) & 0xFFu) == (unsigned)pp ? yr[i][e] : 0.f;
+          *reinterpret_cast<v4f*>(Yl + (rl * WP + q) * CH + ((ch ^ (q & 15)) * 4)) = v;
+        }
+      } else {
+        const int q = px + PW;
+        *reinterpret_cast<v4f*>(Yl + (rl * WP + q) * CH + ((ch ^ (q & 15)) * 4)) = yr[i];
+      }
+    }
+  };
+  auto fetch_w = [&](int kw, int h) {   // slice (kw, h): Wd rows kw * CA + h * CH .. + 63
+    const int sbase = __builtin_amdgcn_readfirstlane((kw * CA + h * CH) * CN * 4);
+#pragma unroll
+    for (int i = 0; i < TPT; ++i)
+      wr[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rsW, sbase + (tid + i * NT) * 16, 0, 0));
+  };
+  auto stage_w = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < TPT; ++i) {
+      const int c = tid + i * NT, k = c / (CN / 4), col = (c % (CN / 4)) * 4;
+      *reinterpret_cast<v4f*>(&Wl[buf][k * CN + (col ^ (((k >> 2) & 1) << 5))]) = wr[i];
+    }
+  };
+  int arow[RB], apos[RB];
+#pragma unroll
+  for (int i = 0; i < RB; ++i) {
+    const int p = (rb0 + i) * 32 + (lane & 31);
+    arow[i] = (p / WD) * WP;
+    apos[i] = p % WD;
+  }
+  const int lh = lane >> 5, lc = lane & 31;
+  const int bcol = (cb * 32 + lc) ^ (lh << 5);
+  int g = blockIdx.x;
+  if (g < a.groups) fetch_y(g, 0);
+  fetch_w(0, 0);
+  while (g < a.groups) {
+    const int gn = g + (int)gridDim.x;
+    f32x16 acc[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      stage_y();
+      stage_w(0);
+      __syncthreads();
+      if (h == 0) fetch_y(g, 1);                  // the second half lands during the first half's MFMAs
+      else if (gn < a.groups) fetch_y(gn, 0);     // the next tile's first half during the second's
+#pragma unroll 1
+      for (int kw = 0; kw < KW; ++kw) {
+        if (kw + 1 < KW) fetch_w(kw + 1, h);
+        else fetch_w(0, h ^ 1);                   // the next half's (or the next tile's) first slice
+        const float* Ws = Wl[kw & 1];
+        auto frags = [&](int kb, v4f (&fa)[RB], v4f& fb) {
+          const float* q0 = Ws + (kb * 8 + 4 * lh) * CN + bcol;
+          fb = v4f{q0[0], q0[CN], q0[2 * CN], q0[3 * CN]};
+          const int ch = 2 * kb + lh;
+#pragma unroll
+          for (int i = 0; i < RB; ++i) {
+            const int q = apos[i] + 2 * PW - kw;   // dY position w + PW - kw in the staged (haloed) row
+            fa[i] = *reinterpret_cast<const v4f*>(Yl + (arow[i] + q) * CH + ((ch ^ (q & 15)) * 4));
+          }
+        };
+        v4f fa[2][RB], fb[2];
+        frags(0, fa[0], fb[0]);
+#pragma unroll
+        for (int kb = 0; kb < CH / 8; ++kb) {
+          const int c = kb & 1;
+          if (kb + 1 < CH / 8) frags(kb + 1, fa[c ^ 1], fb[c ^ 1]);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+            for (int i = 0; i < RB; ++i)
+              acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[c][i][s2], fb[c][s2], acc[i], 0, 0, 0);
+        }
+        if (kw + 1 < KW) stage_w((kw + 1) & 1);   // that buffer was last read in tap kw - 1 (behind the barrier)
+        __syncthreads();
+      }
+    }
+    float* const xbase = a.dx + (size_t)g * R * WD * CN;
+    const int nreal = (a.rows - g * R) * WD;   // real pixels of this tile
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int p = (rb0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (p < nreal) xbase[p * CN + cb * 32 + lc] = acc[i][r];
+      }
+    g = gn;
+  }
+}
+
 // The data gradient of the same conv: dX[w][ci] = sum over (kw, co) of dY[w + PW - kw][co] Wd[(kw,
 // co)][ci] — the implicit GEMM's k order, so bitwise its result.  dY (128 channels) has twice the bytes per staged
 // position, so the weights cannot stay resident beside 8 staged rows: the workgroup stages 8 rows of the dense 16-bit
@@ -2525,6 +2687,24 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
       hipLaunchKernelGGL((srk::conv_row16_dgrad_kernel<2, 7, 3, 40, 128, 64, 8, true>), grid, block, 0, s, ra);
     else
       hipLaunchKernelGGL((srk::conv_row16_dgrad_kernel<2, 7, 3, 40, 128, 64, 8>), grid, block, 0, s, ra);
+  } else if (dgrad_implicit && !d16[0] && prec == srk::kPrecF32 && srk::g_opt_conv_row32 && KH == 1 && KW == 7 &&
+             ph == 0 && pw == 3 && sh == 1 && sw == 1 && W == 40 && Ci == 64 && Co == 128 && dy && dy_arg &&
+             (N * H) < (1LL << 29) / (W * Co)) {
+    // fbanks_cnn conv2's data gradient on fp32 operands (the pooled backward: the pooled gradient + argmax): the
+    // row-staged kernel (conv_row32_dgrad_kernel; its dense-dY form spills at one wave per SIMD, not used)
+    srk::Row32DgArgs ra{};
+    ra.dy = dy;
+    ra.arg = dy_arg;
+    ra.wd = ws;
+    ra.dx = dx;
+    ra.rows = (int)(N * H);
+    ra.groups = (int)((N * H + 7) / 8);
+    srk::ProfScope prof("conv_dgrad", s, 2.0 * (double)(N * H * W) * (double)Ci * (double)(KW * Co));
+    prof.detail("conv_row32_dgrad_kernel<unpool> %lldx%lldx%lld", (long long)(N * H * W), (long long)Ci,
+                (long long)(KW * Co));
+    prof.bytes(5.0 / 4.0 * (double)(N * H * W) * Co + 4.0 * (double)(KW * Co) * Ci + 4.0 * (double)(N * H * W) * Ci);
+    const dim3 grid((unsigned)std::min<int64_t>(ra.groups, srk::kCUs)), block(256);
+    hipLaunchKernelGGL((srk::conv_row32_dgrad_kernel<7, 3, 40, 128, 64, 8, true>), grid, block, 0, s, ra);
   } else if (dgrad_implicit) {
     srk::ConvArgs d = c;
     d.wmat = ws; d.out = dx;
@@ -2651,8 +2831,10 @@ int srk_conv2d_nhwc_fwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
       return SRK_OK;
     }
   }
-  // fbanks_cnn conv2 + maxpool2 on fp32 operands: the row-staged kernel (weights streamed per tap)
-  if (!c.a16 && srk::matmul_prec() == srk::kPrecF32 && srk::g_opt_conv_row32 && KH == 1 && KW == 7 && ph == 0 &&
+  // fbanks_cnn conv2 + maxpool2 on fp32 operands: the row-staged kernel (weights streamed per tap), unless the
+  // ring pooled forward is asked for (conv_ring bit 7)
+  if (!c.a16 && srk::matmul_prec() == srk::kPrecF32 && srk::g_opt_conv_row32 && !(srk::g_opt_conv_ring & 0x80) &&
+      KH == 1 && KW == 7 && ph == 0 &&
       pw == 3 && W == 40 && Ci == 64 && Co == 128 && pool_w == 4 && (N * H) < (1LL << 31) / (W * Ci * 4)) {
     srk::Row32Args ra{};
     ra.x = x;

@@ -496,3 +496,39 @@ def test_conv_row32_equals_gemm(gpu, N):
     nan = torch.isnan(y1)
     assert bool(nan.any()) and torch.equal(nan, torch.isnan(y0))
     assert torch.equal(y1[~nan], y0[~nan])
+    # the backward (finite input): the argmax the gradients route through is the implicit GEMM's (weight and bias
+    # gradients, on the same kernels either way, bitwise); the data gradient on the row-staged kernel
+    # (conv_row32_dgrad_kernel: the pooled gradient unpooled at staging, k order (half, kw, co)) within 1e-5 of
+    # the implicit GEMM's and of float64
+    x[0, 0, :8] = 0.5
+    gy = torch.randn(N, H, W // 4, Co, generator=g).cuda()
+    grads = []
+    try:
+        for row in (1, 0):
+            _lib.set_option("conv_row32", row)
+            _lib.prof_enable(True)
+            xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
+            (snn._ConvPoolNHWCFn.apply(xm, wm, bm, (0, 3), 4) * gy).sum().backward()
+            torch.cuda.synchronize()
+            used = any("conv_row32_dgrad" in e["kernel"] for e in _lib.prof_kernels())
+            _lib.prof_enable(False)
+            grads.append((xm.grad, wm.grad, bm.grad, used))
+    finally:
+        _lib.set_option("conv_row32", 1)
+        _lib.prof_enable(False)
+    assert grads[0][3] and not grads[1][3]
+    for a_, c_ in zip(grads[0][1:3], grads[1][1:3]):
+        assert torch.isfinite(a_).all() and torch.equal(a_, c_)
+    dx1, dx0 = grads[0][0].double(), grads[1][0].double()
+    assert torch.isfinite(dx1).all()
+    assert ((dx1 - dx0).abs().max() / dx0.abs().max()).item() <= 1e-5
+    # float64 reference of the data gradient: unpool through the argmax, then conv_transpose
+    with torch.no_grad():
+        xd = x.double().permute(0, 3, 1, 2)
+        wd = w.double()
+        yd = torch.nn.functional.conv2d(xd, wd, b.double(), padding=(0, 3))     # [N, Co, H, W]
+        win = yd.reshape(N, Co, H, W // 4, 4)
+        am = win.argmax(-1, keepdim=True)
+        dyd = torch.zeros_like(win).scatter_(-1, am, gy.double().permute(0, 3, 1, 2).unsqueeze(-1)).reshape(N, Co, H, W)
+        dx64 = torch.nn.grad.conv2d_input(xd.shape, wd, dyd, padding=(0, 3)).permute(0, 2, 3, 1)
+    assert ((dx1 - dx64).abs().max() / dx64.abs().max()).item() <= 1e-5

@@ -202,6 +202,7 @@ def test_conv_pool_fused_equals_separate(gpu, gather, ring, precision, N, H, W, 
         _lib.set_matmul_precision(precision)
         _lib.set_option("conv_unpool_gather", gather)
         _lib.set_option("conv_ring", ring)
+        _lib.set_option("conv_row32", 0)   # the implicit-GEMM paths (row-staged: test_conv_row32_equals_gemm)
         for fused in (True, False):
             _lib.set_fused_conv_pool(fused)
             with torch.no_grad():
@@ -216,6 +217,7 @@ def test_conv_pool_fused_equals_separate(gpu, gather, ring, precision, N, H, W, 
     finally:
         _lib.set_option("conv_unpool_gather", 1)
         _lib.set_option("conv_ring", 0x77)
+        _lib.set_option("conv_row32", 1)
         _lib.set_fused_conv_pool(True)
         _lib.set_matmul_precision("fp32")
     for i, (a, c) in enumerate(zip(*outs)):

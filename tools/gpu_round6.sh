@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-5 GPU evidence:  gpurun --timeout 1150 -- bash tools/gpu_round5.sh TAG
+# Round-6 GPU evidence:  gpurun --timeout 1150 -- bash tools/gpu_round6.sh TAG
 # pytest -m gpu, smoke, the default bench line, rocprofv3 --kernel-trace --stats of the cfg2 bench
 # command and of each config command (graph replays), summarised on the box.  Every GPU step has its
 # own time limit; steps are chained with && (a failure ends the call).
 set -o pipefail
-TAG=${1:-r05}
+TAG=${1:-r06}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp

@@ -2117,6 +2117,142 @@ __global__ __launch_bounds__(256, 1) void conv_row32_dgrad_kernel(Row32DgArgs a)
   }
 }
 
+// The fp32 weight gradient of the same conv (option conv_row32): dWt[(kw, ci)][co] = sum over pixels p of
+// X[p + kw - PW][ci] dY[p][co], dY = the pooled gradient unpooled through its window argmax (fbanks_cnn's pooled
+// backward).  The implicit GEMM (conv_gemm_kernel<wgrad, unpool>) re-gathers every x pixel once per tap from L2
+// with per-unit index math and writes 126 split-K slabs; here a persistent workgroup stages R = 8 image rows of x
+// ([8][46 padded positions][64 ci] fp32, halo zeros written once, 92 KB) and the same rows' pooled dY + argmax
+// ([8][10][128] fp32 + bytes, 50 KB) once per tile.  The GEMM's k is the tile's pixels, so the 7 taps are 7
+// shifted reads of the staged rows and one B fragment — unpooled at read time by a select on the argmax byte —
+// serves all 7.  8 waves: wave = co block w & 3 x ci half w >> 2, all 7 taps (7 accumulators on
+// v_mfma_f32_32x32x2_f32; lane half h supplies pixel 2 s + h of k-step s).  The next tile's rows load into
+// registers during this tile's MFMAs.  Each workgroup writes its partial dWt (and the column sums of dY over its
+// rows, the bias gradient) to its own slab, reduced in a fixed order afterwards: deterministic.  k order
+// (workgroup's tiles, row, pixel pair) — another fp32 summation order than the implicit GEMM's (tests: 1e-5).
+struct Row32WgArgs {
+  const float* x;       // [rows][WD][CI]
+  const float* dy;      // POOLED [rows][WD / 4][CO]
+  const uint8_t* arg;   // [rows][WD / 4][CO] window argmax
+  float* slab;          // [gridDim.x][KW * CI][CO]
+  float* bpart;         // [gridDim.x][CO], or null (no bias gradient)
+  int rows, groups;
+};
+template <int KW, int PW, int WD, int CI, int CO, int R>
+__global__ __launch_bounds__(512, 1) void conv_row32_wgrad_kernel(Row32WgArgs a) {
+  static_assert(CO == 128 && CI == 64 && WD % 4 == 0 && 2 * PW == KW - 1, "row32 wgrad geometry");
+  constexpr int NT = 512;
+  constexpr int WP = WD + 2 * PW;             // padded positions per staged row (46)
+  constexpr int PQ = WD / 4;                  // pooled positions per row (10)
+  constexpr int XCH = R * WD * (CI / 4);      // 16-B chunks of a tile's x rows (5120)
+  constexpr int XPT = XCH / NT;               // per thread (10)
+  constexpr int YCH = R * PQ * (CO / 4);      // 16-B chunks of the pooled dY rows (2560)
+  constexpr int YPT = YCH / NT;               // per thread (5)
+  constexpr int ACH = R * PQ * CO / 4;        // 4-B words of the argmax rows (2560)
+  constexpr int APT = ACH / NT;               // per thread (5)
+  static_assert(XCH % NT == 0 && YCH % NT == 0 && ACH % NT == 0, "row32 wgrad tile split");
+  __shared__ __attribute__((aligned(16))) float Xl[R * WP * CI];        // [row][pos][ci]
+  __shared__ __attribute__((aligned(16))) float Pl[R * PQ * CO];        // [row][q][co]
+  __shared__ __attribute__((aligned(16))) unsigned Al[R * PQ * CO / 4];  // bytes [row][q][co]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cb = wave & 3, hb = wave >> 2, lh = lane >> 5, lc = lane & 31;
+  for (int c = tid; c < R * 2 * PW * (CI / 4); c += NT) {   // the halo positions, once
+    const int rl = c / (2 * PW * (CI / 4)), rem = c % (2 * PW * (CI / 4));
+    const int pp = rem / (CI / 4), ch = rem % (CI / 4);
+    const int q = pp < PW ? pp : WD + pp;
+    *reinterpret_cast<v4f*>(Xl + (rl * WP + q) * CI + ch * 4) = v4f{0.f, 0.f, 0.f, 0.f};
+  }
+  v4f xr[XPT], yr[YPT];
+  unsigned ar[APT];
+  const auto rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x), (short)0, 0x7ffffff0, 0x00020000);
+  const auto rsY = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.dy), (short)0, 0x7ffffff0, 0x00020000);
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.arg), (short)0, 0x7ffffff0, 0x00020000);
+  constexpr int kOOB = (int)0x80000000u;   // past num_records: the load returns zeros
+  auto fetch = [&](int g) {   // tile g's rows into registers (past the last row: zeros)
+    const int real = a.rows - g * R;
+    const int sx = __builtin_amdgcn_readfirstlane(g * R * WD * CI * 4);
+    const int sy = __builtin_amdgcn_readfirstlane(g * R * PQ * CO * 4);
+    const int sa = __builtin_amdgcn_readfirstlane(g * R * PQ * CO);
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int c = tid + i * NT;
+      xr[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rsX, c < real * WD * (CI / 4) ? sx + c * 16 : kOOB,
+                                                                             0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) {
+      const int c = tid + i * NT;
+      yr[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rsY, c < real * PQ * (CO / 4) ? sy + c * 16 : kOOB,
+                                                                             0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int c = tid + i * NT;
+      ar[i] = __builtin_amdgcn_raw_buffer_load_b32(rsA, c < real * PQ * CO / 4 ? sa + c * 4 : kOOB, 0, 0);
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int c = tid + i * NT, rl = c / (WD * (CI / 4)), rem = c % (WD * (CI / 4));
+      const int px = rem / (CI / 4), ch = rem % (CI / 4);
+      *reinterpret_cast<v4f*>(Xl + (rl * WP + px + PW) * CI + ch * 4) = xr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) *reinterpret_cast<v4f*>(Pl + (tid + i * NT) * 4) = yr[i];
+#pragma unroll
+    for (int i = 0; i < APT; ++i) Al[tid + i * NT] = ar[i];
+  };
+  f32x16 acc[KW];
+#pragma unroll
+  for (int t = 0; t < KW; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  float bsum = 0.f;   // the column sum of dY at co = 32 cb + lc over this workgroup's rows (both lane halves)
+  const int col = cb * 32 + lc;
+  const float* xlane = Xl + lh * CI + hb * 32 + lc;   // + (row * WP + pixel pair base + tap) * CI
+  const uint8_t* abytes = reinterpret_cast<const uint8_t*>(Al);
+  int g = blockIdx.x;
+  if (g < a.groups) fetch(g);
+  while (g < a.groups) {
+    stage();
+    __syncthreads();
+    const int gn = g + (int)gridDim.x;
+    if (gn < a.groups) fetch(gn);   // lands during the MFMAs below
+#pragma unroll 1
+    for (int rl = 0; rl < R; ++rl) {
+      const float* xrow = xlane + rl * WP * CI;
+      const float* prow = Pl + rl * PQ * CO + col;
+      const uint8_t* arow = abytes + rl * PQ * CO + col;
+#pragma unroll
+      for (int q = 0; q < PQ; ++q) {
+        const float pv = prow[q * CO];
+        const int am = arow[q * CO];
+        bsum += pv;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {   // k-step: pixels 4 q + 2 s2 (lane half 0) and + 1 (half 1)
+          const float bv = am == 2 * s2 + lh ? pv : 0.f;
+          float av[KW];
+#pragma unroll
+          for (int t = 0; t < KW; ++t) av[t] = xrow[(4 * q + 2 * s2 + t) * CI];
+#pragma unroll
+          for (int t = 0; t < KW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t], bv, acc[t], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();   // every wave is done reading the tile before the next one is staged
+    g = gn;
+  }
+  float* sl = a.slab + (size_t)blockIdx.x * (KW * CI * CO);
+#pragma unroll
+  for (int t = 0; t < KW; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ci = hb * 32 + 8 * (r >> 2) + 4 * lh + (r & 3);
+      sl[(t * CI + ci) * CO + col] = acc[t][r];
+    }
+  if (a.bpart && hb == 0 && lh == 0) a.bpart[(size_t)blockIdx.x * CO + col] = bsum;
+}
+
 // The data gradient of the same conv: dX[w][ci] = sum over (kw, co) of dY[w + PW - kw][co] Wd[(kw,
 // co)][ci] — the implicit GEMM's k order, so bitwise its result.  dY (128 channels) has twice the bytes per staged
 // position, so the weights cannot stay resident beside 8 staged rows: the workgroup stages 8 rows of the dense 16-bit
@@ -2715,7 +2851,38 @@ int conv_bwd(const float* x, int64_t N, int64_t H, int64_t W, int64_t Ci, const 
     }
     if ((rc = srk::run_conv_gemm<srk::kDgrad>(d, s, "conv_dgrad"))) return rc;
   }
-  {
+  if (!d16[0] && prec == srk::kPrecF32 && srk::g_opt_conv_row32 && KH == 1 && KW == 7 && ph == 0 && pw == 3 &&
+      sh == 1 && sw == 1 && W == 40 && Ci == 64 && Co == 128 && dy && dy_arg && (N * H) < (1LL << 31) / (W * Ci * 4)) {
+    // fbanks_cnn conv2's weight gradient on fp32 operands from the pooled gradient + argmax: the row-staged kernel
+    // (conv_row32_wgrad_kernel), one slab per workgroup, reduced in order; the bias gradient from the same pass
+    const int64_t rows = N * H, groups = (rows + 7) / 8, G = std::min<int64_t>(groups, srk::kCUs);
+    const int64_t nslab = KW * Ci * Co;
+    float* slab = nullptr;
+    float* bpart = nullptr;
+    if ((rc = srk::conv_scratch((size_t)(G * nslab), &slab))) return rc;
+    if (db && (rc = srk::conv_scratch((size_t)(G * Co), &bpart, srk::g_csb))) return rc;
+    srk::Row32WgArgs ra{};
+    ra.x = x;
+    ra.dy = dy;
+    ra.arg = dy_arg;
+    ra.slab = slab;
+    ra.bpart = bpart;
+    ra.rows = (int)rows;
+    ra.groups = (int)groups;
+    {
+      srk::ProfScope prof("conv_wgrad", s, 2.0 * (double)(N * H * W) * (double)(KW * Ci) * (double)Co);
+      prof.detail("conv_row32_wgrad_kernel<unpool> %lldx%lldx%lld", (long long)(KW * Ci), (long long)Co,
+                  (long long)(N * H * W));
+      prof.bytes(4.0 * (double)(N * H * W) * Ci + 5.0 / 4.0 * (double)(N * H * W) * Co + 4.0 * (double)(G * nslab));
+      hipLaunchKernelGGL((srk::conv_row32_wgrad_kernel<7, 3, 40, 64, 128, 8>), dim3((unsigned)G), dim3(512), 0, s, ra);
+    }
+    srk::launch_splitk_sum(slab, (int)G, nslab, Co, nullptr, ws, s);
+    if (db)
+      hipLaunchKernelGGL(srk::colsum_blocks_kernel, dim3((unsigned)((Co + 63) / 64)), dim3(64 * srk::kCsWaves), 0, s,
+                         bpart, (int)G, (int)Co, db);
+    hipLaunchKernelGGL(srk::weight_grad_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, ws,
+                       (int)Co, (int)Ci, (int)KH, (int)KW, dw, dw_accumulate);
+  } else {
     srk::ConvArgs g = c;
     g.out = ws;   // dWt [(kh,kw,ci)][co], then re-laid out into dw
     g.M = KH * KW * Ci; g.Nn = Co; g.K = N * Ho * Wo;

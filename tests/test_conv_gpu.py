@@ -512,18 +512,22 @@ def test_conv_row32_equals_gemm(gpu, N):
             xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
             (snn._ConvPoolNHWCFn.apply(xm, wm, bm, (0, 3), 4) * gy).sum().backward()
             torch.cuda.synchronize()
-            used = any("conv_row32_dgrad" in e["kernel"] for e in _lib.prof_kernels())
+            ks = [e["kernel"] for e in _lib.prof_kernels()]
+            used = any("conv_row32_dgrad" in k for k in ks) and any("conv_row32_wgrad" in k for k in ks)
             _lib.prof_enable(False)
             grads.append((xm.grad, wm.grad, bm.grad, used))
     finally:
         _lib.set_option("conv_row32", 1)
         _lib.prof_enable(False)
     assert grads[0][3] and not grads[1][3]
-    for a_, c_ in zip(grads[0][1:3], grads[1][1:3]):
-        assert torch.isfinite(a_).all() and torch.equal(a_, c_)
+    # every gradient on the row-staged kernels (data: conv_row32_dgrad_kernel; weight and bias:
+    # conv_row32_wgrad_kernel, k = (workgroup's tiles, row, pixel pair), one slab per workgroup reduced in
+    # order) within 1e-5 of the implicit GEMM's (another fp32 summation order) and of float64 below
+    for a_, c_ in zip(grads[0][:3], grads[1][:3]):
+        a_, c_ = a_.double(), c_.double()
+        assert torch.isfinite(a_).all()
+        assert ((a_ - c_).abs().max() / c_.abs().max()).item() <= 1e-5
     dx1, dx0 = grads[0][0].double(), grads[1][0].double()
-    assert torch.isfinite(dx1).all()
-    assert ((dx1 - dx0).abs().max() / dx0.abs().max()).item() <= 1e-5
     # float64 reference of the data gradient: unpool through the argmax, then conv_transpose
     with torch.no_grad():
         xd = x.double().permute(0, 3, 1, 2)
@@ -533,4 +537,12 @@ def test_conv_row32_equals_gemm(gpu, N):
         am = win.argmax(-1, keepdim=True)
         dyd = torch.zeros_like(win).scatter_(-1, am, gy.double().permute(0, 3, 1, 2).unsqueeze(-1)).reshape(N, Co, H, W)
         dx64 = torch.nn.grad.conv2d_input(xd.shape, wd, dyd, padding=(0, 3)).permute(0, 2, 3, 1)
+        dw64 = torch.nn.grad.conv2d_weight(xd, wd.shape, dyd, padding=(0, 3))
+        db64 = dyd.sum((0, 2, 3))
     assert ((dx1 - dx64).abs().max() / dx64.abs().max()).item() <= 1e-5
+    for got, ref in ((grads[0][1].double(), dw64), (grads[0][2].double(), db64)):
+        assert ((got - ref).abs().max() / ref.abs().max()).item() <= 1e-5
+    # deterministic: the same inputs give the same bits (fixed tile -> workgroup map, slabs reduced in order)
+    xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
+    (snn._ConvPoolNHWCFn.apply(xm, wm, bm, (0, 3), 4) * gy).sum().backward()
+    assert torch.equal(wm.grad, grads[0][1]) and torch.equal(bm.grad, grads[0][2])

@@ -52,6 +52,11 @@ def _conv_group(name):
     m = re.search(r"conv_ring(16)?_kernel<(\d+)", name)
     if m:
         return modes[int(m.group(2))] + ("_lp" if m.group(1) else "")
+    # the row-staged fbanks_cnn conv2 kernels (conv.hip): fp32 = conv_row32_*, 16-bit = conv_row16_*
+    m = re.search(r"conv_row(16|32)_(pool|dgrad|wgrad)_kernel", name)
+    if m:
+        return {"pool": "conv_fwd", "dgrad": "conv_dgrad", "wgrad": "conv_wgrad"}[m.group(2)] + \
+            ("_lp" if m.group(1) == "16" else "")
     return None
 
 

@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256, 4) void fbank_kernel(const T* __restrict__ pcm
 #pragma unroll
       for (int u = 0; u < 5; ++u) tw[u] = s_tw[(g + u) * 16 + j];
 #pragma unroll
-      for (int u = 0; u < 5; ++u) tb[f * 272 + (g + u) * 17 + j] = cm2(a[g + u], tw[u]);
+      for (int u = 0; u < 5; ++u) tb[f * 272 + (g + u) * 17 + j] = pcmul(a[g + u], tw[u]);
     }
     wave_lds_fence();
     // pass B: lane = (f, k1): 16-point DFT over j -> Z[k1 + 16 k2]
@@ -174,21 +174,19 @@ __global__ __launch_bounds__(256, 4) void fbank_kernel(const T* __restrict__ pcm
       }
       __builtin_amdgcn_sched_barrier(0);
       float* pf = pb + f * 272;
-      auto two_bins = [&](float ax, float ay, float bx, float by, v2f w, int k) {
-        const float sx = ax + bx, sy = ay - by, ux = ay + by, uy = bx - ax;
-        const float wr = fmaf(w.x, ux, -(w.y * uy)), wi = fmaf(w.y, ux, w.x * uy);
-        const float r1 = sx + wr, i1 = sy + wi, r2 = sx - wr, i2 = sy - wi;
-        pf[256 - k] = 0.25f * fmaf(r2, r2, i2 * i2);   // first: bin 128 pairs with itself
-        pf[k] = 0.25f * fmaf(r1, r1, i1 * i1);
+      auto two_bins = [&](v2f A, v2f B, v2f w, int k) {
+        const v2f p = 0.25f * untangle_pk(A, B, w);
+        pf[256 - k] = p.y;   // first: bin 128 pairs with itself
+        pf[k] = p.x;
       };
 #pragma unroll
       for (int k2 = 0; k2 < 8; ++k2) {
         const float bx = j == 0 ? b[(16 - k2) & 15].x : Bx[k2];
         const float by = j == 0 ? b[(16 - k2) & 15].y : By[k2];
-        two_bins(b[k2].x, b[k2].y, bx, by, wpost[k2], j + 16 * k2);
+        two_bins(b[k2], v2f{bx, by}, wpost[k2], j + 16 * k2);
       }
       if (j == 0) {
-        two_bins(b[8].x, b[8].y, b[8].x, b[8].y, w128, 128);
+        two_bins(b[8], b[8], w128, 128);
         pf[0] = (float)(dc * dc);     // DC / Nyquist from the fp64 sums (the pre-emphasised DC bin
         pf[256] = (float)(ny * ny);   // cancels in fp32)
       }
@@ -338,7 +336,7 @@ __global__ __launch_bounds__(256, 4) void spec_kernel(const T* __restrict__ pcm,
     dft20v(a);
     if (fa < 3) {
 #pragma unroll
-      for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? cm2(a[k1], tw[k1 - 1]) : a[0];
+      for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? pcmul(a[k1], tw[k1 - 1]) : a[0];
     }
     wave_lds_fence();
     v2f b[16];
@@ -365,7 +363,7 @@ __global__ __launch_bounds__(256, 4) void spec_kernel(const T* __restrict__ pcm,
         const v2f Bz = tb[ff * 320 + (k == 0 ? 0 : 320 - k)];
         const v2f Bc = v2f{Bz.x, -Bz.y};
         const v2f e = 0.5f * (A + Bc), oo = mi2(0.5f * (A - Bc));
-        const v2f X = e + cm2(s_post[k], oo);
+        const v2f X = e + pcmul(oo, s_post[k]);
         float v = X.x * X.x + X.y * X.y;
         if (k == 0) v = (float)(dcf * dcf);
         if (k == 320) v = (float)(nyf * nyf);
@@ -568,7 +566,7 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const T* __rest
     dft20v(a);
     if (fa < 3) {
 #pragma unroll
-      for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? cm2(a[k1], tw[k1 - 1]) : a[0];
+      for (int k1 = 0; k1 < 20; ++k1) tb[fa * 340 + k1 * 17 + j] = k1 ? pcmul(a[k1], tw[k1 - 1]) : a[0];
     }
     MFCC_STAMP(0);
     {  // next: this clip's next chunk, else the next clip's first (past the end: a re-read)
@@ -617,20 +615,18 @@ __global__ __launch_bounds__(64 * kM3Waves, 2) void mfcc3_kernel(const T* __rest
     }
     __builtin_amdgcn_sched_barrier(0);   // keep the 24 requests ahead of their consumers
     float* pf = pb + fbw * 321;
-    auto two_bins = [&](float ax, float ay, float bx, float by, v2f w, int k) {
-      const float sx = ax + bx, sy = ay - by, ux = ay + by, uy = bx - ax;
-      const float wr = fmaf(w.x, ux, -(w.y * uy)), wi = fmaf(w.y, ux, w.x * uy);
-      const float r1 = sx + wr, i1 = sy + wi, r2 = sx - wr, i2 = sy - wi;
-      pf[320 - k] = fmaf(r2, r2, i2 * i2);   // first: bin 160 pairs with itself, |S + W U|^2 stands
-      pf[k] = fmaf(r1, r1, i1 * i1);
+    auto two_bins = [&](v2f A, v2f B, v2f w, int k) {
+      const v2f p = untangle_pk(A, B, w);
+      pf[320 - k] = p.y;   // first: bin 160 pairs with itself, |S + W U|^2 stands
+      pf[k] = p.x;
     };
 #pragma unroll
     for (int k2 = 0; k2 < 8; ++k2) {
       const float bx = k1b == 0 ? b[(16 - k2) & 15].x : Bx[k2];
       const float by = k1b == 0 ? b[(16 - k2) & 15].y : By[k2];
-      two_bins(b[k2].x, b[k2].y, bx, by, wpost[k2], k1b + 20 * k2);
+      two_bins(b[k2], v2f{bx, by}, wpost[k2], k1b + 20 * k2);
     }
-    if (k1b == 0) two_bins(b[8].x, b[8].y, b[8].x, b[8].y, w160, 160);
+    if (k1b == 0) two_bins(b[8], b[8], w160, 160);
     if (SRK_MFCC_STOP == 3) return;
     wave_lds_fence();
     MFCC_STAMP(2);

@@ -1908,8 +1908,9 @@ __global__ __launch_bounds__(512, 1) void conv_row32_pool_kernel(Row32Args a) {
     for (int kw = 0; kw < KW; ++kw) {
       fetch_w(kw + 1 < KW ? kw + 1 : 0);   // the next tap (tap 0 again for the next tile)
       const float* Ws = Wl[kw & 1];
-      // one 8-deep block's fragments at a time (a double-buffered prefetch spilled at 2 waves per SIMD: the
-      // other wave of the SIMD covers the LDS latency)
+      // one 8-deep block's fragments at a time (a double-buffered prefetch spilled at 2 waves per SIMD, and a 4-wave
+      // form with it — 512 registers, 10 row blocks per wave — measured slower, 2.35 vs 2.08 ms per cfg3 step, r06g:
+      // the other wave of the SIMD covers the LDS latency)
 #pragma unroll 1
       for (int kb = 0; kb < CI / 8; ++kb) {
         const float* q0 = Ws + (kb * 8 + 4 * lh) * CO + bcol;
@@ -2253,6 +2254,161 @@ __global__ __launch_bounds__(512, 1) void conv_row32_wgrad_kernel(Row32WgArgs a)
   if (a.bpart && hb == 0 && lh == 0) a.bpart[(size_t)blockIdx.x * CO + col] = bsum;
 }
 
+// The same weight gradient in 16-bit modes (option conv_row16): x's 16-bit copy (the forward's) and the pooled
+// gradient + argmax, unpooled and rounded to 16 bits at staging (the operand values of unpool16 + to16, without
+// the dense 16-bit dY in HBM).  v_mfma_f32_32x32x16 with k = 16 pixels per step: the A operand (x^T, m = ci) and
+// the B operand (dY, n = co) are both row-contiguous [pixel][channel] images read by ds_read_b64_tr_b16 — a lane
+// supplies the address of 4 channels at one pixel, so the 7 taps are 7 base offsets of the same staged rows
+// (each lane's pixel + tap, any alignment).  Images: x [8 rows][46 positions][96] (64 channels + 32 pad: the 4
+// pixels of a 16-lane read land on 4 distinct 16-bank spans) and dY [320 pixels][128] with 16-B units XOR'd by
+// (pixel & 3) << 2 (the ring kernels' TR swizzle).  The bias gradient: fp32 column sums of the pooled gradient
+// (before rounding), per thread over its fixed 4 channels, then in a fixed order through LDS.  One slab per
+// workgroup, reduced in order (deterministic).
+struct Row16WgArgs {
+  const unsigned short* x16;   // [rows][WD][CI] 16-bit
+  const float* dy;             // POOLED [rows][WD / 4][CO] fp32
+  const uint8_t* arg;          // [rows][WD / 4][CO]
+  float* slab;                 // [gridDim.x][KW * CI][CO]
+  float* bpart;                // [gridDim.x][CO], or null
+  int rows, groups;
+};
+template <int LP, int KW, int PW, int WD, int CI, int CO, int R>
+__global__ __launch_bounds__(512, 1) void conv_row16_wgrad_kernel(Row16WgArgs a) {
+  static_assert(CO == 128 && CI == 64 && WD % 8 == 0 && 2 * PW == KW - 1 && (R * WD) % 16 == 0, "row16 wgrad geometry");
+  constexpr int NT = 512;
+  constexpr int WP = WD + 2 * PW;             // padded positions per staged row (46)
+  constexpr int XP = CI + 32;                 // x image pitch per position (96 elements)
+  constexpr int PQ = WD / 4;                  // pooled positions per row (10)
+  constexpr int XCH = R * WD * (CI / 8);      // 16-B chunks of a tile's x16 rows (2560)
+  constexpr int XPT = XCH / NT;               // per thread (5)
+  constexpr int YCH = R * PQ * (CO / 4);      // 16-B chunks of the pooled dY rows (2560)
+  constexpr int YPT = YCH / NT;               // per thread (5)
+  constexpr int KS = R * WD / 16;             // k-steps per tile (20)
+  static_assert(XCH % NT == 0 && YCH % NT == 0 && NT % (CO / 4) == 0, "row16 wgrad tile split");
+  __shared__ __attribute__((aligned(16))) unsigned short Xl[R * WP * XP];   // [row][pos][96]
+  __shared__ __attribute__((aligned(16))) unsigned short Yl[R * WD * CO];   // [pixel][128], units swizzled
+  __shared__ float Bs[NT / (CO / 4)][CO];                                    // bias partials of the thread rows
+  using E4 = typename ConvLp<LP>::e4;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cb = wave & 3, hb = wave >> 2, lh = lane >> 5, lc = lane & 31;
+  for (int c = tid; c < R * 2 * PW * (CI / 8); c += NT) {   // the halo positions, once
+    const int rl = c / (2 * PW * (CI / 8)), rem = c % (2 * PW * (CI / 8));
+    const int pp = rem / (CI / 8), ch = rem % (CI / 8);
+    const int q = pp < PW ? pp : WD + pp;
+    *reinterpret_cast<u32x4_*>(Xl + (rl * WP + q) * XP + ch * 8) = u32x4_{0u, 0u, 0u, 0u};
+  }
+  u32x4_ xr[XPT];
+  v4f yr[YPT];
+  unsigned ar[YPT];
+  const auto rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(a.x16), (short)0, 0x7ffffff0, 0x00020000);
+  const auto rsY = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.dy), (short)0, 0x7ffffff0, 0x00020000);
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.arg), (short)0, 0x7ffffff0, 0x00020000);
+  constexpr int kOOB = (int)0x80000000u;
+  auto fetch = [&](int g) {   // tile g's rows into registers (past the last row: zeros)
+    const int real = a.rows - g * R;
+    const int sx = __builtin_amdgcn_readfirstlane(g * R * WD * CI * 2);
+    const int sy = __builtin_amdgcn_readfirstlane(g * R * PQ * CO * 4);
+    const int sa = __builtin_amdgcn_readfirstlane(g * R * PQ * CO);
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int c = tid + i * NT;
+      xr[i] = __builtin_bit_cast(u32x4_, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rsX, c < real * WD * (CI / 8) ? sx + c * 16 : kOOB, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) {
+      const int c = tid + i * NT;
+      const bool ok = c < real * PQ * (CO / 4);
+      yr[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rsY, ok ? sy + c * 16 : kOOB, 0, 0));
+      ar[i] = __builtin_amdgcn_raw_buffer_load_b32(rsA, ok ? sa + c * 4 : kOOB, 0, 0);
+    }
+  };
+  // dY unit swizzle: 16-B unit u (8 channels) of pixel p at slot u ^ ((p & 3) << 2)
+  auto yoff = [](int p, int n) { return p * CO + ((((n >> 3) ^ ((p & 3) << 2))) << 3) + (n & 7); };
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};   // channels 4 (tid % 32) .. + 3 (every chunk of this thread)
+  auto stage = [&]() {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int c = tid + i * NT, rl = c / (WD * (CI / 8)), rem = c % (WD * (CI / 8));
+      const int px = rem / (CI / 8), ch = rem % (CI / 8);
+      *reinterpret_cast<u32x4_*>(Xl + (rl * WP + px + PW) * XP + ch * 8) = xr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) {
+      const int c = tid + i * NT, rl = c / (PQ * (CO / 4)), rem = c % (PQ * (CO / 4));
+      const int q = rem / (CO / 4), n = (rem % (CO / 4)) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bsum[e] += yr[i][e];
+#pragma unroll
+      for (int pp = 0; pp < 4; ++pp) {   // the pooled value at the window position its argmax names, zeros elsewhere
+        v4f v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = ((ar[i] >> (8 * e)) & 0xFFu) == (unsigned)pp ? yr[i][e] : 0.f;
+        *reinterpret_cast<u32x2_*>(Yl + yoff(rl * WD + 4 * q + pp, n)) = __builtin_bit_cast(u32x2_, __builtin_convertvector(v, E4));
+      }
+    }
+  };
+  f32x16 acc[KW];
+#pragma unroll
+  for (int t = 0; t < KW; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  // this lane's tr16 addresses: 4 channels (m = 16 ((lane >> 4) & 1) + 4 (lane & 3) of its 32-block) at pixel
+  // 16 s + 8 lh + q of k-step s (q = (lane >> 2) & 3) and at + 4 (the fragment's upper half); an 8-pixel run never
+  // crosses a row (WD % 8 == 0), so both halves sit in the same staged row
+  const int q4 = (lane >> 2) & 3, mo = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  const unsigned short* xl = Xl + hb * 32 + mo;
+  const unsigned short* yl = Yl + yoff(8 * lh + q4, cb * 32 + mo);   // pixel 8 lh + q4; + 16 s pixels = 16 s * CO
+  int g = blockIdx.x;
+  if (g < a.groups) fetch(g);
+  while (g < a.groups) {
+    stage();
+    __syncthreads();
+    const int gn = g + (int)gridDim.x;
+    if (gn < a.groups) fetch(gn);   // lands during the MFMAs below
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int p0 = 16 * s + 8 * lh + q4;          // this lane's pixel (lower half)
+      const int pos = p0 + 2 * PW * (p0 / WD);       // its staged position (tap 0 = pixel - PW + PW)
+      const unsigned short* xb = xl + pos * XP;
+      const unsigned short* yb = yl + 16 * s * CO;   // (16 s) & 3 == 0: the same swizzle as pixel 8 lh + q4
+      const s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)yb);
+      const s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(yb + 4 * CO));
+      const u32x2_ b2l = __builtin_bit_cast(u32x2_, blo), b2h = __builtin_bit_cast(u32x2_, bhi);
+      const u32x4_ bf = u32x4_{b2l.x, b2l.y, b2h.x, b2h.y};
+#pragma unroll
+      for (int t = 0; t < KW; ++t) {
+        const s16x4 alo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xb + t * XP));
+        const s16x4 ahi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xb + (t + 4) * XP));
+        const u32x2_ l2 = __builtin_bit_cast(u32x2_, alo), h2 = __builtin_bit_cast(u32x2_, ahi);
+        acc[t] = ConvLp<LP>::mma(u32x4_{l2.x, l2.y, h2.x, h2.y}, bf, acc[t]);
+      }
+    }
+    __syncthreads();   // every wave is done reading the tile before the next one is staged
+    g = gn;
+  }
+  float* sl = a.slab + (size_t)blockIdx.x * (KW * CI * CO);
+#pragma unroll
+  for (int t = 0; t < KW; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ci = hb * 32 + 8 * (r >> 2) + 4 * lh + (r & 3);
+      sl[(t * CI + ci) * CO + cb * 32 + lc] = acc[t][r];
+    }
+  if (a.bpart) {   // the 16 thread rows sharing channels 4 (tid % 32) .. + 3, added in row order
+#pragma unroll
+    for (int e = 0; e < 4; ++e) Bs[tid / (CO / 4)][(tid % (CO / 4)) * 4 + e] = bsum[e];
+    __syncthreads();
+    if (tid < CO) {
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < NT / (CO / 4); ++r) t += Bs[r][tid];
+      a.bpart[(size_t)blockIdx.x * CO + tid] = t;
+    }
+  }
+}
+
 // The data gradient of the same conv: dX[w][ci] = sum over (kw, co) of dY[w + PW - kw][co] Wd[(kw,
 // co)][ci] — the implicit GEMM's k order, so bitwise its result.  dY (128 channels) has twice the bytes per staged
 // position, so the weights cannot stay resident beside 8 staged rows: the workgroup stages 8 rows of the dense 16-bit
@@ -2264,11 +2420,16 @@ struct RowDgArgs {
   const unsigned short* wd16;   // [(kw, co)][CN] 16-bit (the dgrad weight matrix Wd)
   float* dx;                    // [rows][W][CN]
   int rows, groups;
+  const float* dyp;             // POOLED: [rows][W / 4][CA] fp32 pooled gradient (instead of dy16) ...
+  const uint8_t* argp;          // ... and its window argmax, unpooled and rounded to 16 bits at staging
 };
 // BAL (option conv_row16_dgrad = 2): the 20 (row block, column block) units of the tile 5 per wave instead —
 // wave w owns units 5w .. 5w + 4 (unit u = row block u / 2, column block u % 2): 3 A + 2 B fragment reads per 5
 // MFMAs, every SIMD the same MFMA count (the 3 / 3 / 2 / 2 split leaves two SIMDs idle 1/3 of each k-step).
-template <int LP, int KW, int PW, int WD, int CA, int CN, int R, bool BAL = false>
+// POOLED: dY arrives as the pooled gradient + argmax (fbanks_cnn's pooled backward) and is unpooled and rounded at
+// staging — the staged values bitwise those of unpool16 + to16 (the same conversion), without the dense 16-bit dY in
+// HBM (and without the pass that writes it).
+template <int LP, int KW, int PW, int WD, int CA, int CN, int R, bool BAL = false, bool POOLED = false>
 __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
   static_assert(CA == 128 && CN == 64 && (R * WD) % 32 == 0 && 2 * PW == KW - 1, "row16 dgrad geometry");
   constexpr int WP = WD + 2 * PW;
@@ -2290,27 +2451,67 @@ __global__ __launch_bounds__(256, 1) void conv_row16_dgrad_kernel(RowDgArgs a) {
     const int q = pp < PW ? pp : WD + pp;
     *reinterpret_cast<u32x4_*>(Yl + (rl * WP + q) * CA + ((ch ^ (q & 15)) * 8)) = u32x4_{0u, 0u, 0u, 0u};
   }
-  u32x4_ yr[XPT], wr[TPT];
+  constexpr int PCH = R * (WD / 4) * (CA / 4);   // POOLED: 16-B chunks of the pooled fp32 rows (2560)
+  constexpr int PPT = PCH / 256;                  // per thread (10)
+  static_assert(!POOLED || (PCH % 256 == 0 && WD % 4 == 0), "row16 dgrad pooled tile split");
+  u32x4_ yr[POOLED ? 1 : XPT], wr[TPT];
+  v4f pr[POOLED ? PPT : 1];
+  unsigned par[POOLED ? PPT : 1];
   // the loads take 32-bit buffer offsets (past the last row -> 16 zero bytes): 64-bit addresses of the 20 + 4 loads,
   // hoisted out of the loops, spilled; the epilogue stores 32-bit offsets off the tile's base pointer
   const auto rsY = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(a.dy16), (short)0, 0x7ffffff0, 0x00020000);
   const auto rsW = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(a.wd16), (short)0, 0x7ffffff0, 0x00020000);
+  const auto rsP = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(POOLED ? a.dyp : nullptr), (short)0, 0x7ffffff0,
+                                                     0x00020000);
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(POOLED ? a.argp : nullptr), (short)0,
+                                                     0x7ffffff0, 0x00020000);
   auto fetch_y = [&](int g) {
-    const int last = (a.rows - g * R) * WD * (CA / 8);   // chunks of real rows in this tile
-    const int sbase = __builtin_amdgcn_readfirstlane(g * R * WD * CA * 2);
+    if constexpr (POOLED) {
+      const int lastp = (a.rows - g * R) * (WD / 4) * (CA / 4);
+      const int sp = __builtin_amdgcn_readfirstlane(g * R * (WD / 4) * CA * 4);
+      const int sa = __builtin_amdgcn_readfirstlane(g * R * (WD / 4) * CA);
 #pragma unroll
-    for (int i = 0; i < XPT; ++i) {
-      const int c = tid + i * 256;
-      yr[i] = __builtin_bit_cast(u32x4_, __builtin_amdgcn_raw_buffer_load_b128(
-                                              rsY, c < last ? sbase + c * 16 : (int)0x80000000u, 0, 0));
+      for (int i = 0; i < PPT; ++i) {
+        const int c = tid + i * 256;
+        const bool ok = c < lastp;
+        pr[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rsP, ok ? sp + c * 16 : (int)0x80000000u, 0, 0));
+        par[i] = __builtin_amdgcn_raw_buffer_load_b32(rsA, ok ? sa + c * 4 : (int)0x80000000u, 0, 0);
+      }
+    } else {
+      const int last = (a.rows - g * R) * WD * (CA / 8);   // chunks of real rows in this tile
+      const int sbase = __builtin_amdgcn_readfirstlane(g * R * WD * CA * 2);
+#pragma unroll
+      for (int i = 0; i < XPT; ++i) {
+        const int c = tid + i * 256;
+        yr[i] = __builtin_bit_cast(u32x4_, __builtin_amdgcn_raw_buffer_load_b128(
+                                                rsY, c < last ? sbase + c * 16 : (int)0x80000000u, 0, 0));
+      }
     }
   };
   auto stage_y = [&]() {
+    if constexpr (POOLED) {
+      using E4 = typename ConvLp<LP>::e4;
 #pragma unroll
-    for (int i = 0; i < XPT; ++i) {
-      const int c = tid + i * 256, rl = c / (WD * (CA / 8)), rem = c % (WD * (CA / 8));
-      const int px = rem / (CA / 8), ch = rem % (CA / 8), q = px + PW;
-      *reinterpret_cast<u32x4_*>(Yl + (rl * WP + q) * CA + ((ch ^ (q & 15)) * 8)) = yr[i];
+      for (int i = 0; i < PPT; ++i) {
+        const int c = tid + i * 256, rl = c / ((WD / 4) * (CA / 4)), rem = c % ((WD / 4) * (CA / 4));
+        const int q4 = rem / (CA / 4), n = (rem % (CA / 4)) * 4, ch = n >> 3;
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {   // the pooled value at the position its argmax names, zeros elsewhere
+          const int q = 4 * q4 + pp + PW;
+          v4f v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = ((par[i] >> (8 * e)) & 0xFFu) == (unsigned)pp ? pr[i][e] : 0.f;
+          *reinterpret_cast<u32x2_*>(Yl + (rl * WP + q) * CA + ((ch ^ (q & 15)) * 8) + (n & 4)) =
+              __builtin_bit_cast(u32x2_, __builtin_convertvector(v, E4));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < XPT; ++i) {
+        const int c = tid + i * 256, rl = c / (WD * (CA / 8)), rem = c % (WD * (CA / 8));
+        const int px = rem / (CA / 8), ch = rem % (CA / 8), q = px + PW;
+        *reinterpret_cast<u32x4_*>(Yl + (rl * WP + q) * CA + ((ch ^ (q & 15)) * 8)) = yr[i];
+      }
     }
   };
   auto fetch_w = [&](int kw) {
@@ -2475,7 +2676,21 @@ int try_conv_ring(ConvArgs& c, hipStream_t s, const char* name, float* final_out
   if (xb >= 2.1e9 || yb >= 2.1e9 || wb >= 2.1e9) return 1;
   const int BN = c.Nn >= 256 ? 256 : 128;
   const int64_t tm = (c.M + 255) / 256, tn = (c.Nn + BN - 1) / BN;
-  const int splits0 = choose_splits(tm * tn, c.K, RBK, kCUs, MODE == kWgrad ? 256 : 16);
+  int splits0 = choose_splits(tm * tn, c.K, RBK, kCUs, MODE == kWgrad ? 256 : 16);
+  if (MODE != kWgrad && splits0 > 1) {
+    // a split forward / data gradient writes and re-reads its full-size output once per split (the slabs)
+    // before the reduction writes it: keep the split only where the MFMA rounds it saves outweigh that traffic
+    // (fbanks_cnn conv4's 16-bit forward, 50176 x 512 x 1792: 392 tiles, 181 us on 784 half-K blocks + a 91 us
+    // slab reduction vs ~180 us unsplit; the fp32 ResNet layers keep theirs).  Rates: the ring kernels' measured
+    // ~0.5 PF (16-bit) / ~0.11 PF (fp32), ~4 TB/s for the slab traffic.
+    const double rate = lp ? 0.5e15 : 0.11e15, flops = 2.0 * (double)c.M * (double)c.Nn * (double)c.K;
+    auto t_of = [&](int64_t sp) {
+      const int64_t w = tm * tn * sp, rounds = (w + kCUs - 1) / kCUs;
+      const double eff = (double)w / (double)(rounds * kCUs);
+      return flops / (eff * rate) + (sp > 1 ? 2.0 * sp * 4.0 * (double)c.M * (double)c.Nn / 4e12 : 0.0);
+    };
+    if (t_of(1) <= t_of(splits0)) splits0 = 1;
+  }
   c.kchunk = splits0 > 1 ? ((c.K + splits0 - 1) / splits0 + RBK - 1) / RBK * RBK : std::max<int64_t>(c.K, 1);
   const int splits = splits0 > 1 ? (int)((c.K + c.kchunk - 1) / c.kchunk) : 1;
   c.tiles_m = (int)tm;
@@ -2659,6 +2874,82 @@ int run_conv_gemm(ConvArgs c, hipStream_t s, const char* name) {
   return SRK_OK;
 }
 
+// fbanks_cnn conv2's pooled backward in 16-bit modes (options conv_row16 and conv_row16_dgrad on): both gradients on
+// the row-staged kernels straight from the pooled gradient + argmax — the data gradient (conv_row16_dgrad_kernel
+// <POOLED>) and the weight gradient (conv_row16_wgrad_kernel, one slab per workgroup reduced in order, the bias sums
+// in the same pass) unpool and round dY at staging, so the dense 16-bit dY (and the pass that writes it with the
+// bias sums, colsum8 / unpool16) is never made.  x's 16-bit copy is the forward's when it kept one.
+int conv2_bwd16_pooled(const float* x, int64_t N, int64_t H, const float* w, const float* dyp, const uint8_t* arg,
+                       float* dx, float* dw, float* db, float* ws, const void* x16, hipStream_t s) {
+  constexpr int64_t W = 40, Ci = 64, Co = 128, KH = 1, KW = 7;
+  const int prec = matmul_prec();
+  const int64_t nw = Co * Ci * KH * KW, rows = N * H, groups = (rows + 7) / 8;
+  int rc;
+  if (dx)
+    hipLaunchKernelGGL(weight_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, (int)Co, (int)Ci,
+                       (int)KH, (int)KW, 1, ws);
+  unsigned short* d16[2] = {static_cast<unsigned short*>(const_cast<void*>(x16)), nullptr};   // x, Wd
+  {
+    const float* src[2] = {x, ws};
+    const int64_t n[2] = {rows * W * Ci, nw};
+    const bool ready[2] = {x16 != nullptr, false};
+    if ((rc = to16_all(prec, src, n, dx ? 2 : 1, d16, s, ready))) return rc;
+  }
+  if (dx) {
+    RowDgArgs ra{};
+    ra.wd16 = d16[1];
+    ra.dx = dx;
+    ra.rows = (int)rows;
+    ra.groups = (int)groups;
+    ra.dyp = dyp;
+    ra.argp = arg;
+    ProfScope prof("conv_dgrad_lp", s, 2.0 * (double)(rows * W) * (double)Ci * (double)(KW * Co));
+    prof.detail("conv_row16_dgrad_kernel<unpool> %lldx%lldx%lld", (long long)(rows * W), (long long)Ci, (long long)(KW * Co));
+    prof.bytes(5.0 / 4.0 * (double)(rows * W) * Co + 2.0 * (double)(KW * Co) * Ci + 4.0 * (double)(rows * W) * Ci);
+    const dim3 grid((unsigned)std::min<int64_t>(groups, kCUs)), block(256);
+    const bool bal = g_opt_conv_row16_dgrad == 2;
+    if (prec == kPrecBF16 && bal)
+      hipLaunchKernelGGL((conv_row16_dgrad_kernel<1, 7, 3, 40, 128, 64, 8, true, true>), grid, block, 0, s, ra);
+    else if (prec == kPrecBF16)
+      hipLaunchKernelGGL((conv_row16_dgrad_kernel<1, 7, 3, 40, 128, 64, 8, false, true>), grid, block, 0, s, ra);
+    else if (bal)
+      hipLaunchKernelGGL((conv_row16_dgrad_kernel<2, 7, 3, 40, 128, 64, 8, true, true>), grid, block, 0, s, ra);
+    else
+      hipLaunchKernelGGL((conv_row16_dgrad_kernel<2, 7, 3, 40, 128, 64, 8, false, true>), grid, block, 0, s, ra);
+    SRK_CHECK_HIP(hipGetLastError());
+  }
+  const int64_t G = std::min<int64_t>(groups, kCUs), nslab = KW * Ci * Co;
+  float* slab = nullptr;
+  float* bpart = nullptr;
+  if ((rc = conv_scratch((size_t)(G * nslab), &slab))) return rc;
+  if (db && (rc = conv_scratch((size_t)(G * Co), &bpart, g_csb))) return rc;
+  Row16WgArgs wa{};
+  wa.x16 = d16[0];
+  wa.dy = dyp;
+  wa.arg = arg;
+  wa.slab = slab;
+  wa.bpart = bpart;
+  wa.rows = (int)rows;
+  wa.groups = (int)groups;
+  {
+    ProfScope prof("conv_wgrad_lp", s, 2.0 * (double)(rows * W) * (double)(KW * Ci) * (double)Co);
+    prof.detail("conv_row16_wgrad_kernel<unpool> %lldx%lldx%lld", (long long)(KW * Ci), (long long)Co, (long long)(rows * W));
+    prof.bytes(2.0 * (double)(rows * W) * Ci + 5.0 / 4.0 * (double)(rows * W) * Co + 4.0 * (double)(G * nslab));
+    if (prec == kPrecBF16)
+      hipLaunchKernelGGL((conv_row16_wgrad_kernel<1, 7, 3, 40, 64, 128, 8>), dim3((unsigned)G), dim3(512), 0, s, wa);
+    else
+      hipLaunchKernelGGL((conv_row16_wgrad_kernel<2, 7, 3, 40, 64, 128, 8>), dim3((unsigned)G), dim3(512), 0, s, wa);
+  }
+  launch_splitk_sum(slab, (int)G, nslab, Co, nullptr, ws, s);
+  if (bpart)
+    hipLaunchKernelGGL(colsum_blocks_kernel, dim3((unsigned)((Co + 63) / 64)), dim3(64 * kCsWaves), 0, s, bpart, (int)G,
+                       (int)Co, db);
+  hipLaunchKernelGGL(weight_grad_layout_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, ws, (int)Co,
+                     (int)Ci, (int)KH, (int)KW, dw, 0);
+  SRK_CHECK_HIP(hipGetLastError());
+  return SRK_OK;
+}
+
 int check(int64_t N, int64_t H, int64_t W, int64_t Ci, int64_t Co, int64_t KH, int64_t KW, int64_t ph, int64_t pw,
           int64_t sh, int64_t sw, int64_t* Ho, int64_t* Wo) {
   SRK_REQUIRE(N > 0 && H > 0 && W > 0 && Ci > 0 && Co > 0 && KH > 0 && KW > 0 && ph >= 0 && pw >= 0 && sh > 0 && sw > 0,
@@ -2702,11 +2993,29 @@ int srk_conv2d_nhwc_fwd16(const float* x, int64_t N, int64_t H, int64_t W, int64
   c.KH = (int)KH; c.KW = (int)KW; c.ph = (int)ph; c.pw = (int)pw; c.sh = (int)sh; c.sw = (int)sw;
   c.x = x; c.wmat = ws; c.out = y; c.bias = bias;
   c.M = N * Ho * Wo; c.Nn = Co; c.K = KH * KW * Ci;
+  // A full-width "valid" conv (model_fbanks_cnn.py:74, conv3 (1, 10) on width 10) is the plain GEMM
+  //   Y[(n,h)][co] = X[(n,h)][(kw,ci)] . Wt[(kw,ci)][co] + bias
+  // (x rows are already the GEMM rows: no gather, no split-K slabs of the implicit GEMM's tall 2-tile-wide grid)
+  const bool full_width = KH == 1 && ph == 0 && pw == 0 && sh == 1 && KW == W && Wo == 1 && srk::g_opt_conv_fw_gemm;
+  auto fw_gemm = [&](const unsigned short* a16, const unsigned short* b16, const char* cat) -> int {
+    srk::GemmDesc g;
+    g.M = N * H; g.N = Co; g.K = KW * Ci;
+    g.A = x; g.lda = KW * Ci;
+    g.B = ws; g.ldb = Co;
+    g.C = y; g.ldc = Co;
+    g.bias = bias; g.bias_mode = bias ? 1 : 0;
+    g.A16 = a16; g.B16 = b16;
+    srk::ProfScope prof(cat, s, 2.0 * (double)g.M * (double)g.N * (double)g.K);
+    prof.detail("conv_fwd_as_gemm %lldx%lldx%lld", (long long)g.M, (long long)g.N, (long long)g.K);
+    prof.bytes((a16 ? 2.0 : 4.0) * ((double)g.M * g.K + (double)g.K * g.N) + 4.0 * (double)g.M * g.N);
+    return srk::gemm_f32(g, s);
+  };
   if (srk::g_opt_conv_fwd_fp32 && srk::matmul_prec() != srk::kPrecF32) {
     // the faithful 16-bit mode: this forward on fp32 operands; a producer's 16-bit copy of x stays the
     // backward's (its weight gradient runs 16-bit)
     if (x16_ready && x16_written) *x16_written = 1;
     srk::PrecScope fp32(srk::kPrecF32);
+    if (full_width) return fw_gemm(nullptr, nullptr, "conv_fwd");
     return srk::run_conv_gemm<srk::kFwd>(c, s, "conv_fwd");
   }
   const int prec = srk::matmul_prec();
@@ -2720,6 +3029,7 @@ int srk_conv2d_nhwc_fwd16(const float* x, int64_t N, int64_t H, int64_t W, int64
     c.b16 = d16[1];
     if (x16 && x16_written) *x16_written = 1;
   }
+  if (full_width) return fw_gemm(c.a16, c.b16, prec == srk::kPrecF32 ? "conv_fwd" : "conv_fwd_lp");
   return srk::run_conv_gemm<srk::kFwd>(c, s, "conv_fwd");
   SRK_API_END
 }
@@ -3044,6 +3354,11 @@ int srk_conv2d_nhwc_bwd_pool(const float* x, int64_t N, int64_t H, int64_t W, in
   const int64_t rows = N * Ho * Wo / pool_w;
   const int prec = srk::matmul_prec();
   if (srk::g_opt_conv_unpool16 && !full_width && Co % 8 == 0 && srk::s16_ok(prec, Ci, Co, {x, w, x16, ws})) {
+    // fbanks_cnn conv2 (Conv2d(64, 128, (1, 7), padding (0, 3)) over W = 40 + MaxPool2d((1, 4))): both gradients from
+    // the pooled gradient on the row-staged kernels, no dense dY
+    if (srk::g_opt_conv_row16 && srk::g_opt_conv_row16_dgrad && KH == 1 && KW == 7 && ph == 0 && pw == 3 && W == 40 &&
+        Ci == 64 && Co == 128 && dw && (N * H) < (1LL << 30) / (W * Co))
+      return srk::conv2_bwd16_pooled(x, N, H, w, dy_pooled, argmax, dx, dw, db, ws, x16, s);
     // 16-bit-source modes: the dense dY straight as its 16-bit copy, the bias gradient from the pooled
     // gradient (each pooled value sits once in the dense dY, the rest are zeros), then the backward
     float* d = nullptr;

@@ -32,6 +32,7 @@ int g_opt_conv_ring_qs = 6;
 int g_opt_conv_fast16 = 1;
 int g_opt_conv_row16 = 1;
 int g_opt_conv_row32 = 1;
+int g_opt_conv_fw_gemm = 1;
 int g_opt_conv_row16_dgrad = 2;
 int g_opt_bn_tree = 0;
 int g_opt_mfcc_variant = 3;
@@ -409,6 +410,10 @@ int srk_set_option(const char* name, int64_t value) {
   }
   if (n == "conv_row32") {   // fbanks conv2 on fp32 operands: row-staged kernels (1) or the implicit GEMM (0)
     srk::g_opt_conv_row32 = value != 0;
+    return SRK_OK;
+  }
+  if (n == "conv_fw_gemm") {   // full-width "valid" conv forward as a plain GEMM (1) or the implicit GEMM (0)
+    srk::g_opt_conv_fw_gemm = value != 0;
     return SRK_OK;
   }
   if (n == "conv_fast16") {   // 16-bit-source register-staged convs: uniform-tap fast gathers (1) or generic (0)

@@ -138,6 +138,9 @@ extern int g_opt_conv_row16;
 // fbanks_cnn conv2 (+ maxpool2) on fp32 operands on the row-staged kernels (x rows staged once per tile, the weights
 // streamed one tap at a time) ("conv_row32", default 1; 0 = the implicit-GEMM kernels)
 extern int g_opt_conv_row32;
+// a full-width "valid" conv's forward (fbanks_cnn conv3, (1, 10) over width 10) as the plain GEMM x . Wt + bias
+// ("conv_fw_gemm", default 1; 0 = the implicit GEMM)
+extern int g_opt_conv_fw_gemm;
 // the row-staged data gradient of the same conv ("conv_row16_dgrad", default 2 = 5 units per wave; 1 = 3 / 3 / 2 / 2
 // row blocks per wave, 418 vs 475-485 us, r05p; 0 = the implicit GEMM)
 extern int g_opt_conv_row16_dgrad;

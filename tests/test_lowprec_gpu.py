@@ -794,7 +794,9 @@ def test_conv_row16_equals_gemm(prec, N, form):
             xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
             (snn._ConvPoolNHWCFn.apply(xm, wm, bm, (0, 3), 4) * gy).sum().backward()
             torch.cuda.synchronize()
-            grads.append((xm.grad, wm.grad, bm.grad, any("conv_row16_dgrad" in e["kernel"] for e in _lib.prof_kernels())))
+            ks = [e["kernel"] for e in _lib.prof_kernels()]
+            grads.append((xm.grad, wm.grad, bm.grad, any("conv_row16_dgrad" in k for k in ks),
+                          any("conv_row16_wgrad" in k for k in ks)))
             _lib.prof_enable(False)
             xm, wm, bm = (t.clone().requires_grad_(True) for t in (x, w, b))
             (snn._Conv2dNHWCFn.apply(xm, wm, bm, (0, 3), (1, 1)) * gd).sum().backward()
@@ -804,6 +806,13 @@ def test_conv_row16_equals_gemm(prec, N, form):
         _lib.set_option("conv_row16", 1)
         _lib.set_option("conv_row16_dgrad", 2)
         _lib.prof_enable(False)
-    assert grads[0][3] and not grads[1][3]
-    for a_, c_ in list(zip(grads[0][:3], grads[1][:3])) + list(zip(*dense)):
+    assert grads[0][3] and not grads[1][3] and grads[0][4] and not grads[1][4]
+    # the data gradient and the dense-dY conv's gradients bitwise; the pooled conv's weight and bias gradients on
+    # the row-staged conv_row16_wgrad_kernel (the same 16-bit operands — x's copy, dY unpooled and rounded at
+    # staging — in another fp32 summation order: workgroup slabs reduced in order) within 1e-5 of the implicit GEMM's
+    for a_, c_ in [(grads[0][0], grads[1][0])] + list(zip(*dense)):
         assert torch.isfinite(a_).all() and torch.equal(a_, c_)
+    for a_, c_ in zip(grads[0][1:3], grads[1][1:3]):
+        a_, c_ = a_.double(), c_.double()
+        assert torch.isfinite(a_).all()
+        assert ((a_ - c_).abs().max() / c_.abs().max()).item() <= 1e-5

@@ -1,6 +1,7 @@
 #!/bin/bash
 # One conv change on the GPU:  gpurun --timeout 900 -- bash tools/gpu_conv_check.sh TAG "test files" ["-k expression"]
-# the selected tests, then rocprofv3 kernel stats of the cfg3 fp32 and bf16 bench commands (graph replays).
+# the selected tests, then rocprofv3 kernel stats of the cfg3 fp32 and bf16 bench commands (graph replays);
+# AB_OPTS="opt=v,...": a third cfg3 fp32 run with those srk options (SRK_OPTIONS).
 set -o pipefail
 TAG=${1:-conv}
 SEL=${2:-tests/test_conv_gpu.py}
@@ -21,4 +22,5 @@ rc=$?
 echo "pytest rc=$rc: $(tail -1 $OUT/pytest.log)"
 [ $rc -eq 0 ] || exit $rc
 stats cfg3 --model fbanks_cnn --no-lowprec --steps 10 && echo "cfg3: $(tail -c 300 $OUT/stats_cfg3.json | head -c 200)" \
-  && stats cfg3b --model fbanks_cnn --precision bf16 --no-lowprec --steps 10 && echo "stats ok"
+  && stats cfg3b --model fbanks_cnn --precision bf16 --no-lowprec --steps 10 \
+  && { [ -z "$AB_OPTS" ] || SRK_OPTIONS="$AB_OPTS" stats cfg3ab --model fbanks_cnn --no-lowprec --steps 10; } && echo "stats ok"

@@ -17,6 +17,10 @@
 //  16  partner on another XCD (blocks 0 and 1) instead of the same XCD (blocks 0 and 8)
 //  32  pipelined polls: four flag loads in flight (issued ~64 clk apart), each checked as it returns
 //      (vmcnt retires in order), instead of one load -> wait -> check -> sleep at a time
+//  64  tagged payload (round 6, VERDICT r05 "next" #3): the step number rides in the last dword of every
+//      lane's 16-B chunk, written by the chunk's one 16-B store; every lane polls its own chunk with an sc1
+//      16-B load until the tag says `need` (__all over the wave), so the poll IS the payload load — no flag
+//      store, no vmcnt(0) drain before it, no second L2 round trip.  The floor a tagged hand-off would have.
 // Every spin is bounded (a hop that waits > ~1 s gives up and the run reports it), and every
 // workgroup of the grid reaches the end.
 #include <hip/hip_runtime.h>
@@ -39,7 +43,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rs(const void* p) {
 template <int V>
 __global__ __launch_bounds__(256) void pingpong(unsigned* flags, float* payload, unsigned long long* out, int iters,
                                                 unsigned* failed) {
-  constexpr bool WT = V & 1, NOSLEEP = V & 2, NOPAY = V & 4, FOURW = V & 8, CROSS = V & 16, PIPE = V & 32;
+  constexpr bool WT = V & 1, NOSLEEP = V & 2, NOPAY = V & 4, FOURW = V & 8, CROSS = V & 16, PIPE = V & 32, TAG = V & 64;
   const int partner = CROSS ? 1 : 8;
   const int role = blockIdx.x == 0 ? 0 : blockIdx.x == partner ? 1 : -1;
   if (role < 0) return;
@@ -57,6 +61,27 @@ __global__ __launch_bounds__(256) void pingpong(unsigned* flags, float* payload,
   for (int i = 0; i < iters; ++i) {
     // wait: role 0 waits for the partner's step i (none at i = 0), role 1 for step i + 1
     const unsigned need = role == 0 ? (unsigned)i : (unsigned)(i + 1);
+    if constexpr (TAG) {   // every wave polls its own chunks: the load that sees the tag carries the payload
+      const unsigned off = (unsigned)((wave * 64 + lane) * 16);
+      v4f x = {0.f, 0.f, 0.f, 0.f};
+      if (need > 0) {
+        unsigned spins = 0;
+        while (true) {
+          x = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rother, (int)off, 0, kSc1));
+          if (__all(__float_as_uint(x.w) >= need)) break;
+          if (!NOSLEEP) __builtin_amdgcn_s_sleep(1);
+          if (++spins >= kSpin) {
+            if (lane == 0) bad = 1;
+            break;
+          }
+        }
+      }
+      if (bad) break;
+      acc += v4f{x.x, x.y, x.z, 0.f};
+      const v4f v = {(float)i, acc.x, acc.y, __uint_as_float((unsigned)(i + 1))};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rmy, (int)off, 0, WT ? kSc1 : 0);
+      continue;
+    }
     if (need > 0) {
       if (wave == 0 && PIPE) {
         unsigned spins = 0;
@@ -166,6 +191,10 @@ int main() {
       {32, "pipelined polls, plain payload+flag (XCD-local)"},
       {40, "pipelined polls, 4 waves + barriers, plain (XCD-local)"},
       {49, "pipelined polls, write-through, other XCD"},
+      {64, "tagged payload (poll = load), XCD-local, sleep"},
+      {66, "tagged payload (poll = load), XCD-local, no sleep"},
+      {72, "tagged payload, 4 waves, XCD-local, sleep"},
+      {81, "tagged payload, write-through, other XCD, sleep"},
   };
   for (auto& e : vs) {
     unsigned xcc[2] = {99, 99};
@@ -184,6 +213,10 @@ int main() {
       case 32: ns = run<32>(flags, pay, out, failed, iters, xcc); break;
       case 40: ns = run<40>(flags, pay, out, failed, iters, xcc); break;
       case 49: ns = run<49>(flags, pay, out, failed, iters, xcc); break;
+      case 64: ns = run<64>(flags, pay, out, failed, iters, xcc); break;
+      case 66: ns = run<66>(flags, pay, out, failed, iters, xcc); break;
+      case 72: ns = run<72>(flags, pay, out, failed, iters, xcc); break;
+      case 81: ns = run<81>(flags, pay, out, failed, iters, xcc); break;
     }
     std::printf("variant %2d  %-55s  %8.1f ns/hop  (xcc %u / %u)\n", e.v, e.what, ns, xcc[0], xcc[1]);
   }

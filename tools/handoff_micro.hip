@@ -67,6 +67,9 @@ __global__ __launch_bounds__(256) void pingpong(unsigned* flags, float* payload,
       if (need > 0) {
         unsigned spins = 0;
         while (true) {
+          // the memory clobber re-issues the load every spin (the same sc1 load as the payload reads; it is not
+          // hoisted as loop-invariant)
+          asm volatile("" ::: "memory");
           x = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rother, (int)off, 0, kSc1));
           if (__all(__float_as_uint(x.w) >= need)) break;
           if (!NOSLEEP) __builtin_amdgcn_s_sleep(1);
@@ -169,6 +172,7 @@ double run(unsigned* flags, float* pay, unsigned long long* out, unsigned* faile
 }
 
 int main() {
+  std::setvbuf(stdout, nullptr, _IOLBF, 0);   // a line per variant as it finishes (stdout may be a file)
   unsigned *flags, *failed;
   float* pay;
   unsigned long long* out;

@@ -26,9 +26,10 @@ std::atomic<bool> g_on{false};
 std::mutex g_mu;
 std::vector<Rec> g_recs;
 std::vector<hipEvent_t> g_pool;
-// scope nesting on this host thread: only the outermost scope records (a conv run as a plain GEMM is timed
-// once, under the conv's name, not again under the GEMM's)
-thread_local int t_depth = 0;
+// scope nesting on this host thread: only the innermost scope records — a conv run as a plain GEMM is timed once,
+// under the GEMM's name (the kernel that ran: rocprofv3 and the PMC files group it the same way), not again under
+// the conv's
+thread_local unsigned long long t_opened = 0;
 
 hipEvent_t take_event() {
   if (!g_pool.empty()) {
@@ -53,16 +54,20 @@ void recycle_all() {
 
 ProfScope::ProfScope(const char* name, hipStream_t s, double work) : name_(name), s_(s), a_(nullptr), work_(work) {
   detail_[0] = 0;
-  if (t_depth++ > 0 || !g_on.load(std::memory_order_relaxed)) return;
+  opened_ = ++t_opened;
+  if (!g_on.load(std::memory_order_relaxed)) return;
   std::lock_guard<std::mutex> lk(g_mu);
   a_ = take_event();
   if (a_) (void)hipEventRecord(static_cast<hipEvent_t>(a_), s_);
 }
 
 ProfScope::~ProfScope() {
-  --t_depth;
   if (!a_) return;
   std::lock_guard<std::mutex> lk(g_mu);
+  if (t_opened != opened_) {   // a scope opened inside this one recorded the launches: drop this one
+    g_pool.push_back(static_cast<hipEvent_t>(a_));
+    return;
+  }
   hipEvent_t b = take_event();
   if (!b) return;
   (void)hipEventRecord(b, s_);

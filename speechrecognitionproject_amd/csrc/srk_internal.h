@@ -189,6 +189,7 @@ class ProfScope {
   void* a_;
   double work_;
   double bytes_ = 0.0;
+  unsigned long long opened_ = 0;   // this scope's number among the thread's scopes (innermost-wins nesting)
   char detail_[96];
 };
 

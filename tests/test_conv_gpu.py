@@ -220,10 +220,13 @@ def test_conv_pool_fused_equals_separate(gpu, gather, ring, precision, N, H, W, 
         _lib.set_option("conv_row32", 1)
         _lib.set_fused_conv_pool(True)
         _lib.set_matmul_precision("fp32")
+    row_wgrad = (W, Ci, Co, KH, KW, ph, pw) == (40, 64, 128, 1, 7, 0, 3)   # fbanks_cnn conv2's shape
     for i, (a, c) in enumerate(zip(*outs)):
-        if i == 3 and precision != "fp32":
+        if precision != "fp32" and (i == 3 or (i == 2 and row_wgrad)):
             # 16-bit modes (option conv_unpool16): the fused backward sums the bias gradient over the
-            # pooled rows, the separate one over the dense dY (the same values and zeros, another order)
+            # pooled rows, the separate one over the dense dY (the same values and zeros, another order);
+            # conv2's fused backward takes its weight gradient from the pooled gradient on the row-staged
+            # conv_row16_wgrad_kernel (workgroup slabs reduced in order: another fp32 summation order)
             assert rel_err(a.numpy(), c.numpy()) <= 1e-5
         else:
             assert torch.equal(a, c)
@@ -571,7 +574,9 @@ def test_conv_full_width_fwd_gemm(gpu, prec, N):
             with torch.no_grad():
                 y = snn._Conv2dNHWCFn.apply(x, w, b, (0, 0), (1, 1))
             torch.cuda.synchronize()
-            used = any("conv_fwd_as_gemm" in e["kernel"] for e in _lib.prof_kernels())
+            # the plain GEMM's launch (innermost profiling scope: M x N x K = N H x Co x W Ci)
+            used = any(e["kernel"].startswith("gemm_") and "%dx%dx%d" % (N * H, Co, W * Ci) in e["kernel"]
+                       for e in _lib.prof_kernels())
             _lib.prof_enable(False)
             ys.append((y.double(), used))
     finally:

@@ -1557,34 +1557,63 @@ __global__ __launch_bounds__(512, 1) void gemm_p32_kernel(KernelArgs ka) {
 }
 
 // Stream-K fixup: a tile covered by several runs = the sum of its partial slabs in run order, then
-// alpha / bias / beta (the splitk_reduce epilogue).  One workgroup per tile; whole tiles return.
+// alpha / bias / beta (the splitk_reduce epilogue).  kSkFixupSlices workgroups per tile, each 256 / that
+// rows, every thread's (row, column quad) items loaded together (all slab loads in flight before the
+// in-order adds: one workgroup per tile read at ~1.8 TB/s, r06); whole tiles return.
+constexpr int kSkFixupSlices = 8;
 __global__ __launch_bounds__(256) void sk_fixup_kernel(KernelArgs ka) {
   const GemmDesc& d = ka.d;
-  const int t = blockIdx.x;
+  const int t = blockIdx.x / kSkFixupSlices, slice = blockIdx.x - t * kSkFixupSlices;
   const int64_t total = (int64_t)ka.tiles * ka.sk_ki, t0 = (int64_t)t * ka.sk_ki;
   const int w0 = sk_owner(t0, total, ka.sk_wgs), w1 = sk_owner(t0 + ka.sk_ki - 1, total, ka.sk_wgs);
   if (w1 == w0) return;
   int tm, tn;
   tile_of(t, ka.tiles_m, ka.tiles_n, ka.group_m, tm, tn);
-  const int nseg = w1 - w0 + 1;
+  const int nseg = w1 - w0 + 1;   // <= 3 (launch_p32: tiles >= W / 2)
   const int64_t MN = d.M * d.N;
   const bool vec = d.N % 4 == 0 && d.ldc % 4 == 0 && (uintptr_t)d.C % 16 == 0 && (uintptr_t)ka.sk_slab % 16 == 0 &&
                    (d.bias_mode != 1 || (uintptr_t)d.bias % 16 == 0);
-  for (int i = threadIdx.x; i < 256 * 64; i += 256) {   // (row, column quad) of the 256 x 256 tile
-    const int64_t row = (int64_t)tm * 256 + (i >> 6), col = (int64_t)tn * 256 + (i & 63) * 4;
+  constexpr int ROWS = 256 / kSkFixupSlices, ITEMS = ROWS * 64 / 256;   // per thread
+  const int64_t r0 = (int64_t)tm * 256 + slice * ROWS;
+  if (vec) {
+    v4f v[ITEMS];
+    int64_t off[ITEMS];
+    bool ok[ITEMS];
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) {   // (row, column quad) of the slice
+      const int i = threadIdx.x + 256 * u;
+      const int64_t row = r0 + (i >> 6), col = (int64_t)tn * 256 + (i & 63) * 4;
+      ok[u] = row < d.M && col < d.N;   // col + 3 < N (N % 4 == 0)
+      off[u] = ok[u] ? row * d.N + col : 0;
+      v[u] = *reinterpret_cast<const v4f*>(ka.sk_slab + off[u]);
+    }
+    v4f v1[ITEMS], v2[ITEMS];
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) v1[u] = *reinterpret_cast<const v4f*>(ka.sk_slab + MN + off[u]);
+    if (nseg > 2) {
+#pragma unroll
+      for (int u = 0; u < ITEMS; ++u) v2[u] = *reinterpret_cast<const v4f*>(ka.sk_slab + 2 * MN + off[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) {
+      if (!ok[u]) continue;
+      v4f x = v[u] + v1[u];
+      if (nseg > 2) x += v2[u];
+      const int i = threadIdx.x + 256 * u;
+      const int64_t row = r0 + (i >> 6), col = (int64_t)tn * 256 + (i & 63) * 4;
+      x *= d.alpha;
+      if (d.bias_mode == 1) x += *reinterpret_cast<const v4f*>(d.bias + col);
+      else if (d.bias_mode == 2) x += d.bias[row];
+      float* c = d.C + row * d.ldc + col;
+      if (d.beta != 0.f) x += d.beta * *reinterpret_cast<const v4f*>(c);
+      *reinterpret_cast<v4f*>(c) = x;
+    }
+    return;
+  }
+  for (int i = threadIdx.x; i < ROWS * 64; i += 256) {
+    const int64_t row = r0 + (i >> 6), col = (int64_t)tn * 256 + (i & 63) * 4;
     if (row >= d.M || col >= d.N) continue;
     const int64_t o = row * d.N + col;
-    if (vec) {   // col + 3 < N
-      v4f v = *reinterpret_cast<const v4f*>(ka.sk_slab + o);
-      for (int g = 1; g < nseg; ++g) v += *reinterpret_cast<const v4f*>(ka.sk_slab + g * MN + o);
-      v *= d.alpha;
-      if (d.bias_mode == 1) v += *reinterpret_cast<const v4f*>(d.bias + col);
-      else if (d.bias_mode == 2) v += d.bias[row];
-      float* c = d.C + row * d.ldc + col;
-      if (d.beta != 0.f) v += d.beta * *reinterpret_cast<const v4f*>(c);
-      *reinterpret_cast<v4f*>(c) = v;
-      continue;
-    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       if (col + e >= d.N) break;
@@ -1629,6 +1658,7 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(GemmDesc d, const f
   partial += (int64_t)blockIdx.y * splits * slab;
   d.C += (int64_t)blockIdx.y * d.sC;
   v4f s = *reinterpret_cast<const v4f*>(partial + i);
+#pragma unroll 8   // loads ahead of the in-order adds
   for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const v4f*>(partial + (int64_t)k * slab + i);
   v4f v = d.alpha * s;
   if (d.bias_mode == 1) v += *reinterpret_cast<const v4f*>(d.bias + col);
@@ -1925,7 +1955,7 @@ int launch_p32(const GemmDesc& d, hipStream_t s) {
   prof.detail("gemm_p32_kernel<%c%c> %lldx%lldx%lld b%d s%d%s", TA ? 'T' : 'N', TB ? 'T' : 'N', (long long)d.M,
               (long long)d.N, (long long)d.K, d.batch, splits, streamk ? " streamk" : "");
   hipLaunchKernelGGL((gemm_p32_kernel<TA, TB>), dim3((unsigned)ka.nblk, (unsigned)d.batch), dim3(512), 0, s, ka);
-  if (streamk) hipLaunchKernelGGL(sk_fixup_kernel, dim3((unsigned)ka.tiles), dim3(256), 0, s, ka);
+  if (streamk) hipLaunchKernelGGL(sk_fixup_kernel, dim3((unsigned)ka.tiles * kSkFixupSlices), dim3(256), 0, s, ka);
   return finish_splits(d, ka, splits, s);
 }
 

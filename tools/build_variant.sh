@@ -20,6 +20,7 @@ for src in "$root"/speechrecognitionproject_amd/csrc/*.hip "$root"/speechrecogni
   fi
   objs+=("$o")
 done
+objs+=("$root/speechrecognitionproject_amd/_build/stamp.cpp.o")   # srk_source_stamp (the main build's)
 for job in $(jobs -p); do wait "$job" || { echo "variant $name: a compile failed" >&2; exit 1; }; done
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 "${objs[@]}" -o "$root/tools/_exp/libsrk_$name.so"
 echo "$root/tools/_exp/libsrk_$name.so"

@@ -1,5 +1,5 @@
 """GEMM micro-benchmark: the fp32 GEMM shapes of one model_mfcc_bgru train step (B = 256, T = 51,
-H = 512), timed with srk_prof events and checked against torch fp32 matmul on the same device.
+H = 512 by default; --B 512 --T 49 for cfg5), timed with srk_prof events and checked against torch fp32 matmul on the same device.
 
     python tools/gemm_bench.py [--reps 10] [--precision fp32|bf16|fp16]
                                                  (env SRK_GEMM_REMAP=0 disables the XCD remap)
@@ -17,17 +17,20 @@ import torch  # noqa: E402
 
 from speechrecognitionproject_amd import _lib  # noqa: E402
 
-B, T, H = 256, 51, 512
-BT = B * T
-# name, ta, tb, M, N, K, lda, ldb  (A stored [M][K] or [K][M] when ta; B stored [K][N] or [N][K] when tb)
-SHAPES = [
-    ("gi_l1", 0, 1, BT, 6 * H, 1024, 1024, 1024),
-    ("gi_l0", 0, 1, BT, 6 * H, 39, 39, 39),
-    ("dx_l1", 0, 0, BT, 1024, 6 * H, 6 * H, 1024),
-    ("dWih_l1", 1, 0, 6 * H, 1024, BT, 6 * H, 1024),
-    ("dWih_l0", 1, 0, 6 * H, 39, BT, 6 * H, 39),
-    ("dWhh", 1, 0, 3 * H, H, BT - 1, 3 * H, 2 * H),
-]
+H = 512
+
+
+def shapes(B, T):
+    BT = B * T
+    # name, ta, tb, M, N, K, lda, ldb  (A stored [M][K] or [K][M] when ta; B stored [K][N] or [N][K] when tb)
+    return [
+        ("gi_l1", 0, 1, BT, 6 * H, 1024, 1024, 1024),
+        ("gi_l0", 0, 1, BT, 6 * H, 39, 39, 39),
+        ("dx_l1", 0, 0, BT, 1024, 6 * H, 6 * H, 1024),
+        ("dWih_l1", 1, 0, 6 * H, 1024, BT, 6 * H, 1024),
+        ("dWih_l0", 1, 0, 6 * H, 39, BT, 6 * H, 39),
+        ("dWhh", 1, 0, 3 * H, H, BT - 1, 3 * H, 2 * H),
+    ]
 
 
 def main():
@@ -38,6 +41,9 @@ def main():
     ap.add_argument("--kernel16", type=int, default=0,
                     help="srk option gemm16_kernel: 0 by shape, 1 register-staged, 2 LDS-DMA ping-pong")
     ap.add_argument("--kernel32", type=int, default=0, help="srk option gemm32_kernel (the same for fp32)")
+    ap.add_argument("--B", type=int, default=256, help="clips per step (cfg5: 512)")
+    ap.add_argument("--T", type=int, default=51, help="frames per clip (cfg5: 49)")
+    ap.add_argument("--only", default="", help="comma-separated shape names")
     a = ap.parse_args()
     _lib.set_matmul_precision(a.precision)
     _lib.call("srk_set_option", b"gemm16_kernel", a.kernel16)
@@ -50,7 +56,9 @@ def main():
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     res = {}
     g = torch.Generator(device=dev).manual_seed(0)
-    for name, ta, tb, M, N, K, lda, ldb in SHAPES:
+    for name, ta, tb, M, N, K, lda, ldb in shapes(a.B, a.T):
+        if a.only and name not in a.only.split(","):
+            continue
         A = torch.randn((K if ta else M) * lda, device=dev, generator=g)
         Bm = torch.randn((N if tb else K) * ldb, device=dev, generator=g)
         C = torch.empty(M * N, device=dev)
